@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""bench.py -- spans/sec aggregated (RED + HLL + CMS) on N x MI355X.
+
+A "step" is one pass of the hot path over one device-resident batch: one
+sa_ingest_device launch aggregating `--spans` synthetic SoA v1 spans (BASELINE
+config 2 shape: 10M spans, ~500 (service, span) pairs -> <=1,500 series,
+default buckets, per-service HLL p=14 + count-min 4x2048 over 10 s windows).
+With N ranks every rank aggregates its own trace-id shard (weak scaling; no
+collective on the data path); after the timed region the ranks merge their
+partials once over RCCL (reported as merge_ms, outside `value`).
+
+Prints ONE JSON line on rank 0. `roofline` prices the ingest kernel against
+HBM (44 algorithmic bytes per span / 8 TB/s); its per-launch time comes from
+HIP events recorded on the launch stream around every timed launch.
+`cpu_baseline` times the CPU oracle port (oracle/, RED+HLL+CMS, 1 thread) on
+rank 0 at N=1 over a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "opentelemetry-demo_amd"))
+
+METRIC = "spans/sec aggregated (RED+HLL+CMS) at 1/8 GPU; % of HBM roofline"
+BYTES_PER_SPAN = 44
+HBM_PEAK_GBS = 8000.0
+
+
+def cpu_baseline(wl, seconds: float):
+    """Oracle port (RED + HLL + CMS over SoA v1, one thread) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+
+    sample = wl.batch.slice(0, min(len(wl.batch), 2_000_000))
+    o = pyoracle.Oracle(n_services=wl.n_services)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        o.ingest(sample)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    o.close()
+    port = {"value": reps * len(sample) / el, "unit": "spans/s", "cores": 1, "kind": "port",
+            "sample": f"first {len(sample):,} spans of the rank-0 batch ingested {reps}x "
+                      f"({reps * len(sample):,} spans, {el:.1f} s) by oracle/ or_ingest "
+                      "(RED + HLL + CMS, Go-faithful float64 bucketing)"}
+    # Connector-faithful RED only: NUL-joined string key built per span and
+    # looked up in a string-keyed map (what aggregateMetrics does per span).
+    from spanagg.synth import SERVICES, SPAN_NAMES
+    strings = list(SERVICES) + [n for n, _ in SPAN_NAMES]
+    m = len(sample)
+    n_series, _, dt = pyoracle.aggregate_strings(
+        strings, wl.service_id[:m], len(SERVICES) + wl.name_id[:m] % len(SPAN_NAMES), wl.kind[:m],
+        wl.status[:m], wl.batch.start_ns[:m], wl.batch.end_ns[:m])
+    conn = {"value": m / dt, "unit": "spans/s", "cores": 1, "kind": "port",
+            "sample": f"first {m:,} spans, string-keyed buildKey + map lookup + "
+                      f"SearchFloat64s (RED only, {n_series} series, {dt:.2f} s)"}
+    return port, conn
+
+
+def load_traffic(path, workload):
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("workload") == workload:
+            return t.get("hbm_bytes_per_launch"), path
+    except (OSError, ValueError):
+        pass
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--spans", type=int, default=10_000_000, help="spans per step per GPU")
+    ap.add_argument("--workload", choices=["c2", "c4"], default="c2")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from spanagg import Config, Engine
+    from spanagg.dist import EnginePartial, merge_red, merge_window
+    from spanagg.synth import generate_c2, generate_highcard
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print("run N>1 under torch.distributed.run (one process per GPU)", file=sys.stderr)
+            return 2
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    n = args.spans
+    if args.workload == "c2":
+        wl = generate_c2(n, seed=42 + rank)
+        batch, first_window, n_services, key_capacity = wl.batch, wl.first_window, wl.n_services, 1000
+        workload = ("C2: synthetic SoA v1 spans, 20 services x 25 span names (Zipf 1.1) x 3 "
+                    "status codes -> <=1,500 series, default spanmetrics buckets, lognormal "
+                    "durations, ~10 spans/trace, per-service HLL p=14 + error count-min 4x2048, "
+                    "10 s windows")
+    else:
+        batch, _, first_window = generate_highcard(n, seed=7 + rank)
+        wl, n_services, key_capacity = None, 1, 1_200_000
+        workload = ("C4: 1,000,000 series (2,000 http.route x 500 k8s.pod.name), uniform, "
+                    "HBM key table, HLL + count-min")
+    cols = []
+    for c in batch.columns():
+        t = torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32))
+        cols.append(t.to(device))
+    eng = Engine(Config(n_services=max(n_services, 1), n_windows=16, key_capacity=key_capacity,
+                        device=local_rank))
+    eng.window_advance(first_window)
+    stream = torch.cuda.current_stream(device)
+
+    def step():
+        eng.ingest_device(*cols, n=n, stream=stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        evs[i][0].record(stream)
+        step()
+        evs[i][1].record(stream)
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    barrier()
+    kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+
+    # one flush (+ RCCL merge across ranks) after the timed region
+    torch.cuda.synchronize(device)
+    tm = time.perf_counter()
+    if world > 1:
+        part = EnginePartial(eng, device)
+        red = merge_red(part, reset=True)
+        merge_window(part, first_window + 1)
+    else:
+        red = eng.flush()
+    torch.cuda.synchronize(device)
+    merge_ms = (time.perf_counter() - tm) * 1e3
+    total_local = (args.warmup + args.steps) * n
+    calls_ok = int(red.calls.sum()) == total_local * world
+
+    result = None
+    if rank == 0:
+        value = world * n * args.steps / elapsed
+        achieved = BYTES_PER_SPAN * n / (kernel_ms * 1e-3) / 1e9
+        traffic, tsrc = load_traffic(args.traffic, args.workload)
+        result = {
+            "metric": METRIC, "value": value, "unit": "spans/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (seeded PCG64 generator, spanagg/synth.py; one shard per rank)",
+            "config": {"workload": workload, "spans_per_step_per_gpu": n,
+                       "global_spans_per_step": n * world,
+                       "parallelism": f"trace-id shards x{world}, RCCL merge at flush"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic, "kernel": "ingest (spanagg_kernels.hip)",
+                         "kernel_ms": kernel_ms, "bytes_per_span": BYTES_PER_SPAN,
+                         "traffic_source": tsrc},
+            "merge_ms": merge_ms, "calls_check": calls_ok,
+        }
+        if world == 1 and not args.no_cpu_baseline and wl is not None:
+            port, conn = cpu_baseline(wl, args.cpu_seconds)
+            result["cpu_baseline"] = port
+            result["cpu_baseline_connector"] = conn
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if calls_ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

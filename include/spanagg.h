@@ -1,0 +1,183 @@
+/*
+ * spanagg.h -- C-ABI of libspanagg, the MI355X (gfx950) span-aggregation engine.
+ *
+ * Drop-in replacement for the per-span work of the otel-collector `spanmetrics`
+ * connector that the reference demo wires into its traces pipeline
+ * (/root/reference/src/otel-collector/otelcol-config.yml:115-116 declares it,
+ * :118-127 makes it an exporter of `traces` and a receiver of `metrics`).
+ * The connector itself is Go ([UPSTREAM] opentelemetry-collector-contrib
+ * connector/spanmetricsconnector v0.125.0, image tag /root/reference/.env:14);
+ * its source is not vendored, so the upstream entry points are cited by name.
+ *
+ *   upstream (Go)                                   replaced by
+ *   ----------------------------------------------  -------------------------------
+ *   createDefaultConfig / Config                    sa_config + sa_config_default
+ *   createTracesToMetricsConnector, Start           sa_create
+ *   ConsumeTraces -> aggregateMetrics (per span)    sa_ingest / sa_ingest_device
+ *   exportMetrics -> buildMetrics + resetState      sa_flush (+ host-side encoding)
+ *   Shutdown                                        sa_destroy
+ *   (new) per-service HLL + error count-min         sa_window_read / sa_window_advance
+ *
+ * Boundary rules (mirroring the connector's contracts):
+ *  - Ownership: batches are borrowed for the duration of the call; results are
+ *    owned by the library and released with sa_red_result_free /
+ *    sa_sketch_result_free.
+ *  - Errors: every call returns an sa_status (0 ok, <0 error); nothing throws
+ *    or aborts across the ABI; sa_last_error() gives the message.
+ *  - Threading: one engine is single-producer (the connector serialises
+ *    ConsumeTraces and the export ticker on one mutex); callers serialise.
+ *  - No torch / HIP types appear in signatures; device pointers and streams
+ *    are passed as plain pointers.
+ *
+ * SoA v1 span batch (44 algorithmic bytes per span, one column per array):
+ *   key_hash  u64  series id: hash of (resource identity, NUL-joined metric key);
+ *                  computed by the host; 0 is reserved (counted as invalid)
+ *   start_ns  u64  span.start_time_unix_nano
+ *   end_ns    u64  span.end_time_unix_nano
+ *   trace_w0  u64  trace_id bytes 0..7 read little-endian (memcpy of the wire bytes)
+ *   trace_w1  u64  trace_id bytes 8..15 read little-endian
+ *   meta      u32  bits 0-15 service_id, 16-18 span.kind, 19-20 status.code
+ */
+#ifndef SPANAGG_H
+#define SPANAGG_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SA_ABI_VERSION 1
+#define SA_MAX_BOUNDS 62
+
+typedef enum {
+    SA_OK = 0,
+    SA_EINVAL = -1,   /* bad argument / config */
+    SA_ENOMEM = -2,   /* host or device allocation failed */
+    SA_EDEVICE = -3,  /* HIP runtime error or no usable gfx950 device */
+    SA_EFULL = -4,    /* key table full: spans were dropped (see stats) */
+    SA_ERANGE = -5,   /* window id outside the resident ring */
+    SA_ESTATE = -6    /* call not valid in the engine's current state */
+} sa_status;
+
+typedef enum { SA_UNIT_MS = 0, SA_UNIT_S = 1 } sa_unit;
+
+typedef struct {
+    /* histogram.explicit.buckets (sorted ascending, finite) and histogram.unit */
+    const double *bounds;
+    uint32_t n_bounds;
+    uint32_t unit;          /* sa_unit */
+    /* build-owned sketches */
+    uint32_t hll_p;         /* HLL precision, 4..18 (default 14) */
+    uint32_t cms_d;         /* count-min rows, 1..8 (default 4) */
+    uint32_t cms_w;         /* count-min columns, power of two (default 2048) */
+    uint64_t window_ns;     /* sketch window length (default 10 s) */
+    uint32_t n_windows;     /* resident window ring, power of two (default 8) */
+    uint32_t n_services;    /* service ids 0..n_services-1 get sketches */
+    uint64_t key_capacity;  /* expected distinct series; table sized >= 2x, pow2 */
+    int32_t device;         /* HIP device ordinal (one engine per GPU / rank) */
+    uint32_t flags;         /* reserved, 0 */
+} sa_config;
+
+typedef struct {
+    const uint64_t *key_hash, *start_ns, *end_ns, *trace_w0, *trace_w1;
+    const uint32_t *meta;
+    uint64_t n;
+} sa_span_batch;
+
+/* Delta RED state since the previous sa_flush, one row per series with any
+ * span, sorted by key_hash ascending. */
+typedef struct {
+    uint64_t n_series;
+    uint32_t n_buckets;            /* n_bounds + 1 */
+    const uint64_t *key_hash;      /* [n_series] */
+    const uint64_t *bucket_counts; /* [n_series][n_buckets] */
+    const uint64_t *calls;         /* [n_series] == sum of bucket_counts (A8) */
+    const uint64_t *sum_ns;        /* [n_series] exact sum of durations in ns */
+    const double *sum;             /* [n_series] sum_ns / unit divisor (ms or s) */
+} sa_red_result;
+
+typedef struct {
+    uint64_t window_id;
+    uint32_t n_services, hll_p;
+    const uint8_t *hll;            /* [n_services][2^hll_p] registers */
+    uint32_t cms_d, cms_w;
+    const uint32_t *cms;           /* [cms_d][cms_w], saturating u32 */
+} sa_sketch_result;
+
+typedef struct {
+    uint64_t spans;                /* spans accepted by sa_ingest* */
+    uint64_t zero_key;             /* spans with key_hash == 0 (no RED update) */
+    uint64_t invalid_service;      /* service_id >= n_services (no sketch update) */
+    uint64_t window_out_of_range;  /* window outside the resident ring (no sketch update) */
+    uint64_t dropped_table_full;   /* spans lost because the key table was full */
+    uint64_t n_keys;               /* distinct series resident in the key table */
+    uint64_t table_capacity;
+    uint64_t window_base;          /* oldest resident window id */
+    uint32_t small_table;          /* 1 = LDS-mirrored table path, 0 = HBM path */
+    uint32_t pad;
+} sa_stats;
+
+typedef struct sa_engine sa_engine;
+
+/* createDefaultConfig: default buckets {2,4,6,8,10,50,100,200,400,800,1000,1400,
+ * 2000,5000,10000,15000} ms, HLL p=14, CMS 4x2048, 10 s windows, 8-window ring. */
+void sa_config_default(sa_config *cfg);
+int sa_abi_version(void);
+
+int sa_create(const sa_config *cfg, sa_engine **out);
+void sa_destroy(sa_engine *e);
+const char *sa_last_error(const sa_engine *e);
+
+/* Host-memory batch: staged to HBM by the library, then aggregated. */
+int sa_ingest(sa_engine *e, const sa_span_batch *batch);
+/* Device-resident batch (pointers into HBM of this engine's device).
+ * `stream` is a hipStream_t (NULL = the engine's own stream). Asynchronous:
+ * the batch must stay valid until the stream reaches this point. */
+int sa_ingest_device(sa_engine *e, const sa_span_batch *batch, void *stream);
+int sa_sync(sa_engine *e);
+
+/* exportMetrics: delta since the last flush, then the engine's RED counters are
+ * reset (keys stay resident). Returns SA_EFULL (with the result still filled)
+ * if spans were dropped since the previous flush. */
+int sa_flush(sa_engine *e, sa_red_result **out);
+void sa_red_result_free(sa_red_result *r);
+
+/* Sketches of one resident window (not cleared). */
+int sa_window_read(sa_engine *e, uint64_t window_id, sa_sketch_result **out);
+/* Retire every window < new_base (clears their ring slots); spans whose window
+ * is below the base or >= base + n_windows are counted in window_out_of_range. */
+int sa_window_advance(sa_engine *e, uint64_t new_base);
+void sa_sketch_result_free(sa_sketch_result *r);
+
+int sa_get_stats(sa_engine *e, sa_stats *out);
+
+/* ---- multi-GPU merge hooks (device pointers on this engine's device) ----
+ * Used by the host's RCCL merge: gather the local key list, build the sorted
+ * union across ranks, densify local counters against it, all-reduce. */
+/* Folds pending partials into the HBM table and writes the resident keys that
+ * have a non-zero delta into d_keys (capacity `cap`); *n_out = count (may exceed
+ * cap, in which case nothing beyond cap is written). */
+int sa_export_keys(sa_engine *e, uint64_t *d_keys, uint64_t cap, uint64_t *n_out, void *stream);
+/* d_rows[i] = [bucket counts..., sum_ns] (n_buckets+1 u64) for d_keys[i]
+ * (zeros if absent). reset != 0 clears the engine's delta counters afterwards. */
+int sa_gather_dense(sa_engine *e, const uint64_t *d_keys, uint64_t n, uint64_t *d_rows,
+                    int reset, void *stream);
+/* Window sketches into device buffers: d_hll [n_services][2^p] u8 and
+ * d_cms [d][w] u64 (unsaturated, for sum all-reduce). */
+int sa_window_export(sa_engine *e, uint64_t window_id, uint8_t *d_hll, uint64_t *d_cms,
+                     void *stream);
+
+/* ---- pure host helpers (no device needed) ---- */
+/* Integer bucket thresholds: bucket(d_ns) = n_neg + #{i : d_ns > thr[i]} equals
+ * sort.SearchFloat64s(bounds, float64(d_ns)/div) for every u64 d_ns. Returns
+ * n_neg via *n_neg and fills thr[0 .. n_bounds-n_neg). */
+int sa_bucket_thresholds(const double *bounds, uint32_t n_bounds, uint32_t unit,
+                         uint64_t *thr, uint32_t *n_neg);
+/* HLL estimate of one register array (standard estimator + linear counting). */
+double sa_hll_estimate(const uint8_t *regs, uint32_t p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,77 @@
+// sa_internal.h -- shared definitions between the HIP kernels and the C-ABI
+// engine of libspanagg (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace sa {
+
+constexpr int kMaxBounds = 62;          // SA_MAX_BOUNDS
+constexpr uint32_t kNotFound = 0xFFFFFFFFu;
+constexpr uint64_t kPhi = 0x9E3779B97F4A7C15ULL;  // Fibonacci hashing multiplier
+
+// stats slots (device array of u64)
+enum : int {
+  kStatZeroKey = 0,
+  kStatInvalidService = 1,
+  kStatWindowOOR = 2,
+  kStatDropped = 3,
+  kNumStats = 4
+};
+
+// Everything the ingest kernels need, passed by value (kernel-argument segment,
+// read through the scalar cache).
+struct IngestParams {
+  // SoA v1 batch (device pointers, 16-B aligned)
+  const uint64_t *key, *start, *end, *w0, *w1;
+  const uint32_t *meta;
+  uint64_t n;
+  // key table (open addressing, linear probing, EMPTY = 0)
+  unsigned long long *gkeys;
+  uint32_t log2cap;
+  uint32_t max_probe;
+  // small-table path: per-workgroup slabs [G][cap][nbk] u32 and [G][cap] u64
+  uint32_t *slab_cnt;
+  unsigned long long *slab_sum;
+  // HBM-table path: counters [cap][nbk+1] u64 (last = sum_ns)
+  unsigned long long *gcounts;
+  // histogram: bucket(d) = nneg + #{i < npos : d > thr[i]}
+  uint64_t thr[kMaxBounds];
+  uint32_t npos, nneg, nbk;
+  uint32_t epoch_tiles;  // small path: LDS u16 counters flushed every epoch_tiles tiles
+  // sketches
+  uint8_t *hll;                 // [W][S][2^p]
+  unsigned long long *cms;      // [W][d][w]
+  uint64_t window_ns, win_magic, win_base;
+  uint32_t win_mask, n_windows;
+  uint32_t p, n_services, cms_d, cms_shift, cms_w;
+  uint32_t pad0;
+  uint64_t cms_seed[8];
+  unsigned long long *stats;
+};
+
+__host__ __device__ inline uint64_t slot_of(uint64_t key, uint32_t log2cap) {
+  return (key * kPhi) >> (64 - log2cap);
+}
+
+// launchers (spanagg_kernels.hip)
+hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, uint32_t block,
+                               size_t lds_bytes, hipStream_t s);
+hipError_t launch_ingest_hbm(const IngestParams &P, uint32_t grid, uint32_t block,
+                             hipStream_t s);
+hipError_t prepare_ingest_small(size_t lds_bytes);
+hipError_t launch_reduce_slabs(uint32_t *slab_cnt, unsigned long long *slab_sum,
+                               unsigned long long *gcounts, uint32_t G, uint64_t cap,
+                               uint32_t nbk, hipStream_t s);
+hipError_t launch_compact(const unsigned long long *gkeys, unsigned long long *gcounts,
+                          uint64_t cap, uint32_t stride, unsigned long long *out_keys,
+                          unsigned long long *out_rows, unsigned long long *out_n,
+                          uint64_t out_cap, int reset, hipStream_t s);
+hipError_t launch_gather_dense(const unsigned long long *gkeys, const unsigned long long *gcounts,
+                               uint32_t log2cap, uint32_t max_probe, uint32_t stride,
+                               const uint64_t *keys, uint64_t n, uint64_t *rows, hipStream_t s);
+hipError_t launch_count_keys(const unsigned long long *gkeys, uint64_t cap,
+                             unsigned long long *out, hipStream_t s);
+
+}  // namespace sa

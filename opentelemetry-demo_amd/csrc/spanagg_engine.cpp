@@ -1,0 +1,638 @@
+// spanagg_engine.cpp -- C-ABI of libspanagg (include/spanagg.h): engine state in
+// HBM, staging, flush/compaction and the multi-GPU merge hooks.  One engine owns
+// one gfx950 device; the product path has no CPU fallback -- sa_create fails with
+// SA_EDEVICE when no gfx950 device is usable.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "sa_internal.h"
+#include "spanagg.h"
+
+using sa::IngestParams;
+
+namespace {
+
+constexpr double kDefaultBounds[16] = {2,   4,   6,    8,    10,   50,   100,   200,
+                                       400, 800, 1000, 1400, 2000, 5000, 10000, 15000};
+constexpr uint64_t kCmsSeed[8] = {0x9E3779B97F4A7C15ULL, 0xBF58476D1CE4E5B9ULL,
+                                  0x94D049BB133111EBULL, 0xD6E8FEB86659FD93ULL,
+                                  0xA0761D6478BD642FULL, 0xE7037ED1A0B428DBULL,
+                                  0x8EBC6AF09C88C6E3ULL, 0x589965CC75374CC3ULL};
+constexpr size_t kLdsBudget = 144 * 1024;  // small-table path LDS ceiling per workgroup
+constexpr uint32_t kSmallBlock = 1024;
+constexpr uint32_t kHbmBlock = 256;
+constexpr uint32_t kMaxProbe = 4096;
+constexpr uint64_t kSlabLimit = 1ULL << 31;  // per-workgroup spans between slab reductions
+
+bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
+uint32_t log2u(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
+uint64_t next_pow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+}  // namespace
+
+struct sa_engine {
+  sa_config cfg{};
+  std::vector<double> bounds;
+  int dev = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_a = nullptr, ev_b = nullptr;
+  uint32_t nbk = 0, npos = 0, nneg = 0;
+  uint64_t thr[sa::kMaxBounds]{};
+  uint32_t log2cap = 0;
+  uint64_t cap = 0;
+  bool small = false;
+  uint32_t G = 0, block = 0, cus = 0;
+  size_t lds_bytes = 0;
+  unsigned long long *gkeys = nullptr, *gcounts = nullptr, *slab_sum = nullptr, *cms = nullptr,
+                     *stats = nullptr, *out_keys = nullptr, *out_rows = nullptr, *scratch = nullptr;
+  uint32_t *slab_cnt = nullptr;
+  uint8_t *hll = nullptr;
+  size_t hll_slot_bytes = 0, cms_slot_elems = 0;
+  void *stage = nullptr;
+  uint64_t stage_spans = 0;
+  uint64_t win_base = 0, spans = 0, slab_load = 0, dropped_seen = 0;
+  std::string err;
+};
+
+namespace {
+
+int fail(sa_engine *e, int code, const std::string &msg) {
+  if (e) e->err = msg;
+  return code;
+}
+
+#define SA_HIP(e, call)                                                                   \
+  do {                                                                                    \
+    hipError_t _st = (call);                                                              \
+    if (_st != hipSuccess)                                                                \
+      return fail((e), SA_EDEVICE, std::string(#call) + ": " + hipGetErrorString(_st));  \
+  } while (0)
+
+int set_dev(sa_engine *e) {
+  SA_HIP(e, hipSetDevice(e->dev));
+  return SA_OK;
+}
+
+int validate_config(const sa_config *c, std::string &why) {
+  if (!c) return why = "null config", SA_EINVAL;
+  if (c->n_bounds > SA_MAX_BOUNDS) return why = "too many histogram bounds", SA_EINVAL;
+  if (c->n_bounds && !c->bounds) return why = "bounds pointer is null", SA_EINVAL;
+  if (c->unit > SA_UNIT_S) return why = "unit must be ms or s", SA_EINVAL;
+  if (c->hll_p < 4 || c->hll_p > 18) return why = "hll_p must be in 4..18", SA_EINVAL;
+  if (c->cms_d < 1 || c->cms_d > 8) return why = "cms_d must be in 1..8", SA_EINVAL;
+  if (c->cms_w < 2 || !is_pow2(c->cms_w)) return why = "cms_w must be a power of two >= 2", SA_EINVAL;
+  if (c->window_ns == 0) return why = "window_ns must be > 0", SA_EINVAL;
+  if (!is_pow2(c->n_windows) || c->n_windows > 4096)
+    return why = "n_windows must be a power of two <= 4096", SA_EINVAL;
+  if (c->n_services < 1 || c->n_services > 65536)
+    return why = "n_services must be in 1..65536", SA_EINVAL;
+  if (c->key_capacity < 1 || c->key_capacity > (1ULL << 30))
+    return why = "key_capacity must be in 1..2^30", SA_EINVAL;
+  return SA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sa_abi_version(void) { return SA_ABI_VERSION; }
+
+void sa_config_default(sa_config *c) {
+  if (!c) return;
+  std::memset(c, 0, sizeof *c);
+  c->bounds = kDefaultBounds;
+  c->n_bounds = 16;
+  c->unit = SA_UNIT_MS;
+  c->hll_p = 14;
+  c->cms_d = 4;
+  c->cms_w = 2048;
+  c->window_ns = 10ULL * 1000000000ULL;
+  c->n_windows = 8;
+  c->n_services = 64;
+  c->key_capacity = 1000;  // the connector's dimensions_cache_size default
+  c->device = 0;
+}
+
+int sa_bucket_thresholds(const double *bounds, uint32_t n, uint32_t unit, uint64_t *thr,
+                         uint32_t *n_neg) {
+  if (n > SA_MAX_BOUNDS || (n && (!bounds || !thr)) || !n_neg || unit > SA_UNIT_S)
+    return SA_EINVAL;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (std::isnan(bounds[i])) return SA_EINVAL;
+    if (i && !(bounds[i - 1] <= bounds[i])) return SA_EINVAL;
+  }
+  const double div = unit == SA_UNIT_S ? 1e9 : 1e6;
+  uint32_t neg = 0;
+  while (neg < n && bounds[neg] < 0.0) ++neg;
+  for (uint32_t i = neg; i < n; ++i) {
+    const double b = bounds[i];
+    // T = max{d in u64 : float64(d)/div <= b}; f(d) is monotone non-decreasing.
+    auto f_le = [&](uint64_t d) { return (double)d / div <= b; };
+    uint64_t t;
+    if (f_le(UINT64_MAX)) {
+      t = UINT64_MAX;
+    } else {
+      uint64_t lo = 0, hi = UINT64_MAX;  // f_le(lo) holds since b >= 0
+      while (hi - lo > 1) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (f_le(mid)) lo = mid;
+        else hi = mid;
+      }
+      t = lo;
+    }
+    thr[i - neg] = t;
+  }
+  *n_neg = neg;
+  return SA_OK;
+}
+
+double sa_hll_estimate(const uint8_t *regs, uint32_t p) {
+  if (!regs || p < 4 || p > 18) return -1.0;
+  const uint32_t m = 1u << p;
+  double sum = 0.0;
+  uint32_t zeros = 0;
+  for (uint32_t j = 0; j < m; ++j) {
+    sum += std::ldexp(1.0, -(int)regs[j]);
+    zeros += regs[j] == 0;
+  }
+  const double alpha = m == 16 ? 0.673 : m == 32 ? 0.697 : m == 64 ? 0.709
+                                                                  : 0.7213 / (1.0 + 1.079 / m);
+  double est = alpha * (double)m * (double)m / sum;
+  if (est <= 2.5 * m && zeros) est = (double)m * std::log((double)m / (double)zeros);
+  return est;
+}
+
+int sa_create(const sa_config *cfg, sa_engine **out) {
+  if (!out) return SA_EINVAL;
+  *out = nullptr;
+  std::string why;
+  if (int rc = validate_config(cfg, why)) {
+    std::fprintf(stderr, "sa_create: %s\n", why.c_str());
+    return rc;
+  }
+  auto *e = new sa_engine();
+  e->cfg = *cfg;
+  e->bounds.assign(cfg->bounds, cfg->bounds + cfg->n_bounds);
+  e->cfg.bounds = e->bounds.data();
+  e->nbk = cfg->n_bounds + 1;
+  if (sa_bucket_thresholds(e->bounds.data(), cfg->n_bounds, cfg->unit, e->thr, &e->nneg) != SA_OK) {
+    std::fprintf(stderr, "sa_create: histogram bounds must be sorted ascending and not NaN\n");
+    delete e;
+    return SA_EINVAL;
+  }
+  e->npos = cfg->n_bounds - e->nneg;
+
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || cfg->device < 0 ||
+      cfg->device >= ndev) {
+    std::fprintf(stderr, "sa_create: no HIP device %d (found %d)\n", cfg->device, ndev);
+    delete e;
+    return SA_EDEVICE;
+  }
+  e->dev = cfg->device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, e->dev) != hipSuccess ||
+      std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    std::fprintf(stderr, "sa_create: device %d is not gfx950 (%s)\n", e->dev, prop.gcnArchName);
+    delete e;
+    return SA_EDEVICE;
+  }
+  e->cus = (uint32_t)prop.multiProcessorCount;
+
+  auto bail = [&](int rc) {
+    std::fprintf(stderr, "sa_create: %s\n", e->err.c_str());
+    sa_destroy(e);
+    return rc;
+  };
+  if (int rc = set_dev(e)) return bail(rc);
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_a, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_b, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(e, SA_EDEVICE, "stream/event creation failed"));
+
+  e->cap = std::max<uint64_t>(16, next_pow2(2 * cfg->key_capacity));
+  e->log2cap = log2u(e->cap);
+  const uint32_t nw = (e->nbk + 1) / 2;
+  e->lds_bytes = (size_t)e->cap * 16 + (size_t)e->cap * nw * 4;
+  e->small = e->lds_bytes <= kLdsBudget;
+  if (e->small) {
+    e->block = kSmallBlock;
+    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2, (uint32_t)((160 * 1024) / e->lds_bytes)));
+    e->G = e->cus * per_cu;
+    if (hipError_t st = sa::prepare_ingest_small(e->lds_bytes); st != hipSuccess)
+      return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
+  } else {
+    e->block = kHbmBlock;
+    e->G = e->cus * 8;
+  }
+
+  const uint32_t stride = e->nbk + 1;
+  const uint64_t S = cfg->n_services, W = cfg->n_windows;
+  e->hll_slot_bytes = (size_t)S << cfg->hll_p;
+  e->cms_slot_elems = (size_t)cfg->cms_d * cfg->cms_w;
+  auto alloc = [&](void **p, size_t bytes) -> int {
+    if (hipMalloc(p, bytes) != hipSuccess) return fail(e, SA_ENOMEM, "hipMalloc failed");
+    if (hipMemset(*p, 0, bytes) != hipSuccess) return fail(e, SA_EDEVICE, "hipMemset failed");
+    return SA_OK;
+  };
+  int rc = SA_OK;
+  if ((rc = alloc((void **)&e->gkeys, e->cap * 8)) ||
+      (rc = alloc((void **)&e->gcounts, e->cap * stride * 8)) ||
+      (rc = alloc((void **)&e->hll, e->hll_slot_bytes * W)) ||
+      (rc = alloc((void **)&e->cms, e->cms_slot_elems * W * 8)) ||
+      (rc = alloc((void **)&e->stats, 64)) || (rc = alloc((void **)&e->scratch, 64)))
+    return bail(rc);
+  if (e->small) {
+    if ((rc = alloc((void **)&e->slab_cnt, (size_t)e->G * e->cap * e->nbk * 4)) ||
+        (rc = alloc((void **)&e->slab_sum, (size_t)e->G * e->cap * 8)))
+      return bail(rc);
+  }
+  if (hipDeviceSynchronize() != hipSuccess) return bail(fail(e, SA_EDEVICE, "device sync failed"));
+  *out = e;
+  return SA_OK;
+}
+
+void sa_destroy(sa_engine *e) {
+  if (!e) return;
+  (void)hipSetDevice(e->dev);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (void *p : {(void *)e->gkeys, (void *)e->gcounts, (void *)e->slab_sum, (void *)e->cms,
+                  (void *)e->stats, (void *)e->out_keys, (void *)e->out_rows, (void *)e->scratch,
+                  (void *)e->slab_cnt, (void *)e->hll, e->stage})
+    if (p) (void)hipFree(p);
+  if (e->ev_a) (void)hipEventDestroy(e->ev_a);
+  if (e->ev_b) (void)hipEventDestroy(e->ev_b);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+const char *sa_last_error(const sa_engine *e) { return e ? e->err.c_str() : "null engine"; }
+
+static int reduce_slabs(sa_engine *e, hipStream_t s) {
+  if (!e->small || e->slab_load == 0) return SA_OK;
+  SA_HIP(e, sa::launch_reduce_slabs(e->slab_cnt, e->slab_sum, e->gcounts, e->G, e->cap, e->nbk, s));
+  e->slab_load = 0;
+  return SA_OK;
+}
+
+static int ingest_on(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
+  if (b->n == 0) return SA_OK;
+  const uint64_t tile = (uint64_t)e->block * 2;
+  const uint64_t tiles = (b->n + tile - 1) / tile;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, e->G);
+  if (e->small) {
+    const uint64_t per_wg = ((tiles + grid - 1) / grid) * tile;
+    if (e->slab_load + per_wg > kSlabLimit)
+      if (int rc = reduce_slabs(e, s)) return rc;
+    e->slab_load += per_wg;
+  }
+  IngestParams P{};
+  P.key = b->key_hash;
+  P.start = b->start_ns;
+  P.end = b->end_ns;
+  P.w0 = b->trace_w0;
+  P.w1 = b->trace_w1;
+  P.meta = b->meta;
+  P.n = b->n;
+  P.gkeys = e->gkeys;
+  P.log2cap = e->log2cap;
+  P.max_probe = kMaxProbe;
+  P.slab_cnt = e->slab_cnt;
+  P.slab_sum = e->slab_sum;
+  P.gcounts = e->gcounts;
+  std::memcpy(P.thr, e->thr, sizeof e->thr);
+  P.npos = e->npos;
+  P.nneg = e->nneg;
+  P.nbk = e->nbk;
+  P.epoch_tiles = (uint32_t)(65535 / tile);
+  P.hll = e->hll;
+  P.cms = e->cms;
+  P.window_ns = e->cfg.window_ns;
+  P.win_magic = UINT64_MAX / e->cfg.window_ns;
+  P.win_base = e->win_base;
+  P.win_mask = e->cfg.n_windows - 1;
+  P.n_windows = e->cfg.n_windows;
+  P.p = e->cfg.hll_p;
+  P.n_services = e->cfg.n_services;
+  P.cms_d = e->cfg.cms_d;
+  P.cms_w = e->cfg.cms_w;
+  P.cms_shift = 64 - log2u(e->cfg.cms_w);
+  std::memcpy(P.cms_seed, kCmsSeed, sizeof kCmsSeed);
+  P.stats = e->stats;
+  hipError_t st = e->small ? sa::launch_ingest_small(P, grid, e->block, e->lds_bytes, s)
+                           : sa::launch_ingest_hbm(P, grid, e->block, s);
+  if (st != hipSuccess) return fail(e, SA_EDEVICE, std::string("ingest launch: ") + hipGetErrorString(st));
+  e->spans += b->n;
+  return SA_OK;
+}
+
+static int check_batch(sa_engine *e, const sa_span_batch *b, bool device) {
+  if (!e) return SA_EINVAL;
+  if (!b) return fail(e, SA_EINVAL, "null batch");
+  if (b->n == 0) return SA_OK;
+  const void *cols[5] = {b->key_hash, b->start_ns, b->end_ns, b->trace_w0, b->trace_w1};
+  for (const void *c : cols) {
+    if (!c) return fail(e, SA_EINVAL, "null batch column");
+    if (device && (reinterpret_cast<uintptr_t>(c) & 15))
+      return fail(e, SA_EINVAL, "device batch u64 columns must be 16-byte aligned");
+  }
+  if (!b->meta) return fail(e, SA_EINVAL, "null meta column");
+  if (device && (reinterpret_cast<uintptr_t>(b->meta) & 7))
+    return fail(e, SA_EINVAL, "device batch meta column must be 8-byte aligned");
+  return SA_OK;
+}
+
+int sa_ingest_device(sa_engine *e, const sa_span_batch *b, void *stream) {
+  if (int rc = check_batch(e, b, true)) return rc;
+  if (int rc = set_dev(e)) return rc;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+  if (s != e->stream) {  // order against the engine stream both ways
+    SA_HIP(e, hipEventRecord(e->ev_a, e->stream));
+    SA_HIP(e, hipStreamWaitEvent(s, e->ev_a, 0));
+  }
+  if (int rc = ingest_on(e, b, s)) return rc;
+  if (s != e->stream) {
+    SA_HIP(e, hipEventRecord(e->ev_b, s));
+    SA_HIP(e, hipStreamWaitEvent(e->stream, e->ev_b, 0));
+  }
+  return SA_OK;
+}
+
+int sa_ingest(sa_engine *e, const sa_span_batch *b) {
+  if (int rc = check_batch(e, b, false)) return rc;
+  if (b->n == 0) return SA_OK;
+  if (int rc = set_dev(e)) return rc;
+  const uint64_t chunk = std::min<uint64_t>(b->n, 1ULL << 22);
+  if (e->stage_spans < chunk) {
+    if (e->stage) {
+      SA_HIP(e, hipStreamSynchronize(e->stream));
+      (void)hipFree(e->stage);
+      e->stage = nullptr;
+      e->stage_spans = 0;
+    }
+    if (hipMalloc(&e->stage, chunk * 44 + 256) != hipSuccess)
+      return fail(e, SA_ENOMEM, "staging hipMalloc failed");
+    e->stage_spans = chunk;
+  }
+  char *base = static_cast<char *>(e->stage);
+  uint64_t *dk = reinterpret_cast<uint64_t *>(base);
+  uint64_t *ds = dk + e->stage_spans, *de = ds + e->stage_spans, *da = de + e->stage_spans,
+           *db = da + e->stage_spans;
+  uint32_t *dm = reinterpret_cast<uint32_t *>(db + e->stage_spans);
+  for (uint64_t off = 0; off < b->n; off += chunk) {
+    const uint64_t m = std::min(chunk, b->n - off);
+    SA_HIP(e, hipMemcpyAsync(dk, b->key_hash + off, m * 8, hipMemcpyHostToDevice, e->stream));
+    SA_HIP(e, hipMemcpyAsync(ds, b->start_ns + off, m * 8, hipMemcpyHostToDevice, e->stream));
+    SA_HIP(e, hipMemcpyAsync(de, b->end_ns + off, m * 8, hipMemcpyHostToDevice, e->stream));
+    SA_HIP(e, hipMemcpyAsync(da, b->trace_w0 + off, m * 8, hipMemcpyHostToDevice, e->stream));
+    SA_HIP(e, hipMemcpyAsync(db, b->trace_w1 + off, m * 8, hipMemcpyHostToDevice, e->stream));
+    SA_HIP(e, hipMemcpyAsync(dm, b->meta + off, m * 4, hipMemcpyHostToDevice, e->stream));
+    sa_span_batch sub{dk, ds, de, da, db, dm, m};
+    if (int rc = ingest_on(e, &sub, e->stream)) return rc;
+  }
+  SA_HIP(e, hipStreamSynchronize(e->stream));
+  return SA_OK;
+}
+
+int sa_sync(sa_engine *e) {
+  if (!e) return SA_EINVAL;
+  if (int rc = set_dev(e)) return rc;
+  SA_HIP(e, hipStreamSynchronize(e->stream));
+  return SA_OK;
+}
+
+static int ensure_out(sa_engine *e) {
+  if (e->out_keys) return SA_OK;
+  const uint32_t stride = e->nbk + 1;
+  if (hipMalloc((void **)&e->out_keys, e->cap * 8) != hipSuccess ||
+      hipMalloc((void **)&e->out_rows, e->cap * stride * 8) != hipSuccess)
+    return fail(e, SA_ENOMEM, "flush buffers hipMalloc failed");
+  return SA_OK;
+}
+
+static int read_stats(sa_engine *e, uint64_t out[sa::kNumStats]) {
+  SA_HIP(e, hipMemcpyAsync(out, e->stats, sa::kNumStats * 8, hipMemcpyDeviceToHost, e->stream));
+  SA_HIP(e, hipStreamSynchronize(e->stream));
+  return SA_OK;
+}
+
+struct red_holder {
+  sa_red_result r;
+  std::vector<uint64_t> keys, counts, calls, sum_ns;
+  std::vector<double> sum;
+};
+
+int sa_flush(sa_engine *e, sa_red_result **out) {
+  if (!e || !out) return SA_EINVAL;
+  *out = nullptr;
+  if (int rc = set_dev(e)) return rc;
+  if (int rc = ensure_out(e)) return rc;
+  if (int rc = reduce_slabs(e, e->stream)) return rc;
+  const uint32_t stride = e->nbk + 1;
+  SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, e->stream));
+  SA_HIP(e, sa::launch_compact(e->gkeys, e->gcounts, e->cap, stride, e->out_keys, e->out_rows,
+                               e->scratch, e->cap, 1, e->stream));
+  uint64_t n = 0;
+  SA_HIP(e, hipMemcpyAsync(&n, e->scratch, 8, hipMemcpyDeviceToHost, e->stream));
+  SA_HIP(e, hipStreamSynchronize(e->stream));
+  std::vector<uint64_t> k(n), rows(n * stride);
+  if (n) {
+    SA_HIP(e, hipMemcpyAsync(k.data(), e->out_keys, n * 8, hipMemcpyDeviceToHost, e->stream));
+    SA_HIP(e, hipMemcpyAsync(rows.data(), e->out_rows, n * stride * 8, hipMemcpyDeviceToHost, e->stream));
+    SA_HIP(e, hipStreamSynchronize(e->stream));
+  }
+  std::vector<uint64_t> ord(n);
+  std::iota(ord.begin(), ord.end(), 0);
+  std::sort(ord.begin(), ord.end(), [&](uint64_t a, uint64_t b) { return k[a] < k[b]; });
+  auto *h = new red_holder();
+  h->keys.resize(n);
+  h->counts.resize(n * e->nbk);
+  h->calls.resize(n);
+  h->sum_ns.resize(n);
+  h->sum.resize(n);
+  const double div = e->cfg.unit == SA_UNIT_S ? 1e9 : 1e6;
+  for (uint64_t r = 0; r < n; ++r) {
+    const uint64_t i = ord[r];
+    h->keys[r] = k[i];
+    uint64_t c = 0;
+    for (uint32_t b = 0; b < e->nbk; ++b) {
+      h->counts[r * e->nbk + b] = rows[i * stride + b];
+      c += rows[i * stride + b];
+    }
+    h->calls[r] = c;
+    h->sum_ns[r] = rows[i * stride + e->nbk];
+    h->sum[r] = (double)h->sum_ns[r] / div;
+  }
+  h->r.n_series = n;
+  h->r.n_buckets = e->nbk;
+  h->r.key_hash = h->keys.data();
+  h->r.bucket_counts = h->counts.data();
+  h->r.calls = h->calls.data();
+  h->r.sum_ns = h->sum_ns.data();
+  h->r.sum = h->sum.data();
+  *out = &h->r;
+  uint64_t st[sa::kNumStats];
+  if (int rc = read_stats(e, st)) return rc;
+  if (st[sa::kStatDropped] != e->dropped_seen) {
+    e->dropped_seen = st[sa::kStatDropped];
+    return fail(e, SA_EFULL, "key table full: spans were dropped since the previous flush");
+  }
+  return SA_OK;
+}
+
+void sa_red_result_free(sa_red_result *r) { delete reinterpret_cast<red_holder *>(r); }
+
+struct sketch_holder {
+  sa_sketch_result r;
+  std::vector<uint8_t> hll;
+  std::vector<uint32_t> cms;
+};
+
+static bool resident(const sa_engine *e, uint64_t w) {
+  return w >= e->win_base && w - e->win_base < e->cfg.n_windows;
+}
+
+int sa_window_read(sa_engine *e, uint64_t window_id, sa_sketch_result **out) {
+  if (!e || !out) return SA_EINVAL;
+  *out = nullptr;
+  if (!resident(e, window_id)) return fail(e, SA_ERANGE, "window not resident");
+  if (int rc = set_dev(e)) return rc;
+  const uint64_t ws = window_id & (e->cfg.n_windows - 1);
+  auto *h = new sketch_holder();
+  h->hll.resize(e->hll_slot_bytes);
+  std::vector<uint64_t> cms64(e->cms_slot_elems);
+  hipError_t a = hipMemcpyAsync(h->hll.data(), e->hll + ws * e->hll_slot_bytes, e->hll_slot_bytes,
+                                hipMemcpyDeviceToHost, e->stream);
+  hipError_t b = hipMemcpyAsync(cms64.data(), e->cms + ws * e->cms_slot_elems,
+                                e->cms_slot_elems * 8, hipMemcpyDeviceToHost, e->stream);
+  hipError_t c = hipStreamSynchronize(e->stream);
+  if (a != hipSuccess || b != hipSuccess || c != hipSuccess) {
+    delete h;
+    return fail(e, SA_EDEVICE, "window read failed");
+  }
+  h->cms.resize(e->cms_slot_elems);
+  for (size_t i = 0; i < cms64.size(); ++i)
+    h->cms[i] = cms64[i] > UINT32_MAX ? UINT32_MAX : (uint32_t)cms64[i];
+  h->r.window_id = window_id;
+  h->r.n_services = e->cfg.n_services;
+  h->r.hll_p = e->cfg.hll_p;
+  h->r.hll = h->hll.data();
+  h->r.cms_d = e->cfg.cms_d;
+  h->r.cms_w = e->cfg.cms_w;
+  h->r.cms = h->cms.data();
+  *out = &h->r;
+  return SA_OK;
+}
+
+void sa_sketch_result_free(sa_sketch_result *r) { delete reinterpret_cast<sketch_holder *>(r); }
+
+int sa_window_advance(sa_engine *e, uint64_t new_base) {
+  if (!e) return SA_EINVAL;
+  if (new_base < e->win_base) return fail(e, SA_EINVAL, "window base cannot move backwards");
+  if (int rc = set_dev(e)) return rc;
+  const uint64_t n = std::min<uint64_t>(new_base - e->win_base, e->cfg.n_windows);
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint64_t ws = (e->win_base + k) & (e->cfg.n_windows - 1);
+    SA_HIP(e, hipMemsetAsync(e->hll + ws * e->hll_slot_bytes, 0, e->hll_slot_bytes, e->stream));
+    SA_HIP(e, hipMemsetAsync(e->cms + ws * e->cms_slot_elems, 0, e->cms_slot_elems * 8, e->stream));
+  }
+  e->win_base = new_base;
+  return SA_OK;
+}
+
+int sa_get_stats(sa_engine *e, sa_stats *o) {
+  if (!e || !o) return SA_EINVAL;
+  if (int rc = set_dev(e)) return rc;
+  uint64_t st[sa::kNumStats];
+  SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, e->stream));
+  SA_HIP(e, sa::launch_count_keys(e->gkeys, e->cap, e->scratch, e->stream));
+  uint64_t nk = 0;
+  SA_HIP(e, hipMemcpyAsync(&nk, e->scratch, 8, hipMemcpyDeviceToHost, e->stream));
+  if (int rc = read_stats(e, st)) return rc;
+  std::memset(o, 0, sizeof *o);
+  o->spans = e->spans;
+  o->zero_key = st[sa::kStatZeroKey];
+  o->invalid_service = st[sa::kStatInvalidService];
+  o->window_out_of_range = st[sa::kStatWindowOOR];
+  o->dropped_table_full = st[sa::kStatDropped];
+  o->n_keys = nk;
+  o->table_capacity = e->cap;
+  o->window_base = e->win_base;
+  o->small_table = e->small ? 1 : 0;
+  return SA_OK;
+}
+
+int sa_export_keys(sa_engine *e, uint64_t *d_keys, uint64_t cap, uint64_t *n_out, void *stream) {
+  if (!e || !n_out || (cap && !d_keys)) return SA_EINVAL;
+  if (int rc = set_dev(e)) return rc;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+  if (s != e->stream) {
+    SA_HIP(e, hipEventRecord(e->ev_a, e->stream));
+    SA_HIP(e, hipStreamWaitEvent(s, e->ev_a, 0));
+  }
+  if (int rc = reduce_slabs(e, s)) return rc;
+  SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, s));
+  SA_HIP(e, sa::launch_compact(e->gkeys, e->gcounts, e->cap, e->nbk + 1,
+                               reinterpret_cast<unsigned long long *>(d_keys), nullptr, e->scratch,
+                               cap, 0, s));
+  SA_HIP(e, hipMemcpyAsync(n_out, e->scratch, 8, hipMemcpyDeviceToHost, s));
+  SA_HIP(e, hipStreamSynchronize(s));
+  return SA_OK;
+}
+
+int sa_gather_dense(sa_engine *e, const uint64_t *d_keys, uint64_t n, uint64_t *d_rows, int reset,
+                    void *stream) {
+  if (!e || (n && (!d_keys || !d_rows))) return SA_EINVAL;
+  if (int rc = set_dev(e)) return rc;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+  if (s != e->stream) {
+    SA_HIP(e, hipEventRecord(e->ev_a, e->stream));
+    SA_HIP(e, hipStreamWaitEvent(s, e->ev_a, 0));
+  }
+  if (int rc = reduce_slabs(e, s)) return rc;
+  SA_HIP(e, sa::launch_gather_dense(e->gkeys, e->gcounts, e->log2cap, kMaxProbe, e->nbk + 1,
+                                    d_keys, n, d_rows, s));
+  if (reset) SA_HIP(e, hipMemsetAsync(e->gcounts, 0, e->cap * (e->nbk + 1) * 8, s));
+  if (s != e->stream) {
+    SA_HIP(e, hipEventRecord(e->ev_b, s));
+    SA_HIP(e, hipStreamWaitEvent(e->stream, e->ev_b, 0));
+  }
+  return SA_OK;
+}
+
+int sa_window_export(sa_engine *e, uint64_t window_id, uint8_t *d_hll, uint64_t *d_cms,
+                     void *stream) {
+  if (!e) return SA_EINVAL;
+  if (!resident(e, window_id)) return fail(e, SA_ERANGE, "window not resident");
+  if (int rc = set_dev(e)) return rc;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+  if (s != e->stream) {
+    SA_HIP(e, hipEventRecord(e->ev_a, e->stream));
+    SA_HIP(e, hipStreamWaitEvent(s, e->ev_a, 0));
+  }
+  const uint64_t ws = window_id & (e->cfg.n_windows - 1);
+  if (d_hll)
+    SA_HIP(e, hipMemcpyAsync(d_hll, e->hll + ws * e->hll_slot_bytes, e->hll_slot_bytes,
+                             hipMemcpyDeviceToDevice, s));
+  if (d_cms)
+    SA_HIP(e, hipMemcpyAsync(d_cms, e->cms + ws * e->cms_slot_elems, e->cms_slot_elems * 8,
+                             hipMemcpyDeviceToDevice, s));
+  if (s != e->stream) {
+    SA_HIP(e, hipEventRecord(e->ev_b, s));
+    SA_HIP(e, hipStreamWaitEvent(e->stream, e->ev_b, 0));
+  }
+  return SA_OK;
+}
+
+}  // extern "C"

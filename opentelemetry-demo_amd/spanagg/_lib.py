@@ -1,0 +1,118 @@
+"""ctypes binding of libspanagg's C-ABI (include/spanagg.h).
+
+The shared library is built in-tree (``make -C opentelemetry-demo_amd``) next to
+this file.  There is no fallback: if the library is missing, ``load()`` raises,
+and if no gfx950 device is present ``sa_create`` fails with SA_EDEVICE.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libspanagg.so")
+
+SA_OK, SA_EINVAL, SA_ENOMEM, SA_EDEVICE, SA_EFULL, SA_ERANGE, SA_ESTATE = 0, -1, -2, -3, -4, -5, -6
+SA_UNIT_MS, SA_UNIT_S = 0, 1
+SA_MAX_BOUNDS = 62
+STATUS_NAMES = {
+    SA_OK: "SA_OK", SA_EINVAL: "SA_EINVAL", SA_ENOMEM: "SA_ENOMEM", SA_EDEVICE: "SA_EDEVICE",
+    SA_EFULL: "SA_EFULL", SA_ERANGE: "SA_ERANGE", SA_ESTATE: "SA_ESTATE",
+}
+
+u64p = C.POINTER(C.c_uint64)
+u32p = C.POINTER(C.c_uint32)
+u8p = C.POINTER(C.c_uint8)
+f64p = C.POINTER(C.c_double)
+
+
+class sa_config(C.Structure):
+    _fields_ = [
+        ("bounds", f64p), ("n_bounds", C.c_uint32), ("unit", C.c_uint32),
+        ("hll_p", C.c_uint32), ("cms_d", C.c_uint32), ("cms_w", C.c_uint32),
+        ("window_ns", C.c_uint64), ("n_windows", C.c_uint32), ("n_services", C.c_uint32),
+        ("key_capacity", C.c_uint64), ("device", C.c_int32), ("flags", C.c_uint32),
+    ]
+
+
+class sa_span_batch(C.Structure):
+    _fields_ = [
+        ("key_hash", C.c_void_p), ("start_ns", C.c_void_p), ("end_ns", C.c_void_p),
+        ("trace_w0", C.c_void_p), ("trace_w1", C.c_void_p), ("meta", C.c_void_p),
+        ("n", C.c_uint64),
+    ]
+
+
+class sa_red_result(C.Structure):
+    _fields_ = [
+        ("n_series", C.c_uint64), ("n_buckets", C.c_uint32),
+        ("key_hash", u64p), ("bucket_counts", u64p), ("calls", u64p),
+        ("sum_ns", u64p), ("sum", f64p),
+    ]
+
+
+class sa_sketch_result(C.Structure):
+    _fields_ = [
+        ("window_id", C.c_uint64), ("n_services", C.c_uint32), ("hll_p", C.c_uint32),
+        ("hll", u8p), ("cms_d", C.c_uint32), ("cms_w", C.c_uint32), ("cms", u32p),
+    ]
+
+
+class sa_stats(C.Structure):
+    _fields_ = [
+        ("spans", C.c_uint64), ("zero_key", C.c_uint64), ("invalid_service", C.c_uint64),
+        ("window_out_of_range", C.c_uint64), ("dropped_table_full", C.c_uint64),
+        ("n_keys", C.c_uint64), ("table_capacity", C.c_uint64), ("window_base", C.c_uint64),
+        ("small_table", C.c_uint32), ("pad", C.c_uint32),
+    ]
+
+
+# (name, restype, argtypes) for every entry point declared in include/spanagg.h
+SIGNATURES = [
+    ("sa_config_default", None, [C.POINTER(sa_config)]),
+    ("sa_abi_version", C.c_int, []),
+    ("sa_create", C.c_int, [C.POINTER(sa_config), C.POINTER(C.c_void_p)]),
+    ("sa_destroy", None, [C.c_void_p]),
+    ("sa_last_error", C.c_char_p, [C.c_void_p]),
+    ("sa_ingest", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch)]),
+    ("sa_ingest_device", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch), C.c_void_p]),
+    ("sa_sync", C.c_int, [C.c_void_p]),
+    ("sa_flush", C.c_int, [C.c_void_p, C.POINTER(C.POINTER(sa_red_result))]),
+    ("sa_red_result_free", None, [C.POINTER(sa_red_result)]),
+    ("sa_window_read", C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.POINTER(sa_sketch_result))]),
+    ("sa_window_advance", C.c_int, [C.c_void_p, C.c_uint64]),
+    ("sa_sketch_result_free", None, [C.POINTER(sa_sketch_result)]),
+    ("sa_get_stats", C.c_int, [C.c_void_p, C.POINTER(sa_stats)]),
+    ("sa_export_keys", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, u64p, C.c_void_p]),
+    ("sa_gather_dense", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int, C.c_void_p]),
+    ("sa_window_export", C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("sa_bucket_thresholds", C.c_int, [f64p, C.c_uint32, C.c_uint32, u64p, u32p]),
+    ("sa_hll_estimate", C.c_double, [u8p, C.c_uint32]),
+]
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libspanagg.so (in-tree build). Raises if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libspanagg.so not found at {LIB_PATH}; build it with "
+                "`make -C opentelemetry-demo_amd` (or __graft_entry__.build())")
+        lib = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.sa_abi_version() != 1:
+            raise RuntimeError("libspanagg ABI version mismatch")
+        _lib = lib
+    return _lib
+
+
+class SpanAggError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{STATUS_NAMES.get(code, code)}: {msg}")
+        self.code = code

@@ -1,0 +1,256 @@
+"""Python host wrapper of one libspanagg engine (one engine per GPU / rank).
+
+Maps the connector's lifecycle onto the C-ABI:
+``Engine(config)`` ~ createTracesToMetricsConnector + Start, ``ingest`` ~ the
+per-span body of ConsumeTraces, ``flush`` ~ exportMetrics' buildMetrics +
+resetState (delta since the previous flush), ``close`` ~ Shutdown.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import SpanAggError
+
+DEFAULT_BOUNDS_MS = (2, 4, 6, 8, 10, 50, 100, 200, 400, 800, 1000, 1400, 2000, 5000, 10000, 15000)
+
+KIND_SHIFT, STATUS_SHIFT = 16, 19
+
+
+def pack_meta(service_id, kind, status) -> np.ndarray:
+    """meta = service_id | kind << 16 | status << 19 (SoA v1)."""
+    s = np.asarray(service_id, dtype=np.uint32)
+    k = np.asarray(kind, dtype=np.uint32)
+    c = np.asarray(status, dtype=np.uint32)
+    if np.any(s > 0xFFFF) or np.any(k > 7) or np.any(c > 3):
+        raise ValueError("meta field out of range")
+    return (s | (k << KIND_SHIFT) | (c << STATUS_SHIFT)).astype(np.uint32)
+
+
+def trace_words(trace_ids: np.ndarray):
+    """[n,16] u8 wire trace ids -> (w0, w1) little-endian u64 words."""
+    t = np.ascontiguousarray(trace_ids, dtype=np.uint8).reshape(-1, 16)
+    w = t.view("<u8").reshape(-1, 2)
+    return np.ascontiguousarray(w[:, 0]), np.ascontiguousarray(w[:, 1])
+
+
+@dataclass
+class Config:
+    """Mirror of the spanmetrics Config fields this engine consumes plus the
+    build-owned sketch parameters (defaults = the reference's empty
+    `spanmetrics:` block, otelcol-config.yml:115-116)."""
+    bounds: Sequence[float] = DEFAULT_BOUNDS_MS
+    unit: str = "ms"
+    hll_p: int = 14
+    cms_d: int = 4
+    cms_w: int = 2048
+    window_ns: int = 10_000_000_000
+    n_windows: int = 8
+    n_services: int = 64
+    key_capacity: int = 1000
+    device: int = 0
+
+    def to_c(self):
+        arr = (C.c_double * max(1, len(self.bounds)))(*[float(b) for b in self.bounds])
+        c = _lib.sa_config()
+        c.bounds = C.cast(arr, _lib.f64p)
+        c.n_bounds = len(self.bounds)
+        c.unit = _lib.SA_UNIT_S if self.unit == "s" else _lib.SA_UNIT_MS
+        c.hll_p, c.cms_d, c.cms_w = self.hll_p, self.cms_d, self.cms_w
+        c.window_ns, c.n_windows, c.n_services = self.window_ns, self.n_windows, self.n_services
+        c.key_capacity, c.device, c.flags = self.key_capacity, self.device, 0
+        return c, arr
+
+
+@dataclass
+class SpanBatch:
+    key_hash: np.ndarray
+    start_ns: np.ndarray
+    end_ns: np.ndarray
+    trace_w0: np.ndarray
+    trace_w1: np.ndarray
+    meta: np.ndarray
+
+    def __post_init__(self):
+        for name in ("key_hash", "start_ns", "end_ns", "trace_w0", "trace_w1"):
+            setattr(self, name, np.ascontiguousarray(getattr(self, name), dtype=np.uint64))
+        self.meta = np.ascontiguousarray(self.meta, dtype=np.uint32)
+        n = len(self.key_hash)
+        if any(len(getattr(self, f)) != n for f in
+               ("start_ns", "end_ns", "trace_w0", "trace_w1", "meta")):
+            raise ValueError("ragged SoA batch")
+
+    def __len__(self):
+        return len(self.key_hash)
+
+    def slice(self, a: int, b: int) -> "SpanBatch":
+        return SpanBatch(self.key_hash[a:b], self.start_ns[a:b], self.end_ns[a:b],
+                         self.trace_w0[a:b], self.trace_w1[a:b], self.meta[a:b])
+
+    def columns(self):
+        return (self.key_hash, self.start_ns, self.end_ns, self.trace_w0, self.trace_w1, self.meta)
+
+
+@dataclass
+class RedResult:
+    key_hash: np.ndarray          # [n] u64, ascending
+    bucket_counts: np.ndarray     # [n, n_buckets] u64
+    calls: np.ndarray             # [n] u64
+    sum_ns: np.ndarray            # [n] u64
+    sum: np.ndarray               # [n] f64 (ms or s)
+    status: int = 0
+
+
+@dataclass
+class SketchResult:
+    window_id: int
+    hll: np.ndarray               # [n_services, 2^p] u8
+    cms: np.ndarray               # [d, w] u32
+    p: int = 14
+
+    def distinct_traces(self, service_id: int) -> float:
+        return hll_estimate(self.hll[service_id], self.p)
+
+
+def hll_estimate(regs: np.ndarray, p: int) -> float:
+    lib = _lib.load()
+    r = np.ascontiguousarray(regs, dtype=np.uint8)
+    return float(lib.sa_hll_estimate(r.ctypes.data_as(_lib.u8p), p))
+
+
+def bucket_thresholds(bounds, unit: str = "ms"):
+    lib = _lib.load()
+    b = np.ascontiguousarray(bounds, dtype=np.float64)
+    thr = np.zeros(max(1, len(b)), dtype=np.uint64)
+    nneg = C.c_uint32(0)
+    rc = lib.sa_bucket_thresholds(b.ctypes.data_as(_lib.f64p), len(b),
+                                  _lib.SA_UNIT_S if unit == "s" else _lib.SA_UNIT_MS,
+                                  thr.ctypes.data_as(_lib.u64p), C.byref(nneg))
+    if rc != 0:
+        raise SpanAggError(rc, "invalid histogram bounds")
+    return thr[: len(b) - nneg.value], nneg.value
+
+
+def _ptr(x) -> int:
+    """Device pointer of a torch tensor, or an int passthrough."""
+    if isinstance(x, int):
+        return x
+    return int(x.data_ptr())
+
+
+class Engine:
+    def __init__(self, config: Optional[Config] = None, **kw):
+        self.lib = _lib.load()
+        self.config = config or Config(**kw)
+        c, self._bounds_keepalive = self.config.to_c()
+        h = C.c_void_p()
+        rc = self.lib.sa_create(C.byref(c), C.byref(h))
+        if rc != 0:
+            raise SpanAggError(rc, "sa_create failed (is a gfx950 GPU visible?)")
+        self._h = h
+        self.n_buckets = len(self.config.bounds) + 1
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.sa_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            raise SpanAggError(rc, f"{what}: {self.lib.sa_last_error(self._h).decode()}")
+
+    # -- hot path ----------------------------------------------------------
+    def ingest(self, batch: SpanBatch):
+        b = _lib.sa_span_batch(*[c.ctypes.data for c in batch.columns()], len(batch))
+        self._check(self.lib.sa_ingest(self._h, C.byref(b)), "sa_ingest")
+
+    def ingest_device(self, key, start, end, w0, w1, meta, n: Optional[int] = None,
+                      stream: Optional[int] = None):
+        """Device-resident batch: torch tensors (or raw device pointers)."""
+        if n is None:
+            n = int(key.numel())
+        b = _lib.sa_span_batch(_ptr(key), _ptr(start), _ptr(end), _ptr(w0), _ptr(w1),
+                               _ptr(meta), n)
+        self._check(self.lib.sa_ingest_device(self._h, C.byref(b), C.c_void_p(stream or 0)),
+                    "sa_ingest_device")
+
+    def sync(self):
+        self._check(self.lib.sa_sync(self._h), "sa_sync")
+
+    # -- export ------------------------------------------------------------
+    def flush(self, allow_drops: bool = False) -> RedResult:
+        out = C.POINTER(_lib.sa_red_result)()
+        rc = self.lib.sa_flush(self._h, C.byref(out))
+        if rc not in (0, _lib.SA_EFULL) or not out:
+            self._check(rc, "sa_flush")
+        try:
+            r = out.contents
+            n, nb = int(r.n_series), int(r.n_buckets)
+
+            def arr(p, shape, dt):
+                if n == 0:
+                    return np.zeros(shape, dtype=dt)
+                return np.ctypeslib.as_array(p, shape=shape).copy()
+
+            res = RedResult(arr(r.key_hash, (n,), np.uint64),
+                            arr(r.bucket_counts, (n, nb), np.uint64),
+                            arr(r.calls, (n,), np.uint64), arr(r.sum_ns, (n,), np.uint64),
+                            arr(r.sum, (n,), np.float64), rc)
+        finally:
+            self.lib.sa_red_result_free(out)
+        if rc == _lib.SA_EFULL and not allow_drops:
+            self._check(rc, "sa_flush")
+        return res
+
+    def window_read(self, window_id: int) -> SketchResult:
+        out = C.POINTER(_lib.sa_sketch_result)()
+        self._check(self.lib.sa_window_read(self._h, window_id, C.byref(out)), "sa_window_read")
+        try:
+            r = out.contents
+            hll = np.ctypeslib.as_array(r.hll, shape=(r.n_services, 1 << r.hll_p)).copy()
+            cms = np.ctypeslib.as_array(r.cms, shape=(r.cms_d, r.cms_w)).copy()
+            return SketchResult(int(r.window_id), hll, cms, int(r.hll_p))
+        finally:
+            self.lib.sa_sketch_result_free(out)
+
+    def window_advance(self, new_base: int):
+        self._check(self.lib.sa_window_advance(self._h, int(new_base)), "sa_window_advance")
+
+    def stats(self) -> dict:
+        s = _lib.sa_stats()
+        self._check(self.lib.sa_get_stats(self._h, C.byref(s)), "sa_get_stats")
+        return {name: int(getattr(s, name)) for name, _ in _lib.sa_stats._fields_ if name != "pad"}
+
+    # -- multi-GPU merge hooks (device pointers) ----------------------------
+    def export_keys(self, d_keys, cap: int, stream: Optional[int] = None) -> int:
+        n = C.c_uint64(0)
+        self._check(self.lib.sa_export_keys(self._h, C.c_void_p(_ptr(d_keys) if cap else 0), cap,
+                                            C.byref(n), C.c_void_p(stream or 0)), "sa_export_keys")
+        return int(n.value)
+
+    def gather_dense(self, d_keys, n: int, d_rows, reset: bool, stream: Optional[int] = None):
+        self._check(self.lib.sa_gather_dense(self._h, C.c_void_p(_ptr(d_keys) if n else 0), n,
+                                             C.c_void_p(_ptr(d_rows) if n else 0), int(reset),
+                                             C.c_void_p(stream or 0)), "sa_gather_dense")
+
+    def window_export(self, window_id: int, d_hll, d_cms, stream: Optional[int] = None):
+        self._check(self.lib.sa_window_export(self._h, window_id, C.c_void_p(_ptr(d_hll)),
+                                              C.c_void_p(_ptr(d_cms)), C.c_void_p(stream or 0)),
+                    "sa_window_export")

@@ -1,0 +1,266 @@
+"""GPU parity: libspanagg's HIP path vs the golden vectors and the CPU oracle.
+
+Bar (north_star): bucket counts, calls, HLL registers and CMS cells bit-exact;
+duration sums within 1e-9 relative (the engine sums exact u64 ns; the oracle
+sums float64 ms in Go's arrival order).
+"""
+import numpy as np
+import pytest
+
+import pyoracle
+from parity_util import assert_red_equal, assert_red_golden, sketch_sparse
+from spanagg import Config, Engine, SpanBatch, pack_meta
+from spanagg import _lib
+from spanagg.synth import generate_c2, generate_highcard
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(spans):
+    cols = list(zip(*spans)) if spans else [[]] * 6
+    mk = lambda i, dt: np.array([int(x) for x in cols[i]], dtype=dt)
+    return SpanBatch(mk(0, np.uint64), mk(1, np.uint64), mk(2, np.uint64), mk(3, np.uint64),
+                     mk(4, np.uint64), mk(5, np.uint32))
+
+
+def _pow2_at_least(x):
+    p = 1
+    while p < x:
+        p <<= 1
+    return p
+
+
+def engine_for_case(case, key_capacity=1000, **kw):
+    wins = [w["window"] for w in case["expected"]["windows"]]
+    lo = min(wins) if wins else 0
+    nwin = _pow2_at_least((max(wins) - lo + 1) if wins else 1)
+    e = Engine(Config(bounds=case["bounds"], unit=case["unit"], hll_p=case["hll_p"],
+                      cms_d=case["cms_d"], cms_w=case["cms_w"], window_ns=case["window_ns"],
+                      n_windows=nwin, n_services=case["n_services"], key_capacity=key_capacity,
+                      **kw))
+    e.window_advance(lo)
+    return e
+
+
+@pytest.mark.parametrize("idx", range(5))
+@pytest.mark.parametrize("key_capacity", [1000, 300_000])  # LDS-mirrored and HBM-table paths
+def test_golden_cases(golden, idx, key_capacity):
+    case = golden["cases"][idx]
+    with engine_for_case(case, key_capacity=key_capacity) as e:
+        assert e.stats()["small_table"] == (1 if key_capacity == 1000 else 0)
+        e.ingest(_batch(case["spans"]))
+        res = e.flush()
+        assert_red_golden(res, case["expected"]["series"])
+        for w in case["expected"]["windows"]:
+            sk = e.window_read(w["window"])
+            h, c = sketch_sparse(sk.hll, sk.cms)
+            assert h == w["hll"], case["name"]
+            assert c == w["cms"], case["name"]
+        st = e.stats()
+        exp = case["expected"]["stats"]
+        assert st["spans"] == exp["spans"]
+        assert st["zero_key"] == exp["zero_key"]
+        assert st["invalid_service"] == exp["invalid_service"]
+        assert st["window_out_of_range"] == 0
+        assert st["dropped_table_full"] == 0
+
+
+def _oracle_run(wl_batch, n_services, **kw):
+    o = pyoracle.Oracle(n_services=n_services, **kw)
+    o.ingest(wl_batch)
+    return o
+
+
+def _check_windows(e, o, first_window, n_services):
+    ids = o.window_ids()
+    assert ids, "no windows"
+    for wid in ids:
+        sk = e.window_read(wid)
+        hll, cms = o.window(wid)
+        assert np.array_equal(sk.hll, hll), wid
+        assert np.array_equal(sk.cms, cms), wid
+        for s in range(n_services):
+            assert sk.distinct_traces(s) == pytest.approx(pyoracle.hll_estimate(hll[s], 14),
+                                                          rel=1e-12)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 1023, 2049, 100_003])
+def test_c2_small_sizes_vs_oracle(n):
+    wl = generate_c2(n, seed=n)
+    with Engine(Config(n_services=wl.n_services, n_windows=16)) as e:
+        e.window_advance(wl.first_window)
+        e.ingest(wl.batch)
+        res = e.flush()
+        o = _oracle_run(wl.batch, wl.n_services)
+        assert_red_equal(res, o.series())
+        _check_windows(e, o, wl.first_window, wl.n_services)
+
+
+def test_empty_batch():
+    with Engine(Config()) as e:
+        e.ingest(SpanBatch(*(np.zeros(0, np.uint64) for _ in range(5)), np.zeros(0, np.uint32)))
+        res = e.flush()
+        assert len(res.key_hash) == 0
+        assert e.stats()["spans"] == 0
+
+
+def test_ragged_batch_rejected():
+    with pytest.raises(ValueError):
+        SpanBatch(np.zeros(3, np.uint64), np.zeros(2, np.uint64), np.zeros(3, np.uint64),
+                  np.zeros(3, np.uint64), np.zeros(3, np.uint64), np.zeros(3, np.uint32))
+
+
+def test_c2_full_size_bit_exact():
+    """BASELINE config 2 at full size: 10M spans, default buckets."""
+    wl = generate_c2(10_000_000, seed=42)
+    with Engine(Config(n_services=wl.n_services, n_windows=16)) as e:
+        e.window_advance(wl.first_window)
+        e.ingest(wl.batch)
+        res = e.flush()
+        o = _oracle_run(wl.batch, wl.n_services)
+        assert_red_equal(res, o.series())
+        _check_windows(e, o, wl.first_window, wl.n_services)
+        # size-independent properties
+        assert int(res.calls.sum()) == 10_000_000 - e.stats()["zero_key"]
+        assert e.stats()["dropped_table_full"] == 0
+
+
+def test_device_ingest_matches_host_ingest():
+    import torch
+    wl = generate_c2(500_000, seed=5)
+    cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).cuda()
+            for c in wl.batch.columns()]
+    with Engine(Config(n_services=wl.n_services, n_windows=16)) as e1, \
+            Engine(Config(n_services=wl.n_services, n_windows=16)) as e2:
+        e1.window_advance(wl.first_window)
+        e2.window_advance(wl.first_window)
+        e1.ingest(wl.batch)
+        stream = torch.cuda.current_stream().cuda_stream
+        # several device batches on torch's stream, split at odd offsets
+        cuts = [0, 1, 77_777, 300_001, 500_000]
+        for a, b in zip(cuts, cuts[1:]):
+            sl = [c[a:b] for c in cols]
+            # sub-views must stay 16-B aligned: re-materialise odd offsets
+            sl = [s.clone() for s in sl]
+            e2.ingest_device(*sl, n=b - a, stream=stream)
+        torch.cuda.synchronize()
+        r1, r2 = e1.flush(), e2.flush()
+        for f in ("key_hash", "bucket_counts", "calls", "sum_ns"):
+            assert np.array_equal(getattr(r1, f), getattr(r2, f))
+        for wid in range(wl.first_window, wl.first_window + 10):
+            a, b = e1.window_read(wid), e2.window_read(wid)
+            assert np.array_equal(a.hll, b.hll) and np.array_equal(a.cms, b.cms)
+
+
+def test_flush_is_delta_and_resets():
+    wl = generate_c2(200_000, seed=9)
+    half = 100_000
+    with Engine(Config(n_services=wl.n_services, n_windows=16)) as e:
+        e.window_advance(wl.first_window)
+        e.ingest(wl.batch.slice(0, half))
+        r1 = e.flush()
+        e.ingest(wl.batch.slice(half, len(wl.batch)))
+        r2 = e.flush()
+        r3 = e.flush()
+        assert len(r3.key_hash) == 0
+        o1 = _oracle_run(wl.batch.slice(0, half), wl.n_services)
+        o2 = _oracle_run(wl.batch.slice(half, len(wl.batch)), wl.n_services)
+        assert_red_equal(r1, o1.series())
+        assert_red_equal(r2, o2.series())
+
+
+def test_epoch_flush_u16_counters():
+    """> 65,535 spans of one (key, bucket) per workgroup: exercises the LDS
+    u16 epoch flush into the workgroup slabs."""
+    import torch
+    n = 40_000_000
+    dev = "cuda"
+    key = torch.full((n,), 12345, dtype=torch.int64, device=dev)
+    start = torch.full((n,), 10**18, dtype=torch.int64, device=dev)
+    end = start + 1_000_000
+    w0 = torch.arange(n, dtype=torch.int64, device=dev)
+    w1 = torch.zeros(n, dtype=torch.int64, device=dev)
+    meta = torch.zeros(n, dtype=torch.int32, device=dev)
+    with Engine(Config(n_windows=8)) as e:
+        e.window_advance(10**18 // 10**10)
+        e.ingest_device(key, start, end, w0, w1, meta, stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        res = e.flush()
+        assert res.key_hash.tolist() == [12345]
+        assert int(res.bucket_counts[0, 0]) == n
+        assert int(res.bucket_counts[0].sum()) == n
+        assert int(res.sum_ns[0]) == n * 1_000_000
+
+
+def test_table_full_reports_drops():
+    rng = np.random.default_rng(1)
+    n = 5000
+    keys = rng.integers(1, 2**63, 200, dtype=np.int64).astype(np.uint64)
+    b = SpanBatch(keys[rng.integers(0, 200, n)], np.full(n, 10**18, np.uint64),
+                  np.full(n, 10**18 + 5, np.uint64), rng.integers(0, 2**62, n).astype(np.uint64),
+                  np.zeros(n, np.uint64), np.zeros(n, np.uint32))
+    with Engine(Config(key_capacity=8)) as e:  # 16 slots
+        e.window_advance(10**18 // 10**10)
+        e.ingest(b)
+        with pytest.raises(_lib.SpanAggError) as ei:
+            e.flush()
+        assert ei.value.code == _lib.SA_EFULL
+        st = e.stats()
+        assert st["n_keys"] == 16
+        assert st["dropped_table_full"] > 0
+    with Engine(Config(key_capacity=8)) as e:
+        e.ingest(b)
+        res = e.flush(allow_drops=True)
+        assert int(res.calls.sum()) + e.stats()["dropped_table_full"] == n
+
+
+def test_window_ring_out_of_range_and_advance():
+    base = 176_722_560
+    w = 10_000_000_000
+    ends = np.array([(base + k) * w + 5 for k in (-1, 0, 1, 3, 4, 9)], dtype=np.uint64)
+    n = len(ends)
+    b = SpanBatch(np.arange(1, n + 1, dtype=np.uint64), ends - 1, ends, np.arange(n, dtype=np.uint64),
+                  np.ones(n, np.uint64), pack_meta(np.zeros(n), 2, 2))
+    with Engine(Config(n_windows=4)) as e:
+        e.window_advance(base)
+        e.ingest(b)
+        assert e.stats()["window_out_of_range"] == 3   # base-1, base+4, base+9
+        s0 = e.window_read(base)
+        assert s0.hll.sum() > 0 and s0.cms.sum() == 4  # one ERROR span x 4 rows
+        with pytest.raises(_lib.SpanAggError):
+            e.window_read(base + 4)
+        e.window_advance(base + 2)
+        with pytest.raises(_lib.SpanAggError):
+            e.window_read(base)
+        s3 = e.window_read(base + 3)
+        assert s3.cms.sum() == 4
+        s5 = e.window_read(base + 5)                   # recycled slot starts clean
+        assert s5.hll.sum() == 0 and s5.cms.sum() == 0
+
+
+def test_high_cardinality_hbm_table_vs_oracle():
+    """Config 4 shape at reduced size: HBM key-table path with many keys."""
+    batch, khash, w0 = generate_highcard(1_000_000, routes=400, pods=250)
+    with Engine(Config(n_services=1, n_windows=16, key_capacity=200_000)) as e:
+        assert e.stats()["small_table"] == 0
+        e.window_advance(w0)
+        e.ingest(batch)
+        res = e.flush()
+        o = _oracle_run(batch, 1)
+        assert_red_equal(res, o.series())
+        for wid in o.window_ids():
+            sk = e.window_read(wid)
+            hll, cms = o.window(wid)
+            assert np.array_equal(sk.hll, hll) and np.array_equal(sk.cms, cms)
+
+
+def test_repeat_runs_identical():
+    wl = generate_c2(1_000_000, seed=77)
+    outs = []
+    for _ in range(2):
+        with Engine(Config(n_services=wl.n_services, n_windows=16)) as e:
+            e.window_advance(wl.first_window)
+            e.ingest(wl.batch)
+            outs.append(e.flush())
+    for f in ("key_hash", "bucket_counts", "sum_ns"):
+        assert np.array_equal(getattr(outs[0], f), getattr(outs[1], f))
