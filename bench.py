@@ -131,7 +131,9 @@ def main():
     eng = Engine(Config(n_services=max(n_services, 1), n_windows=16, key_capacity=key_capacity,
                         device=local_rank))
     eng.window_advance(first_window)
-    stream = torch.cuda.current_stream(device)
+    # a dedicated (non-null) stream: the kernels and the timing events share it
+    stream = torch.cuda.Stream(device)
+    torch.cuda.set_stream(stream)
 
     def step():
         eng.ingest_device(*cols, n=n, stream=stream.cuda_stream)

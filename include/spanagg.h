@@ -62,6 +62,12 @@ typedef enum {
 
 typedef enum { SA_UNIT_MS = 0, SA_UNIT_S = 1 } sa_unit;
 
+/* Diagnostic ablations (sa_config.flags), used only to attribute kernel time. */
+#define SA_DIAG_NO_RED 1u     /* skip key lookup + counter updates */
+#define SA_DIAG_NO_HLL 2u     /* skip HLL hashing + register updates */
+#define SA_DIAG_NO_CMS 4u     /* skip count-min updates */
+#define SA_DIAG_NO_FLUSH 8u   /* skip the LDS -> slab flush */
+
 typedef struct {
     /* histogram.explicit.buckets (sorted ascending, finite) and histogram.unit */
     const double *bounds;
@@ -76,7 +82,8 @@ typedef struct {
     uint32_t n_services;    /* service ids 0..n_services-1 get sketches */
     uint64_t key_capacity;  /* expected distinct series; table sized >= 2x, pow2 */
     int32_t device;         /* HIP device ordinal (one engine per GPU / rank) */
-    uint32_t flags;         /* reserved, 0 */
+    uint32_t flags;         /* 0 for production; SA_DIAG_* bits are profiling-only
+                               ablations that skip work and make results WRONG */
 } sa_config;
 
 typedef struct {
@@ -167,6 +174,12 @@ int sa_gather_dense(sa_engine *e, const uint64_t *d_keys, uint64_t n, uint64_t *
  * d_cms [d][w] u64 (unsaturated, for sum all-reduce). */
 int sa_window_export(sa_engine *e, uint64_t window_id, uint8_t *d_hll, uint64_t *d_cms,
                      void *stream);
+
+/* Diagnostic only: per-workgroup s_memrealtime stamps (100 MHz) of the last
+ * small-table ingest launch, [G][8] = {start, after LDS setup, after the span
+ * loop, after the slab flush, 0...}; filled only when the engine was created
+ * with SPANAGG_STAMPS set in the environment (*n_out = 0 otherwise). */
+int sa_debug_stamps(sa_engine *e, uint64_t *out, uint64_t cap, uint64_t *n_out);
 
 /* ---- pure host helpers (no device needed) ---- */
 /* Integer bucket thresholds: bucket(d_ns) = n_neg + #{i : d_ns > thr[i]} equals

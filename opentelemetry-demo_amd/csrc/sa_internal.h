@@ -43,23 +43,36 @@ struct IngestParams {
   // sketches
   uint8_t *hll;                 // [W][S][2^p]
   unsigned long long *cms;      // [W][d][w]
+  unsigned long long *errcnt;   // [W][cap] exact ERROR-span counts per (window, key slot)
   uint64_t window_ns, win_magic, win_base;
   uint32_t win_mask, n_windows;
   uint32_t p, n_services, cms_d, cms_shift, cms_w;
-  uint32_t pad0;
+  uint32_t diag;  // SA_DIAG_* ablation bits (0 in production)
   uint64_t cms_seed[8];
   unsigned long long *stats;
+  unsigned long long *dbg;  // diagnostic timestamps [G][8] (nullptr in production)
 };
 
 __host__ __device__ inline uint64_t slot_of(uint64_t key, uint32_t log2cap) {
   return (key * kPhi) >> (64 - log2cap);
 }
 
+// Ingest kernel variants: spans per lane, next-tile prefetch, block size
+// (small-table path; the HBM-table path always uses 256-thread blocks).
+struct Variant {
+  int spl;
+  bool prefetch;
+  uint32_t block;
+};
+constexpr int kNumVariants = 4;
+constexpr Variant kVariants[kNumVariants] = {{4, false, 1024}, {2, true, 1024}, {4, true, 512},
+                                             {2, false, 1024}};
+constexpr uint32_t kHbmBlock = 256;
+
 // launchers (spanagg_kernels.hip)
-hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, uint32_t block,
-                               size_t lds_bytes, hipStream_t s);
-hipError_t launch_ingest_hbm(const IngestParams &P, uint32_t grid, uint32_t block,
-                             hipStream_t s);
+hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,
+                               hipStream_t s, int variant);
+hipError_t launch_ingest_hbm(const IngestParams &P, uint32_t grid, hipStream_t s, int variant);
 hipError_t prepare_ingest_small(size_t lds_bytes);
 hipError_t launch_reduce_slabs(uint32_t *slab_cnt, unsigned long long *slab_sum,
                                unsigned long long *gcounts, uint32_t G, uint64_t cap,
@@ -71,6 +84,9 @@ hipError_t launch_compact(const unsigned long long *gkeys, unsigned long long *g
 hipError_t launch_gather_dense(const unsigned long long *gkeys, const unsigned long long *gcounts,
                                uint32_t log2cap, uint32_t max_probe, uint32_t stride,
                                const uint64_t *keys, uint64_t n, uint64_t *rows, hipStream_t s);
+hipError_t launch_fold_errcnt(const unsigned long long *gkeys, unsigned long long *errcnt,
+                              uint64_t cap, unsigned long long *cms, uint32_t d, uint32_t w,
+                              uint32_t shift, const uint64_t *seeds, hipStream_t s);
 hipError_t launch_count_keys(const unsigned long long *gkeys, uint64_t cap,
                              unsigned long long *out, hipStream_t s);
 

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -26,10 +27,9 @@ constexpr uint64_t kCmsSeed[8] = {0x9E3779B97F4A7C15ULL, 0xBF58476D1CE4E5B9ULL,
                                   0xA0761D6478BD642FULL, 0xE7037ED1A0B428DBULL,
                                   0x8EBC6AF09C88C6E3ULL, 0x589965CC75374CC3ULL};
 constexpr size_t kLdsBudget = 144 * 1024;  // small-table path LDS ceiling per workgroup
-constexpr uint32_t kSmallBlock = 1024;
-constexpr uint32_t kHbmBlock = 256;
 constexpr uint32_t kMaxProbe = 4096;
 constexpr uint64_t kSlabLimit = 1ULL << 31;  // per-workgroup spans between slab reductions
+constexpr int kDefaultVariant = 0;            // sa::kVariants index (SPANAGG_VARIANT overrides)
 
 bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 uint32_t log2u(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
@@ -52,10 +52,15 @@ struct sa_engine {
   uint32_t log2cap = 0;
   uint64_t cap = 0;
   bool small = false;
+  int variant = 0;
+  uint32_t spl = 4;
   uint32_t G = 0, block = 0, cus = 0;
   size_t lds_bytes = 0;
   unsigned long long *gkeys = nullptr, *gcounts = nullptr, *slab_sum = nullptr, *cms = nullptr,
-                     *stats = nullptr, *out_keys = nullptr, *out_rows = nullptr, *scratch = nullptr;
+                     *stats = nullptr, *out_keys = nullptr, *out_rows = nullptr, *scratch = nullptr,
+                     *errcnt = nullptr;
+  uint64_t *d_seeds = nullptr;
+  unsigned long long *dbg = nullptr;  // SPANAGG_STAMPS diagnostic timestamps
   uint32_t *slab_cnt = nullptr;
   uint8_t *hll = nullptr;
   size_t hll_slot_bytes = 0, cms_slot_elems = 0;
@@ -216,7 +221,9 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     return rc;
   };
   if (int rc = set_dev(e)) return bail(rc);
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+  // A blocking stream: it orders against the legacy null stream, so callers
+  // that produce batches on the null stream (stream == NULL) stay race-free.
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamDefault) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_a, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_b, hipEventDisableTiming) != hipSuccess)
     return bail(fail(e, SA_EDEVICE, "stream/event creation failed"));
@@ -226,14 +233,19 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   const uint32_t nw = (e->nbk + 1) / 2;
   e->lds_bytes = (size_t)e->cap * 16 + (size_t)e->cap * nw * 4;
   e->small = e->lds_bytes <= kLdsBudget;
+  e->variant = kDefaultVariant;
+  if (const char *v = std::getenv("SPANAGG_VARIANT"))  // tuning knob for A/B runs
+    e->variant = std::max(0, std::min(sa::kNumVariants - 1, std::atoi(v)));
+  e->spl = (uint32_t)sa::kVariants[e->variant].spl;
   if (e->small) {
-    e->block = kSmallBlock;
-    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2, (uint32_t)((160 * 1024) / e->lds_bytes)));
+    e->block = sa::kVariants[e->variant].block;
+    const uint32_t per_cu = std::max<uint32_t>(
+        1, std::min<uint32_t>(2048 / e->block, (uint32_t)((160 * 1024) / e->lds_bytes)));
     e->G = e->cus * per_cu;
     if (hipError_t st = sa::prepare_ingest_small(e->lds_bytes); st != hipSuccess)
       return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
   } else {
-    e->block = kHbmBlock;
+    e->block = sa::kHbmBlock;
     e->G = e->cus * 8;
   }
 
@@ -251,10 +263,17 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       (rc = alloc((void **)&e->gcounts, e->cap * stride * 8)) ||
       (rc = alloc((void **)&e->hll, e->hll_slot_bytes * W)) ||
       (rc = alloc((void **)&e->cms, e->cms_slot_elems * W * 8)) ||
+      (rc = alloc((void **)&e->errcnt, (size_t)W * e->cap * 8)) ||
+      (rc = alloc((void **)&e->d_seeds, sizeof kCmsSeed)) ||
       (rc = alloc((void **)&e->stats, 64)) || (rc = alloc((void **)&e->scratch, 64)))
     return bail(rc);
+  if (std::getenv("SPANAGG_STAMPS") && (rc = alloc((void **)&e->dbg, (size_t)e->G * 64)))
+    return bail(rc);
+  if (hipMemcpy(e->d_seeds, kCmsSeed, sizeof kCmsSeed, hipMemcpyHostToDevice) != hipSuccess)
+    return bail(fail(e, SA_EDEVICE, "seed upload failed"));
   if (e->small) {
-    if ((rc = alloc((void **)&e->slab_cnt, (size_t)e->G * e->cap * e->nbk * 4)) ||
+    const size_t srow = (e->nbk + 1) & ~1u;  // slab row = 2 * ceil(nbk/2) u32 cells
+    if ((rc = alloc((void **)&e->slab_cnt, (size_t)e->G * e->cap * srow * 4)) ||
         (rc = alloc((void **)&e->slab_sum, (size_t)e->G * e->cap * 8)))
       return bail(rc);
   }
@@ -269,7 +288,9 @@ void sa_destroy(sa_engine *e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (void *p : {(void *)e->gkeys, (void *)e->gcounts, (void *)e->slab_sum, (void *)e->cms,
                   (void *)e->stats, (void *)e->out_keys, (void *)e->out_rows, (void *)e->scratch,
-                  (void *)e->slab_cnt, (void *)e->hll, e->stage})
+                  (void *)e->slab_cnt, (void *)e->hll, (void *)e->errcnt, (void *)e->d_seeds,
+                  (void *)e->dbg,
+                  e->stage})
     if (p) (void)hipFree(p);
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
   if (e->ev_b) (void)hipEventDestroy(e->ev_b);
@@ -286,13 +307,29 @@ static int reduce_slabs(sa_engine *e, hipStream_t s) {
   return SA_OK;
 }
 
+static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s);
+
+// Splits a batch so that each workgroup's range stays addressable by a 32-bit
+// buffer offset (< 2^27 spans per workgroup per launch).
 static int ingest_on(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
+  const uint64_t max_n = (uint64_t)e->G << 27;
+  for (uint64_t off = 0; off < b->n; off += max_n) {
+    const uint64_t m = std::min(max_n, b->n - off);
+    sa_span_batch sub{b->key_hash + off, b->start_ns + off, b->end_ns + off, b->trace_w0 + off,
+                      b->trace_w1 + off, b->meta + off, m};
+    if (int rc = ingest_launch(e, &sub, s)) return rc;
+  }
+  return SA_OK;
+}
+
+static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   if (b->n == 0) return SA_OK;
-  const uint64_t tile = (uint64_t)e->block * 2;
+  const uint64_t tile = (uint64_t)e->block * e->spl;
   const uint64_t tiles = (b->n + tile - 1) / tile;
+  // each workgroup gets one contiguous range of >= one tile (kernel: wg_range)
   const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, e->G);
   if (e->small) {
-    const uint64_t per_wg = ((tiles + grid - 1) / grid) * tile;
+    const uint64_t per_wg = ((b->n + grid - 1) / grid + 3) / 4 * 4;
     if (e->slab_load + per_wg > kSlabLimit)
       if (int rc = reduce_slabs(e, s)) return rc;
     e->slab_load += per_wg;
@@ -318,6 +355,7 @@ static int ingest_on(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.epoch_tiles = (uint32_t)(65535 / tile);
   P.hll = e->hll;
   P.cms = e->cms;
+  P.errcnt = e->errcnt;
   P.window_ns = e->cfg.window_ns;
   P.win_magic = UINT64_MAX / e->cfg.window_ns;
   P.win_base = e->win_base;
@@ -330,8 +368,10 @@ static int ingest_on(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.cms_shift = 64 - log2u(e->cfg.cms_w);
   std::memcpy(P.cms_seed, kCmsSeed, sizeof kCmsSeed);
   P.stats = e->stats;
-  hipError_t st = e->small ? sa::launch_ingest_small(P, grid, e->block, e->lds_bytes, s)
-                           : sa::launch_ingest_hbm(P, grid, e->block, s);
+  P.diag = e->cfg.flags;
+  P.dbg = e->dbg;
+  hipError_t st = e->small ? sa::launch_ingest_small(P, grid, e->lds_bytes, s, e->variant)
+                           : sa::launch_ingest_hbm(P, grid, s, e->variant);
   if (st != hipSuccess) return fail(e, SA_EDEVICE, std::string("ingest launch: ") + hipGetErrorString(st));
   e->spans += b->n;
   return SA_OK;
@@ -503,12 +543,22 @@ static bool resident(const sa_engine *e, uint64_t w) {
   return w >= e->win_base && w - e->win_base < e->cfg.n_windows;
 }
 
+// Derive the count-min cells of window slot ws from its exact per-slot error
+// counts (see sketch_post in spanagg_kernels.hip).
+static int fold_window(sa_engine *e, uint64_t ws, hipStream_t s) {
+  SA_HIP(e, sa::launch_fold_errcnt(e->gkeys, e->errcnt + ws * e->cap, e->cap,
+                                   e->cms + ws * e->cms_slot_elems, e->cfg.cms_d, e->cfg.cms_w,
+                                   64 - log2u(e->cfg.cms_w), e->d_seeds, s));
+  return SA_OK;
+}
+
 int sa_window_read(sa_engine *e, uint64_t window_id, sa_sketch_result **out) {
   if (!e || !out) return SA_EINVAL;
   *out = nullptr;
   if (!resident(e, window_id)) return fail(e, SA_ERANGE, "window not resident");
   if (int rc = set_dev(e)) return rc;
   const uint64_t ws = window_id & (e->cfg.n_windows - 1);
+  if (int rc = fold_window(e, ws, e->stream)) return rc;
   auto *h = new sketch_holder();
   h->hll.resize(e->hll_slot_bytes);
   std::vector<uint64_t> cms64(e->cms_slot_elems);
@@ -546,8 +596,19 @@ int sa_window_advance(sa_engine *e, uint64_t new_base) {
     const uint64_t ws = (e->win_base + k) & (e->cfg.n_windows - 1);
     SA_HIP(e, hipMemsetAsync(e->hll + ws * e->hll_slot_bytes, 0, e->hll_slot_bytes, e->stream));
     SA_HIP(e, hipMemsetAsync(e->cms + ws * e->cms_slot_elems, 0, e->cms_slot_elems * 8, e->stream));
+    SA_HIP(e, hipMemsetAsync(e->errcnt + ws * e->cap, 0, e->cap * 8, e->stream));
   }
   e->win_base = new_base;
+  return SA_OK;
+}
+
+int sa_debug_stamps(sa_engine *e, uint64_t *out, uint64_t cap, uint64_t *n_out) {
+  if (!e || !n_out) return SA_EINVAL;
+  *n_out = e->dbg ? (uint64_t)e->G * 8 : 0;
+  if (!e->dbg || !out) return SA_OK;
+  if (int rc = set_dev(e)) return rc;
+  SA_HIP(e, hipStreamSynchronize(e->stream));
+  SA_HIP(e, hipMemcpy(out, e->dbg, std::min<uint64_t>(cap, *n_out) * 8, hipMemcpyDeviceToHost));
   return SA_OK;
 }
 
@@ -622,6 +683,7 @@ int sa_window_export(sa_engine *e, uint64_t window_id, uint8_t *d_hll, uint64_t 
     SA_HIP(e, hipStreamWaitEvent(s, e->ev_a, 0));
   }
   const uint64_t ws = window_id & (e->cfg.n_windows - 1);
+  if (int rc = fold_window(e, ws, s)) return rc;
   if (d_hll)
     SA_HIP(e, hipMemcpyAsync(d_hll, e->hll + ws * e->hll_slot_bytes, e->hll_slot_bytes,
                              hipMemcpyDeviceToDevice, s));

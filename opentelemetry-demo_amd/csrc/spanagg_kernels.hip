@@ -51,13 +51,16 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return z ^ (z >> 31);
 }
 
-// floor(n / d) with magic = floor((2^64-1)/d): estimate is low by at most 2.
+// floor(n / d) with magic = floor((2^64-1)/d): the estimate is low by at most
+// 2, fixed by two branch-free correction steps.
 __device__ __forceinline__ uint64_t fast_div(uint64_t n, uint64_t d, uint64_t magic) {
   uint64_t q = __umul64hi(n, magic);
   uint64_t r = n - q * d;
-  while (r >= d) {
-    ++q;
-    r -= d;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const bool c = r >= d;
+    q += c ? 1 : 0;
+    r -= c ? d : 0;
   }
   return q;
 }
@@ -124,32 +127,6 @@ struct LaneStats {
   uint32_t zero_key, bad_svc, oor, dropped;
 };
 
-// Per-span sketch work: HLL of distinct trace ids per (window, service);
-// count-min of ERROR spans per window keyed by the series hash.
-// Returns 0 when applied, 1 for an invalid service id, 2 for a window outside
-// the resident ring.
-__device__ __forceinline__ uint32_t sketch_span(const IngestParams &P, uint64_t key, uint64_t end,
-                                                uint64_t w0, uint64_t w1, uint32_t meta) {
-  const uint32_t svc = meta & 0xFFFFu;
-  if (svc >= P.n_services) return 1;
-  const uint64_t win = fast_div(end, P.window_ns, P.win_magic);
-  if (win - P.win_base >= (uint64_t)P.n_windows) return 2;
-  const uint64_t ws = win & P.win_mask;
-  const uint64_t x = xxh64_16(w0, w1);
-  const uint64_t idx = x >> (64 - P.p);
-  const uint32_t rho = (uint32_t)__clzll((long long)((x << P.p) | (1ULL << (P.p - 1)))) + 1;
-  uint8_t *reg = P.hll + (((ws * P.n_services + svc) << P.p) + idx);
-  if (*reg < rho) hll_raise(reg, rho);
-  if (((meta >> 19) & 3u) == 2u) {
-    unsigned long long *row = P.cms + ws * P.cms_d * P.cms_w;
-    for (uint32_t j = 0; j < P.cms_d; ++j) {
-      const uint64_t col = splitmix64(key ^ P.cms_seed[j]) >> P.cms_shift;
-      atomicAdd(row + (uint64_t)j * P.cms_w + col, 1ULL);
-    }
-  }
-  return 0;
-}
-
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -167,39 +144,155 @@ __device__ __forceinline__ void flush_stats(const IngestParams &P, LaneStats &st
   }
 }
 
-// Loads 2 consecutive spans (16-B per column) or one at the tail.
-struct Span2 {
-  uint64_t key[2], s[2], e[2], a[2], b[2];
-  uint32_t meta[2];
+// Per-workgroup buffer descriptors over the SoA columns of its span range
+// [lo, hi).  Loads are bounds-checked by the hardware (out-of-range dwords
+// read as 0), so every lane issues the same loads -- also in the last tile --
+// and the compiler's vmcnt accounting stays exact across the prefetch.
+struct Cols {
+  __amdgpu_buffer_rsrc_t key, start, end, w0, w1, meta;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ Cols make_cols(const IngestParams &P, uint64_t lo, uint64_t hi) {
+  const uint32_t b8 = (uint32_t)((hi - lo) * 8), b4 = (uint32_t)((hi - lo) * 4);
+  Cols c;
+  c.key = rsrc(P.key + lo, b8);
+  c.start = rsrc(P.start + lo, b8);
+  c.end = rsrc(P.end + lo, b8);
+  c.w0 = rsrc(P.w0 + lo, b8);
+  c.w1 = rsrc(P.w1 + lo, b8);
+  c.meta = rsrc(P.meta + lo, b4);
+  return c;
+}
+
+// S consecutive spans per lane per tile: each u64 column is read with S/2
+// 16-B loads (one wave-instruction = 1 KiB), meta with one 4*S-B load.
+template <int S>
+struct SpanTile {
+  uint64_t key[S], s[S], e[S], a[S], b[S];
+  uint32_t meta[S];
   int cnt;
 };
 
-__device__ __forceinline__ void load_span2(const IngestParams &P, uint64_t i0, Span2 &v) {
-  if (i0 + 1 < P.n) {
-    const ulonglong2 k = *reinterpret_cast<const ulonglong2 *>(P.key + i0);
-    const ulonglong2 s = *reinterpret_cast<const ulonglong2 *>(P.start + i0);
-    const ulonglong2 e = *reinterpret_cast<const ulonglong2 *>(P.end + i0);
-    const ulonglong2 a = *reinterpret_cast<const ulonglong2 *>(P.w0 + i0);
-    const ulonglong2 b = *reinterpret_cast<const ulonglong2 *>(P.w1 + i0);
-    const uint2 m = *reinterpret_cast<const uint2 *>(P.meta + i0);
-    v.key[0] = k.x; v.key[1] = k.y;
-    v.s[0] = s.x; v.s[1] = s.y;
-    v.e[0] = e.x; v.e[1] = e.y;
-    v.a[0] = a.x; v.a[1] = a.y;
-    v.b[0] = b.x; v.b[1] = b.y;
-    v.meta[0] = m.x; v.meta[1] = m.y;
-    v.cnt = 2;
-  } else if (i0 < P.n) {
-    v.key[0] = P.key[i0];
-    v.s[0] = P.start[i0];
-    v.e[0] = P.end[i0];
-    v.a[0] = P.w0[i0];
-    v.b[0] = P.w1[i0];
-    v.meta[0] = P.meta[i0];
-    v.cnt = 1;
-  } else {
-    v.cnt = 0;
+__device__ __forceinline__ void u64x2(__amdgpu_buffer_rsrc_t r, int off, uint64_t &x, uint64_t &y) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  x = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
+  y = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
+}
+
+template <int S>
+__device__ __forceinline__ void load_tile(const Cols &c, uint32_t off, uint32_t len,
+                                          SpanTile<S> &v) {
+  static_assert(S == 2 || S == 4, "2 or 4 spans per lane");
+#pragma unroll
+  for (int h = 0; h < S / 2; ++h) {
+    const int ob = (int)(off * 8 + 16 * h);
+    u64x2(c.key, ob, v.key[2 * h], v.key[2 * h + 1]);
+    u64x2(c.start, ob, v.s[2 * h], v.s[2 * h + 1]);
+    u64x2(c.end, ob, v.e[2 * h], v.e[2 * h + 1]);
+    u64x2(c.w0, ob, v.a[2 * h], v.a[2 * h + 1]);
+    u64x2(c.w1, ob, v.b[2 * h], v.b[2 * h + 1]);
   }
+  if constexpr (S == 4) {
+    const auto m = __builtin_amdgcn_raw_buffer_load_b128(c.meta, (int)(off * 4), 0, 0);
+    v.meta[0] = m[0]; v.meta[1] = m[1]; v.meta[2] = m[2]; v.meta[3] = m[3];
+  } else {
+    const auto m = __builtin_amdgcn_raw_buffer_load_b64(c.meta, (int)(off * 4), 0, 0);
+    v.meta[0] = m[0]; v.meta[1] = m[1];
+  }
+  v.cnt = off < len ? ((len - off) < (uint32_t)S ? (int)(len - off) : S) : 0;
+}
+
+// Sketch phase A: validate service / window, hash the trace id and issue the
+// HLL register read (consumed in phase B, after the RED work, so the read's
+// latency hides under it).
+template <int S>
+struct SketchPre {
+  uint8_t *reg[S];
+  uint32_t rho[S];   // 0 = no HLL update for this span
+  uint32_t cur[S];
+  uint32_t ws[S];    // window slot, 0xFFFFFFFF = no sketch update
+};
+
+template <int S>
+__device__ __forceinline__ void sketch_pre(const IngestParams &P, const SpanTile<S> &v,
+                                           SketchPre<S> &k, LaneStats &st) {
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    k.rho[j] = 0;
+    k.ws[j] = 0xFFFFFFFFu;
+    k.reg[j] = P.hll;
+    if (j < v.cnt) {
+      const uint32_t svc = v.meta[j] & 0xFFFFu;
+      const bool svc_ok = svc < P.n_services;
+      const uint64_t win = fast_div(v.e[j], P.window_ns, P.win_magic);
+      const bool win_ok = win - P.win_base < (uint64_t)P.n_windows;
+      st.bad_svc += svc_ok ? 0u : 1u;
+      st.oor += (svc_ok && !win_ok) ? 1u : 0u;
+      if (svc_ok && win_ok) {
+        const uint32_t ws = (uint32_t)(win & P.win_mask);
+        k.ws[j] = ws;
+        if (!(P.diag & 2u)) {
+          const uint64_t x = xxh64_16(v.a[j], v.b[j]);
+          const uint64_t idx = x >> (64 - P.p);
+          k.rho[j] = (uint32_t)__clzll((long long)((x << P.p) | (1ULL << (P.p - 1)))) + 1;
+          k.reg[j] = P.hll + ((((uint64_t)ws * P.n_services + svc) << P.p) + idx);
+        }
+      }
+    }
+  }
+  // Unconditional reads (a skipped span reads the array's first byte): a
+  // per-span "load or constant" makes hipcc branch around each load with its
+  // own vmcnt(0), serialising the reads and draining any prefetch in flight.
+#pragma unroll
+  for (int j = 0; j < S; ++j) k.cur[j] = *k.reg[j];
+}
+
+// Direct count-min update of one ERROR span (d atomics).
+__device__ __forceinline__ void cms_add(const IngestParams &P, uint32_t ws, uint64_t key,
+                                        unsigned long long c) {
+  unsigned long long *row = P.cms + (uint64_t)ws * P.cms_d * P.cms_w;
+  for (uint32_t r = 0; r < P.cms_d; ++r) {
+    const uint64_t col = splitmix64(key ^ P.cms_seed[r]) >> P.cms_shift;
+    atomicAdd(row + (uint64_t)r * P.cms_w + col, c);
+  }
+}
+
+// Sketch phase B: raise HLL registers that grew; count ERROR spans.  A span
+// whose series has a key-table slot adds 1 to the exact per-(window, slot)
+// error counter (one atomic); the count-min cells are derived from those
+// counters when the window is read (fold_errcnt_kernel).  Because the sketch
+// is linear in its inputs this is bit-identical to d per-span cell updates.
+// Spans without a slot (key 0, table full) update the cells directly.
+// The no-return error atomics are issued before the HLL compare, so the wait
+// for the register reads is a counted vmcnt behind the prefetch.
+template <int S>
+__device__ __forceinline__ void sketch_post(const IngestParams &P, const SpanTile<S> &v,
+                                            const SketchPre<S> &k, const uint32_t (&slot)[S]) {
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    if (k.ws[j] != 0xFFFFFFFFu && ((v.meta[j] >> 19) & 3u) == 2u && !(P.diag & 4u)) {
+      if (slot[j] != kNotFound)
+        atomicAdd(P.errcnt + ((uint64_t)k.ws[j] << P.log2cap) + slot[j], 1ULL);
+      else
+        cms_add(P, k.ws[j], v.key[j], 1ULL);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < S; ++j)
+    if ((k.cur[j] & 0xFFu) < k.rho[j]) hll_raise(k.reg[j], k.rho[j]);
+}
+
+// Contiguous per-workgroup span range [lo, hi), lo a multiple of 4.
+__device__ __forceinline__ void wg_range(uint64_t n, uint64_t &lo, uint64_t &hi) {
+  uint64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+  chunk = (chunk + 3) / 4 * 4;
+  lo = (uint64_t)blockIdx.x * chunk;
+  if (lo > n) lo = n;
+  hi = lo + chunk < n ? lo + chunk : n;
 }
 
 // ---------------------------------------------------------------------------
@@ -207,34 +300,59 @@ __device__ __forceinline__ void load_span2(const IngestParams &P, uint64_t i0, S
 //   lkeys [cap] u64   mirror of the HBM key table (same slot positions)
 //   lsum  [cap] u64   per-slot ns sum of this epoch
 //   lcnt  [cap][nw] u32, nw = ceil(nbk/2): two u16 bucket counters per word
-template <int NB>
-__device__ __forceinline__ void flush_lds(const IngestParams &P, uint32_t cap, uint32_t nbk,
-                                          uint32_t nw, unsigned long long *lsum, uint32_t *lcnt) {
-  uint32_t *scnt = P.slab_cnt + (uint64_t)blockIdx.x * cap * nbk;
-  unsigned long long *ssum = P.slab_sum + (uint64_t)blockIdx.x * cap;
-  const uint32_t cells = cap * nw;
-  for (uint32_t c = threadIdx.x; c < cells; c += blockDim.x) {
-    const uint32_t v = lcnt[c];
-    if (v) {
-      const uint32_t slot = c / nw, w = c - slot * nw;
-      uint32_t *dst = scnt + (uint64_t)slot * nbk + 2 * w;
-      if (v & 0xFFFFu) dst[0] += v & 0xFFFFu;
-      if (v >> 16) dst[1] += v >> 16;
-      lcnt[c] = 0;
+// The workgroup's HBM slab is [cap][2*nw] u32 (+ [cap] u64 sums): LDS word w
+// maps to slab cells 2w and 2w+1, so a pair of LDS words is one 16-B slab
+// vector and the flush is a vectorised read-modify-write of touched cells.
+__device__ __forceinline__ void flush_lds(const IngestParams &P, uint32_t cap, uint32_t nw,
+                                          unsigned long long *lsum, uint32_t *lcnt) {
+  if (P.diag & 8u) return;
+  uint4 *scnt = reinterpret_cast<uint4 *>(P.slab_cnt + (uint64_t)blockIdx.x * cap * 2 * nw);
+  uint2 *lw = reinterpret_cast<uint2 *>(lcnt);
+  const uint32_t pairs = cap * nw / 2;
+  constexpr int U = 4;
+  for (uint32_t k0 = threadIdx.x; k0 < pairs; k0 += U * blockDim.x) {
+    uint2 w[U];
+    uint4 g[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t k = k0 + u * blockDim.x;
+      w[u] = k < pairs ? lw[k] : make_uint2(0, 0);
+      g[u] = (w[u].x | w[u].y) ? scnt[k] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t k = k0 + u * blockDim.x;
+      if (w[u].x | w[u].y) {
+        g[u].x += w[u].x & 0xFFFFu;
+        g[u].y += w[u].x >> 16;
+        g[u].z += w[u].y & 0xFFFFu;
+        g[u].w += w[u].y >> 16;
+        scnt[k] = g[u];
+        lw[k] = make_uint2(0, 0);
+      }
     }
   }
-  for (uint32_t s = threadIdx.x; s < cap; s += blockDim.x) {
-    const unsigned long long v = lsum[s];
-    if (v) {
-      ssum[s] += v;
-      lsum[s] = 0;
+  ulonglong2 *ss = reinterpret_cast<ulonglong2 *>(P.slab_sum + (uint64_t)blockIdx.x * cap);
+  ulonglong2 *ls = reinterpret_cast<ulonglong2 *>(lsum);
+  for (uint32_t k = threadIdx.x; k < cap / 2; k += blockDim.x) {
+    const ulonglong2 v = ls[k];
+    if (v.x | v.y) {
+      ulonglong2 g = ss[k];
+      g.x += v.x;
+      g.y += v.y;
+      ss[k] = g;
+      ls[k] = make_ulonglong2(0, 0);
     }
   }
 }
 
-template <int NB>
-__global__ __launch_bounds__(1024) void ingest_small_kernel(IngestParams P) {
+// NB: positive-threshold count when it is 16 with no negative bounds (the
+// default buckets, fully unrolled), else -1 (runtime).  S: spans per lane per
+// tile.  PF: issue the next tile's loads before this tile's RED work.
+template <int NB, int S, bool PF, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ingest_small_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t cap = 1u << P.log2cap;
   const uint64_t mask = cap - 1;
   const uint32_t nbk = NB >= 0 ? (uint32_t)NB + 1 : P.nbk;
@@ -243,37 +361,55 @@ __global__ __launch_bounds__(1024) void ingest_small_kernel(IngestParams P) {
   unsigned long long *lsum = lkeys + cap;
   uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + cap);
 
-  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
+  uint64_t lo, hi;
+  wg_range(P.n, lo, hi);
+  const Cols c = make_cols(P, lo, hi);
+  const uint32_t len = (uint32_t)(hi - lo);
+  const uint32_t tile = BLOCK * S;
+  uint32_t off = threadIdx.x * S;
+  SpanTile<S> cur;
+  load_tile<S>(c, off, len, cur);  // first tile's loads overlap the LDS setup
+
+  for (uint32_t i = threadIdx.x; i < cap; i += BLOCK) {
     lkeys[i] = __hip_atomic_load(&P.gkeys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     lsum[i] = 0;
   }
-  for (uint32_t i = threadIdx.x; i < cap * nw; i += blockDim.x) lcnt[i] = 0;
+  for (uint32_t i = threadIdx.x; i < cap * nw; i += BLOCK) lcnt[i] = 0;
   __syncthreads();
+  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
 
   LaneStats st{0, 0, 0, 0};
-  const uint64_t tile = (uint64_t)blockDim.x * 2;
-  const uint64_t ntiles = (P.n + tile - 1) / tile;
   uint32_t in_epoch = 0;
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    Span2 v;
-    load_span2(P, t * tile + (uint64_t)threadIdx.x * 2, v);
+  for (uint32_t t0 = 0; t0 < len; t0 += tile, off += tile) {
+    SketchPre<S> k;
+    sketch_pre<S>(P, cur, k, st);
+    SpanTile<S> nxt;
+    if constexpr (PF) {
+      __builtin_amdgcn_sched_barrier(0);
+      load_tile<S>(c, off + tile, len, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    uint32_t slot[S];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (j < v.cnt) {
-        const uint64_t key = v.key[j];
-        const uint64_t d = v.e[j] > v.s[j] ? v.e[j] - v.s[j] : 0;
+    for (int j = 0; j < S; ++j) {
+      slot[j] = kNotFound;
+      if (j < cur.cnt) {
+        const uint64_t key = cur.key[j];
+        const uint64_t d = cur.e[j] > cur.s[j] ? cur.e[j] - cur.s[j] : 0;
         st.zero_key += key == 0 ? 1u : 0u;
-        if (key != 0) {
+        if (P.diag & 1u) {
+          st.dropped += (uint32_t)(((key ^ d) & 0xFFFFFFFFFFFFULL) == 0x123456789ABCULL);  // keep live
+        } else if (key != 0) {
           const uint32_t b = bucket_of<NB>(d, P);
           uint64_t s = slot_of(key, P.log2cap);
           uint32_t found = kNotFound;
           for (uint32_t q = 0; q < P.max_probe; ++q) {
-            const unsigned long long k = lkeys[s];
-            if (k == key) {
+            const unsigned long long kk = lkeys[s];
+            if (kk == key) {
               found = (uint32_t)s;
               break;
             }
-            if (k == 0) break;
+            if (kk == 0) break;
             s = (s + 1) & mask;
           }
           if (found == kNotFound) {
@@ -285,43 +421,63 @@ __global__ __launch_bounds__(1024) void ingest_small_kernel(IngestParams P) {
             atomicAdd(&lsum[found], (unsigned long long)d);
           }
           st.dropped += found == kNotFound ? 1u : 0u;
+          slot[j] = found;
         }
-        const uint32_t sk = sketch_span(P, key, v.e[j], v.a[j], v.b[j], v.meta[j]);
-        st.bad_svc += sk == 1 ? 1u : 0u;
-        st.oor += sk == 2 ? 1u : 0u;
       }
     }
-    if (++in_epoch == P.epoch_tiles) {
+    sketch_post<S>(P, cur, k, slot);
+    if constexpr (PF) {
+      cur = nxt;
+    } else {
+      load_tile<S>(c, off + tile, len, cur);
+    }
+    if (++in_epoch == P.epoch_tiles) {  // u16 LDS counters: flush before they can wrap
       __syncthreads();
-      flush_lds<NB>(P, cap, nbk, nw, lsum, lcnt);
+      flush_lds(P, cap, nw, lsum, lcnt);
       __syncthreads();
       in_epoch = 0;
     }
   }
+  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
-  flush_lds<NB>(P, cap, nbk, nw, lsum, lcnt);
+  flush_lds(P, cap, nw, lsum, lcnt);
+  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime();
   flush_stats(P, st);
 }
 
 // ---------------------------------------------------------------------------
 // HBM-table path (table larger than LDS): CAS insert + u64 atomics per span.
-template <int NB>
-__global__ __launch_bounds__(256) void ingest_hbm_kernel(IngestParams P) {
+template <int NB, int S, bool PF, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ingest_hbm_kernel(IngestParams P) {
   LaneStats st{0, 0, 0, 0};
   const uint32_t nbk = NB >= 0 ? (uint32_t)NB + 1 : P.nbk;
   const uint32_t stride = nbk + 1;
-  const uint64_t tile = (uint64_t)blockDim.x * 2;
-  const uint64_t ntiles = (P.n + tile - 1) / tile;
-  for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    Span2 v;
-    load_span2(P, t * tile + (uint64_t)threadIdx.x * 2, v);
+  uint64_t lo, hi;
+  wg_range(P.n, lo, hi);
+  const Cols c = make_cols(P, lo, hi);
+  const uint32_t len = (uint32_t)(hi - lo);
+  const uint32_t tile = BLOCK * S;
+  uint32_t off = threadIdx.x * S;
+  SpanTile<S> cur;
+  load_tile<S>(c, off, len, cur);
+  for (uint32_t t0 = 0; t0 < len; t0 += tile, off += tile) {
+    SketchPre<S> k;
+    sketch_pre<S>(P, cur, k, st);
+    SpanTile<S> nxt;
+    if constexpr (PF) {
+      __builtin_amdgcn_sched_barrier(0);
+      load_tile<S>(c, off + tile, len, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    uint32_t slot[S];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      if (j < v.cnt) {
-        const uint64_t key = v.key[j];
-        const uint64_t d = v.e[j] > v.s[j] ? v.e[j] - v.s[j] : 0;
+    for (int j = 0; j < S; ++j) {
+      slot[j] = kNotFound;
+      if (j < cur.cnt) {
+        const uint64_t key = cur.key[j];
+        const uint64_t d = cur.e[j] > cur.s[j] ? cur.e[j] - cur.s[j] : 0;
         st.zero_key += key == 0 ? 1u : 0u;
-        if (key != 0) {
+        if (key != 0 && !(P.diag & 1u)) {
           const uint32_t b = bucket_of<NB>(d, P);
           const uint32_t found = g_find_insert(P.gkeys, key, P.log2cap, P.max_probe);
           if (found != kNotFound) {
@@ -330,11 +486,15 @@ __global__ __launch_bounds__(256) void ingest_hbm_kernel(IngestParams P) {
             atomicAdd(row + nbk, (unsigned long long)d);
           }
           st.dropped += found == kNotFound ? 1u : 0u;
+          slot[j] = found;
         }
-        const uint32_t sk = sketch_span(P, key, v.e[j], v.a[j], v.b[j], v.meta[j]);
-        st.bad_svc += sk == 1 ? 1u : 0u;
-        st.oor += sk == 2 ? 1u : 0u;
       }
+    }
+    sketch_post<S>(P, cur, k, slot);
+    if constexpr (PF) {
+      cur = nxt;
+    } else {
+      load_tile<S>(c, off + tile, len, cur);
     }
   }
   flush_stats(P, st);
@@ -345,7 +505,8 @@ __global__ __launch_bounds__(256) void ingest_hbm_kernel(IngestParams P) {
 __global__ void reduce_slabs_kernel(uint32_t *slab_cnt, unsigned long long *slab_sum,
                                     unsigned long long *gcounts, uint32_t G, uint64_t cap,
                                     uint32_t nbk) {
-  const uint64_t cells = cap * nbk;
+  const uint32_t srow = (nbk + 1) & ~1u;  // 2 * ceil(nbk / 2)
+  const uint64_t cells = cap * srow;
   const uint32_t stride = nbk + 1;
   for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < cells + cap;
        c += (uint64_t)gridDim.x * blockDim.x) {
@@ -359,10 +520,8 @@ __global__ void reduce_slabs_kernel(uint32_t *slab_cnt, unsigned long long *slab
           *p = 0;
         }
       }
-      if (acc) {
-        const uint64_t slot = c / nbk, b = c - slot * nbk;
-        gcounts[slot * stride + b] += acc;
-      }
+      const uint64_t slot = c / srow, b = c - slot * srow;
+      if (acc && b < nbk) gcounts[slot * stride + b] += acc;
     } else {
       const uint64_t slot = c - cells;
       unsigned long long acc = 0;
@@ -427,6 +586,24 @@ __global__ void count_keys_kernel(const unsigned long long *gkeys, uint64_t cap,
   if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, (unsigned long long)c);
 }
 
+// Window read: add the exact per-slot error counts of window slot `ws` into
+// its count-min cells, then clear them (so reads are idempotent).
+__global__ void fold_errcnt_kernel(const unsigned long long *gkeys, unsigned long long *errcnt,
+                                   uint64_t cap, unsigned long long *cms, uint32_t d, uint32_t w,
+                                   uint32_t shift, const uint64_t *seeds) {
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long c = errcnt[s];
+    if (!c) continue;
+    const uint64_t key = gkeys[s];
+    for (uint32_t r = 0; r < d; ++r) {
+      const uint64_t col = splitmix64(key ^ seeds[r]) >> shift;
+      atomicAdd(cms + (uint64_t)r * w + col, c);
+    }
+    errcnt[s] = 0;
+  }
+}
+
 uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap_blocks) {
   uint64_t g = (work + block - 1) / block;
   if (g < 1) g = 1;
@@ -434,33 +611,61 @@ uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap_blocks) {
   return (uint32_t)g;
 }
 
+// Kernel variants (spans per lane, next-tile prefetch, block size); see
+// sa_internal.h kVariants.  Index = variant id.
+#define SA_SMALL(NB, V)                                                                      \
+  (V == 0 ? (const void *)&ingest_small_kernel<NB, 4, false, 1024>                          \
+   : V == 1 ? (const void *)&ingest_small_kernel<NB, 2, true, 1024>                         \
+   : V == 2 ? (const void *)&ingest_small_kernel<NB, 4, true, 512>                          \
+            : (const void *)&ingest_small_kernel<NB, 2, false, 1024>)
+
+template <int NB>
+static void launch_small_nb(const IngestParams &P, uint32_t grid, size_t lds, hipStream_t s,
+                            int v) {
+  switch (v) {
+    case 1: hipLaunchKernelGGL((ingest_small_kernel<NB, 2, true, 1024>), dim3(grid), dim3(1024), lds, s, P); break;
+    case 2: hipLaunchKernelGGL((ingest_small_kernel<NB, 4, true, 512>), dim3(grid), dim3(512), lds, s, P); break;
+    case 3: hipLaunchKernelGGL((ingest_small_kernel<NB, 2, false, 1024>), dim3(grid), dim3(1024), lds, s, P); break;
+    default: hipLaunchKernelGGL((ingest_small_kernel<NB, 4, false, 1024>), dim3(grid), dim3(1024), lds, s, P); break;
+  }
+}
+
+template <int NB>
+static void launch_hbm_nb(const IngestParams &P, uint32_t grid, hipStream_t s, int v) {
+  switch (v) {
+    case 1: hipLaunchKernelGGL((ingest_hbm_kernel<NB, 2, true, 256>), dim3(grid), dim3(256), 0, s, P); break;
+    case 2: hipLaunchKernelGGL((ingest_hbm_kernel<NB, 4, true, 256>), dim3(grid), dim3(256), 0, s, P); break;
+    case 3: hipLaunchKernelGGL((ingest_hbm_kernel<NB, 2, false, 256>), dim3(grid), dim3(256), 0, s, P); break;
+    default: hipLaunchKernelGGL((ingest_hbm_kernel<NB, 4, false, 256>), dim3(grid), dim3(256), 0, s, P); break;
+  }
+}
+
 }  // namespace
 
 hipError_t prepare_ingest_small(size_t lds_bytes) {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&ingest_small_kernel<16>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute(reinterpret_cast<const void *>(&ingest_small_kernel<-1>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  for (int v = 0; v < kNumVariants; ++v) {
+    const void *f16 = SA_SMALL(16, v), *fr = SA_SMALL(-1, v);
+    hipError_t e = hipFuncSetAttribute(f16, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute(fr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
-hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, uint32_t block,
-                               size_t lds_bytes, hipStream_t s) {
-  if (P.nneg == 0 && P.npos == 16)
-    hipLaunchKernelGGL(ingest_small_kernel<16>, dim3(grid), dim3(block), lds_bytes, s, P);
-  else
-    hipLaunchKernelGGL(ingest_small_kernel<-1>, dim3(grid), dim3(block), lds_bytes, s, P);
+hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,
+                               hipStream_t s, int variant) {
+  if (P.nneg == 0 && P.npos == 16) launch_small_nb<16>(P, grid, lds_bytes, s, variant);
+  else launch_small_nb<-1>(P, grid, lds_bytes, s, variant);
   return hipGetLastError();
 }
 
-hipError_t launch_ingest_hbm(const IngestParams &P, uint32_t grid, uint32_t block,
-                             hipStream_t s) {
-  if (P.nneg == 0 && P.npos == 16)
-    hipLaunchKernelGGL(ingest_hbm_kernel<16>, dim3(grid), dim3(block), 0, s, P);
-  else
-    hipLaunchKernelGGL(ingest_hbm_kernel<-1>, dim3(grid), dim3(block), 0, s, P);
+hipError_t launch_ingest_hbm(const IngestParams &P, uint32_t grid, hipStream_t s, int variant) {
+  if (P.nneg == 0 && P.npos == 16) launch_hbm_nb<16>(P, grid, s, variant);
+  else launch_hbm_nb<-1>(P, grid, s, variant);
   return hipGetLastError();
 }
+
 
 hipError_t launch_reduce_slabs(uint32_t *slab_cnt, unsigned long long *slab_sum,
                                unsigned long long *gcounts, uint32_t G, uint64_t cap,
@@ -488,6 +693,15 @@ hipError_t launch_gather_dense(const unsigned long long *gkeys, const unsigned l
   const uint32_t block = 256;
   hipLaunchKernelGGL(gather_dense_kernel, dim3(grid_for(n, block, 4096)), dim3(block), 0, s,
                      gkeys, gcounts, log2cap, max_probe, stride, keys, n, rows);
+  return hipGetLastError();
+}
+
+hipError_t launch_fold_errcnt(const unsigned long long *gkeys, unsigned long long *errcnt,
+                              uint64_t cap, unsigned long long *cms, uint32_t d, uint32_t w,
+                              uint32_t shift, const uint64_t *seeds, hipStream_t s) {
+  const uint32_t block = 256;
+  hipLaunchKernelGGL(fold_errcnt_kernel, dim3(grid_for(cap, block, 2048)), dim3(block), 0, s, gkeys,
+                     errcnt, cap, cms, d, w, shift, seeds);
   return hipGetLastError();
 }
 

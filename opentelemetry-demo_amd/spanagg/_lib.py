@@ -86,6 +86,7 @@ SIGNATURES = [
     ("sa_export_keys", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, u64p, C.c_void_p]),
     ("sa_gather_dense", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int, C.c_void_p]),
     ("sa_window_export", C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("sa_debug_stamps", C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p]),
     ("sa_bucket_thresholds", C.c_int, [f64p, C.c_uint32, C.c_uint32, u64p, u32p]),
     ("sa_hll_estimate", C.c_double, [u8p, C.c_uint32]),
 ]

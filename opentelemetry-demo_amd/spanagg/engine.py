@@ -53,6 +53,7 @@ class Config:
     n_services: int = 64
     key_capacity: int = 1000
     device: int = 0
+    flags: int = 0  # SA_DIAG_* profiling ablations only (results are wrong when set)
 
     def to_c(self):
         arr = (C.c_double * max(1, len(self.bounds)))(*[float(b) for b in self.bounds])
@@ -62,7 +63,7 @@ class Config:
         c.unit = _lib.SA_UNIT_S if self.unit == "s" else _lib.SA_UNIT_MS
         c.hll_p, c.cms_d, c.cms_w = self.hll_p, self.cms_d, self.cms_w
         c.window_ns, c.n_windows, c.n_services = self.window_ns, self.n_windows, self.n_services
-        c.key_capacity, c.device, c.flags = self.key_capacity, self.device, 0
+        c.key_capacity, c.device, c.flags = self.key_capacity, self.device, self.flags
         return c, arr
 
 
@@ -216,7 +217,7 @@ class Engine:
         finally:
             self.lib.sa_red_result_free(out)
         if rc == _lib.SA_EFULL and not allow_drops:
-            self._check(rc, "sa_flush")
+            raise SpanAggError(rc, f"sa_flush: spans dropped (key table full); stats={self.stats()}")
         return res
 
     def window_read(self, window_id: int) -> SketchResult:

@@ -112,8 +112,9 @@ def generate_c2(n: int, seed: int = 42, n_services: int = 20, names_per_service:
     tr = rng.integers(0, n_traces, n)
     batch = SpanBatch(key_hashes[key_index], start, end, tw0[tr], tw1[tr],
                       pack_meta(svc, kind, status))
-    first_window = T0_NS // 10_000_000_000
-    n_win = (spread_s + 60) // 10 + 1
+    # spans with end < start near T0 fall in the window before T0's
+    first_window = int(end.min()) // 10_000_000_000 if n else T0_NS // 10_000_000_000
+    n_win = int(end.max()) // 10_000_000_000 - first_window + 1 if n else 1
     return Workload(batch, key_strings, key_hashes, key_index, svc, name, kind, status,
                     int(first_window), int(n_win), n_services)
 
@@ -148,4 +149,4 @@ def generate_highcard(n: int, seed: int = 7, routes: int = 2000, pods: int = 500
     tw1 = rng.integers(0, 2**63, n_traces, dtype=np.int64).astype(np.uint64)
     tr = rng.integers(0, n_traces, n)
     batch = SpanBatch(khash[kidx], start, end, tw0[tr], tw1[tr], pack_meta(svc, 2, status))
-    return batch, khash, T0_NS // 10_000_000_000
+    return batch, khash, int(end.min()) // 10_000_000_000

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Attribute ingest-kernel time by ablation (cdna_hip_programming.md section 7,
+diagnostic loop step 2): the same C2 batch through engines built with
+SA_DIAG_* bits, timed in interleaved rounds in ONE process (HIP events on the
+launch stream), median per variant.  Results of ablated variants are wrong by
+design; only their time matters."""
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "opentelemetry-demo_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from spanagg import Config, Engine  # noqa: E402
+from spanagg.synth import generate_c2  # noqa: E402
+
+NO_RED, NO_HLL, NO_CMS, NO_FLUSH = 1, 2, 4, 8
+VARIANTS = {
+    "full": 0,
+    "no_cms": NO_CMS,
+    "no_hll": NO_HLL,
+    "no_sketch": NO_HLL | NO_CMS,
+    "no_flush": NO_FLUSH,
+    "no_red": NO_RED | NO_FLUSH,
+    "loads_only": NO_RED | NO_HLL | NO_CMS | NO_FLUSH,
+}
+
+
+def main():
+    n = int(os.environ.get("ABL_SPANS", 10_000_000))
+    rounds = int(os.environ.get("ABL_ROUNDS", 7))
+    reps = int(os.environ.get("ABL_REPS", 10))
+    wl = generate_c2(n, seed=42)
+    dev = torch.device("cuda", 0)
+    cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(dev)
+            for c in wl.batch.columns()]
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    engines = {}
+    base_variant = os.environ.get("SPANAGG_VARIANT", "0")
+    for name, fl in VARIANTS.items():
+        e = Engine(Config(n_services=wl.n_services, n_windows=16, flags=fl))
+        e.window_advance(wl.first_window)
+        engines[name] = e
+    # kernel-structure variants (sa_internal.h kVariants), full work
+    for v in range(4):
+        os.environ["SPANAGG_VARIANT"] = str(v)
+        e = Engine(Config(n_services=wl.n_services, n_windows=16))
+        e.window_advance(wl.first_window)
+        engines[f"variant{v}"] = e
+    os.environ["SPANAGG_VARIANT"] = base_variant
+    times = {k: [] for k in engines}
+    for r in range(rounds):
+        for name, e in engines.items():
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e.ingest_device(*cols, n=n, stream=stream.cuda_stream)  # warm
+            a.record(stream)
+            for _ in range(reps):
+                e.ingest_device(*cols, n=n, stream=stream.cuda_stream)
+            b.record(stream)
+            b.synchronize()
+            times[name].append(a.elapsed_time(b) / reps * 1e3)  # us per launch
+    # pure-read reference: torch reductions over the same 44 B/span
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(2):
+        a.record(stream)
+        for _ in range(reps):
+            s = sum(c.sum() for c in cols)
+        b.record(stream)
+        b.synchronize()
+    torch_read_us = a.elapsed_time(b) / reps * 1e3
+    out = {"spans": n, "bytes": 44 * n, "rounds": rounds, "reps": reps, "variants": {}}
+    for k, v in times.items():
+        med = statistics.median(v)
+        out["variants"][k] = {"median_us": med, "min_us": min(v),
+                              "gbs": 44 * n / (med * 1e-6) / 1e9,
+                              "spans_per_s": n / (med * 1e-6)}
+    out["torch_sum_read_us"] = torch_read_us
+    out["torch_sum_read_gbs"] = 44 * n / (torch_read_us * 1e-6) / 1e9
+    print(json.dumps(out, indent=1))
+    for e in engines.values():
+        e.close()
+
+
+if __name__ == "__main__":
+    main()

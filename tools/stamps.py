@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Per-workgroup timeline of the small-table ingest kernel from in-kernel
+s_memrealtime stamps (diagnostic build path, SPANAGG_STAMPS=1)."""
+import ctypes as C
+import json
+import os
+import sys
+
+os.environ["SPANAGG_STAMPS"] = "1"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "opentelemetry-demo_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from spanagg import Config, Engine, _lib  # noqa: E402
+from spanagg.synth import generate_c2  # noqa: E402
+
+
+def timeline(e):
+    n = C.c_uint64(0)
+    e.lib.sa_debug_stamps(e._h, None, 0, C.byref(n))
+    buf = np.zeros(n.value, np.uint64)
+    e.lib.sa_debug_stamps(e._h, buf.ctypes.data_as(_lib.u64p), n.value, C.byref(n))
+    t = buf.reshape(-1, 8)[:, :4].astype(np.int64)
+    t = t[t[:, 0] > 0]
+    us = lambda x: x / 100.0  # 100 MHz
+    t0 = t[:, 0].min()
+    q = lambda a: {"min": float(us(a.min())), "med": float(us(np.median(a))), "max": float(us(a.max()))}
+    return {"wgs": int(len(t)), "start_skew": q(t[:, 0] - t0), "init": q(t[:, 1] - t[:, 0]),
+            "loop": q(t[:, 2] - t[:, 1]), "flush": q(t[:, 3] - t[:, 2]),
+            "end": q(t[:, 3] - t0)}
+
+
+def main():
+    n = 10_000_000
+    wl = generate_c2(n, seed=42)
+    dev = torch.device("cuda", 0)
+    cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(dev)
+            for c in wl.batch.columns()]
+    s = torch.cuda.Stream(dev)
+    out = {}
+    for name, fl in (("full", 0), ("loads_only", 15), ("no_sketch", 6)):
+        for v in (0, 1):
+            os.environ["SPANAGG_VARIANT"] = str(v)
+            with Engine(Config(n_services=wl.n_services, n_windows=16, flags=fl)) as e:
+                e.window_advance(wl.first_window)
+                for _ in range(3):
+                    e.ingest_device(*cols, n=n, stream=s.cuda_stream)
+                torch.cuda.synchronize()
+                out[f"{name}/v{v}"] = timeline(e)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
