@@ -20,6 +20,15 @@ enum : int {
   kNumStats = 4
 };
 
+// Bucket lookup table: bin k = floor(log2 d) (k = 64 for d = 0).  For d in
+// bin k, bucket = base + [d > ta] + [d > tb] (ta/tb = UINT64_MAX when absent);
+// valid when no bin holds more than two thresholds.
+struct BinEntry {
+  unsigned long long ta, tb;
+  uint32_t base, pad[3];
+};
+constexpr int kBins = 65;
+
 // Everything the ingest kernels need, passed by value (kernel-argument segment,
 // read through the scalar cache).
 struct IngestParams {
@@ -45,20 +54,29 @@ struct IngestParams {
   unsigned long long *cms;      // [W][d][w]
   unsigned long long *errcnt;   // [W][cap] exact ERROR-span counts per (window, key slot)
   uint64_t window_ns, win_magic, win_base;
+  uint64_t base_ns, ring_ns;  // win_base * window_ns, n_windows * window_ns (< 2^63)
+  float inv_window;           // 1 / window_ns
+  uint32_t base_slot;         // win_base & win_mask
+  const BinEntry *bintab;     // [kBins] or nullptr (linear thresholds)
   uint32_t win_mask, n_windows;
   uint32_t p, n_services, cms_d, cms_shift, cms_w;
   uint32_t diag;  // SA_DIAG_* ablation bits (0 in production)
-  uint64_t cms_seed[8];
+  const uint64_t *seeds;  // [8] count-min row seeds (device memory)
   unsigned long long *stats;
   unsigned long long *dbg;  // diagnostic timestamps [G][8] (nullptr in production)
 };
 
-__host__ __device__ inline uint64_t slot_of(uint64_t key, uint32_t log2cap) {
-  return (key * kPhi) >> (64 - log2cap);
+// Key-table slot: 32-bit multiplicative hash of the folded id (one v_mul on
+// the device; ids are xxh64 outputs from the host, log2cap in 4..31).
+__host__ __device__ inline uint32_t slot_of(uint64_t key, uint32_t log2cap) {
+  const uint32_t h = (uint32_t)(key ^ (key >> 32)) * 0x9E3779B1u;
+  return h >> (32 - log2cap);
 }
 
-// Ingest kernel variants: spans per lane, next-tile prefetch, block size
-// (small-table path; the HBM-table path always uses 256-thread blocks).
+
+// HBM-table path variants (spans per lane, prefetch; 256-thread blocks).  The
+// small-table path has two: 0 = next-tile prefetch, 1 = none (1,024 threads,
+// 4 spans per lane); the block field below is unused by it.
 struct Variant {
   int spl;
   bool prefetch;
@@ -68,6 +86,11 @@ constexpr int kNumVariants = 4;
 constexpr Variant kVariants[kNumVariants] = {{4, false, 1024}, {2, true, 1024}, {4, true, 512},
                                              {2, false, 1024}};
 constexpr uint32_t kHbmBlock = 256;
+constexpr int kNumLdsVariants = 4;                // {4,PF} {4,-} {2,PF} {2,-}
+constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2};
+constexpr uint32_t kHllQueue = 2048;  // deferred HLL raises per workgroup (8 B each)
+// ingest_lds_kernel LDS beyond the table: HLL queue + its count + bin table
+constexpr size_t kLdsExtraBytes = kHllQueue * 8 + 16 + kBins * sizeof(BinEntry);
 
 // launchers (spanagg_kernels.hip)
 hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,

@@ -60,6 +60,7 @@ struct sa_engine {
                      *stats = nullptr, *out_keys = nullptr, *out_rows = nullptr, *scratch = nullptr,
                      *errcnt = nullptr;
   uint64_t *d_seeds = nullptr;
+  sa::BinEntry *d_bins = nullptr;  // bucket bin table (nullptr: linear thresholds)
   unsigned long long *dbg = nullptr;  // SPANAGG_STAMPS diagnostic timestamps
   uint32_t *slab_cnt = nullptr;
   uint8_t *hll = nullptr;
@@ -104,10 +105,37 @@ int validate_config(const sa_config *c, std::string &why) {
     return why = "n_services must be in 1..65536", SA_EINVAL;
   if (c->key_capacity < 1 || c->key_capacity > (1ULL << 30))
     return why = "key_capacity must be in 1..2^30", SA_EINVAL;
+  if (c->window_ns >= (1ULL << 63) / c->n_windows)
+    return why = "n_windows * window_ns must stay below 2^63 ns", SA_EINVAL;
+  if (((uint64_t)c->n_windows * c->n_services << c->hll_p) >= (1ULL << 32))
+    return why = "n_windows * n_services * 2^hll_p must stay below 2^32 registers", SA_EINVAL;
   return SA_OK;
 }
 
 }  // namespace
+
+// Bucket bin table for the LDS kernels: bin k = floor(log2 d) (64 for d = 0).
+// Returns false (use linear thresholds) if any bin holds more than 2 of them.
+static bool build_bins(const sa_engine *e, sa::BinEntry (&bins)[sa::kBins]) {
+  for (int k = 0; k < sa::kBins; ++k) {
+    bins[k] = sa::BinEntry{UINT64_MAX, UINT64_MAX, e->nneg, {0, 0, 0}};
+    if (k == 64) continue;  // d = 0: no u64 threshold is below 0
+    const uint64_t lo = 1ULL << k, hi = k == 63 ? UINT64_MAX : (2ULL << k) - 1;
+    uint32_t below = 0, inside = 0;
+    for (uint32_t i = 0; i < e->npos; ++i) {
+      const uint64_t t = e->thr[i];
+      if (t < lo) ++below;                  // every d in the bin exceeds it
+      else if (t < hi) {                    // decided per span
+        if (inside == 0) bins[k].ta = t;
+        else if (inside == 1) bins[k].tb = t;
+        ++inside;
+      }
+    }
+    if (inside > 2) return false;
+    bins[k].base = e->nneg + below;
+  }
+  return true;
+}
 
 extern "C" {
 
@@ -231,14 +259,15 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   e->cap = std::max<uint64_t>(16, next_pow2(2 * cfg->key_capacity));
   e->log2cap = log2u(e->cap);
   const uint32_t nw = (e->nbk + 1) / 2;
-  e->lds_bytes = (size_t)e->cap * 16 + (size_t)e->cap * nw * 4;
+  // lkeys + lsum + lcnt + deferred-HLL queue (+ its counter), see ingest_lds_kernel
+  e->lds_bytes = (size_t)e->cap * 16 + (size_t)e->cap * nw * 4 + sa::kLdsExtraBytes;
   e->small = e->lds_bytes <= kLdsBudget;
   e->variant = kDefaultVariant;
   if (const char *v = std::getenv("SPANAGG_VARIANT"))  // tuning knob for A/B runs
     e->variant = std::max(0, std::min(sa::kNumVariants - 1, std::atoi(v)));
-  e->spl = (uint32_t)sa::kVariants[e->variant].spl;
   if (e->small) {
-    e->block = sa::kVariants[e->variant].block;
+    e->spl = (uint32_t)sa::kLdsSpl[e->variant];
+    e->block = 1024;
     const uint32_t per_cu = std::max<uint32_t>(
         1, std::min<uint32_t>(2048 / e->block, (uint32_t)((160 * 1024) / e->lds_bytes)));
     e->G = e->cus * per_cu;
@@ -246,6 +275,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
   } else {
     e->block = sa::kHbmBlock;
+    e->spl = (uint32_t)sa::kVariants[e->variant].spl;
     e->G = e->cus * 8;
   }
 
@@ -269,6 +299,14 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     return bail(rc);
   if (std::getenv("SPANAGG_STAMPS") && (rc = alloc((void **)&e->dbg, (size_t)e->G * 64)))
     return bail(rc);
+  {
+    sa::BinEntry bins[sa::kBins];
+    if (build_bins(e, bins)) {
+      if ((rc = alloc((void **)&e->d_bins, sizeof bins))) return bail(rc);
+      if (hipMemcpy(e->d_bins, bins, sizeof bins, hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(e, SA_EDEVICE, "bin table upload failed"));
+    }
+  }
   if (hipMemcpy(e->d_seeds, kCmsSeed, sizeof kCmsSeed, hipMemcpyHostToDevice) != hipSuccess)
     return bail(fail(e, SA_EDEVICE, "seed upload failed"));
   if (e->small) {
@@ -289,7 +327,7 @@ void sa_destroy(sa_engine *e) {
   for (void *p : {(void *)e->gkeys, (void *)e->gcounts, (void *)e->slab_sum, (void *)e->cms,
                   (void *)e->stats, (void *)e->out_keys, (void *)e->out_rows, (void *)e->scratch,
                   (void *)e->slab_cnt, (void *)e->hll, (void *)e->errcnt, (void *)e->d_seeds,
-                  (void *)e->dbg,
+                  (void *)e->dbg, (void *)e->d_bins,
                   e->stage})
     if (p) (void)hipFree(p);
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
@@ -359,6 +397,11 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.window_ns = e->cfg.window_ns;
   P.win_magic = UINT64_MAX / e->cfg.window_ns;
   P.win_base = e->win_base;
+  P.base_ns = e->win_base * e->cfg.window_ns;  // < 2^64: checked in sa_window_advance
+  P.ring_ns = (uint64_t)e->cfg.n_windows * e->cfg.window_ns;
+  P.inv_window = (float)(1.0 / (double)e->cfg.window_ns);
+  P.base_slot = (uint32_t)(e->win_base & (e->cfg.n_windows - 1));
+  P.bintab = e->d_bins;
   P.win_mask = e->cfg.n_windows - 1;
   P.n_windows = e->cfg.n_windows;
   P.p = e->cfg.hll_p;
@@ -366,7 +409,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.cms_d = e->cfg.cms_d;
   P.cms_w = e->cfg.cms_w;
   P.cms_shift = 64 - log2u(e->cfg.cms_w);
-  std::memcpy(P.cms_seed, kCmsSeed, sizeof kCmsSeed);
+  P.seeds = e->d_seeds;
   P.stats = e->stats;
   P.diag = e->cfg.flags;
   P.dbg = e->dbg;
@@ -590,6 +633,8 @@ void sa_sketch_result_free(sa_sketch_result *r) { delete reinterpret_cast<sketch
 int sa_window_advance(sa_engine *e, uint64_t new_base) {
   if (!e) return SA_EINVAL;
   if (new_base < e->win_base) return fail(e, SA_EINVAL, "window base cannot move backwards");
+  if (new_base > UINT64_MAX / e->cfg.window_ns)
+    return fail(e, SA_EINVAL, "window base beyond the u64 nanosecond range");
   if (int rc = set_dev(e)) return rc;
   const uint64_t n = std::min<uint64_t>(new_base - e->win_base, e->cfg.n_windows);
   for (uint64_t k = 0; k < n; ++k) {

@@ -256,7 +256,7 @@ __device__ __forceinline__ void cms_add(const IngestParams &P, uint32_t ws, uint
                                         unsigned long long c) {
   unsigned long long *row = P.cms + (uint64_t)ws * P.cms_d * P.cms_w;
   for (uint32_t r = 0; r < P.cms_d; ++r) {
-    const uint64_t col = splitmix64(key ^ P.cms_seed[r]) >> P.cms_shift;
+    const uint64_t col = splitmix64(key ^ P.seeds[r]) >> P.cms_shift;
     atomicAdd(row + (uint64_t)r * P.cms_w + col, c);
   }
 }
@@ -309,7 +309,7 @@ __device__ __forceinline__ void flush_lds(const IngestParams &P, uint32_t cap, u
   uint4 *scnt = reinterpret_cast<uint4 *>(P.slab_cnt + (uint64_t)blockIdx.x * cap * 2 * nw);
   uint2 *lw = reinterpret_cast<uint2 *>(lcnt);
   const uint32_t pairs = cap * nw / 2;
-  constexpr int U = 4;
+  constexpr int U = 5;  // two rounds of loads for cap 2048 x nw 9 at 1,024 threads
   for (uint32_t k0 = threadIdx.x; k0 < pairs; k0 += U * blockDim.x) {
     uint2 w[U];
     uint4 g[U];
@@ -346,91 +346,222 @@ __device__ __forceinline__ void flush_lds(const IngestParams &P, uint32_t cap, u
   }
 }
 
-// NB: positive-threshold count when it is 16 with no negative bounds (the
-// default buckets, fully unrolled), else -1 (runtime).  S: spans per lane per
-// tile.  PF: issue the next tile's loads before this tile's RED work.
-template <int NB, int S, bool PF, int BLOCK>
-__global__ __launch_bounds__(BLOCK) void ingest_small_kernel(IngestParams P) {
+constexpr uint32_t kLdsBlock = 1024;
+
+// Window slot of `end` in the resident ring, or 0xFFFFFFFF when outside it:
+// q = (end - base_ns) / window_ns from a float estimate (|error| <= 1 for
+// q < 2^22) fixed by one signed correction each way -- 2 integer multiplies
+// instead of a 64-bit magic division.
+__device__ __forceinline__ uint32_t window_slot(const IngestParams &P, uint64_t end) {
+  const uint64_t delta = end - P.base_ns;  // wraps (huge) for end < base
+  const float f = (float)(uint32_t)(delta >> 32) * 4294967296.0f + (float)(uint32_t)delta;
+  uint32_t q = (uint32_t)(f * P.inv_window);
+  long long r = (long long)(delta - (uint64_t)q * P.window_ns);
+  const bool lo = r < 0;
+  q -= lo ? 1u : 0u;
+  r += lo ? (long long)P.window_ns : 0;
+  q += r >= (long long)P.window_ns ? 1u : 0u;
+  return delta < P.ring_ns ? ((P.base_slot + q) & P.win_mask) : 0xFFFFFFFFu;
+}
+
+// Bucket via the LDS bin table (BK = 1) or linear thresholds (BK = 0).
+template <int BK>
+__device__ __forceinline__ uint32_t bucket_lds(uint64_t d, const BinEntry *bins,
+                                               const IngestParams &P) {
+  if constexpr (BK == 1) {
+    const uint32_t bin = d ? 63u - (uint32_t)__clzll((long long)d) : 64u;
+    const BinEntry &e = bins[bin];
+    return e.base + (d > e.ta ? 1u : 0u) + (d > e.tb ? 1u : 0u);
+  } else {
+    return bucket_of<-1>(d, P);
+  }
+}
+
+// Probe the LDS key mirror past slot s (already known not to hold `key`);
+// returns the slot or kNotFound (empty slot reached / probe limit).
+__device__ __forceinline__ uint32_t lds_probe_rest(const unsigned long long *lkeys, uint64_t key,
+                                                   uint32_t s, uint32_t mask, uint32_t max_probe) {
+  for (uint32_t q = 1; q < max_probe; ++q) {
+    s = (s + 1) & mask;
+    const unsigned long long kk = lkeys[s];
+    if (kk == key) return s;
+    if (kk == 0) break;
+  }
+  return kNotFound;
+}
+
+// Small-table path (key table mirrored in LDS), 1,024 threads, S spans per
+// lane per tile.  Per tile:
+//   1. wait for the tile, compact it to (key, duration, bucket, HLL offset,
+//      rho, window slot) -- the raw 44 B/span registers are then free;
+//   2. S LDS key probes back to back -> key-table slots;
+//   3. ERROR spans: one no-return atomic on the exact (window, slot) counter;
+//   4. issue the S HLL register reads;
+//   5. PF: prefetch the next tile into the freed tile registers, then the LDS
+//      counter / sum atomics;
+//   6. HLL compare (a counted vmcnt: the prefetch stays in flight); a register
+//      that grows is queued in LDS and raised after the loop, so no returning
+//      global atomic (and its vmcnt(0)) sits in the loop.
+// BK: 1 = bucket by the LDS bin table, 0 = linear thresholds.  DIAG: honour
+// the SA_DIAG_* ablation bits (profiling builds only).
+// LDS: lkeys[cap] u64 | lsum[cap] u64 | lcnt[cap][nw] u32 | hq[kHllQueue] u64 |
+//      hq_n (16 B) | bins[kBins]
+template <int BK, int S, bool PF, bool DIAG>
+__global__ __launch_bounds__(kLdsBlock) void ingest_lds_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t cap = 1u << P.log2cap;
-  const uint64_t mask = cap - 1;
-  const uint32_t nbk = NB >= 0 ? (uint32_t)NB + 1 : P.nbk;
+  const uint32_t mask = cap - 1;
+  const uint32_t nbk = P.nbk;
   const uint32_t nw = (nbk + 1) >> 1;
+  const uint32_t diag = DIAG ? P.diag : 0u;
   unsigned long long *lkeys = reinterpret_cast<unsigned long long *>(smem);
   unsigned long long *lsum = lkeys + cap;
   uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + cap);
+  uint2 *hq = reinterpret_cast<uint2 *>(lcnt + cap * nw);
+  uint32_t *hq_n = reinterpret_cast<uint32_t *>(hq + kHllQueue);
+  BinEntry *lbins = reinterpret_cast<BinEntry *>(hq_n + 4);
 
   uint64_t lo, hi;
   wg_range(P.n, lo, hi);
   const Cols c = make_cols(P, lo, hi);
   const uint32_t len = (uint32_t)(hi - lo);
-  const uint32_t tile = BLOCK * S;
+  const uint32_t tile = kLdsBlock * S;
   uint32_t off = threadIdx.x * S;
-  SpanTile<S> cur;
-  load_tile<S>(c, off, len, cur);  // first tile's loads overlap the LDS setup
 
-  for (uint32_t i = threadIdx.x; i < cap; i += BLOCK) {
-    lkeys[i] = __hip_atomic_load(&P.gkeys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    lsum[i] = 0;
+  // Key-table (and bin-table) loads first, then the first tile's loads: the
+  // LDS setup waits only for the keys (vmcnt counts in issue order).
+  unsigned long long kv[8];
+  const uint32_t per = (cap + kLdsBlock - 1) / kLdsBlock;  // <= 8 for cap <= 8192
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const uint32_t i = threadIdx.x + u * kLdsBlock;
+    kv[u] = (u < (int)per && i < cap)
+                ? __hip_atomic_load(&P.gkeys[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                : 0ULL;
   }
-  for (uint32_t i = threadIdx.x; i < cap * nw; i += BLOCK) lcnt[i] = 0;
+  uint4 bv = make_uint4(0, 0, 0, 0);
+  if (BK == 1 && threadIdx.x < kBins * 2) bv = reinterpret_cast<const uint4 *>(P.bintab)[threadIdx.x];
+  SpanTile<S> cur;
+  load_tile<S>(c, off, len, cur);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const uint32_t i = threadIdx.x + u * kLdsBlock;
+    if (u < (int)per && i < cap) {
+      lkeys[i] = kv[u];
+      lsum[i] = 0;
+    }
+  }
+  if (BK == 1 && threadIdx.x < kBins * 2) reinterpret_cast<uint4 *>(lbins)[threadIdx.x] = bv;
+  for (uint32_t i = threadIdx.x; i < cap * nw; i += kLdsBlock) lcnt[i] = 0;
+  if (threadIdx.x == 0) *hq_n = 0;
   __syncthreads();
-  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
 
   LaneStats st{0, 0, 0, 0};
   uint32_t in_epoch = 0;
   for (uint32_t t0 = 0; t0 < len; t0 += tile, off += tile) {
-    SketchPre<S> k;
-    sketch_pre<S>(P, cur, k, st);
-    SpanTile<S> nxt;
-    if constexpr (PF) {
-      __builtin_amdgcn_sched_barrier(0);
-      load_tile<S>(c, off + tile, len, nxt);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    uint32_t slot[S];
+    // 1. compact the landed tile; info = bucket | rho << 6 | err << 13 | ws << 14
+    //    (bucket < 64, rho <= 65, ws < 4096 window slots)
+    uint64_t key[S], dur[S];
+    uint32_t hoff[S], info[S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      slot[j] = kNotFound;
-      if (j < cur.cnt) {
-        const uint64_t key = cur.key[j];
-        const uint64_t d = cur.e[j] > cur.s[j] ? cur.e[j] - cur.s[j] : 0;
-        st.zero_key += key == 0 ? 1u : 0u;
-        if (P.diag & 1u) {
-          st.dropped += (uint32_t)(((key ^ d) & 0xFFFFFFFFFFFFULL) == 0x123456789ABCULL);  // keep live
-        } else if (key != 0) {
-          const uint32_t b = bucket_of<NB>(d, P);
-          uint64_t s = slot_of(key, P.log2cap);
-          uint32_t found = kNotFound;
-          for (uint32_t q = 0; q < P.max_probe; ++q) {
-            const unsigned long long kk = lkeys[s];
-            if (kk == key) {
-              found = (uint32_t)s;
-              break;
-            }
-            if (kk == 0) break;
-            s = (s + 1) & mask;
+      const bool valid = j < cur.cnt;
+      key[j] = valid ? cur.key[j] : 0;
+      st.zero_key += (valid && cur.key[j] == 0) ? 1u : 0u;
+      dur[j] = cur.e[j] > cur.s[j] ? cur.e[j] - cur.s[j] : 0;
+      const uint32_t bkt = bucket_lds<BK>(dur[j], lbins, P);
+      const uint32_t svc = cur.meta[j] & 0xFFFFu;
+      const bool svc_ok = svc < P.n_services;
+      const uint32_t ws = window_slot(P, cur.e[j]);
+      const bool win_ok = ws != 0xFFFFFFFFu;
+      st.bad_svc += (valid && !svc_ok) ? 1u : 0u;
+      st.oor += (valid && svc_ok && !win_ok) ? 1u : 0u;
+      const bool sk = valid && svc_ok && win_ok;
+      const uint32_t err = (sk && ((cur.meta[j] >> 19) & 3u) == 2u && !(diag & 4u)) ? 1u : 0u;
+      uint32_t rho = 0;
+      hoff[j] = 0;
+      if (sk && !(diag & 2u)) {
+        const uint64_t x = xxh64_16(cur.a[j], cur.b[j]);
+        rho = (uint32_t)__clzll((long long)((x << P.p) | (1ULL << (P.p - 1)))) + 1;
+        hoff[j] = (((ws * P.n_services + svc) << P.p) + (uint32_t)(x >> (64 - P.p)));
+      }
+      info[j] = bkt | (rho << 6) | (err << 13) | ((ws & 4095u) << 14);
+    }
+    // 2. RED lookup: S LDS probes back to back (key no longer needed after)
+    uint32_t found[S];
+    if (!(diag & 1u)) {
+      uint32_t sl[S];
+      unsigned long long k0[S];
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        sl[j] = slot_of(key[j], P.log2cap);
+        k0[j] = lkeys[sl[j]];
+      }
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        found[j] = kNotFound;
+        if (key[j] != 0) {
+          found[j] = k0[j] == key[j] ? sl[j]
+                     : k0[j] == 0    ? kNotFound
+                                     : lds_probe_rest(lkeys, key[j], sl[j], mask, P.max_probe);
+          if (found[j] == kNotFound) {
+            found[j] = g_find_insert(P.gkeys, key[j], P.log2cap, P.max_probe);
+            if (found[j] != kNotFound) lkeys[found[j]] = key[j];
           }
-          if (found == kNotFound) {
-            found = g_find_insert(P.gkeys, key, P.log2cap, P.max_probe);
-            if (found != kNotFound) lkeys[found] = key;
-          }
-          if (found != kNotFound) {
-            atomicAdd(&lcnt[found * nw + (b >> 1)], 1u << ((b & 1) * 16));
-            atomicAdd(&lsum[found], (unsigned long long)d);
-          }
-          st.dropped += found == kNotFound ? 1u : 0u;
-          slot[j] = found;
+          st.dropped += found[j] == kNotFound ? 1u : 0u;
         }
       }
-    }
-    sketch_post<S>(P, cur, k, slot);
-    if constexpr (PF) {
-      cur = nxt;
     } else {
-      load_tile<S>(c, off + tile, len, cur);
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        found[j] = kNotFound;
+        st.dropped += (uint32_t)(((key[j] ^ dur[j] ^ info[j]) & 0xFFFFFFFFFFFFULL) == 0x123456789ABCULL);
+      }
     }
+    // 3. error counts: exact per (window, slot) -- one no-return atomic,
+    //    issued before the prefetch so the loop-top wait never covers it;
+    //    spans without a slot update the count-min cells directly
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      if (info[j] & (1u << 13)) {
+        if (found[j] != kNotFound)
+          atomicAdd(P.errcnt + (((uint64_t)(info[j] >> 14)) << P.log2cap) + found[j], 1ULL);
+        else
+          cms_add(P, info[j] >> 14, key[j], 1ULL);
+      }
+    }
+    // 4. HLL register reads (unconditional: offset 0 when unused)
+    uint32_t hv[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) hv[j] = P.hll[hoff[j]];
+    // 5. prefetch the next tile
+    if constexpr (PF) {
+      __builtin_amdgcn_sched_barrier(0);
+      load_tile<S>(c, off + tile, len, cur);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // 5b. RED update: LDS u16 bucket counter + u64 ns sum
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      if (found[j] != kNotFound) {
+        const uint32_t b = info[j] & 63u;
+        atomicAdd(&lcnt[found[j] * nw + (b >> 1)], 1u << ((b & 1) * 16));
+        atomicAdd(&lsum[found[j]], (unsigned long long)dur[j]);
+      }
+    }
+    // 6. HLL: queue the registers that grow
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const uint32_t rho = (info[j] >> 6) & 127u;
+      if ((hv[j] & 0xFFu) < rho) {
+        const uint32_t q = atomicAdd(hq_n, 1u);
+        if (q < kHllQueue) hq[q] = make_uint2(hoff[j], rho);
+        else hll_raise(P.hll + hoff[j], rho);
+      }
+    }
+    if constexpr (!PF) load_tile<S>(c, off + tile, len, cur);
     if (++in_epoch == P.epoch_tiles) {  // u16 LDS counters: flush before they can wrap
       __syncthreads();
       flush_lds(P, cap, nw, lsum, lcnt);
@@ -438,10 +569,12 @@ __global__ __launch_bounds__(BLOCK) void ingest_small_kernel(IngestParams P) {
       in_epoch = 0;
     }
   }
-  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
   flush_lds(P, cap, nw, lsum, lcnt);
-  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+  const uint32_t nq = *hq_n < kHllQueue ? *hq_n : kHllQueue;
+  for (uint32_t i = threadIdx.x; i < nq; i += kLdsBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
+  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime();
   flush_stats(P, st);
 }
 
@@ -611,22 +744,17 @@ uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap_blocks) {
   return (uint32_t)g;
 }
 
-// Kernel variants (spans per lane, next-tile prefetch, block size); see
-// sa_internal.h kVariants.  Index = variant id.
-#define SA_SMALL(NB, V)                                                                      \
-  (V == 0 ? (const void *)&ingest_small_kernel<NB, 4, false, 1024>                          \
-   : V == 1 ? (const void *)&ingest_small_kernel<NB, 2, true, 1024>                         \
-   : V == 2 ? (const void *)&ingest_small_kernel<NB, 4, true, 512>                          \
-            : (const void *)&ingest_small_kernel<NB, 2, false, 1024>)
-
-template <int NB>
-static void launch_small_nb(const IngestParams &P, uint32_t grid, size_t lds, hipStream_t s,
-                            int v) {
+// Small-table kernels: bin-table bucketing in four (spans/lane, prefetch)
+// variants, the linear-threshold fallback, and the diagnostic build.
+static const void *small_fn(bool bt, int v, bool diag) {
+  if (diag) return bt ? (const void *)&ingest_lds_kernel<1, 4, true, true>
+                      : (const void *)&ingest_lds_kernel<0, 4, true, true>;
+  if (!bt) return (const void *)&ingest_lds_kernel<0, 4, true, false>;
   switch (v) {
-    case 1: hipLaunchKernelGGL((ingest_small_kernel<NB, 2, true, 1024>), dim3(grid), dim3(1024), lds, s, P); break;
-    case 2: hipLaunchKernelGGL((ingest_small_kernel<NB, 4, true, 512>), dim3(grid), dim3(512), lds, s, P); break;
-    case 3: hipLaunchKernelGGL((ingest_small_kernel<NB, 2, false, 1024>), dim3(grid), dim3(1024), lds, s, P); break;
-    default: hipLaunchKernelGGL((ingest_small_kernel<NB, 4, false, 1024>), dim3(grid), dim3(1024), lds, s, P); break;
+    case 1: return (const void *)&ingest_lds_kernel<1, 4, false, false>;
+    case 2: return (const void *)&ingest_lds_kernel<1, 2, true, false>;
+    case 3: return (const void *)&ingest_lds_kernel<1, 2, false, false>;
+    default: return (const void *)&ingest_lds_kernel<1, 4, true, false>;
   }
 }
 
@@ -643,21 +771,21 @@ static void launch_hbm_nb(const IngestParams &P, uint32_t grid, hipStream_t s, i
 }  // namespace
 
 hipError_t prepare_ingest_small(size_t lds_bytes) {
-  for (int v = 0; v < kNumVariants; ++v) {
-    const void *f16 = SA_SMALL(16, v), *fr = SA_SMALL(-1, v);
-    hipError_t e = hipFuncSetAttribute(f16, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute(fr, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    if (e != hipSuccess) return e;
-  }
+  for (int bt = 0; bt < 2; ++bt)
+    for (int v = 0; v < kNumLdsVariants; ++v)
+      for (int d = 0; d < 2; ++d) {
+        hipError_t e = hipFuncSetAttribute(small_fn(bt, v, d),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+        if (e != hipSuccess) return e;
+      }
   return hipSuccess;
 }
 
 hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,
                                hipStream_t s, int variant) {
-  if (P.nneg == 0 && P.npos == 16) launch_small_nb<16>(P, grid, lds_bytes, s, variant);
-  else launch_small_nb<-1>(P, grid, lds_bytes, s, variant);
-  return hipGetLastError();
+  const void *fn = small_fn(P.bintab != nullptr, variant, P.diag != 0 || P.dbg != nullptr);
+  void *args[] = {const_cast<IngestParams *>(&P)};
+  return hipLaunchKernel(fn, dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);
 }
 
 hipError_t launch_ingest_hbm(const IngestParams &P, uint32_t grid, hipStream_t s, int variant) {

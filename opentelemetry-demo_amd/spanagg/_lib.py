@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libspanagg.so")
+# SPANAGG_LIB: diagnostic override (A/B of two builds of the same ABI)
+LIB_PATH = os.environ.get("SPANAGG_LIB") or os.path.join(_HERE, "libspanagg.so")
 
 SA_OK, SA_EINVAL, SA_ENOMEM, SA_EDEVICE, SA_EFULL, SA_ERANGE, SA_ESTATE = 0, -1, -2, -3, -4, -5, -6
 SA_UNIT_MS, SA_UNIT_S = 0, 1
@@ -104,7 +105,11 @@ def load() -> C.CDLL:
                 "`make -C opentelemetry-demo_amd` (or __graft_entry__.build())")
         lib = C.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
-            fn = getattr(lib, name)
+            fn = getattr(lib, name, None)
+            if fn is None and os.environ.get("SPANAGG_LIB"):
+                continue  # an older diagnostic build may lack newer entry points
+            if fn is None:
+                raise RuntimeError(f"libspanagg.so does not export {name}")
             fn.restype = res
             fn.argtypes = args
         if lib.sa_abi_version() != 1:

@@ -1,0 +1,28 @@
+#!/usr/bin/env python3
+"""Profiling driver: N ingest launches of the C2 10M-span batch (device-resident)
+with the library / variant selected by SPANAGG_LIB / SPANAGG_VARIANT."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "opentelemetry-demo_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from spanagg import Config, Engine  # noqa: E402
+from spanagg.synth import generate_c2  # noqa: E402
+
+n = int(os.environ.get("PROF_SPANS", 10_000_000))
+reps = int(os.environ.get("PROF_REPS", 5))
+wl = generate_c2(n, seed=42)
+cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).cuda()
+        for c in wl.batch.columns()]
+s = torch.cuda.Stream()
+with Engine(Config(n_services=wl.n_services, n_windows=16)) as e:
+    e.window_advance(wl.first_window)
+    for _ in range(reps):
+        e.ingest_device(*cols, n=n, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    r = e.flush()
+    print("calls", int(r.calls.sum()), "expected", reps * n)

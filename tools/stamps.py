@@ -41,7 +41,7 @@ def main():
     s = torch.cuda.Stream(dev)
     out = {}
     for name, fl in (("full", 0), ("loads_only", 15), ("no_sketch", 6)):
-        for v in (0, 1):
+        for v in (0, 1, 2, 3):
             os.environ["SPANAGG_VARIANT"] = str(v)
             with Engine(Config(n_services=wl.n_services, n_windows=16, flags=fl)) as e:
                 e.window_advance(wl.first_window)
