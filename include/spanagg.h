@@ -67,6 +67,8 @@ typedef enum { SA_UNIT_MS = 0, SA_UNIT_S = 1 } sa_unit;
 #define SA_DIAG_NO_HLL 2u     /* skip HLL hashing + register updates */
 #define SA_DIAG_NO_CMS 4u     /* skip count-min updates */
 #define SA_DIAG_NO_FLUSH 8u   /* skip the LDS -> slab flush */
+#define SA_DIAG_L2_INPUT 16u  /* every workgroup re-reads the batch's first 4 tiles
+                                 (cache-resident input: prices the HBM stream) */
 
 typedef struct {
     /* histogram.explicit.buckets (sorted ascending, finite) and histogram.unit */
@@ -176,9 +178,10 @@ int sa_window_export(sa_engine *e, uint64_t window_id, uint8_t *d_hll, uint64_t 
                      void *stream);
 
 /* Diagnostic only: per-workgroup s_memrealtime stamps (100 MHz) of the last
- * small-table ingest launch, [G][8] = {start, after LDS setup, after the span
- * loop, after the slab flush, 0...}; filled only when the engine was created
- * with SPANAGG_STAMPS set in the environment (*n_out = 0 otherwise). */
+ * small-table ingest launch, [G][136] = {start, after LDS setup, after the span
+ * loop, after the slab flush, 0 x 4, then per wave 8 segment cycle sums};
+ * filled only when the engine was created with SPANAGG_STAMPS set in the
+ * environment (*n_out = 0 otherwise). */
 int sa_debug_stamps(sa_engine *e, uint64_t *out, uint64_t cap, uint64_t *n_out);
 
 /* ---- pure host helpers (no device needed) ---- */

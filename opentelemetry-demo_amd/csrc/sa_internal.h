@@ -36,6 +36,7 @@ struct IngestParams {
   const uint64_t *key, *start, *end, *w0, *w1;
   const uint32_t *meta;
   uint64_t n;
+  uint64_t wg_chunk;  // spans per workgroup (multiple of 4; host-computed, = kernel wg_range)
   // key table (open addressing, linear probing, EMPTY = 0)
   unsigned long long *gkeys;
   uint32_t log2cap;
@@ -66,12 +67,29 @@ struct IngestParams {
   unsigned long long *dbg;  // diagnostic timestamps [G][8] (nullptr in production)
 };
 
-// Key-table slot: 32-bit multiplicative hash of the folded id (one v_mul on
-// the device; ids are xxh64 outputs from the host, log2cap in 4..31).
-__host__ __device__ inline uint32_t slot_of(uint64_t key, uint32_t log2cap) {
-  const uint32_t h = (uint32_t)(key ^ (key >> 32)) * 0x9E3779B1u;
-  return h >> (32 - log2cap);
+// Key-table layout: cap = 2^log2cap slots in buckets of 4 (log2cap in 4..31).
+// A key's probe sequence is its first-choice bucket b1, then its second-choice
+// bucket b2, then the buckets after b2 in order (every slot within cap + 4
+// positions).  Inserts CAS into the first empty slot of the sequence and slots
+// never empty again, so concurrent inserts of one key meet at the same slot.
+// Two choices keep 97-99 % of a ~0.7-load table's keys in b1/b2, so the LDS
+// lookup of the ingest kernel is two fixed 32-B bucket reads with no probe
+// loop (ids are xxh64 outputs from the host; any bits are usable).
+struct ProbeSeq {
+  uint32_t b1, b2, nbmask;
+};
+__host__ __device__ inline ProbeSeq probe_seq(uint64_t key, uint32_t log2cap) {
+  const uint32_t h1 = ((uint32_t)key ^ (uint32_t)(key >> 32)) * 0x9E3779B1u;
+  const uint32_t h2 = (h1 ^ (h1 >> 16)) * 0x85EBCA6Bu;
+  const uint32_t sh = 34 - log2cap;  // top (log2cap - 2) bits
+  return ProbeSeq{h1 >> sh, h2 >> sh, (1u << (log2cap - 2)) - 1};
 }
+__host__ __device__ inline uint32_t seq_slot(const ProbeSeq &p, uint32_t i) {
+  if (i < 4) return p.b1 * 4 + i;
+  const uint32_t q = i - 4;
+  return ((p.b2 + (q >> 2)) & p.nbmask) * 4 + (q & 3);
+}
+inline uint32_t max_probe_of(uint32_t log2cap) { return (1u << log2cap) + 4; }
 
 
 // HBM-table path variants (spans per lane, prefetch; 256-thread blocks).  The
@@ -86,8 +104,11 @@ constexpr int kNumVariants = 4;
 constexpr Variant kVariants[kNumVariants] = {{4, false, 1024}, {2, true, 1024}, {4, true, 512},
                                              {2, false, 1024}};
 constexpr uint32_t kHbmBlock = 256;
-constexpr int kNumLdsVariants = 4;                // {4,PF} {4,-} {2,PF} {2,-}
-constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2};
+// small-table kernels: 0-3 ingest_lds_kernel {4,PF} {4,-} {2,PF} {2,-}, 4-7 the
+// same with nt loads; 8-11 ingest_v2_kernel (S,NBUF,AUX) {2,2,0} {2,3,0} {4,1,0} {2,2,nt}
+constexpr int kNumLdsVariants = 19;
+constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2};
+constexpr uint32_t kDbgPerWg = 136;  // diagnostic stamps per workgroup: 8 + 16 waves x 8
 constexpr uint32_t kHllQueue = 2048;  // deferred HLL raises per workgroup (8 B each)
 // ingest_lds_kernel LDS beyond the table: HLL queue + its count + bin table
 constexpr size_t kLdsExtraBytes = kHllQueue * 8 + 16 + kBins * sizeof(BinEntry);

@@ -27,7 +27,6 @@ constexpr uint64_t kCmsSeed[8] = {0x9E3779B97F4A7C15ULL, 0xBF58476D1CE4E5B9ULL,
                                   0xA0761D6478BD642FULL, 0xE7037ED1A0B428DBULL,
                                   0x8EBC6AF09C88C6E3ULL, 0x589965CC75374CC3ULL};
 constexpr size_t kLdsBudget = 144 * 1024;  // small-table path LDS ceiling per workgroup
-constexpr uint32_t kMaxProbe = 4096;
 constexpr uint64_t kSlabLimit = 1ULL << 31;  // per-workgroup spans between slab reductions
 constexpr int kDefaultVariant = 0;            // sa::kVariants index (SPANAGG_VARIANT overrides)
 
@@ -264,7 +263,8 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   e->small = e->lds_bytes <= kLdsBudget;
   e->variant = kDefaultVariant;
   if (const char *v = std::getenv("SPANAGG_VARIANT"))  // tuning knob for A/B runs
-    e->variant = std::max(0, std::min(sa::kNumVariants - 1, std::atoi(v)));
+    e->variant = std::max(0, std::min((e->small ? sa::kNumLdsVariants : sa::kNumVariants) - 1,
+                                      std::atoi(v)));
   if (e->small) {
     e->spl = (uint32_t)sa::kLdsSpl[e->variant];
     e->block = 1024;
@@ -297,7 +297,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       (rc = alloc((void **)&e->d_seeds, sizeof kCmsSeed)) ||
       (rc = alloc((void **)&e->stats, 64)) || (rc = alloc((void **)&e->scratch, 64)))
     return bail(rc);
-  if (std::getenv("SPANAGG_STAMPS") && (rc = alloc((void **)&e->dbg, (size_t)e->G * 64)))
+  if (std::getenv("SPANAGG_STAMPS") && (rc = alloc((void **)&e->dbg, (size_t)e->G * sa::kDbgPerWg * 8)))
     return bail(rc);
   {
     sa::BinEntry bins[sa::kBins];
@@ -350,7 +350,9 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s);
 // Splits a batch so that each workgroup's range stays addressable by a 32-bit
 // buffer offset (< 2^27 spans per workgroup per launch).
 static int ingest_on(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
-  const uint64_t max_n = (uint64_t)e->G << 27;
+  // v2 small-table kernels keep u16 LDS counters for the whole launch: at most
+  // 65532 spans per workgroup per launch (ingest_v2_kernel has no epoch flush)
+  const uint64_t max_n = (uint64_t)e->G * ((e->small && e->variant >= 8) ? 65532u : (1u << 27));
   for (uint64_t off = 0; off < b->n; off += max_n) {
     const uint64_t m = std::min(max_n, b->n - off);
     sa_span_batch sub{b->key_hash + off, b->start_ns + off, b->end_ns + off, b->trace_w0 + off,
@@ -380,9 +382,10 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.w1 = b->trace_w1;
   P.meta = b->meta;
   P.n = b->n;
+  P.wg_chunk = ((b->n + grid - 1) / grid + 3) / 4 * 4;
   P.gkeys = e->gkeys;
   P.log2cap = e->log2cap;
-  P.max_probe = kMaxProbe;
+  P.max_probe = sa::max_probe_of(e->log2cap);
   P.slab_cnt = e->slab_cnt;
   P.slab_sum = e->slab_sum;
   P.gcounts = e->gcounts;
@@ -649,7 +652,7 @@ int sa_window_advance(sa_engine *e, uint64_t new_base) {
 
 int sa_debug_stamps(sa_engine *e, uint64_t *out, uint64_t cap, uint64_t *n_out) {
   if (!e || !n_out) return SA_EINVAL;
-  *n_out = e->dbg ? (uint64_t)e->G * 8 : 0;
+  *n_out = e->dbg ? (uint64_t)e->G * sa::kDbgPerWg : 0;
   if (!e->dbg || !out) return SA_OK;
   if (int rc = set_dev(e)) return rc;
   SA_HIP(e, hipStreamSynchronize(e->stream));
@@ -707,7 +710,7 @@ int sa_gather_dense(sa_engine *e, const uint64_t *d_keys, uint64_t n, uint64_t *
     SA_HIP(e, hipStreamWaitEvent(s, e->ev_a, 0));
   }
   if (int rc = reduce_slabs(e, s)) return rc;
-  SA_HIP(e, sa::launch_gather_dense(e->gkeys, e->gcounts, e->log2cap, kMaxProbe, e->nbk + 1,
+  SA_HIP(e, sa::launch_gather_dense(e->gkeys, e->gcounts, e->log2cap, sa::max_probe_of(e->log2cap), e->nbk + 1,
                                     d_keys, n, d_rows, s));
   if (reset) SA_HIP(e, hipMemsetAsync(e->gcounts, 0, e->cap * (e->nbk + 1) * 8, s));
   if (s != e->stream) {

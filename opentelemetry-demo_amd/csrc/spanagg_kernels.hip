@@ -79,45 +79,57 @@ __device__ __forceinline__ uint32_t bucket_of(uint64_t d, const IngestParams &P)
   }
 }
 
+// Find-or-insert along the key's probe sequence (sa_internal.h), starting at
+// sequence position i0; kNotFound when the table is full.
 __device__ __forceinline__ uint32_t g_find_insert(unsigned long long *keys, uint64_t key,
-                                                  uint32_t log2cap, uint32_t max_probe) {
-  const uint64_t mask = (1ULL << log2cap) - 1;
-  uint64_t s = slot_of(key, log2cap);
-  for (uint32_t i = 0; i < max_probe; ++i) {
+                                                  uint32_t log2cap, uint32_t max_probe,
+                                                  uint32_t i0 = 0) {
+  const ProbeSeq pr = probe_seq(key, log2cap);
+  for (uint32_t i = i0; i < max_probe; ++i) {
+    const uint32_t s = seq_slot(pr, i);
     unsigned long long k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (k == key) return (uint32_t)s;
+    if (k == key) return s;
     if (k == 0) {
       unsigned long long prev = atomicCAS(&keys[s], 0ULL, (unsigned long long)key);
-      if (prev == 0 || prev == key) return (uint32_t)s;
+      if (prev == 0 || prev == key) return s;
     }
-    s = (s + 1) & mask;
   }
   return kNotFound;
 }
 
 __device__ __forceinline__ uint32_t g_find(const unsigned long long *keys, uint64_t key,
                                            uint32_t log2cap, uint32_t max_probe) {
-  const uint64_t mask = (1ULL << log2cap) - 1;
-  uint64_t s = slot_of(key, log2cap);
+  const ProbeSeq pr = probe_seq(key, log2cap);
   for (uint32_t i = 0; i < max_probe; ++i) {
+    const uint32_t s = seq_slot(pr, i);
     unsigned long long k = keys[s];
-    if (k == key) return (uint32_t)s;
+    if (k == key) return s;
     if (k == 0) return kNotFound;
-    s = (s + 1) & mask;
   }
   return kNotFound;
 }
 
 // Raise one u8 HLL register to rho (CAS on the containing aligned u32).
+// Address-space-qualified views (so cold paths use global_/s_load forms, not
+// flat: flat ops count in both vmcnt and lgkmcnt and complete out of order,
+// which makes every later wait in the loop conservative).
+#define SA_GLOBAL __attribute__((address_space(1)))
+#define SA_CONST __attribute__((address_space(4)))
+template <class T>
+__device__ __forceinline__ SA_GLOBAL T *gbl(T *p) {
+  return (SA_GLOBAL T *)p;
+}
+
 __device__ __forceinline__ void hll_raise(uint8_t *reg, uint32_t rho) {
-  uint32_t *word = reinterpret_cast<uint32_t *>(reinterpret_cast<uintptr_t>(reg) & ~uintptr_t(3));
+  SA_GLOBAL uint32_t *word =
+      gbl(reinterpret_cast<uint32_t *>(reinterpret_cast<uintptr_t>(reg) & ~uintptr_t(3)));
   const uint32_t sh = (uint32_t)(reinterpret_cast<uintptr_t>(reg) & 3) * 8;
   uint32_t old = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  while (((old >> sh) & 0xFFu) < rho) {
+  while (((old >> sh) & 0xFFu) < rho) {  // a failed CAS refreshes `old`
     const uint32_t nw = (old & ~(0xFFu << sh)) | (rho << sh);
-    const uint32_t prev = atomicCAS(word, old, nw);
-    if (prev == old) break;
-    old = prev;
+    if (__hip_atomic_compare_exchange_strong(word, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      break;
   }
 }
 
@@ -177,33 +189,58 @@ struct SpanTile {
   int cnt;
 };
 
+template <int AUX = 0>
 __device__ __forceinline__ void u64x2(__amdgpu_buffer_rsrc_t r, int off, uint64_t &x, uint64_t &y) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
   x = (uint64_t)v[0] | ((uint64_t)v[1] << 32);
   y = (uint64_t)v[2] | ((uint64_t)v[3] << 32);
 }
 
-template <int S>
+// AUX: buffer-load cache policy (gfx950: 2 = nt, streamed once; keeps the
+// key table / HLL registers resident in L2 instead of the span stream).
+template <int S, int AUX = 0>
 __device__ __forceinline__ void load_tile(const Cols &c, uint32_t off, uint32_t len,
                                           SpanTile<S> &v) {
   static_assert(S == 2 || S == 4, "2 or 4 spans per lane");
 #pragma unroll
   for (int h = 0; h < S / 2; ++h) {
     const int ob = (int)(off * 8 + 16 * h);
-    u64x2(c.key, ob, v.key[2 * h], v.key[2 * h + 1]);
-    u64x2(c.start, ob, v.s[2 * h], v.s[2 * h + 1]);
-    u64x2(c.end, ob, v.e[2 * h], v.e[2 * h + 1]);
-    u64x2(c.w0, ob, v.a[2 * h], v.a[2 * h + 1]);
-    u64x2(c.w1, ob, v.b[2 * h], v.b[2 * h + 1]);
+    u64x2<AUX>(c.key, ob, v.key[2 * h], v.key[2 * h + 1]);
+    u64x2<AUX>(c.start, ob, v.s[2 * h], v.s[2 * h + 1]);
+    u64x2<AUX>(c.end, ob, v.e[2 * h], v.e[2 * h + 1]);
+    u64x2<AUX>(c.w0, ob, v.a[2 * h], v.a[2 * h + 1]);
+    u64x2<AUX>(c.w1, ob, v.b[2 * h], v.b[2 * h + 1]);
   }
   if constexpr (S == 4) {
-    const auto m = __builtin_amdgcn_raw_buffer_load_b128(c.meta, (int)(off * 4), 0, 0);
+    const auto m = __builtin_amdgcn_raw_buffer_load_b128(c.meta, (int)(off * 4), 0, AUX);
     v.meta[0] = m[0]; v.meta[1] = m[1]; v.meta[2] = m[2]; v.meta[3] = m[3];
   } else {
-    const auto m = __builtin_amdgcn_raw_buffer_load_b64(c.meta, (int)(off * 4), 0, 0);
+    const auto m = __builtin_amdgcn_raw_buffer_load_b64(c.meta, (int)(off * 4), 0, AUX);
     v.meta[0] = m[0]; v.meta[1] = m[1];
   }
   v.cnt = off < len ? ((len - off) < (uint32_t)S ? (int)(len - off) : S) : 0;
+}
+
+// Tile loads with per-tile buffer descriptors: the descriptors are rebuilt
+// from the column pointers at every tile (a few SALU), so only the six 64-bit
+// column bases stay live across the loop instead of six 4-SGPR descriptors.
+// `first` = first span of the tile (absolute), `remain` = spans of the
+// workgroup's range from `first` on (0 when past the end).
+template <int S, int AUX = 0>
+__device__ __forceinline__ void load_tile_at(const IngestParams &P, uint64_t first, uint32_t remain,
+                                             uint32_t lane_off, SpanTile<S> &v) {
+  Cols c;
+  // readfirstlane: hipcc lowers the caller's saturating subtract to a VALU
+  // op, and a descriptor word in a VGPR turns every load into a waterfall loop
+  remain = (uint32_t)__builtin_amdgcn_readfirstlane((int)remain);
+  const uint32_t b8 = remain * 8, b4 = remain * 4;
+  c.key = rsrc(P.key + first, b8);
+  c.start = rsrc(P.start + first, b8);
+  c.end = rsrc(P.end + first, b8);
+  c.w0 = rsrc(P.w0 + first, b8);
+  c.w1 = rsrc(P.w1 + first, b8);
+  c.meta = rsrc(P.meta + first, b4);
+  load_tile<S, AUX>(c, lane_off, remain, v);
 }
 
 // Sketch phase A: validate service / window, hash the trace id and issue the
@@ -284,6 +321,14 @@ __device__ __forceinline__ void sketch_post(const IngestParams &P, const SpanTil
 #pragma unroll
   for (int j = 0; j < S; ++j)
     if ((k.cur[j] & 0xFFu) < k.rho[j]) hll_raise(k.reg[j], k.rho[j]);
+}
+
+// Contiguous per-workgroup span range [lo, hi) from the host-computed chunk
+// (scalar arithmetic only: no 64-bit division in the kernel).
+__device__ __forceinline__ void wg_range_p(const IngestParams &P, uint64_t &lo, uint64_t &hi) {
+  lo = (uint64_t)blockIdx.x * P.wg_chunk;
+  if (lo > P.n) lo = P.n;
+  hi = lo + P.wg_chunk < P.n ? lo + P.wg_chunk : P.n;
 }
 
 // Contiguous per-workgroup span range [lo, hi), lo a multiple of 4.
@@ -377,12 +422,15 @@ __device__ __forceinline__ uint32_t bucket_lds(uint64_t d, const BinEntry *bins,
   }
 }
 
-// Probe the LDS key mirror past slot s (already known not to hold `key`);
-// returns the slot or kNotFound (empty slot reached / probe limit).
+// Probe the LDS key mirror along the key's sequence from position i0 (the
+// earlier positions are known not to hold `key`); returns the slot or
+// kNotFound (empty slot reached / probe limit).
 __device__ __forceinline__ uint32_t lds_probe_rest(const unsigned long long *lkeys, uint64_t key,
-                                                   uint32_t s, uint32_t mask, uint32_t max_probe) {
-  for (uint32_t q = 1; q < max_probe; ++q) {
-    s = (s + 1) & mask;
+                                                   uint32_t log2cap, uint32_t i0,
+                                                   uint32_t max_probe) {
+  const ProbeSeq pr = probe_seq(key, log2cap);
+  for (uint32_t i = i0; i < max_probe; ++i) {
+    const uint32_t s = seq_slot(pr, i);
     const unsigned long long kk = lkeys[s];
     if (kk == key) return s;
     if (kk == 0) break;
@@ -406,10 +454,10 @@ __device__ __forceinline__ uint32_t lds_probe_rest(const unsigned long long *lke
 // the SA_DIAG_* ablation bits (profiling builds only).
 // LDS: lkeys[cap] u64 | lsum[cap] u64 | lcnt[cap][nw] u32 | hq[kHllQueue] u64 |
 //      hq_n (16 B) | bins[kBins]
-template <int BK, int S, bool PF, bool DIAG>
+template <int BK, int S, bool PF, bool DIAG, int AUX = 0>
 __global__ __launch_bounds__(kLdsBlock) void ingest_lds_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t cap = 1u << P.log2cap;
   const uint32_t mask = cap - 1;
   const uint32_t nbk = P.nbk;
@@ -443,7 +491,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_lds_kernel(IngestParams P) {
   uint4 bv = make_uint4(0, 0, 0, 0);
   if (BK == 1 && threadIdx.x < kBins * 2) bv = reinterpret_cast<const uint4 *>(P.bintab)[threadIdx.x];
   SpanTile<S> cur;
-  load_tile<S>(c, off, len, cur);
+  load_tile<S, AUX>(c, off, len, cur);
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const uint32_t i = threadIdx.x + u * kLdsBlock;
@@ -456,7 +504,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_lds_kernel(IngestParams P) {
   for (uint32_t i = threadIdx.x; i < cap * nw; i += kLdsBlock) lcnt[i] = 0;
   if (threadIdx.x == 0) *hq_n = 0;
   __syncthreads();
-  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 1] = __builtin_amdgcn_s_memrealtime();
 
   LaneStats st{0, 0, 0, 0};
   uint32_t in_epoch = 0;
@@ -496,7 +544,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_lds_kernel(IngestParams P) {
       unsigned long long k0[S];
 #pragma unroll
       for (int j = 0; j < S; ++j) {
-        sl[j] = slot_of(key[j], P.log2cap);
+        sl[j] = probe_seq(key[j], P.log2cap).b1 * 4;
         k0[j] = lkeys[sl[j]];
       }
 #pragma unroll
@@ -505,7 +553,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_lds_kernel(IngestParams P) {
         if (key[j] != 0) {
           found[j] = k0[j] == key[j] ? sl[j]
                      : k0[j] == 0    ? kNotFound
-                                     : lds_probe_rest(lkeys, key[j], sl[j], mask, P.max_probe);
+                                     : lds_probe_rest(lkeys, key[j], P.log2cap, 1, P.max_probe);
           if (found[j] == kNotFound) {
             found[j] = g_find_insert(P.gkeys, key[j], P.log2cap, P.max_probe);
             if (found[j] != kNotFound) lkeys[found[j]] = key[j];
@@ -535,11 +583,12 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_lds_kernel(IngestParams P) {
     // 4. HLL register reads (unconditional: offset 0 when unused)
     uint32_t hv[S];
 #pragma unroll
-    for (int j = 0; j < S; ++j) hv[j] = P.hll[hoff[j]];
+    for (int j = 0; j < S; ++j)
+      hv[j] = *reinterpret_cast<const uint32_t *>(P.hll + (hoff[j] & ~3u));
     // 5. prefetch the next tile
     if constexpr (PF) {
       __builtin_amdgcn_sched_barrier(0);
-      load_tile<S>(c, off + tile, len, cur);
+      load_tile<S, AUX>(c, off + tile, len, cur);
       __builtin_amdgcn_sched_barrier(0);
     }
     // 5b. RED update: LDS u16 bucket counter + u64 ns sum
@@ -561,7 +610,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_lds_kernel(IngestParams P) {
         else hll_raise(P.hll + hoff[j], rho);
       }
     }
-    if constexpr (!PF) load_tile<S>(c, off + tile, len, cur);
+    if constexpr (!PF) load_tile<S, AUX>(c, off + tile, len, cur);
     if (++in_epoch == P.epoch_tiles) {  // u16 LDS counters: flush before they can wrap
       __syncthreads();
       flush_lds(P, cap, nw, lsum, lcnt);
@@ -569,13 +618,419 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_lds_kernel(IngestParams P) {
       in_epoch = 0;
     }
   }
-  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 2] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
   flush_lds(P, cap, nw, lsum, lcnt);
   const uint32_t nq = *hq_n < kHllQueue ? *hq_n : kHllQueue;
   for (uint32_t i = threadIdx.x; i < nq; i += kLdsBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
-  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 3] = __builtin_amdgcn_s_memrealtime();
   flush_stats(P, st);
+}
+
+// ---------------------------------------------------------------------------
+// Small-table path, v2.  Same LDS layout and slab flush as ingest_lds_kernel;
+// the span loop is rebuilt for latency tolerance at 16 waves per CU:
+//   * NBUF tiles of S spans per lane in flight per wave (a register ring): a
+//     tile is re-filled right after it is compacted, so every wave keeps
+//     loads outstanding while it computes;
+//   * the key lookup reads the key's two 4-slot buckets from the LDS mirror
+//     (4 x 16-B reads, fixed cost, no probe loop); only keys outside their two
+//     buckets (a few % of a 0.7-load table, none at all after the first
+//     launch for C2) take the wave-uniform cold path;
+//   * HLL register reads are issued one step ahead of their compare, so the
+//     wait for them is a counted vmcnt that leaves two tiles in flight;
+//   * event statistics are per-wave ballot counts (scalar registers).
+// LDS: lkeys[cap] u64 | lsum[cap] u64 | lcnt[cap][nw] u32 | hq[kHllQueue] u64 |
+//      hq_n (16 B) | bins[kBins]
+// Cold paths of ingest_v2_kernel.  They are inlined, but read the kernel
+// parameters they need through a laundered kernarg pointer inside the cold
+// block: those loads cannot be hoisted to kernel entry, so the parameters only
+// the cold paths use do not occupy scalar registers across the span loop.
+__device__ __forceinline__ SA_CONST const IngestParams &cold_params() {
+  SA_CONST const IngestParams *kp =
+      (SA_CONST const IngestParams *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(kp));
+  return *kp;
+}
+
+// Wave-cooperative find-or-insert of ONE (wave-uniform) key: the 64 lanes
+// test 64 consecutive positions of its probe sequence at once, first in the
+// LDS mirror, then in the HBM table (where the first empty position is
+// claimed by CAS).  No divergent loop, so no per-lane exec-mask nesting.
+// Must be called with all lanes active; returns the slot (uniform) or
+// kNotFound when the table is full.
+__device__ __forceinline__ uint32_t wave_find_insert(unsigned long long *lkeys, uint64_t k,
+                                                     uint32_t log2cap) {
+  SA_CONST const IngestParams &Q = cold_params();
+  const uint32_t lane = threadIdx.x & 63;
+  const ProbeSeq pr = probe_seq(k, log2cap);
+  const uint32_t maxp = Q.max_probe;
+  for (uint32_t i0 = 0; i0 < maxp; i0 += 64) {  // LDS mirror
+    const uint32_t pos = i0 + lane;
+    const uint32_t sl = seq_slot(pr, pos < maxp ? pos : maxp - 1);
+    const unsigned long long v = lkeys[sl];
+    const uint64_t mh = __ballot(v == k), me = __ballot(v == 0);
+    if (mh | me) {
+      if (mh && (!me || __builtin_ctzll(mh) < __builtin_ctzll(me)))
+        return (uint32_t)__builtin_amdgcn_readlane((int)sl, __builtin_ctzll(mh));
+      break;
+    }
+  }
+  SA_GLOBAL unsigned long long *gk = gbl(Q.gkeys);
+  for (uint32_t i0 = 0; i0 < maxp;) {  // HBM table
+    const uint32_t pos = i0 + lane;
+    const uint32_t sl = seq_slot(pr, pos < maxp ? pos : maxp - 1);
+    const unsigned long long v = __hip_atomic_load(&gk[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t mh = __ballot(v == k), me = __ballot(v == 0 && pos < maxp);
+    if (!(mh | me)) {
+      i0 += 64;
+      continue;
+    }
+    const int first = __builtin_ctzll(mh | me);
+    const uint32_t fsl = (uint32_t)__builtin_amdgcn_readlane((int)sl, first);
+    if ((mh >> first) & 1) {
+      lkeys[fsl] = k;
+      return fsl;
+    }
+    unsigned long long prev = 0;
+    if ((int)lane == first) {
+      unsigned long long expect = 0;
+      __hip_atomic_compare_exchange_strong(&gk[fsl], &expect, (unsigned long long)k,
+                                           __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      prev = expect;
+    }
+    const uint32_t plo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)prev, first);
+    const uint32_t phi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(prev >> 32), first);
+    const uint64_t pv = ((uint64_t)phi << 32) | plo;
+    if (pv == 0 || pv == k) {
+      lkeys[fsl] = k;
+      return fsl;
+    }
+    i0 += (uint32_t)first;  // lost the race for that slot: re-read from it
+  }
+  return kNotFound;
+}
+
+// Resolves the lanes with `need` one distinct key at a time (lanes sharing a
+// key are resolved together); call with all lanes active.
+__device__ __forceinline__ void cold_lookup_wave(unsigned long long *lkeys, bool need, uint64_t key,
+                                                 uint32_t log2cap, uint32_t &found) {
+  uint64_t m = __ballot(need);
+  while (m) {
+    const int l = __builtin_ctzll(m);
+    const uint32_t klo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, l);
+    const uint32_t khi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(key >> 32), l);
+    const uint64_t k = ((uint64_t)khi << 32) | klo;
+    const uint32_t f = wave_find_insert(lkeys, k, log2cap);
+    const bool same = need && key == k;
+    found = same ? f : found;
+    m &= ~__ballot(same);
+  }
+}
+
+__device__ __forceinline__ void cold_cms_add(uint32_t ws, uint64_t key) {
+  SA_CONST const IngestParams &Q = cold_params();
+  SA_GLOBAL unsigned long long *row0 = gbl(Q.cms) + (uint64_t)ws * Q.cms_d * Q.cms_w;
+  const SA_GLOBAL uint64_t *seeds = gbl(Q.seeds);
+  for (uint32_t r = 0; r < Q.cms_d; ++r) {
+    const uint64_t col = splitmix64(key ^ seeds[r]) >> Q.cms_shift;
+    __hip_atomic_fetch_add(row0 + (uint64_t)r * Q.cms_w + col, 1ULL, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ __forceinline__ void cold_hll_raise(uint32_t hoff, uint32_t rho) {
+  hll_raise(cold_params().hll + hoff, rho);
+}
+
+template <int S>
+struct Pending {  // one step's HLL reads, compared one step later
+  uint32_t hoff[S], rho[S], hv[S];
+};
+
+__device__ __forceinline__ uint64_t copy_u64(uint64_t x) {
+  uint32_t lo, hi;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(lo) : "v"((uint32_t)x));
+  asm volatile("v_mov_b32 %0, %1" : "=v"(hi) : "v"((uint32_t)(x >> 32)));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t copy_u32(uint32_t x) {
+  uint32_t y;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+  return y;
+}
+
+__device__ __forceinline__ uint32_t wave_count(bool p) {
+  return (uint32_t)__popcll(__ballot(p));
+}
+
+// LC / NWC / PC: table log2 capacity, counter words per slot and HLL precision
+// fixed at compile time for the common geometry (0 = read from P).
+// HAUX >= 0: HLL register reads as buffer loads with that cache policy (gfx950:
+// 1 = sc0, 2 = nt, 16 = sc1); -1 = plain global loads.
+template <int S, int NBUF, int AUX, bool DIAG, int LC = 0, int NWC = 0, int PC = 0, int HAUX = -1>
+__global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 0] = __builtin_amdgcn_s_memrealtime();
+  const uint32_t log2cap = LC ? (uint32_t)LC : P.log2cap;
+  const uint32_t cap = 1u << log2cap;
+  const uint32_t nw = NWC ? (uint32_t)NWC : (P.nbk + 1) >> 1;
+  const uint32_t hp = PC ? (uint32_t)PC : P.p;
+  const uint32_t diag = DIAG ? P.diag : 0u;
+  unsigned long long *lkeys = reinterpret_cast<unsigned long long *>(smem);
+  unsigned long long *lsum = lkeys + cap;
+  uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + cap);
+  uint2 *hq = reinterpret_cast<uint2 *>(lcnt + cap * nw);
+  uint32_t *hq_n = reinterpret_cast<uint32_t *>(hq + kHllQueue);
+  BinEntry *lbins = reinterpret_cast<BinEntry *>(hq_n + 4);
+
+  uint64_t lo, hi;
+  wg_range_p(P, lo, hi);
+  const uint32_t len = (uint32_t)(hi - lo);
+  constexpr uint32_t tile = kLdsBlock * S;
+  const uint32_t lane_off = threadIdx.x * S;
+
+  // Prologue: key-table loads (16 B per lane, <= 4 per lane for cap <= 8192)
+  // and the bin table first, then the first NBUF tiles; the LDS setup then
+  // waits only for the key-table loads (vmcnt counts in issue order).
+  ulonglong2 kv[4];
+  const uint32_t per = (cap + 2 * kLdsBlock - 1) / (2 * kLdsBlock);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const uint32_t i = 2 * (threadIdx.x + u * kLdsBlock);
+    kv[u] = (u < (int)per && i < cap) ? *reinterpret_cast<const ulonglong2 *>(P.gkeys + i)
+                                      : make_ulonglong2(0, 0);
+  }
+  uint4 bv = make_uint4(0, 0, 0, 0);
+  if (threadIdx.x < kBins * 2) bv = reinterpret_cast<const uint4 *>(P.bintab)[threadIdx.x];
+  // Issue order = the steady state's (tile, then S HLL reads, per step), so
+  // the loop header's vmcnt accounting is the same from both predecessors;
+  // the prologue's HLL reads seed `pend` (rho 0: never raised).
+  SpanTile<S> buf[NBUF];
+  Pending<S> pend;
+#pragma unroll
+  for (int b = 0; b < NBUF; ++b) {
+    const uint32_t t = b * tile;
+    load_tile_at<S, AUX>(P, (diag & 16u) ? t % (4 * tile) : lo + t, len > t ? len - t : 0u,
+                         lane_off, buf[b]);
+    if (b == NBUF - 1) {
+      uint32_t z;  // a VGPR zero: keeps these vector loads (a uniform address would be s_load)
+      asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+#pragma unroll
+      for (int j = 0; j < S; ++j) pend.hv[j] = *reinterpret_cast<const uint32_t *>(P.hll + z);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const uint32_t i = 2 * (threadIdx.x + u * kLdsBlock);
+    if (u < (int)per && i < cap) {
+      reinterpret_cast<ulonglong2 *>(lkeys)[i / 2] = kv[u];
+      reinterpret_cast<ulonglong2 *>(lsum)[i / 2] = make_ulonglong2(0, 0);
+    }
+  }
+  if (threadIdx.x < kBins * 2) reinterpret_cast<uint4 *>(lbins)[threadIdx.x] = bv;
+  for (uint32_t i = threadIdx.x * 4; i < cap * nw; i += kLdsBlock * 4)
+    *reinterpret_cast<uint4 *>(lcnt + i) = make_uint4(0, 0, 0, 0);
+  if (threadIdx.x == 0) *hq_n = 0;
+  __syncthreads();
+  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 1] = __builtin_amdgcn_s_memrealtime();
+
+  // diagnostic build: per-wave cycle sums of the step's segments (s_memtime;
+  // the stamp's lgkmcnt(0) serialises LDS, so read shares, not lengths)
+  uint64_t seg[6] = {0, 0, 0, 0, 0, 0}, t_prev = 0;
+  auto stamp = [&](int i) {
+    if (DIAG && P.dbg) {
+      __builtin_amdgcn_sched_barrier(0);
+      uint64_t t;
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (i >= 0) seg[i] += t - t_prev;
+      t_prev = t;
+    }
+  };
+  stamp(-1);
+  const __amdgpu_buffer_rsrc_t hll_rsrc = rsrc(P.hll, 0xFFFFFFFFu);
+  // wave-uniform event counts (scalar registers)
+  uint32_t n_zero = 0, n_badsvc = 0, n_oor = 0, n_drop = 0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) pend.hoff[j] = pend.rho[j] = 0;
+
+  // HLL compare of the previous step's reads; registers that grow are queued
+  // in LDS and raised after the loop (no returning global atomic in the loop).
+  auto hll_settle = [&](const Pending<S> &q) {
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      // hv: the aligned u32 word holding the register (a u8 load would be
+      // zero-extended by a v_and at the loop-carried copy, which waits for it)
+      if (((q.hv[j] >> ((q.hoff[j] & 3u) * 8)) & 0xFFu) < q.rho[j]) {
+        const uint32_t slot = atomicAdd(hq_n, 1u);
+        if (slot < kHllQueue) hq[slot] = make_uint2(q.hoff[j], q.rho[j]);
+        else cold_hll_raise(q.hoff[j], q.rho[j]);
+      }
+    }
+  };
+
+  auto step = [&](SpanTile<S> &T, uint32_t toff) {
+    // 1. compact the landed tile (its registers are re-filled in step 3)
+    uint64_t key[S], dur[S];
+    uint32_t bkt[S], ws[S], hoff[S], rho[S];
+    bool err[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const bool valid = lane_off + toff + (uint32_t)j < len;
+      // 0 past the range (buffer bounds check).  An explicit copy: the key is
+      // used after the tile registers are re-filled, and sharing them would
+      // make the allocator rotate the tile ring through copies that wait.
+      key[j] = copy_u64(T.key[j]);
+      if (!(diag & 128u)) n_zero += wave_count(valid && key[j] == 0);
+      dur[j] = T.e[j] > T.s[j] ? T.e[j] - T.s[j] : 0;
+      bkt[j] = (diag & 32u) ? (uint32_t)dur[j] & 15u : bucket_lds<1>(dur[j], lbins, P);
+      const uint32_t meta = copy_u32(T.meta[j]);  // see key
+      const uint32_t svc = meta & 0xFFFFu;
+      const bool svc_ok = svc < P.n_services;
+      ws[j] = (diag & 64u) ? (uint32_t)(T.e[j] >> 34) & 7u : window_slot(P, T.e[j]);
+      const bool win_ok = ws[j] != 0xFFFFFFFFu;
+      if (!(diag & 128u)) {
+        n_badsvc += wave_count(valid && !svc_ok);
+        n_oor += wave_count(valid && svc_ok && !win_ok);
+      }
+      const bool sk = valid && svc_ok && win_ok;
+      err[j] = sk && ((meta >> 19) & 3u) == 2u && !(diag & 4u);
+      rho[j] = 0;
+      hoff[j] = 0;
+      if (!(diag & 2u)) {
+        const uint64_t x = xxh64_16(T.a[j], T.b[j]);
+        const uint32_t r = (uint32_t)__clzll((long long)((x << hp) | (1ULL << (hp - 1)))) + 1;
+        rho[j] = sk ? r : 0u;
+        hoff[j] = sk ? ((ws[j] * P.n_services + svc) << hp) + (uint32_t)(x >> (64 - hp)) : 0u;
+      }
+    }
+    stamp(0);
+    // 2. this step's HLL register reads (unconditional: offset 0 when unused)
+    uint32_t hv[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      if (DIAG && (diag & 512u)) {  // diag: blind byte store instead of the read
+        P.hll[hoff[j]] = (uint8_t)rho[j];
+        hv[j] = 0xFFFFFFFFu;
+      } else if (DIAG && (diag & 1024u)) {  // diag: no read at all
+        hv[j] = 0xFFFFFFFFu;
+      } else {
+        hv[j] = HAUX < 0 ? *reinterpret_cast<const uint32_t *>(P.hll + (hoff[j] & ~3u))
+                         : (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(
+                               hll_rsrc, (int)(hoff[j] & ~3u), 0, HAUX < 0 ? 0 : HAUX);
+      }
+    }
+    // 3. re-fill the tile registers with the tile NBUF steps ahead
+    __builtin_amdgcn_sched_barrier(0);
+    {
+      const uint32_t t = toff + NBUF * tile;
+      load_tile_at<S, AUX>(P, (diag & 16u) ? t % (4 * tile) : lo + t, len > t ? len - t : 0u,
+                           lane_off, T);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    stamp(1);
+    // 4. key lookup: the two candidate buckets in the LDS mirror
+    uint32_t found[S];
+    if (!(diag & 1u)) {
+      bool need[S];
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        const ProbeSeq pr = probe_seq(key[j], log2cap);
+        const ulonglong2 *b1 = reinterpret_cast<const ulonglong2 *>(lkeys + pr.b1 * 4);
+        const ulonglong2 *b2 = reinterpret_cast<const ulonglong2 *>(lkeys + pr.b2 * 4);
+        const ulonglong2 q1a = b1[0], q1b = b1[1], q2a = b2[0], q2b = b2[1];
+        const unsigned long long k = key[j];
+        uint32_t f = kNotFound;
+        f = q2b.y == k ? pr.b2 * 4 + 3 : f;
+        f = q2b.x == k ? pr.b2 * 4 + 2 : f;
+        f = q2a.y == k ? pr.b2 * 4 + 1 : f;
+        f = q2a.x == k ? pr.b2 * 4 + 0 : f;
+        f = q1b.y == k ? pr.b1 * 4 + 3 : f;
+        f = q1b.x == k ? pr.b1 * 4 + 2 : f;
+        f = q1a.y == k ? pr.b1 * 4 + 1 : f;
+        f = q1a.x == k ? pr.b1 * 4 + 0 : f;
+        found[j] = k != 0 ? f : kNotFound;
+        need[j] = k != 0 && f == kNotFound;
+      }
+      // 5. cold path (wave-uniform): keys outside their two buckets or not yet
+      //    in this workgroup's mirror
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        if (__builtin_expect(__ballot(need[j]) != 0, 0)) {
+          cold_lookup_wave(lkeys, need[j], key[j], log2cap, found[j]);
+          n_drop += wave_count(need[j] && found[j] == kNotFound);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        found[j] = kNotFound;
+        n_drop += wave_count(((key[j] ^ dur[j] ^ bkt[j]) & 0xFFFFFFFFFFFFULL) == 0x123456789ABCULL);
+      }
+    }
+    stamp(2);
+    // 6. ERROR spans: exact per-(window, slot) counter (one no-return atomic);
+    //    spans without a slot update the count-min cells directly
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      if (err[j]) {
+        if (found[j] != kNotFound)
+          atomicAdd(P.errcnt + ((uint64_t)ws[j] << log2cap) + found[j], 1ULL);
+        else
+          cold_cms_add(ws[j], key[j]);
+      }
+    }
+    // 7. RED update: LDS u16 bucket counter + u64 ns sum
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      if (found[j] != kNotFound) {
+        const uint32_t b = bkt[j];
+        atomicAdd(&lcnt[found[j] * nw + (b >> 1)], 1u << ((b & 1) * 16));
+        atomicAdd(&lsum[found[j]], (unsigned long long)dur[j]);
+      }
+    }
+    stamp(3);
+    // 8. settle the previous step's HLL reads, keep this step's for the next
+    hll_settle(pend);
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      pend.hoff[j] = hoff[j];
+      pend.rho[j] = rho[j];
+      pend.hv[j] = hv[j];
+    }
+    stamp(4);
+  };
+
+  // Whole rounds of NBUF steps (a step past the range sees only zero-filled
+  // lanes and does nothing): no exit between the steps of a round, so the
+  // register allocator keeps each in-flight tile in one set of registers
+  // across the back-edge instead of copying it (a copy waits for the loads).
+  const uint32_t loop_len = (diag & 256u) ? 0u : len;  // diag: prologue/epilogue only
+  for (uint32_t t0 = 0; t0 < loop_len; t0 += NBUF * tile) {
+#pragma unroll
+    for (int b = 0; b < NBUF; ++b) step(buf[b], t0 + b * tile);
+  }
+  hll_settle(pend);
+  const uint64_t wave_loop_end = DIAG && P.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 2] = __builtin_amdgcn_s_memrealtime();
+  __syncthreads();
+  flush_lds(P, cap, nw, lsum, lcnt);
+  const uint32_t nq = *hq_n < kHllQueue ? *hq_n : kHllQueue;
+  for (uint32_t i = threadIdx.x; i < nq; i += kLdsBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
+  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 3] = __builtin_amdgcn_s_memrealtime();
+  if (DIAG && P.dbg && (threadIdx.x & 63) == 0) {
+    for (int i = 0; i < 6; ++i) P.dbg[blockIdx.x * kDbgPerWg + 8 + (threadIdx.x >> 6) * 8 + i] = seg[i];
+    P.dbg[blockIdx.x * kDbgPerWg + 8 + (threadIdx.x >> 6) * 8 + 6] = wave_loop_end;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (n_zero) atomicAdd(&P.stats[kStatZeroKey], (unsigned long long)n_zero);
+    if (n_badsvc) atomicAdd(&P.stats[kStatInvalidService], (unsigned long long)n_badsvc);
+    if (n_oor) atomicAdd(&P.stats[kStatWindowOOR], (unsigned long long)n_oor);
+    if (n_drop) atomicAdd(&P.stats[kStatDropped], (unsigned long long)n_drop);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -747,6 +1202,22 @@ uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap_blocks) {
 // Small-table kernels: bin-table bucketing in four (spans/lane, prefetch)
 // variants, the linear-threshold fallback, and the diagnostic build.
 static const void *small_fn(bool bt, int v, bool diag) {
+  if (bt && v >= 8) {  // v2 kernels (bin-table bucketing only)
+    if (diag) return (const void *)&ingest_v2_kernel<2, 2, 0, true>;
+    switch (v) {
+      case 9: return (const void *)&ingest_v2_kernel<2, 3, 0, false>;
+      case 10: return (const void *)&ingest_v2_kernel<4, 1, 0, false>;
+      case 11: return (const void *)&ingest_v2_kernel<2, 2, 2, false>;
+      case 12: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14>;
+      case 13: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14, 1>;
+      case 14: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14, 2>;
+      case 15: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14, 16>;
+      case 16: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14, 3>;
+      case 17: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, 2>;
+      case 18: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, 0>;
+      default: return (const void *)&ingest_v2_kernel<2, 2, 0, false>;
+    }
+  }
   if (diag) return bt ? (const void *)&ingest_lds_kernel<1, 4, true, true>
                       : (const void *)&ingest_lds_kernel<0, 4, true, true>;
   if (!bt) return (const void *)&ingest_lds_kernel<0, 4, true, false>;
@@ -754,6 +1225,10 @@ static const void *small_fn(bool bt, int v, bool diag) {
     case 1: return (const void *)&ingest_lds_kernel<1, 4, false, false>;
     case 2: return (const void *)&ingest_lds_kernel<1, 2, true, false>;
     case 3: return (const void *)&ingest_lds_kernel<1, 2, false, false>;
+    case 4: return (const void *)&ingest_lds_kernel<1, 4, true, false, 2>;
+    case 5: return (const void *)&ingest_lds_kernel<1, 4, false, false, 2>;
+    case 6: return (const void *)&ingest_lds_kernel<1, 2, true, false, 2>;
+    case 7: return (const void *)&ingest_lds_kernel<1, 2, false, false, 2>;
     default: return (const void *)&ingest_lds_kernel<1, 4, true, false>;
   }
 }
@@ -783,6 +1258,8 @@ hipError_t prepare_ingest_small(size_t lds_bytes) {
 
 hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,
                                hipStream_t s, int variant) {
+  // the specialised v2 build is only valid for its compile-time geometry
+  if (variant >= 12 && !(P.log2cap == 11 && (P.nbk + 1) / 2 == 9 && P.p == 14)) variant = 8;
   const void *fn = small_fn(P.bintab != nullptr, variant, P.diag != 0 || P.dbg != nullptr);
   void *args[] = {const_cast<IngestParams *>(&P)};
   return hipLaunchKernel(fn, dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);

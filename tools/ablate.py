@@ -18,8 +18,24 @@ import torch  # noqa: E402
 from spanagg import Config, Engine  # noqa: E402
 from spanagg.synth import generate_c2  # noqa: E402
 
-NO_RED, NO_HLL, NO_CMS, NO_FLUSH = 1, 2, 4, 8
+NO_RED, NO_HLL, NO_CMS, NO_FLUSH, L2_INPUT = 1, 2, 4, 8, 16
+NO_BIN, NO_WIN, NO_STAT, NO_LOOP = 32, 64, 128, 256
+LO = NO_RED | NO_HLL | NO_CMS | NO_FLUSH
+VARIANTS_FINE = {
+    "prologue_only": NO_LOOP | NO_FLUSH,
+    "prologue_flush": NO_LOOP,
+    "lo_nobin": LO | NO_BIN,
+    "lo_nowin": LO | NO_WIN,
+    "lo_nostat": LO | NO_STAT,
+    "lo_bare": LO | NO_BIN | NO_WIN | NO_STAT,
+    "lo_bare_l2": LO | NO_BIN | NO_WIN | NO_STAT | L2_INPUT,
+    "hll_store": 512,
+    "hll_noread": 1024,
+}
 VARIANTS = {
+    "l2_input": L2_INPUT,
+    "l2_input_no_hll": L2_INPUT | NO_HLL,
+    "l2_input_loads_only": L2_INPUT | NO_RED | NO_HLL | NO_CMS | NO_FLUSH,
     "full": 0,
     "no_cms": NO_CMS,
     "no_hll": NO_HLL,
@@ -42,12 +58,15 @@ def main():
     torch.cuda.set_stream(stream)
     engines = {}
     base_variant = os.environ.get("SPANAGG_VARIANT", "0")
+    os.environ["SPANAGG_VARIANT"] = os.environ.get("ABL_BASE", base_variant)
+    if os.environ.get("ABL_FINE"):
+        VARIANTS.update(VARIANTS_FINE)
     for name, fl in VARIANTS.items():
         e = Engine(Config(n_services=wl.n_services, n_windows=16, flags=fl))
         e.window_advance(wl.first_window)
         engines[name] = e
     # kernel-structure variants (sa_internal.h kVariants), full work
-    for v in range(4):
+    for v in [int(x) for x in os.environ.get("ABL_VARS", "0,8,11,12").split(",")]:
         os.environ["SPANAGG_VARIANT"] = str(v)
         e = Engine(Config(n_services=wl.n_services, n_windows=16))
         e.window_advance(wl.first_window)

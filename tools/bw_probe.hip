@@ -51,6 +51,39 @@ __global__ __launch_bounds__(BLOCK) void read_contig(Cols c, unsigned long long 
   if (acc == 0x123456789ULL) out[0] = acc;
 }
 
+// contiguous ranges through buffer loads with cache-policy bits AUX
+// (gfx950: 1 = sc0, 2 = nt, 16 = sc1)
+template <int AUX>
+__global__ __launch_bounds__(1024) void read_buf(Cols c, unsigned long long n, unsigned long long *out) {
+  unsigned long long chunk = (n + gridDim.x - 1) / gridDim.x;
+  chunk = (chunk + 3) / 4 * 4;
+  unsigned long long lo = blockIdx.x * chunk;
+  if (lo > n) lo = n;
+  const unsigned long long hi = lo + chunk < n ? lo + chunk : n;
+  const unsigned len = (unsigned)(hi - lo);
+  auto mk = [&](const void *p, unsigned b) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)b, 0x00020000);
+  };
+  const auto rk = mk(c.k + lo, len * 8), rs = mk(c.s + lo, len * 8), re = mk(c.e + lo, len * 8),
+             ra = mk(c.a + lo, len * 8), rb = mk(c.b + lo, len * 8), rm = mk(c.m + lo, len * 4);
+  unsigned acc = 0;
+  for (unsigned i = threadIdx.x * 4; i < len; i += 1024 * 4) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int o = (int)(i * 8 + 16 * h);
+      const auto k = __builtin_amdgcn_raw_buffer_load_b128(rk, o, 0, AUX);
+      const auto s = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, AUX);
+      const auto e = __builtin_amdgcn_raw_buffer_load_b128(re, o, 0, AUX);
+      const auto a = __builtin_amdgcn_raw_buffer_load_b128(ra, o, 0, AUX);
+      const auto b = __builtin_amdgcn_raw_buffer_load_b128(rb, o, 0, AUX);
+      acc ^= k[0] ^ k[3] ^ s[1] ^ s[2] ^ e[0] ^ e[3] ^ a[1] ^ a[2] ^ b[0] ^ b[3];
+    }
+    const auto m = __builtin_amdgcn_raw_buffer_load_b128(rm, (int)(i * 4), 0, AUX);
+    acc ^= m[0] ^ m[1] ^ m[2] ^ m[3];
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
+
 // grid-stride (interleaved) tiles
 template <int S, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void read_stride(Cols c, unsigned long long n,
@@ -111,6 +144,10 @@ int main(int argc, char **argv) {
   auto report = [&](const char *name, float us) {
     std::printf("{\"probe\": \"%s\", \"us\": %.2f, \"GBps\": %.1f}\n", name, us, bytes / (us * 1e-6) / 1e9);
   };
+  report("buf aux0 b1024 x1/CU", time_it([&] { read_buf<0><<<cus, 1024>>>(c, n, out); }, reps));
+  report("buf nt b1024 x1/CU", time_it([&] { read_buf<2><<<cus, 1024>>>(c, n, out); }, reps));
+  report("buf sc0 b1024 x1/CU", time_it([&] { read_buf<1><<<cus, 1024>>>(c, n, out); }, reps));
+  report("buf aux0 b1024 x1/CU", time_it([&] { read_buf<0><<<cus, 1024>>>(c, n, out); }, reps));
   for (int per_cu : {1, 2, 4}) {
     const int g = cus * per_cu;
     char nm[96];

@@ -19,7 +19,8 @@ wl = generate_c2(n, seed=42)
 cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).cuda()
         for c in wl.batch.columns()]
 s = torch.cuda.Stream()
-with Engine(Config(n_services=wl.n_services, n_windows=16)) as e:
+flags = int(os.environ.get("PROF_FLAGS", 0))
+with Engine(Config(n_services=wl.n_services, n_windows=16, flags=flags)) as e:
     e.window_advance(wl.first_window)
     for _ in range(reps):
         e.ingest_device(*cols, n=n, stream=s.cuda_stream)

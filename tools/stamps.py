@@ -22,14 +22,23 @@ def timeline(e):
     e.lib.sa_debug_stamps(e._h, None, 0, C.byref(n))
     buf = np.zeros(n.value, np.uint64)
     e.lib.sa_debug_stamps(e._h, buf.ctypes.data_as(_lib.u64p), n.value, C.byref(n))
-    t = buf.reshape(-1, 8)[:, :4].astype(np.int64)
-    t = t[t[:, 0] > 0]
+    full = buf.reshape(-1, 136).astype(np.int64)
+    t = full[:, :4]
+    keep = t[:, 0] > 0
+    t = t[keep]
+    w = full[keep, 8:].reshape(-1, 16, 8)
+    segs = w[:, :, :6].sum(axis=(0, 1)).astype(float)
+    wend = w[:, :, 6] - t[:, :1]  # per-wave loop end relative to the WG start
     us = lambda x: x / 100.0  # 100 MHz
     t0 = t[:, 0].min()
     q = lambda a: {"min": float(us(a.min())), "med": float(us(np.median(a))), "max": float(us(a.max()))}
     return {"wgs": int(len(t)), "start_skew": q(t[:, 0] - t0), "init": q(t[:, 1] - t[:, 0]),
             "loop": q(t[:, 2] - t[:, 1]), "flush": q(t[:, 3] - t[:, 2]),
-            "end": q(t[:, 3] - t0)}
+            "end": q(t[:, 3] - t0),
+            "seg_share": [round(x / max(segs.sum(), 1), 3) for x in segs],
+            "wave_loop_end": q(wend.reshape(-1)),
+            "wave_skew_in_wg": q(wend.max(axis=1) - wend.min(axis=1)),
+            "loop_end_by_wave_med": [round(us(float(np.median(wend[:, i]))), 1) for i in range(16)]}
 
 
 def main():
@@ -41,7 +50,7 @@ def main():
     s = torch.cuda.Stream(dev)
     out = {}
     for name, fl in (("full", 0), ("loads_only", 15), ("no_sketch", 6)):
-        for v in (0, 1, 2, 3):
+        for v in [int(x) for x in os.environ.get("STAMP_VARS", "0,8").split(",")]:
             os.environ["SPANAGG_VARIANT"] = str(v)
             with Engine(Config(n_services=wl.n_services, n_windows=16, flags=fl)) as e:
                 e.window_advance(wl.first_window)
