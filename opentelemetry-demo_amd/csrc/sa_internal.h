@@ -54,6 +54,9 @@ struct IngestParams {
   uint8_t *hll;                 // [W][S][2^p]
   unsigned long long *cms;      // [W][d][w]
   unsigned long long *errcnt;   // [W][cap] exact ERROR-span counts per (window, key slot)
+  // v2 kernels: per-workgroup ERROR counts [G][W << log2cap] u32, gathered in an
+  // LDS table during the launch and added here at its end (nullptr: errcnt atomics)
+  uint32_t *errslab;
   uint64_t window_ns, win_magic, win_base;
   uint64_t base_ns, ring_ns;  // win_base * window_ns, n_windows * window_ns (< 2^63)
   float inv_window;           // 1 / window_ns
@@ -105,13 +108,16 @@ constexpr Variant kVariants[kNumVariants] = {{4, false, 1024}, {2, true, 1024}, 
                                              {2, false, 1024}};
 constexpr uint32_t kHbmBlock = 256;
 // small-table kernels: 0-3 ingest_lds_kernel {4,PF} {4,-} {2,PF} {2,-}, 4-7 the
-// same with nt loads; 8-11 ingest_v2_kernel (S,NBUF,AUX) {2,2,0} {2,3,0} {4,1,0} {2,2,nt}
-constexpr int kNumLdsVariants = 19;
-constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2};
+// same with nt loads; 8-13 ingest_v2_kernel: 8 generic (nt tile loads), 9 three
+// tiles in flight, 10 four spans per lane, 11 generic (default cache policy),
+// 12 / 13 = 8 / 11 specialised for cap 2048, 17 buckets, HLL p 14.
+constexpr int kNumLdsVariants = 14;
+constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2};
 constexpr uint32_t kDbgPerWg = 136;  // diagnostic stamps per workgroup: 8 + 16 waves x 8
 constexpr uint32_t kHllQueue = 2048;  // deferred HLL raises per workgroup (8 B each)
+constexpr uint32_t kErrTab = 1024;    // LDS (window, slot) -> ERROR count table per workgroup (4 B each)
 // ingest_lds_kernel LDS beyond the table: HLL queue + its count + bin table
-constexpr size_t kLdsExtraBytes = kHllQueue * 8 + 16 + kBins * sizeof(BinEntry);
+constexpr size_t kLdsExtraBytes = kHllQueue * 8 + 16 + kBins * sizeof(BinEntry) + kErrTab * 4;
 
 // launchers (spanagg_kernels.hip)
 hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,
@@ -131,6 +137,8 @@ hipError_t launch_gather_dense(const unsigned long long *gkeys, const unsigned l
 hipError_t launch_fold_errcnt(const unsigned long long *gkeys, unsigned long long *errcnt,
                               uint64_t cap, unsigned long long *cms, uint32_t d, uint32_t w,
                               uint32_t shift, const uint64_t *seeds, hipStream_t s);
+hipError_t launch_reduce_errslab(uint32_t *errslab, uint32_t G, uint64_t per_wg, uint64_t ws,
+                                 uint32_t log2cap, unsigned long long *errcnt_ws, hipStream_t s);
 hipError_t launch_count_keys(const unsigned long long *gkeys, uint64_t cap,
                              unsigned long long *out, hipStream_t s);
 

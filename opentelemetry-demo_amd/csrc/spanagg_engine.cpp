@@ -28,7 +28,7 @@ constexpr uint64_t kCmsSeed[8] = {0x9E3779B97F4A7C15ULL, 0xBF58476D1CE4E5B9ULL,
                                   0x8EBC6AF09C88C6E3ULL, 0x589965CC75374CC3ULL};
 constexpr size_t kLdsBudget = 144 * 1024;  // small-table path LDS ceiling per workgroup
 constexpr uint64_t kSlabLimit = 1ULL << 31;  // per-workgroup spans between slab reductions
-constexpr int kDefaultVariant = 0;            // sa::kVariants index (SPANAGG_VARIANT overrides)
+constexpr int kDefaultVariant = 12;  // small path: ingest_v2_kernel (SPANAGG_VARIANT overrides)
 
 bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 uint32_t log2u(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
@@ -62,6 +62,7 @@ struct sa_engine {
   sa::BinEntry *d_bins = nullptr;  // bucket bin table (nullptr: linear thresholds)
   unsigned long long *dbg = nullptr;  // SPANAGG_STAMPS diagnostic timestamps
   uint32_t *slab_cnt = nullptr;
+  uint32_t *errslab = nullptr;  // v2: [G][n_windows << log2cap] per-workgroup ERROR counts
   uint8_t *hll = nullptr;
   size_t hll_slot_bytes = 0, cms_slot_elems = 0;
   void *stage = nullptr;
@@ -261,7 +262,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   // lkeys + lsum + lcnt + deferred-HLL queue (+ its counter), see ingest_lds_kernel
   e->lds_bytes = (size_t)e->cap * 16 + (size_t)e->cap * nw * 4 + sa::kLdsExtraBytes;
   e->small = e->lds_bytes <= kLdsBudget;
-  e->variant = kDefaultVariant;
+  e->variant = e->small ? kDefaultVariant : 0;
   if (const char *v = std::getenv("SPANAGG_VARIANT"))  // tuning knob for A/B runs
     e->variant = std::max(0, std::min((e->small ? sa::kNumLdsVariants : sa::kNumVariants) - 1,
                                       std::atoi(v)));
@@ -314,6 +315,10 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     if ((rc = alloc((void **)&e->slab_cnt, (size_t)e->G * e->cap * srow * 4)) ||
         (rc = alloc((void **)&e->slab_sum, (size_t)e->G * e->cap * 8)))
       return bail(rc);
+    // (window, slot) keys of the v2 kernels' LDS ERROR table are 16-bit
+    if (e->variant >= 8 && (uint64_t)cfg->n_windows * e->cap < 65535 &&
+        (rc = alloc((void **)&e->errslab, (size_t)e->G * cfg->n_windows * e->cap * 4)))
+      return bail(rc);
   }
   if (hipDeviceSynchronize() != hipSuccess) return bail(fail(e, SA_EDEVICE, "device sync failed"));
   *out = e;
@@ -327,7 +332,7 @@ void sa_destroy(sa_engine *e) {
   for (void *p : {(void *)e->gkeys, (void *)e->gcounts, (void *)e->slab_sum, (void *)e->cms,
                   (void *)e->stats, (void *)e->out_keys, (void *)e->out_rows, (void *)e->scratch,
                   (void *)e->slab_cnt, (void *)e->hll, (void *)e->errcnt, (void *)e->d_seeds,
-                  (void *)e->dbg, (void *)e->d_bins,
+                  (void *)e->dbg, (void *)e->d_bins, (void *)e->errslab,
                   e->stage})
     if (p) (void)hipFree(p);
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
@@ -397,6 +402,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.hll = e->hll;
   P.cms = e->cms;
   P.errcnt = e->errcnt;
+  P.errslab = e->errslab;
   P.window_ns = e->cfg.window_ns;
   P.win_magic = UINT64_MAX / e->cfg.window_ns;
   P.win_base = e->win_base;
@@ -591,7 +597,15 @@ static bool resident(const sa_engine *e, uint64_t w) {
 
 // Derive the count-min cells of window slot ws from its exact per-slot error
 // counts (see sketch_post in spanagg_kernels.hip).
+static int fold_errslab(sa_engine *e, uint64_t ws, hipStream_t s) {
+  if (!e->errslab) return SA_OK;
+  SA_HIP(e, sa::launch_reduce_errslab(e->errslab, e->G, (uint64_t)e->cfg.n_windows * e->cap, ws,
+                                      e->log2cap, e->errcnt + ws * e->cap, s));
+  return SA_OK;
+}
+
 static int fold_window(sa_engine *e, uint64_t ws, hipStream_t s) {
+  if (int rc = fold_errslab(e, ws, s)) return rc;
   SA_HIP(e, sa::launch_fold_errcnt(e->gkeys, e->errcnt + ws * e->cap, e->cap,
                                    e->cms + ws * e->cms_slot_elems, e->cfg.cms_d, e->cfg.cms_w,
                                    64 - log2u(e->cfg.cms_w), e->d_seeds, s));
@@ -644,6 +658,7 @@ int sa_window_advance(sa_engine *e, uint64_t new_base) {
     const uint64_t ws = (e->win_base + k) & (e->cfg.n_windows - 1);
     SA_HIP(e, hipMemsetAsync(e->hll + ws * e->hll_slot_bytes, 0, e->hll_slot_bytes, e->stream));
     SA_HIP(e, hipMemsetAsync(e->cms + ws * e->cms_slot_elems, 0, e->cms_slot_elems * 8, e->stream));
+    if (int rc = fold_errslab(e, ws, e->stream)) return rc;  // clears the slab cells
     SA_HIP(e, hipMemsetAsync(e->errcnt + ws * e->cap, 0, e->cap * 8, e->stream));
   }
   e->win_base = new_base;

@@ -744,6 +744,28 @@ __device__ __forceinline__ void cold_hll_raise(uint32_t hoff, uint32_t rho) {
   hll_raise(cold_params().hll + hoff, rho);
 }
 
+// Adds one ERROR span of (window slot, key slot) key `ek` (< 65535) to the
+// workgroup's LDS table (open addressing, 4 probes); false when those are taken
+// by other keys (the caller then falls back to a global atomic).
+__device__ __forceinline__ bool lds_err_add(uint32_t *etab, uint32_t ek) {
+  const uint32_t tag = (ek + 1) << 16;
+  const uint32_t h = (ek * 0x9E3779B1u) >> (32 - 10);  // kErrTab = 1024
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t *c = etab + ((h + q) & (kErrTab - 1));
+    uint32_t v = *c;
+    if (v == 0) {
+      v = atomicCAS(c, 0u, tag | 1u);
+      if (v == 0) return true;
+    }
+    if ((v & 0xFFFF0000u) == tag) {
+      atomicAdd(c, 1u);
+      return true;
+    }
+  }
+  return false;
+}
+
 template <int S>
 struct Pending {  // one step's HLL reads, compared one step later
   uint32_t hoff[S], rho[S], hv[S];
@@ -785,6 +807,8 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   uint2 *hq = reinterpret_cast<uint2 *>(lcnt + cap * nw);
   uint32_t *hq_n = reinterpret_cast<uint32_t *>(hq + kHllQueue);
   BinEntry *lbins = reinterpret_cast<BinEntry *>(hq_n + 4);
+  uint32_t *etab = reinterpret_cast<uint32_t *>(lbins + kBins);  // [kErrTab]: (key+1) << 16 | count
+  const bool err_lds = P.errslab != nullptr;
 
   uint64_t lo, hi;
   wg_range_p(P, lo, hi);
@@ -834,6 +858,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   for (uint32_t i = threadIdx.x * 4; i < cap * nw; i += kLdsBlock * 4)
     *reinterpret_cast<uint4 *>(lcnt + i) = make_uint4(0, 0, 0, 0);
   if (threadIdx.x == 0) *hq_n = 0;
+  etab[threadIdx.x] = 0;  // kErrTab == kLdsBlock
   __syncthreads();
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 1] = __builtin_amdgcn_s_memrealtime();
 
@@ -977,10 +1002,13 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       if (err[j]) {
-        if (found[j] != kNotFound)
-          atomicAdd(P.errcnt + ((uint64_t)ws[j] << log2cap) + found[j], 1ULL);
-        else
+        if (found[j] == kNotFound) {
           cold_cms_add(ws[j], key[j]);
+        } else {
+          const uint32_t ek = (ws[j] << log2cap) | found[j];
+          if (!(err_lds && lds_err_add(etab, ek)))
+            atomicAdd(P.errcnt + ((uint64_t)ws[j] << log2cap) + found[j], 1ULL);
+        }
       }
     }
     // 7. RED update: LDS u16 bucket counter + u64 ns sum
@@ -1018,6 +1046,13 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 2] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
   flush_lds(P, cap, nw, lsum, lcnt);
+  if (err_lds) {  // this workgroup's ERROR counts -> its private slab (plain RMW)
+    const uint32_t e = etab[threadIdx.x];
+    if (e) {
+      uint32_t *cell = P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1);
+      *cell += e & 0xFFFFu;
+    }
+  }
   const uint32_t nq = *hq_n < kHllQueue ? *hq_n : kHllQueue;
   for (uint32_t i = threadIdx.x; i < nq; i += kLdsBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 3] = __builtin_amdgcn_s_memrealtime();
@@ -1164,6 +1199,26 @@ __global__ void gather_dense_kernel(const unsigned long long *gkeys,
   }
 }
 
+// errcnt[ws][slot] += sum over workgroups of errslab[g][ws << log2cap | slot];
+// the slab cells are cleared.
+__global__ void reduce_errslab_kernel(uint32_t *errslab, uint32_t G, uint64_t per_wg, uint64_t ws,
+                                      uint32_t log2cap, unsigned long long *errcnt_ws) {
+  const uint64_t cap = 1ULL << log2cap;
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    unsigned long long acc = 0;
+    for (uint32_t g = 0; g < G; ++g) {
+      uint32_t *p = errslab + g * per_wg + (ws << log2cap) + s;
+      const uint32_t v = *p;
+      if (v) {
+        acc += v;
+        *p = 0;
+      }
+    }
+    if (acc) errcnt_ws[s] += acc;
+  }
+}
+
 __global__ void count_keys_kernel(const unsigned long long *gkeys, uint64_t cap,
                                   unsigned long long *out) {
   uint32_t c = 0;
@@ -1203,19 +1258,14 @@ uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap_blocks) {
 // variants, the linear-threshold fallback, and the diagnostic build.
 static const void *small_fn(bool bt, int v, bool diag) {
   if (bt && v >= 8) {  // v2 kernels (bin-table bucketing only)
-    if (diag) return (const void *)&ingest_v2_kernel<2, 2, 0, true>;
+    if (diag) return (const void *)&ingest_v2_kernel<2, 2, 2, true>;
     switch (v) {
       case 9: return (const void *)&ingest_v2_kernel<2, 3, 0, false>;
       case 10: return (const void *)&ingest_v2_kernel<4, 1, 0, false>;
-      case 11: return (const void *)&ingest_v2_kernel<2, 2, 2, false>;
-      case 12: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14>;
-      case 13: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14, 1>;
-      case 14: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14, 2>;
-      case 15: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14, 16>;
-      case 16: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14, 3>;
-      case 17: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, 2>;
-      case 18: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, 0>;
-      default: return (const void *)&ingest_v2_kernel<2, 2, 0, false>;
+      case 11: return (const void *)&ingest_v2_kernel<2, 2, 0, false>;
+      case 12: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14>;
+      case 13: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14>;
+      default: return (const void *)&ingest_v2_kernel<2, 2, 2, false>;
     }
   }
   if (diag) return bt ? (const void *)&ingest_lds_kernel<1, 4, true, true>
@@ -1259,7 +1309,8 @@ hipError_t prepare_ingest_small(size_t lds_bytes) {
 hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,
                                hipStream_t s, int variant) {
   // the specialised v2 build is only valid for its compile-time geometry
-  if (variant >= 12 && !(P.log2cap == 11 && (P.nbk + 1) / 2 == 9 && P.p == 14)) variant = 8;
+  if ((variant == 12 || variant == 13) && !(P.log2cap == 11 && (P.nbk + 1) / 2 == 9 && P.p == 14))
+    variant = variant == 12 ? 8 : 11;
   const void *fn = small_fn(P.bintab != nullptr, variant, P.diag != 0 || P.dbg != nullptr);
   void *args[] = {const_cast<IngestParams *>(&P)};
   return hipLaunchKernel(fn, dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);
@@ -1307,6 +1358,14 @@ hipError_t launch_fold_errcnt(const unsigned long long *gkeys, unsigned long lon
   const uint32_t block = 256;
   hipLaunchKernelGGL(fold_errcnt_kernel, dim3(grid_for(cap, block, 2048)), dim3(block), 0, s, gkeys,
                      errcnt, cap, cms, d, w, shift, seeds);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce_errslab(uint32_t *errslab, uint32_t G, uint64_t per_wg, uint64_t ws,
+                                 uint32_t log2cap, unsigned long long *errcnt_ws, hipStream_t s) {
+  const uint32_t block = 256;
+  hipLaunchKernelGGL(reduce_errslab_kernel, dim3(grid_for(1ULL << log2cap, block, 1024)), dim3(block), 0,
+                     s, errslab, G, per_wg, ws, log2cap, errcnt_ws);
   return hipGetLastError();
 }
 

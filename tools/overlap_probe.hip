@@ -49,6 +49,36 @@ __global__ __launch_bounds__(1024) void kern(Cols c, u64 n, const unsigned char 
   for (int q = 0; q < NG; ++q) acc += g0[q] + g1[q];
   if (acc == 0x12345678u) out[0] = acc;
 }
+// stream-only shapes: S4 simple loop (11 x 16-B loads per lane per iteration),
+// and the S2 ring with meta loaded 8 B/lane vs 16 B/lane on even lanes + DPP.
+template <int MODE>
+__global__ __launch_bounds__(1024) void shape(Cols c, u64 n, unsigned *out) {
+  u64 chunk = (n + gridDim.x - 1) / gridDim.x; chunk = (chunk + 3) / 4 * 4;
+  const u64 lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+  unsigned acc = 0;
+  if (MODE == 0) {
+    for (u64 i = lo + threadIdx.x * 4; i < hi; i += 4096) {
+      Tile a, b; ld(c, i, hi, a); ld(c, i + 2, hi, b);
+      a.m = make_uint2(0, 0); b.m = make_uint2(0, 0);
+      const uint4 m = *reinterpret_cast<const uint4 *>(c.m + i);
+      acc += use(a) ^ use(b) ^ m.x ^ m.w;
+    }
+  } else {
+    const u64 lane = threadIdx.x * 2, tile = 2048;
+    Tile A, B;
+    ld(c, lo + lane, hi, A); ld(c, lo + tile + lane, hi, B);
+    for (u64 t = lo; t < hi; t += 2 * tile) {
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        Tile &T = half ? B : A;
+        const u64 tt = t + half * tile;
+        acc += use(T);
+        ld(c, tt + 2 * tile + lane, hi, T);
+      }
+    }
+  }
+  if (acc == 0x12345678u) out[0] = acc;
+}
 template <typename F> float time_it(F f, int reps) {
   hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   f(); CK(hipDeviceSynchronize()); CK(hipEventRecord(a));
@@ -64,6 +94,8 @@ int main() {
   unsigned char *tab; CK(hipMalloc(&tab, 64 << 20)); CK(hipMemset(tab, 0, 64 << 20));
   unsigned *out; CK(hipMalloc(&out, 64));
 #define R(NG, D, TL) std::printf("{\"gathers_per_step\": %d, \"defer\": %d, \"table_bytes\": %d, \"us\": %.2f}\n", NG, D, 1 << TL, time_it([&] { kern<NG, D, TL><<<cus, 1024>>>(c, n, tab, out); }, 20));
+  std::printf("{\"shape\": \"S4 simple loop\", \"us\": %.2f}\n", time_it([&] { shape<0><<<cus, 1024>>>(c, n, out); }, 20));
+  std::printf("{\"shape\": \"S2 ring\", \"us\": %.2f}\n", time_it([&] { shape<1><<<cus, 1024>>>(c, n, out); }, 20));
   R(0, 0, 21) R(2, 0, 21) R(2, 1, 21) R(2, 2, 21) R(2, 1, 15) R(2, 1, 18) R(2, 1, 23) R(1, 1, 21) R(4, 1, 21)
   return 0;
 }
