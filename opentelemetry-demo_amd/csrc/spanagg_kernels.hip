@@ -1125,39 +1125,38 @@ __global__ __launch_bounds__(BLOCK) void ingest_hbm_kernel(IngestParams P) {
 
 // ---------------------------------------------------------------------------
 // Flush-time kernels.
-__global__ void reduce_slabs_kernel(uint32_t *slab_cnt, unsigned long long *slab_sum,
+// slabs -> counters.  blockIdx.y takes a group of kSlabGroup workgroup slabs;
+// each thread sums one 4-cell quad of them and adds the partial into the u64
+// counters (coalesced no-return atomics, G / kSlabGroup per cell).  The slabs
+// are cleared by a memset afterwards.
+constexpr uint32_t kSlabGroup = 16;
+__global__ void reduce_slabs_kernel(const uint32_t *slab_cnt, const unsigned long long *slab_sum,
                                     unsigned long long *gcounts, uint32_t G, uint64_t cap,
                                     uint32_t nbk) {
   const uint32_t srow = (nbk + 1) & ~1u;  // 2 * ceil(nbk / 2)
-  const uint64_t cells = cap * srow;
+  const uint64_t cells = cap * srow, quads = cells / 4;
   const uint32_t stride = nbk + 1;
-  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < cells + cap;
-       c += (uint64_t)gridDim.x * blockDim.x) {
-    if (c < cells) {
-      unsigned long long acc = 0;
-      for (uint32_t g = 0; g < G; ++g) {
-        uint32_t *p = slab_cnt + (uint64_t)g * cells + c;
-        const uint32_t v = *p;
-        if (v) {
-          acc += v;
-          *p = 0;
-        }
-      }
-      const uint64_t slot = c / srow, b = c - slot * srow;
-      if (acc && b < nbk) gcounts[slot * stride + b] += acc;
-    } else {
-      const uint64_t slot = c - cells;
-      unsigned long long acc = 0;
-      for (uint32_t g = 0; g < G; ++g) {
-        unsigned long long *p = slab_sum + (uint64_t)g * cap + slot;
-        const unsigned long long v = *p;
-        if (v) {
-          acc += v;
-          *p = 0;
-        }
-      }
-      if (acc) gcounts[slot * stride + nbk] += acc;
+  const uint32_t g0 = blockIdx.y * kSlabGroup, g1 = min(G, g0 + kSlabGroup);
+  const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (q < quads) {
+    unsigned long long acc[4] = {0, 0, 0, 0};
+    for (uint32_t g = g0; g < g1; ++g) {
+      const uint4 v = reinterpret_cast<const uint4 *>(slab_cnt + (uint64_t)g * cells)[q];
+      acc[0] += v.x;
+      acc[1] += v.y;
+      acc[2] += v.z;
+      acc[3] += v.w;
     }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint64_t c = q * 4 + i, slot = c / srow, b = c - slot * srow;
+      if (acc[i] && b < nbk) atomicAdd(gcounts + slot * stride + b, acc[i]);
+    }
+  } else if (q < quads + cap) {
+    const uint64_t slot = q - quads;
+    unsigned long long acc = 0;
+    for (uint32_t g = g0; g < g1; ++g) acc += slab_sum[(uint64_t)g * cap + slot];
+    if (acc) atomicAdd(gcounts + slot * stride + nbk, acc);
   }
 }
 
@@ -1199,24 +1198,18 @@ __global__ void gather_dense_kernel(const unsigned long long *gkeys,
   }
 }
 
-// errcnt[ws][slot] += sum over workgroups of errslab[g][ws << log2cap | slot];
-// the slab cells are cleared.
-__global__ void reduce_errslab_kernel(uint32_t *errslab, uint32_t G, uint64_t per_wg, uint64_t ws,
-                                      uint32_t log2cap, unsigned long long *errcnt_ws) {
+// errcnt[ws][slot] += sum over workgroups of errslab[g][ws << log2cap | slot]
+// (blockIdx.y = a group of kSlabGroup workgroups; no-return u64 atomics).
+__global__ void reduce_errslab_kernel(const uint32_t *errslab, uint32_t G, uint64_t per_wg,
+                                      uint64_t ws, uint32_t log2cap,
+                                      unsigned long long *errcnt_ws) {
   const uint64_t cap = 1ULL << log2cap;
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    unsigned long long acc = 0;
-    for (uint32_t g = 0; g < G; ++g) {
-      uint32_t *p = errslab + g * per_wg + (ws << log2cap) + s;
-      const uint32_t v = *p;
-      if (v) {
-        acc += v;
-        *p = 0;
-      }
-    }
-    if (acc) errcnt_ws[s] += acc;
-  }
+  const uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (s >= cap) return;
+  const uint32_t g0 = blockIdx.y * kSlabGroup, g1 = min(G, g0 + kSlabGroup);
+  unsigned long long acc = 0;
+  for (uint32_t g = g0; g < g1; ++g) acc += errslab[g * per_wg + (ws << log2cap) + s];
+  if (acc) atomicAdd(errcnt_ws + s, acc);
 }
 
 __global__ void count_keys_kernel(const unsigned long long *gkeys, uint64_t cap,
@@ -1327,9 +1320,14 @@ hipError_t launch_reduce_slabs(uint32_t *slab_cnt, unsigned long long *slab_sum,
                                unsigned long long *gcounts, uint32_t G, uint64_t cap,
                                uint32_t nbk, hipStream_t s) {
   const uint32_t block = 256;
-  hipLaunchKernelGGL(reduce_slabs_kernel, dim3(grid_for(cap * (nbk + 1), block, 4096)),
-                     dim3(block), 0, s, slab_cnt, slab_sum, gcounts, G, cap, nbk);
-  return hipGetLastError();
+  const uint64_t srow = (nbk + 1) & ~1u, work = cap * srow / 4 + cap;
+  const dim3 grid((uint32_t)((work + block - 1) / block), (G + kSlabGroup - 1) / kSlabGroup);
+  hipLaunchKernelGGL(reduce_slabs_kernel, grid, dim3(block), 0, s, slab_cnt, slab_sum, gcounts, G,
+                     cap, nbk);
+  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  if (hipError_t e = hipMemsetAsync(slab_cnt, 0, (size_t)G * cap * srow * 4, s); e != hipSuccess)
+    return e;
+  return hipMemsetAsync(slab_sum, 0, (size_t)G * cap * 8, s);
 }
 
 hipError_t launch_compact(const unsigned long long *gkeys, unsigned long long *gcounts,
@@ -1364,9 +1362,13 @@ hipError_t launch_fold_errcnt(const unsigned long long *gkeys, unsigned long lon
 hipError_t launch_reduce_errslab(uint32_t *errslab, uint32_t G, uint64_t per_wg, uint64_t ws,
                                  uint32_t log2cap, unsigned long long *errcnt_ws, hipStream_t s) {
   const uint32_t block = 256;
-  hipLaunchKernelGGL(reduce_errslab_kernel, dim3(grid_for(1ULL << log2cap, block, 1024)), dim3(block), 0,
-                     s, errslab, G, per_wg, ws, log2cap, errcnt_ws);
-  return hipGetLastError();
+  const uint64_t cap = 1ULL << log2cap;
+  const dim3 grid((uint32_t)((cap + block - 1) / block), (G + kSlabGroup - 1) / kSlabGroup);
+  hipLaunchKernelGGL(reduce_errslab_kernel, grid, dim3(block), 0, s, errslab, G, per_wg, ws, log2cap,
+                     errcnt_ws);
+  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  // clear window ws's cells of every workgroup slab (a strided 2-D memset)
+  return hipMemset2DAsync(errslab + (ws << log2cap), per_wg * 4, 0, cap * 4, G, s);
 }
 
 hipError_t launch_count_keys(const unsigned long long *gkeys, uint64_t cap,
