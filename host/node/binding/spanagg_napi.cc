@@ -1,0 +1,533 @@
+// spanagg_napi.cc -- Node N-API addon over libspanagg's C-ABI (include/spanagg.h).
+//
+// This is the "TypeScript (Node N-API addon) calling a thin C-ABI HIP library"
+// host of BASELINE.json's north_star: every export is a one-to-one wrapper of an
+// sa_* entry point, with typed arrays as the column carriers (BigUint64Array for
+// u64 columns, Uint32Array for meta) so a batch crosses into C++ without copies.
+// The connector logic (key building, OTLP, temporality) lives in JS
+// (lib/connector.js); nothing here aggregates.
+//
+// Error behaviour mirrors the ABI: a non-zero sa_status becomes a thrown JS
+// Error with .code = the status and the engine's sa_last_error() text, except
+// flush(), which returns SA_EFULL in .status (the result is still valid), as
+// sa_flush does.
+#include <node_api.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "spanagg.h"
+
+namespace {
+
+napi_value throw_napi(napi_env env, const char *what) {
+    const napi_extended_error_info *info = nullptr;
+    napi_get_last_error_info(env, &info);
+    bool pending = false;
+    napi_is_exception_pending(env, &pending);
+    if (!pending) {
+        std::string msg = std::string("spanagg addon: ") + what;
+        if (info && info->error_message) msg += std::string(": ") + info->error_message;
+        napi_throw_error(env, nullptr, msg.c_str());
+    }
+    return nullptr;
+}
+
+napi_value throw_status(napi_env env, int rc, const std::string &msg) {
+    napi_value m, err, code;
+    napi_create_string_utf8(env, msg.c_str(), msg.size(), &m);
+    napi_create_error(env, nullptr, m, &err);
+    napi_create_int32(env, rc, &code);
+    napi_set_named_property(env, err, "code", code);
+    napi_throw(env, err);
+    return nullptr;
+}
+
+napi_value throw_type(napi_env env, const std::string &msg) {
+    napi_throw_type_error(env, nullptr, msg.c_str());
+    return nullptr;
+}
+
+// Engine handle: a JS object wrapping the sa_engine*, destroyed by destroy()
+// or, failing that, by the GC finalizer.
+struct Handle {
+    sa_engine *e = nullptr;
+};
+
+void finalize_handle(napi_env, void *data, void *) {
+    auto *h = static_cast<Handle *>(data);
+    if (h->e) sa_destroy(h->e);
+    delete h;
+}
+
+bool get_args(napi_env env, napi_callback_info info, size_t want, napi_value *argv) {
+    size_t argc = want;
+    if (napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr) != napi_ok) return false;
+    for (size_t i = argc; i < want; ++i) napi_get_undefined(env, &argv[i]);
+    return true;
+}
+
+Handle *get_handle(napi_env env, napi_value v) {
+    void *p = nullptr;
+    if (napi_unwrap(env, v, &p) != napi_ok || !p) {
+        throw_type(env, "expected a spanagg engine handle");
+        return nullptr;
+    }
+    auto *h = static_cast<Handle *>(p);
+    if (!h->e) {
+        throw_status(env, SA_ESTATE, "engine already destroyed");
+        return nullptr;
+    }
+    return h;
+}
+
+napi_value engine_error(napi_env env, Handle *h, int rc, const char *what) {
+    std::string msg = std::string(what) + ": " + (h && h->e ? sa_last_error(h->e) : "");
+    return throw_status(env, rc, msg);
+}
+
+// ---- value helpers -------------------------------------------------------
+
+bool is_undefined(napi_env env, napi_value v) {
+    napi_valuetype t;
+    return napi_typeof(env, v, &t) != napi_ok || t == napi_undefined || t == napi_null;
+}
+
+// Number or BigInt -> u64 (throws on other types, negatives and lossy values)
+bool to_u64(napi_env env, napi_value v, uint64_t *out, const char *name) {
+    napi_valuetype t;
+    napi_typeof(env, v, &t);
+    if (t == napi_bigint) {
+        bool lossless = false;
+        napi_get_value_bigint_uint64(env, v, out, &lossless);
+        if (!lossless) {
+            throw_type(env, std::string(name) + ": BigInt out of u64 range");
+            return false;
+        }
+        return true;
+    }
+    if (t == napi_number) {
+        double d;
+        napi_get_value_double(env, v, &d);
+        if (!(d >= 0) || d > 9007199254740991.0 ||
+            d != static_cast<double>(static_cast<uint64_t>(d))) {
+            throw_type(env, std::string(name) + ": expected a non-negative integer");
+            return false;
+        }
+        *out = static_cast<uint64_t>(d);
+        return true;
+    }
+    throw_type(env, std::string(name) + ": expected a number or BigInt");
+    return false;
+}
+
+bool to_u32(napi_env env, napi_value v, uint32_t *out, const char *name) {
+    uint64_t x;
+    if (!to_u64(env, v, &x, name)) return false;
+    if (x > 0xFFFFFFFFull) {
+        throw_type(env, std::string(name) + ": out of u32 range");
+        return false;
+    }
+    *out = static_cast<uint32_t>(x);
+    return true;
+}
+
+napi_value num(napi_env env, double d) {
+    napi_value v;
+    napi_create_double(env, d, &v);
+    return v;
+}
+
+napi_value big(napi_env env, uint64_t x) {
+    napi_value v;
+    napi_create_bigint_uint64(env, x, &v);
+    return v;
+}
+
+void set(napi_env env, napi_value obj, const char *k, napi_value v) {
+    napi_set_named_property(env, obj, k, v);
+}
+
+// Typed-array view of one element type; *len = element count.
+bool typed(napi_env env, napi_value v, napi_typedarray_type want, void **data, size_t *len,
+           const char *name) {
+    static const char *names[] = {"Int8Array",    "Uint8Array",    "Uint8ClampedArray",
+                                  "Int16Array",   "Uint16Array",   "Int32Array",
+                                  "Uint32Array",  "Float32Array",  "Float64Array",
+                                  "BigInt64Array", "BigUint64Array"};
+    bool is = false;
+    napi_is_typedarray(env, v, &is);
+    napi_typedarray_type t;
+    napi_value ab;
+    size_t off;
+    if (!is || napi_get_typedarray_info(env, v, &t, len, data, &ab, &off) != napi_ok || t != want) {
+        throw_type(env, std::string(name) + ": expected a " + names[want]);
+        return false;
+    }
+    return true;
+}
+
+// Fresh typed array holding a copy of n elements of src.
+napi_value make_typed(napi_env env, napi_typedarray_type t, size_t elem, const void *src, size_t n) {
+    void *dst = nullptr;
+    napi_value ab, arr;
+    if (napi_create_arraybuffer(env, n * elem, &dst, &ab) != napi_ok) return nullptr;
+    if (n) std::memcpy(dst, src, n * elem);
+    if (napi_create_typedarray(env, t, n, ab, 0, &arr) != napi_ok) return nullptr;
+    return arr;
+}
+
+napi_value prop(napi_env env, napi_value obj, const char *k) {
+    napi_value v = nullptr;
+    bool has = false;
+    if (is_undefined(env, obj) || napi_has_named_property(env, obj, k, &has) != napi_ok || !has) {
+        napi_get_undefined(env, &v);
+        return v;
+    }
+    napi_get_named_property(env, obj, k, &v);
+    return v;
+}
+
+bool read_bounds(napi_env env, napi_value v, std::vector<double> *out) {
+    bool is_arr = false;
+    napi_is_array(env, v, &is_arr);
+    if (is_arr) {
+        uint32_t n;
+        napi_get_array_length(env, v, &n);
+        out->resize(n);
+        for (uint32_t i = 0; i < n; ++i) {
+            napi_value x;
+            napi_get_element(env, v, i, &x);
+            if (napi_get_value_double(env, x, &(*out)[i]) != napi_ok) {
+                throw_type(env, "bounds: expected numbers");
+                return false;
+            }
+        }
+        return true;
+    }
+    void *d;
+    size_t n;
+    if (!typed(env, v, napi_float64_array, &d, &n, "bounds")) return false;
+    out->assign(static_cast<double *>(d), static_cast<double *>(d) + n);
+    return true;
+}
+
+bool read_unit(napi_env env, napi_value v, uint32_t *unit) {
+    if (is_undefined(env, v)) {
+        *unit = SA_UNIT_MS;
+        return true;
+    }
+    char buf[8] = {0};
+    size_t n = 0;
+    if (napi_get_value_string_utf8(env, v, buf, sizeof buf, &n) != napi_ok ||
+        (std::strcmp(buf, "ms") != 0 && std::strcmp(buf, "s") != 0)) {
+        throw_type(env, "unit: expected 'ms' or 's'");
+        return false;
+    }
+    *unit = buf[0] == 's' ? SA_UNIT_S : SA_UNIT_MS;
+    return true;
+}
+
+// ---- exports -------------------------------------------------------------
+
+napi_value AbiVersion(napi_env env, napi_callback_info) { return num(env, sa_abi_version()); }
+
+// createDefaultConfig, as a plain object (bounds in the histogram unit)
+napi_value ConfigDefault(napi_env env, napi_callback_info) {
+    sa_config c;
+    sa_config_default(&c);
+    napi_value o, bounds, unit;
+    if (napi_create_object(env, &o) != napi_ok ||
+        napi_create_array_with_length(env, c.n_bounds, &bounds) != napi_ok)
+        return throw_napi(env, "configDefault");
+    for (uint32_t i = 0; i < c.n_bounds; ++i) napi_set_element(env, bounds, i, num(env, c.bounds[i]));
+    set(env, o, "bounds", bounds);
+    napi_create_string_utf8(env, c.unit == SA_UNIT_S ? "s" : "ms", NAPI_AUTO_LENGTH, &unit);
+    set(env, o, "unit", unit);
+    set(env, o, "hllP", num(env, c.hll_p));
+    set(env, o, "cmsD", num(env, c.cms_d));
+    set(env, o, "cmsW", num(env, c.cms_w));
+    set(env, o, "windowNs", big(env, c.window_ns));
+    set(env, o, "nWindows", num(env, c.n_windows));
+    set(env, o, "nServices", num(env, c.n_services));
+    set(env, o, "keyCapacity", num(env, static_cast<double>(c.key_capacity)));
+    set(env, o, "device", num(env, c.device));
+    set(env, o, "flags", num(env, c.flags));
+    return o;
+}
+
+// bucketThresholds(bounds, unit) -> {thresholds: BigUint64Array, nNeg}
+napi_value BucketThresholds(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
+    std::vector<double> b;
+    uint32_t unit;
+    if (!read_bounds(env, argv[0], &b) || !read_unit(env, argv[1], &unit)) return nullptr;
+    std::vector<uint64_t> thr(b.size() + 1);
+    uint32_t nneg = 0;
+    int rc = sa_bucket_thresholds(b.data(), static_cast<uint32_t>(b.size()), unit, thr.data(), &nneg);
+    if (rc != SA_OK) return throw_status(env, rc, "invalid histogram bounds");
+    napi_value o;
+    if (napi_create_object(env, &o) != napi_ok) return throw_napi(env, "bucketThresholds");
+    set(env, o, "thresholds", make_typed(env, napi_biguint64_array, 8, thr.data(), b.size() - nneg));
+    set(env, o, "nNeg", num(env, nneg));
+    return o;
+}
+
+// hllEstimate(Uint8Array regs, p) -> number
+napi_value HllEstimate(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
+    void *d;
+    size_t n;
+    uint32_t p;
+    if (!typed(env, argv[0], napi_uint8_array, &d, &n, "regs") || !to_u32(env, argv[1], &p, "p"))
+        return nullptr;
+    if (p < 4 || p > 18 || n != (size_t(1) << p))
+        return throw_status(env, SA_EINVAL, "hllEstimate: regs.length must be 2^p, 4 <= p <= 18");
+    return num(env, sa_hll_estimate(static_cast<const uint8_t *>(d), p));
+}
+
+// create(config) -> handle.  Missing fields take createDefaultConfig values.
+napi_value Create(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
+    sa_config c;
+    sa_config_default(&c);
+    std::vector<double> bounds(c.bounds, c.bounds + c.n_bounds);
+    napi_value cfg = argv[0], v;
+    if (!is_undefined(env, v = prop(env, cfg, "bounds")) && !read_bounds(env, v, &bounds)) return nullptr;
+    if (!read_unit(env, prop(env, cfg, "unit"), &c.unit)) return nullptr;
+    struct U32Field {
+        const char *k;
+        uint32_t *dst;
+    } u32s[] = {{"hllP", &c.hll_p},         {"cmsD", &c.cms_d},
+                {"cmsW", &c.cms_w},         {"nWindows", &c.n_windows},
+                {"nServices", &c.n_services}, {"flags", &c.flags}};
+    for (auto &f : u32s)
+        if (!is_undefined(env, v = prop(env, cfg, f.k)) && !to_u32(env, v, f.dst, f.k)) return nullptr;
+    if (!is_undefined(env, v = prop(env, cfg, "windowNs")) && !to_u64(env, v, &c.window_ns, "windowNs"))
+        return nullptr;
+    if (!is_undefined(env, v = prop(env, cfg, "keyCapacity")) &&
+        !to_u64(env, v, &c.key_capacity, "keyCapacity"))
+        return nullptr;
+    if (!is_undefined(env, v = prop(env, cfg, "device"))) {
+        uint32_t dev = 0;
+        if (!to_u32(env, v, &dev, "device")) return nullptr;
+        c.device = static_cast<int32_t>(dev);
+    }
+    c.bounds = bounds.data();
+    c.n_bounds = static_cast<uint32_t>(bounds.size());
+    sa_engine *e = nullptr;
+    int rc = sa_create(&c, &e);
+    if (rc != SA_OK || !e)
+        return throw_status(env, rc ? rc : SA_EDEVICE,
+                            "sa_create failed (invalid config, or no gfx950 GPU visible)");
+    napi_value obj;
+    auto *h = new Handle{e};
+    if (napi_create_object(env, &obj) != napi_ok ||
+        napi_wrap(env, obj, h, finalize_handle, nullptr, nullptr) != napi_ok) {
+        sa_destroy(e);
+        delete h;
+        return throw_napi(env, "napi_wrap");
+    }
+    return obj;
+}
+
+napi_value Destroy(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
+    void *p = nullptr;
+    if (napi_unwrap(env, argv[0], &p) == napi_ok && p) {
+        auto *h = static_cast<Handle *>(p);
+        if (h->e) sa_destroy(h->e);
+        h->e = nullptr;
+    }
+    return nullptr;
+}
+
+napi_value LastError(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
+    Handle *h = get_handle(env, argv[0]);
+    if (!h) return nullptr;
+    napi_value s;
+    napi_create_string_utf8(env, sa_last_error(h->e), NAPI_AUTO_LENGTH, &s);
+    return s;
+}
+
+// ingest(h, {keyHash, startNs, endNs, traceW0, traceW1: BigUint64Array, meta: Uint32Array}):
+// ConsumeTraces' per-span body for one columnar batch in host memory (the
+// library stages it to HBM and launches the ingest kernel).
+napi_value Ingest(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
+    Handle *h = get_handle(env, argv[0]);
+    if (!h) return nullptr;
+    static const char *cols[] = {"keyHash", "startNs", "endNs", "traceW0", "traceW1"};
+    const uint64_t *p64[5];
+    size_t n = 0;
+    for (int i = 0; i < 5; ++i) {
+        void *d;
+        size_t len;
+        if (!typed(env, prop(env, argv[1], cols[i]), napi_biguint64_array, &d, &len, cols[i]))
+            return nullptr;
+        if (i == 0) n = len;
+        else if (len != n) return throw_status(env, SA_EINVAL, "ingest: ragged SoA batch");
+        p64[i] = static_cast<const uint64_t *>(d);
+    }
+    void *md;
+    size_t mlen;
+    if (!typed(env, prop(env, argv[1], "meta"), napi_uint32_array, &md, &mlen, "meta")) return nullptr;
+    if (mlen != n) return throw_status(env, SA_EINVAL, "ingest: ragged SoA batch");
+    sa_span_batch b{p64[0], p64[1], p64[2], p64[3], p64[4], static_cast<const uint32_t *>(md), n};
+    int rc = sa_ingest(h->e, &b);
+    if (rc != SA_OK) return engine_error(env, h, rc, "sa_ingest");
+    return nullptr;
+}
+
+napi_value Sync(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
+    Handle *h = get_handle(env, argv[0]);
+    if (!h) return nullptr;
+    int rc = sa_sync(h->e);
+    if (rc != SA_OK) return engine_error(env, h, rc, "sa_sync");
+    return nullptr;
+}
+
+// flush(h) -> {status, nSeries, nBuckets, keyHash, bucketCounts [n*nb], calls, sumNs, sum}
+napi_value Flush(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
+    Handle *h = get_handle(env, argv[0]);
+    if (!h) return nullptr;
+    sa_red_result *r = nullptr;
+    int rc = sa_flush(h->e, &r);
+    if ((rc != SA_OK && rc != SA_EFULL) || !r) {
+        if (r) sa_red_result_free(r);
+        return engine_error(env, h, rc ? rc : SA_ESTATE, "sa_flush");
+    }
+    const size_t n = r->n_series, nb = r->n_buckets;
+    napi_value o;
+    if (napi_create_object(env, &o) != napi_ok) {
+        sa_red_result_free(r);
+        return throw_napi(env, "napi_create_object");
+    }
+    set(env, o, "status", num(env, rc));
+    set(env, o, "nSeries", num(env, static_cast<double>(n)));
+    set(env, o, "nBuckets", num(env, static_cast<double>(nb)));
+    set(env, o, "keyHash", make_typed(env, napi_biguint64_array, 8, r->key_hash, n));
+    set(env, o, "bucketCounts", make_typed(env, napi_biguint64_array, 8, r->bucket_counts, n * nb));
+    set(env, o, "calls", make_typed(env, napi_biguint64_array, 8, r->calls, n));
+    set(env, o, "sumNs", make_typed(env, napi_biguint64_array, 8, r->sum_ns, n));
+    set(env, o, "sum", make_typed(env, napi_float64_array, 8, r->sum, n));
+    sa_red_result_free(r);
+    return o;
+}
+
+// windowRead(h, windowId) -> {windowId, nServices, hllP, hll, cmsD, cmsW, cms}
+napi_value WindowRead(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
+    Handle *h = get_handle(env, argv[0]);
+    uint64_t wid;
+    if (!h || !to_u64(env, argv[1], &wid, "windowId")) return nullptr;
+    sa_sketch_result *r = nullptr;
+    int rc = sa_window_read(h->e, wid, &r);
+    if (rc != SA_OK || !r) {
+        if (r) sa_sketch_result_free(r);
+        return engine_error(env, h, rc ? rc : SA_ESTATE, "sa_window_read");
+    }
+    napi_value o;
+    if (napi_create_object(env, &o) != napi_ok) {
+        sa_sketch_result_free(r);
+        return throw_napi(env, "napi_create_object");
+    }
+    set(env, o, "windowId", big(env, r->window_id));
+    set(env, o, "nServices", num(env, r->n_services));
+    set(env, o, "hllP", num(env, r->hll_p));
+    set(env, o, "hll",
+        make_typed(env, napi_uint8_array, 1, r->hll, size_t(r->n_services) << r->hll_p));
+    set(env, o, "cmsD", num(env, r->cms_d));
+    set(env, o, "cmsW", num(env, r->cms_w));
+    set(env, o, "cms", make_typed(env, napi_uint32_array, 4, r->cms, size_t(r->cms_d) * r->cms_w));
+    sa_sketch_result_free(r);
+    return o;
+}
+
+napi_value WindowAdvance(napi_env env, napi_callback_info info) {
+    napi_value argv[2];
+    if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
+    Handle *h = get_handle(env, argv[0]);
+    uint64_t base;
+    if (!h || !to_u64(env, argv[1], &base, "newBase")) return nullptr;
+    int rc = sa_window_advance(h->e, base);
+    if (rc != SA_OK) return engine_error(env, h, rc, "sa_window_advance");
+    return nullptr;
+}
+
+napi_value Stats(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
+    Handle *h = get_handle(env, argv[0]);
+    if (!h) return nullptr;
+    sa_stats s;
+    int rc = sa_get_stats(h->e, &s);
+    if (rc != SA_OK) return engine_error(env, h, rc, "sa_get_stats");
+    napi_value o, b;
+    if (napi_create_object(env, &o) != napi_ok) return throw_napi(env, "napi_create_object");
+    set(env, o, "spans", big(env, s.spans));
+    set(env, o, "zeroKey", big(env, s.zero_key));
+    set(env, o, "invalidService", big(env, s.invalid_service));
+    set(env, o, "windowOutOfRange", big(env, s.window_out_of_range));
+    set(env, o, "droppedTableFull", big(env, s.dropped_table_full));
+    set(env, o, "nKeys", big(env, s.n_keys));
+    set(env, o, "tableCapacity", big(env, s.table_capacity));
+    set(env, o, "windowBase", big(env, s.window_base));
+    napi_get_boolean(env, s.small_table != 0, &b);
+    set(env, o, "smallTable", b);
+    return o;
+}
+
+napi_value Init(napi_env env, napi_value exports) {
+    struct Fn {
+        const char *name;
+        napi_callback cb;
+    } fns[] = {{"abiVersion", AbiVersion},
+               {"configDefault", ConfigDefault},
+               {"bucketThresholds", BucketThresholds},
+               {"hllEstimate", HllEstimate},
+               {"create", Create},
+               {"destroy", Destroy},
+               {"lastError", LastError},
+               {"ingest", Ingest},
+               {"sync", Sync},
+               {"flush", Flush},
+               {"windowRead", WindowRead},
+               {"windowAdvance", WindowAdvance},
+               {"stats", Stats}};
+    for (auto &f : fns) {
+        napi_value v;
+        if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &v) != napi_ok ||
+            napi_set_named_property(env, exports, f.name, v) != napi_ok)
+            return throw_napi(env, f.name);
+    }
+    napi_value st;
+    napi_create_object(env, &st);
+    struct Code {
+        const char *k;
+        int v;
+    } codes[] = {{"OK", SA_OK},         {"EINVAL", SA_EINVAL}, {"ENOMEM", SA_ENOMEM},
+                 {"EDEVICE", SA_EDEVICE}, {"EFULL", SA_EFULL},   {"ERANGE", SA_ERANGE},
+                 {"ESTATE", SA_ESTATE}};
+    for (auto &c : codes) set(env, st, c.k, num(env, c.v));
+    set(env, exports, "status", st);
+    return exports;
+}
+
+}  // namespace
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, Init)

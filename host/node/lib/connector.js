@@ -1,0 +1,455 @@
+'use strict';
+/**
+ * SpanMetricsConnector -- the Node host of the spanmetrics connector, with the
+ * per-span aggregation on the GPU through the N-API addon (SURVEY.md 8b).
+ *
+ * Mirrors the upstream component ([UPSTREAM] opentelemetry-collector-contrib
+ * connector/spanmetricsconnector v0.125.0, wired by
+ * /root/reference/src/otel-collector/otelcol-config.yml:115-127):
+ *
+ *   upstream (Go)                          here
+ *   -------------------------------------  ---------------------------------------
+ *   createDefaultConfig / Config           normalizeConfig (YAML field names)
+ *   createTracesToMetricsConnector + Start constructor + start()
+ *   ConsumeTraces -> aggregateMetrics      consumeTraces (keys on the host, the
+ *                                          numeric work in addon.ingest)
+ *   exportMetrics -> buildMetrics          exportMetrics (addon.flush delta ->
+ *     + resetState                         cumulative/delta OTLP metrics)
+ *   getOrCreateResourceMetrics + LRU       _resource (LRU with evicted side map)
+ *   Shutdown                               shutdown()
+ *   (new) HLL / count-min windows          windowSketch / sketch metrics
+ *
+ * The host owns the string world (keys, attributes, resources); the device sees
+ * only u64 series ids (keys.js seriesHash) in SoA v1 columns.  Spans are
+ * columnised into a reusable buffer and handed to the engine when it fills
+ * (`batch_size` spans) or at export -- the batching the demo's `batch`
+ * processor does upstream of the connector (otelcol-config.yml:100,121).
+ */
+const addonLoader = require('./addon');
+const keys = require('./keys');
+const otlp = require('./otlp');
+
+const M64 = (1n << 64n) - 1n;
+const CMS_SEED = [0x9E3779B97F4A7C15n, 0xBF58476D1CE4E5B9n, 0x94D049BB133111EBn,
+  0xD6E8FEB86659FD93n, 0xA0761D6478BD642Fn, 0xE7037ED1A0B428DBn, 0x8EBC6AF09C88C6E3n,
+  0x589965CC75374CC3n];
+
+/** splitmix64 finaliser (the count-min column hash, SURVEY.md a17). */
+function splitmix64(x) {
+  let z = (x + 0x9E3779B97F4A7C15n) & M64;
+  z = ((z ^ (z >> 30n)) * 0xBF58476D1CE4E5B9n) & M64;
+  z = ((z ^ (z >> 27n)) * 0x94D049BB133111EBn) & M64;
+  return z ^ (z >> 31n);
+}
+
+const DUR_UNITS = { ns: 1, us: 1e3, 'µs': 1e3, 'μs': 1e3, ms: 1e6, s: 1e9, m: 60e9, h: 3600e9 };
+
+/** Go time.ParseDuration subset ("2ms", "1.5s", "1m30s") -> nanoseconds (Number). */
+function parseDurationNs(s) {
+  if (typeof s === 'number') return s;
+  const str = String(s).trim();
+  if (str === '0') return 0;
+  const re = /(\d+(?:\.\d*)?|\.\d+)(ns|us|µs|μs|ms|s|m|h)/gy;
+  let total = 0, m, pos = 0, sign = 1, body = str;
+  if (body[0] === '-' || body[0] === '+') { sign = body[0] === '-' ? -1 : 1; body = body.slice(1); }
+  re.lastIndex = 0;
+  while (pos < body.length && (m = re.exec(body)) !== null) {
+    total += parseFloat(m[1]) * DUR_UNITS[m[2]];
+    pos = re.lastIndex;
+  }
+  if (pos !== body.length || pos === 0) throw new Error(`invalid duration ${JSON.stringify(s)}`);
+  return sign * total;
+}
+
+const TEMPORALITY = {
+  AGGREGATION_TEMPORALITY_CUMULATIVE: otlp.AGGREGATION_TEMPORALITY.CUMULATIVE,
+  AGGREGATION_TEMPORALITY_DELTA: otlp.AGGREGATION_TEMPORALITY.DELTA,
+};
+
+/**
+ * Config with the spanmetrics YAML field names; defaults = createDefaultConfig
+ * (the reference declares `spanmetrics:` with an empty body, SURVEY.md a1).
+ * `sketches`, `key_capacity`, `device`, `batch_size` are this build's own.
+ * Histogram buckets: duration strings ("2ms") as in YAML, or numbers already
+ * in the histogram unit.
+ */
+function normalizeConfig(cfg = {}, addon) {
+  const d = addon.configDefault();
+  const hist = cfg.histogram || {};
+  const unit = hist.unit || 'ms';
+  if (unit !== 'ms' && unit !== 's') throw new Error(`histogram.unit must be ms or s, got ${unit}`);
+  if (hist.exponential) throw new Error('exponential histograms are not supported by this engine');
+  const div = unit === 's' ? 1e9 : 1e6;
+  let bounds = d.bounds.slice();
+  if (hist.explicit && Array.isArray(hist.explicit.buckets)) {
+    // durationsToUnits: float64(d.Nanoseconds()) / unitDivider
+    bounds = hist.explicit.buckets.map((b) => (typeof b === 'number' ? b : parseDurationNs(b) / div));
+  }
+  const temporality = cfg.aggregation_temporality || 'AGGREGATION_TEMPORALITY_CUMULATIVE';
+  if (!(temporality in TEMPORALITY)) throw new Error(`unknown aggregation_temporality ${temporality}`);
+  const dims = (cfg.dimensions || []).map((x) => ({ name: x.name,
+    default: x.default === undefined || x.default === null ? undefined : String(x.default) }));
+  const sk = cfg.sketches || {};
+  const windowNs = sk.window !== undefined ? BigInt(Math.round(parseDurationNs(sk.window))) : d.windowNs;
+  return {
+    unit, bounds, dims,
+    exclude: new Set(cfg.exclude_dimensions || []),
+    temporality: TEMPORALITY[temporality],
+    namespace: cfg.namespace === undefined ? 'traces.span.metrics' : cfg.namespace,
+    flushIntervalMs: cfg.metrics_flush_interval !== undefined
+      ? parseDurationNs(cfg.metrics_flush_interval) / 1e6 : 60000,
+    resourceCacheSize: cfg.resource_metrics_cache_size || 1000,
+    resourceKeyAttributes: cfg.resource_metrics_key_attributes || [],
+    hllP: sk.hll_p || d.hllP, cmsD: sk.cms_d || d.cmsD, cmsW: sk.cms_w || d.cmsW,
+    windowNs, nWindows: sk.n_windows || d.nWindows, nServices: sk.n_services || d.nServices,
+    emitSketches: !!sk.emit, topK: sk.top_k || 10,
+    keyCapacity: cfg.key_capacity || d.keyCapacity,
+    device: cfg.device || 0,
+    batchSize: cfg.batch_size || 1 << 16,
+  };
+}
+
+/** Reusable SoA v1 column buffer (44 B/span). */
+class Columns {
+  constructor(cap) {
+    this.cap = cap;
+    this.n = 0;
+    this.keyHash = new BigUint64Array(cap);
+    this.startNs = new BigUint64Array(cap);
+    this.endNs = new BigUint64Array(cap);
+    this.traceW0 = new BigUint64Array(cap);
+    this.traceW1 = new BigUint64Array(cap);
+    this.meta = new Uint32Array(cap);
+    this.w0u8 = new Uint8Array(this.traceW0.buffer);
+    this.w1u8 = new Uint8Array(this.traceW1.buffer);
+  }
+  view() {
+    const n = this.n;
+    return { keyHash: this.keyHash.subarray(0, n), startNs: this.startNs.subarray(0, n),
+      endNs: this.endNs.subarray(0, n), traceW0: this.traceW0.subarray(0, n),
+      traceW1: this.traceW1.subarray(0, n), meta: this.meta.subarray(0, n) };
+  }
+}
+
+class SpanMetricsConnector {
+  /**
+   * @param cfg spanmetrics YAML-shaped config (see normalizeConfig)
+   * @param opts {addon, clock: () => BigInt ns, metricsConsumer: (req) => void}
+   */
+  constructor(cfg = {}, opts = {}) {
+    this.addon = opts.addon || addonLoader.load();
+    this.cfg = normalizeConfig(cfg, this.addon);
+    this.clock = opts.clock || (() => BigInt(Date.now()) * 1000000n);
+    this.metricsConsumer = opts.metricsConsumer || null;
+    const c = this.cfg;
+    this.handle = this.addon.create({ bounds: c.bounds, unit: c.unit, hllP: c.hllP, cmsD: c.cmsD,
+      cmsW: c.cmsW, windowNs: c.windowNs, nWindows: c.nWindows, nServices: c.nServices,
+      keyCapacity: c.keyCapacity, device: c.device });
+    this.cols = new Columns(c.batchSize);
+    this.resources = new Map();   // resHash -> resource record (LRU order: oldest first)
+    this.evicted = new Map();     // evicted this flush interval, revivable until export
+    this.series = new Map();      // sid -> series record
+    this.services = new Map();    // service.name -> service id (first-seen order)
+    this.lastDeltaTs = new Map(); // sid -> last delta export timestamp
+    this.windowBase = null;
+    this.maxWindowSeen = -1n;
+    this.sketchWatermark = 0n;
+    this.closedWindows = [];
+    this.droppedFlushes = 0;
+    this.ticker = null;
+  }
+
+  capabilities() { return { mutatesData: false }; }
+
+  /** Start: the flush ticker (metrics_flush_interval) feeding metricsConsumer. */
+  start() {
+    if (this.ticker || !this.metricsConsumer) return;
+    this.ticker = setInterval(() => this.metricsConsumer(this.exportMetrics()), this.cfg.flushIntervalMs);
+    if (this.ticker.unref) this.ticker.unref();
+  }
+
+  shutdown() {
+    if (this.ticker) clearInterval(this.ticker);
+    this.ticker = null;
+    if (this.handle) this.addon.destroy(this.handle);
+    this.handle = null;
+  }
+
+  // ------------------------------------------------------------ ingest
+
+  _serviceId(name) {
+    let id = this.services.get(name);
+    if (id === undefined) {
+      id = Math.min(this.services.size, 0xFFFF);
+      this.services.set(name, id);
+    }
+    return id;
+  }
+
+  /** getOrCreateResourceMetrics: LRU(resource_metrics_cache_size) + evicted side map. */
+  _resource(resAttrs) {
+    const keyAttrs = this.cfg.resourceKeyAttributes;
+    let hashAttrs = resAttrs;
+    if (keyAttrs.length) {
+      hashAttrs = new Map();
+      for (const k of keyAttrs) if (resAttrs.has(k)) hashAttrs.set(k, resAttrs.get(k));
+    }
+    const h = keys.resourceHash(hashAttrs);
+    let r = this.resources.get(h);
+    if (r !== undefined) {
+      this.resources.delete(h);  // refresh LRU position
+      this.resources.set(h, r);
+      return r;
+    }
+    r = this.evicted.get(h);
+    if (r !== undefined) this.evicted.delete(h);
+    else r = { hash: h, attributes: resAttrs, startTs: this.clock(), byKey: new Map(), sids: [] };
+    this.resources.set(h, r);
+    if (this.resources.size > this.cfg.resourceCacheSize) {
+      const [oldest, rec] = this.resources.entries().next().value;
+      this.resources.delete(oldest);
+      this.evicted.set(oldest, rec);
+    }
+    return r;
+  }
+
+  _seriesId(res, service, span, resAttrs) {
+    const c = this.cfg;
+    const spanAttrs = c.dims.length ? keys.attrMap(span.attributes) : undefined;
+    const status = span.status ? span.status.code : 0;
+    const keyStr = keys.buildKeyString(service, span.name, span.kind, status, c.dims, spanAttrs,
+      resAttrs, c.exclude);
+    let sid = res.byKey.get(keyStr);
+    if (sid !== undefined) return sid;
+    const keyBuf = Buffer.from(keyStr, 'utf8');
+    sid = keys.seriesHash(res.hash, keyBuf);
+    const cur = this.series.get(sid);
+    if (cur !== undefined && (cur.res.hash !== res.hash || cur.keyStr !== keyStr)) {
+      throw new Error('64-bit series id collision; re-salt required');
+    }
+    if (cur === undefined) {
+      // buildAttributes once per key: the first span seen fixes the attributes (A5/A6)
+      const dpAttrs = keys.buildAttributes(service, span.name, span.kind, status, c.dims,
+        spanAttrs, resAttrs, c.exclude);
+      this.series.set(sid, { sid, res, keyStr, dpAttrs, status,
+        counts: null, sumNs: 0n });
+      res.sids.push(sid);
+    }
+    res.byKey.set(keyStr, sid);
+    return sid;
+  }
+
+  /** ConsumeTraces: ExportTraceServiceRequest bytes or a decoded request (otlp.js shape). */
+  consumeTraces(req) {
+    if (!this.handle) throw new Error('connector is shut down');
+    if (Buffer.isBuffer(req) || req instanceof Uint8Array) req = otlp.decodeTraces(req);
+    const cols = this.cols;
+    for (const rs of req.resourceSpans || []) {
+      const resAttrs = keys.attrMap(rs.resource && rs.resource.attributes);
+      const svc = resAttrs.get(keys.SERVICE_NAME_KEY);
+      if (svc === undefined) continue;  // A1: no service.name -> nothing
+      const service = svc.type === 'string' ? svc.value : '';  // pcommon.Value.Str()
+      const res = this._resource(resAttrs);
+      const svcId = this._serviceId(service);
+      for (const ss of rs.scopeSpans || []) {
+        for (const span of ss.spans || []) {
+          const sid = this._seriesId(res, service, span, resAttrs);
+          const i = cols.n;
+          cols.keyHash[i] = sid;
+          cols.startNs[i] = BigInt.asUintN(64, BigInt(span.startTimeUnixNano || 0));
+          cols.endNs[i] = BigInt.asUintN(64, BigInt(span.endTimeUnixNano || 0));
+          const tid = span.traceId;
+          if (tid && tid.length === 16) {
+            cols.w0u8.set(tid.subarray(0, 8), 8 * i);
+            cols.w1u8.set(tid.subarray(8, 16), 8 * i);
+          } else {
+            cols.traceW0[i] = 0n;
+            cols.traceW1[i] = 0n;
+          }
+          const kind = span.kind >= 0 && span.kind <= 7 ? span.kind : 7;  // >5: "" either way
+          const code = span.status ? span.status.code : 0;
+          const st = code >= 0 && code <= 3 ? code : 3;
+          cols.meta[i] = (svcId | (kind << 16) | (st << 19)) >>> 0;
+          cols.n = i + 1;
+          if (cols.n === cols.cap) this._drain();
+        }
+      }
+    }
+  }
+
+  /** Hand the buffered columns to the engine, advancing the window ring first. */
+  _drain() {
+    const cols = this.cols;
+    if (cols.n === 0) return;
+    let maxEnd = 0n;
+    for (let i = 0; i < cols.n; i++) if (cols.endNs[i] > maxEnd) maxEnd = cols.endNs[i];
+    const maxWid = maxEnd / this.cfg.windowNs;
+    const nw = BigInt(this.cfg.nWindows);
+    if (this.windowBase === null) {
+      const base = maxWid >= nw - 1n ? maxWid - (nw - 1n) : 0n;
+      this.addon.windowAdvance(this.handle, base);
+      this.windowBase = base;
+      this.sketchWatermark = base;
+    } else if (maxWid >= this.windowBase + nw) {
+      const base = maxWid - nw + 1n;
+      if (this.cfg.emitSketches) {  // read windows about to be retired, once
+        const top = base < this.maxWindowSeen + 1n ? base : this.maxWindowSeen + 1n;
+        for (let w = this.sketchWatermark > this.windowBase ? this.sketchWatermark : this.windowBase; w < top; w++) {
+          this.closedWindows.push(this._readWindow(w));
+        }
+      }
+      if (this.sketchWatermark < base) this.sketchWatermark = base;
+      this.addon.windowAdvance(this.handle, base);
+      this.windowBase = base;
+    }
+    if (maxWid > this.maxWindowSeen) this.maxWindowSeen = maxWid;
+    this.addon.ingest(this.handle, cols.view());
+    cols.n = 0;
+  }
+
+  // ------------------------------------------------------------ export
+
+  /**
+   * exportMetrics: drain, flush the engine's delta, fold it into the host's
+   * cumulative state (or emit it as delta) and build the OTLP metrics request
+   * (buildMetrics).  Returns the request object; otlp.encodeMetrics() gives bytes.
+   */
+  exportMetrics() {
+    if (!this.handle) throw new Error('connector is shut down');
+    this._drain();
+    const now = this.clock();
+    const r = this.addon.flush(this.handle);
+    if (r.status === this.addon.status.EFULL) this.droppedFlushes += 1;
+    const nb = r.nBuckets;
+    const delta = this.cfg.temporality === otlp.AGGREGATION_TEMPORALITY.DELTA;
+    const touched = new Set();
+    for (let i = 0; i < r.nSeries; i++) {
+      const s = this.series.get(r.keyHash[i]);
+      if (s === undefined) continue;  // evicted and dropped since; its delta is discarded
+      if (delta || s.counts === null) { s.counts = new Array(nb).fill(0n); s.sumNs = 0n; }
+      for (let b = 0; b < nb; b++) s.counts[b] += r.bucketCounts[i * nb + b];
+      s.sumNs += r.sumNs[i];
+      touched.add(s.sid);
+    }
+    const resourceMetrics = [];
+    const emitResource = (res) => {
+      const sids = res.sids.filter((sid) => (delta ? touched.has(sid) : this.series.get(sid).counts !== null));
+      if (sids.length === 0) return;
+      resourceMetrics.push({ resource: { attributes: Array.from(res.attributes, ([key, value]) => ({ key, value })) },
+        scopeMetrics: [{ scope: { name: 'spanmetricsconnector' },
+          metrics: this._buildMetrics(res, sids, now, delta) }] });
+    };
+    for (const res of this.resources.values()) emitResource(res);
+    for (const res of this.evicted.values()) emitResource(res);
+    // resetState: delta purges; cumulative drops what the LRU evicted
+    for (const res of this.evicted.values()) {
+      for (const sid of res.sids) { this.series.delete(sid); this.lastDeltaTs.delete(sid); }
+    }
+    this.evicted.clear();
+    if (delta) for (const sid of touched) this.series.get(sid) && (this.series.get(sid).counts = null);
+    if (this.cfg.emitSketches) {
+      for (let w = this.sketchWatermark; this.windowBase !== null && w < this.maxWindowSeen; w++) {
+        this.closedWindows.push(this._readWindow(w));
+      }
+      if (this.windowBase !== null && this.sketchWatermark < this.maxWindowSeen) this.sketchWatermark = this.maxWindowSeen;
+      if (this.closedWindows.length) resourceMetrics.push(this._sketchMetrics(this.closedWindows));
+      this.closedWindows = [];
+    }
+    return { resourceMetrics };
+  }
+
+  _buildMetrics(res, sids, now, delta) {
+    const c = this.cfg;
+    const ns = c.namespace ? c.namespace + '.' : '';
+    const temporality = c.temporality;
+    const div = c.unit === 's' ? 1e9 : 1e6;
+    const calls = [], hists = [];
+    for (const sid of sids) {
+      const s = this.series.get(sid);
+      let start = res.startTs;
+      if (delta) {
+        const last = this.lastDeltaTs.get(sid);
+        if (last !== undefined) start = last;
+        this.lastDeltaTs.set(sid, now);
+      }
+      let count = 0n;
+      for (const x of s.counts) count += x;
+      calls.push({ attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, asInt: count });
+      hists.push({ attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, count,
+        sum: Number(s.sumNs) / div, bucketCounts: s.counts.slice(), explicitBounds: c.bounds });
+    }
+    return [
+      { name: ns + 'calls', sum: { dataPoints: calls, aggregationTemporality: temporality, isMonotonic: true } },
+      { name: ns + 'duration', unit: c.unit, histogram: { dataPoints: hists, aggregationTemporality: temporality } },
+    ];
+  }
+
+  // ------------------------------------------------------------ sketches
+
+  /**
+   * Sketches of one resident window: distinct traces per service (HLL) and a
+   * count-min point query of ERROR spans per series.
+   */
+  windowSketch(windowId) {
+    if (!this.handle) throw new Error('connector is shut down');
+    this._drain();
+    return this._readWindow(windowId);
+  }
+
+  _readWindow(windowId) {
+    const w = this.addon.windowRead(this.handle, BigInt(windowId));
+    const m = 1 << w.hllP;
+    const distinct = new Map();
+    for (const [name, id] of this.services) {
+      if (id < w.nServices) distinct.set(name, this.addon.hllEstimate(w.hll.subarray(id * m, (id + 1) * m), w.hllP));
+    }
+    const shift = 64n - BigInt(Math.log2(w.cmsW));
+    const errorCount = (sid) => {
+      let best = 0xFFFFFFFF;
+      for (let j = 0; j < w.cmsD; j++) {
+        const col = Number(splitmix64(BigInt.asUintN(64, sid) ^ CMS_SEED[j]) >> shift);
+        best = Math.min(best, w.cms[j * w.cmsW + col]);
+      }
+      return best;
+    };
+    const topErrors = (k = this.cfg.topK) => {
+      const out = [];
+      for (const s of this.series.values()) {
+        if (s.status !== 2) continue;
+        const n = errorCount(s.sid);
+        if (n > 0) out.push({ sid: s.sid, key: s.keyStr, attributes: s.dpAttrs, errors: n });
+      }
+      out.sort((a, b) => b.errors - a.errors);
+      return out.slice(0, k);
+    };
+    return { windowId: w.windowId, startNs: w.windowId * this.cfg.windowNs, distinct, errorCount,
+      topErrors, raw: w };
+  }
+
+  _sketchMetrics(windows) {
+    const ns = this.cfg.namespace ? this.cfg.namespace + '.' : '';
+    const distinct = [], errors = [];
+    for (const w of windows) {
+      const t0 = w.startNs, t1 = w.startNs + this.cfg.windowNs;
+      for (const [name, est] of w.distinct) {
+        if (est === 0) continue;
+        distinct.push({ attributes: [{ key: keys.SERVICE_NAME_KEY, value: { type: 'string', value: name } }],
+          startTimeUnixNano: t0, timeUnixNano: t1, asDouble: est });
+      }
+      for (const e of w.topErrors()) {
+        errors.push({ attributes: e.attributes, startTimeUnixNano: t0, timeUnixNano: t1, asInt: BigInt(e.errors) });
+      }
+    }
+    return { resource: { attributes: [] }, scopeMetrics: [{ scope: { name: 'spanmetricsconnector' }, metrics: [
+      { name: ns + 'window.distinct_traces', gauge: { dataPoints: distinct } },
+      { name: ns + 'window.errors', gauge: { dataPoints: errors } }] }] };
+  }
+
+  stats() {
+    const s = this.addon.stats(this.handle);
+    return Object.assign(s, { resources: this.resources.size, series: this.series.size,
+      services: this.services.size, droppedFlushes: this.droppedFlushes });
+  }
+}
+
+module.exports = { SpanMetricsConnector, normalizeConfig, parseDurationNs, splitmix64, Columns };

@@ -1,0 +1,306 @@
+'use strict';
+/**
+ * CPU tests of the Node host (no GPU needed): OTLP codec round trips, the
+ * transform rules, key building, config parsing, the addon's pure helpers and
+ * error path, and the connector's host logic (resources, temporality, LRU
+ * eviction, A1/A10/A12) over a test-only stand-in for the addon.
+ *
+ * Run: node test/run.js   (exit code 1 on the first failing test)
+ */
+const assert = require('assert');
+const path = require('path');
+
+const lib = path.join(__dirname, '..', 'lib');
+const otlp = require(path.join(lib, 'otlp'));
+const keys = require(path.join(lib, 'keys'));
+const { applyRules, DEMO_SPAN_NAME_RULES } = require(path.join(lib, 'transform'));
+const { SpanMetricsConnector, parseDurationNs, normalizeConfig } = require(path.join(lib, 'connector'));
+const { FakeAddon } = require('./fake_addon');
+
+const tests = [];
+const test = (name, fn) => tests.push({ name, fn });
+const str = (value) => ({ type: 'string', value });
+
+function span(name, opts = {}) {
+  return Object.assign({ traceId: Uint8Array.from({ length: 16 }, (_, i) => i + 1),
+    spanId: new Uint8Array(8).fill(7), name, kind: 2,
+    startTimeUnixNano: 1000000000000n, endTimeUnixNano: 1000003000000n,
+    attributes: [], status: { code: 0, message: '' } }, opts);
+}
+function request(resources) {
+  return { resourceSpans: resources.map(([attrs, spans]) => ({
+    resource: { attributes: Object.entries(attrs).map(([key, v]) => ({ key,
+      value: typeof v === 'object' ? v : str(v) })) },
+    scopeSpans: [{ scope: { name: 'test' }, spans }] })) };
+}
+
+// ------------------------------------------------------------------ OTLP
+
+test('otlp traces round trip keeps every field the connector reads', () => {
+  const req = request([[{ 'service.name': 'frontend', 'k8s.pod.name': 'p-1' }, [
+    span('GET /api/cart', { kind: 3, status: { code: 2, message: 'boom' },
+      attributes: [{ key: 'http.route', value: str('/api/cart') },
+        { key: 'n', value: { type: 'int', value: -42n } },
+        { key: 'f', value: { type: 'double', value: 0.25 } },
+        { key: 'b', value: { type: 'bool', value: false } },
+        { key: 'arr', value: { type: 'array', value: [str('x'), { type: 'int', value: 3n }] } },
+        { key: 'kv', value: { type: 'kvlist', value: [{ key: 'a', value: str('b') }] } },
+        { key: 'raw', value: { type: 'bytes', value: Uint8Array.from([0, 255]) } }] })]]]);
+  const dec = otlp.decodeTraces(otlp.encodeTraces(req));
+  const s = dec.resourceSpans[0].scopeSpans[0].spans[0];
+  assert.strictEqual(s.name, 'GET /api/cart');
+  assert.strictEqual(s.kind, 3);
+  assert.deepStrictEqual(s.status, { code: 2, message: 'boom' });
+  assert.strictEqual(s.startTimeUnixNano, 1000000000000n);
+  assert.strictEqual(s.endTimeUnixNano, 1000003000000n);
+  assert.deepStrictEqual(Array.from(s.traceId), Array.from({ length: 16 }, (_, i) => i + 1));
+  assert.deepStrictEqual(s.attributes[1].value, { type: 'int', value: -42n });
+  assert.deepStrictEqual(s.attributes[4].value.value[1], { type: 'int', value: 3n });
+  assert.deepStrictEqual(Array.from(s.attributes[6].value.value), [0, 255]);
+  assert.strictEqual(dec.resourceSpans[0].resource.attributes[1].value.value, 'p-1');
+});
+
+test('otlp decoder skips unknown fields and rejects truncation', () => {
+  const w = new otlp.Writer();
+  w.tag(99, 0).varint(5);            // unknown varint
+  w.tag(98, 2).string('ignored');    // unknown length-delimited
+  const body = otlp.encodeTraces(request([[{ 'service.name': 's' }, [span('a')]]]));
+  const buf = Buffer.concat([w.finish(), body]);
+  assert.strictEqual(otlp.decodeTraces(buf).resourceSpans.length, 1);
+  assert.throws(() => otlp.decodeTraces(body.subarray(0, body.length - 3)), /truncated/);
+  assert.deepStrictEqual(otlp.decodeTraces(Buffer.alloc(0)), { resourceSpans: [] });
+});
+
+test('otlp metrics encode/decode round trip (sum, histogram, gauge)', () => {
+  const req = { resourceMetrics: [{ resource: { attributes: [{ key: 'service.name', value: str('x') }] },
+    scopeMetrics: [{ scope: { name: 'spanmetricsconnector' }, metrics: [
+      { name: 'calls', sum: { aggregationTemporality: 2, isMonotonic: true,
+        dataPoints: [{ attributes: [], startTimeUnixNano: 5n, timeUnixNano: 9n, asInt: 12n }] } },
+      { name: 'duration', unit: 'ms', histogram: { aggregationTemporality: 1, dataPoints: [{
+        attributes: [{ key: 'span.name', value: str('a') }], startTimeUnixNano: 5n, timeUnixNano: 9n,
+        count: 3n, sum: 0, bucketCounts: [0n, 3n], explicitBounds: [2.5] }] } },
+      { name: 'g', gauge: { dataPoints: [{ attributes: [], startTimeUnixNano: 1n, timeUnixNano: 2n, asDouble: 1.5 }] } },
+    ] }] }] };
+  const d = otlp.decodeMetrics(otlp.encodeMetrics(req));
+  const [calls, dur, g] = d.resourceMetrics[0].scopeMetrics[0].metrics;
+  assert.strictEqual(calls.sum.dataPoints[0].asInt, 12n);
+  assert.strictEqual(calls.sum.isMonotonic, true);
+  assert.strictEqual(dur.histogram.aggregationTemporality, 1);
+  assert.strictEqual(dur.histogram.dataPoints[0].sum, 0);  // optional sum keeps presence
+  assert.deepStrictEqual(dur.histogram.dataPoints[0].bucketCounts, [0n, 3n]);
+  assert.deepStrictEqual(dur.histogram.dataPoints[0].explicitBounds, [2.5]);
+  assert.strictEqual(g.gauge.dataPoints[0].asDouble, 1.5);
+});
+
+// ------------------------------------------------------------- transform
+
+test('demo transform rules (A12)', () => {
+  assert.strictEqual(applyRules('GET /api/products/0PUK6V6EV0?x=1', DEMO_SPAN_NAME_RULES),
+    'GET /api/products/{productId}');
+  assert.strictEqual(applyRules('GET /api/cart?sessionId=1', DEMO_SPAN_NAME_RULES), 'GET /api/cart');
+  assert.strictEqual(applyRules('POST /api/products/1', DEMO_SPAN_NAME_RULES), 'POST /api/products/1');
+  assert.strictEqual(applyRules('GET /api/products/', DEMO_SPAN_NAME_RULES), 'GET /api/products/{productId}');
+});
+
+// ------------------------------------------------------------- keys
+
+test('buildKey skips missing dims with no separator (A5) and uses AsString (A6)', () => {
+  const dims = [{ name: 'A' }, { name: 'B' }];
+  const k1 = keys.buildKeyString('svc', 'op', 2, 0, dims, new Map([['A', str('x')]]));
+  const k2 = keys.buildKeyString('svc', 'op', 2, 0, dims, new Map([['B', str('x')]]));
+  assert.strictEqual(k1, k2);
+  assert.strictEqual(k1, 'svc\0op\0SPAN_KIND_SERVER\0STATUS_CODE_UNSET\0x');
+  const ki = keys.buildKeyString('s', 'o', 9, 7, [{ name: 'c' }], new Map([['c', { type: 'int', value: 200n }]]));
+  assert.strictEqual(ki, ['s', 'o', '', '', '200'].join('\u0000'));  // A7: out-of-range enums -> ""
+});
+
+test('Go FormatFloat(f, -1) for double dimension values', () => {
+  assert.strictEqual(keys.formatFloat(1e21), '1000000000000000000000');
+  assert.strictEqual(keys.formatFloat(1.5e-7), '0.00000015');
+  assert.strictEqual(keys.formatFloat(3), '3');
+  assert.strictEqual(keys.formatFloat(-0.1), '-0.1');
+});
+
+// ------------------------------------------------------------- config
+
+test('config: durations, defaults and validation', () => {
+  assert.strictEqual(parseDurationNs('2ms'), 2e6);
+  assert.strictEqual(parseDurationNs('1m30s'), 90e9);
+  assert.strictEqual(parseDurationNs('1.5s'), 1.5e9);
+  assert.throws(() => parseDurationNs('5 parsecs'));
+  const fa = new FakeAddon();
+  const c = normalizeConfig({}, fa);
+  assert.deepStrictEqual(c.bounds, fa.configDefault().bounds);
+  assert.strictEqual(c.namespace, 'traces.span.metrics');
+  const c2 = normalizeConfig({ histogram: { unit: 's', explicit: { buckets: ['100ms', '1s', 2] } } }, fa);
+  assert.deepStrictEqual(c2.bounds, [0.1, 1, 2]);
+  assert.throws(() => normalizeConfig({ histogram: { unit: 'us' } }, fa));
+  assert.throws(() => normalizeConfig({ aggregation_temporality: 'X' }, fa));
+});
+
+// ------------------------------------------------------------- addon
+
+test('addon loads; pure helpers work; engine errors carry sa_status codes', () => {
+  const addon = require('../lib/addon').load();
+  assert.strictEqual(addon.abiVersion(), 1);
+  const d = addon.configDefault();
+  assert.deepStrictEqual(d.bounds, [2, 4, 6, 8, 10, 50, 100, 200, 400, 800, 1000, 1400, 2000, 5000, 10000, 15000]);
+  const t = addon.bucketThresholds(d.bounds, 'ms');
+  assert.strictEqual(t.nNeg, 0);
+  assert.deepStrictEqual(Array.from(t.thresholds), d.bounds.map((b) => BigInt(b) * 1000000n));
+  assert.throws(() => addon.bucketThresholds([3, 2], 'ms'), (e) => e.code === addon.status.EINVAL);
+  assert.strictEqual(addon.hllEstimate(new Uint8Array(1 << 14), 14), 0);
+  assert.throws(() => addon.hllEstimate(new Uint8Array(10), 14), (e) => e.code === addon.status.EINVAL);
+  assert.throws(() => addon.create({ cmsW: 1000 }), (e) => e.code === addon.status.EINVAL ||
+    e.code === addon.status.EDEVICE);
+  assert.throws(() => addon.ingest({}, {}), TypeError);
+  if (!process.env.SPANAGG_NODE_GPU) {
+    assert.throws(() => addon.create({}), (e) => e.code === addon.status.EDEVICE);
+  }
+});
+
+// ------------------------------------------------------------- connector (host logic)
+
+function mkConnector(cfg = {}, t = { now: 1000n }) {
+  const addon = new FakeAddon();
+  const conn = new SpanMetricsConnector(Object.assign({ batch_size: 4 }, cfg), { addon, clock: () => t.now });
+  return { conn, addon, t };
+}
+const dpsOf = (req, metric) => req.resourceMetrics.flatMap((rm) => rm.scopeMetrics[0].metrics
+  .filter((m) => m.name === metric).flatMap((m) => (m.sum || m.histogram || m.gauge).dataPoints
+    .map((dp) => Object.assign({ resource: rm.resource }, dp))));
+const attr = (dp, k) => (dp.attributes.find((a) => a.key === k) || {}).value;
+
+test('connector: A1 skip, A10 resource grouping, calls == histogram count', () => {
+  const { conn } = mkConnector();
+  conn.consumeTraces(request([
+    [{ 'service.name': 'a' }, [span('x'), span('x'), span('y', { status: { code: 2 } })]],
+    [{ 'host.name': 'nosvc' }, [span('x')]],                                  // A1
+    [{ 'service.name': 'a', 'k8s.pod.name': 'p2' }, [span('x')]],             // A10
+  ]));
+  const out = conn.exportMetrics();
+  assert.strictEqual(out.resourceMetrics.length, 2);
+  const calls = dpsOf(out, 'traces.span.metrics.calls');
+  const hist = dpsOf(out, 'traces.span.metrics.duration');
+  assert.deepStrictEqual(calls.map((d) => d.asInt), [2n, 1n, 1n]);
+  assert.deepStrictEqual(hist.map((d) => d.count), [2n, 1n, 1n]);
+  assert.strictEqual(attr(calls[1], 'status.code').value, 'STATUS_CODE_ERROR');
+  assert.strictEqual(hist[0].sum, 6);   // 2 x 3 ms
+  assert.deepStrictEqual(hist[0].bucketCounts.slice(0, 3), [0n, 2n, 0n]);  // 3 ms -> (2,4]
+  assert.strictEqual(out.resourceMetrics[0].scopeMetrics[0].scope.name, 'spanmetricsconnector');
+  const m = out.resourceMetrics[0].scopeMetrics[0].metrics;
+  assert.strictEqual(m[1].unit, 'ms');
+  assert.strictEqual(m[0].sum.aggregationTemporality, otlp.AGGREGATION_TEMPORALITY.CUMULATIVE);
+});
+
+test('connector: cumulative keeps totals and the resource start time', () => {
+  const { conn, t } = mkConnector();
+  conn.consumeTraces(request([[{ 'service.name': 'a' }, [span('x')]]]));
+  t.now = 2000n;
+  conn.exportMetrics();
+  t.now = 3000n;
+  conn.consumeTraces(request([[{ 'service.name': 'a' }, [span('x'), span('z')]]]));
+  t.now = 4000n;
+  const out = conn.exportMetrics();
+  const calls = dpsOf(out, 'traces.span.metrics.calls');
+  assert.deepStrictEqual(calls.map((d) => [d.asInt, d.startTimeUnixNano, d.timeUnixNano]),
+    [[2n, 1000n, 4000n], [1n, 1000n, 4000n]]);
+  t.now = 5000n;
+  assert.strictEqual(dpsOf(conn.exportMetrics(), 'traces.span.metrics.calls').length, 2);  // no new data
+});
+
+test('connector: delta emits only touched series, start = previous export', () => {
+  const { conn, t } = mkConnector({ aggregation_temporality: 'AGGREGATION_TEMPORALITY_DELTA' });
+  conn.consumeTraces(request([[{ 'service.name': 'a' }, [span('x'), span('y')]]]));
+  t.now = 2000n;
+  let out = conn.exportMetrics();
+  assert.deepStrictEqual(dpsOf(out, 'traces.span.metrics.calls').map((d) => [d.asInt, d.startTimeUnixNano]),
+    [[1n, 1000n], [1n, 1000n]]);
+  conn.consumeTraces(request([[{ 'service.name': 'a' }, [span('x'), span('x')]]]));
+  t.now = 3000n;
+  out = conn.exportMetrics();
+  const c = dpsOf(out, 'traces.span.metrics.calls');
+  assert.deepStrictEqual(c.map((d) => [attr(d, 'span.name').value, d.asInt, d.startTimeUnixNano, d.timeUnixNano]),
+    [['x', 2n, 2000n, 3000n]]);
+  assert.strictEqual(dpsOf(conn.exportMetrics(), 'traces.span.metrics.calls').length, 0);
+});
+
+test('connector: resource LRU evicts, exports the evicted once, then forgets it', () => {
+  const { conn, t } = mkConnector({ resource_metrics_cache_size: 1 });
+  conn.consumeTraces(request([[{ 'service.name': 'a' }, [span('x')]],
+    [{ 'service.name': 'b' }, [span('x')]]]));
+  let out = conn.exportMetrics();
+  assert.strictEqual(out.resourceMetrics.length, 2);   // b live, a evicted but still exported
+  out = conn.exportMetrics();
+  assert.strictEqual(out.resourceMetrics.length, 1);   // a dropped after that export
+  t.now = 9000n;
+  conn.consumeTraces(request([[{ 'service.name': 'a' }, [span('x')]]]));
+  out = conn.exportMetrics();
+  const a = dpsOf(out, 'traces.span.metrics.calls').filter((d) => attr(d, 'service.name').value === 'a');
+  assert.deepStrictEqual(a.map((d) => [d.asInt, d.startTimeUnixNano]), [[1n, 9000n]]);  // fresh start
+});
+
+test('connector: dimensions, defaults, exclude_dimensions and first-seen attribute types', () => {
+  const { conn } = mkConnector({ dimensions: [{ name: 'http.status_code' }, { name: 'region', default: 'eu' }],
+    exclude_dimensions: ['span.kind'] });
+  conn.consumeTraces(request([[{ 'service.name': 'a' }, [
+    span('x', { attributes: [{ key: 'http.status_code', value: { type: 'int', value: 200n } }] }),
+    span('x', { attributes: [{ key: 'http.status_code', value: str('200') }] }),   // A6: same key
+    span('x')]]]));
+  const c = dpsOf(conn.exportMetrics(), 'traces.span.metrics.calls');
+  assert.strictEqual(c.length, 2);
+  assert.strictEqual(c[0].asInt, 2n);
+  assert.deepStrictEqual(attr(c[0], 'http.status_code'), { type: 'int', value: 200n });  // first seen
+  assert.deepStrictEqual(attr(c[0], 'region'), str('eu'));
+  assert.strictEqual(attr(c[0], 'span.kind'), undefined);
+  assert.strictEqual(attr(c[1], 'http.status_code'), undefined);
+});
+
+test('connector: consumes OTLP bytes; columns carry trace ids and meta bits', () => {
+  const { conn, addon } = mkConnector({ batch_size: 2 });
+  const tid = Uint8Array.from({ length: 16 }, (_, i) => 0xA0 + i);
+  conn.consumeTraces(otlp.encodeTraces(request([[{ 'service.name': 'a' }, [
+    span('x', { traceId: tid, kind: 4, status: { code: 2 } }), span('y', { kind: 11 })]]])));
+  assert.strictEqual(addon.batches.length, 1);   // batch_size reached -> one ingest
+  const b = addon.batches[0];
+  assert.strictEqual(b.traceW0[0], Buffer.from(tid).readBigUInt64LE(0));
+  assert.strictEqual(b.traceW1[0], Buffer.from(tid).readBigUInt64LE(8));
+  assert.strictEqual(b.meta[0], 0 | (4 << 16) | (2 << 19));
+  assert.strictEqual(b.meta[1], 0 | (7 << 16));   // out-of-range kind clamps into the 3-bit field
+});
+
+test('connector: window ring follows the data and sketch metrics are emitted once', () => {
+  const { conn, addon } = mkConnector({ sketches: { emit: true, n_windows: 4 } });
+  const W = 10000000000n;
+  const at = (w, name, code = 0) => span(name, { startTimeUnixNano: w * W + 1n, endTimeUnixNano: w * W + 5n,
+    status: { code } });
+  conn.consumeTraces(request([[{ 'service.name': 'a' }, [at(100n, 'x'), at(101n, 'x', 2)]]]));
+  let out = conn.exportMetrics();
+  assert.strictEqual(addon.base, 98n);                   // base = max window - (n_windows - 1)
+  // window 101 is still open (the newest one seen); window 100 is closed
+  assert.deepStrictEqual(dpsOf(out, 'traces.span.metrics.window.distinct_traces')
+    .map((x) => [x.startTimeUnixNano / W, x.asDouble > 0]), [[100n, true]]);
+  conn.consumeTraces(request([[{ 'service.name': 'a' }, [at(110n, 'x')]]]));
+  out = conn.exportMetrics();
+  assert.strictEqual(addon.base, 107n);                  // 101 was read before it was retired
+  const d = dpsOf(out, 'traces.span.metrics.window.distinct_traces');
+  assert.deepStrictEqual(d.map((x) => x.startTimeUnixNano / W), [101n]);
+  const e = dpsOf(out, 'traces.span.metrics.window.errors');
+  assert.deepStrictEqual(e.map((x) => [x.startTimeUnixNano / W, x.asInt]), [[101n, 1n]]);
+  assert.strictEqual(dpsOf(conn.exportMetrics(), 'traces.span.metrics.window.distinct_traces').length, 0);
+});
+
+// ------------------------------------------------------------------ runner
+let failed = 0;
+for (const t of tests) {
+  try {
+    t.fn();
+    console.log(`ok   ${t.name}`);
+  } catch (e) {
+    failed += 1;
+    console.log(`FAIL ${t.name}\n${e.stack}`);
+    break;
+  }
+}
+console.log(`${tests.length - failed}/${tests.length} passed`);
+process.exit(failed ? 1 : 0);

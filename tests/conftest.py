@@ -25,6 +25,10 @@ def _ensure_built():
                        stdout=subprocess.DEVNULL)
     if not os.path.exists(os.path.join(PKG, "spanagg", "libspanagg.so")):
         subprocess.run(["make", "-C", PKG, "-j4"], check=True, stdout=subprocess.DEVNULL)
+    node_addon = os.path.join(ROOT, "host", "node", "build", "spanagg.node")
+    if not os.path.exists(node_addon) and os.path.exists("/usr/include/node/node_api.h"):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "host", "node")], check=True,
+                       stdout=subprocess.DEVNULL)
 
 
 _ensure_built()
