@@ -154,8 +154,16 @@ test('addon loads; pure helpers work; engine errors carry sa_status codes', () =
   assert.throws(() => addon.create({ cmsW: 1000 }), (e) => e.code === addon.status.EINVAL ||
     e.code === addon.status.EDEVICE);
   assert.throws(() => addon.ingest({}, {}), TypeError);
-  if (!process.env.SPANAGG_NODE_GPU) {
-    assert.throws(() => addon.create({}), (e) => e.code === addon.status.EDEVICE);
+  let h = null;
+  try {
+    h = addon.create({});
+  } catch (e) {
+    assert.strictEqual(e.code, addon.status.EDEVICE);  // no GPU here: fails loudly, no fallback
+  }
+  if (h) {  // a GPU is visible: the handle works until destroyed
+    assert.strictEqual(addon.stats(h).spans, 0n);
+    addon.destroy(h);
+    assert.throws(() => addon.stats(h), (e) => e.code === addon.status.ESTATE);
   }
 });
 
