@@ -111,8 +111,10 @@ constexpr uint32_t kHbmBlock = 256;
 // same with nt loads; 8-13 ingest_v2_kernel: 8 generic (nt tile loads), 9 three
 // tiles in flight, 10 four spans per lane, 11 generic (default cache policy),
 // 12 / 13 = 8 / 11 specialised for cap 2048, 17 buckets, HLL p 14.
-constexpr int kNumLdsVariants = 14;
-constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2};
+constexpr int kNumLdsVariants = 16;
+constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2};
+// v2 kernels keep u16 LDS counters for a whole launch: spans per workgroup per launch
+constexpr uint32_t kMaxWgSpans = 65532;
 constexpr uint32_t kDbgPerWg = 136;  // diagnostic stamps per workgroup: 8 + 16 waves x 8
 constexpr uint32_t kHllQueue = 2048;  // deferred HLL raises per workgroup (8 B each)
 constexpr uint32_t kErrTab = 1024;    // LDS (window, slot) -> ERROR count table per workgroup (4 B each)

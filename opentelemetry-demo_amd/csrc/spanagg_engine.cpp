@@ -357,7 +357,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s);
 static int ingest_on(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   // v2 small-table kernels keep u16 LDS counters for the whole launch: at most
   // 65532 spans per workgroup per launch (ingest_v2_kernel has no epoch flush)
-  const uint64_t max_n = (uint64_t)e->G * ((e->small && e->variant >= 8) ? 65532u : (1u << 27));
+  const uint64_t max_n = (uint64_t)e->G * ((e->small && e->variant >= 8) ? sa::kMaxWgSpans : (1u << 27));
   for (uint64_t off = 0; off < b->n; off += max_n) {
     const uint64_t m = std::min(max_n, b->n - off);
     sa_span_batch sub{b->key_hash + off, b->start_ns + off, b->end_ns + off, b->trace_w0 + off,

@@ -792,7 +792,15 @@ __device__ __forceinline__ uint32_t wave_count(bool p) {
 // fixed at compile time for the common geometry (0 = read from P).
 // HAUX >= 0: HLL register reads as buffer loads with that cache policy (gfx950:
 // 1 = sc0, 2 = nt, 16 = sc1); -1 = plain global loads.
-template <int S, int NBUF, int AUX, bool DIAG, int LC = 0, int NWC = 0, int PC = 0, int HAUX = -1>
+// DYN: inside the workgroup's range, waves claim chunks of NBUF wave-tiles
+// from an LDS counter instead of owning a fixed slice of every workgroup
+// tile, so waves the memory arbiter serves late simply take fewer chunks and
+// all 16 finish together (the fixed split left the 4 youngest waves of every
+// workgroup streaming alone for the last ~25% of the launch).  A grid-wide
+// counter in HBM was tried first: its returning atomic put a vmcnt(0) at the
+// top of every round and ran 3.4x slower.
+template <int S, int NBUF, int AUX, bool DIAG, int LC = 0, int NWC = 0, int PC = 0, int HAUX = -1,
+          bool DYN = false>
 __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 0] = __builtin_amdgcn_s_memrealtime();
@@ -813,8 +821,23 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   uint64_t lo, hi;
   wg_range_p(P, lo, hi);
   const uint32_t len = (uint32_t)(hi - lo);
-  constexpr uint32_t tile = kLdsBlock * S;
-  const uint32_t lane_off = threadIdx.x * S;
+  // static: a step covers one workgroup tile (kLdsBlock * S spans, lane_off
+  // by thread); DYN: one wave tile (64 * S spans, lane_off by lane) and a
+  // claim is NBUF consecutive wave tiles
+  constexpr uint32_t tile = DYN ? 64 * S : kLdsBlock * S;
+  constexpr uint32_t chunk = NBUF * tile;
+  const uint32_t lane_off = (DYN ? (threadIdx.x & 63u) : threadIdx.x) * S;
+  constexpr uint32_t kWaves = kLdsBlock / 64;
+  const uint32_t n_chunks = DYN ? (len + chunk - 1) / chunk : 0u;
+  // wave-uniform by construction; readfirstlane keeps it (and every tile
+  // base derived from it) in SGPRs for the buffer descriptors
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  // the first two chunks of every wave are fixed; claims continue after them
+  uint32_t c0 = wave, c1 = wave + kWaves;
+  auto tstart = [&](uint32_t unit, int b) -> uint32_t {  // step b's first span, relative to lo
+    return DYN ? unit * chunk + (uint32_t)b * tile : unit + (uint32_t)b * tile;
+  };
+  auto tremain = [&](uint32_t t) -> uint32_t { return len > t ? len - t : 0u; };
 
   // Prologue: key-table loads (16 B per lane, <= 4 per lane for cap <= 8192)
   // and the bin table first, then the first NBUF tiles; the LDS setup then
@@ -836,9 +859,8 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   Pending<S> pend;
 #pragma unroll
   for (int b = 0; b < NBUF; ++b) {
-    const uint32_t t = b * tile;
-    load_tile_at<S, AUX>(P, (diag & 16u) ? t % (4 * tile) : lo + t, len > t ? len - t : 0u,
-                         lane_off, buf[b]);
+    const uint32_t t = tstart(DYN ? c0 : 0u, b);
+    load_tile_at<S, AUX>(P, (diag & 16u) ? t % (4 * tile) : lo + t, tremain(t), lane_off, buf[b]);
     if (b == NBUF - 1) {
       uint32_t z;  // a VGPR zero: keeps these vector loads (a uniform address would be s_load)
       asm volatile("v_mov_b32 %0, 0" : "=v"(z));
@@ -857,7 +879,10 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   if (threadIdx.x < kBins * 2) reinterpret_cast<uint4 *>(lbins)[threadIdx.x] = bv;
   for (uint32_t i = threadIdx.x * 4; i < cap * nw; i += kLdsBlock * 4)
     *reinterpret_cast<uint4 *>(lcnt + i) = make_uint4(0, 0, 0, 0);
-  if (threadIdx.x == 0) *hq_n = 0;
+  if (threadIdx.x == 0) {
+    hq_n[0] = 0;
+    hq_n[1] = 2u * kWaves;  // DYN: next unclaimed chunk of this workgroup's range
+  }
   etab[threadIdx.x] = 0;  // kErrTab == kLdsBlock
   __syncthreads();
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 1] = __builtin_amdgcn_s_memrealtime();
@@ -897,7 +922,9 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     }
   };
 
-  auto step = [&](SpanTile<S> &T, uint32_t toff) {
+  // step: consume the landed tile T (first span toff) and re-fill its
+  // registers with the tile at pf (relative to lo)
+  auto step = [&](SpanTile<S> &T, uint32_t toff, uint32_t pf) {
     // 1. compact the landed tile (its registers are re-filled in step 3)
     uint64_t key[S], dur[S];
     uint32_t bkt[S], ws[S], hoff[S], rho[S];
@@ -950,11 +977,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     }
     // 3. re-fill the tile registers with the tile NBUF steps ahead
     __builtin_amdgcn_sched_barrier(0);
-    {
-      const uint32_t t = toff + NBUF * tile;
-      load_tile_at<S, AUX>(P, (diag & 16u) ? t % (4 * tile) : lo + t, len > t ? len - t : 0u,
-                           lane_off, T);
-    }
+    load_tile_at<S, AUX>(P, (diag & 16u) ? pf % (4 * tile) : lo + pf, tremain(pf), lane_off, T);
     __builtin_amdgcn_sched_barrier(0);
     stamp(1);
     // 4. key lookup: the two candidate buckets in the LDS mirror
@@ -1037,9 +1060,26 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   // register allocator keeps each in-flight tile in one set of registers
   // across the back-edge instead of copying it (a copy waits for the loads).
   const uint32_t loop_len = (diag & 256u) ? 0u : len;  // diag: prologue/epilogue only
-  for (uint32_t t0 = 0; t0 < loop_len; t0 += NBUF * tile) {
+  if constexpr (DYN) {
+    // c0: this round's chunk (its tiles are in buf), c1: the next round's
+    // (prefetched during this round), c2: claimed now for the round after.
+    // The claim returns while the round runs; its result is read at the end.
+    while (c0 < n_chunks) {
+      // every lane runs the atomic (no branch: a divergent claim made the
+      // compiler wait for it at the join); only lane 0 adds, lane 0's return
+      // is the claim
+      const uint32_t c2 = (uint32_t)__builtin_amdgcn_readfirstlane(
+          (int)atomicAdd(&hq_n[1], (threadIdx.x & 63u) == 0 ? 1u : 0u));
 #pragma unroll
-    for (int b = 0; b < NBUF; ++b) step(buf[b], t0 + b * tile);
+      for (int b = 0; b < NBUF; ++b) step(buf[b], tstart(c0, b), tstart(c1, b));
+      c0 = c1;
+      c1 = c2;
+    }
+  } else {
+    for (uint32_t t0 = 0; t0 < loop_len; t0 += NBUF * tile) {
+#pragma unroll
+      for (int b = 0; b < NBUF; ++b) step(buf[b], t0 + b * tile, t0 + (NBUF + b) * tile);
+    }
   }
   hll_settle(pend);
   const uint64_t wave_loop_end = DIAG && P.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -1258,6 +1298,8 @@ static const void *small_fn(bool bt, int v, bool diag) {
       case 11: return (const void *)&ingest_v2_kernel<2, 2, 0, false>;
       case 12: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14>;
       case 13: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14>;
+      case 14: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true>;
+      case 15: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true>;
       default: return (const void *)&ingest_v2_kernel<2, 2, 2, false>;
     }
   }
@@ -1302,8 +1344,9 @@ hipError_t prepare_ingest_small(size_t lds_bytes) {
 hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,
                                hipStream_t s, int variant) {
   // the specialised v2 build is only valid for its compile-time geometry
-  if ((variant == 12 || variant == 13) && !(P.log2cap == 11 && (P.nbk + 1) / 2 == 9 && P.p == 14))
-    variant = variant == 12 ? 8 : 11;
+  if ((variant == 12 || variant == 13 || variant == 14) &&
+      !(P.log2cap == 11 && (P.nbk + 1) / 2 == 9 && P.p == 14))
+    variant = variant == 12 ? 8 : variant == 13 ? 11 : 15;
   const void *fn = small_fn(P.bintab != nullptr, variant, P.diag != 0 || P.dbg != nullptr);
   void *args[] = {const_cast<IngestParams *>(&P)};
   return hipLaunchKernel(fn, dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);

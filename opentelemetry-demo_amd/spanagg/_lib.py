@@ -103,6 +103,14 @@ def load() -> C.CDLL:
             raise RuntimeError(
                 f"libspanagg.so not found at {LIB_PATH}; build it with "
                 "`make -C opentelemetry-demo_amd` (or __graft_entry__.build())")
+        # torch ships its own libamdhip64.so.7. Loading torch first makes
+        # libspanagg bind to that same HIP runtime (same soname), so device
+        # pointers and streams are shared; loading /opt/rocm's copy first
+        # leaves torch with a second runtime that sees no GPUs.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = C.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
             fn = getattr(lib, name, None)
