@@ -28,7 +28,7 @@ constexpr uint64_t kCmsSeed[8] = {0x9E3779B97F4A7C15ULL, 0xBF58476D1CE4E5B9ULL,
                                   0x8EBC6AF09C88C6E3ULL, 0x589965CC75374CC3ULL};
 constexpr size_t kLdsBudget = 144 * 1024;  // small-table path LDS ceiling per workgroup
 constexpr uint64_t kSlabLimit = 1ULL << 31;  // per-workgroup spans between slab reductions
-constexpr int kDefaultVariant = 12;  // small path: ingest_v2_kernel (SPANAGG_VARIANT overrides)
+constexpr int kDefaultVariant = 14;  // small path: ingest_v2_kernel (SPANAGG_VARIANT overrides)
 
 bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 uint32_t log2u(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
