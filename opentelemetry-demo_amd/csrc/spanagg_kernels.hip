@@ -1291,7 +1291,9 @@ uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap_blocks) {
 // variants, the linear-threshold fallback, and the diagnostic build.
 static const void *small_fn(bool bt, int v, bool diag) {
   if (bt && v >= 8) {  // v2 kernels (bin-table bucketing only)
-    if (diag) return (const void *)&ingest_v2_kernel<2, 2, 2, true>;
+    if (diag)
+      return (v == 14 || v == 15) ? (const void *)&ingest_v2_kernel<2, 2, 2, true, 0, 0, 0, -1, true>
+                                  : (const void *)&ingest_v2_kernel<2, 2, 2, true>;
     switch (v) {
       case 9: return (const void *)&ingest_v2_kernel<2, 3, 0, false>;
       case 10: return (const void *)&ingest_v2_kernel<4, 1, 0, false>;

@@ -49,6 +49,52 @@ __global__ __launch_bounds__(1024) void kern(Cols c, u64 n, const unsigned char 
   for (int q = 0; q < NG; ++q) acc += g0[q] + g1[q];
   if (acc == 0x12345678u) out[0] = acc;
 }
+// The same, but the gathers go through the scalar unit: each lane's address is
+// read out with v_readlane, loaded with s_load_dword (constant address space,
+// so the address path of the vector memory pipeline is not used), and written
+// back with a per-lane select.  16 loads are in flight per batch.
+using cu32 = const __attribute__((address_space(4))) unsigned;
+template <int NG, int D, int TABLE_LOG2>
+__global__ __launch_bounds__(1024) void kern_s(Cols c, u64 n, const unsigned char *tab, unsigned *out) {
+  u64 chunk = (n + gridDim.x - 1) / gridDim.x; chunk = (chunk + 3) / 4 * 4;
+  const u64 lo = blockIdx.x * chunk, hi = lo + chunk < n ? lo + chunk : n;
+  const u64 lane = threadIdx.x * 2, tile = 2048;
+  Tile A, B;
+  ld(c, lo + lane, hi, A); ld(c, lo + tile + lane, hi, B);
+  unsigned acc = 0, g0[NG] = {}, g1[NG] = {};
+  const unsigned mask = (1u << TABLE_LOG2) - 1;
+  cu32 *ctab = (cu32 *)tab;
+  const unsigned lid = __lane_id();
+  for (u64 t = lo; t < hi; t += 2 * tile) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      Tile &T = half ? B : A;
+      const u64 tt = t + half * tile;
+      acc += use(T);
+      unsigned g[NG];
+#pragma unroll
+      for (int q = 0; q < NG; ++q) {
+        const unsigned h = ((unsigned)(tt + lane + q) * 0x9E3779B1u) ^ ((unsigned)(tt >> 11) * 0x85EBCA6Bu);
+        const unsigned w = ((h >> 5) & mask) >> 2;  // u32 word index
+        unsigned v = 0;
+#pragma unroll
+        for (int L0 = 0; L0 < 64; L0 += 16) {
+          unsigned sv[16];
+#pragma unroll
+          for (int L = 0; L < 16; ++L) sv[L] = ctab[__builtin_amdgcn_readlane((int)w, L0 + L)];
+#pragma unroll
+          for (int L = 0; L < 16; ++L) v = (lid == (unsigned)(L0 + L)) ? sv[L] : v;
+        }
+        g[q] = v;
+      }
+      ld(c, tt + 2 * tile + lane, hi, T);
+      if (D == 0) { for (int q = 0; q < NG; ++q) acc += g[q]; }
+      if (D == 1) { for (int q = 0; q < NG; ++q) { acc += g0[q]; g0[q] = g[q]; } }
+    }
+  }
+  for (int q = 0; q < NG; ++q) acc += g0[q] + g1[q];
+  if (acc == 0x12345678u) out[0] = acc;
+}
 // stream-only shapes: S4 simple loop (11 x 16-B loads per lane per iteration),
 // and the S2 ring with meta loaded 8 B/lane vs 16 B/lane on even lanes + DPP.
 template <int MODE>
@@ -97,5 +143,7 @@ int main() {
   std::printf("{\"shape\": \"S4 simple loop\", \"us\": %.2f}\n", time_it([&] { shape<0><<<cus, 1024>>>(c, n, out); }, 20));
   std::printf("{\"shape\": \"S2 ring\", \"us\": %.2f}\n", time_it([&] { shape<1><<<cus, 1024>>>(c, n, out); }, 20));
   R(0, 0, 21) R(2, 0, 21) R(2, 1, 21) R(2, 2, 21) R(2, 1, 15) R(2, 1, 18) R(2, 1, 23) R(1, 1, 21) R(4, 1, 21)
+#define RS(NG, D, TL) std::printf("{\"scalar_gathers_per_step\": %d, \"defer\": %d, \"table_bytes\": %d, \"us\": %.2f}\n", NG, D, 1 << TL, time_it([&] { kern_s<NG, D, TL><<<cus, 1024>>>(c, n, tab, out); }, 20));
+  RS(2, 0, 21) RS(2, 1, 21) RS(1, 1, 21) RS(2, 1, 15)
   return 0;
 }
