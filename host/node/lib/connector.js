@@ -61,6 +61,10 @@ function parseDurationNs(s) {
   return sign * total;
 }
 
+// reserved key strings (a real key never starts with U+0001 / U+0002)
+const OVERFLOW_KEY = '\u0001otel.metric.overflow';
+const EVENT_KEY_PREFIX = '\u0002events\u0000';
+
 const TEMPORALITY = {
   AGGREGATION_TEMPORALITY_CUMULATIVE: otlp.AGGREGATION_TEMPORALITY.CUMULATIVE,
   AGGREGATION_TEMPORALITY_DELTA: otlp.AGGREGATION_TEMPORALITY.DELTA,
@@ -103,6 +107,12 @@ function normalizeConfig(cfg = {}, addon) {
     hllP: sk.hll_p || d.hllP, cmsD: sk.cms_d || d.cmsD, cmsW: sk.cms_w || d.cmsW,
     windowNs, nWindows: sk.n_windows || d.nWindows, nServices: sk.n_services || d.nServices,
     emitSketches: !!sk.emit, topK: sk.top_k || 10,
+    cardinalityLimit: cfg.aggregation_cardinality_limit || 0,
+    exemplars: !!(cfg.exemplars && cfg.exemplars.enabled),
+    exemplarsMax: (cfg.exemplars && cfg.exemplars.max_per_data_point) || 5,
+    events: !!(cfg.events && cfg.events.enabled),
+    eventDims: ((cfg.events && cfg.events.dimensions) || []).map((x) => ({ name: x.name,
+      default: x.default === undefined || x.default === null ? undefined : String(x.default) })),
     keyCapacity: cfg.key_capacity || d.keyCapacity,
     device: cfg.device || 0,
     batchSize: cfg.batch_size || 1 << 16,
@@ -156,6 +166,7 @@ class SpanMetricsConnector {
     this.sketchWatermark = 0n;
     this.closedWindows = [];
     this.droppedFlushes = 0;
+    this.eventRecords = 0;
     this.ticker = null;
   }
 
@@ -180,7 +191,7 @@ class SpanMetricsConnector {
   _serviceId(name) {
     let id = this.services.get(name);
     if (id === undefined) {
-      id = Math.min(this.services.size, 0xFFFF);
+      id = Math.min(this.services.size, 0xFFFE);  // 0xFFFF: event records (no sketch)
       this.services.set(name, id);
     }
     return id;
@@ -203,7 +214,7 @@ class SpanMetricsConnector {
     }
     r = this.evicted.get(h);
     if (r !== undefined) this.evicted.delete(h);
-    else r = { hash: h, attributes: resAttrs, startTs: this.clock(), byKey: new Map(), sids: [] };
+    else r = { hash: h, attributes: resAttrs, startTs: this.clock(), byKey: new Map(), sids: [], nSpanSeries: 0 };
     this.resources.set(h, r);
     if (this.resources.size > this.cfg.resourceCacheSize) {
       const [oldest, rec] = this.resources.entries().next().value;
@@ -213,12 +224,12 @@ class SpanMetricsConnector {
     return r;
   }
 
-  _seriesId(res, service, span, resAttrs) {
-    const c = this.cfg;
-    const spanAttrs = c.dims.length ? keys.attrMap(span.attributes) : undefined;
-    const status = span.status ? span.status.code : 0;
-    const keyStr = keys.buildKeyString(service, span.name, span.kind, status, c.dims, spanAttrs,
-      resAttrs, c.exclude);
+  /**
+   * Series id of a key string in a resource, interning it on first sight.
+   * `mkAttrs` builds the datapoint attributes (called once per key: the first
+   * span seen fixes them, A5/A6).  kind: 'span' | 'event' | 'overflow'.
+   */
+  _intern(res, keyStr, kind, status, mkAttrs) {
     let sid = res.byKey.get(keyStr);
     if (sid !== undefined) return sid;
     const keyBuf = Buffer.from(keyStr, 'utf8');
@@ -228,15 +239,45 @@ class SpanMetricsConnector {
       throw new Error('64-bit series id collision; re-salt required');
     }
     if (cur === undefined) {
-      // buildAttributes once per key: the first span seen fixes the attributes (A5/A6)
-      const dpAttrs = keys.buildAttributes(service, span.name, span.kind, status, c.dims,
-        spanAttrs, resAttrs, c.exclude);
-      this.series.set(sid, { sid, res, keyStr, dpAttrs, status,
-        counts: null, sumNs: 0n });
+      this.series.set(sid, { sid, res, keyStr, dpAttrs: mkAttrs(), status, kind,
+        counts: null, sumNs: 0n, exemplars: [] });
       res.sids.push(sid);
+      if (kind === 'span') res.nSpanSeries += 1;
     }
     res.byKey.set(keyStr, sid);
     return sid;
+  }
+
+  _seriesId(res, service, span, resAttrs, spanAttrs) {
+    const c = this.cfg;
+    const status = span.status ? span.status.code : 0;
+    const keyStr = keys.buildKeyString(service, span.name, span.kind, status, c.dims, spanAttrs,
+      resAttrs, c.exclude);
+    const known = res.byKey.get(keyStr);
+    if (known !== undefined) return known;
+    // aggregation_cardinality_limit: past `limit` series in a resource, new keys
+    // share one overflow series (attribute otel.metric.overflow = true)
+    if (c.cardinalityLimit > 0 && res.nSpanSeries >= c.cardinalityLimit) {
+      return this._intern(res, OVERFLOW_KEY, 'overflow', 0,
+        () => [{ key: 'otel.metric.overflow', value: { type: 'bool', value: true } }]);
+    }
+    return this._intern(res, keyStr, 'span', status, () => keys.buildAttributes(service, span.name,
+      span.kind, status, c.dims, spanAttrs, resAttrs, c.exclude));
+  }
+
+  /** events.enabled: one record per span event, keyed by the span key + event dimensions. */
+  _eventId(res, service, span, resAttrs, spanAttrs, event) {
+    const c = this.cfg;
+    const status = span.status ? span.status.code : 0;
+    const evAttrs = keys.attrMap(event.attributes);
+    const base = keys.buildKeyString(service, span.name, span.kind, status, c.dims, spanAttrs,
+      resAttrs, c.exclude);
+    const evKey = keys.buildKeyString('', '', 0, 0, c.eventDims, evAttrs, new Map(),
+      new Set([keys.SERVICE_NAME_KEY, 'span.name', 'span.kind', 'status.code']));
+    return this._intern(res, EVENT_KEY_PREFIX + base + evKey, 'event', status, () =>
+      keys.buildAttributes(service, span.name, span.kind, status, c.dims, spanAttrs, resAttrs, c.exclude)
+        .concat(keys.buildAttributes('', '', 0, 0, c.eventDims, evAttrs, new Map(),
+          new Set([keys.SERVICE_NAME_KEY, 'span.name', 'span.kind', 'status.code']))));
   }
 
   /** ConsumeTraces: ExportTraceServiceRequest bytes or a decoded request (otlp.js shape). */
@@ -253,7 +294,12 @@ class SpanMetricsConnector {
       const svcId = this._serviceId(service);
       for (const ss of rs.scopeSpans || []) {
         for (const span of ss.spans || []) {
-          const sid = this._seriesId(res, service, span, resAttrs);
+          const spanAttrs = this.cfg.dims.length ? keys.attrMap(span.attributes) : undefined;
+          const sid = this._seriesId(res, service, span, resAttrs, spanAttrs);
+          if (this.cfg.exemplars) this._exemplar(sid, span);
+          if (this.cfg.events && span.events && span.events.length) {
+            for (const ev of span.events) this._pushEvent(this._eventId(res, service, span, resAttrs, spanAttrs, ev));
+          }
           const i = cols.n;
           cols.keyHash[i] = sid;
           cols.startNs[i] = BigInt.asUintN(64, BigInt(span.startTimeUnixNano || 0));
@@ -275,6 +321,31 @@ class SpanMetricsConnector {
         }
       }
     }
+  }
+
+  /** exemplars.enabled: the first max_per_data_point spans of each series per export. */
+  _exemplar(sid, span) {
+    const s = this.series.get(sid);
+    if (s.exemplars.length >= this.cfg.exemplarsMax) return;
+    const st = BigInt(span.startTimeUnixNano || 0), en = BigInt(span.endTimeUnixNano || 0);
+    s.exemplars.push({ traceId: span.traceId, spanId: span.spanId, timeUnixNano: en,
+      asDouble: Number(en > st ? en - st : 0n) / (this.cfg.unit === 's' ? 1e9 : 1e6) });
+  }
+
+  /** An event record: counted by the engine like a span of duration 0, with an
+   * out-of-range service id so it touches no sketch. */
+  _pushEvent(sid) {
+    const cols = this.cols;
+    const i = cols.n;
+    cols.keyHash[i] = sid;
+    cols.startNs[i] = 0n;
+    cols.endNs[i] = 0n;
+    cols.traceW0[i] = 0n;
+    cols.traceW1[i] = 0n;
+    cols.meta[i] = 0xFFFF;
+    cols.n = i + 1;
+    this.eventRecords += 1;
+    if (cols.n === cols.cap) this._drain();
   }
 
   /** Hand the buffered columns to the engine, advancing the window ring first. */
@@ -363,7 +434,7 @@ class SpanMetricsConnector {
     const ns = c.namespace ? c.namespace + '.' : '';
     const temporality = c.temporality;
     const div = c.unit === 's' ? 1e9 : 1e6;
-    const calls = [], hists = [];
+    const calls = [], hists = [], events = [];
     for (const sid of sids) {
       const s = this.series.get(sid);
       let start = res.startTs;
@@ -374,14 +445,26 @@ class SpanMetricsConnector {
       }
       let count = 0n;
       for (const x of s.counts) count += x;
+      if (s.kind === 'event') {
+        events.push({ attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, asInt: count });
+        continue;
+      }
       calls.push({ attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, asInt: count });
-      hists.push({ attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, count,
-        sum: Number(s.sumNs) / div, bucketCounts: s.counts.slice(), explicitBounds: c.bounds });
+      const h = { attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, count,
+        sum: Number(s.sumNs) / div, bucketCounts: s.counts.slice(), explicitBounds: c.bounds };
+      if (s.exemplars.length) h.exemplars = s.exemplars;
+      hists.push(h);
+      s.exemplars = [];  // exemplars cover one export interval, both temporalities
     }
-    return [
+    const out = [
       { name: ns + 'calls', sum: { dataPoints: calls, aggregationTemporality: temporality, isMonotonic: true } },
       { name: ns + 'duration', unit: c.unit, histogram: { dataPoints: hists, aggregationTemporality: temporality } },
     ];
+    if (c.events) {
+      out.push({ name: ns + 'events', sum: { dataPoints: events, aggregationTemporality: temporality,
+        isMonotonic: true } });
+    }
+    return out;
   }
 
   // ------------------------------------------------------------ sketches
@@ -448,7 +531,8 @@ class SpanMetricsConnector {
   stats() {
     const s = this.addon.stats(this.handle);
     return Object.assign(s, { resources: this.resources.size, series: this.series.size,
-      services: this.services.size, droppedFlushes: this.droppedFlushes });
+      services: this.services.size, droppedFlushes: this.droppedFlushes,
+      eventRecords: this.eventRecords });
   }
 }
 

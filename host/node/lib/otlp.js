@@ -160,11 +160,22 @@ function decodeStatus(r) {
   return s;
 }
 
+function decodeEvent(r) {
+  const e = { timeUnixNano: 0n, name: '', attributes: [] };
+  r.fields((f, wt) => {
+    if (f === 1 && wt === WT_I64) { e.timeUnixNano = r.fixed64(); return true; }
+    if (f === 2 && wt === WT_LEN) { e.name = r.string(); return true; }
+    if (f === 3 && wt === WT_LEN) { e.attributes.push(decodeKeyValue(r.sub())); return true; }
+    return false;
+  });
+  return e;
+}
+
 function decodeSpan(r) {
   const s = {
     traceId: new Uint8Array(16), spanId: new Uint8Array(8), parentSpanId: new Uint8Array(0),
     traceState: '', name: '', kind: 0, startTimeUnixNano: 0n, endTimeUnixNano: 0n,
-    attributes: [], status: { message: '', code: 0 }, flags: 0,
+    attributes: [], events: [], status: { message: '', code: 0 }, flags: 0,
   };
   r.fields((f, wt) => {
     switch (f) {
@@ -177,9 +188,10 @@ function decodeSpan(r) {
       case 7: if (wt !== WT_I64) return false; s.startTimeUnixNano = r.fixed64(); return true;
       case 8: if (wt !== WT_I64) return false; s.endTimeUnixNano = r.fixed64(); return true;
       case 9: if (wt !== WT_LEN) return false; s.attributes.push(decodeKeyValue(r.sub())); return true;
+      case 11: if (wt !== WT_LEN) return false; s.events.push(decodeEvent(r.sub())); return true;
       case 15: if (wt !== WT_LEN) return false; s.status = decodeStatus(r.sub()); return true;
       case 16: if (wt !== WT_I32) return false; s.flags = r.fixed32(); return true;
-      default: return false;  // events, links, dropped counts: not used by the connector
+      default: return false;  // links, dropped counts: not used by the connector
     }
   });
   return s;
@@ -317,6 +329,13 @@ function encodeSpan(w, s) {
   w.fFixed64(7, s.startTimeUnixNano);
   w.fFixed64(8, s.endTimeUnixNano);
   for (const kv of s.attributes || []) w.fMsg(9, encodeKeyValue, kv);
+  for (const ev of s.events || []) {
+    w.fMsg(11, (ww, e) => {
+      ww.fFixed64(1, e.timeUnixNano);
+      ww.fString(2, e.name);
+      for (const kv of e.attributes || []) ww.fMsg(3, encodeKeyValue, kv);
+    }, ev);
+  }
   const st = s.status || {};
   if (st.message || st.code) {
     w.fMsg(15, (ww, x) => { ww.fString(2, x.message); ww.fVarint(3, x.code); }, st);
@@ -369,6 +388,16 @@ function encodeHistogramDataPoint(w, dp) {
     dp.explicitBounds.forEach((x, i) => b.writeDoubleLE(x, 8 * i));
     w.tag(7, WT_LEN).bytes(b);
   }
+  for (const ex of dp.exemplars || []) w.fMsg(8, encodeExemplar, ex);
+}
+
+function encodeExemplar(w, ex) {
+  w.fFixed64(2, ex.timeUnixNano);
+  if (ex.asInt !== undefined) w.tag(6, WT_I64).fixed64(BigInt.asUintN(64, BigInt(ex.asInt)));
+  else w.tag(3, WT_I64).double(ex.asDouble || 0);
+  w.fBytes(4, ex.spanId);
+  w.fBytes(5, ex.traceId);
+  for (const kv of ex.filteredAttributes || []) w.fMsg(7, encodeKeyValue, kv);
 }
 
 function encodeMetric(w, m) {
@@ -439,6 +468,20 @@ function decodePackedFixed64(r, wt, out, asDouble) {
   return true;
 }
 
+function decodeExemplar(r) {
+  const ex = { timeUnixNano: 0n, spanId: new Uint8Array(0), traceId: new Uint8Array(0), filteredAttributes: [] };
+  r.fields((f, wt) => {
+    if (f === 2 && wt === WT_I64) { ex.timeUnixNano = r.fixed64(); return true; }
+    if (f === 3 && wt === WT_I64) { ex.asDouble = r.double(); return true; }
+    if (f === 6 && wt === WT_I64) { ex.asInt = BigInt.asIntN(64, r.fixed64()); return true; }
+    if (f === 4 && wt === WT_LEN) { ex.spanId = Uint8Array.from(r.bytes()); return true; }
+    if (f === 5 && wt === WT_LEN) { ex.traceId = Uint8Array.from(r.bytes()); return true; }
+    if (f === 7 && wt === WT_LEN) { ex.filteredAttributes.push(decodeKeyValue(r.sub())); return true; }
+    return false;
+  });
+  return ex;
+}
+
 function decodeHistogramDataPoint(r) {
   const dp = { attributes: [], startTimeUnixNano: 0n, timeUnixNano: 0n, count: 0n,
     bucketCounts: [], explicitBounds: [] };
@@ -448,6 +491,7 @@ function decodeHistogramDataPoint(r) {
     if (f === 3 && wt === WT_I64) { dp.timeUnixNano = r.fixed64(); return true; }
     if (f === 4 && wt === WT_I64) { dp.count = r.fixed64(); return true; }
     if (f === 5 && wt === WT_I64) { dp.sum = r.double(); return true; }
+    if (f === 8 && wt === WT_LEN) { (dp.exemplars = dp.exemplars || []).push(decodeExemplar(r.sub())); return true; }
     if (f === 6) return decodePackedFixed64(r, wt, dp.bucketCounts, false);
     if (f === 7) return decodePackedFixed64(r, wt, dp.explicitBounds, true);
     return false;

@@ -298,6 +298,52 @@ test('connector: window ring follows the data and sketch metrics are emitted onc
   assert.strictEqual(dpsOf(conn.exportMetrics(), 'traces.span.metrics.window.distinct_traces').length, 0);
 });
 
+test('connector: aggregation_cardinality_limit folds new keys into one overflow series', () => {
+  const { conn } = mkConnector({ aggregation_cardinality_limit: 2 });
+  conn.consumeTraces(request([[{ 'service.name': 'a' }, [span('x'), span('y'), span('z'), span('w'),
+    span('x')]], [{ 'service.name': 'b' }, [span('q')]]]));
+  const c = dpsOf(conn.exportMetrics(), 'traces.span.metrics.calls');
+  const a = c.filter((d) => d.resource.attributes[0].value.value === 'a');
+  assert.deepStrictEqual(a.map((d) => d.asInt), [2n, 1n, 2n]);
+  assert.deepStrictEqual(a[2].attributes, [{ key: 'otel.metric.overflow', value: { type: 'bool', value: true } }]);
+  assert.strictEqual(c.length, 4);   // the limit is per resource
+});
+
+test('connector: events metric counts span events per key + event dimensions', () => {
+  const { conn, addon } = mkConnector({ events: { enabled: true, dimensions: [{ name: 'exception.type' }] } });
+  const ev = (t) => ({ timeUnixNano: 5n, name: 'exception', attributes: t ? [{ key: 'exception.type', value: str(t) }] : [] });
+  conn.consumeTraces(otlp.encodeTraces(request([[{ 'service.name': 'a' }, [
+    span('x', { events: [ev('IOError'), ev('IOError'), ev('Timeout')] }), span('x', { events: [ev(null)] })]]])));
+  const out = conn.exportMetrics();
+  const e = dpsOf(out, 'traces.span.metrics.events');
+  assert.deepStrictEqual(e.map((d) => [(attr(d, 'exception.type') || {}).value, d.asInt]),
+    [['IOError', 2n], ['Timeout', 1n], [undefined, 1n]]);
+  assert.strictEqual(attr(e[0], 'span.name').value, 'x');
+  assert.deepStrictEqual(dpsOf(out, 'traces.span.metrics.calls').map((d) => d.asInt), [2n]);
+  assert.strictEqual(conn.stats().eventRecords, 4);
+  const metas = addon.batches.flatMap((b) => Array.from(b.meta));
+  assert.strictEqual(metas.filter((m) => m === 0xFFFF).length, 4);  // no sketch for event records
+});
+
+test('connector: exemplars carry trace/span ids and the duration, one export interval each', () => {
+  const { conn } = mkConnector({ exemplars: { enabled: true, max_per_data_point: 2 } });
+  const tid = Uint8Array.from({ length: 16 }, (_, i) => 0x10 + i);
+  conn.consumeTraces(request([[{ 'service.name': 'a' }, [span('x', { traceId: tid }), span('x'), span('x')]]]));
+  let out = conn.exportMetrics();
+  let h = dpsOf(out, 'traces.span.metrics.duration')[0];
+  assert.strictEqual(h.exemplars.length, 2);
+  assert.deepStrictEqual(Array.from(h.exemplars[0].traceId), Array.from(tid));
+  assert.strictEqual(h.exemplars[0].asDouble, 3);
+  const dec = otlp.decodeMetrics(otlp.encodeMetrics(out));
+  const hd = dec.resourceMetrics[0].scopeMetrics[0].metrics[1].histogram.dataPoints[0];
+  assert.strictEqual(hd.exemplars.length, 2);
+  assert.deepStrictEqual(Array.from(hd.exemplars[0].traceId), Array.from(tid));
+  assert.strictEqual(hd.exemplars[0].timeUnixNano, 1000003000000n);
+  out = conn.exportMetrics();
+  h = dpsOf(out, 'traces.span.metrics.duration')[0];
+  assert.strictEqual(h.exemplars, undefined);
+});
+
 // ------------------------------------------------------------------ runner
 let failed = 0;
 for (const t of tests) {

@@ -1143,7 +1143,7 @@ __global__ __launch_bounds__(BLOCK) void ingest_hbm_kernel(IngestParams P) {
         if (key != 0 && !(P.diag & 1u)) {
           const uint32_t b = bucket_of<NB>(d, P);
           const uint32_t found = g_find_insert(P.gkeys, key, P.log2cap, P.max_probe);
-          if (found != kNotFound) {
+          if (found != kNotFound && !(P.diag & 2048u)) {  // diag 2048: lookups only
             unsigned long long *row = P.gcounts + (uint64_t)found * stride;
             atomicAdd(row + b, 1ULL);
             atomicAdd(row + nbk, (unsigned long long)d);

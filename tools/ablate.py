@@ -32,6 +32,10 @@ VARIANTS_FINE = {
     "hll_store": 512,
     "hll_noread": 1024,
 }
+VARIANTS_C4 = {
+    "lookup_only": 2048,  # HBM path: key-table lookups, no counter atomics
+    "lookup_only_no_sketch": 2048 | NO_HLL | NO_CMS,
+}
 VARIANTS = {
     "l2_input": L2_INPUT,
     "l2_input_no_hll": L2_INPUT | NO_HLL,
@@ -50,7 +54,17 @@ def main():
     n = int(os.environ.get("ABL_SPANS", 10_000_000))
     rounds = int(os.environ.get("ABL_ROUNDS", 7))
     reps = int(os.environ.get("ABL_REPS", 10))
-    wl = generate_c2(n, seed=42)
+    c4 = os.environ.get("ABL_WORKLOAD") == "c4"
+    if c4:  # high-cardinality HBM-table path (1 M keys, one service)
+        from spanagg.synth import generate_highcard
+        hb, _, hfirst = generate_highcard(n, seed=7, routes=int(os.environ.get("ABL_ROUTES", 2000)))
+
+        class _W:
+            batch, first_window, n_services = hb, hfirst, 1
+        wl = _W()
+    else:
+        wl = generate_c2(n, seed=42)
+    kcap = int(os.environ.get("ABL_KCAP", 1_200_000 if c4 else 1000))
     dev = torch.device("cuda", 0)
     cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(dev)
             for c in wl.batch.columns()]
@@ -59,19 +73,25 @@ def main():
     engines = {}
     base_variant = os.environ.get("SPANAGG_VARIANT", "0")
     os.environ["SPANAGG_VARIANT"] = os.environ.get("ABL_BASE", base_variant)
+    if c4:
+        VARIANTS.update(VARIANTS_C4)
     if os.environ.get("ABL_FINE"):
         VARIANTS.update(VARIANTS_FINE)
     for name, fl in VARIANTS.items():
-        e = Engine(Config(n_services=wl.n_services, n_windows=16, flags=fl))
+        e = Engine(Config(n_services=wl.n_services, n_windows=16, flags=fl, key_capacity=kcap))
         e.window_advance(wl.first_window)
         engines[name] = e
     # kernel-structure variants (sa_internal.h kVariants), full work
     for v in [int(x) for x in os.environ.get("ABL_VARS", "0,8,11,12").split(",")]:
         os.environ["SPANAGG_VARIANT"] = str(v)
-        e = Engine(Config(n_services=wl.n_services, n_windows=16))
+        e = Engine(Config(n_services=wl.n_services, n_windows=16, key_capacity=kcap))
         e.window_advance(wl.first_window)
         engines[f"variant{v}"] = e
     os.environ["SPANAGG_VARIANT"] = base_variant
+    for kc in [int(x) for x in os.environ.get("ABL_KCAPS", "").split(",") if x]:
+        e = Engine(Config(n_services=wl.n_services, n_windows=16, key_capacity=kc))
+        e.window_advance(wl.first_window)
+        engines[f"key_capacity{kc}"] = e
     times = {k: [] for k in engines}
     for r in range(rounds):
         for name, e in engines.items():
