@@ -175,7 +175,10 @@ class SpanMetricsConnector {
   /** Start: the flush ticker (metrics_flush_interval) feeding metricsConsumer. */
   start() {
     if (this.ticker || !this.metricsConsumer) return;
-    this.ticker = setInterval(() => this.metricsConsumer(this.exportMetrics()), this.cfg.flushIntervalMs);
+    this.ticker = setInterval(() => {
+      // export failures are the consumer's to count; the ticker keeps going
+      Promise.resolve().then(() => this.metricsConsumer(this.exportMetrics())).catch(() => {});
+    }, this.cfg.flushIntervalMs);
     if (this.ticker.unref) this.ticker.unref();
   }
 

@@ -1,0 +1,78 @@
+'use strict';
+/**
+ * The demo collector's traces -> spanmetrics -> metrics path as one object
+ * (/root/reference/src/otel-collector/otelcol-config.yml:118-127):
+ *
+ *   traces:  receivers [otlp] -> processors [memory_limiter, transform, batch]
+ *            -> exporters [spanmetrics]
+ *   metrics: receivers [spanmetrics] -> exporters [otlphttp/prometheus]
+ *
+ * `batch` is the connector's column buffer (spans are handed to the GPU in
+ * batches of `spanmetrics.batch_size`).  The other exporters of the demo's
+ * traces pipeline (Jaeger, debug) are outside this path.
+ */
+const otlp = require('./otlp');
+const { applyRules, DEMO_SPAN_NAME_RULES } = require('./transform');
+const { SpanMetricsConnector } = require('./connector');
+const { OtlpReceiver, OtlpHttpExporter, MemoryLimiter } = require('./receiver');
+
+class TracesToMetricsPipeline {
+  /**
+   * @param opts.spanmetrics  connector config (YAML field names)
+   * @param opts.transform    span-name rules (default: the demo's two rules; [] disables)
+   * @param opts.memoryLimiter MemoryLimiter options (default: the demo's 80% / 25%), or false
+   * @param opts.receiver     OtlpReceiver options ({httpPort, grpcPort, host}), or false
+   * @param opts.exporter     OtlpHttpExporter options ({endpoint}), or false
+   * @param opts.addon, opts.clock  passed to the connector
+   */
+  constructor(opts = {}) {
+    this.rules = opts.transform === undefined ? DEMO_SPAN_NAME_RULES : opts.transform;
+    this.limiter = opts.memoryLimiter === false ? null
+      : new MemoryLimiter(Object.assign({ limit_percentage: 80, spike_limit_percentage: 25 }, opts.memoryLimiter));
+    this.exporter = opts.exporter ? new OtlpHttpExporter(opts.exporter) : null;
+    this.connector = new SpanMetricsConnector(opts.spanmetrics || {}, { addon: opts.addon, clock: opts.clock,
+      metricsConsumer: (req) => this._export(req) });
+    this.receiver = opts.receiver === false ? null
+      : new OtlpReceiver(Object.assign({}, opts.receiver, { onTraces: (b) => this.consumeTraces(b) }));
+    this.exportErrors = 0;
+    this.lastExport = null;
+  }
+
+  async start() {
+    if (this.receiver) await this.receiver.start();
+    this.connector.start();
+    return this;
+  }
+
+  /** memory_limiter -> decode -> transform -> spanmetrics. */
+  consumeTraces(bytes) {
+    if (this.limiter) this.limiter.check();
+    const req = Buffer.isBuffer(bytes) || bytes instanceof Uint8Array ? otlp.decodeTraces(bytes) : bytes;
+    if (this.rules.length) {
+      for (const rs of req.resourceSpans || []) {
+        for (const ss of rs.scopeSpans || []) for (const s of ss.spans || []) s.name = applyRules(s.name, this.rules);
+      }
+    }
+    this.connector.consumeTraces(req);
+  }
+
+  _export(req) {
+    const bytes = otlp.encodeMetrics(req);
+    this.lastExport = bytes;
+    if (!this.exporter) return Promise.resolve(bytes);
+    return this.exporter.export(bytes).then(() => bytes, (e) => {
+      this.exportErrors += 1;
+      throw e;
+    });
+  }
+
+  /** One export now (what the connector's ticker does every metrics_flush_interval). */
+  flush() { return this._export(this.connector.exportMetrics()); }
+
+  async shutdown() {
+    if (this.receiver) await this.receiver.close();
+    this.connector.shutdown();
+  }
+}
+
+module.exports = { TracesToMetricsPipeline };

@@ -344,17 +344,139 @@ test('connector: exemplars carry trace/span ids and the duration, one export int
   assert.strictEqual(h.exemplars, undefined);
 });
 
-// ------------------------------------------------------------------ runner
-let failed = 0;
-for (const t of tests) {
-  try {
-    t.fn();
-    console.log(`ok   ${t.name}`);
-  } catch (e) {
-    failed += 1;
-    console.log(`FAIL ${t.name}\n${e.stack}`);
-    break;
-  }
+// ------------------------------------------------- receiver / exporter / pipeline
+const http = require('http');
+const http2 = require('http2');
+const zlib = require('zlib');
+const { OtlpReceiver, MemoryLimiter, grpcFrame, grpcUnframe, TRACE_EXPORT_PATH } = require(path.join(lib, 'receiver'));
+const { TracesToMetricsPipeline } = require(path.join(lib, 'pipeline'));
+
+function post(port, pathName, body, headers) {
+  return new Promise((resolve, reject) => {
+    const req = http.request({ host: '127.0.0.1', port, path: pathName, method: 'POST', headers }, (res) => {
+      const chunks = [];
+      res.on('data', (c) => chunks.push(c));
+      res.on('end', () => resolve({ status: res.statusCode, body: Buffer.concat(chunks) }));
+    });
+    req.on('error', reject);
+    req.end(body);
+  });
 }
-console.log(`${tests.length - failed}/${tests.length} passed`);
-process.exit(failed ? 1 : 0);
+
+function grpcCall(port, pathName, frames, extra = {}) {
+  return new Promise((resolve, reject) => {
+    const client = http2.connect(`http://127.0.0.1:${port}`);
+    client.on('error', reject);
+    const req = client.request(Object.assign({ ':method': 'POST', ':path': pathName,
+      'content-type': 'application/grpc', te: 'trailers' }, extra));
+    const chunks = [];
+    let trailers = {};
+    req.on('trailers', (t) => { trailers = t; });
+    req.on('data', (c) => chunks.push(c));
+    req.on('end', () => { client.close(); resolve({ body: Buffer.concat(chunks), trailers }); });
+    req.on('error', reject);
+    req.end(frames);
+  });
+}
+
+test('receiver: OTLP/HTTP and OTLP/gRPC deliver request bytes; errors map to retryable codes', async () => {
+  const got = [];
+  let refuse = false;
+  const rx = await new OtlpReceiver({ httpPort: 0, grpcPort: 0, onTraces: (b) => {
+    if (refuse) { const e = new Error('full'); e.refused = true; throw e; }
+    got.push(otlp.decodeTraces(b));
+  } }).start();
+  try {
+    const body = otlp.encodeTraces(request([[{ 'service.name': 'a' }, [span('x'), span('y')]]]));
+    let r = await post(rx.httpPort, '/v1/traces', body, { 'Content-Type': 'application/x-protobuf' });
+    assert.strictEqual(r.status, 200);
+    r = await post(rx.httpPort, '/v1/traces', zlib.gzipSync(body),
+      { 'Content-Type': 'application/x-protobuf', 'Content-Encoding': 'gzip' });
+    assert.strictEqual(r.status, 200);
+    r = await post(rx.httpPort, '/v1/traces', Buffer.from('{}'), { 'Content-Type': 'application/json' });
+    assert.strictEqual(r.status, 415);
+    r = await post(rx.httpPort, '/v1/metrics', body, { 'Content-Type': 'application/x-protobuf' });
+    assert.strictEqual(r.status, 404);
+    let g = await grpcCall(rx.grpcPort, TRACE_EXPORT_PATH, Buffer.concat([grpcFrame(body), grpcFrame(body)]));
+    assert.strictEqual(g.trailers['grpc-status'], '0');
+    assert.deepStrictEqual(grpcUnframe(g.body), [Buffer.alloc(0)]);
+    const gz = zlib.gzipSync(body);
+    const cf = grpcFrame(gz);
+    cf[0] = 1;  // compressed flag
+    g = await grpcCall(rx.grpcPort, TRACE_EXPORT_PATH, cf, { 'grpc-encoding': 'gzip' });
+    assert.strictEqual(g.trailers['grpc-status'], '0');
+    assert.strictEqual(got.length, 5);
+    assert.strictEqual(got[4].resourceSpans[0].scopeSpans[0].spans[1].name, 'y');
+    g = await grpcCall(rx.grpcPort, '/x.Y/Z', grpcFrame(body));
+    assert.strictEqual(g.trailers['grpc-status'], '12');
+    refuse = true;
+    r = await post(rx.httpPort, '/v1/traces', body, { 'Content-Type': 'application/x-protobuf' });
+    assert.strictEqual(r.status, 503);
+    g = await grpcCall(rx.grpcPort, TRACE_EXPORT_PATH, grpcFrame(body));
+    assert.strictEqual(g.trailers['grpc-status'], '14');
+  } finally {
+    await rx.close();
+  }
+});
+
+test('memory_limiter: refuses above the soft limit, recovers below it', () => {
+  let rss = 10;
+  const m = new MemoryLimiter({ limit_mib: 100, spike_limit_mib: 20, check_interval_ms: 0, usage: () => rss * 1048576 });
+  m.check();
+  rss = 81;
+  assert.throws(() => m.check(), (e) => e.refused === true);
+  rss = 79;
+  m.check();
+  assert.strictEqual(m.refused, 1);
+  const demo = new MemoryLimiter({ total: 1000, usage: () => 0 });
+  assert.strictEqual(demo.limit, 800);
+  assert.strictEqual(demo.soft, 550);
+});
+
+test('pipeline: OTLP/HTTP in -> transform -> connector -> otlphttp out', async () => {
+  const posted = [];
+  const sink = http.createServer((req, res) => {
+    const chunks = [];
+    req.on('data', (c) => chunks.push(c));
+    req.on('end', () => { posted.push({ url: req.url, type: req.headers['content-type'], body: Buffer.concat(chunks) }); res.end(); });
+  });
+  await new Promise((r) => sink.listen(0, '127.0.0.1', r));
+  const p = await new TracesToMetricsPipeline({ addon: new FakeAddon(), clock: () => 7n,
+    receiver: { httpPort: 0, grpcPort: 0 }, memoryLimiter: { limit_mib: 1e9 },
+    exporter: { endpoint: `http://127.0.0.1:${sink.address().port}/api/v1/otlp` } }).start();
+  try {
+    const body = otlp.encodeTraces(request([[{ 'service.name': 'frontend' }, [
+      span('GET /api/products/ABC?currency=USD'), span('GET /api/products/XYZ')]]]));
+    const r = await post(p.receiver.httpPort, '/v1/traces', body, { 'Content-Type': 'application/x-protobuf' });
+    assert.strictEqual(r.status, 200);
+    await p.flush();
+    assert.strictEqual(posted.length, 1);
+    assert.strictEqual(posted[0].url, '/api/v1/otlp/v1/metrics');
+    assert.strictEqual(posted[0].type, 'application/x-protobuf');
+    const m = otlp.decodeMetrics(posted[0].body);
+    const calls = m.resourceMetrics[0].scopeMetrics[0].metrics[0].sum.dataPoints;
+    assert.strictEqual(calls.length, 1);  // both names collapse to one series (A12)
+    assert.strictEqual(calls[0].asInt, 2n);
+    assert.strictEqual(attr(calls[0], 'span.name').value, 'GET /api/products/{productId}');
+  } finally {
+    await p.shutdown();
+    await new Promise((r) => sink.close(r));
+  }
+});
+
+// ------------------------------------------------------------------ runner
+(async () => {
+  let failed = 0;
+  for (const t of tests) {
+    try {
+      await t.fn();
+      console.log(`ok   ${t.name}`);
+    } catch (e) {
+      failed += 1;
+      console.log(`FAIL ${t.name}\n${e.stack}`);
+      break;
+    }
+  }
+  console.log(`${tests.length - failed}/${tests.length} passed`);
+  process.exit(failed ? 1 : 0);
+})();

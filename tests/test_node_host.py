@@ -420,3 +420,35 @@ def test_node_host_end_to_end_matches_oracle():
             assert not hll.any() and not cms.any()
     st = out["stats"]
     assert int(st["spans"]) == n and int(st["windowOutOfRange"]) == 0 and int(st["droppedTableFull"]) == 0
+
+
+def test_receiver_interoperates_with_grpcio_and_http_clients():
+    """A real gRPC stack (grpcio, HTTP/2) and a plain HTTP client talk to the
+    Node receiver; the bytes are Python-protobuf encoded."""
+    grpc = pytest.importorskip("grpc")
+    import urllib.request
+
+    p = subprocess.Popen([NODE, os.path.join(NODE_DIR, "test", "serve.js")], stdin=subprocess.PIPE,
+                         stdout=subprocess.PIPE, text=True)
+    try:
+        ports = json.loads(p.stdout.readline())
+        raw = _py_traces_request(SPEC).SerializeToString()
+        with grpc.insecure_channel(f"127.0.0.1:{ports['grpc']}") as ch:
+            export = ch.unary_unary("/opentelemetry.proto.collector.trace.v1.TraceService/Export",
+                                    request_serializer=None, response_deserializer=None)
+            assert export(raw, timeout=10) == b""  # empty ExportTraceServiceResponse
+            with pytest.raises(grpc.RpcError) as ei:
+                ch.unary_unary("/opentelemetry.proto.collector.trace.v1.TraceService/Nope")(raw, timeout=10)
+            assert ei.value.code() == grpc.StatusCode.UNIMPLEMENTED
+        req = urllib.request.Request(f"http://127.0.0.1:{ports['http']}/v1/traces", data=raw,
+                                     headers={"Content-Type": "application/x-protobuf"}, method="POST")
+        with urllib.request.urlopen(req, timeout=10) as r:
+            assert r.status == 200
+        out, _ = p.communicate(timeout=30)
+    finally:
+        if p.poll() is None:
+            p.kill()
+    summary = json.loads(out.strip().splitlines()[-1])
+    assert summary["requests"] == 2
+    assert summary["spans"] == 2 * sum(len(spans) for _, spans in SPEC)
+    assert summary["names"][:2] == [s["name"] for s in SPEC[0][1]]
