@@ -20,6 +20,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
+import subprocess
 import sys
 import time
 
@@ -75,6 +77,27 @@ def load_traffic(path, workload):
     return None, None
 
 
+def host_otlp_rate(spans: int):
+    """the OTLP decode+aggregate rate from protobuf bytes on one
+    core -- the Node host (native columnizer in the N-API addon) feeding this
+    GPU through sa_ingest (host memory, PCIe included).  Not `value`."""
+    node = shutil.which("node")
+    script = os.path.join(ROOT, "host", "node", "test", "host_rate.js")
+    if node is None or not os.path.exists(os.path.join(ROOT, "host", "node", "build", "spanagg.node")):
+        return None
+    try:
+        p = subprocess.run([node, script, str(spans), "--gpu"], capture_output=True, text=True,
+                           timeout=120)
+        r = json.loads(p.stdout.strip().splitlines()[-1])
+    except Exception as e:  # reported, never fatal for the bench line
+        return {"error": str(e)[:200]}
+    return {"value": r["spans_per_s"], "unit": "spans/s", "cores": 1, "mb_per_s": r["mb_per_s"],
+            "calls_check": r["calls_check"], "columnizer": r["columnizer"],
+            "sample": f"{r['spans']:,} spans in {r['requests']} OTLP requests of 512 spans, "
+                      "20 services x 25 names, decode + transform rules + keying + columnise + "
+                      "sa_ingest (H2D + kernel)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -85,6 +108,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--host-otlp-spans", type=int, default=500_000,
+                    help="spans for the Node host's OTLP->GPU rate (0 = skip)")
     args = ap.parse_args()
 
     import numpy as np
@@ -197,6 +222,8 @@ def main():
             port, conn = cpu_baseline(wl, args.cpu_seconds)
             result["cpu_baseline"] = port
             result["cpu_baseline_connector"] = conn
+        if world == 1 and args.host_otlp_spans > 0:
+            result["host_otlp"] = host_otlp_rate(args.host_otlp_spans)
         print(json.dumps(result), flush=True)
     eng.close()
     if world > 1:

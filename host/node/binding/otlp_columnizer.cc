@@ -1,0 +1,711 @@
+// otlp_columnizer.cc -- see otlp_columnizer.h.
+#include "otlp_columnizer.h"
+
+#include <algorithm>
+#include <charconv>
+#include <cmath>
+#include <cstring>
+#include <string_view>
+
+namespace otlpcol {
+namespace {
+
+// ---------------------------------------------------------------- xxHash64
+constexpr uint64_t P1 = 0x9E3779B185EBCA87ULL, P2 = 0xC2B2AE3D27D4EB4FULL, P3 = 0x165667B19E3779F9ULL,
+                   P4 = 0x85EBCA77C2B2AE63ULL, P5 = 0x27D4EB2F165667C5ULL;
+inline uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+inline uint64_t rd64(const uint8_t *p) {
+  uint64_t v;
+  std::memcpy(&v, p, 8);  // little-endian host (x86-64)
+  return v;
+}
+inline uint32_t rd32(const uint8_t *p) {
+  uint32_t v;
+  std::memcpy(&v, p, 4);
+  return v;
+}
+inline uint64_t round1(uint64_t acc, uint64_t in) { return rotl(acc + in * P2, 31) * P1; }
+inline uint64_t merge1(uint64_t acc, uint64_t v) { return (acc ^ round1(0, v)) * P1 + P4; }
+
+// ---------------------------------------------------------------- protobuf
+struct PB {
+  const uint8_t *p, *end;
+  bool ok = true;
+  PB(const uint8_t *a, const uint8_t *b) : p(a), end(b) {}
+  void fail() { ok = false; p = end; }
+  uint64_t varint() {
+    uint64_t x = 0;
+    for (int s = 0; s < 64 && p < end; s += 7) {
+      const uint8_t b = *p++;
+      x |= (uint64_t)(b & 0x7f) << s;
+      if (!(b & 0x80)) return x;
+    }
+    fail();
+    return 0;
+  }
+  uint64_t fixed64() {
+    if (end - p < 8) return fail(), 0;
+    const uint64_t v = rd64(p);
+    p += 8;
+    return v;
+  }
+  double dbl() {
+    const uint64_t u = fixed64();
+    double d;
+    std::memcpy(&d, &u, 8);
+    return d;
+  }
+  PB sub() {
+    const uint64_t n = varint();
+    if (!ok || n > (uint64_t)(end - p)) {
+      fail();
+      return PB(end, end);
+    }
+    PB s(p, p + n);
+    p += n;
+    return s;
+  }
+  std::string_view str() {
+    PB s = sub();
+    return std::string_view(reinterpret_cast<const char *>(s.p), (size_t)(s.end - s.p));
+  }
+  void skip(int wt) {
+    switch (wt) {
+      case 0: varint(); break;
+      case 1: if (end - p < 8) fail(); else p += 8; break;
+      case 2: sub(); break;
+      case 5: if (end - p < 4) fail(); else p += 4; break;
+      default: fail();
+    }
+  }
+  // next field; false at the end or on error (check ok)
+  bool next(uint32_t &f, int &wt) {
+    if (p >= end) return false;
+    const uint64_t t = varint();
+    if (!ok) return false;
+    f = (uint32_t)(t >> 3);
+    wt = (int)(t & 7);
+    if (f == 0) return fail(), false;
+    return true;
+  }
+};
+
+// ---------------------------------------------------------------- strings
+bool valid_utf8(std::string_view s) {
+  const auto *p = reinterpret_cast<const uint8_t *>(s.data()), *e = p + s.size();
+  while (p < e) {
+    const uint8_t c = *p;
+    if (c < 0x80) { ++p; continue; }
+    int n;
+    uint32_t cp;
+    if ((c & 0xE0) == 0xC0) n = 1, cp = c & 0x1F;
+    else if ((c & 0xF0) == 0xE0) n = 2, cp = c & 0x0F;
+    else if ((c & 0xF8) == 0xF0) n = 3, cp = c & 0x07;
+    else return false;
+    if (e - p <= n) return false;
+    for (int i = 1; i <= n; ++i) {
+      if ((p[i] & 0xC0) != 0x80) return false;
+      cp = (cp << 6) | (p[i] & 0x3F);
+    }
+    if ((n == 1 && cp < 0x80) || (n == 2 && cp < 0x800) || (n == 3 && cp < 0x10000) || cp > 0x10FFFF ||
+        (cp >= 0xD800 && cp <= 0xDFFF))
+      return false;
+    p += n + 1;
+  }
+  return true;
+}
+
+std::vector<uint32_t> code_points(std::string_view s) {  // s is valid UTF-8
+  std::vector<uint32_t> out;
+  const auto *p = reinterpret_cast<const uint8_t *>(s.data()), *e = p + s.size();
+  while (p < e) {
+    const uint8_t c = *p;
+    int n = c < 0x80 ? 0 : (c & 0xE0) == 0xC0 ? 1 : (c & 0xF0) == 0xE0 ? 2 : 3;
+    uint32_t cp = n == 0 ? c : n == 1 ? (c & 0x1F) : n == 2 ? (c & 0x0F) : (c & 0x07);
+    for (int i = 1; i <= n; ++i) cp = (cp << 6) | (p[i] & 0x3F);
+    out.push_back(cp);
+    p += n + 1;
+  }
+  return out;
+}
+
+const char *kB64 = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+std::string base64(std::string_view b) {
+  std::string o;
+  o.reserve((b.size() + 2) / 3 * 4);
+  size_t i = 0;
+  const auto *u = reinterpret_cast<const uint8_t *>(b.data());
+  for (; i + 3 <= b.size(); i += 3) {
+    const uint32_t v = (u[i] << 16) | (u[i + 1] << 8) | u[i + 2];
+    o += kB64[v >> 18]; o += kB64[(v >> 12) & 63]; o += kB64[(v >> 6) & 63]; o += kB64[v & 63];
+  }
+  if (b.size() - i == 1) {
+    const uint32_t v = u[i] << 16;
+    o += kB64[v >> 18]; o += kB64[(v >> 12) & 63]; o += "==";
+  } else if (b.size() - i == 2) {
+    const uint32_t v = (u[i] << 16) | (u[i + 1] << 8);
+    o += kB64[v >> 18]; o += kB64[(v >> 12) & 63]; o += kB64[(v >> 6) & 63]; o += '=';
+  }
+  return o;
+}
+
+// JSON.stringify of a (valid UTF-8) string
+void json_string(std::string &o, std::string_view s) {
+  static const char *hex = "0123456789abcdef";
+  o += '"';
+  for (const char ch : s) {
+    const uint8_t c = (uint8_t)ch;
+    switch (c) {
+      case '"': o += "\\\""; break;
+      case '\\': o += "\\\\"; break;
+      case '\b': o += "\\b"; break;
+      case '\f': o += "\\f"; break;
+      case '\n': o += "\\n"; break;
+      case '\r': o += "\\r"; break;
+      case '\t': o += "\\t"; break;
+      default:
+        if (c < 0x20) {
+          o += "\\u00";
+          o += hex[c >> 4];
+          o += hex[c & 15];
+        } else {
+          o += ch;
+        }
+    }
+  }
+  o += '"';
+}
+
+// shortest round-trip digits and decimal exponent: v = 0.d1d2... * 10^n (JS's n)
+void shortest(double v, std::string &digits, int &n) {
+  char buf[64];
+  auto r = std::to_chars(buf, buf + sizeof buf, v, std::chars_format::scientific);
+  std::string_view s(buf, (size_t)(r.ptr - buf));  // d[.ddd]e±xx
+  const size_t epos = s.find('e');
+  digits.clear();
+  for (size_t i = 0; i < epos; ++i)
+    if (s[i] != '.') digits += s[i];
+  int e = 0;
+  std::from_chars(s.data() + epos + 1 + (s[epos + 1] == '+'), s.data() + s.size(), e);
+  while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+  n = e + 1;
+}
+
+// JavaScript Number.prototype.toString() for finite v
+std::string js_number(double v) {
+  if (v == 0) return "0";
+  std::string sign = std::signbit(v) ? "-" : "";
+  std::string d;
+  int n;
+  shortest(std::fabs(v), d, n);
+  const int k = (int)d.size();
+  if (k <= n && n <= 21) return sign + d + std::string(n - k, '0');
+  if (0 < n && n <= 21) return sign + d.substr(0, n) + "." + d.substr(n);
+  if (-6 < n && n <= 0) return sign + "0." + std::string(-n, '0') + d;
+  const int e = n - 1;
+  std::string o = sign + d.substr(0, 1);
+  if (k > 1) o += "." + d.substr(1);
+  return o + "e" + (e >= 0 ? "+" : "-") + std::to_string(std::abs(e));
+}
+
+// ---------------------------------------------------------------- AnyValue
+enum VType { kEmpty, kStr, kBool, kInt, kDouble, kBytes, kArray, kKvlist };
+const char *kTypeTag[] = {"NoneType", "str", "bool", "int", "float", "bytes", "list", "dict"};
+
+struct Any {
+  VType type = kEmpty;
+  std::string_view s;  // kStr / kBytes
+  bool b = false;
+  int64_t i = 0;
+  double d = 0;
+  PB body{nullptr, nullptr};  // kArray / kKvlist
+};
+
+Any parse_any(PB pb) {
+  Any a;  // last field wins, like otlp.js decodeAnyValue
+  uint32_t f;
+  int wt;
+  while (pb.next(f, wt)) {
+    if (f == 1 && wt == 2) a = Any{}, a.type = kStr, a.s = pb.str();
+    else if (f == 2 && wt == 0) a = Any{}, a.type = kBool, a.b = pb.varint() != 0;
+    else if (f == 3 && wt == 0) a = Any{}, a.type = kInt, a.i = (int64_t)pb.varint();
+    else if (f == 4 && wt == 1) a = Any{}, a.type = kDouble, a.d = pb.dbl();
+    else if (f == 5 && wt == 2) a = Any{}, a.type = kArray, a.body = pb.sub();
+    else if (f == 6 && wt == 2) a = Any{}, a.type = kKvlist, a.body = pb.sub();
+    else if (f == 7 && wt == 2) a = Any{}, a.type = kBytes, a.s = pb.str();
+    else pb.skip(wt);
+  }
+  if (!pb.ok) a.type = kEmpty, a.body = PB(nullptr, nullptr), a.s = {}, a.i = 0;
+  return a;
+}
+
+// KeyValue -> (key, value); ok=false on malformed input
+bool parse_kv(PB pb, std::string_view &key, Any &val) {
+  key = {};
+  val = Any{};
+  uint32_t f;
+  int wt;
+  while (pb.next(f, wt)) {
+    if (f == 1 && wt == 2) key = pb.str();
+    else if (f == 2 && wt == 2) val = parse_any(pb.sub());
+    else pb.skip(wt);
+  }
+  return pb.ok;
+}
+
+bool raw_json(std::string &o, const Any &a);
+
+bool raw_json_array(std::string &o, PB pb) {
+  o += '[';
+  bool first = true;
+  uint32_t f;
+  int wt;
+  while (pb.next(f, wt)) {
+    if (f == 1 && wt == 2) {
+      if (!first) o += ',';
+      first = false;
+      if (!raw_json(o, parse_any(pb.sub()))) return false;
+    } else {
+      pb.skip(wt);
+    }
+  }
+  o += ']';
+  return pb.ok;
+}
+
+bool raw_json_kvlist(std::string &o, PB pb) {
+  o += '{';
+  bool first = true;
+  uint32_t f;
+  int wt;
+  while (pb.next(f, wt)) {
+    if (f == 1 && wt == 2) {
+      std::string_view k;
+      Any v;
+      if (!parse_kv(pb.sub(), k, v) || !valid_utf8(k)) return false;
+      if (!first) o += ',';
+      first = false;
+      json_string(o, k);
+      o += ':';
+      if (!raw_json(o, v)) return false;
+    } else {
+      pb.skip(wt);
+    }
+  }
+  o += '}';
+  return pb.ok;
+}
+
+// keys.js rawJson
+bool raw_json(std::string &o, const Any &a) {
+  switch (a.type) {
+    case kStr:
+      if (!valid_utf8(a.s)) return false;
+      json_string(o, a.s);
+      return true;
+    case kBool: o += a.b ? "true" : "false"; return true;
+    case kInt: o += std::to_string(a.i); return true;
+    case kDouble:
+      if (std::isfinite(a.d)) o += js_number(a.d);
+      else json_string(o, format_float(a.d));
+      return true;
+    case kBytes: json_string(o, base64(a.s)); return true;
+    case kArray: return raw_json_array(o, a.body);
+    case kKvlist: return raw_json_kvlist(o, a.body);
+    default: o += "null"; return true;
+  }
+}
+
+// keys.js asString; false when the value cannot be keyed natively
+bool as_string(const Any &a, std::string &o) {
+  o.clear();
+  switch (a.type) {
+    case kStr:
+      if (!valid_utf8(a.s)) return false;
+      o.assign(a.s);
+      return true;
+    case kBool: o = a.b ? "true" : "false"; return true;
+    case kInt: o = std::to_string(a.i); return true;
+    case kDouble: o = format_float(a.d); return true;
+    case kBytes: o = base64(a.s); return true;
+    case kArray: case kKvlist: return raw_json(o, a);
+    default: return true;
+  }
+}
+
+const char *kKindStr[] = {"SPAN_KIND_UNSPECIFIED", "SPAN_KIND_INTERNAL", "SPAN_KIND_SERVER",
+                          "SPAN_KIND_CLIENT", "SPAN_KIND_PRODUCER", "SPAN_KIND_CONSUMER"};
+const char *kStatusStr[] = {"STATUS_CODE_UNSET", "STATUS_CODE_OK", "STATUS_CODE_ERROR"};
+
+bool glob_match(const std::vector<uint32_t> &pat, const std::vector<uint32_t> &s) {
+  size_t p = 0, i = 0, star = std::string::npos, mark = 0;
+  while (i < s.size()) {
+    if (p < pat.size() && (pat[p] == '?' || (pat[p] != '*' && pat[p] == s[i]))) {
+      ++p, ++i;
+    } else if (p < pat.size() && pat[p] == '*') {
+      star = p++;
+      mark = i;
+    } else if (star != std::string::npos) {
+      p = star + 1;
+      i = ++mark;
+    } else {
+      return false;
+    }
+  }
+  while (p < pat.size() && pat[p] == '*') ++p;
+  return p == pat.size();
+}
+
+struct Attr {
+  std::string_view key;
+  Any val;
+};
+
+// attrMap semantics: one entry per key, the last value wins
+void dedupe_last(std::vector<Attr> &v) {
+  std::vector<Attr> out;
+  out.reserve(v.size());
+  for (size_t i = 0; i < v.size(); ++i) {
+    bool later = false;
+    for (size_t j = i + 1; j < v.size() && !later; ++j) later = v[j].key == v[i].key;
+    if (!later) out.push_back(v[i]);
+  }
+  v.swap(out);
+}
+
+const Any *find_attr(const std::vector<Attr> &v, std::string_view k) {
+  for (auto it = v.rbegin(); it != v.rend(); ++it)
+    if (it->key == k) return &it->val;
+  return nullptr;
+}
+
+}  // namespace
+
+uint64_t xxh64(const void *data, size_t len, uint64_t seed) {
+  const uint8_t *p = static_cast<const uint8_t *>(data), *end = p + len;
+  uint64_t h;
+  if (len >= 32) {
+    uint64_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+    const uint8_t *limit = end - 32;
+    do {
+      v1 = round1(v1, rd64(p));
+      v2 = round1(v2, rd64(p + 8));
+      v3 = round1(v3, rd64(p + 16));
+      v4 = round1(v4, rd64(p + 24));
+      p += 32;
+    } while (p <= limit);
+    h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+    h = merge1(h, v1);
+    h = merge1(h, v2);
+    h = merge1(h, v3);
+    h = merge1(h, v4);
+  } else {
+    h = seed + P5;
+  }
+  h += (uint64_t)len;
+  for (; p + 8 <= end; p += 8) h = rotl(h ^ round1(0, rd64(p)), 27) * P1 + P4;
+  if (p + 4 <= end) {
+    h = rotl(h ^ ((uint64_t)rd32(p) * P1), 23) * P2 + P3;
+    p += 4;
+  }
+  for (; p < end; ++p) h = rotl(h ^ ((uint64_t)*p * P5), 11) * P1;
+  h ^= h >> 33;
+  h *= P2;
+  h ^= h >> 29;
+  h *= P3;
+  h ^= h >> 32;
+  return h;
+}
+
+std::string format_float(double v) {
+  if (std::isnan(v)) return "NaN";
+  if (std::isinf(v)) return v > 0 ? "+Inf" : "-Inf";
+  if (v == 0) return std::signbit(v) ? "-0" : "0";
+  std::string d;
+  int n;
+  shortest(std::fabs(v), d, n);
+  const std::string sign = v < 0 ? "-" : "";
+  const int k = (int)d.size();
+  if (n >= k) return sign + d + std::string(n - k, '0');
+  if (n > 0) return sign + d.substr(0, n) + "." + d.substr(n);
+  return sign + "0." + std::string(-n, '0') + d;
+}
+
+void Rule::prepare() {
+  cps = code_points(pattern);
+  prefix.clear();
+  for (char c : pattern) {
+    if (c == '*' || c == '?') break;
+    prefix += c;
+  }
+}
+
+std::string apply_rules(const std::vector<Rule> &rules, std::string name) {
+  for (const Rule &r : rules) {  // kGlob rules must have been prepare()d
+    if (r.kind == Rule::kStripQuery) {
+      // Go regexp `\?.*`, ReplaceAllString(.., ""): `.` stops at '\n'
+      std::string o;
+      o.reserve(name.size());
+      for (size_t i = 0; i < name.size();) {
+        if (name[i] == '?') {
+          while (i < name.size() && name[i] != '\n') ++i;
+        } else {
+          o += name[i++];
+        }
+      }
+      name.swap(o);
+    } else if (name.compare(0, r.prefix.size(), r.prefix) == 0 &&
+               glob_match(r.cps, code_points(name))) {
+      name = r.replacement;
+    }
+  }
+  return name;
+}
+
+uint32_t Columnizer::service_id(const std::string &name, bool *is_new) {
+  auto it = services_.find(name);
+  if (it != services_.end()) {
+    if (is_new) *is_new = false;
+    return it->second;
+  }
+  const uint32_t id = (uint32_t)std::min<size_t>(services_.size(), 0xFFFE);  // 0xFFFF: event records
+  services_.emplace(name, id);
+  if (is_new) *is_new = true;
+  return id;
+}
+
+Result Columnizer::columnize(const uint8_t *buf, size_t len) {
+  Result res;
+  const size_t n0 = key_.size();
+  const uint64_t max0 = max_end_;
+  // dictionary entries made by this call: committed only on success
+  std::vector<std::pair<uint64_t, std::string>> added_keys;
+  std::vector<std::string> added_services;
+  std::vector<uint64_t> added_resources;
+
+  auto rollback = [&](Result::Status st, const char *why) {
+    key_.resize(n0); start_.resize(n0); end_.resize(n0); w0_.resize(n0); w1_.resize(n0); meta_.resize(n0);
+    max_end_ = max0;
+    for (auto &k : added_keys) {
+      auto it = res_keys_.find(k.first);
+      if (it != res_keys_.end()) it->second.erase(k.second);
+    }
+    for (uint64_t h : added_resources) res_keys_.erase(h);
+    for (auto &s : added_services) services_.erase(s);
+    Result r;
+    r.status = st;
+    r.error = why;
+    return r;
+  };
+
+  PB req(buf, buf + len);
+  uint32_t f;
+  int wt;
+  std::vector<Attr> rattrs, sattrs;
+  std::string tmp, keystr, sname;
+  std::vector<uint8_t> hbuf;
+  while (req.next(f, wt)) {
+    if (f != 1 || wt != 2) {
+      req.skip(wt);
+      continue;
+    }
+    PB rs = req.sub();
+    // pass 1: the Resource message (it may follow scope_spans on the wire)
+    PB resource(nullptr, nullptr);
+    bool has_resource = false;
+    {
+      PB scan = rs;
+      uint32_t g;
+      int wt2;
+      while (scan.next(g, wt2)) {
+        if (g == 1 && wt2 == 2) resource = scan.sub(), has_resource = true;
+        else scan.skip(wt2);
+      }
+      if (!scan.ok) return rollback(Result::kError, "malformed ResourceSpans");
+    }
+    rattrs.clear();
+    if (has_resource) {
+      PB r = resource;
+      uint32_t g;
+      int wt2;
+      while (r.next(g, wt2)) {
+        if (g == 1 && wt2 == 2) {
+          Attr a;
+          if (!parse_kv(r.sub(), a.key, a.val)) return rollback(Result::kError, "malformed KeyValue");
+          if (!valid_utf8(a.key)) return rollback(Result::kFallback, "non-UTF-8 attribute key");
+          rattrs.push_back(a);
+        } else {
+          r.skip(wt2);
+        }
+      }
+      if (!r.ok) return rollback(Result::kError, "malformed Resource");
+    }
+    dedupe_last(rattrs);
+    const Any *svc = find_attr(rattrs, "service.name");
+    if (!svc) continue;  // A1: a resource without service.name contributes nothing
+    std::string service;
+    if (svc->type == kStr) {
+      if (!valid_utf8(svc->s)) return rollback(Result::kFallback, "non-UTF-8 service.name");
+      service.assign(svc->s);
+    }
+    // resource identity (keys.js resourceHash over the key attributes)
+    std::vector<const Attr *> hv;
+    for (const Attr &a : rattrs) {
+      if (opt_.key_attributes.empty() ||
+          std::find(opt_.key_attributes.begin(), opt_.key_attributes.end(), a.key) != opt_.key_attributes.end())
+        hv.push_back(&a);
+    }
+    std::sort(hv.begin(), hv.end(), [](const Attr *x, const Attr *y) { return x->key < y->key; });
+    hbuf.clear();
+    for (const Attr *a : hv) {
+      if (!as_string(a->val, tmp)) return rollback(Result::kFallback, "resource attribute not keyable natively");
+      hbuf.insert(hbuf.end(), a->key.begin(), a->key.end());
+      hbuf.push_back(0);
+      hbuf.insert(hbuf.end(), tmp.begin(), tmp.end());
+      hbuf.push_back(0);
+      const char *tag = kTypeTag[a->val.type];
+      hbuf.insert(hbuf.end(), tag, tag + std::strlen(tag));
+      hbuf.push_back(1);
+    }
+    const uint64_t rhash = xxh64(hbuf.data(), hbuf.size(), 0);
+    auto rit = res_keys_.find(rhash);
+    if (rit == res_keys_.end()) {
+      rit = res_keys_.emplace(rhash, std::unordered_map<std::string, uint64_t>{}).first;
+      added_resources.push_back(rhash);
+      res.new_resources.push_back({rhash, has_resource ? (int64_t)(resource.p - buf) : -1,
+                                   has_resource ? (uint32_t)(resource.end - resource.p) : 0u});
+    }
+    auto &keys = rit->second;
+    res.resources.push_back(rhash);
+    bool svc_new = false;
+    const uint32_t svc_id = service_id(service, &svc_new);
+    if (svc_new) {
+      added_services.push_back(service);
+      res.new_services.emplace_back(service, svc_id);
+    }
+
+    // pass 2: scope_spans -> spans
+    PB scan = rs;
+    uint32_t g;
+    int wt2;
+    while (scan.next(g, wt2)) {
+      if (g != 2 || wt2 != 2) {
+        scan.skip(wt2);
+        continue;
+      }
+      PB ss = scan.sub();
+      uint32_t h;
+      int wt3;
+      while (ss.next(h, wt3)) {
+        if (h != 2 || wt3 != 2) {
+          ss.skip(wt3);
+          continue;
+        }
+        PB sp = ss.sub();
+        const uint8_t *span_begin = sp.p, *span_end = sp.end;
+        const uint8_t *tid = nullptr;
+        size_t tid_len = 0;
+        std::string_view name;
+        int32_t kind = 0, code = 0;
+        uint64_t st = 0, en = 0;
+        sattrs.clear();
+        uint32_t k;
+        int wt4;
+        while (sp.next(k, wt4)) {
+          if (k == 1 && wt4 == 2) {
+            const std::string_view t = sp.str();
+            tid = reinterpret_cast<const uint8_t *>(t.data());
+            tid_len = t.size();
+          } else if (k == 5 && wt4 == 2) {
+            name = sp.str();
+          } else if (k == 6 && wt4 == 0) {
+            kind = (int32_t)(uint32_t)sp.varint();
+          } else if (k == 7 && wt4 == 1) {
+            st = sp.fixed64();
+          } else if (k == 8 && wt4 == 1) {
+            en = sp.fixed64();
+          } else if (k == 9 && wt4 == 2 && !opt_.dims.empty()) {
+            Attr a;
+            if (!parse_kv(sp.sub(), a.key, a.val)) return rollback(Result::kError, "malformed KeyValue");
+            sattrs.push_back(a);
+          } else if (k == 15 && wt4 == 2) {
+            PB stt = sp.sub();
+            uint32_t m;
+            int wt5;
+            code = 0;  // a later Status message replaces an earlier one
+            while (stt.next(m, wt5)) {
+              if (m == 3 && wt5 == 0) code = (int32_t)(uint32_t)stt.varint();
+              else stt.skip(wt5);
+            }
+            if (!stt.ok) return rollback(Result::kError, "malformed Status");
+          } else {
+            sp.skip(wt4);
+          }
+        }
+        if (!sp.ok) return rollback(Result::kError, "malformed Span");
+        if (!valid_utf8(name)) return rollback(Result::kFallback, "non-UTF-8 span name");
+        sname = apply_rules(opt_.rules, std::string(name));
+        // key = buildKey
+        keystr.clear();
+        bool first = true;
+        auto part = [&](const std::string &s) {
+          if (!first) keystr += '\0';
+          first = false;
+          keystr += s;
+        };
+        if (!opt_.ex_service) part(service);
+        if (!opt_.ex_name) part(sname);
+        if (!opt_.ex_kind) part(kind >= 0 && kind < 6 ? kKindStr[kind] : "");
+        if (!opt_.ex_status) part(code >= 0 && code < 3 ? kStatusStr[code] : "");
+        for (const Dim &d : opt_.dims) {
+          const Any *v = find_attr(sattrs, d.name);
+          if (!v) v = find_attr(rattrs, d.name);
+          if (v) {
+            if (!as_string(*v, tmp)) return rollback(Result::kFallback, "dimension value not keyable natively");
+          } else if (d.has_default) {
+            tmp = d.def;
+          } else {
+            continue;  // A5: missing optional dimension, no separator
+          }
+          keystr += '\0';
+          keystr += tmp;
+        }
+        uint64_t sid;
+        auto kit = keys.find(keystr);
+        if (kit != keys.end()) {
+          sid = kit->second;
+        } else {
+          hbuf.resize(8 + keystr.size());
+          std::memcpy(hbuf.data(), &rhash, 8);
+          std::memcpy(hbuf.data() + 8, keystr.data(), keystr.size());
+          sid = xxh64(hbuf.data(), hbuf.size(), 0);
+          if (sid == 0) sid = xxh64(hbuf.data(), hbuf.size(), 1);
+          keys.emplace(keystr, sid);
+          added_keys.emplace_back(rhash, keystr);
+          res.new_series.push_back({sid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});
+        }
+        key_.push_back(sid);
+        start_.push_back(st);
+        end_.push_back(en);
+        if (en > max_end_) max_end_ = en;
+        if (tid && tid_len == 16) {
+          w0_.push_back(rd64(tid));
+          w1_.push_back(rd64(tid + 8));
+        } else {
+          w0_.push_back(0);
+          w1_.push_back(0);
+        }
+        const uint32_t kk = kind >= 0 && kind <= 7 ? (uint32_t)kind : 7u;
+        const uint32_t cc = code >= 0 && code <= 3 ? (uint32_t)code : 3u;
+        meta_.push_back(svc_id | (kk << 16) | (cc << 19));
+        ++res.spans;
+      }
+      if (!ss.ok) return rollback(Result::kError, "malformed ScopeSpans");
+    }
+    if (!scan.ok) return rollback(Result::kError, "malformed ResourceSpans");
+  }
+  if (!req.ok) return rollback(Result::kError, "malformed ExportTraceServiceRequest");
+  return res;
+}
+
+}  // namespace otlpcol

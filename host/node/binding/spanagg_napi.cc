@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "otlp_columnizer.h"
 #include "spanagg.h"
 
 namespace {
@@ -492,6 +493,276 @@ napi_value Stats(napi_env env, napi_callback_info info) {
     return o;
 }
 
+// ---- native OTLP columnizer (otlp_columnizer.h) ----------------------------
+//
+// createColumnizer(engine, {dims, exclude, rules, keyAttributes}) -> columnizer
+// columnize(c, Buffer) -> {status, error, spans, buffered, maxEnd, resources,
+//                          newResources, newSeries, newServices}
+// columnizerIngest(c)           sa_ingest of the buffered columns, then clear
+// columnizerTake(c)             the buffered columns as typed arrays, then clear
+// columnizerServiceId(c, name)  -> [id, isNew]
+// columnizerForget(c, resHash)  drop a resource's key cache (LRU eviction)
+
+struct ColHandle {
+  otlpcol::Columnizer col;
+  napi_ref engine_ref = nullptr;  // keeps the engine handle object alive
+  Handle *engine = nullptr;
+  explicit ColHandle(otlpcol::Options o) : col(std::move(o)) {}
+};
+
+void finalize_col(napi_env env, void *data, void *) {
+  auto *c = static_cast<ColHandle *>(data);
+  if (c->engine_ref) napi_delete_reference(env, c->engine_ref);
+  delete c;
+}
+
+ColHandle *get_col(napi_env env, napi_value v) {
+  void *p = nullptr;
+  napi_valuetype t;
+  if (napi_typeof(env, v, &t) != napi_ok || t != napi_object || napi_unwrap(env, v, &p) != napi_ok || !p) {
+    throw_type(env, "expected a columnizer");
+    return nullptr;
+  }
+  return static_cast<ColHandle *>(p);
+}
+
+bool get_string(napi_env env, napi_value v, std::string *out, const char *name) {
+  size_t n = 0;
+  if (napi_get_value_string_utf8(env, v, nullptr, 0, &n) != napi_ok) {
+    throw_type(env, std::string(name) + ": expected a string");
+    return false;
+  }
+  out->resize(n);
+  napi_get_value_string_utf8(env, v, &(*out)[0], n + 1, &n);
+  return true;
+}
+
+bool array_items(napi_env env, napi_value v, std::vector<napi_value> *out, const char *name) {
+  out->clear();
+  if (is_undefined(env, v)) return true;
+  bool is = false;
+  napi_is_array(env, v, &is);
+  if (!is) {
+    throw_type(env, std::string(name) + ": expected an array");
+    return false;
+  }
+  uint32_t n = 0;
+  napi_get_array_length(env, v, &n);
+  for (uint32_t i = 0; i < n; ++i) {
+    napi_value x;
+    napi_get_element(env, v, i, &x);
+    out->push_back(x);
+  }
+  return true;
+}
+
+napi_value CreateColumnizer(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
+  // engine: a handle from create(), or null for a columnizer that is only
+  // drained with columnizerTake (tests, non-GPU consumers)
+  void *hp = nullptr;
+  const bool no_engine = is_undefined(env, argv[0]);
+  if (!no_engine && (napi_unwrap(env, argv[0], &hp) != napi_ok || !hp))
+    return throw_type(env, "expected a spanagg engine handle or null");
+  otlpcol::Options o;
+  std::vector<napi_value> items;
+  if (!array_items(env, prop(env, argv[1], "dims"), &items, "dims")) return nullptr;
+  for (napi_value d : items) {
+    otlpcol::Dim dim;
+    if (!get_string(env, prop(env, d, "name"), &dim.name, "dims[].name")) return nullptr;
+    napi_value def = prop(env, d, "default");
+    if (!is_undefined(env, def)) {
+      dim.has_default = true;
+      if (!get_string(env, def, &dim.def, "dims[].default")) return nullptr;
+    }
+    o.dims.push_back(std::move(dim));
+  }
+  if (!array_items(env, prop(env, argv[1], "exclude"), &items, "exclude")) return nullptr;
+  for (napi_value x : items) {
+    std::string k;
+    if (!get_string(env, x, &k, "exclude[]")) return nullptr;
+    if (k == "service.name") o.ex_service = true;
+    else if (k == "span.name") o.ex_name = true;
+    else if (k == "span.kind") o.ex_kind = true;
+    else if (k == "status.code") o.ex_status = true;
+  }
+  if (!array_items(env, prop(env, argv[1], "rules"), &items, "rules")) return nullptr;
+  for (napi_value x : items) {
+    otlpcol::Rule r;
+    std::string kind;
+    if (!get_string(env, prop(env, x, "kind"), &kind, "rules[].kind")) return nullptr;
+    if (kind == "strip_query") {
+      r.kind = otlpcol::Rule::kStripQuery;
+    } else if (kind == "glob") {
+      r.kind = otlpcol::Rule::kGlob;
+      if (!get_string(env, prop(env, x, "pattern"), &r.pattern, "rules[].pattern") ||
+          !get_string(env, prop(env, x, "replacement"), &r.replacement, "rules[].replacement"))
+        return nullptr;
+      r.prepare();
+    } else {
+      return throw_status(env, SA_EINVAL, "rules[].kind must be strip_query or glob");
+    }
+    o.rules.push_back(std::move(r));
+  }
+  if (!array_items(env, prop(env, argv[1], "keyAttributes"), &items, "keyAttributes")) return nullptr;
+  for (napi_value x : items) {
+    std::string k;
+    if (!get_string(env, x, &k, "keyAttributes[]")) return nullptr;
+    o.key_attributes.push_back(std::move(k));
+  }
+  auto *c = new ColHandle(std::move(o));
+  c->engine = static_cast<Handle *>(hp);
+  napi_value obj;
+  if (napi_create_object(env, &obj) != napi_ok ||
+      (!no_engine && napi_create_reference(env, argv[0], 1, &c->engine_ref) != napi_ok) ||
+      napi_wrap(env, obj, c, finalize_col, nullptr, nullptr) != napi_ok) {
+    if (c->engine_ref) napi_delete_reference(env, c->engine_ref);
+    delete c;
+    return throw_napi(env, "createColumnizer");
+  }
+  return obj;
+}
+
+napi_value Columnize(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
+  ColHandle *c = get_col(env, argv[0]);
+  if (!c) return nullptr;
+  void *data;
+  size_t len;
+  if (!typed(env, argv[1], napi_uint8_array, &data, &len, "request")) return nullptr;
+  otlpcol::Result r = c->col.columnize(static_cast<const uint8_t *>(data), len);
+  napi_value o, arr, s;
+  if (napi_create_object(env, &o) != napi_ok) return throw_napi(env, "napi_create_object");
+  const char *st = r.status == otlpcol::Result::kOk ? "ok" : r.status == otlpcol::Result::kFallback ? "fallback" : "error";
+  napi_create_string_utf8(env, st, NAPI_AUTO_LENGTH, &s);
+  set(env, o, "status", s);
+  napi_create_string_utf8(env, r.error.c_str(), NAPI_AUTO_LENGTH, &s);
+  set(env, o, "error", s);
+  set(env, o, "spans", num(env, (double)r.spans));
+  set(env, o, "buffered", num(env, (double)c->col.buffered()));
+  set(env, o, "maxEnd", big(env, c->col.max_end()));
+  set(env, o, "resources", make_typed(env, napi_biguint64_array, 8, r.resources.data(), r.resources.size()));
+  napi_create_array_with_length(env, r.new_resources.size(), &arr);
+  for (size_t i = 0; i < r.new_resources.size(); ++i) {
+    napi_value e;
+    napi_create_object(env, &e);
+    set(env, e, "hash", big(env, r.new_resources[i].hash));
+    set(env, e, "off", num(env, (double)r.new_resources[i].off));
+    set(env, e, "len", num(env, r.new_resources[i].len));
+    napi_set_element(env, arr, (uint32_t)i, e);
+  }
+  set(env, o, "newResources", arr);
+  napi_create_array_with_length(env, r.new_series.size(), &arr);
+  for (size_t i = 0; i < r.new_series.size(); ++i) {
+    napi_value e;
+    napi_create_object(env, &e);
+    set(env, e, "sid", big(env, r.new_series[i].sid));
+    set(env, e, "resHash", big(env, r.new_series[i].res_hash));
+    set(env, e, "off", num(env, r.new_series[i].span_off));
+    set(env, e, "len", num(env, r.new_series[i].span_len));
+    napi_set_element(env, arr, (uint32_t)i, e);
+  }
+  set(env, o, "newSeries", arr);
+  napi_create_array_with_length(env, r.new_services.size(), &arr);
+  for (size_t i = 0; i < r.new_services.size(); ++i) {
+    napi_value e, nm;
+    napi_create_array_with_length(env, 2, &e);
+    napi_create_string_utf8(env, r.new_services[i].first.c_str(), r.new_services[i].first.size(), &nm);
+    napi_set_element(env, e, 0, nm);
+    napi_set_element(env, e, 1, num(env, r.new_services[i].second));
+    napi_set_element(env, arr, (uint32_t)i, e);
+  }
+  set(env, o, "newServices", arr);
+  return o;
+}
+
+napi_value ColumnizerIngest(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
+  ColHandle *c = get_col(env, argv[0]);
+  if (!c) return nullptr;
+  if (!c->engine || !c->engine->e) return throw_status(env, SA_ESTATE, "the columnizer has no live engine");
+  const size_t n = c->col.buffered();
+  if (n) {
+    sa_span_batch b{c->col.key(), c->col.start(), c->col.end(), c->col.w0(), c->col.w1(), c->col.meta(), n};
+    const int rc = sa_ingest(c->engine->e, &b);
+    if (rc != SA_OK) return engine_error(env, c->engine, rc, "sa_ingest");
+  }
+  c->col.clear_buffer();
+  return num(env, (double)n);
+}
+
+// columnizerTake(c) -> the buffered SoA columns (copies), then clear
+napi_value ColumnizerTake(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
+  ColHandle *c = get_col(env, argv[0]);
+  if (!c) return nullptr;
+  const size_t n = c->col.buffered();
+  napi_value o;
+  napi_create_object(env, &o);
+  set(env, o, "keyHash", make_typed(env, napi_biguint64_array, 8, c->col.key(), n));
+  set(env, o, "startNs", make_typed(env, napi_biguint64_array, 8, c->col.start(), n));
+  set(env, o, "endNs", make_typed(env, napi_biguint64_array, 8, c->col.end(), n));
+  set(env, o, "traceW0", make_typed(env, napi_biguint64_array, 8, c->col.w0(), n));
+  set(env, o, "traceW1", make_typed(env, napi_biguint64_array, 8, c->col.w1(), n));
+  set(env, o, "meta", make_typed(env, napi_uint32_array, 4, c->col.meta(), n));
+  c->col.clear_buffer();
+  return o;
+}
+
+napi_value ColumnizerServiceId(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
+  ColHandle *c = get_col(env, argv[0]);
+  std::string name;
+  if (!c || !get_string(env, argv[1], &name, "name")) return nullptr;
+  bool is_new = false;
+  const uint32_t id = c->col.service_id(name, &is_new);
+  napi_value arr, b;
+  napi_create_array_with_length(env, 2, &arr);
+  napi_set_element(env, arr, 0, num(env, id));
+  napi_get_boolean(env, is_new, &b);
+  napi_set_element(env, arr, 1, b);
+  return arr;
+}
+
+napi_value ColumnizerForget(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
+  ColHandle *c = get_col(env, argv[0]);
+  uint64_t h;
+  if (!c || !to_u64(env, argv[1], &h, "resHash")) return nullptr;
+  c->col.forget_resource(h);
+  return nullptr;
+}
+
+// building blocks, for tests: {xxh64(hex, seed) -> BigInt, formatFloat(x), applyRules(rules, name)}
+napi_value ColumnizerSelfTest(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return throw_napi(env, "args");
+  std::string what;
+  if (!get_string(env, argv[0], &what, "what")) return nullptr;
+  if (what == "xxh64") {
+    void *d;
+    size_t n;
+    uint64_t seed;
+    if (!typed(env, argv[1], napi_uint8_array, &d, &n, "data") || !to_u64(env, argv[2], &seed, "seed")) return nullptr;
+    return big(env, otlpcol::xxh64(d, n, seed));
+  }
+  if (what == "formatFloat") {
+    double x;
+    if (napi_get_value_double(env, argv[1], &x) != napi_ok) return throw_type(env, "x: expected a number");
+    const std::string s = otlpcol::format_float(x);
+    napi_value out;
+    napi_create_string_utf8(env, s.c_str(), s.size(), &out);
+    return out;
+  }
+  return throw_status(env, SA_EINVAL, "unknown self-test");
+}
+
 napi_value Init(napi_env env, napi_value exports) {
     struct Fn {
         const char *name;
@@ -508,7 +779,14 @@ napi_value Init(napi_env env, napi_value exports) {
                {"flush", Flush},
                {"windowRead", WindowRead},
                {"windowAdvance", WindowAdvance},
-               {"stats", Stats}};
+               {"stats", Stats},
+               {"createColumnizer", CreateColumnizer},
+               {"columnize", Columnize},
+               {"columnizerIngest", ColumnizerIngest},
+               {"columnizerTake", ColumnizerTake},
+               {"columnizerServiceId", ColumnizerServiceId},
+               {"columnizerForget", ColumnizerForget},
+               {"columnizerSelfTest", ColumnizerSelfTest}};
     for (auto &f : fns) {
         napi_value v;
         if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &v) != napi_ok ||

@@ -28,6 +28,7 @@
 const addonLoader = require('./addon');
 const keys = require('./keys');
 const otlp = require('./otlp');
+const { applyRules } = require('./transform');
 
 const M64 = (1n << 64n) - 1n;
 const CMS_SEED = [0x9E3779B97F4A7C15n, 0xBF58476D1CE4E5B9n, 0x94D049BB133111EBn,
@@ -144,11 +145,14 @@ class Columns {
 class SpanMetricsConnector {
   /**
    * @param cfg spanmetrics YAML-shaped config (see normalizeConfig)
-   * @param opts {addon, clock: () => BigInt ns, metricsConsumer: (req) => void}
+   * @param opts {addon, clock: () => BigInt ns, metricsConsumer: (req) => void,
+   *              rules: span-name rules applied before keying (transform.js),
+   *              native: false to force the JavaScript columnizer}
    */
   constructor(cfg = {}, opts = {}) {
     this.addon = opts.addon || addonLoader.load();
     this.cfg = normalizeConfig(cfg, this.addon);
+    this.rules = opts.rules || [];
     this.clock = opts.clock || (() => BigInt(Date.now()) * 1000000n);
     this.metricsConsumer = opts.metricsConsumer || null;
     const c = this.cfg;
@@ -156,6 +160,19 @@ class SpanMetricsConnector {
       cmsW: c.cmsW, windowNs: c.windowNs, nWindows: c.nWindows, nServices: c.nServices,
       keyCapacity: c.keyCapacity, device: c.device });
     this.cols = new Columns(c.batchSize);
+    // native OTLP columnizer (binding/otlp_columnizer.cc) for request bytes, when
+    // every enabled option is one it implements; otherwise the JS path below
+    this.col = null;
+    this.nativeMaxEnd = 0n;
+    this.nativeBuffered = 0;
+    this.nativeRequests = 0;
+    this.jsRequests = 0;
+    if (opts.native !== false && typeof this.addon.createColumnizer === 'function' &&
+        !c.events && !c.exemplars && !c.cardinalityLimit && this.rules.every((r) => r.native)) {
+      this.col = this.addon.createColumnizer(this.handle, { dims: c.dims,
+        exclude: [...c.exclude], rules: this.rules.map((r) => r.native),
+        keyAttributes: c.resourceKeyAttributes });
+    }
     this.resources = new Map();   // resHash -> resource record (LRU order: oldest first)
     this.evicted = new Map();     // evicted this flush interval, revivable until export
     this.series = new Map();      // sid -> series record
@@ -194,7 +211,9 @@ class SpanMetricsConnector {
   _serviceId(name) {
     let id = this.services.get(name);
     if (id === undefined) {
-      id = Math.min(this.services.size, 0xFFFE);  // 0xFFFF: event records (no sketch)
+      // one numbering for both columnizers: the native one owns it when present
+      id = this.col ? this.addon.columnizerServiceId(this.col, name)[0]
+        : Math.min(this.services.size, 0xFFFE);  // 0xFFFF: event records (no sketch)
       this.services.set(name, id);
     }
     return id;
@@ -209,6 +228,13 @@ class SpanMetricsConnector {
       for (const k of keyAttrs) if (resAttrs.has(k)) hashAttrs.set(k, resAttrs.get(k));
     }
     const h = keys.resourceHash(hashAttrs);
+    return this._touchResource(h) ||
+      this._admitResource({ hash: h, attributes: resAttrs, startTs: this.clock(), byKey: new Map(),
+        sids: [], nSpanSeries: 0 });
+  }
+
+  /** LRU hit (or revival from the evicted side map) by resource hash; undefined on a miss. */
+  _touchResource(h) {
     let r = this.resources.get(h);
     if (r !== undefined) {
       this.resources.delete(h);  // refresh LRU position
@@ -216,13 +242,18 @@ class SpanMetricsConnector {
       return r;
     }
     r = this.evicted.get(h);
-    if (r !== undefined) this.evicted.delete(h);
-    else r = { hash: h, attributes: resAttrs, startTs: this.clock(), byKey: new Map(), sids: [], nSpanSeries: 0 };
-    this.resources.set(h, r);
+    if (r === undefined) return undefined;
+    this.evicted.delete(h);
+    return this._admitResource(r);
+  }
+
+  _admitResource(r) {
+    this.resources.set(r.hash, r);
     if (this.resources.size > this.cfg.resourceCacheSize) {
       const [oldest, rec] = this.resources.entries().next().value;
       this.resources.delete(oldest);
       this.evicted.set(oldest, rec);
+      if (this.col) this.addon.columnizerForget(this.col, oldest);
     }
     return r;
   }
@@ -283,10 +314,23 @@ class SpanMetricsConnector {
           new Set([keys.SERVICE_NAME_KEY, 'span.name', 'span.kind', 'status.code']))));
   }
 
-  /** ConsumeTraces: ExportTraceServiceRequest bytes or a decoded request (otlp.js shape). */
+  /**
+   * ConsumeTraces: ExportTraceServiceRequest bytes or a decoded request
+   * (otlp.js shape).  The span-name rules are applied first (a decoded
+   * request's names are rewritten in place).
+   */
   consumeTraces(req) {
     if (!this.handle) throw new Error('connector is shut down');
-    if (Buffer.isBuffer(req) || req instanceof Uint8Array) req = otlp.decodeTraces(req);
+    const isBytes = Buffer.isBuffer(req) || req instanceof Uint8Array;
+    if (isBytes && this.col && this._consumeNative(Buffer.isBuffer(req) ? req
+      : Buffer.from(req.buffer, req.byteOffset, req.byteLength))) return;
+    if (isBytes) req = otlp.decodeTraces(req);
+    this.jsRequests += 1;
+    if (this.rules.length) {
+      for (const rs of req.resourceSpans || []) {
+        for (const ss of rs.scopeSpans || []) for (const sp of ss.spans || []) sp.name = applyRules(sp.name, this.rules);
+      }
+    }
     const cols = this.cols;
     for (const rs of req.resourceSpans || []) {
       const resAttrs = keys.attrMap(rs.resource && rs.resource.attributes);
@@ -326,6 +370,44 @@ class SpanMetricsConnector {
     }
   }
 
+  /**
+   * Native path: the addon columnises the request into its own buffer and
+   * reports what is new (services, resources, series); the host decodes only
+   * those messages to keep its dictionary, and checks that it derives the same
+   * ids.  Returns false when the request needs the JavaScript path.
+   */
+  _consumeNative(bytes) {
+    const r = this.addon.columnize(this.col, bytes);
+    if (r.status === 'fallback') return false;
+    if (r.status !== 'ok') throw new Error(`OTLP request: ${r.error}`);
+    this.nativeRequests += 1;
+    for (const [name, id] of r.newServices) this.services.set(name, id);
+    for (const nr of r.newResources) {
+      if (this._touchResource(nr.hash)) continue;  // known to the host, forgotten natively
+      const attrs = nr.off >= 0 ? otlp.decodeResource(new otlp.Reader(bytes, nr.off, nr.off + nr.len)).attributes : [];
+      const res = this._resource(keys.attrMap(attrs));
+      if (res.hash !== nr.hash) throw new Error('native/JS resource hash mismatch');
+    }
+    for (const h of r.resources) this._touchResource(h);
+    for (const ns of r.newSeries) {
+      const res = this.resources.get(ns.resHash) || this.evicted.get(ns.resHash);
+      if (!res) throw new Error('native series for an unknown resource');
+      const span = otlp.decodeSpan(new otlp.Reader(bytes, ns.off, ns.off + ns.len));
+      span.name = applyRules(span.name, this.rules);
+      const svc = res.attributes.get(keys.SERVICE_NAME_KEY);
+      const service = svc && svc.type === 'string' ? svc.value : '';
+      const spanAttrs = this.cfg.dims.length ? keys.attrMap(span.attributes) : undefined;
+      const sid = this._seriesId(res, service, span, res.attributes, spanAttrs);
+      if (sid !== ns.sid) throw new Error('native/JS series id mismatch');
+    }
+    if (r.spans) {
+      if (r.maxEnd > this.nativeMaxEnd) this.nativeMaxEnd = r.maxEnd;
+      this.nativeBuffered = r.buffered;
+      if (r.buffered >= this.cols.cap) this._drain();
+    }
+    return true;
+  }
+
   /** exemplars.enabled: the first max_per_data_point spans of each series per export. */
   _exemplar(sid, span) {
     const s = this.series.get(sid);
@@ -354,8 +436,8 @@ class SpanMetricsConnector {
   /** Hand the buffered columns to the engine, advancing the window ring first. */
   _drain() {
     const cols = this.cols;
-    if (cols.n === 0) return;
-    let maxEnd = 0n;
+    if (cols.n === 0 && this.nativeBuffered === 0) return;
+    let maxEnd = this.nativeBuffered ? this.nativeMaxEnd : 0n;
     for (let i = 0; i < cols.n; i++) if (cols.endNs[i] > maxEnd) maxEnd = cols.endNs[i];
     const maxWid = maxEnd / this.cfg.windowNs;
     const nw = BigInt(this.cfg.nWindows);
@@ -377,8 +459,11 @@ class SpanMetricsConnector {
       this.windowBase = base;
     }
     if (maxWid > this.maxWindowSeen) this.maxWindowSeen = maxWid;
-    this.addon.ingest(this.handle, cols.view());
+    if (cols.n) this.addon.ingest(this.handle, cols.view());
     cols.n = 0;
+    if (this.nativeBuffered) this.addon.columnizerIngest(this.col);
+    this.nativeBuffered = 0;
+    this.nativeMaxEnd = 0n;
   }
 
   // ------------------------------------------------------------ export
@@ -535,7 +620,7 @@ class SpanMetricsConnector {
     const s = this.addon.stats(this.handle);
     return Object.assign(s, { resources: this.resources.size, series: this.series.size,
       services: this.services.size, droppedFlushes: this.droppedFlushes,
-      eventRecords: this.eventRecords });
+      eventRecords: this.eventRecords, nativeRequests: this.nativeRequests, jsRequests: this.jsRequests });
   }
 }
 

@@ -557,6 +557,6 @@ function decodeMetrics(buf) {
   return req;
 }
 
-module.exports = { Reader, Writer, decodeAnyValue, decodeKeyValue, decodeSpan, decodeTraces,
+module.exports = { Reader, Writer, decodeAnyValue, decodeKeyValue, decodeSpan, decodeResource, decodeTraces,
   encodeAnyValue, encodeKeyValue, encodeSpan, encodeTraces, encodeMetrics, decodeMetrics,
   AGGREGATION_TEMPORALITY };

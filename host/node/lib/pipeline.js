@@ -12,7 +12,7 @@
  * traces pipeline (Jaeger, debug) are outside this path.
  */
 const otlp = require('./otlp');
-const { applyRules, DEMO_SPAN_NAME_RULES } = require('./transform');
+const { DEMO_SPAN_NAME_RULES } = require('./transform');
 const { SpanMetricsConnector } = require('./connector');
 const { OtlpReceiver, OtlpHttpExporter, MemoryLimiter } = require('./receiver');
 
@@ -31,7 +31,7 @@ class TracesToMetricsPipeline {
       : new MemoryLimiter(Object.assign({ limit_percentage: 80, spike_limit_percentage: 25 }, opts.memoryLimiter));
     this.exporter = opts.exporter ? new OtlpHttpExporter(opts.exporter) : null;
     this.connector = new SpanMetricsConnector(opts.spanmetrics || {}, { addon: opts.addon, clock: opts.clock,
-      metricsConsumer: (req) => this._export(req) });
+      rules: this.rules, native: opts.native, metricsConsumer: (req) => this._export(req) });
     this.receiver = opts.receiver === false ? null
       : new OtlpReceiver(Object.assign({}, opts.receiver, { onTraces: (b) => this.consumeTraces(b) }));
     this.exportErrors = 0;
@@ -44,16 +44,10 @@ class TracesToMetricsPipeline {
     return this;
   }
 
-  /** memory_limiter -> decode -> transform -> spanmetrics. */
+  /** memory_limiter -> (decode, transform, columnise: inside the connector) -> spanmetrics. */
   consumeTraces(bytes) {
     if (this.limiter) this.limiter.check();
-    const req = Buffer.isBuffer(bytes) || bytes instanceof Uint8Array ? otlp.decodeTraces(bytes) : bytes;
-    if (this.rules.length) {
-      for (const rs of req.resourceSpans || []) {
-        for (const ss of rs.scopeSpans || []) for (const s of ss.spans || []) s.name = applyRules(s.name, this.rules);
-      }
-    }
-    this.connector.consumeTraces(req);
+    this.connector.consumeTraces(bytes);
   }
 
   _export(req) {

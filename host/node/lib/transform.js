@@ -19,17 +19,28 @@ function globToRegExp(glob) {
     else if (ch === '?') re += '[\\s\\S]';
     else re += ch.replace(/[.*+?^${}()|[\]\\/]/g, '\\$&');
   }
-  return new RegExp(re + '$');
+  return new RegExp(re + '$', 'u');  // `?` matches one code point, as in Go
 }
 
+/**
+ * replace_pattern(name, pattern, replacement): JS RegExp semantics, except
+ * the demo's `\?.*`, which is given Go's meaning (`.` stops only at '\n').
+ * Rules with a `.native` descriptor also run in the native columnizer.
+ */
 function replacePattern(pattern, replacement) {
-  const re = new RegExp(pattern, 'g');
-  return (name) => name.replace(re, replacement);
+  const goStrip = pattern === '\\?.*' && replacement === '';
+  const re = goStrip ? /\?[^\n]*/g : new RegExp(pattern, 'g');
+  const rule = (name) => name.replace(re, replacement);
+  if (goStrip) rule.native = { kind: 'strip_query' };
+  return rule;
 }
 
+/** replace_match(name, glob, replacement): whole-value glob with `*` and `?`. */
 function replaceMatch(glob, replacement) {
   const re = globToRegExp(glob);
-  return (name) => (re.test(name) ? replacement : name);
+  const rule = (name) => (re.test(name) ? replacement : name);
+  if (!/[[\]{}\\]/.test(glob)) rule.native = { kind: 'glob', pattern: glob, replacement };
+  return rule;
 }
 
 /** The two statements of otelcol-config.yml:111-113, in order. */

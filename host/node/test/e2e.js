@@ -14,7 +14,7 @@ const path = require('path');
 const lib = path.join(__dirname, '..', 'lib');
 const addonLoader = require(path.join(lib, 'addon'));
 const otlp = require(path.join(lib, 'otlp'));
-const { applyRules, DEMO_SPAN_NAME_RULES } = require(path.join(lib, 'transform'));
+const { DEMO_SPAN_NAME_RULES } = require(path.join(lib, 'transform'));
 const { SpanMetricsConnector } = require(path.join(lib, 'connector'));
 
 const b64 = (ta) => Buffer.from(ta.buffer, ta.byteOffset, ta.byteLength).toString('base64');
@@ -36,15 +36,16 @@ function main(cmd) {
     return r;
   };
   let t = 1700000000000000000n;
-  const conn = new SpanMetricsConnector(cmd.config || {}, { addon, clock: () => (t += 1000000000n) });
+  // native: request bytes through the addon's columnizer (sa_ingest from C++);
+  // otherwise decoded in JavaScript and ingested through addon.ingest (captured)
+  const native = cmd.native !== false;
+  const conn = new SpanMetricsConnector(cmd.config || {}, { addon, clock: () => (t += 1000000000n),
+    rules: DEMO_SPAN_NAME_RULES, native });
   const metrics = [];
   const exportsAfter = new Set(cmd.exports_after || []);
   cmd.requests.forEach((r, i) => {
-    const req = otlp.decodeTraces(Buffer.from(r, 'base64'));
-    for (const rs of req.resourceSpans) {
-      for (const ss of rs.scopeSpans) for (const s of ss.spans) s.name = applyRules(s.name, DEMO_SPAN_NAME_RULES);
-    }
-    conn.consumeTraces(req);
+    const bytes = Buffer.from(r, 'base64');
+    conn.consumeTraces(native ? bytes : otlp.decodeTraces(bytes));
     if (exportsAfter.has(i)) metrics.push(otlp.encodeMetrics(conn.exportMetrics()).toString('base64'));
   });
   metrics.push(otlp.encodeMetrics(conn.exportMetrics()).toString('base64'));
@@ -65,6 +66,7 @@ function main(cmd) {
     columns[k] = b64(out);
   }
   const st = conn.stats();
+  if (native !== (st.nativeRequests > 0) || (native && st.jsRequests)) throw new Error('wrong columnizer path');
   const stats = {};
   for (const [k, v] of Object.entries(st)) stats[k] = typeof v === 'bigint' ? v.toString() : v;
   const services = Object.fromEntries(conn.services);

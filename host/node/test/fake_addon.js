@@ -125,4 +125,25 @@ class FakeAddon {
   stats() { return { spans: 0n }; }
 }
 
-module.exports = { FakeAddon };
+/**
+ * FakeAddon plus the REAL native columnizer of build/spanagg.node (it needs no
+ * GPU): requests are columnised natively and the columns handed to the fake
+ * engine, so native and JavaScript columnising can be compared on CPU.
+ */
+class NativeColumnizerFakeAddon extends FakeAddon {
+  constructor() {
+    super();
+    this.real = require('../lib/addon').load();
+  }
+  createColumnizer(h, opts) { return this.real.createColumnizer(null, opts); }
+  columnize(c, bytes) { return this.real.columnize(c, bytes); }
+  columnizerServiceId(c, name) { return this.real.columnizerServiceId(c, name); }
+  columnizerForget(c, h) { return this.real.columnizerForget(c, h); }
+  columnizerIngest(c) {
+    const b = this.real.columnizerTake(c);
+    this.ingest(null, b);
+    return b.keyHash.length;
+  }
+}
+
+module.exports = { FakeAddon, NativeColumnizerFakeAddon };

@@ -1,0 +1,80 @@
+'use strict';
+/**
+ * Host-side rate of the Node path on one core: OTLP/protobuf request bytes ->
+ * decode -> transform rules -> keying -> SoA columns -> addon.ingest.
+ * SURVEY.md 8(d) asks for the OTLP decode+aggregate rate from protobuf bytes.
+ *
+ *   node test/host_rate.js [spans] [--gpu]
+ *
+ * Without --gpu the addon's ingest is a no-op stub (host work only); with
+ * --gpu the real addon ingests (host memory -> HBM -> kernel) and the result
+ * is checked for span count.  Prints one JSON line.
+ */
+const path = require('path');
+const lib = path.join(__dirname, '..', 'lib');
+const otlp = require(path.join(lib, 'otlp'));
+const { TracesToMetricsPipeline } = require(path.join(lib, 'pipeline'));
+const { NativeColumnizerFakeAddon } = require('./fake_addon');
+
+const n = parseInt(process.argv[2] || '200000', 10);
+const gpu = process.argv.includes('--gpu');
+const jsOnly = process.argv.includes('--js');  // force the JavaScript columnizer
+const PER_REQUEST = 512;  // an SDK batch span processor's default export batch
+const SERVICES = 20, NAMES = 25;
+
+function makeRequests() {
+  let seed = 42;
+  const rnd = () => { seed = (seed * 1103515245 + 12345) >>> 0; return seed / 4294967296; };
+  const reqs = [];
+  const T0 = 1700000000000000000n;
+  for (let done = 0; done < n; done += PER_REQUEST) {
+    const svc = Math.floor(rnd() * SERVICES);
+    const spans = [];
+    for (let i = 0; i < Math.min(PER_REQUEST, n - done); i++) {
+      const name = Math.floor(rnd() * NAMES);
+      const start = T0 + BigInt(Math.floor(rnd() * 6e10));
+      const tid = new Uint8Array(16);
+      for (let k = 0; k < 16; k++) tid[k] = Math.floor(rnd() * 256);
+      spans.push({ traceId: tid, spanId: tid.subarray(0, 8), name: name % 5 === 0 ? `GET /api/products/${name}?x=1` : `op-${name}`,
+        kind: 2, startTimeUnixNano: start, endTimeUnixNano: start + BigInt(Math.floor(rnd() * 2e7)),
+        attributes: [{ key: 'http.method', value: { type: 'string', value: 'GET' } }],
+        status: { code: rnd() < 0.02 ? 2 : 0, message: '' } });
+    }
+    reqs.push(otlp.encodeTraces({ resourceSpans: [{ resource: { attributes: [
+      { key: 'service.name', value: { type: 'string', value: `svc-${svc}` } },
+      { key: 'telemetry.sdk.language', value: { type: 'string', value: 'go' } }] },
+      scopeSpans: [{ scope: { name: 'bench' }, spans }] }] }));
+  }
+  return reqs;
+}
+
+const reqs = makeRequests();
+const bytes = reqs.reduce((a, b) => a + b.length, 0);
+let addon;
+if (gpu) {
+  addon = require(path.join(lib, 'addon')).load();
+} else {
+  addon = new NativeColumnizerFakeAddon();  // the real columnizer, no engine
+  addon.ingest = () => {};                  // host work only
+  addon.columnizerIngest = (c) => addon.real.columnizerTake(c).keyHash.length;
+}
+const p = new TracesToMetricsPipeline({ addon, receiver: false, exporter: false, memoryLimiter: false,
+  native: !jsOnly, spanmetrics: { n_services: 64 } });
+// warm-up on a tenth of the requests (JIT), then time the whole set
+for (const r of reqs.slice(0, Math.max(1, reqs.length / 10))) p.consumeTraces(r);
+p.connector.exportMetrics();
+const t0 = process.hrtime.bigint();
+for (const r of reqs) p.consumeTraces(r);
+p.connector._drain();
+if (gpu) addon.sync(p.connector.handle);
+const secs = Number(process.hrtime.bigint() - t0) / 1e9;
+const out = p.connector.exportMetrics();
+let calls = 0n;
+for (const rm of out.resourceMetrics) for (const dp of rm.scopeMetrics[0].metrics[0].sum.dataPoints) calls += dp.asInt;
+const native = p.connector.stats().nativeRequests > 0;
+p.shutdown();
+console.log(JSON.stringify({ spans: n, requests: reqs.length, otlp_bytes: bytes, seconds: secs,
+  spans_per_s: n / secs, mb_per_s: bytes / secs / 1e6, cores: 1, gpu,
+  columnizer: native ? 'native (binding/otlp_columnizer.cc)' : 'javascript',
+  calls_check: gpu ? calls === BigInt(n) : null,
+  path: 'OTLP protobuf decode + transform + keying + SoA columnize' + (gpu ? ' + sa_ingest (H2D + kernel)' : ' (engine ingest stubbed)') }));

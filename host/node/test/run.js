@@ -344,6 +344,107 @@ test('connector: exemplars carry trace/span ids and the duration, one export int
   assert.strictEqual(h.exemplars, undefined);
 });
 
+// ------------------------------------------------- native columnizer vs JavaScript
+
+const { NativeColumnizerFakeAddon } = require('./fake_addon');
+
+function mixedRequests() {
+  const tid = (k) => Uint8Array.from({ length: 16 }, (_, i) => (i * 7 + k) & 255);
+  const W = 10000000000n;
+  const base = 170000000n * W;
+  let k = 0;
+  const sp = (name, o = {}) => span(name, Object.assign({ traceId: tid(++k),
+    startTimeUnixNano: base + BigInt(k) * 1000003n, endTimeUnixNano: base + BigInt(k) * 1000003n + BigInt(k * 7919 % 50) * 1000000n }, o));
+  const reqs = [];
+  for (let r = 0; r < 6; r++) {
+    reqs.push(request([
+      [{ 'service.name': 'frontend', 'k8s.pod.name': `fe-${r % 2}`, 'pid': { type: 'int', value: BigInt(100 + (r % 3)) },
+        'ratio': { type: 'double', value: 0.25 }, 'args': { type: 'array', value: [str('node'), { type: 'int', value: 2n }] } }, [
+        sp('GET /api/products/0PUK6V6EV0?currencyCode=USD'), sp('GET /api/products/'),
+        sp('GET /api/cart?x=1\nsecond?y'), sp('ΣΠΑΝ 😀', { kind: 9, status: { code: 7 } }),
+        sp('checkout', { status: { code: 2 }, kind: -1, traceId: new Uint8Array(3),
+          attributes: [{ key: 'http.status_code', value: { type: 'int', value: 500n } }] }),
+        sp('checkout', { attributes: [{ key: 'http.status_code', value: str('500') },
+          { key: 'region', value: { type: 'kvlist', value: [{ key: 'a', value: { type: 'double', value: 1e21 } }] } }] }),
+        sp('bytes', { attributes: [{ key: 'http.status_code', value: { type: 'bytes', value: Uint8Array.from([0, 255, 7]) } }] }),
+        sp('dbl', { attributes: [{ key: 'http.status_code', value: { type: 'double', value: 1.5e-7 } }] }),
+      ]],
+      [{ 'host.name': 'no-service' }, [sp('skipped')]],
+      [{ 'service.name': { type: 'int', value: 5n } }, [sp('non-string service')]],
+      [{ 'service.name': 'cart', 'service.name ': 'x' }, [sp('op-' + r), sp('op-' + r, { kind: 3 })]],
+    ]));
+  }
+  return reqs;
+}
+
+function runBoth(cfg, rules, reqs) {
+  const out = [];
+  for (const native of [true, false]) {
+    const addon = native ? new NativeColumnizerFakeAddon() : new FakeAddon();
+    const t = { now: 1000n };
+    const conn = new SpanMetricsConnector(Object.assign({ batch_size: 16 }, cfg),
+      { addon, rules, native, clock: () => (t.now += 1n) });
+    const exports = [];
+    reqs.forEach((r, i) => {
+      conn.consumeTraces(otlp.encodeTraces(r));
+      if (i % 2 === 1) exports.push(otlp.encodeMetrics(conn.exportMetrics()).toString('hex'));
+    });
+    exports.push(otlp.encodeMetrics(conn.exportMetrics()).toString('hex'));
+    const cols = {};
+    for (const c of ['keyHash', 'startNs', 'endNs', 'traceW0', 'traceW1', 'meta']) {
+      cols[c] = addon.batches.flatMap((b) => Array.from(b[c]));
+    }
+    out.push({ exports, cols, stats: conn.stats(), services: [...conn.services] });
+  }
+  return out;
+}
+
+test('native columnizer: same columns and same OTLP metrics as the JavaScript path', () => {
+  const reqs = mixedRequests();
+  for (const [cfg, rules] of [
+    [{}, DEMO_SPAN_NAME_RULES],
+    [{ dimensions: [{ name: 'http.status_code' }, { name: 'region', default: 'eu' }, { name: 'k8s.pod.name' },
+      { name: 'args' }, { name: 'ratio' }] }, DEMO_SPAN_NAME_RULES],
+    [{ exclude_dimensions: ['span.kind', 'status.code'], resource_metrics_key_attributes: ['service.name'] }, []],
+    [{ resource_metrics_cache_size: 1, aggregation_temporality: 'AGGREGATION_TEMPORALITY_DELTA' }, DEMO_SPAN_NAME_RULES],
+  ]) {
+    const [nat, js] = runBoth(cfg, rules, reqs);
+    assert.ok(nat.stats.nativeRequests > 0 && nat.stats.jsRequests === 0, JSON.stringify(cfg));
+    assert.strictEqual(js.stats.nativeRequests, 0);
+    assert.deepStrictEqual(nat.cols, js.cols, JSON.stringify(cfg));
+    assert.deepStrictEqual(nat.exports, js.exports, JSON.stringify(cfg));
+    assert.deepStrictEqual(nat.services, js.services);
+  }
+});
+
+test('native columnizer: invalid UTF-8 falls back to JavaScript; malformed bytes are rejected', () => {
+  const addon = new NativeColumnizerFakeAddon();
+  const conn = new SpanMetricsConnector({}, { addon, rules: DEMO_SPAN_NAME_RULES });
+  const body = otlp.encodeTraces(request([[{ 'service.name': 'a' }, [span('GET /x\u00e9')]]]));
+  const bad = Buffer.from(body);
+  bad[bad.indexOf(0xC3)] = 0xFF;  // break the UTF-8 of the span name
+  conn.consumeTraces(bad);
+  assert.strictEqual(conn.stats().jsRequests, 1);
+  conn.consumeTraces(body);
+  assert.strictEqual(conn.stats().nativeRequests, 1);
+  assert.throws(() => conn.consumeTraces(body.subarray(0, body.length - 2)), /OTLP request|truncated/);
+  const c = dpsOf(conn.exportMetrics(), 'traces.span.metrics.calls');
+  assert.strictEqual(c.length, 2);
+});
+
+test('native building blocks: xxh64 and Go FormatFloat agree with the JavaScript ones', () => {
+  const real = require('../lib/addon').load();
+  const { xxh64 } = require(path.join(lib, 'xxh64'));
+  for (let n = 0; n < 80; n++) {
+    const b = Uint8Array.from({ length: n }, (_, i) => (i * 31 + n) & 255);
+    assert.strictEqual(real.columnizerSelfTest('xxh64', b, 0n), xxh64(Buffer.from(b), 0n));
+    assert.strictEqual(real.columnizerSelfTest('xxh64', b, 1n), xxh64(Buffer.from(b), 1n));
+  }
+  const xs = [0, -0, 1, -1, 0.1, 1 / 3, 1e21, 1e-7, 1.5e-7, 123456789.125, 2 ** 53, 5e-324, 1.7976931348623157e308,
+    NaN, Infinity, -Infinity, 1e22, 123e-20, 0.000001, 1e-6];
+  for (const x of xs) assert.strictEqual(real.columnizerSelfTest('formatFloat', x), keys.formatFloat(x), String(x));
+});
+
 // ------------------------------------------------- receiver / exporter / pipeline
 const http = require('http');
 const http2 = require('http2');

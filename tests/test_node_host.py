@@ -330,36 +330,38 @@ def synth_requests(seed, n_requests=12, per_request=2500):
 
 
 @pytest.mark.gpu
-def test_node_host_end_to_end_matches_oracle():
+@pytest.mark.parametrize("native", [True, False], ids=["native-columnizer", "js-columnizer"])
+def test_node_host_end_to_end_matches_oracle(native):
     import pyoracle
     from spanagg.engine import SpanBatch
 
     requests, facts = synth_requests(seed=11)
     env = dict(os.environ, SPANAGG_NODE_GPU="1")
     out = node("e2e.js", {"requests": requests, "config": {"batch_size": 4096, "key_capacity": 4096},
-                          "exports_after": [3, 7]}, timeout=300, env=env)
-
-    cols = {k: np.frombuffer(base64.b64decode(v), dtype=np.uint32 if k == "meta" else np.uint64)
-            for k, v in out["columns"].items()}
+                          "exports_after": [3, 7], "native": native}, timeout=300, env=env)
     n = len(facts)
-    assert len(cols["keyHash"]) == n
 
-    # 1. the columns are exactly what independent Python code derives from the spans
+    # 1. the SoA v1 columns independent Python code derives from the spans
     svc_ids = out["services"]
-    exp_key = np.array([pykeys.series_hash(pykeys.resource_hash(ra), pykeys.build_key(
-        ra["service.name"], nm, k, st)) for ra, nm, k, st, *_ in facts], dtype=np.uint64)
-    assert np.array_equal(cols["keyHash"], exp_key)
-    assert np.array_equal(cols["startNs"], np.array([f[4] for f in facts], dtype=np.uint64))
-    assert np.array_equal(cols["endNs"], np.array([f[5] for f in facts], dtype=np.uint64))
+    exp = {
+        "keyHash": np.array([pykeys.series_hash(pykeys.resource_hash(ra), pykeys.build_key(
+            ra["service.name"], nm, k, st)) for ra, nm, k, st, *_ in facts], dtype=np.uint64),
+        "startNs": np.array([f[4] for f in facts], dtype=np.uint64),
+        "endNs": np.array([f[5] for f in facts], dtype=np.uint64),
+        "meta": np.array([svc_ids[f[0]["service.name"]] | (f[2] << 16) | (f[3] << 19) for f in facts],
+                         dtype=np.uint32),
+    }
     tids = np.frombuffer(b"".join(f[6] for f in facts), dtype="<u8").reshape(-1, 2)
-    assert np.array_equal(cols["traceW0"], tids[:, 0]) and np.array_equal(cols["traceW1"], tids[:, 1])
-    exp_meta = np.array([svc_ids[f[0]["service.name"]] | (f[2] << 16) | (f[3] << 19) for f in facts],
-                        dtype=np.uint32)
-    assert np.array_equal(cols["meta"], exp_meta)
+    exp["traceW0"], exp["traceW1"] = tids[:, 0].copy(), tids[:, 1].copy()
+    if not native:  # the JS path's columns were captured at the N-API boundary
+        cols = {k: np.frombuffer(base64.b64decode(v), dtype=np.uint32 if k == "meta" else np.uint64)
+                for k, v in out["columns"].items()}
+        for k in exp:
+            assert np.array_equal(cols[k], exp[k]), k
 
     # 2. the engine's deltas, summed over the three flushes, equal the oracle bit-exactly
-    batch = SpanBatch(cols["keyHash"], cols["startNs"], cols["endNs"], cols["traceW0"],
-                      cols["traceW1"], cols["meta"])
+    batch = SpanBatch(exp["keyHash"], exp["startNs"], exp["endNs"], exp["traceW0"],
+                      exp["traceW1"], exp["meta"])
     o = pyoracle.Oracle(n_services=64)
     o.ingest(batch)
     ref = o.series()
