@@ -1039,8 +1039,12 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     for (int j = 0; j < S; ++j) {
       if (found[j] != kNotFound) {
         const uint32_t b = bkt[j];
-        atomicAdd(&lcnt[found[j] * nw + (b >> 1)], 1u << ((b & 1) * 16));
-        atomicAdd(&lsum[found[j]], (unsigned long long)dur[j]);
+        // diag 4096: spread the atomics over slots by lane (prices same-address
+        // serialisation of hot keys; counts are wrong)
+        const uint32_t fs = (DIAG && (diag & 4096u)) ? (found[j] + (threadIdx.x & 63u) * 29u) & (cap - 1u)
+                                                     : found[j];
+        atomicAdd(&lcnt[fs * nw + (b >> 1)], 1u << ((b & 1) * 16));
+        atomicAdd(&lsum[fs], (unsigned long long)dur[j]);
       }
     }
     stamp(3);

@@ -150,3 +150,63 @@ def generate_highcard(n: int, seed: int = 7, routes: int = 2000, pods: int = 500
     tr = rng.integers(0, n_traces, n)
     batch = SpanBatch(khash[kidx], start, end, tw0[tr], tw1[tr], pack_meta(svc, 2, status))
     return batch, khash, int(end.min()) // 10_000_000_000
+
+
+@dataclass
+class C5Workload:
+    """C5 stream: spans in end-time order over `duration_s`, plus the anomaly spec."""
+    base: Workload            # C2-shaped spans, re-timed (batch sorted by end_ns)
+    window_ns: int
+    first_window: int
+    n_windows: int
+    error_service: int        # service id whose error rate is multiplied
+    error_windows: tuple      # window offsets [lo, hi] of the error anomaly
+    burst_service: int        # service id with the distinct-trace burst
+    burst_windows: tuple      # window offsets [lo, hi] of the burst
+
+
+def generate_c5(n: int, seed: int = 5, duration_s: int = 600, window_s: int = 10,
+                error_factor: float = 20.0, error_windows=(30, 35), burst_factor: float = 4.0,
+                burst_windows=(40, 42)) -> C5Workload:
+    """C5: C2 traffic re-timed uniformly over 600 s (60 windows
+    of 10 s), sorted by end time as a collector receives it.  Injected
+    anomalies: the `payment` service's error rate x20 in windows 30-35 (the
+    demo's paymentFailure flag, demo.flagd.json:67-80) and a burst of new
+    traces at `frontend` in windows 40-42 (x4 its spans, each extra span in a
+    fresh trace).  The stream holds n spans plus the burst's extra spans."""
+    wl = generate_c2(n, seed=seed)
+    rng = np.random.Generator(np.random.PCG64(seed + 1000))
+    W = window_s * 1_000_000_000
+    t0 = (T0_NS // W) * W
+    b = wl.batch
+    dur = np.where(b.end_ns > b.start_ns, b.end_ns - b.start_ns, 0).astype(np.uint64)
+    dur = np.minimum(dur, np.uint64(W // 2))  # keep each span inside its own window or the next
+    end = (t0 + rng.integers(0, duration_s * 1_000_000_000, n, dtype=np.int64)).astype(np.uint64)
+    start = end - dur
+    win = ((end - np.uint64(t0)) // np.uint64(W)).astype(np.int64)
+    pay = SERVICES.index("payment")
+    fe = SERVICES.index("frontend")
+    status = wl.status.copy()
+    key_index = wl.key_index.copy()
+    # error anomaly: flip OK/UNSET payment spans to ERROR with the extra probability
+    in_err = (wl.service_id == pay) & (win >= error_windows[0]) & (win <= error_windows[1])
+    flip = in_err & (status != 2) & (rng.random(n) < min(1.0, 0.02 * (error_factor - 1)))
+    status[flip] = 2
+    key_index[flip] = key_index[flip] - (key_index[flip] % 3) + 2
+    # distinct-trace burst: (burst_factor - 1) extra copies of every frontend span
+    # in the burst windows, each in a fresh trace
+    in_burst = np.nonzero((wl.service_id == fe) & (win >= burst_windows[0]) & (win <= burst_windows[1]))[0]
+    extra = np.tile(in_burst, int(burst_factor) - 1)
+    m = len(extra)
+    idx = np.concatenate([np.arange(n), extra])
+    w0 = np.concatenate([b.trace_w0, rng.integers(0, 2**63, m, dtype=np.int64).astype(np.uint64)])
+    w1 = np.concatenate([b.trace_w1, rng.integers(0, 2**63, m, dtype=np.int64).astype(np.uint64)])
+    order = np.argsort(end[idx], kind="stable")
+    sel = idx[order]
+    batch = SpanBatch(wl.key_hashes[key_index][sel], start[sel], end[sel], w0[order], w1[order],
+                      pack_meta(wl.service_id[sel], wl.kind[sel], status[sel]))
+    base = Workload(batch, wl.key_strings, wl.key_hashes, key_index[sel], wl.service_id[sel],
+                    wl.name_id[sel], wl.kind[sel], status[sel], int(t0 // W),
+                    duration_s // window_s, wl.n_services)
+    return C5Workload(base, W, int(t0 // W), duration_s // window_s, pay, tuple(error_windows), fe,
+                      tuple(burst_windows))

@@ -31,6 +31,7 @@ VARIANTS_FINE = {
     "lo_bare_l2": LO | NO_BIN | NO_WIN | NO_STAT | L2_INPUT,
     "hll_store": 512,
     "hll_noread": 1024,
+    "lds_spread": 4096,
 }
 VARIANTS_C4 = {
     "lookup_only": 2048,  # HBM path: key-table lookups, no counter atomics
