@@ -1149,8 +1149,14 @@ __global__ __launch_bounds__(BLOCK) void ingest_hbm_kernel(IngestParams P) {
           const uint32_t found = g_find_insert(P.gkeys, key, P.log2cap, P.max_probe);
           if (found != kNotFound && !(P.diag & 2048u)) {  // diag 2048: lookups only
             unsigned long long *row = P.gcounts + (uint64_t)found * stride;
-            atomicAdd(row + b, 1ULL);
-            atomicAdd(row + nbk, (unsigned long long)d);
+            if (P.diag & 8192u) {  // diag: workgroup-scope atomics (XCD-local L2; wrong across XCDs)
+              __hip_atomic_fetch_add(row + b, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              __hip_atomic_fetch_add(row + nbk, (unsigned long long)d, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+              atomicAdd(row + b, 1ULL);
+              atomicAdd(row + nbk, (unsigned long long)d);
+            }
           }
           st.dropped += found == kNotFound ? 1u : 0u;
           slot[j] = found;

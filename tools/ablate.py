@@ -36,6 +36,7 @@ VARIANTS_FINE = {
 VARIANTS_C4 = {
     "lookup_only": 2048,  # HBM path: key-table lookups, no counter atomics
     "lookup_only_no_sketch": 2048 | NO_HLL | NO_CMS,
+    "wg_scope_atomics": 8192,
 }
 VARIANTS = {
     "l2_input": L2_INPUT,
