@@ -66,6 +66,39 @@ def cpu_baseline(wl, seconds: float):
     return port, conn
 
 
+def cpu_worker(seed: int, seconds: float) -> None:
+    """One process of the multi-core CPU baseline: the oracle port over its own
+    2 M-span C2 sample (sharded across the host cores)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from spanagg.synth import generate_c2
+
+    wl = generate_c2(2_000_000, seed=seed)
+    o = pyoracle.Oracle(n_services=wl.n_services)
+    reps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        o.ingest(wl.batch)
+        reps += 1
+    el = time.perf_counter() - t0
+    print(json.dumps({"spans": reps * len(wl.batch), "seconds": el}), flush=True)
+
+
+def cpu_baseline_multicore(workers: int, seconds: float):
+    """`workers` oracle processes at once (each its own shard, no sharing), the
+    way a sharded CPU collector would use the box; rate = sum of their rates."""
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--cpu-worker", str(100 + i),
+                               "--cpu-seconds", str(seconds)], stdout=subprocess.PIPE, text=True)
+             for i in range(workers)]
+    total = 0.0
+    for p in procs:
+        out, _ = p.communicate(timeout=seconds + 120)
+        r = json.loads(out.strip().splitlines()[-1])
+        total += r["spans"] / r["seconds"]
+    return {"value": total, "unit": "spans/s", "cores": workers, "kind": "port",
+            "sample": f"{workers} processes, each the oracle port (RED + HLL + CMS) over its own "
+                      f"2,000,000-span C2 shard for {seconds:.0f} s"}
+
+
 def load_traffic(path, workload):
     try:
         with open(path) as f:
@@ -110,7 +143,13 @@ def main():
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--host-otlp-spans", type=int, default=500_000,
                     help="spans for the Node host's OTLP->GPU rate (0 = skip)")
+    ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1),
+                    help="processes for the multi-core CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.cpu_worker is not None:  # child of cpu_baseline_multicore (no GPU use)
+        cpu_worker(args.cpu_worker, args.cpu_seconds)
+        return 0
 
     import numpy as np
     import torch
@@ -222,6 +261,9 @@ def main():
             port, conn = cpu_baseline(wl, args.cpu_seconds)
             result["cpu_baseline"] = port
             result["cpu_baseline_connector"] = conn
+            if args.cpu_workers > 1:
+                result["cpu_baseline_multicore"] = cpu_baseline_multicore(args.cpu_workers,
+                                                                          args.cpu_seconds / 2)
         if world == 1 and args.host_otlp_spans > 0:
             result["host_otlp"] = host_otlp_rate(args.host_otlp_spans)
         print(json.dumps(result), flush=True)
