@@ -953,7 +953,8 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
       rho[j] = 0;
       hoff[j] = 0;
       if (!(diag & 2u)) {
-        const uint64_t x = xxh64_16(T.a[j], T.b[j]);
+        // diag 16384: one 64-bit multiply instead of xxh64 (prices the hash's VALU)
+        const uint64_t x = (DIAG && (diag & 16384u)) ? (T.a[j] ^ T.b[j]) * XP1 : xxh64_16(T.a[j], T.b[j]);
         const uint32_t r = (uint32_t)__clzll((long long)((x << hp) | (1ULL << (hp - 1)))) + 1;
         rho[j] = sk ? r : 0u;
         hoff[j] = sk ? ((ws[j] * P.n_services + svc) << hp) + (uint32_t)(x >> (64 - hp)) : 0u;

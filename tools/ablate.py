@@ -32,6 +32,7 @@ VARIANTS_FINE = {
     "hll_store": 512,
     "hll_noread": 1024,
     "lds_spread": 4096,
+    "cheap_hash": 16384,
 }
 VARIANTS_C4 = {
     "lookup_only": 2048,  # HBM path: key-table lookups, no counter atomics
