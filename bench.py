@@ -178,7 +178,8 @@ def main():
     n = args.spans
     if args.workload == "c2":
         wl = generate_c2(n, seed=42 + rank)
-        batch, first_window, n_services, key_capacity = wl.batch, wl.first_window, wl.n_services, 1000
+        # 20 services x 25 names x 3 status codes: at most 1,500 series
+        batch, first_window, n_services, key_capacity = wl.batch, wl.first_window, wl.n_services, 1500
         workload = ("C2: synthetic SoA v1 spans, 20 services x 25 span names (Zipf 1.1) x 3 "
                     "status codes -> <=1,500 series, default spanmetrics buckets, lognormal "
                     "durations, ~10 spans/trace, per-service HLL p=14 + error count-min 4x2048, "

@@ -82,7 +82,7 @@ typedef struct {
     uint64_t window_ns;     /* sketch window length (default 10 s) */
     uint32_t n_windows;     /* resident window ring, power of two (default 8) */
     uint32_t n_services;    /* service ids 0..n_services-1 get sketches */
-    uint64_t key_capacity;  /* expected distinct series; table sized >= 2x, pow2 */
+    uint64_t key_capacity;  /* expected distinct series; table = next pow2 >= 1.25x */
     int32_t device;         /* HIP device ordinal (one engine per GPU / rank) */
     uint32_t flags;         /* 0 for production; SA_DIAG_* bits are profiling-only
                                ablations that skip work and make results WRONG */

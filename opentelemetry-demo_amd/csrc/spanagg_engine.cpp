@@ -256,7 +256,9 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       hipEventCreateWithFlags(&e->ev_b, hipEventDisableTiming) != hipSuccess)
     return bail(fail(e, SA_EDEVICE, "stream/event creation failed"));
 
-  e->cap = std::max<uint64_t>(16, next_pow2(2 * cfg->key_capacity));
+  // buckets of 4 slots with two choices stay well-behaved up to ~90% load:
+  // size for 80% at the declared capacity (the LDS mirror path needs cap <= 2048)
+  e->cap = std::max<uint64_t>(16, next_pow2(cfg->key_capacity + (cfg->key_capacity + 3) / 4));
   e->log2cap = log2u(e->cap);
   const uint32_t nw = (e->nbk + 1) / 2;
   // lkeys + lsum + lcnt + deferred-HLL queue (+ its counter), see ingest_lds_kernel
