@@ -33,6 +33,7 @@ VARIANTS_FINE = {
     "hll_noread": 1024,
     "lds_spread": 4096,
     "cheap_hash": 16384,
+    "diag_baseline": 65536,  # an unused bit: the diagnostic build with full work
 }
 VARIANTS_C4 = {
     "lookup_only": 2048,  # HBM path: key-table lookups, no counter atomics
