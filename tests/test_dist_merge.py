@@ -128,3 +128,64 @@ def test_shard_of_keeps_traces_together():
     s = shard_of(w1, 4)
     assert s[0] == s[1]
     assert list(s) == [1, 1, 2, 3]
+
+
+def _gpu_worker(rank, world, port, n, errq):
+    """The real GPU merge hooks (sa_export_keys / sa_gather_dense /
+    sa_window_export through EnginePartial) with two ranks sharing cuda:0 over
+    gloo (RCCL refuses two ranks on one device; the merge code is the same)."""
+    try:
+        for p in (os.path.join(ROOT, "opentelemetry-demo_amd"), os.path.join(ROOT, "oracle"), HERE):
+            sys.path.insert(0, p)
+        import pyoracle
+        from spanagg import Config, Engine, SpanBatch
+        from spanagg.dist import EnginePartial, merge_red, merge_window, shard_of
+        from spanagg.synth import generate_c2
+
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        wl = generate_c2(n, seed=321)
+        idx = np.nonzero(shard_of(wl.batch.trace_w1, world) == rank)[0]
+        sub = SpanBatch(*(c[idx] for c in wl.batch.columns()))
+        full = pyoracle.Oracle(n_services=wl.n_services)
+        full.ingest(wl.batch)
+        ref = full.series()
+        with Engine(Config(n_services=wl.n_services, n_windows=16, key_capacity=1500, device=0)) as e:
+            e.window_advance(wl.first_window)
+            e.ingest(sub)
+            part = EnginePartial(e, torch.device("cuda", 0))
+            red = merge_red(part)
+            assert np.array_equal(red.key_hash, ref["key_hash"])
+            assert np.array_equal(red.bucket_counts, ref["bucket_counts"])
+            assert np.array_equal(red.sum_ns, ref["sum_ns"])
+            for wid in full.window_ids():
+                hll, cms = merge_window(part, wid)
+                rh, rc = full.window(wid)
+                assert np.array_equal(hll, rh), wid
+                assert np.array_equal(cms, rc), wid
+            # merge_red reset the engine's deltas: a second merge is empty
+            assert len(merge_red(part).key_hash) == 0
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException as ex:
+        import traceback
+        errq.put(f"rank {rank}: {ex!r}\n{traceback.format_exc()}")
+        raise
+
+
+@pytest.mark.gpu
+def test_gpu_merge_hooks_two_ranks_match_single_aggregation():
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, 200_000, errq)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=200)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
