@@ -70,6 +70,21 @@ struct IngestParams {
   unsigned long long *dbg;  // diagnostic timestamps [G][8] (nullptr in production)
 };
 
+// Counter row layout (gcounts, one row per key slot): 64-B segments of 8 u64
+// cells -- cell 0 holds that segment's share of the ns sum, cells 1..7 seven
+// bucket counts.  A span's count cell and sum cell share a segment, so when
+// one wave instruction carries both (two adjacent lanes) the memory side
+// handles them as one atomic request (tools/atomic_probe.hip: 2x the rate).
+// The row's ns sum is the sum of its segments' cells.
+constexpr uint32_t kSegBuckets = 7;
+__host__ __device__ inline uint32_t row_stride(uint32_t nbk) {
+  return (nbk + kSegBuckets - 1) / kSegBuckets * 8;
+}
+__host__ __device__ inline uint32_t row_count_cell(uint32_t b) {
+  return b / kSegBuckets * 8 + 1 + b % kSegBuckets;
+}
+__host__ __device__ inline uint32_t row_sum_cell(uint32_t b) { return b / kSegBuckets * 8; }
+
 // Key-table layout: cap = 2^log2cap slots in buckets of 4 (log2cap in 4..31).
 // A key's probe sequence is its first-choice bucket b1, then its second-choice
 // bucket b2, then the buckets after b2 in order (every slot within cap + 4
@@ -130,11 +145,11 @@ hipError_t launch_reduce_slabs(uint32_t *slab_cnt, unsigned long long *slab_sum,
                                unsigned long long *gcounts, uint32_t G, uint64_t cap,
                                uint32_t nbk, hipStream_t s);
 hipError_t launch_compact(const unsigned long long *gkeys, unsigned long long *gcounts,
-                          uint64_t cap, uint32_t stride, unsigned long long *out_keys,
+                          uint64_t cap, uint32_t nbk, unsigned long long *out_keys,
                           unsigned long long *out_rows, unsigned long long *out_n,
                           uint64_t out_cap, int reset, hipStream_t s);
 hipError_t launch_gather_dense(const unsigned long long *gkeys, const unsigned long long *gcounts,
-                               uint32_t log2cap, uint32_t max_probe, uint32_t stride,
+                               uint32_t log2cap, uint32_t max_probe, uint32_t nbk,
                                const uint64_t *keys, uint64_t n, uint64_t *rows, hipStream_t s);
 hipError_t launch_fold_errcnt(const unsigned long long *gkeys, unsigned long long *errcnt,
                               uint64_t cap, unsigned long long *cms, uint32_t d, uint32_t w,

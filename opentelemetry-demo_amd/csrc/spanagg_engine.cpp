@@ -282,7 +282,6 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     e->G = e->cus * 8;
   }
 
-  const uint32_t stride = e->nbk + 1;
   const uint64_t S = cfg->n_services, W = cfg->n_windows;
   e->hll_slot_bytes = (size_t)S << cfg->hll_p;
   e->cms_slot_elems = (size_t)cfg->cms_d * cfg->cms_w;
@@ -293,7 +292,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   };
   int rc = SA_OK;
   if ((rc = alloc((void **)&e->gkeys, e->cap * 8)) ||
-      (rc = alloc((void **)&e->gcounts, e->cap * stride * 8)) ||
+      (rc = alloc((void **)&e->gcounts, e->cap * sa::row_stride(e->nbk) * 8)) ||
       (rc = alloc((void **)&e->hll, e->hll_slot_bytes * W)) ||
       (rc = alloc((void **)&e->cms, e->cms_slot_elems * W * 8)) ||
       (rc = alloc((void **)&e->errcnt, (size_t)W * e->cap * 8)) ||
@@ -535,7 +534,7 @@ int sa_flush(sa_engine *e, sa_red_result **out) {
   if (int rc = reduce_slabs(e, e->stream)) return rc;
   const uint32_t stride = e->nbk + 1;
   SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, e->stream));
-  SA_HIP(e, sa::launch_compact(e->gkeys, e->gcounts, e->cap, stride, e->out_keys, e->out_rows,
+  SA_HIP(e, sa::launch_compact(e->gkeys, e->gcounts, e->cap, e->nbk, e->out_keys, e->out_rows,
                                e->scratch, e->cap, 1, e->stream));
   uint64_t n = 0;
   SA_HIP(e, hipMemcpyAsync(&n, e->scratch, 8, hipMemcpyDeviceToHost, e->stream));
@@ -709,7 +708,7 @@ int sa_export_keys(sa_engine *e, uint64_t *d_keys, uint64_t cap, uint64_t *n_out
   }
   if (int rc = reduce_slabs(e, s)) return rc;
   SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, s));
-  SA_HIP(e, sa::launch_compact(e->gkeys, e->gcounts, e->cap, e->nbk + 1,
+  SA_HIP(e, sa::launch_compact(e->gkeys, e->gcounts, e->cap, e->nbk,
                                reinterpret_cast<unsigned long long *>(d_keys), nullptr, e->scratch,
                                cap, 0, s));
   SA_HIP(e, hipMemcpyAsync(n_out, e->scratch, 8, hipMemcpyDeviceToHost, s));
@@ -727,9 +726,9 @@ int sa_gather_dense(sa_engine *e, const uint64_t *d_keys, uint64_t n, uint64_t *
     SA_HIP(e, hipStreamWaitEvent(s, e->ev_a, 0));
   }
   if (int rc = reduce_slabs(e, s)) return rc;
-  SA_HIP(e, sa::launch_gather_dense(e->gkeys, e->gcounts, e->log2cap, sa::max_probe_of(e->log2cap), e->nbk + 1,
+  SA_HIP(e, sa::launch_gather_dense(e->gkeys, e->gcounts, e->log2cap, sa::max_probe_of(e->log2cap), e->nbk,
                                     d_keys, n, d_rows, s));
-  if (reset) SA_HIP(e, hipMemsetAsync(e->gcounts, 0, e->cap * (e->nbk + 1) * 8, s));
+  if (reset) SA_HIP(e, hipMemsetAsync(e->gcounts, 0, e->cap * sa::row_stride(e->nbk) * 8, s));
   if (s != e->stream) {
     SA_HIP(e, hipEventRecord(e->ev_b, s));
     SA_HIP(e, hipStreamWaitEvent(e->stream, e->ev_b, 0));

@@ -1119,7 +1119,7 @@ template <int NB, int S, bool PF, int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ingest_hbm_kernel(IngestParams P) {
   LaneStats st{0, 0, 0, 0};
   const uint32_t nbk = NB >= 0 ? (uint32_t)NB + 1 : P.nbk;
-  const uint32_t stride = nbk + 1;
+  const uint32_t stride = row_stride(nbk);
   uint64_t lo, hi;
   wg_range(P.n, lo, hi);
   const Cols c = make_cols(P, lo, hi);
@@ -1137,31 +1137,48 @@ __global__ __launch_bounds__(BLOCK) void ingest_hbm_kernel(IngestParams P) {
       load_tile<S>(c, off + tile, len, nxt);
       __builtin_amdgcn_sched_barrier(0);
     }
-    uint32_t slot[S];
+    uint32_t slot[S], bk[S];
+    uint64_t dd[S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       slot[j] = kNotFound;
+      bk[j] = 0;
+      dd[j] = 0;
       if (j < cur.cnt) {
         const uint64_t key = cur.key[j];
         const uint64_t d = cur.e[j] > cur.s[j] ? cur.e[j] - cur.s[j] : 0;
         st.zero_key += key == 0 ? 1u : 0u;
         if (key != 0 && !(P.diag & 1u)) {
-          const uint32_t b = bucket_of<NB>(d, P);
+          bk[j] = bucket_of<NB>(d, P);
+          dd[j] = d;
           const uint32_t found = g_find_insert(P.gkeys, key, P.log2cap, P.max_probe);
-          if (found != kNotFound && !(P.diag & 2048u)) {  // diag 2048: lookups only
-            unsigned long long *row = P.gcounts + (uint64_t)found * stride;
-            if (P.diag & 8192u) {  // diag: workgroup-scope atomics (XCD-local L2; wrong across XCDs)
-              __hip_atomic_fetch_add(row + b, 1ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-              __hip_atomic_fetch_add(row + nbk, (unsigned long long)d, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else {
-              atomicAdd(row + b, 1ULL);
-              atomicAdd(row + nbk, (unsigned long long)d);
-            }
-          }
           st.dropped += found == kNotFound ? 1u : 0u;
           slot[j] = found;
         }
+      }
+    }
+    // Counter atomics in lane pairs: lanes 2i and 2i+1 each add the count of
+    // one span and the sum of the other's, so one instruction carries both
+    // cells of a span -- one 64-B segment, one memory-side atomic request
+    // (the requests, not the bytes, bound this path: tools/atomic_probe.hip).
+    if (!(P.diag & 2048u)) {  // diag 2048: lookups only
+      const bool even = (threadIdx.x & 1u) == 0;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        const uint32_t os = (uint32_t)__shfl_xor((int)slot[j], 1);
+        const uint32_t ob = (uint32_t)__shfl_xor((int)bk[j], 1);
+        const uint64_t od = (uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)dd[j], 1) |
+                            ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(dd[j] >> 32), 1) << 32);
+        // instruction 1: even lane -> its count, odd lane -> the even lane's sum
+        const uint32_t s1 = even ? slot[j] : os, b1 = even ? bk[j] : ob;
+        if (s1 != kNotFound)
+          atomicAdd(P.gcounts + (uint64_t)s1 * stride + (even ? row_count_cell(b1) : row_sum_cell(b1)),
+                    even ? 1ULL : (unsigned long long)od);
+        // instruction 2: odd lane -> its count, even lane -> the odd lane's sum
+        const uint32_t s2 = even ? os : slot[j], b2 = even ? ob : bk[j];
+        if (s2 != kNotFound)
+          atomicAdd(P.gcounts + (uint64_t)s2 * stride + (even ? row_sum_cell(b2) : row_count_cell(b2)),
+                    even ? (unsigned long long)od : 1ULL);
       }
     }
     sketch_post<S>(P, cur, k, slot);
@@ -1186,7 +1203,7 @@ __global__ void reduce_slabs_kernel(const uint32_t *slab_cnt, const unsigned lon
                                     uint32_t nbk) {
   const uint32_t srow = (nbk + 1) & ~1u;  // 2 * ceil(nbk / 2)
   const uint64_t cells = cap * srow, quads = cells / 4;
-  const uint32_t stride = nbk + 1;
+  const uint32_t stride = row_stride(nbk);
   const uint32_t g0 = blockIdx.y * kSlabGroup, g1 = min(G, g0 + kSlabGroup);
   const uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (q < quads) {
@@ -1201,51 +1218,63 @@ __global__ void reduce_slabs_kernel(const uint32_t *slab_cnt, const unsigned lon
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const uint64_t c = q * 4 + i, slot = c / srow, b = c - slot * srow;
-      if (acc[i] && b < nbk) atomicAdd(gcounts + slot * stride + b, acc[i]);
+      if (acc[i] && b < nbk) atomicAdd(gcounts + slot * stride + row_count_cell((uint32_t)b), acc[i]);
     }
   } else if (q < quads + cap) {
     const uint64_t slot = q - quads;
     unsigned long long acc = 0;
     for (uint32_t g = g0; g < g1; ++g) acc += slab_sum[(uint64_t)g * cap + slot];
-    if (acc) atomicAdd(gcounts + slot * stride + nbk, acc);
+    if (acc) atomicAdd(gcounts + slot * stride + row_sum_cell(0), acc);
   }
 }
 
 // Compacts occupied slots with a non-zero row into (out_keys, out_rows); order
 // is arrival order of the atomic ticket (the host sorts by key).
+// Rows leave in the external layout [nbk bucket counts, ns sum].
 __global__ void compact_kernel(const unsigned long long *gkeys, unsigned long long *gcounts,
-                               uint64_t cap, uint32_t stride, unsigned long long *out_keys,
+                               uint64_t cap, uint32_t nbk, unsigned long long *out_keys,
                                unsigned long long *out_rows, unsigned long long *out_n,
                                uint64_t out_cap, int reset) {
+  const uint32_t stride = row_stride(nbk), ostride = nbk + 1;
   for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap;
        s += (uint64_t)gridDim.x * blockDim.x) {
     const unsigned long long k = gkeys[s];
     if (!k) continue;
     unsigned long long *row = gcounts + s * stride;
     bool any = false;
-    for (uint32_t b = 0; b < stride; ++b) any |= row[b] != 0;
+    for (uint32_t c = 0; c < stride; ++c) any |= row[c] != 0;
     if (!any) continue;
     const unsigned long long pos = atomicAdd(out_n, 1ULL);
     if (pos < out_cap) {
       if (out_keys) out_keys[pos] = k;
-      if (out_rows)
-        for (uint32_t b = 0; b < stride; ++b) out_rows[pos * stride + b] = row[b];
+      if (out_rows) {
+        unsigned long long sum = 0;
+        for (uint32_t c = 0; c < stride; c += 8) sum += row[c];
+        for (uint32_t b = 0; b < nbk; ++b) out_rows[pos * ostride + b] = row[row_count_cell(b)];
+        out_rows[pos * ostride + nbk] = sum;
+      }
     }
     if (reset)
-      for (uint32_t b = 0; b < stride; ++b) row[b] = 0;
+      for (uint32_t c = 0; c < stride; ++c) row[c] = 0;
   }
 }
 
+// rows[i] = [nbk bucket counts, ns sum] of keys[i] (zeros if absent).
 __global__ void gather_dense_kernel(const unsigned long long *gkeys,
                                     const unsigned long long *gcounts, uint32_t log2cap,
-                                    uint32_t max_probe, uint32_t stride, const uint64_t *keys,
+                                    uint32_t max_probe, uint32_t nbk, const uint64_t *keys,
                                     uint64_t n, uint64_t *rows) {
+  const uint32_t stride = row_stride(nbk), ostride = nbk + 1;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t k = keys[i];
     const uint32_t s = k ? g_find(gkeys, k, log2cap, max_probe) : kNotFound;
-    for (uint32_t b = 0; b < stride; ++b)
-      rows[i * stride + b] = s == kNotFound ? 0 : gcounts[(uint64_t)s * stride + b];
+    const bool hit = s != kNotFound;
+    const unsigned long long *row = gcounts + (uint64_t)(hit ? s : 0) * stride;
+    unsigned long long sum = 0;
+    for (uint32_t c = 0; c < stride; c += 8) sum += hit ? row[c] : 0;
+    for (uint32_t b = 0; b < nbk; ++b) rows[i * ostride + b] = hit ? row[row_count_cell(b)] : 0;
+    rows[i * ostride + nbk] = sum;
   }
 }
 
@@ -1387,22 +1416,22 @@ hipError_t launch_reduce_slabs(uint32_t *slab_cnt, unsigned long long *slab_sum,
 }
 
 hipError_t launch_compact(const unsigned long long *gkeys, unsigned long long *gcounts,
-                          uint64_t cap, uint32_t stride, unsigned long long *out_keys,
+                          uint64_t cap, uint32_t nbk, unsigned long long *out_keys,
                           unsigned long long *out_rows, unsigned long long *out_n,
                           uint64_t out_cap, int reset, hipStream_t s) {
   const uint32_t block = 256;
   hipLaunchKernelGGL(compact_kernel, dim3(grid_for(cap, block, 4096)), dim3(block), 0, s, gkeys,
-                     gcounts, cap, stride, out_keys, out_rows, out_n, out_cap, reset);
+                     gcounts, cap, nbk, out_keys, out_rows, out_n, out_cap, reset);
   return hipGetLastError();
 }
 
 hipError_t launch_gather_dense(const unsigned long long *gkeys, const unsigned long long *gcounts,
-                               uint32_t log2cap, uint32_t max_probe, uint32_t stride,
+                               uint32_t log2cap, uint32_t max_probe, uint32_t nbk,
                                const uint64_t *keys, uint64_t n, uint64_t *rows, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint32_t block = 256;
   hipLaunchKernelGGL(gather_dense_kernel, dim3(grid_for(n, block, 4096)), dim3(block), 0, s,
-                     gkeys, gcounts, log2cap, max_probe, stride, keys, n, rows);
+                     gkeys, gcounts, log2cap, max_probe, nbk, keys, n, rows);
   return hipGetLastError();
 }
 
