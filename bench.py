@@ -9,9 +9,19 @@ With N ranks every rank aggregates its own trace-id shard (weak scaling; no
 collective on the data path); after the timed region the ranks merge their
 partials once over RCCL (reported as merge_ms, outside `value`).
 
+Steps alternate over `--streams` (default 2) launch streams: the engine keeps
+two sets of per-workgroup slabs, so a launch waits only for the launch two
+back and consecutive batches overlap (the next batch's workgroups start on the
+CUs the current batch's workgroups leave).  `value` and `ms_per_step` are the
+wall clock of the timed steps.
+
 Prints ONE JSON line on rank 0. `roofline` prices the ingest kernel against
-HBM (44 algorithmic bytes per span / 8 TB/s); its per-launch time comes from
-HIP events recorded on the launch stream around every timed launch.
+HBM (44 algorithmic bytes per span / 8 TB/s).  Its `kernel_ms` is the kernel
+alone: HIP events around each of a set of serial launches on one stream,
+inside the run (overlapping launches would double-count, so these are not
+taken from the timed steps); `roofline.pipelined` prices the timed steps'
+device time per step (one start event all streams wait on, to the last
+stream's end event).
 `cpu_baseline` times the CPU oracle port (oracle/, RED+HLL+CMS, 1 thread) on
 rank 0 at N=1 over a bounded sample.
 """
@@ -104,7 +114,7 @@ def load_traffic(path, workload):
         with open(path) as f:
             t = json.load(f)
         if t.get("workload") == workload:
-            return t.get("hbm_bytes_per_launch"), path
+            return t.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
     except (OSError, ValueError):
         pass
     return None, None
@@ -138,6 +148,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--spans", type=int, default=10_000_000, help="spans per step per GPU")
     ap.add_argument("--workload", choices=["c2", "c4"], default="c2")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="launch streams the steps alternate over (the engine's two slab sets "
+                         "let consecutive launches overlap); 1 = strictly serial launches")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -196,33 +209,52 @@ def main():
     eng = Engine(Config(n_services=max(n_services, 1), n_windows=16, key_capacity=key_capacity,
                         device=local_rank))
     eng.window_advance(first_window)
-    # a dedicated (non-null) stream: the kernels and the timing events share it
-    stream = torch.cuda.Stream(device)
+    # dedicated (non-null) streams: the kernels and the timing events share them
+    streams = [torch.cuda.Stream(device) for _ in range(max(1, args.streams))]
+    stream = streams[0]
     torch.cuda.set_stream(stream)
 
-    def step():
-        eng.ingest_device(*cols, n=n, stream=stream.cuda_stream)
+    def step(i, s=None):
+        s = s or streams[i % len(streams)]
+        eng.ingest_device(*cols, n=n, stream=s.cuda_stream)
 
-    for _ in range(args.warmup):
-        step()
+    def ev():
+        return torch.cuda.Event(enable_timing=True)
+
+    for i in range(args.warmup):
+        step(i)
     torch.cuda.synchronize(device)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+    # 1) the kernel alone: serial launches on one stream, HIP events around
+    #    each on that stream (what rocprofv3 reports per launch)
+    iso = [(ev(), ev()) for _ in range(max(3, args.steps // 5))]
+    for a, b in iso:
+        a.record(stream)
+        step(0, stream)
+        b.record(stream)
+    torch.cuda.synchronize(device)
+    kernel_ms = sum(a.elapsed_time(b) for a, b in iso) / len(iso)
+    # 2) the timed steps: alternating over the streams; device time from one
+    #    start event (every stream waits on it) to the last stream's end event
+    start = ev()
+    ends = [ev() for _ in streams]
     barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
+    start.record(stream)
+    for s in streams[1:]:
+        s.wait_event(start)
     for i in range(args.steps):
-        evs[i][0].record(stream)
-        step()
-        evs[i][1].record(stream)
+        step(i)
+    for s, e_ in zip(streams, ends):
+        e_.record(s)
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0
     barrier()
-    kernel_ms = sum(a.elapsed_time(b) for a, b in evs) / max(1, args.steps)
+    device_ms = max(start.elapsed_time(e_) for e_ in ends) / max(1, args.steps)
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, kernel_ms, device_ms], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
+        elapsed, kernel_ms, device_ms = float(t[0]), float(t[1]), float(t[2])
 
     # one flush (+ RCCL merge across ranks) after the timed region
     torch.cuda.synchronize(device)
@@ -235,7 +267,7 @@ def main():
         red = eng.flush()
     torch.cuda.synchronize(device)
     merge_ms = (time.perf_counter() - tm) * 1e3
-    total_local = (args.warmup + args.steps) * n
+    total_local = (args.warmup + len(iso) + args.steps) * n
     calls_ok = int(red.calls.sum()) == total_local * world
 
     result = None
@@ -243,6 +275,7 @@ def main():
         value = world * n * args.steps / elapsed
         achieved = BYTES_PER_SPAN * n / (kernel_ms * 1e-3) / 1e9
         traffic, tsrc = load_traffic(args.traffic, args.workload)
+        piped = BYTES_PER_SPAN * n / (device_ms * 1e-3) / 1e9
         result = {
             "metric": METRIC, "value": value, "unit": "spans/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
@@ -255,7 +288,9 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "kernel": "ingest (spanagg_kernels.hip)",
                          "kernel_ms": kernel_ms, "bytes_per_span": BYTES_PER_SPAN,
-                         "traffic_source": tsrc},
+                         "traffic_source": tsrc,
+                         "pipelined": {"streams": len(streams), "device_ms_per_step": device_ms,
+                                       "achieved": piped, "frac": piped / HBM_PEAK_GBS}},
             "merge_ms": merge_ms, "calls_check": calls_ok,
         }
         if world == 1 and not args.no_cpu_baseline and wl is not None:

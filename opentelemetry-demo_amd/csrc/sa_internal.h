@@ -125,9 +125,10 @@ constexpr uint32_t kHbmBlock = 256;
 // small-table kernels: 0-3 ingest_lds_kernel {4,PF} {4,-} {2,PF} {2,-}, 4-7 the
 // same with nt loads; 8-13 ingest_v2_kernel: 8 generic (nt tile loads), 9 three
 // tiles in flight, 10 four spans per lane, 11 generic (default cache policy),
-// 12 / 13 = 8 / 11 specialised for cap 2048, 17 buckets, HLL p 14.
-constexpr int kNumLdsVariants = 16;
-constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2};
+// 12 / 13 = 8 / 11 specialised for cap 2048, 17 buckets, HLL p 14; 14 = 12 with
+// dynamic wave chunks (default); 15 = 14 generic; 16-18 = 14 with OPT 1 / 3 / 2.
+constexpr int kNumLdsVariants = 19;
+constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2};
 // v2 kernels keep u16 LDS counters for a whole launch: spans per workgroup per launch
 constexpr uint32_t kMaxWgSpans = 65532;
 constexpr uint32_t kDbgPerWg = 136;  // diagnostic stamps per workgroup: 8 + 16 waves x 8

@@ -4,7 +4,6 @@
 // SA_EDEVICE when no gfx950 device is usable.
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -28,7 +27,11 @@ constexpr uint64_t kCmsSeed[8] = {0x9E3779B97F4A7C15ULL, 0xBF58476D1CE4E5B9ULL,
                                   0x8EBC6AF09C88C6E3ULL, 0x589965CC75374CC3ULL};
 constexpr size_t kLdsBudget = 144 * 1024;  // small-table path LDS ceiling per workgroup
 constexpr uint64_t kSlabLimit = 1ULL << 31;  // per-workgroup spans between slab reductions
-constexpr int kDefaultVariant = 14;  // small path: ingest_v2_kernel (SPANAGG_VARIANT overrides)
+// small path: ingest_v2_kernel variant 16 (14 + key-table loads issued ahead
+// of every tile load); SPANAGG_VARIANT overrides
+constexpr int kDefaultVariant = 16;
+constexpr uint32_t kMaxSlabSets = 4;      // per-workgroup slab sets (small path)
+constexpr uint32_t kDefaultSlabSets = 2;  // SPANAGG_SLAB_SETS overrides
 
 bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 uint32_t log2u(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
@@ -46,6 +49,18 @@ struct sa_engine {
   int dev = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev_a = nullptr, ev_b = nullptr;
+  // Slab sets: the small-table path keeps two sets of per-workgroup slabs and
+  // alternates launches between them, so a launch only has to wait for the
+  // launch two back (the previous user of its set), not the previous one.
+  // Launches on different streams can then overlap: the next batch's
+  // workgroups start on the CUs that the current batch's workgroups leave.
+  // ev_set[i] marks the completion of the last launch that used set i (on
+  // set_stream[i]); non-ingest operations join every set onto the engine
+  // stream first, and the next launch orders after them through ev_ctl.
+  uint32_t nsets = 1, set = 0;
+  hipEvent_t ev_set[kMaxSlabSets] = {}, ev_ctl = nullptr;
+  hipStream_t set_stream[kMaxSlabSets] = {};
+  bool ctl_dirty = true;
   uint32_t nbk = 0, npos = 0, nneg = 0;
   uint64_t thr[sa::kMaxBounds]{};
   uint32_t log2cap = 0;
@@ -253,8 +268,12 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   // that produce batches on the null stream (stream == NULL) stay race-free.
   if (hipStreamCreateWithFlags(&e->stream, hipStreamDefault) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_a, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&e->ev_b, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&e->ev_b, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_ctl, hipEventDisableTiming) != hipSuccess)
     return bail(fail(e, SA_EDEVICE, "stream/event creation failed"));
+  for (hipEvent_t &ev : e->ev_set)
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+      return bail(fail(e, SA_EDEVICE, "event creation failed"));
 
   // buckets of 4 slots with two choices stay well-behaved up to ~90% load:
   // size for 80% at the declared capacity (the LDS mirror path needs cap <= 2048)
@@ -312,13 +331,17 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   if (hipMemcpy(e->d_seeds, kCmsSeed, sizeof kCmsSeed, hipMemcpyHostToDevice) != hipSuccess)
     return bail(fail(e, SA_EDEVICE, "seed upload failed"));
   if (e->small) {
+    e->nsets = kDefaultSlabSets;
+    if (const char *v = std::getenv("SPANAGG_SLAB_SETS"))  // tuning knob for A/B runs
+      e->nsets = (uint32_t)std::max(1, std::min((int)kMaxSlabSets, std::atoi(v)));
     const size_t srow = (e->nbk + 1) & ~1u;  // slab row = 2 * ceil(nbk/2) u32 cells
-    if ((rc = alloc((void **)&e->slab_cnt, (size_t)e->G * e->cap * srow * 4)) ||
-        (rc = alloc((void **)&e->slab_sum, (size_t)e->G * e->cap * 8)))
+    const size_t gs = (size_t)e->G * e->nsets;  // slabs of all sets, set-major
+    if ((rc = alloc((void **)&e->slab_cnt, gs * e->cap * srow * 4)) ||
+        (rc = alloc((void **)&e->slab_sum, gs * e->cap * 8)))
       return bail(rc);
     // (window, slot) keys of the v2 kernels' LDS ERROR table are 16-bit
     if (e->variant >= 8 && (uint64_t)cfg->n_windows * e->cap < 65535 &&
-        (rc = alloc((void **)&e->errslab, (size_t)e->G * cfg->n_windows * e->cap * 4)))
+        (rc = alloc((void **)&e->errslab, gs * cfg->n_windows * e->cap * 4)))
       return bail(rc);
   }
   if (hipDeviceSynchronize() != hipSuccess) return bail(fail(e, SA_EDEVICE, "device sync failed"));
@@ -326,10 +349,15 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   return SA_OK;
 }
 
+static void join_sets(sa_engine *e);
+
 void sa_destroy(sa_engine *e) {
   if (!e) return;
   (void)hipSetDevice(e->dev);
-  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->stream) {
+    join_sets(e);
+    (void)hipStreamSynchronize(e->stream);
+  }
   for (void *p : {(void *)e->gkeys, (void *)e->gcounts, (void *)e->slab_sum, (void *)e->cms,
                   (void *)e->stats, (void *)e->out_keys, (void *)e->out_rows, (void *)e->scratch,
                   (void *)e->slab_cnt, (void *)e->hll, (void *)e->errcnt, (void *)e->d_seeds,
@@ -338,15 +366,29 @@ void sa_destroy(sa_engine *e) {
     if (p) (void)hipFree(p);
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
   if (e->ev_b) (void)hipEventDestroy(e->ev_b);
+  for (hipEvent_t ev : e->ev_set)
+    if (ev) (void)hipEventDestroy(ev);
+  if (e->ev_ctl) (void)hipEventDestroy(e->ev_ctl);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
 
 const char *sa_last_error(const sa_engine *e) { return e ? e->err.c_str() : "null engine"; }
 
+// Orders the engine stream after every outstanding launch (each set's last
+// user); the next launch then orders after whatever the caller enqueues on the
+// engine stream now (ev_ctl, recorded lazily by that launch).
+static void join_sets(sa_engine *e) {
+  for (uint32_t i = 0; i < e->nsets; ++i)
+    if (e->set_stream[i] && e->set_stream[i] != e->stream)
+      (void)hipStreamWaitEvent(e->stream, e->ev_set[i], 0);
+  e->ctl_dirty = true;
+}
+
 static int reduce_slabs(sa_engine *e, hipStream_t s) {
   if (!e->small || e->slab_load == 0) return SA_OK;
-  SA_HIP(e, sa::launch_reduce_slabs(e->slab_cnt, e->slab_sum, e->gcounts, e->G, e->cap, e->nbk, s));
+  SA_HIP(e, sa::launch_reduce_slabs(e->slab_cnt, e->slab_sum, e->gcounts, e->G * e->nsets, e->cap,
+                                    e->nbk, s));
   e->slab_load = 0;
   return SA_OK;
 }
@@ -376,10 +418,22 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, e->G);
   if (e->small) {
     const uint64_t per_wg = ((b->n + grid - 1) / grid + 3) / 4 * 4;
-    if (e->slab_load + per_wg > kSlabLimit)
-      if (int rc = reduce_slabs(e, s)) return rc;
+    if (e->slab_load + per_wg > kSlabLimit) {  // fold every set into the counters first
+      join_sets(e);
+      if (int rc = reduce_slabs(e, e->stream)) return rc;
+    }
     e->slab_load += per_wg;
   }
+  // order: after the engine stream's work so far (ev_ctl, re-recorded after
+  // each join) and after the previous launch that used this slab set
+  if (e->ctl_dirty) {
+    SA_HIP(e, hipEventRecord(e->ev_ctl, e->stream));
+    e->ctl_dirty = false;
+  }
+  if (s != e->stream) SA_HIP(e, hipStreamWaitEvent(s, e->ev_ctl, 0));
+  const uint32_t set = e->set;
+  if (e->set_stream[set] && e->set_stream[set] != s) SA_HIP(e, hipStreamWaitEvent(s, e->ev_set[set], 0));
+  const size_t srow = (e->nbk + 1) & ~1u;
   IngestParams P{};
   P.key = b->key_hash;
   P.start = b->start_ns;
@@ -392,8 +446,8 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.gkeys = e->gkeys;
   P.log2cap = e->log2cap;
   P.max_probe = sa::max_probe_of(e->log2cap);
-  P.slab_cnt = e->slab_cnt;
-  P.slab_sum = e->slab_sum;
+  P.slab_cnt = e->slab_cnt ? e->slab_cnt + (size_t)set * e->G * e->cap * srow : nullptr;
+  P.slab_sum = e->slab_sum ? e->slab_sum + (size_t)set * e->G * e->cap : nullptr;
   P.gcounts = e->gcounts;
   std::memcpy(P.thr, e->thr, sizeof e->thr);
   P.npos = e->npos;
@@ -403,7 +457,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.hll = e->hll;
   P.cms = e->cms;
   P.errcnt = e->errcnt;
-  P.errslab = e->errslab;
+  P.errslab = e->errslab ? e->errslab + (size_t)set * e->G * e->cfg.n_windows * e->cap : nullptr;
   P.window_ns = e->cfg.window_ns;
   P.win_magic = UINT64_MAX / e->cfg.window_ns;
   P.win_base = e->win_base;
@@ -426,6 +480,9 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   hipError_t st = e->small ? sa::launch_ingest_small(P, grid, e->lds_bytes, s, e->variant)
                            : sa::launch_ingest_hbm(P, grid, s, e->variant);
   if (st != hipSuccess) return fail(e, SA_EDEVICE, std::string("ingest launch: ") + hipGetErrorString(st));
+  SA_HIP(e, hipEventRecord(e->ev_set[set], s));
+  e->set_stream[set] = s;
+  e->set = (set + 1) % e->nsets;
   e->spans += b->n;
   return SA_OK;
 }
@@ -449,23 +506,18 @@ static int check_batch(sa_engine *e, const sa_span_batch *b, bool device) {
 int sa_ingest_device(sa_engine *e, const sa_span_batch *b, void *stream) {
   if (int rc = check_batch(e, b, true)) return rc;
   if (int rc = set_dev(e)) return rc;
+  // stream-ordered on `stream`: after the engine's earlier work, before the
+  // caller's later work on the same stream; launches on other streams may
+  // overlap it (see sa_engine::nsets)
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
-  if (s != e->stream) {  // order against the engine stream both ways
-    SA_HIP(e, hipEventRecord(e->ev_a, e->stream));
-    SA_HIP(e, hipStreamWaitEvent(s, e->ev_a, 0));
-  }
-  if (int rc = ingest_on(e, b, s)) return rc;
-  if (s != e->stream) {
-    SA_HIP(e, hipEventRecord(e->ev_b, s));
-    SA_HIP(e, hipStreamWaitEvent(e->stream, e->ev_b, 0));
-  }
-  return SA_OK;
+  return ingest_on(e, b, s);
 }
 
 int sa_ingest(sa_engine *e, const sa_span_batch *b) {
   if (int rc = check_batch(e, b, false)) return rc;
   if (b->n == 0) return SA_OK;
   if (int rc = set_dev(e)) return rc;
+  join_sets(e);
   const uint64_t chunk = std::min<uint64_t>(b->n, 1ULL << 22);
   if (e->stage_spans < chunk) {
     if (e->stage) {
@@ -501,6 +553,7 @@ int sa_ingest(sa_engine *e, const sa_span_batch *b) {
 int sa_sync(sa_engine *e) {
   if (!e) return SA_EINVAL;
   if (int rc = set_dev(e)) return rc;
+  join_sets(e);
   SA_HIP(e, hipStreamSynchronize(e->stream));
   return SA_OK;
 }
@@ -530,6 +583,7 @@ int sa_flush(sa_engine *e, sa_red_result **out) {
   if (!e || !out) return SA_EINVAL;
   *out = nullptr;
   if (int rc = set_dev(e)) return rc;
+  join_sets(e);
   if (int rc = ensure_out(e)) return rc;
   if (int rc = reduce_slabs(e, e->stream)) return rc;
   const uint32_t stride = e->nbk + 1;
@@ -600,7 +654,7 @@ static bool resident(const sa_engine *e, uint64_t w) {
 // counts (see sketch_post in spanagg_kernels.hip).
 static int fold_errslab(sa_engine *e, uint64_t ws, hipStream_t s) {
   if (!e->errslab) return SA_OK;
-  SA_HIP(e, sa::launch_reduce_errslab(e->errslab, e->G, (uint64_t)e->cfg.n_windows * e->cap, ws,
+  SA_HIP(e, sa::launch_reduce_errslab(e->errslab, e->G * e->nsets, (uint64_t)e->cfg.n_windows * e->cap, ws,
                                       e->log2cap, e->errcnt + ws * e->cap, s));
   return SA_OK;
 }
@@ -618,6 +672,7 @@ int sa_window_read(sa_engine *e, uint64_t window_id, sa_sketch_result **out) {
   *out = nullptr;
   if (!resident(e, window_id)) return fail(e, SA_ERANGE, "window not resident");
   if (int rc = set_dev(e)) return rc;
+  join_sets(e);
   const uint64_t ws = window_id & (e->cfg.n_windows - 1);
   if (int rc = fold_window(e, ws, e->stream)) return rc;
   auto *h = new sketch_holder();
@@ -654,6 +709,7 @@ int sa_window_advance(sa_engine *e, uint64_t new_base) {
   if (new_base > UINT64_MAX / e->cfg.window_ns)
     return fail(e, SA_EINVAL, "window base beyond the u64 nanosecond range");
   if (int rc = set_dev(e)) return rc;
+  join_sets(e);
   const uint64_t n = std::min<uint64_t>(new_base - e->win_base, e->cfg.n_windows);
   for (uint64_t k = 0; k < n; ++k) {
     const uint64_t ws = (e->win_base + k) & (e->cfg.n_windows - 1);
@@ -671,6 +727,7 @@ int sa_debug_stamps(sa_engine *e, uint64_t *out, uint64_t cap, uint64_t *n_out) 
   *n_out = e->dbg ? (uint64_t)e->G * sa::kDbgPerWg : 0;
   if (!e->dbg || !out) return SA_OK;
   if (int rc = set_dev(e)) return rc;
+  join_sets(e);
   SA_HIP(e, hipStreamSynchronize(e->stream));
   SA_HIP(e, hipMemcpy(out, e->dbg, std::min<uint64_t>(cap, *n_out) * 8, hipMemcpyDeviceToHost));
   return SA_OK;
@@ -679,6 +736,7 @@ int sa_debug_stamps(sa_engine *e, uint64_t *out, uint64_t cap, uint64_t *n_out) 
 int sa_get_stats(sa_engine *e, sa_stats *o) {
   if (!e || !o) return SA_EINVAL;
   if (int rc = set_dev(e)) return rc;
+  join_sets(e);
   uint64_t st[sa::kNumStats];
   SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, e->stream));
   SA_HIP(e, sa::launch_count_keys(e->gkeys, e->cap, e->scratch, e->stream));
@@ -701,6 +759,7 @@ int sa_get_stats(sa_engine *e, sa_stats *o) {
 int sa_export_keys(sa_engine *e, uint64_t *d_keys, uint64_t cap, uint64_t *n_out, void *stream) {
   if (!e || !n_out || (cap && !d_keys)) return SA_EINVAL;
   if (int rc = set_dev(e)) return rc;
+  join_sets(e);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
   if (s != e->stream) {
     SA_HIP(e, hipEventRecord(e->ev_a, e->stream));
@@ -720,6 +779,7 @@ int sa_gather_dense(sa_engine *e, const uint64_t *d_keys, uint64_t n, uint64_t *
                     void *stream) {
   if (!e || (n && (!d_keys || !d_rows))) return SA_EINVAL;
   if (int rc = set_dev(e)) return rc;
+  join_sets(e);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
   if (s != e->stream) {
     SA_HIP(e, hipEventRecord(e->ev_a, e->stream));
@@ -741,6 +801,7 @@ int sa_window_export(sa_engine *e, uint64_t window_id, uint8_t *d_hll, uint64_t 
   if (!e) return SA_EINVAL;
   if (!resident(e, window_id)) return fail(e, SA_ERANGE, "window not resident");
   if (int rc = set_dev(e)) return rc;
+  join_sets(e);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
   if (s != e->stream) {
     SA_HIP(e, hipEventRecord(e->ev_a, e->stream));

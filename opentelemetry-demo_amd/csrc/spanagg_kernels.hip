@@ -799,8 +799,13 @@ __device__ __forceinline__ uint32_t wave_count(bool p) {
 // workgroup streaming alone for the last ~25% of the launch).  A grid-wide
 // counter in HBM was tried first: its returning atomic put a vmcnt(0) at the
 // top of every round and ran 3.4x slower.
+// OPT (DYN only): bit 0 = every wave issues its key-table loads before any
+// wave issues tile loads (a workgroup barrier between them), so the LDS setup
+// does not wait behind the other waves' first tiles; bit 1 = claims of one
+// wave tile instead of NBUF (a round takes NBUF claims), halving the work a
+// wave can still hold when its neighbours run out.
 template <int S, int NBUF, int AUX, bool DIAG, int LC = 0, int NWC = 0, int PC = 0, int HAUX = -1,
-          bool DYN = false>
+          bool DYN = false, int OPT = 0>
 __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 0] = __builtin_amdgcn_s_memrealtime();
@@ -825,7 +830,8 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   // by thread); DYN: one wave tile (64 * S spans, lane_off by lane) and a
   // claim is NBUF consecutive wave tiles
   constexpr uint32_t tile = DYN ? 64 * S : kLdsBlock * S;
-  constexpr uint32_t chunk = NBUF * tile;
+  constexpr bool kTileClaims = DYN && (OPT & 2);
+  constexpr uint32_t chunk = kTileClaims ? tile : NBUF * tile;
   const uint32_t lane_off = (DYN ? (threadIdx.x & 63u) : threadIdx.x) * S;
   constexpr uint32_t kWaves = kLdsBlock / 64;
   const uint32_t n_chunks = DYN ? (len + chunk - 1) / chunk : 0u;
@@ -834,8 +840,16 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   // the first two chunks of every wave are fixed; claims continue after them
   uint32_t c0 = wave, c1 = wave + kWaves;
+  // tile claims: cur[b] / nxt[b] = the tile in buffer b this round / the next
+  // round; the first two rounds are fixed (tile (r * NBUF + b) * kWaves + wave)
+  uint32_t cur[NBUF], nxt[NBUF];
+#pragma unroll
+  for (int b = 0; b < NBUF; ++b) {
+    cur[b] = (uint32_t)b * kWaves + wave;
+    nxt[b] = (uint32_t)(NBUF + b) * kWaves + wave;
+  }
   auto tstart = [&](uint32_t unit, int b) -> uint32_t {  // step b's first span, relative to lo
-    return DYN ? unit * chunk + (uint32_t)b * tile : unit + (uint32_t)b * tile;
+    return kTileClaims ? unit * tile : DYN ? unit * chunk + (uint32_t)b * tile : unit + (uint32_t)b * tile;
   };
   auto tremain = [&](uint32_t t) -> uint32_t { return len > t ? len - t : 0u; };
 
@@ -852,6 +866,12 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   }
   uint4 bv = make_uint4(0, 0, 0, 0);
   if (threadIdx.x < kBins * 2) bv = reinterpret_cast<const uint4 *>(P.bintab)[threadIdx.x];
+  if constexpr (DYN && (OPT & 1)) {
+    // no wait here (gfx950 barriers do not drain vmcnt): only the issue order
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
   // Issue order = the steady state's (tile, then S HLL reads, per step), so
   // the loop header's vmcnt accounting is the same from both predecessors;
   // the prologue's HLL reads seed `pend` (rho 0: never raised).
@@ -859,7 +879,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   Pending<S> pend;
 #pragma unroll
   for (int b = 0; b < NBUF; ++b) {
-    const uint32_t t = tstart(DYN ? c0 : 0u, b);
+    const uint32_t t = kTileClaims ? tstart(cur[b], b) : tstart(DYN ? c0 : 0u, b);
     load_tile_at<S, AUX>(P, (diag & 16u) ? t % (4 * tile) : lo + t, tremain(t), lane_off, buf[b]);
     if (b == NBUF - 1) {
       uint32_t z;  // a VGPR zero: keeps these vector loads (a uniform address would be s_load)
@@ -881,7 +901,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     *reinterpret_cast<uint4 *>(lcnt + i) = make_uint4(0, 0, 0, 0);
   if (threadIdx.x == 0) {
     hq_n[0] = 0;
-    hq_n[1] = 2u * kWaves;  // DYN: next unclaimed chunk of this workgroup's range
+    hq_n[1] = (kTileClaims ? 2u * NBUF : 2u) * kWaves;  // DYN: next unclaimed chunk of this workgroup's range
   }
   etab[threadIdx.x] = 0;  // kErrTab == kLdsBlock
   __syncthreads();
@@ -1065,7 +1085,24 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   // register allocator keeps each in-flight tile in one set of registers
   // across the back-edge instead of copying it (a copy waits for the loads).
   const uint32_t loop_len = (diag & 256u) ? 0u : len;  // diag: prologue/epilogue only
-  if constexpr (DYN) {
+  if constexpr (kTileClaims) {
+    // NBUF claims per round, each returning while the round runs; claims of a
+    // wave increase, so cur[0] is its smallest outstanding tile
+    while (cur[0] * tile < len) {
+      uint32_t nw_[NBUF];
+#pragma unroll
+      for (int b = 0; b < NBUF; ++b)
+        nw_[b] = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)atomicAdd(&hq_n[1], (threadIdx.x & 63u) == 0 ? 1u : 0u));
+#pragma unroll
+      for (int b = 0; b < NBUF; ++b) step(buf[b], tstart(cur[b], b), tstart(nxt[b], b));
+#pragma unroll
+      for (int b = 0; b < NBUF; ++b) {
+        cur[b] = nxt[b];
+        nxt[b] = nw_[b];
+      }
+    }
+  } else if constexpr (DYN) {
     // c0: this round's chunk (its tiles are in buf), c1: the next round's
     // (prefetched during this round), c2: claimed now for the round after.
     // The claim returns while the round runs; its result is read at the end.
@@ -1332,7 +1369,7 @@ uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap_blocks) {
 static const void *small_fn(bool bt, int v, bool diag) {
   if (bt && v >= 8) {  // v2 kernels (bin-table bucketing only)
     if (diag)
-      return (v == 14 || v == 15) ? (const void *)&ingest_v2_kernel<2, 2, 2, true, 0, 0, 0, -1, true>
+      return (v >= 14) ? (const void *)&ingest_v2_kernel<2, 2, 2, true, 0, 0, 0, -1, true>
                                   : (const void *)&ingest_v2_kernel<2, 2, 2, true>;
     switch (v) {
       case 9: return (const void *)&ingest_v2_kernel<2, 3, 0, false>;
@@ -1342,6 +1379,9 @@ static const void *small_fn(bool bt, int v, bool diag) {
       case 13: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14>;
       case 14: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true>;
       case 15: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true>;
+      case 16: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1>;
+      case 17: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 3>;
+      case 18: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 2>;
       default: return (const void *)&ingest_v2_kernel<2, 2, 2, false>;
     }
   }
@@ -1386,7 +1426,7 @@ hipError_t prepare_ingest_small(size_t lds_bytes) {
 hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,
                                hipStream_t s, int variant) {
   // the specialised v2 build is only valid for its compile-time geometry
-  if ((variant == 12 || variant == 13 || variant == 14) &&
+  if ((variant == 12 || variant == 13 || variant >= 14) &&
       !(P.log2cap == 11 && (P.nbk + 1) / 2 == 9 && P.p == 14))
     variant = variant == 12 ? 8 : variant == 13 ? 11 : 15;
   const void *fn = small_fn(P.bintab != nullptr, variant, P.diag != 0 || P.dbg != nullptr);

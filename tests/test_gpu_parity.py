@@ -170,6 +170,33 @@ def test_device_ingest_matches_host_ingest():
             assert np.array_equal(a.hll, b.hll) and np.array_equal(a.cms, b.cms)
 
 
+def test_device_ingest_two_streams_overlap():
+    """Batches alternating over two streams (the pipelined ingest bench.py
+    times): the launches may overlap on the device, each into its own slab set.
+    A flush between them and a null-stream batch check the joins."""
+    import torch
+    wl = generate_c2(1_200_000, seed=11)
+    cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).cuda()
+            for c in wl.batch.columns()]
+    cuts = [0, 150_000, 300_000, 450_000, 600_000, 750_000, 900_000, 1_050_000, 1_200_000]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    with Engine(Config(n_services=wl.n_services, n_windows=16)) as e:
+        e.window_advance(wl.first_window)
+        parts = [[c[a:b] for c in cols] for a, b in zip(cuts, cuts[1:])]  # offsets are 16-B aligned
+        for i in range(4):
+            e.ingest_device(*parts[i], n=cuts[i + 1] - cuts[i], stream=streams[i % 2].cuda_stream)
+        r1 = e.flush()
+        for i in range(4, 8):
+            st = None if i == 6 else streams[i % 2].cuda_stream
+            e.ingest_device(*parts[i], n=cuts[i + 1] - cuts[i], stream=st)
+        r2 = e.flush()
+        torch.cuda.synchronize()
+        assert_red_equal(r1, _oracle_run(wl.batch.slice(0, cuts[4]), wl.n_services).series())
+        assert_red_equal(r2, _oracle_run(wl.batch.slice(cuts[4], cuts[8]), wl.n_services).series())
+        _check_windows(e, _oracle_run(wl.batch, wl.n_services), wl.first_window, wl.n_services)
+
+
 def test_device_ingest_null_stream_orders_with_torch():
     """stream=NULL runs on the engine's stream, which is blocking: batches made
     on torch's legacy default stream and freed right after the call are safe."""

@@ -77,6 +77,8 @@ def main():
     engines = {}
     base_variant = os.environ.get("SPANAGG_VARIANT", "0")
     os.environ["SPANAGG_VARIANT"] = os.environ.get("ABL_BASE", base_variant)
+    if os.environ.get("ABL_NO_DIAG"):  # structure variants only
+        VARIANTS.clear()
     if c4:
         VARIANTS.update(VARIANTS_C4)
     if os.environ.get("ABL_FINE"):

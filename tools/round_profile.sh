@@ -12,6 +12,8 @@ timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/b
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
   -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --host-otlp-spans 0 > "$OUT/trace_bench.json" 2> "$OUT/trace.err"; st trace $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_s1" -o run \
+  -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --host-otlp-spans 0 --streams 1 > "$OUT/trace_s1_bench.json" 2> "$OUT/trace_s1.err"; st trace_s1 $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run \
   -- python3 "$GRAFT_REPO_ROOT/tools/prof_driver.py" > "$OUT/pmc_fetch.log" 2>&1; st pmc_fetch $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run \

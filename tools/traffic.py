@@ -16,7 +16,7 @@ root, out, rnd = sys.argv[1], sys.argv[2], sys.argv[3]
 f, nf = per_launch(f"{root}/pmc_fetch/run_counter_collection.csv", "FETCH_SIZE")
 w, nw = per_launch(f"{root}/pmc_write/run_counter_collection.csv", "WRITE_SIZE")
 spans = 10_000_000
-t = {"workload": "c2", "kernel": "ingest_v2_kernel<2,2,2,false,11,9,14,-1,true> (variant 14)",
+t = {"workload": "c2", "kernel": "ingest_v2_kernel<2,2,2,false,11,9,14,-1,true,1> (variant 16)",
      "spans_per_launch": spans, "algorithmic_bytes_per_launch": 44 * spans,
      "fetch_size_kb_per_launch": f, "write_size_kb_per_launch": w,
      "hbm_bytes_per_launch": int((2 * f + w) * 1024),
