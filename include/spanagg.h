@@ -142,7 +142,11 @@ const char *sa_last_error(const sa_engine *e);
 int sa_ingest(sa_engine *e, const sa_span_batch *batch);
 /* Device-resident batch (pointers into HBM of this engine's device).
  * `stream` is a hipStream_t (NULL = the engine's own stream). Asynchronous:
- * the batch must stay valid until the stream reaches this point. */
+ * the batch must stay valid until the stream reaches this point. Ordered
+ * after the engine's earlier non-ingest work (flush, window calls) and
+ * before the caller's later work on `stream`; ingests on different streams
+ * may run concurrently on the device (the engine orders them only where they
+ * share state), which is how consecutive batches overlap. */
 int sa_ingest_device(sa_engine *e, const sa_span_batch *batch, void *stream);
 int sa_sync(sa_engine *e);
 
