@@ -68,7 +68,24 @@ struct IngestParams {
   const uint64_t *seeds;  // [8] count-min row seeds (device memory)
   unsigned long long *stats;
   unsigned long long *dbg;  // diagnostic timestamps [G][8] (nullptr in production)
+  // partitioned HBM-table path: span records binned by key ([kPartBins][part_cap]
+  // of {key, ns << 7 | bucket}) and the per-bin fill counters
+  ulonglong2 *part_rec;
+  uint32_t *part_fill;
+  uint32_t part_cap;
 };
+
+// Partitioned HBM-table path (high cardinality): part_scatter_kernel bins
+// every span's record by the top 11 bits of its key, part_aggregate_kernel
+// aggregates one bin per workgroup in an LDS table and adds it to the HBM
+// counters once per key.
+constexpr uint32_t kPartBins = 2048;
+constexpr uint32_t kPartSlots = 1024;     // LDS table slots per bin (~490 keys per bin at 1 M keys)
+constexpr uint32_t kPartMaxBk = 17;       // LDS counter row: nbk <= 17 (default buckets)
+constexpr uint32_t kPartBlock = 1024;
+constexpr uint64_t kPartMaxSpans = 1ULL << 24;  // spans per partitioned launch
+__host__ __device__ inline uint32_t part_bin(uint64_t key) { return (uint32_t)(key >> 53); }
+constexpr size_t kPartLdsBytes = (size_t)kPartSlots * (16 + 4 * kPartMaxBk);
 
 // Counter row layout (gcounts, one row per key slot): 64-B segments of 8 u64
 // cells -- cell 0 holds that segment's share of the ns sum, cells 1..7 seven
@@ -141,6 +158,8 @@ constexpr size_t kLdsExtraBytes = kHllQueue * 8 + 16 + kBins * sizeof(BinEntry) 
 hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,
                                hipStream_t s, int variant);
 hipError_t launch_ingest_hbm(const IngestParams &P, uint32_t grid, hipStream_t s, int variant);
+hipError_t launch_ingest_part(const IngestParams &P, hipStream_t s);
+hipError_t prepare_ingest_part();
 hipError_t prepare_ingest_small(size_t lds_bytes);
 hipError_t launch_reduce_slabs(uint32_t *slab_cnt, unsigned long long *slab_sum,
                                unsigned long long *gcounts, uint32_t G, uint64_t cap,

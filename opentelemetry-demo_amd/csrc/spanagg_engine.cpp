@@ -79,6 +79,10 @@ struct sa_engine {
   uint32_t *slab_cnt = nullptr;
   uint32_t *errslab = nullptr;  // v2: [G][n_windows << log2cap] per-workgroup ERROR counts
   uint8_t *hll = nullptr;
+  // partitioned HBM-table path (lazily allocated on the first launch)
+  bool part = false;
+  ulonglong2 *part_rec = nullptr;
+  uint32_t *part_fill = nullptr;
   size_t hll_slot_bytes = 0, cms_slot_elems = 0;
   void *stage = nullptr;
   uint64_t stage_spans = 0;
@@ -299,6 +303,13 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     e->block = sa::kHbmBlock;
     e->spl = (uint32_t)sa::kVariants[e->variant].spl;
     e->G = e->cus * 8;
+    // partitioned path unless the LDS counter row is too small for the
+    // buckets (SPANAGG_HBM_PART=0: per-span atomics, for A/B runs)
+    const char *pv = std::getenv("SPANAGG_HBM_PART");
+    e->part = e->nbk <= sa::kPartMaxBk && !(pv && std::atoi(pv) == 0);
+    if (e->part)
+      if (hipError_t st = sa::prepare_ingest_part(); st != hipSuccess)
+        return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
   }
 
   const uint64_t S = cfg->n_services, W = cfg->n_windows;
@@ -361,7 +372,8 @@ void sa_destroy(sa_engine *e) {
   for (void *p : {(void *)e->gkeys, (void *)e->gcounts, (void *)e->slab_sum, (void *)e->cms,
                   (void *)e->stats, (void *)e->out_keys, (void *)e->out_rows, (void *)e->scratch,
                   (void *)e->slab_cnt, (void *)e->hll, (void *)e->errcnt, (void *)e->d_seeds,
-                  (void *)e->dbg, (void *)e->d_bins, (void *)e->errslab,
+                  (void *)e->dbg, (void *)e->d_bins, (void *)e->errslab, (void *)e->part_rec,
+                  (void *)e->part_fill,
                   e->stage})
     if (p) (void)hipFree(p);
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
@@ -400,7 +412,8 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s);
 static int ingest_on(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   // v2 small-table kernels keep u16 LDS counters for the whole launch: at most
   // 65532 spans per workgroup per launch (ingest_v2_kernel has no epoch flush)
-  const uint64_t max_n = (uint64_t)e->G * ((e->small && e->variant >= 8) ? sa::kMaxWgSpans : (1u << 27));
+  const uint64_t max_n = e->part ? sa::kPartMaxSpans
+                                 : (uint64_t)e->G * ((e->small && e->variant >= 8) ? sa::kMaxWgSpans : (1u << 27));
   for (uint64_t off = 0; off < b->n; off += max_n) {
     const uint64_t m = std::min(max_n, b->n - off);
     sa_span_batch sub{b->key_hash + off, b->start_ns + off, b->end_ns + off, b->trace_w0 + off,
@@ -477,8 +490,26 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.stats = e->stats;
   P.diag = e->cfg.flags;
   P.dbg = e->dbg;
-  hipError_t st = e->small ? sa::launch_ingest_small(P, grid, e->lds_bytes, s, e->variant)
-                           : sa::launch_ingest_hbm(P, grid, s, e->variant);
+  hipError_t st;
+  if (e->small) {
+    st = sa::launch_ingest_small(P, grid, e->lds_bytes, s, e->variant);
+  } else if (e->part) {
+    // records per bin: 1.25x the mean plus slack; a fuller bin spills to the
+    // direct path, so this bounds memory, not correctness
+    const uint64_t per_bin_max = sa::kPartMaxSpans / sa::kPartBins * 5 / 4 + 64;
+    if (!e->part_rec) {
+      if (hipMalloc((void **)&e->part_rec, sa::kPartBins * per_bin_max * sizeof(ulonglong2)) != hipSuccess ||
+          hipMalloc((void **)&e->part_fill, sa::kPartBins * 4) != hipSuccess ||
+          hipMemset(e->part_fill, 0, sa::kPartBins * 4) != hipSuccess)
+        return fail(e, SA_ENOMEM, "partition buffers hipMalloc failed");
+    }
+    P.part_rec = e->part_rec;
+    P.part_fill = e->part_fill;
+    P.part_cap = (uint32_t)std::min<uint64_t>(per_bin_max, (b->n + sa::kPartBins - 1) / sa::kPartBins * 5 / 4 + 64);
+    st = sa::launch_ingest_part(P, s);
+  } else {
+    st = sa::launch_ingest_hbm(P, grid, s, e->variant);
+  }
   if (st != hipSuccess) return fail(e, SA_EDEVICE, std::string("ingest launch: ") + hipGetErrorString(st));
   SA_HIP(e, hipEventRecord(e->ev_set[set], s));
   e->set_stream[set] = s;

@@ -16,6 +16,9 @@
 //   * HBM-table path (high cardinality): lock-free CAS insert + u64 atomics;
 //   * HLL: u8 registers in HBM, read-filtered, CAS-max only when rho grows;
 //   * count-min: u64 cells, atomic add per ERROR span per row.
+#include <algorithm>
+#include <cstdlib>
+
 #include "sa_internal.h"
 
 namespace sa {
@@ -80,14 +83,22 @@ __device__ __forceinline__ uint32_t bucket_of(uint64_t d, const IngestParams &P)
 }
 
 // Find-or-insert along the key's probe sequence (sa_internal.h), starting at
-// sequence position i0; kNotFound when the table is full.
+// sequence position i0; kNotFound when the table is full.  Slots only ever go
+// from 0 to a key, so a plain (possibly stale, L2-cached) read is safe: a
+// stale 0 is corrected by the CAS, which returns the slot's real key.
+// (Agent-scope loads bypass the XCD's L2 on gfx950 and made every probe a
+// memory round trip.)  SA_AGENT_PROBE restores them for A/B runs.
 __device__ __forceinline__ uint32_t g_find_insert(unsigned long long *keys, uint64_t key,
                                                   uint32_t log2cap, uint32_t max_probe,
                                                   uint32_t i0 = 0) {
   const ProbeSeq pr = probe_seq(key, log2cap);
   for (uint32_t i = i0; i < max_probe; ++i) {
     const uint32_t s = seq_slot(pr, i);
+#ifdef SA_AGENT_PROBE
     unsigned long long k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    unsigned long long k = keys[s];
+#endif
     if (k == key) return s;
     if (k == 0) {
       unsigned long long prev = atomicCAS(&keys[s], 0ULL, (unsigned long long)key);
@@ -1229,6 +1240,236 @@ __global__ __launch_bounds__(BLOCK) void ingest_hbm_kernel(IngestParams P) {
 }
 
 // ---------------------------------------------------------------------------
+// Partitioned HBM-table path.  Random per-span lookups and counter atomics
+// into a table far larger than LDS bound ingest_hbm_kernel (10 M spans over
+// 1 M keys: 552 us).  Here every span is first written as a 16-B record into
+// the bin of its key (top 11 bits), then one workgroup per bin aggregates its
+// records in an LDS table (~490 keys per bin at 1 M keys) and adds each key's
+// row to the HBM counters once, with plain read-modify-write: a key belongs
+// to one bin, so its row has one writer per launch.  Records that do not fit
+// (a bin beyond its capacity, durations >= 2^57 ns, an LDS table past its
+// probe limit) take the direct path: lookup + counter atomics, as in
+// ingest_hbm_kernel.  Stats, HLL and ERROR spans are handled in the scatter.
+
+typedef unsigned long long nt_u64x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void direct_red(const IngestParams &P, uint64_t key, uint64_t d,
+                                           uint32_t bk, uint32_t stride, LaneStats &st) {
+  const uint32_t s = g_find_insert(P.gkeys, key, P.log2cap, P.max_probe);
+  if (s == kNotFound) {
+    st.dropped += 1u;
+    return;
+  }
+  atomicAdd(P.gcounts + (uint64_t)s * stride + row_count_cell(bk), 1ULL);
+  atomicAdd(P.gcounts + (uint64_t)s * stride + row_sum_cell(bk), (unsigned long long)d);
+}
+
+template <int NB>
+__global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P) {
+  __shared__ uint32_t cur[kPartBins];  // phase 1: counts; phase 2: next record index
+  __shared__ uint32_t lim[kPartBins];  // end of this workgroup's run in the bin
+  LaneStats st{0, 0, 0, 0};
+  const uint32_t nbk = NB >= 0 ? (uint32_t)NB + 1 : P.nbk;
+  const uint32_t stride = row_stride(nbk);
+  uint64_t lo, hi;
+  wg_range(P.n, lo, hi);
+  for (uint32_t b = threadIdx.x; b < kPartBins; b += blockDim.x) cur[b] = 0;
+  __syncthreads();
+  // 1. records per bin in this workgroup's range (key column only)
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const uint64_t key = P.key[i];
+    if (key != 0) atomicAdd(&cur[part_bin(key)], 1u);
+  }
+  __syncthreads();
+  // 2. reserve one contiguous run per bin (one returning atomic per bin)
+  for (uint32_t b = threadIdx.x; b < kPartBins; b += blockDim.x) {
+    const uint32_t c = cur[b];
+    uint32_t base = 0;
+    if (c) base = atomicAdd(&P.part_fill[b], c);
+    const uint64_t b0 = (uint64_t)b * P.part_cap;
+    cur[b] = (uint32_t)(b0 + min(base, P.part_cap));
+    lim[b] = (uint32_t)(b0 + min(base + c, P.part_cap));
+  }
+  __syncthreads();
+  // 3. every span: stats, sketches, and its record (or the direct path);
+  //    U spans per thread with all their loads issued first
+  constexpr int U = 4;
+  for (uint64_t i0 = lo + threadIdx.x; i0 < hi; i0 += U * blockDim.x) {
+   uint64_t K[U], S0[U], E0[U], A[U], B[U];
+   uint32_t M[U];
+#pragma unroll
+   for (int u = 0; u < U; ++u) {
+     const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+     const bool ok = i < hi;
+     K[u] = ok ? P.key[i] : 0;
+     S0[u] = ok ? P.start[i] : 0;
+     E0[u] = ok ? P.end[i] : 0;
+     A[u] = ok ? P.w0[i] : 0;
+     B[u] = ok ? P.w1[i] : 0;
+     M[u] = ok ? P.meta[i] : 0xFFFFu;  // invalid service marks the padding lane
+   }
+   // sketch phase A for all U spans: the HLL register reads are issued
+   // together (unconditional: a skipped span reads the first byte)
+   uint32_t WS[U], RHO[U], CUR[U];
+   uint8_t *REG[U];
+#pragma unroll
+   for (int u = 0; u < U; ++u) {
+    const bool in = i0 + (uint64_t)u * blockDim.x < hi;
+    const uint32_t svc = M[u] & 0xFFFFu;
+    const bool svc_ok = svc < P.n_services;
+    const uint64_t win = fast_div(E0[u], P.window_ns, P.win_magic);
+    const bool win_ok = win - P.win_base < (uint64_t)P.n_windows;
+    if (in) {
+      st.zero_key += K[u] == 0 ? 1u : 0u;
+      st.bad_svc += svc_ok ? 0u : 1u;
+      st.oor += (svc_ok && !win_ok) ? 1u : 0u;
+    }
+    WS[u] = in && svc_ok && win_ok ? (uint32_t)(win & P.win_mask) : 0xFFFFFFFFu;
+    RHO[u] = 0;
+    REG[u] = P.hll;
+    if (WS[u] != 0xFFFFFFFFu && !(P.diag & 2u)) {
+      const uint64_t x = xxh64_16(A[u], B[u]);
+      RHO[u] = (uint32_t)__clzll((long long)((x << P.p) | (1ULL << (P.p - 1)))) + 1;
+      REG[u] = P.hll + ((((uint64_t)WS[u] * P.n_services + svc) << P.p) + (x >> (64 - P.p)));
+    }
+   }
+#pragma unroll
+   for (int u = 0; u < U; ++u) CUR[u] = *REG[u];
+#pragma unroll
+   for (int u = 0; u < U; ++u) {
+    if (i0 + (uint64_t)u * blockDim.x >= hi) continue;
+    const uint64_t key = K[u], s0 = S0[u], e0 = E0[u];
+    const uint32_t meta = M[u];
+    const uint64_t d = e0 > s0 ? e0 - s0 : 0;
+    const uint32_t bk = bucket_of<NB>(d, P);
+    const uint32_t ws = WS[u];
+    if (key != 0 && !(P.diag & 1u)) {
+      const uint32_t b = part_bin(key);
+      const uint32_t r = d < (1ULL << 57) ? atomicAdd(&cur[b], 1u) : 0xFFFFFFFFu;
+      if (r < lim[b])
+        P.part_rec[r] = make_ulonglong2(key, (d << 7) | bk);  // write-back: partial lines merge in L2
+      else
+        direct_red(P, key, d, bk, stride, st);
+    }
+    // ERROR spans: the exact per-(window, slot) counter (count-min cells are
+    // folded from it); no slot (key 0, table full): the cells directly
+    if (ws != 0xFFFFFFFFu && ((meta >> 19) & 3u) == 2u && !(P.diag & 4u)) {
+      const uint32_t slot = key != 0 ? g_find_insert(P.gkeys, key, P.log2cap, P.max_probe) : kNotFound;
+      if (slot != kNotFound) atomicAdd(P.errcnt + ((uint64_t)ws << P.log2cap) + slot, 1ULL);
+      else cms_add(P, ws, key, 1ULL);
+    }
+   }
+#pragma unroll
+   for (int u = 0; u < U; ++u)
+     if ((CUR[u] & 0xFFu) < RHO[u]) hll_raise(REG[u], RHO[u]);
+  }
+  flush_stats(P, st);
+}
+
+// One workgroup per bin: LDS table of kPartSlots keys (linear probing from a
+// hash of the key's low bits; the bin fixes its top bits), u32 bucket counts
+// and u64 ns sums, then one read-modify-write of each key's HBM row.
+__global__ __launch_bounds__(kPartBlock) void part_aggregate_kernel(IngestParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned long long *lkeys = reinterpret_cast<unsigned long long *>(smem);
+  unsigned long long *lsum = lkeys + kPartSlots;
+  uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + kPartSlots);
+  const uint32_t nbk = P.nbk, stride = row_stride(nbk);
+  LaneStats st{0, 0, 0, 0};
+  __shared__ uint32_t spilled;  // direct-path atomics from this workgroup
+  if (threadIdx.x == 0) spilled = 0;
+  const uint32_t bin = blockIdx.x;
+  const uint32_t n = (P.diag & 1u) ? 0u : min(P.part_fill[bin], P.part_cap);  // diag 1: no records
+  for (uint32_t i = threadIdx.x; i < kPartSlots; i += blockDim.x) lkeys[i] = lsum[i] = 0;
+  for (uint32_t i = threadIdx.x; i < kPartSlots * nbk; i += blockDim.x) lcnt[i] = 0;
+  __syncthreads();
+  const ulonglong2 *rec = P.part_rec + (uint64_t)bin * P.part_cap;
+  constexpr int R = 4;  // records in flight per thread
+  for (uint32_t i0 = 0; i0 < n; i0 += R * blockDim.x) {
+    ulonglong2 v[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const uint32_t i = i0 + u * blockDim.x + threadIdx.x;
+      v[u] = i < n ? rec[i] : make_ulonglong2(0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const unsigned long long key = v[u].x;
+      if (key == 0) continue;
+      const uint64_t d = v[u].y >> 7;
+      const uint32_t bk = (uint32_t)(v[u].y & 127u);
+      uint32_t s = ((uint32_t)key * 0x9E3779B1u) >> (32 - 10), found = kNotFound;
+      for (int pr = 0; pr < 64; ++pr, s = (s + 1) & (kPartSlots - 1)) {
+        unsigned long long k = lkeys[s];
+        if (k == 0) k = atomicCAS(&lkeys[s], 0ULL, key);
+        if (k == 0 || k == key) {
+          found = s;
+          break;
+        }
+      }
+      if (found != kNotFound) {
+        atomicAdd(&lcnt[found * nbk + bk], 1u);
+        atomicAdd(&lsum[found], (unsigned long long)d);
+      } else {
+        direct_red(P, key, d, bk, stride, st);
+        spilled = 1;
+      }
+    }
+  }
+  __syncthreads();
+  // Row updates below use plain loads: a row belongs to this workgroup's bin,
+  // so in this launch only this workgroup writes it (earlier launches' writes
+  // are visible at the kernel boundary).  After a direct-path spill the
+  // row may also hold this launch's atomics, which are performed beyond the
+  // XCD's L2: then fence and read at agent scope.
+  const bool coherent = spilled != 0;
+  if (coherent) {
+    __threadfence();
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) P.part_fill[bin] = 0;  // ready for the next launch
+  for (uint32_t s = threadIdx.x; s < kPartSlots && !(P.diag & 8u); s += blockDim.x) {
+    const unsigned long long key = lkeys[s];
+    if (key == 0) continue;
+    // the key's first-choice bucket in four independent loads (most keys sit
+    // there); the full probe sequence only for the rest
+    const ProbeSeq pr = probe_seq(key, P.log2cap);
+    unsigned long long q[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[j] = P.gkeys[pr.b1 * 4 + j];  // stale reads just miss: see g_find_insert
+    uint32_t g = kNotFound;
+#pragma unroll
+    for (int j = 3; j >= 0; --j) g = q[j] == key ? pr.b1 * 4 + j : g;
+    if (g == kNotFound) g = g_find_insert(P.gkeys, key, P.log2cap, P.max_probe);
+    if (g == kNotFound) {
+      uint32_t calls = 0;
+      for (uint32_t b = 0; b < nbk; ++b) calls += lcnt[s * nbk + b];
+      st.dropped += calls;
+      continue;
+    }
+    unsigned long long *row = P.gcounts + (uint64_t)g * stride;
+    // every load issued before any store (no wait per cell)
+    unsigned long long old[kPartMaxBk + 1];
+    if (coherent) {
+#pragma unroll
+      for (uint32_t b = 0; b < kPartMaxBk; ++b)  // unconditional (in-row address), no branch per load
+        old[b] = __hip_atomic_load(row + (b < nbk ? row_count_cell(b) : 0u), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+      old[kPartMaxBk] = __hip_atomic_load(row + row_sum_cell(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+#pragma unroll
+      for (uint32_t b = 0; b < kPartMaxBk; ++b) old[b] = row[b < nbk ? row_count_cell(b) : 0u];
+      old[kPartMaxBk] = row[row_sum_cell(0)];
+    }
+#pragma unroll
+    for (uint32_t b = 0; b < kPartMaxBk; ++b)
+      if (b < nbk && lcnt[s * nbk + b]) row[row_count_cell(b)] = old[b] + lcnt[s * nbk + b];
+    row[row_sum_cell(0)] = old[kPartMaxBk] + lsum[s];
+  }
+  flush_stats(P, st);
+}
+
+// ---------------------------------------------------------------------------
 // Flush-time kernels.
 // slabs -> counters.  blockIdx.y takes a group of kSlabGroup workgroup slabs;
 // each thread sums one 4-cell quad of them and adds the partial into the u64
@@ -1432,6 +1673,26 @@ hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_
   const void *fn = small_fn(P.bintab != nullptr, variant, P.diag != 0 || P.dbg != nullptr);
   void *args[] = {const_cast<IngestParams *>(&P)};
   return hipLaunchKernel(fn, dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);
+}
+
+hipError_t launch_ingest_part(const IngestParams &P, hipStream_t s) {
+  static const uint32_t max_grid = [] {
+    const char *v = std::getenv("SPANAGG_PART_GRID");  // tuning knob for A/B runs
+    return v ? (uint32_t)std::max(1, std::atoi(v)) : 256u;
+  }();
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(max_grid, (P.n + kPartBlock - 1) / kPartBlock);
+  if (P.nneg == 0 && P.npos == 16)
+    hipLaunchKernelGGL((part_scatter_kernel<16>), dim3(grid), dim3(kPartBlock), 0, s, P);
+  else
+    hipLaunchKernelGGL((part_scatter_kernel<-1>), dim3(grid), dim3(kPartBlock), 0, s, P);
+  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  hipLaunchKernelGGL(part_aggregate_kernel, dim3(kPartBins), dim3(kPartBlock), kPartLdsBytes, s, P);
+  return hipGetLastError();
+}
+
+hipError_t prepare_ingest_part() {
+  return hipFuncSetAttribute((const void *)&part_aggregate_kernel,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPartLdsBytes);
 }
 
 hipError_t launch_ingest_hbm(const IngestParams &P, uint32_t grid, hipStream_t s, int variant) {

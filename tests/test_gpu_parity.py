@@ -318,6 +318,43 @@ def test_high_cardinality_hbm_table_vs_oracle():
             assert np.array_equal(sk.hll, hll) and np.array_equal(sk.cms, cms)
 
 
+@pytest.mark.parametrize("shape", ["zipf_bins_spill", "lds_tables_spill"])
+def test_partitioned_hbm_path_spills_vs_oracle(shape, monkeypatch):
+    """The partitioned HBM-table path (part_scatter + part_aggregate) where it
+    falls back to the direct path: a Zipf key mix overfills the hot keys' bins,
+    and ~2.9 M distinct keys (~1,400 per bin) overfill the 1,024-slot LDS
+    tables.  Two ingests (two launches, bin counters reset between) and the
+    per-span atomic path (SPANAGG_HBM_PART=0) on the same input must agree."""
+    if shape == "zipf_bins_spill":
+        batch, _, w0 = generate_highcard(2_000_000, seed=3, routes=400, pods=250, zipf_s=1.2)
+        kcap = 200_000
+    else:
+        batch, _, w0 = generate_highcard(4_000_000, seed=4, routes=3000, pods=1000)
+        kcap = 3_500_000
+    half = len(batch) // 2 // 16 * 16
+    results = []
+    for part in ("1", "0"):
+        monkeypatch.setenv("SPANAGG_HBM_PART", part)
+        with Engine(Config(n_services=1, n_windows=16, key_capacity=kcap)) as e:
+            assert e.stats()["small_table"] == 0
+            e.window_advance(w0)
+            e.ingest(batch.slice(0, half))
+            e.ingest(batch.slice(half, len(batch)))
+            res = e.flush()
+            wins = {}
+            for wid in range(w0, w0 + 16):
+                sk = e.window_read(wid)
+                wins[wid] = (sk.hll.copy(), sk.cms.copy())
+            results.append((res, wins, e.stats()))
+    o = _oracle_run(batch, 1)
+    for res, wins, st in results:
+        assert st["dropped_table_full"] == 0
+        assert_red_equal(res, o.series())
+        for wid in o.window_ids():
+            hll, cms = o.window(wid)
+            assert np.array_equal(wins[wid][0], hll) and np.array_equal(wins[wid][1], cms)
+
+
 def test_repeat_runs_identical():
     wl = generate_c2(1_000_000, seed=77)
     outs = []

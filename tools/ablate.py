@@ -79,6 +79,9 @@ def main():
     os.environ["SPANAGG_VARIANT"] = os.environ.get("ABL_BASE", base_variant)
     if os.environ.get("ABL_NO_DIAG"):  # structure variants only
         VARIANTS.clear()
+    if os.environ.get("ABL_FLAGS"):  # explicit set: "name:flags,name:flags"
+        VARIANTS.clear()
+        VARIANTS.update({k: int(v) for k, v in (x.split(":") for x in os.environ["ABL_FLAGS"].split(","))})
     if c4:
         VARIANTS.update(VARIANTS_C4)
     if os.environ.get("ABL_FINE"):
@@ -88,7 +91,7 @@ def main():
         e.window_advance(wl.first_window)
         engines[name] = e
     # kernel-structure variants (sa_internal.h kVariants), full work
-    for v in [int(x) for x in os.environ.get("ABL_VARS", "0,8,11,12").split(",")]:
+    for v in [int(x) for x in os.environ.get("ABL_VARS", "0,8,11,12").split(",") if x]:
         os.environ["SPANAGG_VARIANT"] = str(v)
         e = Engine(Config(n_services=wl.n_services, n_windows=16, key_capacity=kcap))
         e.window_advance(wl.first_window)
