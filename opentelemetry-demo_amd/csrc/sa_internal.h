@@ -82,10 +82,16 @@ struct IngestParams {
 constexpr uint32_t kPartBins = 2048;
 constexpr uint32_t kPartSlots = 1024;     // LDS table slots per bin (~490 keys per bin at 1 M keys)
 constexpr uint32_t kPartMaxBk = 17;       // LDS counter row: nbk <= 17 (default buckets)
-constexpr uint32_t kPartBlock = 1024;
+constexpr uint32_t kPartBlock = 1024;     // scatter
+constexpr uint32_t kPartAggBlock = 512;   // aggregate: three workgroups per CU
 constexpr uint64_t kPartMaxSpans = 1ULL << 24;  // spans per partitioned launch
+// records per bin: 1.25x the mean plus slack (a fuller bin spills to the direct path)
+constexpr uint64_t kPartMaxCap = kPartMaxSpans / kPartBins * 5 / 4 + 64;
+// a bin holds < 2^16 records, so its LDS bucket counters are u16 pairs
+static_assert(kPartMaxCap < 65536, "u16 LDS counters");
+constexpr uint32_t kPartWords = (kPartMaxBk + 1) / 2;
 __host__ __device__ inline uint32_t part_bin(uint64_t key) { return (uint32_t)(key >> 53); }
-constexpr size_t kPartLdsBytes = (size_t)kPartSlots * (16 + 4 * kPartMaxBk);
+constexpr size_t kPartLdsBytes = (size_t)kPartSlots * (16 + 4 * kPartWords);  // 52 KiB
 
 // Counter row layout (gcounts, one row per key slot): 64-B segments of 8 u64
 // cells -- cell 0 holds that segment's share of the ns sum, cells 1..7 seven

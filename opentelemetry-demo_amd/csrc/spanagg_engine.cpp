@@ -496,7 +496,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   } else if (e->part) {
     // records per bin: 1.25x the mean plus slack; a fuller bin spills to the
     // direct path, so this bounds memory, not correctness
-    const uint64_t per_bin_max = sa::kPartMaxSpans / sa::kPartBins * 5 / 4 + 64;
+    const uint64_t per_bin_max = sa::kPartMaxCap;
     if (!e->part_rec) {
       if (hipMalloc((void **)&e->part_rec, sa::kPartBins * per_bin_max * sizeof(ulonglong2)) != hipSuccess ||
           hipMalloc((void **)&e->part_fill, sa::kPartBins * 4) != hipSuccess ||

@@ -1367,24 +1367,28 @@ __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P
 }
 
 // One workgroup per bin: LDS table of kPartSlots keys (linear probing from a
-// hash of the key's low bits; the bin fixes its top bits), u32 bucket counts
-// and u64 ns sums, then one read-modify-write of each key's HBM row.
-__global__ __launch_bounds__(kPartBlock) void part_aggregate_kernel(IngestParams P) {
+// hash of the key's low bits; the bin fixes its top bits), u16 bucket-count
+// pairs (a bin holds < 2^16 records) and u64 ns sums -- 52 KiB, three
+// workgroups per CU -- then one read-modify-write of each key's HBM row.
+__global__ __launch_bounds__(kPartAggBlock) void part_aggregate_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned long long *lkeys = reinterpret_cast<unsigned long long *>(smem);
   unsigned long long *lsum = lkeys + kPartSlots;
-  uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + kPartSlots);
+  uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + kPartSlots);  // [kPartSlots][kPartWords]
   const uint32_t nbk = P.nbk, stride = row_stride(nbk);
+  auto cnt = [&](uint32_t s, uint32_t b) -> uint32_t {
+    return (lcnt[s * kPartWords + (b >> 1)] >> ((b & 1u) * 16)) & 0xFFFFu;
+  };
   LaneStats st{0, 0, 0, 0};
   __shared__ uint32_t spilled;  // direct-path atomics from this workgroup
   if (threadIdx.x == 0) spilled = 0;
   const uint32_t bin = blockIdx.x;
   const uint32_t n = (P.diag & 1u) ? 0u : min(P.part_fill[bin], P.part_cap);  // diag 1: no records
   for (uint32_t i = threadIdx.x; i < kPartSlots; i += blockDim.x) lkeys[i] = lsum[i] = 0;
-  for (uint32_t i = threadIdx.x; i < kPartSlots * nbk; i += blockDim.x) lcnt[i] = 0;
+  for (uint32_t i = threadIdx.x; i < kPartSlots * kPartWords; i += blockDim.x) lcnt[i] = 0;
   __syncthreads();
   const ulonglong2 *rec = P.part_rec + (uint64_t)bin * P.part_cap;
-  constexpr int R = 4;  // records in flight per thread
+  constexpr int R = 8;  // records in flight per thread
   for (uint32_t i0 = 0; i0 < n; i0 += R * blockDim.x) {
     ulonglong2 v[R];
 #pragma unroll
@@ -1408,7 +1412,7 @@ __global__ __launch_bounds__(kPartBlock) void part_aggregate_kernel(IngestParams
         }
       }
       if (found != kNotFound) {
-        atomicAdd(&lcnt[found * nbk + bk], 1u);
+        atomicAdd(&lcnt[found * kPartWords + (bk >> 1)], 1u << ((bk & 1u) * 16));
         atomicAdd(&lsum[found], (unsigned long long)d);
       } else {
         direct_red(P, key, d, bk, stride, st);
@@ -1434,16 +1438,16 @@ __global__ __launch_bounds__(kPartBlock) void part_aggregate_kernel(IngestParams
     // the key's first-choice bucket in four independent loads (most keys sit
     // there); the full probe sequence only for the rest
     const ProbeSeq pr = probe_seq(key, P.log2cap);
-    unsigned long long q[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) q[j] = P.gkeys[pr.b1 * 4 + j];  // stale reads just miss: see g_find_insert
+    const ulonglong2 *bq = reinterpret_cast<const ulonglong2 *>(P.gkeys + pr.b1 * 4);
+    const ulonglong2 qa = bq[0], qb = bq[1];  // stale reads just miss: see g_find_insert
+    const unsigned long long q[4] = {qa.x, qa.y, qb.x, qb.y};
     uint32_t g = kNotFound;
 #pragma unroll
     for (int j = 3; j >= 0; --j) g = q[j] == key ? pr.b1 * 4 + j : g;
     if (g == kNotFound) g = g_find_insert(P.gkeys, key, P.log2cap, P.max_probe);
     if (g == kNotFound) {
       uint32_t calls = 0;
-      for (uint32_t b = 0; b < nbk; ++b) calls += lcnt[s * nbk + b];
+      for (uint32_t b = 0; b < nbk; ++b) calls += cnt(s, b);
       st.dropped += calls;
       continue;
     }
@@ -1457,13 +1461,21 @@ __global__ __launch_bounds__(kPartBlock) void part_aggregate_kernel(IngestParams
                                    __HIP_MEMORY_SCOPE_AGENT);
       old[kPartMaxBk] = __hip_atomic_load(row + row_sum_cell(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
+      // the row's (<= 3) 64-B segments as 16-B loads
+      constexpr uint32_t kSeg = (kPartMaxBk + kSegBuckets - 1) / kSegBuckets;
+      const uint32_t nseg = stride / 8;
+      ulonglong2 v[kSeg * 4];
 #pragma unroll
-      for (uint32_t b = 0; b < kPartMaxBk; ++b) old[b] = row[b < nbk ? row_count_cell(b) : 0u];
-      old[kPartMaxBk] = row[row_sum_cell(0)];
+      for (uint32_t k = 0; k < kSeg * 4; ++k)
+        v[k] = reinterpret_cast<const ulonglong2 *>(row)[(k / 4 < nseg ? k : k % 4)];
+      auto cell = [&](uint32_t c) -> unsigned long long { return (c & 1u) ? v[c / 2].y : v[c / 2].x; };
+#pragma unroll
+      for (uint32_t b = 0; b < kPartMaxBk; ++b) old[b] = b < nbk ? cell(row_count_cell(b)) : 0ULL;
+      old[kPartMaxBk] = cell(row_sum_cell(0));
     }
 #pragma unroll
     for (uint32_t b = 0; b < kPartMaxBk; ++b)
-      if (b < nbk && lcnt[s * nbk + b]) row[row_count_cell(b)] = old[b] + lcnt[s * nbk + b];
+      if (b < nbk && cnt(s, b)) row[row_count_cell(b)] = old[b] + cnt(s, b);
     row[row_sum_cell(0)] = old[kPartMaxBk] + lsum[s];
   }
   flush_stats(P, st);
@@ -1686,7 +1698,7 @@ hipError_t launch_ingest_part(const IngestParams &P, hipStream_t s) {
   else
     hipLaunchKernelGGL((part_scatter_kernel<-1>), dim3(grid), dim3(kPartBlock), 0, s, P);
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-  hipLaunchKernelGGL(part_aggregate_kernel, dim3(kPartBins), dim3(kPartBlock), kPartLdsBytes, s, P);
+  hipLaunchKernelGGL(part_aggregate_kernel, dim3(kPartBins), dim3(kPartAggBlock), kPartLdsBytes, s, P);
   return hipGetLastError();
 }
 
