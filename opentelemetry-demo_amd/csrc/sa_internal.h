@@ -86,12 +86,14 @@ constexpr uint32_t kPartBlock = 1024;     // scatter
 constexpr uint32_t kPartAggBlock = 512;   // aggregate: three workgroups per CU
 constexpr uint64_t kPartMaxSpans = 1ULL << 24;  // spans per partitioned launch
 // records per bin: 1.25x the mean plus slack (a fuller bin spills to the direct path)
-constexpr uint64_t kPartMaxCap = kPartMaxSpans / kPartBins * 5 / 4 + 64;
+constexpr uint64_t kPartMaxCap = kPartMaxSpans / kPartBins * 5 / 4 + 64;  // a multiple of 4
 // a bin holds < 2^16 records, so its LDS bucket counters are u16 pairs
 static_assert(kPartMaxCap < 65536, "u16 LDS counters");
 constexpr uint32_t kPartWords = (kPartMaxBk + 1) / 2;
 __host__ __device__ inline uint32_t part_bin(uint64_t key) { return (uint32_t)(key >> 53); }
 constexpr size_t kPartLdsBytes = (size_t)kPartSlots * (16 + 4 * kPartWords);  // 52 KiB
+// scatter: cur, lim, stage counts (u32 per bin) + a 4-record stage per bin
+constexpr size_t kPartScatterLds = (size_t)kPartBins * (12 + 4 * 16);  // 152 KiB
 
 // Counter row layout (gcounts, one row per key slot): 64-B segments of 8 u64
 // cells -- cell 0 holds that segment's share of the ns sum, cells 1..7 seven

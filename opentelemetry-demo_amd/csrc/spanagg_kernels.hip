@@ -1264,16 +1264,22 @@ __device__ __forceinline__ void direct_red(const IngestParams &P, uint64_t key, 
   atomicAdd(P.gcounts + (uint64_t)s * stride + row_sum_cell(bk), (unsigned long long)d);
 }
 
-template <int NB>
+// STAGE: records go through a 4-record (64-B) LDS stage per bin and leave as
+// whole 64-B chunks (runs are reserved in multiples of 4 records, so chunks
+// are segment-aligned); without it each record is its own 16-B store.
+template <int NB, bool STAGE>
 __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P) {
-  __shared__ uint32_t cur[kPartBins];  // phase 1: counts; phase 2: next record index
-  __shared__ uint32_t lim[kPartBins];  // end of this workgroup's run in the bin
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t *cur = reinterpret_cast<uint32_t *>(smem);  // phase 1: counts; then next record index
+  uint32_t *lim = cur + kPartBins;                      // end of this workgroup's run in the bin
+  uint32_t *scnt = lim + kPartBins;                     // STAGE: records staged per bin
+  ulonglong2 *stage = reinterpret_cast<ulonglong2 *>(scnt + kPartBins);  // [kPartBins][4]
   LaneStats st{0, 0, 0, 0};
   const uint32_t nbk = NB >= 0 ? (uint32_t)NB + 1 : P.nbk;
   const uint32_t stride = row_stride(nbk);
   uint64_t lo, hi;
   wg_range(P.n, lo, hi);
-  for (uint32_t b = threadIdx.x; b < kPartBins; b += blockDim.x) cur[b] = 0;
+  for (uint32_t b = threadIdx.x; b < kPartBins; b += blockDim.x) cur[b] = scnt[b] = 0;
   __syncthreads();
   // 1. records per bin in this workgroup's range (key column only)
   for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
@@ -1283,7 +1289,7 @@ __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P
   __syncthreads();
   // 2. reserve one contiguous run per bin (one returning atomic per bin)
   for (uint32_t b = threadIdx.x; b < kPartBins; b += blockDim.x) {
-    const uint32_t c = cur[b];
+    const uint32_t c = STAGE ? (cur[b] + 3u) & ~3u : cur[b];
     uint32_t base = 0;
     if (c) base = atomicAdd(&P.part_fill[b], c);
     const uint64_t b0 = (uint64_t)b * P.part_cap;
@@ -1291,10 +1297,17 @@ __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P
     lim[b] = (uint32_t)(b0 + min(base + c, P.part_cap));
   }
   __syncthreads();
+  auto put = [&](uint32_t b, const ulonglong2 &rec, uint64_t d, uint32_t bk) {  // one record, now
+    const uint32_t r = atomicAdd(&cur[b], 1u);
+    if (r < lim[b]) P.part_rec[r] = rec;  // write-back: partial lines merge in L2
+    else direct_red(P, rec.x, d, bk, stride, st);
+  };
   // 3. every span: stats, sketches, and its record (or the direct path);
-  //    U spans per thread with all their loads issued first
+  //    U spans per thread with all their loads issued first; rounds are
+  //    workgroup-uniform (STAGE flushes between them)
   constexpr int U = 4;
-  for (uint64_t i0 = lo + threadIdx.x; i0 < hi; i0 += U * blockDim.x) {
+  for (uint64_t r0 = lo; r0 < hi; r0 += (uint64_t)U * blockDim.x) {
+   const uint64_t i0 = r0 + threadIdx.x;
    uint64_t K[U], S0[U], E0[U], A[U], B[U];
    uint32_t M[U];
 #pragma unroll
@@ -1306,7 +1319,7 @@ __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P
      E0[u] = ok ? P.end[i] : 0;
      A[u] = ok ? P.w0[i] : 0;
      B[u] = ok ? P.w1[i] : 0;
-     M[u] = ok ? P.meta[i] : 0xFFFFu;  // invalid service marks the padding lane
+     M[u] = ok ? P.meta[i] : 0xFFFFu;  // padding lanes are skipped below
    }
    // sketch phase A for all U spans: the HLL register reads are issued
    // together (unconditional: a skipped span reads the first byte)
@@ -1345,11 +1358,16 @@ __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P
     const uint32_t ws = WS[u];
     if (key != 0 && !(P.diag & 1u)) {
       const uint32_t b = part_bin(key);
-      const uint32_t r = d < (1ULL << 57) ? atomicAdd(&cur[b], 1u) : 0xFFFFFFFFu;
-      if (r < lim[b])
-        P.part_rec[r] = make_ulonglong2(key, (d << 7) | bk);  // write-back: partial lines merge in L2
-      else
+      const ulonglong2 rec = make_ulonglong2(key, (d << 7) | bk);
+      if (d >= (1ULL << 57)) {
         direct_red(P, key, d, bk, stride, st);
+      } else if (STAGE) {
+        const uint32_t slot = atomicAdd(&scnt[b], 1u);
+        if (slot < 4) stage[b * 4 + slot] = rec;
+        else put(b, rec, d, bk);
+      } else {
+        put(b, rec, d, bk);
+      }
     }
     // ERROR spans: the exact per-(window, slot) counter (count-min cells are
     // folded from it); no slot (key 0, table full): the cells directly
@@ -1362,6 +1380,34 @@ __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P
 #pragma unroll
    for (int u = 0; u < U; ++u)
      if ((CUR[u] & 0xFFu) < RHO[u]) hll_raise(REG[u], RHO[u]);
+   if constexpr (STAGE) {  // full stages leave as one 64-B chunk
+     __syncthreads();
+     for (uint32_t b = threadIdx.x; b < kPartBins; b += blockDim.x) {
+       if (scnt[b] < 4) continue;
+       const uint32_t r = cur[b];
+       cur[b] = r + 4;
+       scnt[b] = 0;
+#pragma unroll
+       for (int j = 0; j < 4; ++j) {
+         const ulonglong2 rec = stage[b * 4 + j];
+         if (r + j < lim[b]) P.part_rec[r + j] = rec;
+         else direct_red(P, rec.x, rec.y >> 7, (uint32_t)(rec.y & 127u), stride, st);
+       }
+     }
+     __syncthreads();
+   }
+  }
+  // partial stages, then zero records over the run's unused tail (the
+  // padding, and the slots of spans that took the direct path)
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < kPartBins; b += blockDim.x) {
+    if constexpr (STAGE) {
+      for (uint32_t j = 0; j < scnt[b]; ++j) {
+        const ulonglong2 rec = stage[b * 4 + j];
+        put(b, rec, rec.y >> 7, (uint32_t)(rec.y & 127u));
+      }
+    }
+    for (uint32_t r = cur[b]; r < lim[b]; ++r) P.part_rec[r] = make_ulonglong2(0, 0);
   }
   flush_stats(P, st);
 }
@@ -1693,16 +1739,27 @@ hipError_t launch_ingest_part(const IngestParams &P, hipStream_t s) {
     return v ? (uint32_t)std::max(1, std::atoi(v)) : 256u;
   }();
   const uint32_t grid = (uint32_t)std::min<uint64_t>(max_grid, (P.n + kPartBlock - 1) / kPartBlock);
-  if (P.nneg == 0 && P.npos == 16)
-    hipLaunchKernelGGL((part_scatter_kernel<16>), dim3(grid), dim3(kPartBlock), 0, s, P);
-  else
-    hipLaunchKernelGGL((part_scatter_kernel<-1>), dim3(grid), dim3(kPartBlock), 0, s, P);
+  static const bool stage = [] {
+    const char *v = std::getenv("SPANAGG_PART_STAGE");  // tuning knob for A/B runs
+    return !(v && std::atoi(v) == 0);
+  }();
+  const bool b16 = P.nneg == 0 && P.npos == 16;
+  const void *fn = stage ? (b16 ? (const void *)&part_scatter_kernel<16, true> : (const void *)&part_scatter_kernel<-1, true>)
+                         : (b16 ? (const void *)&part_scatter_kernel<16, false> : (const void *)&part_scatter_kernel<-1, false>);
+  void *args[] = {const_cast<IngestParams *>(&P)};
+  if (hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(kPartBlock), args, kPartScatterLds, s); e != hipSuccess)
+    return e;
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   hipLaunchKernelGGL(part_aggregate_kernel, dim3(kPartBins), dim3(kPartAggBlock), kPartLdsBytes, s, P);
   return hipGetLastError();
 }
 
 hipError_t prepare_ingest_part() {
+  for (const void *fn : {(const void *)&part_scatter_kernel<16, true>, (const void *)&part_scatter_kernel<-1, true>,
+                         (const void *)&part_scatter_kernel<16, false>, (const void *)&part_scatter_kernel<-1, false>})
+    if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPartScatterLds);
+        e != hipSuccess)
+      return e;
   return hipFuncSetAttribute((const void *)&part_aggregate_kernel,
                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPartLdsBytes);
 }
