@@ -1264,6 +1264,9 @@ __device__ __forceinline__ void direct_red(const IngestParams &P, uint64_t key, 
   atomicAdd(P.gcounts + (uint64_t)s * stride + row_sum_cell(bk), (unsigned long long)d);
 }
 
+#ifndef PART_U
+#define PART_U 4
+#endif
 // STAGE: records go through a 4-record (64-B) LDS stage per bin and leave as
 // whole 64-B chunks (runs are reserved in multiples of 4 records, so chunks
 // are segment-aligned); without it each record is its own 16-B store.
@@ -1281,10 +1284,19 @@ __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P
   wg_range(P.n, lo, hi);
   for (uint32_t b = threadIdx.x; b < kPartBins; b += blockDim.x) cur[b] = scnt[b] = 0;
   __syncthreads();
-  // 1. records per bin in this workgroup's range (key column only)
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const uint64_t key = P.key[i];
-    if (key != 0) atomicAdd(&cur[part_bin(key)], 1u);
+  // 1. records per bin in this workgroup's range (key column only; 8 loads
+  //    in flight per thread)
+  constexpr int U1 = 8;
+  for (uint64_t i0 = lo + threadIdx.x; i0 < hi; i0 += (uint64_t)U1 * blockDim.x) {
+    uint64_t k[U1];
+#pragma unroll
+    for (int u = 0; u < U1; ++u) {
+      const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+      k[u] = i < hi ? P.key[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U1; ++u)
+      if (k[u] != 0) atomicAdd(&cur[part_bin(k[u])], 1u);
   }
   __syncthreads();
   // 2. reserve one contiguous run per bin (one returning atomic per bin)
@@ -1305,7 +1317,7 @@ __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P
   // 3. every span: stats, sketches, and its record (or the direct path);
   //    U spans per thread with all their loads issued first; rounds are
   //    workgroup-uniform (STAGE flushes between them)
-  constexpr int U = 4;
+  constexpr int U = PART_U;
   for (uint64_t r0 = lo; r0 < hi; r0 += (uint64_t)U * blockDim.x) {
    const uint64_t i0 = r0 + threadIdx.x;
    uint64_t K[U], S0[U], E0[U], A[U], B[U];
