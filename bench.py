@@ -245,6 +245,7 @@ def main():
         s.wait_event(start)
     for i in range(args.steps):
         step(i)
+    enqueue_s = time.perf_counter() - t0  # host time to enqueue the steps
     for s, e_ in zip(streams, ends):
         e_.record(s)
     torch.cuda.synchronize(device)
@@ -292,6 +293,7 @@ def main():
                          "pipelined": {"streams": len(streams), "device_ms_per_step": device_ms,
                                        "achieved": piped, "frac": piped / HBM_PEAK_GBS}},
             "merge_ms": merge_ms, "calls_check": calls_ok,
+            "host_enqueue_us_per_step": enqueue_s * 1e6 / max(1, args.steps),
         }
         if world == 1 and not args.no_cpu_baseline and wl is not None:
             port, conn = cpu_baseline(wl, args.cpu_seconds)
