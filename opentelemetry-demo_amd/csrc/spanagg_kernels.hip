@@ -470,7 +470,6 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_lds_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t cap = 1u << P.log2cap;
-  const uint32_t mask = cap - 1;
   const uint32_t nbk = P.nbk;
   const uint32_t nw = (nbk + 1) >> 1;
   const uint32_t diag = DIAG ? P.diag : 0u;
