@@ -15,13 +15,19 @@ from spanagg.synth import generate_c2  # noqa: E402
 
 n = int(os.environ.get("PROF_SPANS", 10_000_000))
 reps = int(os.environ.get("PROF_REPS", 5))
-wl = generate_c2(n, seed=42)
+if os.environ.get("PROF_WORKLOAD") == "c4":  # 1 M series, HBM table (partitioned path)
+    from spanagg.synth import generate_highcard
+    batch, _, first = generate_highcard(n, seed=7)
+    n_services, kcap = 1, 1_200_000
+else:
+    wl = generate_c2(n, seed=42)
+    batch, first, n_services, kcap = wl.batch, wl.first_window, wl.n_services, 1500
 cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).cuda()
-        for c in wl.batch.columns()]
+        for c in batch.columns()]
 s = torch.cuda.Stream()
 flags = int(os.environ.get("PROF_FLAGS", 0))
-with Engine(Config(n_services=wl.n_services, n_windows=16, flags=flags)) as e:
-    e.window_advance(wl.first_window)
+with Engine(Config(n_services=n_services, n_windows=16, flags=flags, key_capacity=kcap)) as e:
+    e.window_advance(first)
     for _ in range(reps):
         e.ingest_device(*cols, n=n, stream=s.cuda_stream)
     torch.cuda.synchronize()
