@@ -79,21 +79,29 @@ struct IngestParams {
 // every span's record by the top 11 bits of its key, part_aggregate_kernel
 // aggregates one bin per workgroup in an LDS table and adds it to the HBM
 // counters once per key.
-constexpr uint32_t kPartBins = 2048;
-constexpr uint32_t kPartSlots = 1024;     // LDS table slots per bin (~490 keys per bin at 1 M keys)
+#ifndef SA_PART_BIN_BITS
+#define SA_PART_BIN_BITS 11
+#endif
+constexpr uint32_t kPartBinBits = SA_PART_BIN_BITS;
+constexpr uint32_t kPartBins = 1u << kPartBinBits;
+// LDS table slots per bin: ~2x the mean keys per bin at 1 M keys
+constexpr uint32_t kPartSlotBits = 21 - kPartBinBits;
+constexpr uint32_t kPartSlots = 1u << kPartSlotBits;
+// records staged per bin in the scatter's LDS (one chunk = kPartStage x 16 B)
+constexpr uint32_t kPartStage = kPartBinBits >= 11 ? 4 : 8;
 constexpr uint32_t kPartMaxBk = 17;       // LDS counter row: nbk <= 17 (default buckets)
 constexpr uint32_t kPartBlock = 1024;     // scatter
-constexpr uint32_t kPartAggBlock = 512;   // aggregate: three workgroups per CU
+constexpr uint32_t kPartAggBlock = kPartSlots >= 2048 ? 1024 : 512;  // aggregate workgroup
 constexpr uint64_t kPartMaxSpans = 1ULL << 24;  // spans per partitioned launch
 // records per bin: 1.25x the mean plus slack (a fuller bin spills to the direct path)
-constexpr uint64_t kPartMaxCap = kPartMaxSpans / kPartBins * 5 / 4 + 64;  // a multiple of 4
+constexpr uint64_t kPartMaxCap = kPartMaxSpans / kPartBins * 5 / 4 + 64;  // a multiple of kPartStage
 // a bin holds < 2^16 records, so its LDS bucket counters are u16 pairs
 static_assert(kPartMaxCap < 65536, "u16 LDS counters");
 constexpr uint32_t kPartWords = (kPartMaxBk + 1) / 2;
-__host__ __device__ inline uint32_t part_bin(uint64_t key) { return (uint32_t)(key >> 53); }
-constexpr size_t kPartLdsBytes = (size_t)kPartSlots * (16 + 4 * kPartWords);  // 52 KiB
+__host__ __device__ inline uint32_t part_bin(uint64_t key) { return (uint32_t)(key >> (64 - kPartBinBits)); }
+constexpr size_t kPartLdsBytes = (size_t)kPartSlots * (16 + 4 * kPartWords);  // 52 KiB at 1,024 slots
 // scatter: cur, lim, stage counts (u32 per bin) + a 4-record stage per bin
-constexpr size_t kPartScatterLds = (size_t)kPartBins * (12 + 4 * 16);  // 152 KiB
+constexpr size_t kPartScatterLds = (size_t)kPartBins * (12 + kPartStage * 16);  // 152 / 140 KiB
 
 // Counter row layout (gcounts, one row per key slot): 64-B segments of 8 u64
 // cells -- cell 0 holds that segment's share of the ns sum, cells 1..7 seven

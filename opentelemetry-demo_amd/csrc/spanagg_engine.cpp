@@ -507,7 +507,8 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
     P.part_fill = e->part_fill;
     // a multiple of 4 records: staged 64-B chunks stay segment-aligned
     P.part_cap = (uint32_t)std::min<uint64_t>(
-        per_bin_max, ((b->n + sa::kPartBins - 1) / sa::kPartBins * 5 / 4 + 64 + 3) & ~3ULL);
+        per_bin_max, ((b->n + sa::kPartBins - 1) / sa::kPartBins * 5 / 4 + 64 + sa::kPartStage - 1) &
+                         ~(uint64_t)(sa::kPartStage - 1));
     st = sa::launch_ingest_part(P, s);
   } else {
     st = sa::launch_ingest_hbm(P, grid, s, e->variant);

@@ -1275,7 +1275,7 @@ __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P
   uint32_t *cur = reinterpret_cast<uint32_t *>(smem);  // phase 1: counts; then next record index
   uint32_t *lim = cur + kPartBins;                      // end of this workgroup's run in the bin
   uint32_t *scnt = lim + kPartBins;                     // STAGE: records staged per bin
-  ulonglong2 *stage = reinterpret_cast<ulonglong2 *>(scnt + kPartBins);  // [kPartBins][4]
+  ulonglong2 *stage = reinterpret_cast<ulonglong2 *>(scnt + kPartBins);  // [kPartBins][kPartStage]
   LaneStats st{0, 0, 0, 0};
   const uint32_t nbk = NB >= 0 ? (uint32_t)NB + 1 : P.nbk;
   const uint32_t stride = row_stride(nbk);
@@ -1300,7 +1300,7 @@ __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P
   __syncthreads();
   // 2. reserve one contiguous run per bin (one returning atomic per bin)
   for (uint32_t b = threadIdx.x; b < kPartBins; b += blockDim.x) {
-    const uint32_t c = STAGE ? (cur[b] + 3u) & ~3u : cur[b];
+    const uint32_t c = STAGE ? (cur[b] + kPartStage - 1) & ~(kPartStage - 1) : cur[b];
     uint32_t base = 0;
     if (c) base = atomicAdd(&P.part_fill[b], c);
     const uint64_t b0 = (uint64_t)b * P.part_cap;
@@ -1374,7 +1374,7 @@ __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P
         direct_red(P, key, d, bk, stride, st);
       } else if (STAGE) {
         const uint32_t slot = atomicAdd(&scnt[b], 1u);
-        if (slot < 4) stage[b * 4 + slot] = rec;
+        if (slot < kPartStage) stage[b * kPartStage + slot] = rec;
         else put(b, rec, d, bk);
       } else {
         put(b, rec, d, bk);
@@ -1394,13 +1394,13 @@ __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P
    if constexpr (STAGE) {  // full stages leave as one 64-B chunk
      __syncthreads();
      for (uint32_t b = threadIdx.x; b < kPartBins; b += blockDim.x) {
-       if (scnt[b] < 4) continue;
+       if (scnt[b] < kPartStage) continue;
        const uint32_t r = cur[b];
-       cur[b] = r + 4;
+       cur[b] = r + kPartStage;
        scnt[b] = 0;
 #pragma unroll
-       for (int j = 0; j < 4; ++j) {
-         const ulonglong2 rec = stage[b * 4 + j];
+       for (int j = 0; j < (int)kPartStage; ++j) {
+         const ulonglong2 rec = stage[b * kPartStage + j];
          if (r + j < lim[b]) P.part_rec[r + j] = rec;
          else direct_red(P, rec.x, rec.y >> 7, (uint32_t)(rec.y & 127u), stride, st);
        }
@@ -1414,7 +1414,7 @@ __global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P
   for (uint32_t b = threadIdx.x; b < kPartBins; b += blockDim.x) {
     if constexpr (STAGE) {
       for (uint32_t j = 0; j < scnt[b]; ++j) {
-        const ulonglong2 rec = stage[b * 4 + j];
+        const ulonglong2 rec = stage[b * kPartStage + j];
         put(b, rec, rec.y >> 7, (uint32_t)(rec.y & 127u));
       }
     }
@@ -1459,7 +1459,7 @@ __global__ __launch_bounds__(kPartAggBlock) void part_aggregate_kernel(IngestPar
       if (key == 0) continue;
       const uint64_t d = v[u].y >> 7;
       const uint32_t bk = (uint32_t)(v[u].y & 127u);
-      uint32_t s = ((uint32_t)key * 0x9E3779B1u) >> (32 - 10), found = kNotFound;
+      uint32_t s = ((uint32_t)key * 0x9E3779B1u) >> (32 - kPartSlotBits), found = kNotFound;
       for (int pr = 0; pr < 64; ++pr, s = (s + 1) & (kPartSlots - 1)) {
         unsigned long long k = lkeys[s];
         if (k == 0) k = atomicCAS(&lkeys[s], 0ULL, key);
