@@ -153,7 +153,8 @@ def main():
                          "let consecutive launches overlap); 1 = strictly serial launches")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--traffic", default=None,
+                    help="PMC traffic summary (default profiles/traffic.json, profiles/traffic_c4.json for c4)")
     ap.add_argument("--host-otlp-spans", type=int, default=500_000,
                     help="spans for the Node host's OTLP->GPU rate (0 = skip)")
     ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1),
@@ -275,7 +276,9 @@ def main():
     if rank == 0:
         value = world * n * args.steps / elapsed
         achieved = BYTES_PER_SPAN * n / (kernel_ms * 1e-3) / 1e9
-        traffic, tsrc = load_traffic(args.traffic, args.workload)
+        tpath = args.traffic or os.path.join(
+            ROOT, "profiles", "traffic.json" if args.workload == "c2" else f"traffic_{args.workload}.json")
+        traffic, tsrc = load_traffic(tpath, args.workload)
         piped = BYTES_PER_SPAN * n / (device_ms * 1e-3) / 1e9
         result = {
             "metric": METRIC, "value": value, "unit": "spans/s", "n_gpus": world,
