@@ -88,7 +88,10 @@ constexpr uint32_t kPartBins = 1u << kPartBinBits;
 constexpr uint32_t kPartSlotBits = 21 - kPartBinBits;
 constexpr uint32_t kPartSlots = 1u << kPartSlotBits;
 // records staged per bin in the scatter's LDS (one chunk = kPartStage x 16 B)
-constexpr uint32_t kPartStage = kPartBinBits >= 11 ? 4 : 8;
+#ifndef SA_PART_STAGE
+#define SA_PART_STAGE (SA_PART_BIN_BITS >= 11 ? 4 : 8)
+#endif
+constexpr uint32_t kPartStage = SA_PART_STAGE;
 constexpr uint32_t kPartMaxBk = 17;       // LDS counter row: nbk <= 17 (default buckets)
 constexpr uint32_t kPartBlock = 1024;     // scatter
 constexpr uint32_t kPartAggBlock = kPartSlots >= 2048 ? 1024 : 512;  // aggregate workgroup

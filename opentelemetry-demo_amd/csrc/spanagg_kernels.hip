@@ -1269,8 +1269,11 @@ __device__ __forceinline__ void direct_red(const IngestParams &P, uint64_t key, 
 // STAGE: records go through a 4-record (64-B) LDS stage per bin and leave as
 // whole 64-B chunks (runs are reserved in multiples of 4 records, so chunks
 // are segment-aligned); without it each record is its own 16-B store.
+#ifndef SA_PART_WAVES_EU
+#define SA_PART_WAVES_EU 1  // 8 caps VGPRs at 64: two 1,024-thread workgroups per CU
+#endif
 template <int NB, bool STAGE>
-__global__ __launch_bounds__(kPartBlock) void part_scatter_kernel(IngestParams P) {
+__global__ __launch_bounds__(kPartBlock, SA_PART_WAVES_EU) void part_scatter_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint32_t *cur = reinterpret_cast<uint32_t *>(smem);  // phase 1: counts; then next record index
   uint32_t *lim = cur + kPartBins;                      // end of this workgroup's run in the bin
