@@ -355,6 +355,46 @@ def test_partitioned_hbm_path_spills_vs_oracle(shape, monkeypatch):
             assert np.array_equal(wins[wid][0], hll) and np.array_equal(wins[wid][1], cms)
 
 
+def _check_highcard(e, batch, n):
+    res = e.flush()
+    o = _oracle_run(batch, 1)
+    assert_red_equal(res, o.series())
+    for wid in o.window_ids():
+        sk = e.window_read(wid)
+        hll, cms = o.window(wid)
+        assert np.array_equal(sk.hll, hll) and np.array_equal(sk.cms, cms), wid
+    st = e.stats()
+    assert st["dropped_table_full"] == 0
+    # size-independent: every non-zero-key span is one call, in one series
+    assert int(res.calls.sum()) == n - st["zero_key"]
+    assert len(np.unique(res.key_hash)) == len(res.key_hash)
+
+
+def test_c4_full_size_bit_exact():
+    """BASELINE config 4 at full size: 1 M keys (2,000 routes x 500 pods),
+    10 M spans in one launch of the partitioned path (the bench workload)."""
+    n = 10_000_000
+    batch, _, w0 = generate_highcard(n)
+    with Engine(Config(n_services=1, n_windows=16, key_capacity=1_200_000)) as e:
+        assert e.stats()["small_table"] == 0
+        e.window_advance(w0)
+        e.ingest(batch)
+        _check_highcard(e, batch, n)
+
+
+def test_partitioned_batch_above_launch_limit_is_split():
+    """One sa_ingest of 2^24 + 1,001 spans: more than one partitioned launch
+    takes (kPartMaxSpans), so the engine splits it into two launches whose
+    bin counters and record runs must not leak into each other."""
+    n = (1 << 24) + 1001
+    batch, _, w0 = generate_highcard(n, seed=9, routes=400, pods=250)
+    with Engine(Config(n_services=1, n_windows=16, key_capacity=200_000)) as e:
+        assert e.stats()["small_table"] == 0
+        e.window_advance(w0)
+        e.ingest(batch)
+        _check_highcard(e, batch, n)
+
+
 def test_repeat_runs_identical():
     wl = generate_c2(1_000_000, seed=77)
     outs = []
