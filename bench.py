@@ -147,7 +147,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--spans", type=int, default=10_000_000, help="spans per step per GPU")
-    ap.add_argument("--workload", choices=["c2", "c4"], default="c2")
+    ap.add_argument("--workload", choices=["c2", "c4", "c4zipf"], default="c2")
     ap.add_argument("--streams", type=int, default=2,
                     help="launch streams the steps alternate over (the engine's two slab sets "
                          "let consecutive launches overlap); 1 = strictly serial launches")
@@ -201,10 +201,12 @@ def main():
                     "durations, ~10 spans/trace, per-service HLL p=14 + error count-min 4x2048, "
                     "10 s windows")
     else:
-        batch, _, first_window = generate_highcard(n, seed=7 + rank)
+        zs = 1.1 if args.workload == "c4zipf" else 0.0
+        batch, _, first_window = generate_highcard(n, seed=7 + rank, zipf_s=zs)
         wl, n_services, key_capacity = None, 1, 1_200_000
-        workload = ("C4: 1,000,000 series (2,000 http.route x 500 k8s.pod.name), uniform, "
-                    "HBM key table, HLL + count-min")
+        workload = ("C4: 1,000,000 series (2,000 http.route x 500 k8s.pod.name), "
+                    + (f"Zipf(s={zs}) over keys" if zs else "uniform")
+                    + ", HBM key table, HLL + count-min")
     cols = []
     for c in batch.columns():
         t = torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32))

@@ -104,7 +104,12 @@ constexpr uint32_t kPartWords = (kPartMaxBk + 1) / 2;
 __host__ __device__ inline uint32_t part_bin(uint64_t key) { return (uint32_t)(key >> (64 - kPartBinBits)); }
 constexpr size_t kPartLdsBytes = (size_t)kPartSlots * (16 + 4 * kPartWords);  // 52 KiB at 1,024 slots
 // scatter: cur, lim, stage counts (u32 per bin) + a 4-record stage per bin
-constexpr size_t kPartScatterLds = (size_t)kPartBins * (12 + kPartStage * 16);  // 152 / 140 KiB
+// scatter overflow table: spans whose bin run is full are pre-aggregated per
+// workgroup (key, ns sum, u32 bucket counts) and leave as one row update each
+constexpr uint32_t kPartHotBits = 6;
+constexpr uint32_t kPartHot = 1u << kPartHotBits;
+constexpr size_t kPartScatterLds =
+    (size_t)kPartBins * (12 + kPartStage * 16) + (size_t)kPartHot * (16 + 4 * kPartMaxBk);  // 157 KiB
 
 // Counter row layout (gcounts, one row per key slot): 64-B segments of 8 u64
 // cells -- cell 0 holds that segment's share of the ns sum, cells 1..7 seven

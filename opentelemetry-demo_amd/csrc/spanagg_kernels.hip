@@ -1279,12 +1279,17 @@ __global__ __launch_bounds__(kPartBlock, SA_PART_WAVES_EU) void part_scatter_ker
   uint32_t *lim = cur + kPartBins;                      // end of this workgroup's run in the bin
   uint32_t *scnt = lim + kPartBins;                     // STAGE: records staged per bin
   ulonglong2 *stage = reinterpret_cast<ulonglong2 *>(scnt + kPartBins);  // [kPartBins][kPartStage]
+  unsigned long long *hkey = reinterpret_cast<unsigned long long *>(stage + kPartBins * kPartStage);
+  unsigned long long *hsum = hkey + kPartHot;                           // overflow table
+  uint32_t *hcnt = reinterpret_cast<uint32_t *>(hsum + kPartHot);       // [kPartHot][kPartMaxBk]
   LaneStats st{0, 0, 0, 0};
   const uint32_t nbk = NB >= 0 ? (uint32_t)NB + 1 : P.nbk;
   const uint32_t stride = row_stride(nbk);
   uint64_t lo, hi;
   wg_range(P.n, lo, hi);
   for (uint32_t b = threadIdx.x; b < kPartBins; b += blockDim.x) cur[b] = scnt[b] = 0;
+  for (uint32_t h = threadIdx.x; h < kPartHot; h += blockDim.x) hkey[h] = hsum[h] = 0;
+  for (uint32_t h = threadIdx.x; h < kPartHot * kPartMaxBk; h += blockDim.x) hcnt[h] = 0;
   __syncthreads();
   // 1. records per bin in this workgroup's range (key column only; 8 loads
   //    in flight per thread)
@@ -1311,10 +1316,26 @@ __global__ __launch_bounds__(kPartBlock, SA_PART_WAVES_EU) void part_scatter_ker
     lim[b] = (uint32_t)(b0 + min(base + c, P.part_cap));
   }
   __syncthreads();
+  // a span whose bin run is full: into the overflow table (hot keys of a
+  // skewed mix overfill their bins; per-span global atomics on one row would
+  // serialise), else the direct path
+  auto spill = [&](uint64_t key, uint64_t d, uint32_t bk) {
+    uint32_t h = ((uint32_t)key * 0x9E3779B1u) >> (32 - kPartHotBits);
+    for (int pr = 0; pr < 8; ++pr, h = (h + 1) & (kPartHot - 1)) {
+      unsigned long long k = hkey[h];
+      if (k == 0) k = atomicCAS(&hkey[h], 0ULL, (unsigned long long)key);
+      if (k == 0 || k == key) {
+        atomicAdd(&hcnt[h * kPartMaxBk + bk], 1u);
+        atomicAdd(&hsum[h], (unsigned long long)d);
+        return;
+      }
+    }
+    direct_red(P, key, d, bk, stride, st);
+  };
   auto put = [&](uint32_t b, const ulonglong2 &rec, uint64_t d, uint32_t bk) {  // one record, now
     const uint32_t r = atomicAdd(&cur[b], 1u);
     if (r < lim[b]) P.part_rec[r] = rec;  // write-back: partial lines merge in L2
-    else direct_red(P, rec.x, d, bk, stride, st);
+    else spill(rec.x, d, bk);
   };
   // 3. every span: stats, sketches, and its record (or the direct path);
   //    U spans per thread with all their loads issued first; rounds are
@@ -1405,7 +1426,7 @@ __global__ __launch_bounds__(kPartBlock, SA_PART_WAVES_EU) void part_scatter_ker
        for (int j = 0; j < (int)kPartStage; ++j) {
          const ulonglong2 rec = stage[b * kPartStage + j];
          if (r + j < lim[b]) P.part_rec[r + j] = rec;
-         else direct_red(P, rec.x, rec.y >> 7, (uint32_t)(rec.y & 127u), stride, st);
+         else spill(rec.x, rec.y >> 7, (uint32_t)(rec.y & 127u));
        }
      }
      __syncthreads();
@@ -1422,6 +1443,22 @@ __global__ __launch_bounds__(kPartBlock, SA_PART_WAVES_EU) void part_scatter_ker
       }
     }
     for (uint32_t r = cur[b]; r < lim[b]; ++r) P.part_rec[r] = make_ulonglong2(0, 0);
+  }
+  // the overflow table: one atomic per non-zero cell per key (the aggregate
+  // kernel's plain row updates come after this kernel)
+  __syncthreads();
+  for (uint32_t h = threadIdx.x; h < kPartHot; h += blockDim.x) {
+    const unsigned long long key = hkey[h];
+    if (key == 0) continue;
+    const uint32_t g = g_find_insert(P.gkeys, key, P.log2cap, P.max_probe);
+    if (g == kNotFound) {
+      for (uint32_t b = 0; b < nbk; ++b) st.dropped += hcnt[h * kPartMaxBk + b];
+      continue;
+    }
+    unsigned long long *row = P.gcounts + (uint64_t)g * stride;
+    for (uint32_t b = 0; b < nbk; ++b)
+      if (const uint32_t c = hcnt[h * kPartMaxBk + b]) atomicAdd(row + row_count_cell(b), (unsigned long long)c);
+    atomicAdd(row + row_sum_cell(0), hsum[h]);
   }
   flush_stats(P, st);
 }
