@@ -89,7 +89,7 @@ constexpr uint32_t kPartSlotBits = 21 - kPartBinBits;
 constexpr uint32_t kPartSlots = 1u << kPartSlotBits;
 // records staged per bin in the scatter's LDS (one chunk = kPartStage x 16 B)
 #ifndef SA_PART_STAGE
-#define SA_PART_STAGE (SA_PART_BIN_BITS >= 11 ? 4 : 8)
+#define SA_PART_STAGE (SA_PART_BIN_BITS >= 11 ? 2 : 8)  // 2: LDS left for a 512-entry overflow table
 #endif
 constexpr uint32_t kPartStage = SA_PART_STAGE;
 constexpr uint32_t kPartMaxBk = 17;       // LDS counter row: nbk <= 17 (default buckets)
@@ -106,10 +106,13 @@ constexpr size_t kPartLdsBytes = (size_t)kPartSlots * (16 + 4 * kPartWords);  //
 // scatter: cur, lim, stage counts (u32 per bin) + a 4-record stage per bin
 // scatter overflow table: spans whose bin run is full are pre-aggregated per
 // workgroup (key, ns sum, u32 bucket counts) and leave as one row update each
-constexpr uint32_t kPartHotBits = 6;
+#ifndef SA_PART_HOT_BITS
+#define SA_PART_HOT_BITS 9
+#endif
+constexpr uint32_t kPartHotBits = SA_PART_HOT_BITS;
 constexpr uint32_t kPartHot = 1u << kPartHotBits;
 constexpr size_t kPartScatterLds =
-    (size_t)kPartBins * (12 + kPartStage * 16) + (size_t)kPartHot * (16 + 4 * kPartMaxBk);  // 157 KiB
+    (size_t)kPartBins * (12 + kPartStage * 16) + (size_t)kPartHot * (16 + 4 * kPartMaxBk);  // 130 KiB
 
 // Counter row layout (gcounts, one row per key slot): 64-B segments of 8 u64
 // cells -- cell 0 holds that segment's share of the ns sum, cells 1..7 seven

@@ -1266,9 +1266,9 @@ __device__ __forceinline__ void direct_red(const IngestParams &P, uint64_t key, 
 #ifndef PART_U
 #define PART_U 4
 #endif
-// STAGE: records go through a 4-record (64-B) LDS stage per bin and leave as
-// whole 64-B chunks (runs are reserved in multiples of 4 records, so chunks
-// are segment-aligned); without it each record is its own 16-B store.
+// STAGE: records go through a kPartStage-record LDS stage per bin and leave
+// as whole chunks (runs are reserved in multiples of kPartStage records, so
+// chunks stay aligned); without it each record is its own 16-B store.
 #ifndef SA_PART_WAVES_EU
 #define SA_PART_WAVES_EU 1  // 8 caps VGPRs at 64: two 1,024-thread workgroups per CU
 #endif
