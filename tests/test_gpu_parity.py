@@ -395,6 +395,27 @@ def test_partitioned_batch_above_launch_limit_is_split():
         _check_highcard(e, batch, n)
 
 
+def test_partitioned_one_bin_overflow_table_full_vs_oracle():
+    """Every key in one bin (top 11 bits fixed), 60,000 distinct keys: the bin
+    run overflows at once, each scatter workgroup's LDS overflow table fills
+    (> 512 distinct spilling keys) and the rest takes the direct path; the
+    one bin's aggregate sees more keys than its LDS table holds."""
+    n = 2_000_000
+    batch, _, w0 = generate_highcard(n, seed=11, routes=400, pods=250)
+    cols = batch.columns()
+    rng = np.random.Generator(np.random.PCG64(11))
+    ids = rng.integers(0, 60_000, n).astype(np.uint64)
+    with np.errstate(over="ignore"):
+        low = (ids + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+    keys = (np.uint64(0x2AB) << np.uint64(53)) | (low >> np.uint64(11)) | np.uint64(1)
+    one_bin = SpanBatch(keys, *cols[1:])
+    with Engine(Config(n_services=1, n_windows=16, key_capacity=200_000)) as e:
+        assert e.stats()["small_table"] == 0
+        e.window_advance(w0)
+        e.ingest(one_bin)
+        _check_highcard(e, one_bin, n)
+
+
 def test_repeat_runs_identical():
     wl = generate_c2(1_000_000, seed=77)
     outs = []
