@@ -1,0 +1,35 @@
+"""bench.py host logic on CPU: traffic summaries are picked by workload, and the
+CPU-baseline worker (the oracle port, bench.py's cpu_baseline leg) reports a
+rate.  The timed GPU steps themselves run only on the GPU box."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+@pytest.mark.parametrize("workload,fname", [("c2", "traffic.json"), ("c4", "traffic_c4.json")])
+def test_traffic_summary_matches_workload(workload, fname):
+    path = os.path.join(ROOT, "profiles", fname)
+    traffic, src = bench.load_traffic(path, workload)
+    assert src == os.path.join("profiles", fname)
+    assert traffic > 44 * 10_000_000 * 0.9  # at least the algorithmic bytes (minus noise)
+
+
+def test_traffic_summary_of_another_workload_is_not_used():
+    path = os.path.join(ROOT, "profiles", "traffic_c4.json")
+    assert bench.load_traffic(path, "c4zipf") == (None, None)
+    assert bench.load_traffic(os.path.join(ROOT, "profiles", "missing.json"), "c2") == (None, None)
+
+
+def test_cpu_worker_reports_a_rate():
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--cpu-worker", "1",
+                        "--cpu-seconds", "0.2"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["spans"] >= 2_000_000 and r["seconds"] > 0
