@@ -1269,6 +1269,9 @@ __device__ __forceinline__ void direct_red(const IngestParams &P, uint64_t key, 
 // STAGE: records go through a kPartStage-record LDS stage per bin and leave
 // as whole chunks (runs are reserved in multiples of kPartStage records, so
 // chunks stay aligned); without it each record is its own 16-B store.
+#ifndef SA_PART_SKIP_USED
+#define SA_PART_SKIP_USED 1
+#endif
 #ifndef SA_PART_WAVES_EU
 #define SA_PART_WAVES_EU 1  // 8 caps VGPRs at 64: two 1,024-thread workgroups per CU
 #endif
@@ -1396,6 +1399,8 @@ __global__ __launch_bounds__(kPartBlock, SA_PART_WAVES_EU) void part_scatter_ker
       const ulonglong2 rec = make_ulonglong2(key, (d << 7) | bk);
       if (d >= (1ULL << 57)) {
         direct_red(P, key, d, bk, stride, st);
+      } else if (SA_PART_SKIP_USED && cur[b] >= lim[b]) {  // run used up (stays so): no stage, no cur atomic
+        spill(key, d, bk);
       } else if (STAGE) {
         const uint32_t slot = atomicAdd(&scnt[b], 1u);
         if (slot < kPartStage) stage[b * kPartStage + slot] = rec;
