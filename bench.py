@@ -15,6 +15,12 @@ back and consecutive batches overlap (the next batch's workgroups start on the
 CUs the current batch's workgroups leave).  `value` and `ms_per_step` are the
 wall clock of the timed steps.
 
+Every launch aggregates a distinct trace-id variant of the batch (trace ids
+XORed with a per-variant constant), so HLL registers keep rising as on a live
+stream; the cold first launch on a fresh engine is reported on its own.  At
+N=1 the line also carries `c4` and `c4zipf` sub-objects (BASELINE config 4,
+uniform and Zipf(1.1) over 1 M series) with their own roofline.
+
 Prints ONE JSON line on rank 0. `roofline` prices the ingest kernel against
 HBM (44 algorithmic bytes per span / 8 TB/s).  Its `kernel_ms` is the kernel
 alone: HIP events around each of a set of serial launches on one stream,
@@ -141,39 +147,215 @@ def host_otlp_rate(spans: int):
                       "sa_ingest (H2D + kernel)"}
 
 
+def box_cores():
+    """Host cores this job may use: nproc, the CPU affinity set and the cgroup
+    CPU quota (a GPU box's job gets a share of a larger machine)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            with open(path) as f:
+                parts = f.read().split()
+            if path.endswith("cpu.max") and parts[0] != "max":
+                quota = int(parts[0]) / int(parts[1])
+            elif not path.endswith("cpu.max") and int(parts[0]) > 0:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                    quota = int(parts[0]) / int(f.read().split()[0])
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    usable = min(nproc, aff, int(quota) if quota else nproc)
+    return {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "usable": max(1, usable)}
+
+
+def trace_variants(w0, w1, k, seed):
+    """k distinct trace-id column pairs from one batch's: every trace id XORed
+    with a per-variant random 128-bit constant (a bijection, so the traces of
+    a variant stay distinct and keep their span counts).  Each step of the
+    bench aggregates a variant no launch has seen, so HLL registers keep
+    rising as they would on a live stream."""
+    import numpy as np
+    import torch
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = [(w0, w1)]
+    for _ in range(k - 1):
+        c0, c1 = (int(x) for x in rng.integers(-2**63, 2**63 - 1, 2, dtype=np.int64))
+        out.append((w0 ^ c0, w1 ^ c1))
+    return out
+
+
+WORKLOADS = {
+    "c2": ("C2: synthetic SoA v1 spans, 20 services x 25 span names (Zipf 1.1) x 3 status codes -> "
+           "<=1,500 series, default spanmetrics buckets, lognormal durations, ~10 spans/trace, "
+           "per-service HLL p=14 + error count-min 4x2048, 10 s windows; a fresh trace-id set every step"),
+    "c4": ("C4: 1,000,000 series (2,000 http.route x 500 k8s.pod.name), uniform over keys, binned HBM "
+           "key table, HLL + count-min; a fresh trace-id set every step"),
+    "c4zipf": ("C4 Zipf: 1,000,000 series (2,000 http.route x 500 k8s.pod.name), Zipf(s=1.1) over keys, "
+               "binned HBM key table, HLL + count-min; a fresh trace-id set every step"),
+}
+
+
+def run_workload(name, n, args, device, rank, world, barrier):
+    """One workload on this rank: a fresh engine, device-resident columns,
+    cold first launch, warm-up, the kernel alone (serial launches, HIP events
+    on the launch stream), then the timed steps over the streams.  Every
+    launch aggregates a distinct trace-id variant of the batch."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from spanagg import Config, Engine
+    from spanagg.synth import generate_c2, generate_highcard
+
+    if name == "c2":
+        wl = generate_c2(n, seed=42 + rank)
+        batch, first_window, n_services, key_capacity = wl.batch, wl.first_window, wl.n_services, 1500
+    else:
+        batch, _, first_window = generate_highcard(n, seed=7 + rank, zipf_s=1.1 if name == "c4zipf" else 0.0)
+        wl, n_services, key_capacity = None, 1, 1_200_000
+    cols = []
+    for c in batch.columns():
+        cols.append(torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(device))
+    n_iso = max(3, args.steps // 5)
+    n_var = min(args.variants, 1 + args.warmup + n_iso + args.steps)
+    variants = trace_variants(cols[3], cols[4], n_var, seed=1000 + rank)
+    eng = Engine(Config(n_services=max(n_services, 1), n_windows=16, key_capacity=key_capacity,
+                        device=device.index))
+    eng.window_advance(first_window)
+    streams = [torch.cuda.Stream(device) for _ in range(max(1, args.streams))]
+    stream = streams[0]
+    torch.cuda.set_stream(stream)
+    launches = [0]
+
+    def step(i, s=None):
+        s = s or streams[i % len(streams)]
+        v = variants[launches[0] % len(variants)]
+        launches[0] += 1
+        eng.ingest_device(cols[0], cols[1], cols[2], v[0], v[1], cols[5], n=n, stream=s.cuda_stream)
+
+    def ev():
+        return torch.cuda.Event(enable_timing=True)
+
+    torch.cuda.synchronize(device)
+    # 0) the cold first launch on a fresh engine (empty key table and sketches)
+    c0, c1 = ev(), ev()
+    c0.record(stream)
+    step(0, stream)
+    c1.record(stream)
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(device)
+    cold_ms = c0.elapsed_time(c1)
+    # 1) the kernel alone: serial launches on one stream, HIP events around each
+    iso = [(ev(), ev()) for _ in range(n_iso)]
+    for a, b in iso:
+        a.record(stream)
+        step(0, stream)
+        b.record(stream)
+    torch.cuda.synchronize(device)
+    kernel_ms = sum(a.elapsed_time(b) for a, b in iso) / len(iso)
+    # 2) the timed steps, alternating over the streams
+    start = ev()
+    ends = [ev() for _ in streams]
+    barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    start.record(stream)
+    for s in streams[1:]:
+        s.wait_event(start)
+    for i in range(args.steps):
+        step(i)
+    enqueue_s = time.perf_counter() - t0
+    for s, e_ in zip(streams, ends):
+        e_.record(s)
+    torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    barrier()
+    device_ms = max(start.elapsed_time(e_) for e_ in ends) / max(1, args.steps)
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms, device_ms, cold_ms], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms, device_ms, cold_ms = (float(x) for x in t)
+    # one flush (+ RCCL merge across ranks) after the timed region
+    torch.cuda.synchronize(device)
+    tm = time.perf_counter()
+    if world > 1:
+        from spanagg.dist import EnginePartial, merge_red, merge_window
+        part = EnginePartial(eng, device)
+        red = merge_red(part, reset=True)
+        merge_window(part, first_window + 1)
+    else:
+        red = eng.flush()
+    torch.cuda.synchronize(device)
+    merge_ms = (time.perf_counter() - tm) * 1e3
+    st = eng.stats()
+    calls_ok = int(red.calls.sum()) == launches[0] * n * world - st["zero_key"] * (1 if world == 1 else world)
+    out = {"wl": wl, "batch": batch, "eng": eng, "first_window": first_window, "elapsed": elapsed,
+           "kernel_ms": kernel_ms, "device_ms": device_ms, "cold_ms": cold_ms, "merge_ms": merge_ms,
+           "calls_ok": calls_ok, "enqueue_s": enqueue_s, "streams": len(streams), "variants": n_var,
+           "launches": launches[0], "hll_p": 14}
+    del variants, cols
+    return out
+
+
+def roofline(name, n, r, traffic_path=None):
+    achieved = BYTES_PER_SPAN * n / (r["kernel_ms"] * 1e-3) / 1e9
+    tpath = traffic_path or os.path.join(ROOT, "profiles", "traffic.json" if name == "c2" else f"traffic_{name}.json")
+    traffic, tsrc = load_traffic(tpath, name)
+    piped = BYTES_PER_SPAN * n / (r["device_ms"] * 1e-3) / 1e9
+    kern = {"c2": "ingest_v2_kernel (spanagg_kernels.hip)",
+            "c4": "bt_scatter_kernel + bt_aggregate_kernel (spanagg_binned.hip)",
+            "c4zipf": "bt_scatter_kernel + bt_aggregate_kernel (spanagg_binned.hip)"}[name]
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kern, "kernel_ms": r["kernel_ms"],
+            "bytes_per_span": BYTES_PER_SPAN, "traffic_source": tsrc,
+            "pipelined": {"streams": r["streams"], "device_ms_per_step": r["device_ms"], "achieved": piped,
+                          "frac": piped / HBM_PEAK_GBS}}
+    if traffic:
+        # what the kernel really moves (PMC bytes / kernel time), beside the
+        # algorithmic-byte fraction above
+        roof["measured_gbs"] = traffic / (r["kernel_ms"] * 1e-3) / 1e9
+        roof["measured_frac"] = roof["measured_gbs"] / HBM_PEAK_GBS
+        roof["traffic_over_algorithmic"] = traffic / (BYTES_PER_SPAN * n)
+    return roof
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--spans", type=int, default=10_000_000, help="spans per step per GPU")
-    ap.add_argument("--workload", choices=["c2", "c4", "c4zipf"], default="c2")
+    ap.add_argument("--workload", choices=list(WORKLOADS), default="c2")
     ap.add_argument("--streams", type=int, default=2,
                     help="launch streams the steps alternate over (the engine's two slab sets "
                          "let consecutive launches overlap); 1 = strictly serial launches")
+    ap.add_argument("--variants", type=int, default=64,
+                    help="distinct trace-id variants of the batch (one per launch up to this many)")
+    ap.add_argument("--sub", default="c4,c4zipf",
+                    help="extra workloads reported as sub-objects of the line at N=1 ('' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--h2d-reps", type=int, default=5,
                     help="host-buffer sa_ingest repetitions (PCIe-inclusive rate; 0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=None,
-                    help="PMC traffic summary (default profiles/traffic.json, profiles/traffic_c4.json for c4)")
+                    help="PMC traffic summary of the main workload (default profiles/traffic[_<wl>].json)")
     ap.add_argument("--host-otlp-spans", type=int, default=500_000,
                     help="spans for the Node host's OTLP->GPU rate (0 = skip)")
-    ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1),
-                    help="processes for the multi-core CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-workers", type=int, default=None,
+                    help="processes for the multi-core CPU baseline (default: every usable host core; 0 = skip)")
     ap.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_worker is not None:  # child of cpu_baseline_multicore (no GPU use)
         cpu_worker(args.cpu_worker, args.cpu_seconds)
         return 0
 
-    import numpy as np
     import torch
     import torch.distributed as dist
-
-    from spanagg import Config, Engine
-    from spanagg.dist import EnginePartial, merge_red, merge_window
-    from spanagg.synth import generate_c2, generate_highcard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -192,89 +374,8 @@ def main():
             dist.barrier()
 
     n = args.spans
-    if args.workload == "c2":
-        wl = generate_c2(n, seed=42 + rank)
-        # 20 services x 25 names x 3 status codes: at most 1,500 series
-        batch, first_window, n_services, key_capacity = wl.batch, wl.first_window, wl.n_services, 1500
-        workload = ("C2: synthetic SoA v1 spans, 20 services x 25 span names (Zipf 1.1) x 3 "
-                    "status codes -> <=1,500 series, default spanmetrics buckets, lognormal "
-                    "durations, ~10 spans/trace, per-service HLL p=14 + error count-min 4x2048, "
-                    "10 s windows")
-    else:
-        zs = 1.1 if args.workload == "c4zipf" else 0.0
-        batch, _, first_window = generate_highcard(n, seed=7 + rank, zipf_s=zs)
-        wl, n_services, key_capacity = None, 1, 1_200_000
-        workload = ("C4: 1,000,000 series (2,000 http.route x 500 k8s.pod.name), "
-                    + (f"Zipf(s={zs}) over keys" if zs else "uniform")
-                    + ", HBM key table, HLL + count-min")
-    cols = []
-    for c in batch.columns():
-        t = torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32))
-        cols.append(t.to(device))
-    eng = Engine(Config(n_services=max(n_services, 1), n_windows=16, key_capacity=key_capacity,
-                        device=local_rank))
-    eng.window_advance(first_window)
-    # dedicated (non-null) streams: the kernels and the timing events share them
-    streams = [torch.cuda.Stream(device) for _ in range(max(1, args.streams))]
-    stream = streams[0]
-    torch.cuda.set_stream(stream)
-
-    def step(i, s=None):
-        s = s or streams[i % len(streams)]
-        eng.ingest_device(*cols, n=n, stream=s.cuda_stream)
-
-    def ev():
-        return torch.cuda.Event(enable_timing=True)
-
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize(device)
-    # 1) the kernel alone: serial launches on one stream, HIP events around
-    #    each on that stream (what rocprofv3 reports per launch)
-    iso = [(ev(), ev()) for _ in range(max(3, args.steps // 5))]
-    for a, b in iso:
-        a.record(stream)
-        step(0, stream)
-        b.record(stream)
-    torch.cuda.synchronize(device)
-    kernel_ms = sum(a.elapsed_time(b) for a, b in iso) / len(iso)
-    # 2) the timed steps: alternating over the streams; device time from one
-    #    start event (every stream waits on it) to the last stream's end event
-    start = ev()
-    ends = [ev() for _ in streams]
-    barrier()
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    start.record(stream)
-    for s in streams[1:]:
-        s.wait_event(start)
-    for i in range(args.steps):
-        step(i)
-    enqueue_s = time.perf_counter() - t0  # host time to enqueue the steps
-    for s, e_ in zip(streams, ends):
-        e_.record(s)
-    torch.cuda.synchronize(device)
-    elapsed = time.perf_counter() - t0
-    barrier()
-    device_ms = max(start.elapsed_time(e_) for e_ in ends) / max(1, args.steps)
-    if world > 1:
-        t = torch.tensor([elapsed, kernel_ms, device_ms], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms, device_ms = float(t[0]), float(t[1]), float(t[2])
-
-    # one flush (+ RCCL merge across ranks) after the timed region
-    torch.cuda.synchronize(device)
-    tm = time.perf_counter()
-    if world > 1:
-        part = EnginePartial(eng, device)
-        red = merge_red(part, reset=True)
-        merge_window(part, first_window + 1)
-    else:
-        red = eng.flush()
-    torch.cuda.synchronize(device)
-    merge_ms = (time.perf_counter() - tm) * 1e3
-    total_local = (args.warmup + len(iso) + args.steps) * n
-    calls_ok = int(red.calls.sum()) == total_local * world
+    main_r = run_workload(args.workload, n, args, device, rank, world, barrier)
+    eng, batch = main_r["eng"], main_r["batch"]
 
     # the host-buffer boundary (sa_ingest: the batch starts in pageable host
     # memory, PCIe H2D included), timed after the device-resident steps; it
@@ -295,49 +396,59 @@ def main():
                "calls_check": h2d_calls == (args.h2d_reps + 1) * n,
                "sample": f"{args.h2d_reps} x sa_ingest of the {n:,}-span batch from pageable "
                          "host numpy columns (H2D + kernel), after one warm-up ingest"}
+    eng.close()
+
+    subs = {}
+    if world == 1:
+        for sub in [w for w in args.sub.split(",") if w and w != args.workload]:
+            r = run_workload(sub, n, args, device, rank, world, barrier)
+            r["eng"].close()
+            subs[sub] = {"workload": WORKLOADS[sub], "value": n * args.steps / r["elapsed"], "unit": "spans/s",
+                         "ms_per_step": r["elapsed"] * 1e3 / args.steps, "steps": args.steps,
+                         "warmup": args.warmup, "cold_launch_ms": r["cold_ms"],
+                         "roofline": roofline(sub, n, r), "calls_check": r["calls_ok"],
+                         "trace_variants": r["variants"]}
+            torch.cuda.empty_cache()
 
     result = None
+    ok = main_r["calls_ok"] and all(v["calls_check"] for v in subs.values())
     if rank == 0:
-        value = world * n * args.steps / elapsed
-        achieved = BYTES_PER_SPAN * n / (kernel_ms * 1e-3) / 1e9
-        tpath = args.traffic or os.path.join(
-            ROOT, "profiles", "traffic.json" if args.workload == "c2" else f"traffic_{args.workload}.json")
-        traffic, tsrc = load_traffic(tpath, args.workload)
-        piped = BYTES_PER_SPAN * n / (device_ms * 1e-3) / 1e9
+        elapsed = main_r["elapsed"]
         result = {
-            "metric": METRIC, "value": value, "unit": "spans/s", "n_gpus": world,
+            "metric": METRIC, "value": world * n * args.steps / elapsed, "unit": "spans/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
-            "data": "synthetic (seeded PCG64 generator, spanagg/synth.py; one shard per rank)",
-            "config": {"workload": workload, "spans_per_step_per_gpu": n,
+            "data": "synthetic (seeded PCG64 generator, spanagg/synth.py; one shard per rank; every launch "
+                    "a distinct trace-id variant of the rank's batch)",
+            "config": {"workload": WORKLOADS[args.workload], "spans_per_step_per_gpu": n,
                        "global_spans_per_step": n * world,
                        "parallelism": f"trace-id shards x{world}, RCCL merge at flush"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "kernel": "ingest (spanagg_kernels.hip)",
-                         "kernel_ms": kernel_ms, "bytes_per_span": BYTES_PER_SPAN,
-                         "traffic_source": tsrc,
-                         "pipelined": {"streams": len(streams), "device_ms_per_step": device_ms,
-                                       "achieved": piped, "frac": piped / HBM_PEAK_GBS}},
-            "merge_ms": merge_ms, "calls_check": calls_ok,
-            "host_enqueue_us_per_step": enqueue_s * 1e6 / max(1, args.steps),
+            "roofline": roofline(args.workload, n, main_r, args.traffic),
+            "cold_launch_ms": main_r["cold_ms"], "trace_variants": main_r["variants"],
+            "merge_ms": main_r["merge_ms"], "calls_check": main_r["calls_ok"],
+            "host_enqueue_us_per_step": main_r["enqueue_s"] * 1e6 / max(1, args.steps),
         }
+        result.update(subs)
         if h2d is not None:
             result["host_buffer_ingest"] = h2d
+        wl = main_r["wl"]
         if world == 1 and not args.no_cpu_baseline and wl is not None:
             port, conn = cpu_baseline(wl, args.cpu_seconds)
             result["cpu_baseline"] = port
             result["cpu_baseline_connector"] = conn
-            if args.cpu_workers > 1:
-                result["cpu_baseline_multicore"] = cpu_baseline_multicore(args.cpu_workers,
-                                                                          args.cpu_seconds / 2)
+            cores = box_cores()
+            workers = cores["usable"] if args.cpu_workers is None else args.cpu_workers
+            if workers > 1:
+                mc = cpu_baseline_multicore(workers, args.cpu_seconds / 2)
+                mc.update({"nproc": cores["nproc"], "affinity_cpus": cores["affinity"],
+                           "cgroup_quota_cpus": cores["cgroup_quota_cpus"]})
+                result["cpu_baseline_multicore"] = mc
         if world == 1 and args.host_otlp_spans > 0:
             result["host_otlp"] = host_otlp_rate(args.host_otlp_spans)
         print(json.dumps(result), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
-    return 0 if calls_ok else 1
+    return 0 if ok else 1
 
 
 if __name__ == "__main__":

@@ -11,22 +11,24 @@
  * batches of `spanmetrics.batch_size`).  The other exporters of the demo's
  * traces pipeline (Jaeger, debug) are outside this path.
  */
+const fs = require('fs');
 const otlp = require('./otlp');
-const { DEMO_SPAN_NAME_RULES } = require('./transform');
+const collectorConfig = require('./collector_config');
 const { SpanMetricsConnector } = require('./connector');
 const { OtlpReceiver, OtlpHttpExporter, MemoryLimiter } = require('./receiver');
 
 class TracesToMetricsPipeline {
   /**
    * @param opts.spanmetrics  connector config (YAML field names)
-   * @param opts.transform    span-name rules (default: the demo's two rules; [] disables)
+   * @param opts.transform    span-name rules (default: none; fromCollectorConfig derives
+   *                          them from the collector config's transform processors)
    * @param opts.memoryLimiter MemoryLimiter options (default: the demo's 80% / 25%), or false
    * @param opts.receiver     OtlpReceiver options ({httpPort, grpcPort, host}), or false
    * @param opts.exporter     OtlpHttpExporter options ({endpoint}), or false
    * @param opts.addon, opts.clock  passed to the connector
    */
   constructor(opts = {}) {
-    this.rules = opts.transform === undefined ? DEMO_SPAN_NAME_RULES : opts.transform;
+    this.rules = opts.transform || [];
     this.limiter = opts.memoryLimiter === false ? null
       : new MemoryLimiter(Object.assign({ limit_percentage: 80, spike_limit_percentage: 25 }, opts.memoryLimiter));
     this.exporter = opts.exporter ? new OtlpHttpExporter(opts.exporter) : null;
@@ -68,5 +70,30 @@ class TracesToMetricsPipeline {
     this.connector.shutdown();
   }
 }
+
+/**
+ * The pipeline a collector config describes: the traces pipeline that exports
+ * to `spanmetrics` (its transform processors' span-name rules, in pipeline
+ * order, and its memory limiter) and the connector's config block.  `configs`
+ * are YAML texts, or file paths when `opts.files` is set, merged like repeated
+ * `--config` flags (docker-compose.yml:756 passes otelcol-config.yml and
+ * otelcol-config-extras.yml).  `opts` overrides / adds the host's own options
+ * (addon, receiver, exporter, clock, and spanmetrics fields such as
+ * key_capacity).
+ */
+TracesToMetricsPipeline.fromCollectorConfig = function fromCollectorConfig(configs, opts = {}) {
+  const texts = [].concat(configs).map((c) => (opts.files ? fs.readFileSync(c, 'utf8') : c));
+  const cfg = collectorConfig.loadCollectorConfig(texts, opts.env || process.env);
+  const derived = collectorConfig.pipelineOptions(cfg, opts.connectorName || 'spanmetrics');
+  const o = Object.assign({}, opts, {
+    spanmetrics: Object.assign({}, derived.spanmetrics, opts.spanmetrics),
+    transform: derived.transform,
+    memoryLimiter: opts.memoryLimiter !== undefined ? opts.memoryLimiter : derived.memoryLimiter,
+  });
+  const p = new TracesToMetricsPipeline(o);
+  p.collectorConfig = cfg;
+  p.wiring = derived.wiring;
+  return p;
+};
 
 module.exports = { TracesToMetricsPipeline };

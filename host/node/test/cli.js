@@ -12,6 +12,13 @@
  *   {"cmd": "encode_metrics", "req": {...}}     -> {"b64": ...}
  *   {"cmd": "xxh64", "cases": [[hex, seed]...]} -> hex digests
  *   {"cmd": "transform", "names": [...]}        demo transform rules applied
+ *   {"cmd": "collector_config", "texts": [yaml...], "env": {...}, "names": [...]}
+ *        -> the pipeline options a collector config yields (lib/collector_config.js):
+ *           spanmetrics block, memory limiter, wiring, and `names` through the
+ *           transform rules it declares
+ *   {"cmd": "connector_export", "requests": [b64...], "texts": [yaml...]?, "spanmetrics": {...}?}
+ *        -> {"b64": ExportMetricsServiceRequest} from a TracesToMetricsPipeline over
+ *           the test stand-in addon (host logic only: names, attributes, layout)
  */
 const path = require('path');
 const lib = path.join(__dirname, '..', 'lib');
@@ -19,6 +26,9 @@ const otlp = require(path.join(lib, 'otlp'));
 const keys = require(path.join(lib, 'keys'));
 const { xxh64 } = require(path.join(lib, 'xxh64'));
 const { applyRules, DEMO_SPAN_NAME_RULES } = require(path.join(lib, 'transform'));
+const collectorConfig = require(path.join(lib, 'collector_config'));
+const { TracesToMetricsPipeline } = require(path.join(lib, 'pipeline'));
+const { FakeAddon } = require('./fake_addon');
 
 function fromTyped([t, v]) {
   switch (t) {
@@ -106,6 +116,23 @@ function run(cmd) {
     case 'encode_metrics': return { b64: otlp.encodeMetrics(metricsFromJson(cmd.req)).toString('base64') };
     case 'xxh64': return cmd.cases.map(([h, seed]) => u64hex(xxh64(Buffer.from(h, 'hex'), BigInt(seed))));
     case 'transform': return cmd.names.map((n) => applyRules(n, DEMO_SPAN_NAME_RULES));
+    case 'collector_config': {
+      const cfg = collectorConfig.loadCollectorConfig(cmd.texts, cmd.env || {});
+      const o = collectorConfig.pipelineOptions(cfg);
+      return { spanmetrics: o.spanmetrics, memory_limiter: o.memoryLimiter, wiring: o.wiring,
+        n_rules: o.transform.length, error_mode: o.transform.errorMode || null,
+        names: (cmd.names || []).map((n) => applyRules(n, o.transform)) };
+    }
+    case 'connector_export': {
+      const common = { addon: new FakeAddon(), receiver: false, exporter: false, native: false,
+        clock: () => 1700000000000000000n };
+      const p = cmd.texts
+        ? TracesToMetricsPipeline.fromCollectorConfig(cmd.texts, Object.assign(common, { env: {},
+          spanmetrics: cmd.spanmetrics || {} }))
+        : new TracesToMetricsPipeline(Object.assign(common, { spanmetrics: cmd.spanmetrics || {} }));
+      for (const r of cmd.requests) p.consumeTraces(Buffer.from(r, 'base64'));
+      return p.flush().then((bytes) => ({ b64: Buffer.from(bytes).toString('base64') }));
+    }
     default: throw new Error(`unknown cmd ${cmd.cmd}`);
   }
 }
@@ -114,5 +141,6 @@ let input = '';
 process.stdin.setEncoding('utf8');
 process.stdin.on('data', (c) => { input += c; });
 process.stdin.on('end', () => {
-  process.stdout.write(JSON.stringify(run(JSON.parse(input))));
+  Promise.resolve(run(JSON.parse(input))).then((out) => process.stdout.write(JSON.stringify(out)),
+    (e) => { process.stderr.write(String(e && e.stack || e)); process.exit(1); });
 });

@@ -542,8 +542,10 @@ test('pipeline: OTLP/HTTP in -> transform -> connector -> otlphttp out', async (
     req.on('end', () => { posted.push({ url: req.url, type: req.headers['content-type'], body: Buffer.concat(chunks) }); res.end(); });
   });
   await new Promise((r) => sink.listen(0, '127.0.0.1', r));
-  const p = await new TracesToMetricsPipeline({ addon: new FakeAddon(), clock: () => 7n,
-    receiver: { httpPort: 0, grpcPort: 0 }, memoryLimiter: { limit_mib: 1e9 },
+  // a collector config in the demo's shape (otelcol-config.yml:100-127): the
+  // transform rules and wiring come from it
+  const p = await TracesToMetricsPipeline.fromCollectorConfig(DEMO_LIKE_CONFIG, { addon: new FakeAddon(),
+    clock: () => 7n, receiver: { httpPort: 0, grpcPort: 0 }, memoryLimiter: { limit_mib: 1e9 },
     exporter: { endpoint: `http://127.0.0.1:${sink.address().port}/api/v1/otlp` } }).start();
   try {
     const body = otlp.encodeTraces(request([[{ 'service.name': 'frontend' }, [
@@ -563,6 +565,85 @@ test('pipeline: OTLP/HTTP in -> transform -> connector -> otlphttp out', async (
     await p.shutdown();
     await new Promise((r) => sink.close(r));
   }
+});
+
+
+// ------------------------------------------------------------- collector config (YAML + OTTL)
+const cc = require(path.join(lib, 'collector_config'));
+const DEMO_LIKE_CONFIG = [
+  'processors:',
+  '  batch:',
+  '  memory_limiter:',
+  '    check_interval: 5s',
+  '    limit_percentage: 80',
+  '  transform:',
+  '    error_mode: ignore',
+  '    trace_statements:',
+  '      - context: span',
+  '        statements:',
+  '          # a comment between items',
+  '          - replace_pattern(name, "\\\\?.*", "")',
+  '          - replace_match(name, "GET /api/products/*", "GET /api/products/{productId}")',
+  'connectors:',
+  '  spanmetrics:',
+  'service:',
+  '  pipelines:',
+  '    traces:',
+  '      receivers: [otlp]',
+  '      processors: [memory_limiter, transform, batch]',
+  '      exporters: [otlp, debug, spanmetrics]',
+  '    metrics:',
+  '      receivers: [otlp, spanmetrics]',
+  '      exporters: [otlphttp/prometheus]',
+].join('\n');
+
+test('yaml: mappings, sequences, scalars, flow values, comments', () => {
+  const v = cc.parseYaml([
+    'a: 1', 'b: "x\\ty"  # trailing comment', "c: 'it''s'", 'd:', 'e: [1, two, "3"]',
+    'f: {k: v, n: 2}', 'g:', '  - x', '  - k: 1', '    j: true', '  -', '    - nested',
+    'h:', '- same-indent item', 'i: http://host:4318/path#frag', 'j: ~', 'k: 1.5e3', 'l: 5s',
+  ].join('\n'));
+  assert.deepStrictEqual(v, { a: 1, b: 'x\ty', c: "it's", d: null, e: [1, 'two', '3'], f: { k: 'v', n: 2 },
+    g: ['x', { k: 1, j: true }, ['nested']], h: ['same-indent item'], i: 'http://host:4318/path#frag',
+    j: null, k: 1500, l: '5s' });
+  assert.throws(() => cc.parseYaml('a: 1\n   b: 2'), cc.YamlError);
+  assert.throws(() => cc.parseYaml('a: "open'), cc.YamlError);
+});
+
+test('yaml: env expansion and the multi-file deep merge of --config flags', () => {
+  const cfg = cc.loadCollectorConfig(['x:\n  ep: ${env:HOST}:${PORT}\n  keep: 1\nl: [a]',
+    'x:\n  add: 2\nl: [b]'], { HOST: 'h', PORT: '9' });
+  assert.deepStrictEqual(cfg, { x: { ep: 'h:9', keep: 1, add: 2 }, l: ['b'] });
+});
+
+test('collector config: spanmetrics block, transform rules and wiring of the demo shape', () => {
+  const o = cc.pipelineOptions(cc.loadCollectorConfig([DEMO_LIKE_CONFIG], {}));
+  assert.deepStrictEqual(o.spanmetrics, {});
+  assert.deepStrictEqual(o.memoryLimiter, { check_interval: '5s', limit_percentage: 80 });
+  assert.deepStrictEqual(o.wiring.traces.processors, ['memory_limiter', 'transform', 'batch']);
+  assert.strictEqual(o.transform.length, 2);
+  assert.strictEqual(o.transform.errorMode, 'ignore');
+  for (const [a, b] of [['GET /api/products/0PUK6V6EV0?x=1', 'GET /api/products/{productId}'],
+    ['GET /api/cart?sessionId=1', 'GET /api/cart'], ['POST /api/products/1', 'POST /api/products/1']])
+    assert.strictEqual(applyRules(a, o.transform), b);
+  // the rules keep their native descriptors, so the C++ columnizer can run them
+  assert.deepStrictEqual(o.transform.map((r) => r.native.kind), ['strip_query', 'glob']);
+});
+
+test('collector config: unsupported statements and broken wiring are configuration errors', () => {
+  const mk = (stmt) => cc.loadCollectorConfig([DEMO_LIKE_CONFIG.replace(
+    'replace_pattern(name, "\\\\?.*", "")', stmt)], {});
+  assert.throws(() => cc.pipelineOptions(mk('set(attributes["x"], "y")')), cc.ConfigError);
+  assert.throws(() => cc.pipelineOptions(mk('replace_pattern(name, "a", "b") where kind == 1')), cc.ConfigError);
+  assert.throws(() => cc.pipelineOptions(cc.loadCollectorConfig([DEMO_LIKE_CONFIG.replace(
+    'exporters: [otlp, debug, spanmetrics]', 'exporters: [otlp]')], {})), cc.ConfigError);
+  assert.throws(() => cc.spanmetricsConfig({ connectors: {} }), cc.ConfigError);
+  // explicit buckets and dimensions pass through to the connector config
+  const o = cc.pipelineOptions(cc.loadCollectorConfig([DEMO_LIKE_CONFIG.replace('  spanmetrics:',
+    '  spanmetrics:\n    histogram:\n      explicit:\n        buckets: [2ms, 4ms, 1s]\n' +
+    '    dimensions:\n      - name: http.method\n        default: GET')], {}));
+  assert.deepStrictEqual(o.spanmetrics, { histogram: { explicit: { buckets: ['2ms', '4ms', '1s'] } },
+    dimensions: [{ name: 'http.method', default: 'GET' }] });
 });
 
 // ------------------------------------------------------------------ runner

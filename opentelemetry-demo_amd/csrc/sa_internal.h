@@ -73,7 +73,18 @@ struct IngestParams {
   ulonglong2 *part_rec;
   uint32_t *part_fill;
   uint32_t part_cap;
+  // binned-table path (spanagg_binned.hip): key table split into kPartBins
+  // bin-local sub-tables of 2^log2sb slots, keys stored as m = key * kmul,
+  // u32 count rows; records in per-(bin, scatter workgroup) regions of
+  // bt_region records, region fills in bt_cnt [scatter workgroup][bin]
+  uint32_t log2sb;
+  uint32_t bt_region;
+  uint64_t kmul, kinv;
+  ulonglong2 *bt_rec;
+  uint32_t *bt_cnt;
+  uint32_t bt_grid;  // scatter workgroups (regions per bin)
 };
+
 
 // Partitioned HBM-table path (high cardinality): part_scatter_kernel bins
 // every span's record by the top 11 bits of its key, part_aggregate_kernel
@@ -128,6 +139,47 @@ __host__ __device__ inline uint32_t row_count_cell(uint32_t b) {
   return b / kSegBuckets * 8 + 1 + b % kSegBuckets;
 }
 __host__ __device__ inline uint32_t row_sum_cell(uint32_t b) { return b / kSegBuckets * 8; }
+
+// ---------------------------------------------------------------------------
+// Binned key table (high-cardinality path, spanagg_binned.hip).
+// The table of cap = 2^log2cap slots is split into kPartBins bins of
+// SB = 2^log2sb slots: a key lives in the bin given by the top kPartBinBits
+// bits of m = key * kmul (kmul odd, so the map is a bijection and 0 stays the
+// EMPTY marker), at its home slot within the bin or the next free one after
+// it (linear probing that wraps inside the bin).  One aggregate workgroup per
+// bin mirrors the whole sub-table in LDS at the same positions, so the bin's
+// keys and counter rows are read and written as one contiguous block.
+constexpr uint32_t kBinShift = 64 - kPartBinBits;          // bin = m >> kBinShift
+constexpr uint64_t kBinRest = (1ULL << kBinShift) - 1;     // m's bits below the bin
+__host__ __device__ inline uint32_t bt_home(uint64_t m, uint32_t log2sb) {
+  return (((uint32_t)m ^ (uint32_t)(m >> 29)) * 0x9E3779B1u) >> (32 - log2sb);
+}
+__host__ __device__ inline uint32_t bt_slot(uint64_t m, uint32_t log2sb, uint32_t i) {
+  return ((uint32_t)(m >> kBinShift) << log2sb) | ((bt_home(m, log2sb) + i) & ((1u << log2sb) - 1));
+}
+// u32 counter rows of the binned path: words [0, 2) = the u64 ns sum, words
+// [2, 2 + nbk) = bucket counts, padded to whole 16-B quads (80 B at 17 buckets)
+__host__ __device__ inline uint32_t row32_stride(uint32_t nbk) { return (nbk + 2 + 3) & ~3u; }
+constexpr uint32_t kBtStage = 4;     // records per bin stage: one 64-B chunk per flush
+constexpr uint32_t kBtHot = 224;     // scatter overflow table entries
+constexpr uint32_t kBtHq = 256;      // scatter deferred HLL raises
+constexpr uint32_t kBtBlock = 1024;  // scatter workgroup
+constexpr uint32_t kBtAggBlock = 512;
+constexpr uint32_t kBtMaxWgSpans = 65520;  // u16 claim / overflow counters per scatter workgroup
+constexpr size_t kBtScatterLds = (size_t)kPartBins * (8 + kBtStage * 16) + (size_t)kBtHot * (16 + 4 * kPartWords) +
+                                 (size_t)kBtHq * 8 + 16 + (size_t)kBins * sizeof(BinEntry);
+static_assert(kBtScatterLds <= 163840, "binned scatter LDS");
+
+// Geometry of the counter rows and key table for the flush-time kernels
+// (compact, gather, count-min fold): both table layouts, both row layouts.
+struct RowGeom {
+  uint32_t nbk;
+  uint32_t row32;   // 1: u32 count rows (binned path), 0: u64 segment rows
+  uint32_t binned;  // 1: binned key table
+  uint32_t log2cap, log2sb, max_probe;
+  uint64_t kmul, kinv;            // key <-> stored id (1, 1 unless binned)
+  unsigned long long *base64;     // row32: u64 [cap][nbk + 1] folded counts, or nullptr
+};
 
 // Key-table layout: cap = 2^log2cap slots in buckets of 4 (log2cap in 4..31).
 // A key's probe sequence is its first-choice bucket b1, then its second-choice
@@ -192,15 +244,21 @@ hipError_t launch_reduce_slabs(uint32_t *slab_cnt, unsigned long long *slab_sum,
                                unsigned long long *gcounts, uint32_t G, uint64_t cap,
                                uint32_t nbk, hipStream_t s);
 hipError_t launch_compact(const unsigned long long *gkeys, unsigned long long *gcounts,
-                          uint64_t cap, uint32_t nbk, unsigned long long *out_keys,
+                          uint64_t cap, const RowGeom &g, unsigned long long *out_keys,
                           unsigned long long *out_rows, unsigned long long *out_n,
                           uint64_t out_cap, int reset, hipStream_t s);
 hipError_t launch_gather_dense(const unsigned long long *gkeys, const unsigned long long *gcounts,
-                               uint32_t log2cap, uint32_t max_probe, uint32_t nbk,
-                               const uint64_t *keys, uint64_t n, uint64_t *rows, hipStream_t s);
+                               const RowGeom &g, const uint64_t *keys, uint64_t n, uint64_t *rows,
+                               hipStream_t s);
 hipError_t launch_fold_errcnt(const unsigned long long *gkeys, unsigned long long *errcnt,
                               uint64_t cap, unsigned long long *cms, uint32_t d, uint32_t w,
-                              uint32_t shift, const uint64_t *seeds, hipStream_t s);
+                              uint32_t shift, const uint64_t *seeds, uint64_t kinv, hipStream_t s);
+// binned-table path (spanagg_binned.hip)
+hipError_t prepare_ingest_bt(size_t agg_lds);
+size_t bt_agg_lds_bytes(uint32_t log2sb, uint32_t grid);
+hipError_t launch_ingest_bt(const IngestParams &P, size_t agg_lds, hipStream_t s);
+hipError_t launch_fold_rows32(unsigned long long *gcounts, unsigned long long *base64, uint64_t cap,
+                              uint32_t nbk, hipStream_t s);
 hipError_t launch_reduce_errslab(uint32_t *errslab, uint32_t G, uint64_t per_wg, uint64_t ws,
                                  uint32_t log2cap, unsigned long long *errcnt_ws, hipStream_t s);
 hipError_t launch_count_keys(const unsigned long long *gkeys, uint64_t cap,

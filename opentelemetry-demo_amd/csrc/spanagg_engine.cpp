@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -83,6 +84,18 @@ struct sa_engine {
   bool part = false;
   ulonglong2 *part_rec = nullptr;
   uint32_t *part_fill = nullptr;
+  // binned-table path (spanagg_binned.hip): bin-local key sub-tables of
+  // 2^log2sb slots, stored ids m = key * kmul, u32 count rows folded into
+  // base64 before 2^32 spans accumulate (since_fold), span records in
+  // per-(bin, scatter workgroup) regions (lazily allocated)
+  bool bt = false;
+  uint32_t log2sb = 0, bt_grid = 0;
+  uint64_t kmul = 1, kinv = 1;
+  size_t agg_lds = 0;
+  ulonglong2 *bt_rec = nullptr;
+  uint32_t *bt_cnt = nullptr;
+  unsigned long long *base64 = nullptr;
+  uint64_t since_fold = 0, fold_limit = 0xFFFFFFFFULL;
   size_t hll_slot_bytes = 0, cms_slot_elems = 0;
   void *stage = nullptr;
   uint64_t stage_spans = 0;
@@ -154,6 +167,24 @@ static bool build_bins(const sa_engine *e, sa::BinEntry (&bins)[sa::kBins]) {
     bins[k].base = e->nneg + below;
   }
   return true;
+}
+
+static size_t counts_bytes(const sa_engine *e) {
+  return e->bt ? (size_t)e->cap * sa::row32_stride(e->nbk) * 4 : (size_t)e->cap * sa::row_stride(e->nbk) * 8;
+}
+
+static sa::RowGeom geom(const sa_engine *e) {
+  sa::RowGeom g{};
+  g.nbk = e->nbk;
+  g.row32 = e->bt ? 1u : 0u;
+  g.binned = e->bt ? 1u : 0u;
+  g.log2cap = e->log2cap;
+  g.log2sb = e->log2sb;
+  g.max_probe = sa::max_probe_of(e->log2cap);
+  g.kmul = e->kmul;
+  g.kinv = e->kinv;
+  g.base64 = e->base64;
+  return g;
 }
 
 extern "C" {
@@ -310,6 +341,14 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     if (e->part)
       if (hipError_t st = sa::prepare_ingest_part(); st != hipSuccess)
         return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
+    // binned-table path where each bin's sub-table fits an aggregate
+    // workgroup's LDS (256..2048 slots per bin: 2^19..2^22 table slots), the
+    // window slot fits the record (<= 1024 windows) and buckets come from the
+    // bin table (SPANAGG_BINNED=0: the partitioned path, for A/B runs)
+    const char *bv = std::getenv("SPANAGG_BINNED");
+    sa::BinEntry bins_probe[sa::kBins];  // the binned kernels bucket by the bin table
+    e->bt = e->part && e->log2cap >= sa::kPartBinBits + 8 && e->log2cap <= sa::kPartBinBits + 11 &&
+            cfg->n_windows <= 1024 && build_bins(e, bins_probe) && !(bv && std::atoi(bv) == 0);
   }
 
   const uint64_t S = cfg->n_services, W = cfg->n_windows;
@@ -322,7 +361,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   };
   int rc = SA_OK;
   if ((rc = alloc((void **)&e->gkeys, e->cap * 8)) ||
-      (rc = alloc((void **)&e->gcounts, e->cap * sa::row_stride(e->nbk) * 8)) ||
+      (rc = alloc((void **)&e->gcounts, counts_bytes(e))) ||
       (rc = alloc((void **)&e->hll, e->hll_slot_bytes * W)) ||
       (rc = alloc((void **)&e->cms, e->cms_slot_elems * W * 8)) ||
       (rc = alloc((void **)&e->errcnt, (size_t)W * e->cap * 8)) ||
@@ -338,6 +377,26 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       if (hipMemcpy(e->d_bins, bins, sizeof bins, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(e, SA_EDEVICE, "bin table upload failed"));
     }
+  }
+  if (e->bt) {
+    // one scatter workgroup per CU (~160 KiB LDS); 512-thread aggregate
+    // workgroups sized for the bin's sub-table
+    e->log2sb = e->log2cap - sa::kPartBinBits;
+    e->bt_grid = e->cus;
+    e->agg_lds = sa::bt_agg_lds_bytes(e->log2sb, e->bt_grid);
+    if (hipError_t st = sa::prepare_ingest_bt(e->agg_lds); st != hipSuccess)
+      return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
+    // a random odd multiplier per engine: series ids -> stored ids (bins and
+    // home slots), so bin occupancy does not depend on ids a sender chooses
+    std::random_device rd;
+    uint64_t r = ((uint64_t)rd() << 32) ^ rd();
+    if (const char *kv = std::getenv("SPANAGG_KMUL")) r = std::strtoull(kv, nullptr, 0);  // fixed, for A/B runs
+    e->kmul = r | 1ULL;
+    uint64_t x = e->kmul;  // Newton: x = x (2 - a x) doubles the correct low bits
+    for (int i = 0; i < 6; ++i) x *= 2 - e->kmul * x;
+    e->kinv = x;
+    if (const char *fl = std::getenv("SPANAGG_FOLD_LIMIT"))  // test knob: fold u32 rows sooner
+      e->fold_limit = std::max<uint64_t>(1, std::strtoull(fl, nullptr, 0));
   }
   if (hipMemcpy(e->d_seeds, kCmsSeed, sizeof kCmsSeed, hipMemcpyHostToDevice) != hipSuccess)
     return bail(fail(e, SA_EDEVICE, "seed upload failed"));
@@ -373,7 +432,7 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->stats, (void *)e->out_keys, (void *)e->out_rows, (void *)e->scratch,
                   (void *)e->slab_cnt, (void *)e->hll, (void *)e->errcnt, (void *)e->d_seeds,
                   (void *)e->dbg, (void *)e->d_bins, (void *)e->errslab, (void *)e->part_rec,
-                  (void *)e->part_fill,
+                  (void *)e->part_fill, (void *)e->bt_rec, (void *)e->bt_cnt, (void *)e->base64,
                   e->stage})
     if (p) (void)hipFree(p);
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
@@ -412,14 +471,54 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s);
 static int ingest_on(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   // v2 small-table kernels keep u16 LDS counters for the whole launch: at most
   // 65532 spans per workgroup per launch (ingest_v2_kernel has no epoch flush)
-  const uint64_t max_n = e->part ? sa::kPartMaxSpans
-                                 : (uint64_t)e->G * ((e->small && e->variant >= 8) ? sa::kMaxWgSpans : (1u << 27));
+  const uint64_t max_n = e->bt     ? (uint64_t)e->bt_grid * sa::kBtMaxWgSpans
+                         : e->part ? sa::kPartMaxSpans
+                                   : (uint64_t)e->G * ((e->small && e->variant >= 8) ? sa::kMaxWgSpans : (1u << 27));
   for (uint64_t off = 0; off < b->n; off += max_n) {
     const uint64_t m = std::min(max_n, b->n - off);
     sa_span_batch sub{b->key_hash + off, b->start_ns + off, b->end_ns + off, b->trace_w0 + off,
                       b->trace_w1 + off, b->meta + off, m};
     if (int rc = ingest_launch(e, &sub, s)) return rc;
   }
+  return SA_OK;
+}
+
+// Binned path: launch geometry, record regions (allocated once for the
+// largest launch) and the u32 row fold.  Region capacity: the mean records
+// per (bin, scatter workgroup) plus 4 standard deviations and 8, in whole
+// 4-record chunks; records beyond it take the scatter's overflow table.
+static uint32_t bt_region_for(uint64_t wg_chunk) {
+  const double mu = (double)wg_chunk / sa::kPartBins;
+  return ((uint32_t)std::ceil(mu + 4.0 * std::sqrt(mu) + 8.0) + sa::kBtStage - 1) & ~(sa::kBtStage - 1);
+}
+
+static int bt_prepare_launch(sa_engine *e, uint64_t n, IngestParams &P, hipStream_t s) {
+  const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(e->bt_grid, (n + 4095) / 4096));
+  P.bt_grid = grid;
+  P.wg_chunk = ((n + grid - 1) / grid + 3) / 4 * 4;
+  P.bt_region = bt_region_for(P.wg_chunk);
+  if (!e->bt_rec) {
+    const size_t recs = (size_t)sa::kPartBins * e->bt_grid * bt_region_for(sa::kBtMaxWgSpans);
+    if (hipMalloc((void **)&e->bt_rec, recs * sizeof(ulonglong2)) != hipSuccess ||
+        hipMalloc((void **)&e->bt_cnt, (size_t)e->bt_grid * sa::kPartBins * 4) != hipSuccess)
+      return fail(e, SA_ENOMEM, "binned-path record buffers hipMalloc failed");
+  }
+  if (e->since_fold + n > e->fold_limit) {  // u32 bucket counts could wrap: fold them first
+    if (!e->base64) {
+      const size_t bytes = (size_t)e->cap * (e->nbk + 1) * 8;
+      if (hipMalloc((void **)&e->base64, bytes) != hipSuccess)
+        return fail(e, SA_ENOMEM, "fold array hipMalloc failed");
+      SA_HIP(e, hipMemsetAsync(e->base64, 0, bytes, s));
+    }
+    SA_HIP(e, sa::launch_fold_rows32(e->gcounts, e->base64, e->cap, e->nbk, s));
+    e->since_fold = 0;
+  }
+  e->since_fold += n;
+  P.log2sb = e->log2sb;
+  P.kmul = e->kmul;
+  P.kinv = e->kinv;
+  P.bt_rec = e->bt_rec;
+  P.bt_cnt = e->bt_cnt;
   return SA_OK;
 }
 
@@ -493,6 +592,9 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   hipError_t st;
   if (e->small) {
     st = sa::launch_ingest_small(P, grid, e->lds_bytes, s, e->variant);
+  } else if (e->bt) {
+    if (int rc = bt_prepare_launch(e, b->n, P, s)) return rc;
+    st = sa::launch_ingest_bt(P, e->agg_lds, s);
   } else if (e->part) {
     // records per bin: 1.25x the mean plus slack; a fuller bin spills to the
     // direct path, so this bounds memory, not correctness
@@ -622,8 +724,9 @@ int sa_flush(sa_engine *e, sa_red_result **out) {
   if (int rc = reduce_slabs(e, e->stream)) return rc;
   const uint32_t stride = e->nbk + 1;
   SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, e->stream));
-  SA_HIP(e, sa::launch_compact(e->gkeys, e->gcounts, e->cap, e->nbk, e->out_keys, e->out_rows,
+  SA_HIP(e, sa::launch_compact(e->gkeys, e->gcounts, e->cap, geom(e), e->out_keys, e->out_rows,
                                e->scratch, e->cap, 1, e->stream));
+  e->since_fold = 0;
   uint64_t n = 0;
   SA_HIP(e, hipMemcpyAsync(&n, e->scratch, 8, hipMemcpyDeviceToHost, e->stream));
   SA_HIP(e, hipStreamSynchronize(e->stream));
@@ -697,7 +800,7 @@ static int fold_window(sa_engine *e, uint64_t ws, hipStream_t s) {
   if (int rc = fold_errslab(e, ws, s)) return rc;
   SA_HIP(e, sa::launch_fold_errcnt(e->gkeys, e->errcnt + ws * e->cap, e->cap,
                                    e->cms + ws * e->cms_slot_elems, e->cfg.cms_d, e->cfg.cms_w,
-                                   64 - log2u(e->cfg.cms_w), e->d_seeds, s));
+                                   64 - log2u(e->cfg.cms_w), e->d_seeds, e->kinv, s));
   return SA_OK;
 }
 
@@ -801,7 +904,7 @@ int sa_export_keys(sa_engine *e, uint64_t *d_keys, uint64_t cap, uint64_t *n_out
   }
   if (int rc = reduce_slabs(e, s)) return rc;
   SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, s));
-  SA_HIP(e, sa::launch_compact(e->gkeys, e->gcounts, e->cap, e->nbk,
+  SA_HIP(e, sa::launch_compact(e->gkeys, e->gcounts, e->cap, geom(e),
                                reinterpret_cast<unsigned long long *>(d_keys), nullptr, e->scratch,
                                cap, 0, s));
   SA_HIP(e, hipMemcpyAsync(n_out, e->scratch, 8, hipMemcpyDeviceToHost, s));
@@ -820,9 +923,12 @@ int sa_gather_dense(sa_engine *e, const uint64_t *d_keys, uint64_t n, uint64_t *
     SA_HIP(e, hipStreamWaitEvent(s, e->ev_a, 0));
   }
   if (int rc = reduce_slabs(e, s)) return rc;
-  SA_HIP(e, sa::launch_gather_dense(e->gkeys, e->gcounts, e->log2cap, sa::max_probe_of(e->log2cap), e->nbk,
-                                    d_keys, n, d_rows, s));
-  if (reset) SA_HIP(e, hipMemsetAsync(e->gcounts, 0, e->cap * sa::row_stride(e->nbk) * 8, s));
+  SA_HIP(e, sa::launch_gather_dense(e->gkeys, e->gcounts, geom(e), d_keys, n, d_rows, s));
+  if (reset) {
+    SA_HIP(e, hipMemsetAsync(e->gcounts, 0, counts_bytes(e), s));
+    if (e->base64) SA_HIP(e, hipMemsetAsync(e->base64, 0, (size_t)e->cap * (e->nbk + 1) * 8, s));
+    e->since_fold = 0;
+  }
   if (s != e->stream) {
     SA_HIP(e, hipEventRecord(e->ev_b, s));
     SA_HIP(e, hipStreamWaitEvent(e->stream, e->ev_b, 0));

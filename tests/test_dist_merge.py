@@ -130,7 +130,7 @@ def test_shard_of_keeps_traces_together():
     assert list(s) == [1, 1, 2, 3]
 
 
-def _gpu_worker(rank, world, port, n, errq):
+def _gpu_worker(rank, world, port, n, errq, kcap=1500):
     """The real GPU merge hooks (sa_export_keys / sa_gather_dense /
     sa_window_export through EnginePartial) with two ranks sharing cuda:0 over
     gloo (RCCL refuses two ranks on one device; the merge code is the same)."""
@@ -151,7 +151,7 @@ def _gpu_worker(rank, world, port, n, errq):
         full = pyoracle.Oracle(n_services=wl.n_services)
         full.ingest(wl.batch)
         ref = full.series()
-        with Engine(Config(n_services=wl.n_services, n_windows=16, key_capacity=1500, device=0)) as e:
+        with Engine(Config(n_services=wl.n_services, n_windows=16, key_capacity=kcap, device=0)) as e:
             e.window_advance(wl.first_window)
             e.ingest(sub)
             part = EnginePartial(e, torch.device("cuda", 0))
@@ -175,11 +175,12 @@ def _gpu_worker(rank, world, port, n, errq):
 
 
 @pytest.mark.gpu
-def test_gpu_merge_hooks_two_ranks_match_single_aggregation():
+@pytest.mark.parametrize("kcap", [1500, 600_000])  # LDS-mirrored table, binned HBM table
+def test_gpu_merge_hooks_two_ranks_match_single_aggregation(kcap):
     ctx = mp.get_context("spawn")
     errq = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, 200_000, errq)) for r in range(2)]
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, 200_000, errq, kcap)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

@@ -1,0 +1,142 @@
+"""GPU parity of the binned-table high-cardinality path (spanagg_binned.hip:
+bt_scatter_kernel + bt_aggregate_kernel; tables of 2^19..2^22 slots) against
+the CPU oracle, including the spill paths (stage/region overflow table, the
+direct path), the u32 row fold, full bins and launch splitting.
+
+Bar (north_star): bucket counts, calls, HLL registers and count-min cells
+bit-exact; duration sums within 1e-9 relative (parity_util.SUM_RTOL).
+"""
+import numpy as np
+import pytest
+
+import pyoracle
+from parity_util import assert_red_equal
+from spanagg import Config, Engine, SpanBatch
+from spanagg.synth import generate_highcard
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle(batch):
+    o = pyoracle.Oracle(n_services=1)
+    o.ingest(batch)
+    return o
+
+
+def _check(e, batch, o=None, n_dropped=0, o_windows=None):
+    """RED of `batch` since the last flush vs the oracle; sketch windows
+    (cumulative, not reset by flush) vs o_windows (default: the same oracle)."""
+    o = o or _oracle(batch)
+    res = e.flush()
+    assert_red_equal(res, o.series())
+    ow = o_windows or o
+    for wid in ow.window_ids():
+        sk = e.window_read(wid)
+        hll, cms = ow.window(wid)
+        assert np.array_equal(sk.hll, hll), wid
+        assert np.array_equal(sk.cms, cms), wid
+    st = e.stats()
+    assert st["dropped_table_full"] == n_dropped
+    assert int(res.calls.sum()) == len(batch) - st["zero_key"]  # zero_key: 0 in these workloads
+    return res
+
+
+def _engine(kcap, **kw):
+    e = Engine(Config(n_services=1, n_windows=16, key_capacity=kcap, **kw))
+    assert e.stats()["small_table"] == 0
+    return e
+
+
+def test_c4zipf_full_size_bit_exact():
+    """BASELINE config 4, Zipf(1.1) over the 1 M keys, 10 M spans in one
+    binned launch (the bench's c4zipf workload): the hottest keys overfill
+    their stages and regions, so the overflow table and the direct path run."""
+    n = 10_000_000
+    batch, _, w0 = generate_highcard(n, zipf_s=1.1)
+    with _engine(1_200_000) as e:
+        e.window_advance(w0)
+        e.ingest(batch)
+        _check(e, batch)
+
+
+@pytest.mark.parametrize("zipf", [0.0, 1.3])
+def test_binned_matches_partitioned_path(zipf, monkeypatch):
+    """Same input through the binned path and the round-1 partitioned path
+    (SPANAGG_BINNED=0), two ingests each: both equal the oracle."""
+    batch, _, w0 = generate_highcard(3_000_000, seed=13, routes=1000, pods=300, zipf_s=zipf)
+    half = len(batch) // 2
+    o = _oracle(batch)
+    for binned in ("1", "0"):
+        monkeypatch.setenv("SPANAGG_BINNED", binned)
+        with _engine(600_000) as e:
+            e.window_advance(w0)
+            e.ingest(batch.slice(0, half))
+            e.ingest(batch.slice(half, len(batch)))
+            _check(e, batch, o)
+
+
+def test_binned_u32_rows_fold(monkeypatch):
+    """u32 bucket counts are folded into the u64 array before they could
+    wrap; a small fold limit folds between every launch (and after a flush)."""
+    monkeypatch.setenv("SPANAGG_FOLD_LIMIT", "150000")
+    batch, _, w0 = generate_highcard(600_000, seed=17, routes=200, pods=100, zipf_s=1.1)
+    with _engine(600_000) as e:
+        e.window_advance(w0)
+        for a in range(0, 400_000, 100_000):
+            e.ingest(batch.slice(a, a + 100_000))
+        _check(e, batch.slice(0, 400_000))
+        e.ingest(batch.slice(400_000, 600_000))
+        _check(e, batch.slice(400_000, 600_000), o_windows=_oracle(batch))
+
+
+def test_binned_full_bin_reports_drops(monkeypatch):
+    """With the identity id map (SPANAGG_KMUL=1) 1,000 keys that share their
+    top 11 bits all land in one bin of 256 slots: the bin fills, the spans of
+    the keys that found no slot are dropped and reported, every kept series
+    is exact (a key is kept or dropped as a whole: slots never empty)."""
+    monkeypatch.setenv("SPANAGG_KMUL", "1")
+    n = 200_000
+    batch, _, w0 = generate_highcard(n, seed=19, routes=100, pods=100)
+    rng = np.random.Generator(np.random.PCG64(19))
+    ids = rng.integers(0, 1000, n).astype(np.uint64)
+    with np.errstate(over="ignore"):
+        low = (ids + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+    keys = (np.uint64(0x155) << np.uint64(53)) | (low >> np.uint64(11)) | np.uint64(1)
+    one_bin = SpanBatch(keys, *batch.columns()[1:])
+    ref = _oracle(one_bin).series()
+    with _engine(400_000) as e:  # cap 2^19: 2,048 bins of 256 slots
+        e.window_advance(w0)
+        e.ingest(one_bin)
+        res = e.flush(allow_drops=True)
+        st = e.stats()
+        assert len(res.key_hash) == 256
+        assert int(res.calls.sum()) + st["dropped_table_full"] == n
+        pos = np.searchsorted(ref["key_hash"], res.key_hash)
+        assert np.array_equal(ref["key_hash"][pos], res.key_hash)
+        assert np.array_equal(ref["bucket_counts"][pos], res.bucket_counts)
+        assert np.array_equal(ref["sum_ns"][pos], res.sum_ns)
+
+
+def test_binned_batch_above_launch_limit_is_split():
+    """17 M spans in one sa_ingest: more than one binned launch takes (one
+    scatter workgroup per CU x 65,520 spans), so it is split in two."""
+    n = 17_000_000
+    batch, _, w0 = generate_highcard(n, seed=23, routes=400, pods=250)
+    with _engine(600_000) as e:
+        e.window_advance(w0)
+        e.ingest(batch)
+        _check(e, batch)
+
+
+def test_binned_repeat_runs_identical():
+    """Placement (the per-engine random id multiplier, atomics order) never
+    changes results."""
+    batch, _, w0 = generate_highcard(1_000_000, seed=29, routes=500, pods=200, zipf_s=1.1)
+    outs = []
+    for _ in range(2):
+        with _engine(600_000) as e:
+            e.window_advance(w0)
+            e.ingest(batch)
+            outs.append(e.flush())
+    for f in ("key_hash", "bucket_counts", "sum_ns"):
+        assert np.array_equal(getattr(outs[0], f), getattr(outs[1], f))

@@ -56,7 +56,8 @@ def expected_oor(case, lo):
 
 
 @pytest.mark.parametrize("idx", range(5))
-@pytest.mark.parametrize("key_capacity", [1000, 300_000])  # LDS-mirrored and HBM-table paths
+# LDS-mirrored (small) table, partitioned HBM table (2^17 slots), binned table (2^19)
+@pytest.mark.parametrize("key_capacity", [1000, 100_000, 300_000])
 def test_golden_cases(golden, idx, key_capacity):
     case = golden["cases"][idx]
     e, lo = engine_for_case(case, key_capacity=key_capacity)

@@ -58,10 +58,11 @@ def main():
     n = int(os.environ.get("ABL_SPANS", 10_000_000))
     rounds = int(os.environ.get("ABL_ROUNDS", 7))
     reps = int(os.environ.get("ABL_REPS", 10))
-    c4 = os.environ.get("ABL_WORKLOAD") == "c4"
+    c4 = os.environ.get("ABL_WORKLOAD") in ("c4", "c4zipf")
     if c4:  # high-cardinality HBM-table path (1 M keys, one service)
         from spanagg.synth import generate_highcard
-        hb, _, hfirst = generate_highcard(n, seed=7, routes=int(os.environ.get("ABL_ROUTES", 2000)))
+        hb, _, hfirst = generate_highcard(n, seed=7, routes=int(os.environ.get("ABL_ROUTES", 2000)),
+                                          zipf_s=1.1 if os.environ.get("ABL_WORKLOAD") == "c4zipf" else 0.0)
 
         class _W:
             batch, first_window, n_services = hb, hfirst, 1
@@ -82,7 +83,7 @@ def main():
     if os.environ.get("ABL_FLAGS"):  # explicit set: "name:flags,name:flags"
         VARIANTS.clear()
         VARIANTS.update({k: int(v) for k, v in (x.split(":") for x in os.environ["ABL_FLAGS"].split(","))})
-    if c4:
+    if c4 and not os.environ.get("ABL_FLAGS"):
         VARIANTS.update(VARIANTS_C4)
     if os.environ.get("ABL_FINE"):
         VARIANTS.update(VARIANTS_FINE)

@@ -1,0 +1,60 @@
+#!/bin/bash
+# One GPU-box job made of named steps, each under its own time limit.
+#   usage (inside gpurun): TAG=name bash tools/gpu_job.sh STEP [STEP ...]
+# Steps:
+#   tests            every -m gpu test (pytest, per-test timeout)
+#   tests:<file>     one test file, e.g. tests:tests/test_gpu_binned.py
+#   bench            the default bench line (C2 + C4 sub-objects, CPU baselines)
+#   bench_<wl>       a short bench of one workload (c2, c4, c4zipf), no baselines
+#   ablate_<wl>      tools/ablate.py over the ABL_FLAGS variant set for <wl>
+#   trace_<wl>       rocprofv3 --kernel-trace --stats of a short bench of <wl>
+#   pmc_<wl>_<set>   one rocprofv3 --pmc pass (set: fetch, write, lds, sq) over
+#                    tools/prof_driver.py for <wl>
+# Outputs go to gpurun_out/$TAG/.  Any failing step ends the job (exit code
+# kept): a failed test may be a GPU fault, after which nothing more runs on
+# the GPU in that call.  LENIENT=1 lets a step that returned 1 continue.
+set -u
+TAG=${TAG:-job}
+OUT=$PWD/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+ROOTDIR=$PWD
+
+run() {  # name, seconds, command...
+  local name=$1 t=$2
+  shift 2
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" >> "$OUT/status.txt"
+  if [ "$rc" = 0 ] || { [ "$rc" = 1 ] && [ "${LENIENT:-0}" = 1 ]; }; then return 0; fi
+  echo "FATAL $name rc=$rc" >> "$OUT/status.txt"
+  exit $rc
+}
+
+BQ="--no-cpu-baseline --host-otlp-spans 0 --h2d-reps 0"
+for step in "$@"; do
+  case $step in
+    tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    tests:*) f=${step#tests:}; run "tests_$(basename "$f" .py)" 600 python -u -m pytest "$f" -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    bench) run bench 500 python bench.py ;;
+    bench_*) wl=${step#bench_}; run "bench_$wl" 300 python bench.py --workload "$wl" --sub "" --steps 20 $BQ ;;
+    ablate_*) wl=${step#ablate_}; ABL_WORKLOAD=$wl ABL_VARS= run "ablate_$wl" 400 python tools/ablate.py ;;
+    trace_*) wl=${step#trace_}
+      (cd /tmp && run "trace_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$wl" -o run \
+         -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 10 --warmup 2 --streams 1 $BQ) || exit $? ;;
+    pmc_*) rest=${step#pmc_}; wl=${rest%%_*}; set_=${rest#*_}
+      case $set_ in
+        fetch) ctr="FETCH_SIZE" ;;
+        write) ctr="WRITE_SIZE" ;;
+        lds) ctr="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAVES" ;;
+        sq) ctr="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" ;;
+        inst) ctr="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_WAVES" ;;
+        ta) ctr="TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_PENDING_STALL_CYCLES_sum GRBM_GUI_ACTIVE" ;;
+        *) echo "unknown pmc set $set_" >> "$OUT/status.txt"; exit 2 ;;
+      esac
+      (cd /tmp && PROF_WORKLOAD=$wl run "pmc_${wl}_$set_" 120 rocprofv3 --pmc $ctr --output-format csv \
+         -d "$OUT/pmc_${wl}_$set_" -o run -- python3 "$ROOTDIR/tools/prof_driver.py") || exit $? ;;
+    *) echo "unknown step $step" >> "$OUT/status.txt"; exit 2 ;;
+  esac
+done
+echo done >> "$OUT/status.txt"

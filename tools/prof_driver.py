@@ -15,9 +15,10 @@ from spanagg.synth import generate_c2  # noqa: E402
 
 n = int(os.environ.get("PROF_SPANS", 10_000_000))
 reps = int(os.environ.get("PROF_REPS", 5))
-if os.environ.get("PROF_WORKLOAD") == "c4":  # 1 M series, HBM table (partitioned path)
+wk = os.environ.get("PROF_WORKLOAD", "c2")
+if wk in ("c4", "c4zipf"):  # 1 M series, HBM table (binned path)
     from spanagg.synth import generate_highcard
-    batch, _, first = generate_highcard(n, seed=7)
+    batch, _, first = generate_highcard(n, seed=7, zipf_s=1.1 if wk == "c4zipf" else 0.0)
     n_services, kcap = 1, 1_200_000
 else:
     wl = generate_c2(n, seed=42)
