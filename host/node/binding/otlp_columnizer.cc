@@ -239,23 +239,81 @@ Any parse_any(PB pb) {
   return a;
 }
 
-// KeyValue -> (key, value); ok=false on malformed input
-bool parse_kv(PB pb, std::string_view &key, Any &val) {
-  key = {};
-  val = Any{};
+// Nesting limit for array / kvlist attribute values (Go's protobuf decoder
+// also bounds recursion): a deeper value makes the request malformed instead
+// of recursing on the native stack.
+constexpr int kMaxAnyDepth = 100;
+
+// Structure of an AnyValue body (nested arrays / kvlists included) down to
+// kMaxAnyDepth levels: false when malformed or nested deeper.
+bool valid_any_body(PB pb, int depth);
+bool valid_nested(PB pb, bool kvlist, int depth) {
   uint32_t f;
   int wt;
   while (pb.next(f, wt)) {
-    if (f == 1 && wt == 2) key = pb.str();
-    else if (f == 2 && wt == 2) val = parse_any(pb.sub());
-    else pb.skip(wt);
+    if (f == 1 && wt == 2) {
+      PB item = pb.sub();
+      if (!kvlist) {
+        if (!valid_any_body(item, depth + 1)) return false;
+      } else {
+        uint32_t g;
+        int wt2;
+        while (item.next(g, wt2)) {
+          if (g == 2 && wt2 == 2) {
+            if (!valid_any_body(item.sub(), depth + 1)) return false;
+          } else {
+            item.skip(wt2);
+          }
+        }
+        if (!item.ok) return false;
+      }
+    } else {
+      pb.skip(wt);
+    }
+  }
+  return pb.ok;
+}
+bool valid_any_body(PB pb, int depth) {
+  if (depth > kMaxAnyDepth) return false;
+  uint32_t f;
+  int wt;
+  while (pb.next(f, wt)) {
+    if ((f == 5 || f == 6) && wt == 2) {
+      if (!valid_nested(pb.sub(), f == 6, depth)) return false;
+    } else {
+      pb.skip(wt);
+    }
   }
   return pb.ok;
 }
 
-bool raw_json(std::string &o, const Any &a);
+// KeyValue -> (key, value); false on malformed input, a malformed or too
+// deeply nested value included (the request is then rejected, as the Go
+// collector's unmarshal and otlp.js reject it)
+bool parse_kv(PB pb, std::string_view &key, Any &val) {
+  key = {};
+  val = Any{};
+  bool vok = true;
+  uint32_t f;
+  int wt;
+  while (pb.next(f, wt)) {
+    if (f == 1 && wt == 2) {
+      key = pb.str();
+    } else if (f == 2 && wt == 2) {
+      const PB body = pb.sub();
+      val = parse_any(body);
+      vok = valid_any_body(body, 0);
+    } else {
+      pb.skip(wt);
+    }
+  }
+  return pb.ok && vok;
+}
+enum class Keyable { kYes, kNotNative, kTooDeep };
 
-bool raw_json_array(std::string &o, PB pb) {
+Keyable raw_json(std::string &o, const Any &a, int depth);
+
+Keyable raw_json_array(std::string &o, PB pb, int depth) {
   o += '[';
   bool first = true;
   uint32_t f;
@@ -264,16 +322,17 @@ bool raw_json_array(std::string &o, PB pb) {
     if (f == 1 && wt == 2) {
       if (!first) o += ',';
       first = false;
-      if (!raw_json(o, parse_any(pb.sub()))) return false;
+      const Keyable k = raw_json(o, parse_any(pb.sub()), depth + 1);
+      if (k != Keyable::kYes) return k;
     } else {
       pb.skip(wt);
     }
   }
   o += ']';
-  return pb.ok;
+  return pb.ok ? Keyable::kYes : Keyable::kNotNative;
 }
 
-bool raw_json_kvlist(std::string &o, PB pb) {
+Keyable raw_json_kvlist(std::string &o, PB pb, int depth) {
   o += '{';
   bool first = true;
   uint32_t f;
@@ -282,54 +341,58 @@ bool raw_json_kvlist(std::string &o, PB pb) {
     if (f == 1 && wt == 2) {
       std::string_view k;
       Any v;
-      if (!parse_kv(pb.sub(), k, v) || !valid_utf8(k)) return false;
+      if (!parse_kv(pb.sub(), k, v) || !valid_utf8(k)) return Keyable::kNotNative;
       if (!first) o += ',';
       first = false;
       json_string(o, k);
       o += ':';
-      if (!raw_json(o, v)) return false;
+      const Keyable kk = raw_json(o, v, depth + 1);
+      if (kk != Keyable::kYes) return kk;
     } else {
       pb.skip(wt);
     }
   }
   o += '}';
-  return pb.ok;
+  return pb.ok ? Keyable::kYes : Keyable::kNotNative;
 }
 
 // keys.js rawJson
-bool raw_json(std::string &o, const Any &a) {
+Keyable raw_json(std::string &o, const Any &a, int depth) {
   switch (a.type) {
     case kStr:
-      if (!valid_utf8(a.s)) return false;
+      if (!valid_utf8(a.s)) return Keyable::kNotNative;
       json_string(o, a.s);
-      return true;
-    case kBool: o += a.b ? "true" : "false"; return true;
-    case kInt: o += std::to_string(a.i); return true;
+      return Keyable::kYes;
+    case kBool: o += a.b ? "true" : "false"; return Keyable::kYes;
+    case kInt: o += std::to_string(a.i); return Keyable::kYes;
     case kDouble:
       if (std::isfinite(a.d)) o += js_number(a.d);
       else json_string(o, format_float(a.d));
-      return true;
-    case kBytes: json_string(o, base64(a.s)); return true;
-    case kArray: return raw_json_array(o, a.body);
-    case kKvlist: return raw_json_kvlist(o, a.body);
-    default: o += "null"; return true;
+      return Keyable::kYes;
+    case kBytes: json_string(o, base64(a.s)); return Keyable::kYes;
+    case kArray:
+      return depth >= kMaxAnyDepth ? Keyable::kTooDeep : raw_json_array(o, a.body, depth);
+    case kKvlist:
+      return depth >= kMaxAnyDepth ? Keyable::kTooDeep : raw_json_kvlist(o, a.body, depth);
+    default: o += "null"; return Keyable::kYes;
   }
 }
 
-// keys.js asString; false when the value cannot be keyed natively
-bool as_string(const Any &a, std::string &o) {
+// keys.js asString; kNotNative when the value cannot be keyed natively (the
+// JavaScript columnizer takes the request), kTooDeep for a malformed request
+Keyable as_string(const Any &a, std::string &o) {
   o.clear();
   switch (a.type) {
     case kStr:
-      if (!valid_utf8(a.s)) return false;
+      if (!valid_utf8(a.s)) return Keyable::kNotNative;
       o.assign(a.s);
-      return true;
-    case kBool: o = a.b ? "true" : "false"; return true;
-    case kInt: o = std::to_string(a.i); return true;
-    case kDouble: o = format_float(a.d); return true;
-    case kBytes: o = base64(a.s); return true;
-    case kArray: case kKvlist: return raw_json(o, a);
-    default: return true;
+      return Keyable::kYes;
+    case kBool: o = a.b ? "true" : "false"; return Keyable::kYes;
+    case kInt: o = std::to_string(a.i); return Keyable::kYes;
+    case kDouble: o = format_float(a.d); return Keyable::kYes;
+    case kBytes: o = base64(a.s); return Keyable::kYes;
+    case kArray: case kKvlist: return raw_json(o, a, 1);
+    default: return Keyable::kYes;
   }
 }
 
@@ -558,7 +621,9 @@ Result Columnizer::columnize(const uint8_t *buf, size_t len) {
     std::sort(hv.begin(), hv.end(), [](const Attr *x, const Attr *y) { return x->key < y->key; });
     hbuf.clear();
     for (const Attr *a : hv) {
-      if (!as_string(a->val, tmp)) return rollback(Result::kFallback, "resource attribute not keyable natively");
+      if (const Keyable k = as_string(a->val, tmp); k != Keyable::kYes)
+        return k == Keyable::kTooDeep ? rollback(Result::kError, "attribute value nested too deeply")
+                                      : rollback(Result::kFallback, "resource attribute not keyable natively");
       hbuf.insert(hbuf.end(), a->key.begin(), a->key.end());
       hbuf.push_back(0);
       hbuf.insert(hbuf.end(), tmp.begin(), tmp.end());
@@ -661,7 +726,9 @@ Result Columnizer::columnize(const uint8_t *buf, size_t len) {
           const Any *v = find_attr(sattrs, d.name);
           if (!v) v = find_attr(rattrs, d.name);
           if (v) {
-            if (!as_string(*v, tmp)) return rollback(Result::kFallback, "dimension value not keyable natively");
+            if (const Keyable k = as_string(*v, tmp); k != Keyable::kYes)
+              return k == Keyable::kTooDeep ? rollback(Result::kError, "attribute value nested too deeply")
+                                            : rollback(Result::kFallback, "dimension value not keyable natively");
           } else if (d.has_default) {
             tmp = d.def;
           } else {

@@ -105,25 +105,29 @@ class Reader {
   }
 }
 
-function decodeArray(r) {
+/** Nesting limit for array / kvlist values (as the native columnizer's kMaxAnyDepth). */
+const MAX_ANY_DEPTH = 100;
+
+function decodeArray(r, depth) {
   const out = [];
   r.fields((f, wt) => {
-    if (f === 1 && wt === WT_LEN) { out.push(decodeAnyValue(r.sub())); return true; }
+    if (f === 1 && wt === WT_LEN) { out.push(decodeAnyValue(r.sub(), depth + 1)); return true; }
     return false;
   });
   return out;
 }
 
-function decodeKvList(r) {
+function decodeKvList(r, depth) {
   const out = [];
   r.fields((f, wt) => {
-    if (f === 1 && wt === WT_LEN) { out.push(decodeKeyValue(r.sub())); return true; }
+    if (f === 1 && wt === WT_LEN) { out.push(decodeKeyValue(r.sub(), depth + 1)); return true; }
     return false;
   });
   return out;
 }
 
-function decodeAnyValue(r) {
+function decodeAnyValue(r, depth = 0) {
+  if (depth > MAX_ANY_DEPTH) throw new Error('protobuf: attribute value nested too deeply');
   let v = { type: 'empty', value: null };
   r.fields((f, wt) => {
     switch (f) {
@@ -131,8 +135,8 @@ function decodeAnyValue(r) {
       case 2: if (wt !== WT_VARINT) return false; v = { type: 'bool', value: r.varint64() !== 0n }; return true;
       case 3: if (wt !== WT_VARINT) return false; v = { type: 'int', value: BigInt.asIntN(64, r.varint64()) }; return true;
       case 4: if (wt !== WT_I64) return false; v = { type: 'double', value: r.double() }; return true;
-      case 5: if (wt !== WT_LEN) return false; v = { type: 'array', value: decodeArray(r.sub()) }; return true;
-      case 6: if (wt !== WT_LEN) return false; v = { type: 'kvlist', value: decodeKvList(r.sub()) }; return true;
+      case 5: if (wt !== WT_LEN) return false; v = { type: 'array', value: decodeArray(r.sub(), depth) }; return true;
+      case 6: if (wt !== WT_LEN) return false; v = { type: 'kvlist', value: decodeKvList(r.sub(), depth) }; return true;
       case 7: if (wt !== WT_LEN) return false; v = { type: 'bytes', value: Uint8Array.from(r.bytes()) }; return true;
       default: return false;
     }
@@ -140,11 +144,11 @@ function decodeAnyValue(r) {
   return v;
 }
 
-function decodeKeyValue(r) {
+function decodeKeyValue(r, depth = 0) {
   let key = '', value = { type: 'empty', value: null };
   r.fields((f, wt) => {
     if (f === 1 && wt === WT_LEN) { key = r.string(); return true; }
-    if (f === 2 && wt === WT_LEN) { value = decodeAnyValue(r.sub()); return true; }
+    if (f === 2 && wt === WT_LEN) { value = decodeAnyValue(r.sub(), depth); return true; }
     return false;
   });
   return { key, value };

@@ -21,7 +21,7 @@ const zlib = require('zlib');
 
 const TRACE_EXPORT_PATH = '/opentelemetry.proto.collector.trace.v1.TraceService/Export';
 const GRPC_OK = 0, GRPC_INTERNAL = 13, GRPC_UNAVAILABLE = 14, GRPC_UNIMPLEMENTED = 12,
-  GRPC_INVALID_ARGUMENT = 3;
+  GRPC_INVALID_ARGUMENT = 3, GRPC_RESOURCE_EXHAUSTED = 8;
 
 class RefusedError extends Error {
   constructor(msg) { super(msg); this.refused = true; }
@@ -60,11 +60,32 @@ class MemoryLimiter {
   }
 }
 
-function inflate(body, encoding) {
+/**
+ * Request bodies are limited after decompression too (Go's confighttp applies
+ * max_request_body_size to the decompressed body, gRPC its max_recv_msg_size
+ * to the decompressed message): a small gzip bomb fails with tooLarge.
+ */
+function inflate(body, encoding, max = Infinity) {
   if (!encoding || encoding === 'identity') return body;
-  if (encoding === 'gzip') return zlib.gunzipSync(body);
-  if (encoding === 'deflate') return zlib.inflateSync(body);
-  throw new Error(`unsupported content encoding ${encoding}`);
+  const opts = Number.isFinite(max) ? { maxOutputLength: max } : {};
+  try {
+    if (encoding === 'gzip') return zlib.gunzipSync(body, opts);
+    if (encoding === 'deflate') return zlib.inflateSync(body, opts);
+  } catch (e) {
+    const err = new Error(e instanceof RangeError || e.code === 'ERR_BUFFER_TOO_LARGE'
+      ? 'decompressed request body too large' : `bad ${encoding} body: ${e.message}`);
+    if (e instanceof RangeError || e.code === 'ERR_BUFFER_TOO_LARGE') err.tooLarge = true;
+    else err.badRequest = true;
+    throw err;
+  }
+  const err = new Error(`unsupported content encoding ${encoding}`);
+  err.badRequest = true;
+  throw err;
+}
+
+/** Errors that mean the request itself is malformed (-> 400 / INVALID_ARGUMENT). */
+function isBadRequest(e) {
+  return !!(e && (e.badRequest || /^(OTLP request|protobuf)/.test(String(e.message))));
 }
 
 /**
@@ -116,10 +137,11 @@ class OtlpReceiver {
     if (type !== 'application/x-protobuf') return void (req.resume(), reply(415, Buffer.from('only application/x-protobuf is supported'), 'text/plain'));
     readBody(req, this.maxBody).then((raw) => {
       try {
-        this.onTraces(inflate(raw, req.headers['content-encoding']));
+        this.onTraces(inflate(raw, req.headers['content-encoding'], this.maxBody));
         reply(200);  // empty ExportTraceServiceResponse
       } catch (e) {
-        reply(e.refused ? 503 : 500, Buffer.from(String(e.message)), 'text/plain');
+        const code = e.refused ? 503 : e.tooLarge ? 413 : isBadRequest(e) ? 400 : 500;
+        reply(code, Buffer.from(String(e.message)), 'text/plain');
       }
     }, (e) => reply(e.tooLarge ? 413 : 400, Buffer.from(String(e.message)), 'text/plain'));
   }
@@ -142,14 +164,14 @@ class OtlpReceiver {
     readBody(stream, this.maxBody).then((raw) => {
       let msgs;
       try {
-        msgs = grpcUnframe(raw, headers['grpc-encoding']);
+        msgs = grpcUnframe(raw, headers['grpc-encoding'], this.maxBody);
       } catch (e) {
-        return done(GRPC_INVALID_ARGUMENT, e.message);
+        return done(e.tooLarge ? GRPC_RESOURCE_EXHAUSTED : GRPC_INVALID_ARGUMENT, e.message);
       }
       try {
         for (const m of msgs) this.onTraces(m);
       } catch (e) {
-        return done(e.refused ? GRPC_UNAVAILABLE : GRPC_INTERNAL, e.message);
+        return done(e.refused ? GRPC_UNAVAILABLE : isBadRequest(e) ? GRPC_INVALID_ARGUMENT : GRPC_INTERNAL, e.message);
       }
       return done(GRPC_OK, null, grpcFrame(Buffer.alloc(0)));  // empty ExportTraceServiceResponse
     }, (e) => done(GRPC_INVALID_ARGUMENT, e.message));
@@ -184,7 +206,7 @@ function readBody(stream, max) {
 }
 
 /** gRPC length-prefixed messages: [compressed u8][length u32 BE][message]. */
-function grpcUnframe(buf, encoding) {
+function grpcUnframe(buf, encoding, max = Infinity) {
   const out = [];
   let p = 0;
   while (p < buf.length) {
@@ -192,7 +214,7 @@ function grpcUnframe(buf, encoding) {
     const compressed = buf[p], len = buf.readUInt32BE(p + 1);
     if (p + 5 + len > buf.length) throw new Error('truncated gRPC message');
     const msg = buf.subarray(p + 5, p + 5 + len);
-    out.push(compressed ? inflate(msg, encoding || 'gzip') : msg);
+    out.push(compressed ? inflate(msg, encoding || 'gzip', max) : msg);
     p += 5 + len;
   }
   return out;

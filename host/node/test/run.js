@@ -568,6 +568,87 @@ test('pipeline: OTLP/HTTP in -> transform -> connector -> otlphttp out', async (
 });
 
 
+// An ExportTraceServiceRequest whose one resource attribute is an array
+// nested `levels` deep, written back to front in one buffer (no recursion).
+function deepNestedRequest(levels) {
+  const varintLen = (n) => { let l = 1; while (n >= 128) { n = Math.floor(n / 128); l++; } return l; };
+  const inner = Buffer.from([0x0a, 0x01, 0x78]);  // AnyValue{string_value: "x"}
+  let size = inner.length;
+  const sizes = [];
+  for (let i = 0; i < levels; i++) {  // ArrayValue{values: any} then AnyValue{array_value: arr}
+    const arr = 1 + varintLen(size) + size;
+    const any = 1 + varintLen(arr) + arr;
+    sizes.push([size, arr]);
+    size = any;
+  }
+  const buf = Buffer.alloc(size);
+  let p = size - inner.length;
+  inner.copy(buf, p);
+  const putVarint = (n) => {  // ending at p
+    const bytes = [];
+    do { let b = n % 128; n = Math.floor(n / 128); if (n) b |= 128; bytes.push(b); } while (n);
+    p -= bytes.length;
+    Buffer.from(bytes).copy(buf, p);
+  };
+  for (let i = 0; i < levels; i++) {  // innermost level first: the buffer fills back to front
+    const [inSize, arr] = sizes[i];
+    putVarint(inSize); buf[--p] = 0x0a;   // ArrayValue.values (1, LEN)
+    putVarint(arr); buf[--p] = 0x2a;      // AnyValue.array_value (5, LEN)
+  }
+  const w = (field, payload) => Buffer.concat([Buffer.from([(field << 3) | 2]), varintBuf(payload.length), payload]);
+  const varintBuf = (n) => { const b = []; do { let x = n % 128; n = Math.floor(n / 128); if (n) x |= 128; b.push(x); } while (n); return Buffer.from(b); };
+  const kv = (key, anyBytes) => Buffer.concat([w(1, Buffer.from(key)), w(2, anyBytes)]);
+  const resource = Buffer.concat([w(1, kv('service.name', Buffer.from([0x0a, 0x01, 0x61]))), w(1, kv('deep', buf))]);
+  const spanBytes = Buffer.concat([w(1, Buffer.alloc(16, 1)), w(5, Buffer.from('op'))]);
+  const rs = Buffer.concat([w(1, resource), w(2, w(2, spanBytes))]);
+  return w(1, rs);
+}
+
+test('receiver: an attribute nested 100k levels deep is a 400, and the host keeps serving', async () => {
+  const body = deepNestedRequest(100000);
+  for (const addon of [new NativeColumnizerFakeAddon(), new FakeAddon()]) {
+    const p = await new TracesToMetricsPipeline({ addon, clock: () => 7n, exporter: false, memoryLimiter: false,
+      receiver: { httpPort: 0, grpcPort: 0 } }).start();
+    try {
+      let r = await post(p.receiver.httpPort, '/v1/traces', body, { 'Content-Type': 'application/x-protobuf' });
+      assert.strictEqual(r.status, 400, String(r.body));
+      const g = await grpcCall(p.receiver.grpcPort, TRACE_EXPORT_PATH, grpcFrame(body));
+      assert.strictEqual(g.trailers['grpc-status'], '3');
+      const ok = otlp.encodeTraces(request([[{ 'service.name': 'a' }, [span('x')]]]));
+      r = await post(p.receiver.httpPort, '/v1/traces', ok, { 'Content-Type': 'application/x-protobuf' });
+      assert.strictEqual(r.status, 200);
+      // 100 levels is still a valid request
+      r = await post(p.receiver.httpPort, '/v1/traces', deepNestedRequest(99), { 'Content-Type': 'application/x-protobuf' });
+      assert.strictEqual(r.status, 200, String(r.body));
+    } finally {
+      await p.shutdown();
+    }
+  }
+});
+
+test('receiver: the body limit applies after decompression (gzip bomb -> 413 / RESOURCE_EXHAUSTED)', async () => {
+  const seen = [];
+  const rx = await new OtlpReceiver({ httpPort: 0, grpcPort: 0, maxBodyBytes: 1 << 20,
+    onTraces: (b) => seen.push(b.length) }).start();
+  try {
+    const bomb = zlib.gzipSync(Buffer.alloc(64 << 20));  // 64 MiB of zeros in ~64 KiB
+    assert.ok(bomb.length < 1 << 20);
+    let r = await post(rx.httpPort, '/v1/traces', bomb,
+      { 'Content-Type': 'application/x-protobuf', 'Content-Encoding': 'gzip' });
+    assert.strictEqual(r.status, 413);
+    const frame = Buffer.concat([Buffer.from([1, 0, 0, 0, 0]), bomb]);
+    frame.writeUInt32BE(bomb.length, 1);
+    const g = await grpcCall(rx.grpcPort, TRACE_EXPORT_PATH, frame, { 'grpc-encoding': 'gzip' });
+    assert.strictEqual(g.trailers['grpc-status'], '8');
+    r = await post(rx.httpPort, '/v1/traces', Buffer.from('not gzip'),
+      { 'Content-Type': 'application/x-protobuf', 'Content-Encoding': 'gzip' });
+    assert.strictEqual(r.status, 400);
+    assert.deepStrictEqual(seen, []);
+  } finally {
+    await rx.close();
+  }
+});
+
 // ------------------------------------------------------------- collector config (YAML + OTTL)
 const cc = require(path.join(lib, 'collector_config'));
 const DEMO_LIKE_CONFIG = [
