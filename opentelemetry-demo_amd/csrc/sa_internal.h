@@ -76,14 +76,27 @@ struct IngestParams {
   // binned-table path (spanagg_binned.hip): key table split into kPartBins
   // bin-local sub-tables of 2^log2sb slots, keys stored as m = key * kmul,
   // u32 count rows; records in per-(bin, scatter workgroup) regions of
-  // bt_region records, region fills in bt_cnt [scatter workgroup][bin]
+  // bt_region records, region fills in bt_cnt [bin][scatter workgroup]
   uint32_t log2sb;
   uint32_t bt_region;
   uint64_t kmul, kinv;
   ulonglong2 *bt_rec;
   uint32_t *bt_cnt;
   uint32_t bt_grid;  // scatter workgroups (regions per bin)
+  // HLL lower bounds: hll_lb[j] <= every register of sub-block j (registers
+  // [j << lb_shift, (j + 1) << lb_shift)), so a span whose rho is at most its
+  // sub-block's bound cannot raise a register and skips the register read.
+  // lb_n sub-blocks (0: no filter); lb_seq rotates which sub-blocks a launch
+  // refreshes (registers only grow between window clears, which zero the
+  // window's bounds, so a bound read at any time stays a lower bound).
+  uint8_t *hll_lb;
+  uint32_t lb_shift, lb_n, lb_seq;
 };
+
+// HLL bound sub-blocks: 2^kLbMinShift registers or more, at most kLbMaxSub of
+// them per engine (the kernels keep the bounds in LDS)
+constexpr uint32_t kLbMinShift = 10;
+constexpr uint32_t kLbMaxSub = 2048;
 
 
 // Partitioned HBM-table path (high cardinality): part_scatter_kernel bins
@@ -145,17 +158,33 @@ __host__ __device__ inline uint32_t row_sum_cell(uint32_t b) { return b / kSegBu
 // The table of cap = 2^log2cap slots is split into kPartBins bins of
 // SB = 2^log2sb slots: a key lives in the bin given by the top kPartBinBits
 // bits of m = key * kmul (kmul odd, so the map is a bijection and 0 stays the
-// EMPTY marker), at its home slot within the bin or the next free one after
-// it (linear probing that wraps inside the bin).  One aggregate workgroup per
-// bin mirrors the whole sub-table in LDS at the same positions, so the bin's
-// keys and counter rows are read and written as one contiguous block.
+// EMPTY marker).  Within the bin the sub-table is buckets of 4 slots with two
+// choices, as the small table (probe_seq): positions 0-3 are bucket b1,
+// then bucket b2 and the buckets after it in order (wrapping inside the bin),
+// so a lookup is two 32-B bucket reads for nearly every key.  One aggregate
+// workgroup per bin mirrors the whole sub-table in LDS at the same positions,
+// so the bin's keys and counter rows are read and written as one contiguous
+// block.
 constexpr uint32_t kBinShift = 64 - kPartBinBits;          // bin = m >> kBinShift
 constexpr uint64_t kBinRest = (1ULL << kBinShift) - 1;     // m's bits below the bin
-__host__ __device__ inline uint32_t bt_home(uint64_t m, uint32_t log2sb) {
-  return (((uint32_t)m ^ (uint32_t)(m >> 29)) * 0x9E3779B1u) >> (32 - log2sb);
+struct BtSeq {
+  uint32_t b1, b2, nbmask;
+};
+__host__ __device__ inline BtSeq bt_seq(uint64_t m, uint32_t log2sb) {
+  const uint32_t h1 = ((uint32_t)m ^ (uint32_t)(m >> 29)) * 0x9E3779B1u;
+  const uint32_t h2 = (h1 ^ (h1 >> 16)) * 0x85EBCA6Bu;
+  const uint32_t sh = 34 - log2sb;  // top (log2sb - 2) bits
+  return BtSeq{h1 >> sh, h2 >> sh, (1u << (log2sb - 2)) - 1};
 }
+// in-bin slot of probe position i (i < bt_probe_max: every slot is reached)
+__host__ __device__ inline uint32_t bt_pos(const BtSeq &q, uint32_t i) {
+  if (i < 4) return q.b1 * 4 + i;
+  const uint32_t r = i - 4;
+  return ((q.b2 + (r >> 2)) & q.nbmask) * 4 + (r & 3);
+}
+__host__ __device__ inline uint32_t bt_probe_max(uint32_t log2sb) { return (1u << log2sb) + 4; }
 __host__ __device__ inline uint32_t bt_slot(uint64_t m, uint32_t log2sb, uint32_t i) {
-  return ((uint32_t)(m >> kBinShift) << log2sb) | ((bt_home(m, log2sb) + i) & ((1u << log2sb) - 1));
+  return ((uint32_t)(m >> kBinShift) << log2sb) | bt_pos(bt_seq(m, log2sb), i);
 }
 // u32 counter rows of the binned path: words [0, 2) = the u64 ns sum, words
 // [2, 2 + nbk) = bucket counts, padded to whole 16-B quads (80 B at 17 buckets)
@@ -164,11 +193,23 @@ constexpr uint32_t kBtStage = 4;     // records per bin stage: one 64-B chunk pe
 constexpr uint32_t kBtHot = 224;     // scatter overflow table entries
 constexpr uint32_t kBtHq = 256;      // scatter deferred HLL raises
 constexpr uint32_t kBtBlock = 1024;  // scatter workgroup
-constexpr uint32_t kBtAggBlock = 512;
+#ifndef SA_BT_AGG_BLOCK
+#define SA_BT_AGG_BLOCK 512
+#endif
+constexpr uint32_t kBtAggBlock = SA_BT_AGG_BLOCK;
 constexpr uint32_t kBtMaxWgSpans = 65520;  // u16 claim / overflow counters per scatter workgroup
 constexpr size_t kBtScatterLds = (size_t)kPartBins * (8 + kBtStage * 16) + (size_t)kBtHot * (16 + 4 * kPartWords) +
                                  (size_t)kBtHq * 8 + 16 + (size_t)kBins * sizeof(BinEntry);
 static_assert(kBtScatterLds <= 163840, "binned scatter LDS");
+// round-synchronous scatter (bt_scatter2_kernel): per bin a 4-record stage,
+// a u16 claim count (pairs) and a u16 region fill; per wave a flush list of
+// 128 bins; the overflow table; HLL queue; bin table; HLL bounds
+constexpr uint32_t kBt2Hot = 240;
+constexpr uint32_t kBt2HotErr = 128;  // (window slot, overflow entry) -> ERROR count
+constexpr size_t kBt2ScatterLds = (size_t)kPartBins * (kBtStage * 16 + 2 + 2) + (kBtBlock / 64) * 128 * 2 +
+                                  (size_t)kBt2Hot * (16 + 4 * kPartWords) + (size_t)kBtHq * 8 + 16 +
+                                  (size_t)kBins * sizeof(BinEntry) + kLbMaxSub + kBt2HotErr * 8;
+static_assert(kBt2ScatterLds <= 163840, "binned scatter2 LDS");
 
 // Geometry of the counter rows and key table for the flush-time kernels
 // (compact, gather, count-min fold): both table layouts, both row layouts.
@@ -256,6 +297,7 @@ hipError_t launch_fold_errcnt(const unsigned long long *gkeys, unsigned long lon
 // binned-table path (spanagg_binned.hip)
 hipError_t prepare_ingest_bt(size_t agg_lds);
 size_t bt_agg_lds_bytes(uint32_t log2sb, uint32_t grid);
+size_t bt_agg2_lds_bytes(uint32_t log2sb, uint32_t grid);  // (the larger of the two is agg_lds)
 hipError_t launch_ingest_bt(const IngestParams &P, size_t agg_lds, hipStream_t s);
 hipError_t launch_fold_rows32(unsigned long long *gcounts, unsigned long long *base64, uint64_t cap,
                               uint32_t nbk, hipStream_t s);

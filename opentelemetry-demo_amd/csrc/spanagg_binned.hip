@@ -39,9 +39,10 @@ __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory")
 // bin is full.  Plain probe reads, as g_find_insert (a stale 0 is corrected
 // by the CAS).
 __device__ __forceinline__ uint32_t bt_find_insert(unsigned long long *keys, uint64_t m, uint32_t log2sb) {
-  const uint32_t sb = 1u << log2sb;
-  for (uint32_t i = 0; i < sb; ++i) {
-    const uint32_t s = bt_slot(m, log2sb, i);
+  const BtSeq q = bt_seq(m, log2sb);
+  const uint32_t base = (uint32_t)(m >> kBinShift) << log2sb;
+  for (uint32_t i = 0; i < bt_probe_max(log2sb); ++i) {
+    const uint32_t s = base | bt_pos(q, i);
     unsigned long long k = keys[s];
     if (k == m) return s;
     if (k == 0) {
@@ -309,7 +310,7 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter_kernel(IngestParams P) {
         for (uint32_t q = 0; q < c; ++q) hot_rec(b, stage[b * kBtStage + q]);
       }
     }
-    P.bt_cnt[(uint64_t)blockIdx.x * kPartBins + b] = fill;
+    P.bt_cnt[(uint64_t)b * P.bt_grid + blockIdx.x] = fill;
   }
   __syncthreads();
   // the overflow table: one row update per entry (atomics: entries of one
@@ -340,6 +341,358 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter_kernel(IngestParams P) {
   }
 }
 
+// Diagnostic per-workgroup timestamps (SPANAGG_STAMPS builds of the engine):
+// s_memrealtime (100 MHz, comparable across CUs) into dbg[base + k].
+__device__ __forceinline__ void bt_stamp(const IngestParams &P, uint64_t base, uint32_t k) {
+  if (P.dbg && threadIdx.x == 0) P.dbg[base + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ uint32_t min_bytes(uint4 v) {
+  uint32_t m = 0xFFu;
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int s = 0; s < 32; s += 8) m = min(m, (w[i] >> s) & 0xFFu);
+  return m;
+}
+
+// One wave recomputes the lower bound of one HLL sub-block per launch
+// (rotating over launches when there are more sub-blocks than waves).
+__device__ __forceinline__ void hll_lb_refresh(const IngestParams &P, uint32_t wave, uint32_t waves) {
+  if (!P.lb_n) return;
+  const uint32_t total = min(P.lb_n, gridDim.x * waves), gi = blockIdx.x * waves + wave;
+  if (gi >= total) return;
+  const uint32_t sb = (uint32_t)(((uint64_t)P.lb_seq * total + gi) % P.lb_n);
+  const uint32_t lane = threadIdx.x & 63u, quads = (1u << P.lb_shift) / 16;
+  const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
+  uint32_t mn = 0xFFu;
+  for (uint32_t o = lane; o < quads; o += 64) mn = min(mn, min_bytes(src[o]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+  if (lane == 0) P.hll_lb[sb] = (uint8_t)mn;
+}
+
+// Round-synchronous scatter.  The workgroup takes its span range in rounds of
+// 2,048 spans (one 128-span tile per wave, two rounds of tiles in flight);
+// every span claims a slot of its bin's 4-record LDS stage with one LDS
+// atomic.  After a barrier each wave collects the full stages of the 128 bins
+// it owns into a list and writes them out four lanes per stage, so every
+// stage leaves as one aligned 64-B piece of a single store instruction; a
+// second barrier frees the stages for the next round.  Keys already in the
+// overflow table (the hot keys of a skewed mix) are added there directly;
+// a span whose stage is full in its round, or whose region is used up, goes
+// to the overflow table, past that the direct path.  The record layout
+// ({m's low 53 bits | ERROR flag | window slot, duration} per (bin,
+// workgroup) region) is the one bt_aggregate_kernel reads.
+// MODE (ablation): 1 = no records, 2 = no HLL, 4 = overflow-table adds
+// skipped, 8 = overflow-table ERROR counts skipped.
+template <int MODE = 0>
+__global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr uint32_t kWaves = kBtBlock / 64;
+  ulonglong2 *stage = reinterpret_cast<ulonglong2 *>(smem);                          // [bins][4]
+  uint32_t *fillw = reinterpret_cast<uint32_t *>(stage + kPartBins * kBtStage);      // [bins / 2] u16 pairs
+  uint32_t *rcnw = fillw + kPartBins / 2;                                            // [bins / 2] region fills
+  uint16_t *flist = reinterpret_cast<uint16_t *>(rcnw + kPartBins / 2);              // [waves][128]
+  unsigned long long *hkey = reinterpret_cast<unsigned long long *>(flist + kWaves * 128);
+  unsigned long long *hsum = hkey + kBt2Hot;
+  uint32_t *hcnt = reinterpret_cast<uint32_t *>(hsum + kBt2Hot);  // [kBt2Hot][kPartWords] u16 pairs
+  uint2 *hq = reinterpret_cast<uint2 *>(hcnt + kBt2Hot * kPartWords);
+  uint32_t *hq_n = reinterpret_cast<uint32_t *>(hq + kBtHq);
+  BinEntry *lbins = reinterpret_cast<BinEntry *>(hq_n + 4);
+  uint2 *herr = reinterpret_cast<uint2 *>(lbins + kBins);  // [kBt2HotErr] {(ws << 8 | entry) + 1, count}
+  uint8_t *llb = reinterpret_cast<uint8_t *>(herr + kBt2HotErr);
+  const KParams kp = kernel_params();
+  const uint64_t sbase = (uint64_t)kPartBins * 8 + blockIdx.x * 8;
+  bt_stamp(P, sbase, 0);
+
+  uint64_t lo, hi;
+  wg_range_p(P, lo, hi);
+  const uint32_t len = (uint32_t)(hi - lo);
+  constexpr uint32_t kRound = kBtBlock * 2;
+  const uint32_t lane = threadIdx.x & 63u, lane_off = lane * 2;
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t rounds = (len + kRound - 1) / kRound;
+  auto tstart = [&](uint32_t r) -> uint32_t { return r * kRound + wave * 128; };
+  auto tremain = [&](uint32_t t) -> uint32_t { return len > t ? len - t : 0u; };
+
+  // prologue: bin table and bounds, the first two rounds' tiles, LDS setup
+  uint4 bv = make_uint4(0, 0, 0, 0);
+  if (threadIdx.x < kBins * 2) bv = reinterpret_cast<const uint4 *>(P.bintab)[threadIdx.x];
+  const uint32_t lb_on = P.lb_n != 0 && !(MODE & 2);
+  uint32_t lbw = 0;
+  if (lb_on && threadIdx.x * 4 < P.lb_n) lbw = *reinterpret_cast<const uint32_t *>(P.hll_lb + threadIdx.x * 4);
+  SpanTile<2> buf[2];
+  Pending<2> pend, pend2;  // HLL reads of the last two rounds (compared two rounds later:
+                           // the flush stores between a read and its compare would
+                           // otherwise make that wait drain the prefetched tiles too)
+  load_tile_at<2, 2>(P, lo + tstart(0), tremain(tstart(0)), lane_off, buf[0]);
+  load_tile_at<2, 2>(P, lo + tstart(1), tremain(tstart(1)), lane_off, buf[1]);
+  {
+    uint32_t z;  // a VGPR zero keeps these vector loads
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) pend.hv[j] = pend2.hv[j] = *reinterpret_cast<const uint32_t *>(P.hll + z);
+  }
+  for (uint32_t b = threadIdx.x; b < kPartBins / 2; b += kBtBlock) fillw[b] = rcnw[b] = 0;
+  for (uint32_t h = threadIdx.x; h < kBt2Hot; h += kBtBlock) hkey[h] = hsum[h] = 0;
+  for (uint32_t h = threadIdx.x; h < kBt2Hot * kPartWords; h += kBtBlock) hcnt[h] = 0;
+  if (threadIdx.x < kBt2HotErr) herr[threadIdx.x] = make_uint2(0, 0);
+  if (threadIdx.x < kBins * 2) reinterpret_cast<uint4 *>(lbins)[threadIdx.x] = bv;
+  if (lb_on && threadIdx.x * 4 < P.lb_n) reinterpret_cast<uint32_t *>(llb)[threadIdx.x] = lbw;
+  if (threadIdx.x == 0) hq_n[0] = 0;
+  __syncthreads();
+  bt_stamp(P, sbase, 1);
+
+  uint32_t n_zero = 0, n_badsvc = 0, n_oor = 0;  // wave-uniform (SGPR)
+  uint32_t n_drop = 0;                           // per lane
+#pragma unroll
+  for (int j = 0; j < 2; ++j) pend.hoff[j] = pend.rho[j] = pend2.hoff[j] = pend2.rho[j] = 0;
+  const uint32_t region = P.bt_region;
+  ulonglong2 *my_rec = P.bt_rec + (uint64_t)blockIdx.x * region;  // + bin * grid * region
+  const uint64_t bin_stride = (uint64_t)P.bt_grid * region;
+
+  // overflow-table home: an even entry, probed as a pair first
+  auto hot_home = [&](uint64_t m) -> uint32_t {
+    return (uint32_t)(((uint64_t)(uint32_t)(m >> 21) * (kBt2Hot / 2)) >> 32) * 2;
+  };
+  auto hot_acc = [&](uint32_t h, uint64_t m, uint64_t d, bool err, uint32_t ws) {
+    if (MODE & 4) return;
+    const uint32_t bk = bucket_lds<1>(d, lbins, P);
+    atomicAdd(&hcnt[h * kPartWords + (bk >> 1)], 1u << ((bk & 1u) * 16));
+    atomicAdd(&hsum[h], (unsigned long long)d);
+    if (err && !(MODE & 8)) {  // ERROR count per (window slot, entry); a full table takes the key-table path
+      const uint32_t ek = ((ws << 8) | h) + 1;
+      uint32_t e = (ek * 0x9E3779B1u) >> 25;  // kBt2HotErr = 128
+      for (int pr = 0; pr < 4; ++pr, e = (e + 1) & (kBt2HotErr - 1)) {
+        uint32_t k = herr[e].x;
+        if (k == 0) k = atomicCAS(&herr[e].x, 0u, ek);
+        if (k == 0 || k == ek) {
+          atomicAdd(&herr[e].y, 1u);
+          return;
+        }
+      }
+      bt_cold_err(kp, m, ws);
+    }
+  };
+  // a span the stages cannot take: the overflow table, else the direct path
+  auto hot_add = [&](uint64_t m, uint64_t d, bool err, uint32_t ws) {
+    uint32_t h = hot_home(m);
+    for (int pr = 0; pr < 8; ++pr) {
+      unsigned long long k = hkey[h];
+      if (k == 0) k = atomicCAS(&hkey[h], 0ULL, (unsigned long long)m);
+      if (k == 0 || k == m) {
+        hot_acc(h, m, d, err, ws);
+        return;
+      }
+      h = h + 1 == kBt2Hot ? 0u : h + 1;
+    }
+    const uint32_t bk = bucket_lds<1>(d, lbins, P);
+    n_drop += bt_cold_direct(kp, m, d, bk, err, ws);
+  };
+  auto hot_rec = [&](uint32_t b, const ulonglong2 &r) {
+    const uint64_t m = ((uint64_t)b << kBinShift) | (r.x & kBinRest);
+    hot_add(m, r.y, (r.x >> 63) != 0, (uint32_t)(r.x >> kBinShift) & 1023u);
+  };
+  // claims n record positions of bin b's region (u16 pairs); positions at or
+  // past the region's end take the overflow table instead
+  auto claim = [&](uint32_t b, uint32_t n) -> uint32_t {
+    const uint32_t sh = (b & 1u) * 16;
+    return (atomicAdd(&rcnw[b >> 1], n << sh) >> sh) & 0xFFFFu;
+  };
+  auto place = [&](uint64_t m, uint64_t d, bool err, uint32_t ws) {
+    const uint32_t h0 = hot_home(m);
+    const ulonglong2 hk = *reinterpret_cast<const ulonglong2 *>(hkey + h0);
+    if (hk.x == m || hk.y == m) {
+      hot_acc(h0 + (hk.x == m ? 0u : 1u), m, d, err, ws);
+      return;
+    }
+    const uint32_t b = (uint32_t)(m >> kBinShift), sh = (b & 1u) * 16;
+    const uint32_t c = (atomicAdd(&fillw[b >> 1], 1u << sh) >> sh) & 0xFFFFu;
+    const ulonglong2 rec =
+        make_ulonglong2((m & kBinRest) | (err ? (1ULL << 63) | ((uint64_t)ws << kBinShift) : 0ULL), d);
+    if (c < kBtStage) {
+      stage[b * kBtStage + c] = rec;
+      return;
+    }
+    // the stage is full this round.  A key that holds two or more of its
+    // slots is frequent (a hot key of a skewed mix): it moves to the overflow
+    // table; any other record is stored on its own.  (The slots may hold this
+    // round's records or, not yet overwritten, an earlier round's: either way
+    // records of this bin, which is all the test needs.)
+    uint32_t same = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kBtStage; ++q) same += ((stage[b * kBtStage + q].x ^ rec.x) & kBinRest) == 0 ? 1u : 0u;
+    if (same >= 2) {
+      hot_add(m, d, err, ws);
+      return;
+    }
+    const uint32_t at = claim(b, 1);
+    if (at < region) my_rec[b * bin_stride + at] = rec;
+    else hot_add(m, d, err, ws);
+  };
+  auto hll_settle = [&](const Pending<2> &q) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (((q.hv[j] >> ((q.hoff[j] & 3u) * 8)) & 0xFFu) < q.rho[j]) {
+        const uint32_t slot = atomicAdd(&hq_n[0], 1u);
+        if (slot < kBtHq) hq[slot] = make_uint2(q.hoff[j], q.rho[j]);
+        else hll_raise(kp->hll + q.hoff[j], q.rho[j]);
+      }
+    }
+  };
+
+  const uint32_t hp = P.p, lbs = P.lb_shift;
+  auto step = [&](SpanTile<2> &T, uint32_t toff, uint32_t pf) {
+    uint64_t m[2], d[2];
+    uint32_t ws[2], hoff[2], rho[2];
+    bool err[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool valid = lane_off + toff + (uint32_t)j < len;
+      const uint64_t key = copy_u64(T.key[j]);  // 0 past the range
+      n_zero += wave_count(valid && key == 0);
+      d[j] = T.e[j] > T.s[j] ? T.e[j] - T.s[j] : 0;
+      const uint32_t meta = copy_u32(T.meta[j]);
+      const uint32_t svc = meta & 0xFFFFu;
+      const bool svc_ok = svc < P.n_services;
+      ws[j] = window_slot(P, T.e[j]);
+      const bool win_ok = ws[j] != 0xFFFFFFFFu;
+      n_badsvc += wave_count(valid && !svc_ok);
+      n_oor += wave_count(valid && svc_ok && !win_ok);
+      const bool sk = valid && svc_ok && win_ok;
+      err[j] = sk && ((meta >> 19) & 3u) == 2u;
+      const uint64_t x = xxh64_16(T.a[j], T.b[j]);
+      const uint32_t r = (uint32_t)__clzll((long long)((x << hp) | (1ULL << (hp - 1)))) + 1;
+      const uint32_t ho = sk ? ((ws[j] * P.n_services + svc) << hp) + (uint32_t)(x >> (64 - hp)) : 0u;
+      bool up = sk && !(MODE & 2);
+      if (lb_on) up = up && r > llb[ho >> lbs];
+      rho[j] = up ? r : 0u;
+      hoff[j] = up ? ho : 0u;
+      m[j] = key * P.kmul;
+    }
+    uint32_t hv[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      hv[j] = (MODE & 2) ? 0xFFFFFFFFu : *reinterpret_cast<const uint32_t *>(P.hll + (hoff[j] & ~3u));
+    __builtin_amdgcn_sched_barrier(0);
+    load_tile_at<2, 2>(P, lo + pf, tremain(pf), lane_off, T);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (MODE & 1) n_drop += (uint32_t)((m[j] ^ d[j]) == 0x123456789ABCULL);  // keep the values live
+      else if (m[j] != 0) place(m[j], d[j], err[j], ws[j]);
+    }
+    hll_settle(pend2);
+    pend2 = pend;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      pend.hoff[j] = hoff[j];
+      pend.rho[j] = rho[j];
+      pend.hv[j] = hv[j];
+    }
+  };
+  // the waves write out the full stages of their 128 bins (4 lanes a stage)
+  uint16_t *wl = flist + wave * 128;
+  auto flush = [&]() {
+    const uint32_t fw = fillw[threadIdx.x];  // bins 2t, 2t + 1
+    const bool f0 = (fw & 0xFFFFu) >= kBtStage, f1 = (fw >> 16) >= kBtStage;
+    if (f0 || f1) fillw[threadIdx.x] = (f0 ? 0u : (fw & 0xFFFFu)) | (f1 ? 0u : (fw & 0xFFFF0000u));
+    const uint64_t m0 = __ballot(f0), m1 = __ballot(f1);
+    const uint32_t n0 = (uint32_t)__popcll(m0), nf = n0 + (uint32_t)__popcll(m1);
+    if (f0) wl[lane_rank(m0)] = (uint16_t)(2 * threadIdx.x);
+    if (f1) wl[n0 + lane_rank(m1)] = (uint16_t)(2 * threadIdx.x + 1);
+    compiler_fence();  // one wave's LDS operations complete in order
+    for (uint32_t i0 = 0; i0 < nf; i0 += 16) {  // wave-uniform
+      const uint32_t i = i0 + (lane >> 2), q = lane & 3u;
+      const bool act = i < nf;
+      const uint32_t b = act ? wl[i] : 0u;
+      const ulonglong2 r = stage[b * kBtStage + q];
+      uint32_t at = act && q == 0 ? claim(b, kBtStage) : 0u;
+      at = (uint32_t)__shfl((int)at, (int)(lane & ~3u), 64);
+      if (act) {
+        if (MODE & 16) my_rec[(uint64_t)threadIdx.x * 64 + ((i0 + at) & 63)] = r;  // ablation: no scatter
+        else if (MODE & 32) (void)0;                                          // ablation: no store
+        else if (at + q < region) my_rec[b * bin_stride + at + q] = r;
+        else hot_rec(b, r);
+      }
+    }
+  };
+
+  for (uint32_t r = 0; r < rounds; r += 2) {
+    step(buf[0], tstart(r), tstart(r + 2));
+    __syncthreads();
+    if (!(MODE & 1)) flush();
+    __syncthreads();
+    if (r + 1 < rounds) {
+      step(buf[1], tstart(r + 1), tstart(r + 3));
+      __syncthreads();
+      if (!(MODE & 1)) flush();
+      __syncthreads();
+    }
+  }
+  hll_settle(pend2);
+  hll_settle(pend);
+  bt_stamp(P, sbase, 2);
+  // partial stages, then this workgroup's region fills
+  for (uint32_t b = threadIdx.x; b < kPartBins; b += kBtBlock) {
+    const uint32_t c = (fillw[b >> 1] >> ((b & 1u) * 16)) & 0xFFFFu;  // < kBtStage after the last flush
+    const uint32_t at = c ? claim(b, c) : 0u;
+    for (uint32_t q = 0; q < c; ++q) {
+      if (at + q < region) my_rec[b * bin_stride + at + q] = stage[b * kBtStage + q];
+      else hot_rec(b, stage[b * kBtStage + q]);
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < kPartBins; b += kBtBlock)
+    P.bt_cnt[(uint64_t)b * P.bt_grid + blockIdx.x] = min((rcnw[b >> 1] >> ((b & 1u) * 16)) & 0xFFFFu, region);
+  __syncthreads();
+  // the overflow table: one row update per entry (atomics: entries of one
+  // key may come from several workgroups)
+  const uint32_t stride32 = row32_stride(P.nbk);
+  for (uint32_t h = threadIdx.x; h < kBt2Hot; h += kBtBlock) {
+    const unsigned long long m = hkey[h];
+    if (m == 0) continue;
+    const uint32_t s = bt_find_insert(P.gkeys, m, P.log2sb);
+    if (s == kNotFound) {
+      for (uint32_t b = 0; b < P.nbk; ++b) n_drop += (hcnt[h * kPartWords + (b >> 1)] >> ((b & 1u) * 16)) & 0xFFFFu;
+      continue;
+    }
+    for (uint32_t b = 0; b < P.nbk; ++b) {
+      const uint32_t c = (hcnt[h * kPartWords + (b >> 1)] >> ((b & 1u) * 16)) & 0xFFFFu;
+      if (c) row32_add(P.gcounts, stride32, s, b, c, 0);
+    }
+    row32_add(P.gcounts, stride32, s, 0, 0, hsum[h]);
+  }
+  if (threadIdx.x < kBt2HotErr) {
+    const uint2 e = herr[threadIdx.x];
+    if (e.x) {
+      const uint32_t ws = (e.x - 1) >> 8, h = (e.x - 1) & 0xFFu;
+      const uint64_t m = hkey[h];
+      const uint32_t s = bt_find_insert(P.gkeys, m, P.log2sb);
+      if (s != kNotFound) atomicAdd(P.errcnt + ((uint64_t)ws << P.log2cap) + s, (unsigned long long)e.y);
+      else
+        for (uint32_t i = 0; i < e.y; ++i) bt_cms_add(kp, ws, m * P.kinv);
+    }
+  }
+  const uint32_t nq = min(hq_n[0], kBtHq);
+  for (uint32_t i = threadIdx.x; i < nq; i += kBtBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
+  n_drop = wave_sum(n_drop);
+  if (lane == 0) {
+    if (n_zero) atomicAdd(&P.stats[kStatZeroKey], (unsigned long long)n_zero);
+    if (n_badsvc) atomicAdd(&P.stats[kStatInvalidService], (unsigned long long)n_badsvc);
+    if (n_oor) atomicAdd(&P.stats[kStatWindowOOR], (unsigned long long)n_oor);
+    if (n_drop) atomicAdd(&P.stats[kStatDropped], (unsigned long long)n_drop);
+  }
+  hll_lb_refresh(P, wave, kWaves);
+  bt_stamp(P, sbase, 3);
+}
+
 // LDS layout of bt_aggregate_kernel (bytes): keys [sb] u64 | sums [sb] u64 |
 // counts [sb][kPartWords] u32 | region prefix [grid + 1] u32 (16-B padded) |
 // ERROR table [kBtErr] uint2 | bin table [kBins] | misc [4] u32
@@ -367,14 +720,14 @@ __global__ __launch_bounds__(kBtAggBlock) void bt_aggregate_kernel(IngestParams 
 
   // 1. the bin's key slots (kept in registers to find the new ones later),
   //    region fills, zeroed counters
-  constexpr int kMaxPer = 4;  // sb <= 2048 slots at 512 threads
+  constexpr int kMaxPer = 2048 / kBtAggBlock;  // sb <= 2048 slots
   unsigned long long orig[kMaxPer];
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
     const uint32_t s = tid + u * kBtAggBlock;
     orig[u] = s < sb ? gk[s] : 0ULL;
   }
-  for (uint32_t g = tid; g < G; g += kBtAggBlock) pre[g] = P.bt_cnt[(uint64_t)g * kPartBins + bin];
+  for (uint32_t g = tid; g < G; g += kBtAggBlock) pre[g] = P.bt_cnt[(uint64_t)bin * G + g];
   if (tid < kBins * 2) reinterpret_cast<uint4 *>(lbins)[tid] = reinterpret_cast<const uint4 *>(P.bintab)[tid];
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
@@ -448,13 +801,16 @@ __global__ __launch_bounds__(kBtAggBlock) void bt_aggregate_kernel(IngestParams 
       const uint64_t m = ((uint64_t)bin << kBinShift) | (v[u].x & kBinRest);
       const uint64_t d = v[u].y;
       const uint32_t bk = bucket_lds<1>(d, lbins, P);
-      uint32_t s = bt_home(m, log2sb), i = 0;
-      for (; i < sb; ++i, s = (s + 1) & smask) {
+      const BtSeq bq = bt_seq(m, log2sb);
+      const uint32_t pmax = bt_probe_max(log2sb);
+      uint32_t s = 0, i = 0;
+      for (; i < pmax; ++i) {
+        s = bt_pos(bq, i);
         unsigned long long k = lkeys[s];
         if (k == 0) k = atomicCAS(&lkeys[s], 0ULL, (unsigned long long)m);
         if (k == 0 || k == m) break;
       }
-      if (i == sb) {  // the bin's sub-table is full: the span is dropped
+      if (i == pmax) {  // the bin's sub-table is full: the span is dropped
         ++n_drop;
         if (v[u].x >> 63) bt_cms_add(kernel_params(), (uint32_t)(v[u].x >> kBinShift) & 1023u, m * P.kinv);
         continue;
@@ -531,6 +887,218 @@ __global__ __launch_bounds__(kBtAggBlock) void bt_aggregate_kernel(IngestParams 
   if (tid == 0 && misc[0]) atomicAdd(&P.stats[kStatDropped], (unsigned long long)misc[0]);
 }
 
+
+// Aggregate, second form (the default).  One 512-thread workgroup per bin;
+// its LDS holds the bin's key slots (mirror), u64 ns sums and u16 bucket
+// counts (17 per slot, packed), an ERROR table and the region fills: 53 KiB
+// at 1,024 slots, so three workgroups share a CU.  No prefix scan: each
+// wave-instruction reads two regions (lanes 0-31 and 32-63, one record per
+// lane), a wave takes every eighth region pair and issues its loads in
+// batches of eight before it aggregates them.  Then each touched slot's u32
+// row is read, added to and written back (all reads first).
+constexpr uint32_t kBtAgg2Block = 512;
+constexpr uint32_t kBtAgg2Err = 128;
+__host__ __device__ inline uint32_t bt_agg2_cnt_words(uint32_t sb) { return (sb * kPartMaxBk + 1) / 2; }
+__host__ __device__ inline uint32_t bt_agg2_off_err(uint32_t sb) { return (sb * 16 + bt_agg2_cnt_words(sb) * 4 + 7) & ~7u; }
+__host__ __device__ inline uint32_t bt_agg2_off_reg(uint32_t sb) { return bt_agg2_off_err(sb) + kBtAgg2Err * 8; }
+
+// MODE (ablation): 1 = no records aggregated, 2 = no key / row write-back;
+// MAXPER = key slots per thread (sb <= MAXPER * 512)
+template <int MODE = 0, int MAXPER = 2>
+__global__ __launch_bounds__(kBtAgg2Block) void bt_aggregate2_kernel(IngestParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t log2sb = P.log2sb, sb = 1u << log2sb, smask = sb - 1;
+  const uint32_t G = P.bt_grid, bin = blockIdx.x, region = P.bt_region;
+  unsigned long long *lkeys = reinterpret_cast<unsigned long long *>(smem);
+  unsigned long long *lsum = lkeys + sb;
+  uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + sb);  // u16 [sb][17], packed
+  uint2 *etab = reinterpret_cast<uint2 *>(smem + bt_agg2_off_err(sb));
+  uint32_t *rcnt = reinterpret_cast<uint32_t *>(smem + bt_agg2_off_reg(sb));  // [G] region fills
+  uint32_t *misc = rcnt + G;  // [0] dropped
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  unsigned long long *gk = P.gkeys + ((uint64_t)bin << log2sb);
+  bt_stamp(P, (uint64_t)bin * 8, 0);
+
+  // 1. the bin's key slots (kept in registers to find the new ones later),
+  //    region fills, zeroed counters
+  constexpr int kMaxPer = MAXPER;
+  unsigned long long orig[kMaxPer];
+#pragma unroll
+  for (int u = 0; u < kMaxPer; ++u) {
+    const uint32_t s = tid + u * kBtAgg2Block;
+    orig[u] = s < sb ? gk[s] : 0ULL;
+  }
+  for (uint32_t g = tid; g < G; g += kBtAgg2Block) rcnt[g] = P.bt_cnt[(uint64_t)bin * G + g];
+#pragma unroll
+  for (int u = 0; u < kMaxPer; ++u) {
+    const uint32_t s = tid + u * kBtAgg2Block;
+    if (s < sb) {
+      lkeys[s] = orig[u];
+      lsum[s] = 0;
+    }
+  }
+  const uint32_t cw = bt_agg2_cnt_words(sb);
+  for (uint32_t i = tid; i < cw; i += kBtAgg2Block) lcnt[i] = 0;
+  for (uint32_t i = tid; i < kBtAgg2Err; i += kBtAgg2Block) etab[i] = make_uint2(0, 0);
+  if (tid == 0) misc[0] = 0;
+  __syncthreads();
+  bt_stamp(P, (uint64_t)bin * 8, 1);
+
+  // 2. the records (the thresholds live in SGPRs: a runtime-bounded loop over
+  //    P.thr would re-load them from the kernarg segment for every record)
+  const ulonglong2 *bin_rec = P.bt_rec + (uint64_t)bin * G * region;
+  const __amdgpu_buffer_rsrc_t rrec = rsrc(bin_rec, G * region * 16);
+  const uint32_t half = lane >> 5, r0 = lane & 31u;
+  uint64_t thr[kPartMaxBk - 1];
+#pragma unroll
+  for (uint32_t i = 0; i < kPartMaxBk - 1; ++i) thr[i] = i < P.npos ? P.thr[i] : ~0ULL;
+  const uint32_t nneg = P.nneg;
+  uint32_t n_drop = 0;
+  auto agg = [&](const ulonglong2 &v) {
+    const uint64_t m = ((uint64_t)bin << kBinShift) | (v.x & kBinRest);
+    const uint64_t d = v.y;
+    uint32_t bk = nneg;
+#pragma unroll
+    for (uint32_t i = 0; i < kPartMaxBk - 1; ++i) bk += d > thr[i] ? 1u : 0u;
+    // the key's two buckets (four independent 16-B reads), else the probe
+    // sequence (a new key, or one placed past its two buckets)
+    const BtSeq bq = bt_seq(m, log2sb);
+    const ulonglong2 *lk2 = reinterpret_cast<const ulonglong2 *>(lkeys);
+    const ulonglong2 a0 = lk2[bq.b1 * 2], a1 = lk2[bq.b1 * 2 + 1], c0 = lk2[bq.b2 * 2], c1 = lk2[bq.b2 * 2 + 1];
+    uint32_t s = a0.x == m ? bq.b1 * 4 : a0.y == m ? bq.b1 * 4 + 1 : a1.x == m ? bq.b1 * 4 + 2
+               : a1.y == m ? bq.b1 * 4 + 3 : c0.x == m ? bq.b2 * 4 : c0.y == m ? bq.b2 * 4 + 1
+               : c1.x == m ? bq.b2 * 4 + 2 : c1.y == m ? bq.b2 * 4 + 3 : kNotFound;
+    const uint32_t pmax = bt_probe_max(log2sb);
+    uint32_t i = 0;
+    if (s == kNotFound) {
+      for (; i < pmax; ++i) {
+        s = bt_pos(bq, i);
+        unsigned long long k = lkeys[s];
+        if (k == 0) k = atomicCAS(&lkeys[s], 0ULL, (unsigned long long)m);
+        if (k == 0 || k == m) break;
+      }
+    }
+    const bool err = (v.x >> 63) != 0;
+    const uint32_t ws = (uint32_t)(v.x >> kBinShift) & 1023u;
+    if (i == pmax) {  // the bin's sub-table is full: the span is dropped
+      ++n_drop;
+      if (err) bt_cms_add(kernel_params(), ws, m * P.kinv);
+      return;
+    }
+    const uint32_t h = s * kPartMaxBk + bk;
+    atomicAdd(&lcnt[h >> 1], 1u << ((h & 1u) * 16));
+    atomicAdd(&lsum[s], (unsigned long long)d);
+    if (err) {  // (window slot, key slot) -> count
+      const uint32_t ek = ((ws << log2sb) | s) + 1;
+      uint32_t e = (ek * 0x9E3779B1u) >> 25;  // kBtAgg2Err = 128
+      for (int pr = 0; pr < 8; ++pr, e = (e + 1) & (kBtAgg2Err - 1)) {
+        uint32_t kk = etab[e].x;
+        if (kk == 0) kk = atomicCAS(&etab[e].x, 0u, ek);
+        if (kk == 0 || kk == ek) {
+          atomicAdd(&etab[e].y, 1u);
+          return;
+        }
+      }
+      atomicAdd(P.errcnt + ((uint64_t)ws << P.log2cap) + ((uint64_t)bin << log2sb) + s, 1ULL);
+    }
+  };
+  if (!(MODE & 1)) {
+    constexpr uint32_t kWaves = kBtAgg2Block / 64, B = 8;
+    const uint32_t pairs = (G + 1) / 2;
+    for (uint32_t p0 = wave; p0 < pairs; p0 += kWaves * B) {
+      ulonglong2 v[B];
+      uint32_t cnt[B];
+#pragma unroll
+      for (uint32_t b = 0; b < B; ++b) {  // unconditional buffer loads (0 past the end)
+        const uint32_t p = p0 + b * kWaves, g = 2 * p + half;
+        cnt[b] = p < pairs && g < G ? rcnt[g] : 0u;
+        const uint32_t off = r0 < cnt[b] ? (g * region + r0) * 16 : 0xFFFFFFF0u;
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)off, 0, 2);
+        v[b] = make_ulonglong2((uint64_t)x[0] | ((uint64_t)x[1] << 32), (uint64_t)x[2] | ((uint64_t)x[3] << 32));
+      }
+      if (MODE & 4) {  // ablation: records loaded, not aggregated
+#pragma unroll
+        for (uint32_t b = 0; b < B; ++b) n_drop += (r0 < cnt[b] && (v[b].x ^ v[b].y) == 0x12345ULL) ? 1u : 0u;
+        continue;
+      }
+#pragma unroll
+      for (uint32_t b = 0; b < B; ++b)
+        if (r0 < cnt[b]) agg(v[b]);
+      // regions longer than 32 records: the rest, one record per lane
+#pragma unroll 1
+      for (uint32_t b = 0; b < B; ++b) {
+        const uint32_t p = p0 + b * kWaves, g = 2 * p + half;
+        for (uint32_t r = 32 + r0; r < cnt[b]; r += 32) agg(bin_rec[(uint64_t)g * region + r]);
+      }
+    }
+  }
+  n_drop = wave_sum(n_drop);
+  if (lane == 0 && n_drop) atomicAdd(&misc[0], n_drop);
+  __syncthreads();
+  bt_stamp(P, (uint64_t)bin * 8, 2);
+
+  // 3. new keys and touched rows of the bin (one owner: plain stores; every
+  //    row read is issued before the first row is written)
+  if (MODE & 2) return;
+  const uint32_t nbk = P.nbk, stride32 = row32_stride(nbk), nq = stride32 / 4;
+  uint32_t *rows = reinterpret_cast<uint32_t *>(P.gcounts) + ((uint64_t)bin << log2sb) * stride32;
+  uint4 rv[kMaxPer][5];
+  bool touched[kMaxPer];
+#pragma unroll
+  for (int u = 0; u < kMaxPer; ++u) {
+    const uint32_t s = tid + u * kBtAgg2Block;
+    touched[u] = s < sb && lsum[s] != 0;
+    if (s < sb && !touched[u]) {  // a zero ns sum: look at the counts
+      uint32_t any = 0;
+      for (uint32_t b = 0; b < nbk; ++b) {
+        const uint32_t h = s * kPartMaxBk + b;
+        any |= (lcnt[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu;
+      }
+      touched[u] = any != 0;
+    }
+    const uint4 *row = reinterpret_cast<const uint4 *>(rows + (uint64_t)s * stride32);
+#pragma unroll
+    for (uint32_t q = 0; q < 5; ++q) rv[u][q] = touched[u] && q < nq ? row[q] : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int u = 0; u < kMaxPer; ++u) {
+    const uint32_t s = tid + u * kBtAgg2Block;
+    if (s >= sb) continue;
+    const unsigned long long k = lkeys[s];
+    if (k != orig[u]) gk[s] = k;
+    if (!touched[u]) continue;
+    uint32_t c[20];
+#pragma unroll
+    for (uint32_t q = 0; q < 5; ++q) {
+      c[4 * q] = rv[u][q].x;
+      c[4 * q + 1] = rv[u][q].y;
+      c[4 * q + 2] = rv[u][q].z;
+      c[4 * q + 3] = rv[u][q].w;
+    }
+    const unsigned long long sum = ((unsigned long long)c[1] << 32 | c[0]) + lsum[s];
+    c[0] = (uint32_t)sum;
+    c[1] = (uint32_t)(sum >> 32);
+#pragma unroll
+    for (uint32_t b = 0; b < kPartMaxBk; ++b) {
+      const uint32_t h = s * kPartMaxBk + b;
+      if (b < nbk) c[2 + b] += (lcnt[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu;
+    }
+    uint4 *row = reinterpret_cast<uint4 *>(rows + (uint64_t)s * stride32);
+#pragma unroll
+    for (uint32_t q = 0; q < 5; ++q)
+      if (q < nq) row[q] = make_uint4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
+  }
+  for (uint32_t i = tid; i < kBtAgg2Err; i += kBtAgg2Block) {
+    const uint2 e = etab[i];
+    if (e.x == 0) continue;
+    const uint32_t ek = e.x - 1, ws = ek >> log2sb, s = ek & smask;
+    unsigned long long *cell = P.errcnt + ((uint64_t)ws << P.log2cap) + ((uint64_t)bin << log2sb) + s;
+    *cell += e.y;
+  }
+  if (tid == 0 && misc[0]) atomicAdd(&P.stats[kStatDropped], (unsigned long long)misc[0]);
+  bt_stamp(P, (uint64_t)bin * 8, 3);
+}
+
 // u32 count rows -> the u64 fold array (before 2^32 spans can accumulate)
 __global__ void fold_rows32_kernel(uint32_t *rows, unsigned long long *base64, uint64_t cap, uint32_t nbk) {
   const uint32_t stride32 = row32_stride(nbk);
@@ -550,7 +1118,7 @@ __global__ void fold_rows32_kernel(uint32_t *rows, unsigned long long *base64, u
 
 // SA_DIAG bits of the ablation builds (profiling only)
 constexpr uint32_t kDiagBtDirect = 1u << 20, kDiagBtAggNoRows = 1u << 21, kDiagBtNoAgg = 1u << 22,
-                   kDiagBtNoScatter = 1u << 23;
+                   kDiagBtNoScatter = 1u << 23, kDiagBtScatter1 = 1u << 24;
 
 static const void *bt_scatter_fn(uint32_t diag) {
   const int mode = ((diag & 1u) ? 1 : 0) | ((diag & 2u) ? 2 : 0) | ((diag & kDiagBtDirect) ? 4 : 0);
@@ -565,8 +1133,39 @@ static const void *bt_scatter_fn(uint32_t diag) {
   }
 }
 
+constexpr uint32_t kDiagBtHotAcc = 1u << 25, kDiagBtHotErr = 1u << 26, kDiagBtSeqStore = 1u << 27,
+                   kDiagBtNoStore = 1u << 28;
+static const void *bt_scatter2_fn(uint32_t diag) {
+  if (diag & kDiagBtSeqStore) return (const void *)&bt_scatter2_kernel<16>;
+  if (diag & kDiagBtNoStore) return (const void *)&bt_scatter2_kernel<32>;
+  if (diag & kDiagBtHotAcc) return (const void *)&bt_scatter2_kernel<4>;
+  if (diag & kDiagBtHotErr) return (const void *)&bt_scatter2_kernel<8>;
+  switch (diag & 3u) {
+    case 1: return (const void *)&bt_scatter2_kernel<1>;
+    case 2: return (const void *)&bt_scatter2_kernel<2>;
+    case 3: return (const void *)&bt_scatter2_kernel<3>;
+    default: return (const void *)&bt_scatter2_kernel<0>;
+  }
+}
+
+constexpr uint32_t kDiagBtAgg1 = 1u << 29, kDiagBtAggWide = 1u << 30, kDiagBtAggLoadOnly = 1u << 31;
 static const void *bt_agg_fn(uint32_t diag) {
   const int mode = ((diag & 1u) ? 1 : 0) | ((diag & kDiagBtAggNoRows) ? 2 : 0);
+  if (!(diag & kDiagBtAgg1)) {
+    if (diag & kDiagBtAggLoadOnly) return (const void *)&bt_aggregate2_kernel<4, 2>;
+    if (diag & kDiagBtAggWide) switch (mode) {  // bins of 2,048 slots
+        case 1: return (const void *)&bt_aggregate2_kernel<1, 4>;
+        case 2: return (const void *)&bt_aggregate2_kernel<2, 4>;
+        case 3: return (const void *)&bt_aggregate2_kernel<3, 4>;
+        default: return (const void *)&bt_aggregate2_kernel<0, 4>;
+      }
+    switch (mode) {
+      case 1: return (const void *)&bt_aggregate2_kernel<1, 2>;
+      case 2: return (const void *)&bt_aggregate2_kernel<2, 2>;
+      case 3: return (const void *)&bt_aggregate2_kernel<3, 2>;
+      default: return (const void *)&bt_aggregate2_kernel<0, 2>;
+    }
+  }
   switch (mode) {
     case 1: return (const void *)&bt_aggregate_kernel<1>;
     case 2: return (const void *)&bt_aggregate_kernel<2>;
@@ -582,21 +1181,33 @@ hipError_t prepare_ingest_bt(size_t agg_lds) {
         e != hipSuccess)
       return e;
   }
-  for (uint32_t d : {0u, 1u, kDiagBtAggNoRows, 1u | kDiagBtAggNoRows})
-    if (hipError_t e = hipFuncSetAttribute(bt_agg_fn(d), hipFuncAttributeMaxDynamicSharedMemorySize, (int)agg_lds);
+  for (uint32_t d : {0u, 1u, 2u, 3u, kDiagBtHotAcc, kDiagBtHotErr, kDiagBtSeqStore, kDiagBtNoStore})
+    if (hipError_t e = hipFuncSetAttribute(bt_scatter2_fn(d), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)kBt2ScatterLds);
         e != hipSuccess)
       return e;
+  for (uint32_t d : {0u, 1u, kDiagBtAggNoRows, 1u | kDiagBtAggNoRows})
+    for (uint32_t v : {0u, kDiagBtAgg1, kDiagBtAggWide, kDiagBtAggLoadOnly})
+      if (hipError_t e =
+              hipFuncSetAttribute(bt_agg_fn(d | v), hipFuncAttributeMaxDynamicSharedMemorySize, (int)agg_lds);
+          e != hipSuccess)
+        return e;
   return hipSuccess;
 }
 
 hipError_t launch_ingest_bt(const IngestParams &P, size_t agg_lds, hipStream_t s) {
   void *args[] = {const_cast<IngestParams *>(&P)};
-  if (!(P.diag & kDiagBtNoScatter))
-    if (hipError_t e = hipLaunchKernel(bt_scatter_fn(P.diag), dim3(P.bt_grid), dim3(kBtBlock), args, kBtScatterLds, s);
+  if (!(P.diag & kDiagBtNoScatter)) {
+    const bool v1 = (P.diag & (kDiagBtScatter1 | kDiagBtDirect)) != 0;
+    if (hipError_t e = hipLaunchKernel(v1 ? bt_scatter_fn(P.diag) : bt_scatter2_fn(P.diag), dim3(P.bt_grid),
+                                       dim3(kBtBlock), args, v1 ? kBtScatterLds : kBt2ScatterLds, s);
         e != hipSuccess)
       return e;
+  }
   if (P.diag & kDiagBtNoAgg) return hipSuccess;
-  return hipLaunchKernel(bt_agg_fn(P.diag), dim3(kPartBins), dim3(kBtAggBlock), args, agg_lds, s);
+  const uint32_t diag = P.diag | (P.log2sb > 10 ? kDiagBtAggWide : 0u);
+  return hipLaunchKernel(bt_agg_fn(diag), dim3(kPartBins), dim3((P.diag & kDiagBtAgg1) ? kBtAggBlock : kBtAgg2Block),
+                         args, (P.diag & kDiagBtAgg1) ? agg_lds : bt_agg2_lds_bytes(P.log2sb, P.bt_grid), s);
 }
 
 hipError_t launch_fold_rows32(unsigned long long *gcounts, unsigned long long *base64, uint64_t cap,
@@ -604,6 +1215,10 @@ hipError_t launch_fold_rows32(unsigned long long *gcounts, unsigned long long *b
   hipLaunchKernelGGL(fold_rows32_kernel, dim3((uint32_t)std::min<uint64_t>((cap + 255) / 256, 4096)), dim3(256), 0,
                      s, reinterpret_cast<uint32_t *>(gcounts), base64, cap, nbk);
   return hipGetLastError();
+}
+
+size_t bt_agg2_lds_bytes(uint32_t log2sb, uint32_t grid) {
+  return bt_agg2_off_reg(1u << log2sb) + (size_t)grid * 4 + 16;
 }
 
 size_t bt_agg_lds_bytes(uint32_t log2sb, uint32_t grid) {

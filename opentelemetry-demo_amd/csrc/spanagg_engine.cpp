@@ -80,6 +80,11 @@ struct sa_engine {
   uint32_t *slab_cnt = nullptr;
   uint32_t *errslab = nullptr;  // v2: [G][n_windows << log2cap] per-workgroup ERROR counts
   uint8_t *hll = nullptr;
+  // HLL lower bounds per sub-block of 2^lb_shift registers (IngestParams::hll_lb)
+  uint8_t *hll_lb = nullptr;
+  uint32_t lb_shift = 0, lb_n = 0, lb_seq = 0;
+  bool bt_scatter1 = false;  // SPANAGG_BT_SCATTER=1: round-1 scatter kernel (A/B runs)
+  bool bt_agg1 = false;      // SPANAGG_BT_AGG=1: first aggregate kernel (A/B runs)
   // partitioned HBM-table path (lazily allocated on the first launch)
   bool part = false;
   ulonglong2 *part_rec = nullptr;
@@ -368,6 +373,19 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       (rc = alloc((void **)&e->d_seeds, sizeof kCmsSeed)) ||
       (rc = alloc((void **)&e->stats, 64)) || (rc = alloc((void **)&e->scratch, 64)))
     return bail(rc);
+  {
+    // bound sub-blocks: as small as kLbMinShift allows within kLbMaxSub of them
+    // (SPANAGG_HLL_LB=0 turns the filter off, for A/B runs)
+    const uint64_t regs = W * S << cfg->hll_p;
+    uint32_t sh = sa::kLbMinShift;
+    while (sh < cfg->hll_p && (regs >> sh) > sa::kLbMaxSub) ++sh;
+    const char *lv = std::getenv("SPANAGG_HLL_LB");
+    if ((regs >> sh) <= sa::kLbMaxSub && sh <= cfg->hll_p && !(lv && std::atoi(lv) == 0)) {
+      e->lb_shift = sh;
+      e->lb_n = (uint32_t)(regs >> sh);
+      if ((rc = alloc((void **)&e->hll_lb, ((size_t)e->lb_n + 15) & ~(size_t)15))) return bail(rc);
+    }
+  }
   if (std::getenv("SPANAGG_STAMPS") && (rc = alloc((void **)&e->dbg, (size_t)e->G * sa::kDbgPerWg * 8)))
     return bail(rc);
   {
@@ -383,7 +401,9 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     // workgroups sized for the bin's sub-table
     e->log2sb = e->log2cap - sa::kPartBinBits;
     e->bt_grid = e->cus;
-    e->agg_lds = sa::bt_agg_lds_bytes(e->log2sb, e->bt_grid);
+    if (const char *v = std::getenv("SPANAGG_BT_SCATTER")) e->bt_scatter1 = std::atoi(v) == 1;
+    if (const char *v = std::getenv("SPANAGG_BT_AGG")) e->bt_agg1 = std::atoi(v) == 1;
+    e->agg_lds = std::max(sa::bt_agg_lds_bytes(e->log2sb, e->bt_grid), sa::bt_agg2_lds_bytes(e->log2sb, e->bt_grid));
     if (hipError_t st = sa::prepare_ingest_bt(e->agg_lds); st != hipSuccess)
       return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
     // a random odd multiplier per engine: series ids -> stored ids (bins and
@@ -432,7 +452,7 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->stats, (void *)e->out_keys, (void *)e->out_rows, (void *)e->scratch,
                   (void *)e->slab_cnt, (void *)e->hll, (void *)e->errcnt, (void *)e->d_seeds,
                   (void *)e->dbg, (void *)e->d_bins, (void *)e->errslab, (void *)e->part_rec,
-                  (void *)e->part_fill, (void *)e->bt_rec, (void *)e->bt_cnt, (void *)e->base64,
+                  (void *)e->part_fill, (void *)e->bt_rec, (void *)e->bt_cnt, (void *)e->base64, (void *)e->hll_lb,
                   e->stage})
     if (p) (void)hipFree(p);
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
@@ -588,7 +608,13 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.seeds = e->d_seeds;
   P.stats = e->stats;
   P.diag = e->cfg.flags;
+  if (e->bt_scatter1) P.diag |= 1u << 24;
+  if (e->bt_agg1) P.diag |= 1u << 29;
   P.dbg = e->dbg;
+  P.hll_lb = e->hll_lb;
+  P.lb_shift = e->lb_shift;
+  P.lb_n = e->bt ? e->lb_n : 0;  // the kernels that read the bounds
+  P.lb_seq = e->lb_seq++;
   hipError_t st;
   if (e->small) {
     st = sa::launch_ingest_small(P, grid, e->lds_bytes, s, e->variant);
@@ -851,6 +877,10 @@ int sa_window_advance(sa_engine *e, uint64_t new_base) {
   for (uint64_t k = 0; k < n; ++k) {
     const uint64_t ws = (e->win_base + k) & (e->cfg.n_windows - 1);
     SA_HIP(e, hipMemsetAsync(e->hll + ws * e->hll_slot_bytes, 0, e->hll_slot_bytes, e->stream));
+    if (e->hll_lb) {  // the window's bounds go back to 0 with its registers
+      const size_t per = e->hll_slot_bytes >> e->lb_shift;
+      SA_HIP(e, hipMemsetAsync(e->hll_lb + ws * per, 0, per, e->stream));
+    }
     SA_HIP(e, hipMemsetAsync(e->cms + ws * e->cms_slot_elems, 0, e->cms_slot_elems * 8, e->stream));
     if (int rc = fold_errslab(e, ws, e->stream)) return rc;  // clears the slab cells
     SA_HIP(e, hipMemsetAsync(e->errcnt + ws * e->cap, 0, e->cap * 8, e->stream));

@@ -1290,9 +1290,10 @@ __global__ void compact_kernel(const unsigned long long *gkeys, unsigned long lo
 
 __device__ __forceinline__ uint32_t geom_find(const unsigned long long *gkeys, uint64_t m, const RowGeom &g) {
   if (g.binned) {
-    const uint32_t sb = 1u << g.log2sb;
-    for (uint32_t i = 0; i < sb; ++i) {
-      const uint32_t s = bt_slot(m, g.log2sb, i);
+    const BtSeq q = bt_seq(m, g.log2sb);
+    const uint32_t base = (uint32_t)(m >> kBinShift) << g.log2sb;
+    for (uint32_t i = 0; i < bt_probe_max(g.log2sb); ++i) {
+      const uint32_t s = base | bt_pos(q, i);
       const unsigned long long k = gkeys[s];
       if (k == m) return s;
       if (k == 0) return kNotFound;

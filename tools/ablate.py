@@ -98,6 +98,22 @@ def main():
         e.window_advance(wl.first_window)
         engines[f"variant{v}"] = e
     os.environ["SPANAGG_VARIANT"] = base_variant
+    # engine-creation environment variants: "name:VAR=v;VAR2=v,name2:VAR=v"
+    for spec in [x for x in os.environ.get("ABL_ENVS", "").split(",") if x]:
+        name, kv = spec.split(":", 1)
+        saved = {}
+        for item in [y for y in kv.split(";") if y]:
+            k, v = item.split("=", 1)
+            saved[k] = os.environ.get(k)
+            os.environ[k] = v
+        e = Engine(Config(n_services=wl.n_services, n_windows=16, key_capacity=kcap))
+        e.window_advance(wl.first_window)
+        engines[name] = e
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     for kc in [int(x) for x in os.environ.get("ABL_KCAPS", "").split(",") if x]:
         e = Engine(Config(n_services=wl.n_services, n_windows=16, key_capacity=kc))
         e.window_advance(wl.first_window)
