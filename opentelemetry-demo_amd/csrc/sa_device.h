@@ -413,5 +413,31 @@ __device__ __forceinline__ uint32_t wave_count(bool p) {
   return (uint32_t)__popcll(__ballot(p));
 }
 
+__device__ __forceinline__ uint32_t min_bytes(uint4 v) {
+  uint32_t m = 0xFFu;
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int s = 0; s < 32; s += 8) m = min(m, (w[i] >> s) & 0xFFu);
+  return m;
+}
+
+// One wave recomputes the lower bound of one HLL sub-block per launch
+// (rotating over launches when there are more sub-blocks than waves).
+__device__ __forceinline__ void hll_lb_refresh(const IngestParams &P, uint32_t wave, uint32_t waves) {
+  if (!P.lb_n) return;
+  const uint32_t total = min(P.lb_n, gridDim.x * waves), gi = blockIdx.x * waves + wave;
+  if (gi >= total) return;
+  const uint32_t sb = (uint32_t)(((uint64_t)P.lb_seq * total + gi) % P.lb_n);
+  const uint32_t lane = threadIdx.x & 63u, quads = (1u << P.lb_shift) / 16;
+  const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
+  uint32_t mn = 0xFFu;
+  for (uint32_t o = lane; o < quads; o += 64) mn = min(mn, min_bytes(src[o]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+  if (lane == 0) P.hll_lb[sb] = (uint8_t)mn;
+}
+
 }  // namespace
 }  // namespace sa

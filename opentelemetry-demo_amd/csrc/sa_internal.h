@@ -272,7 +272,7 @@ constexpr uint32_t kDbgPerWg = 136;  // diagnostic stamps per workgroup: 8 + 16 
 constexpr uint32_t kHllQueue = 2048;  // deferred HLL raises per workgroup (8 B each)
 constexpr uint32_t kErrTab = 1024;    // LDS (window, slot) -> ERROR count table per workgroup (4 B each)
 // ingest_lds_kernel LDS beyond the table: HLL queue + its count + bin table
-constexpr size_t kLdsExtraBytes = kHllQueue * 8 + 16 + kBins * sizeof(BinEntry) + kErrTab * 4;
+constexpr size_t kLdsExtraBytes = kHllQueue * 8 + 16 + kBins * sizeof(BinEntry) + kErrTab * 4 + kLbMaxSub;
 
 // launchers (spanagg_kernels.hip)
 hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,

@@ -351,32 +351,6 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-__device__ __forceinline__ uint32_t min_bytes(uint4 v) {
-  uint32_t m = 0xFFu;
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int s = 0; s < 32; s += 8) m = min(m, (w[i] >> s) & 0xFFu);
-  return m;
-}
-
-// One wave recomputes the lower bound of one HLL sub-block per launch
-// (rotating over launches when there are more sub-blocks than waves).
-__device__ __forceinline__ void hll_lb_refresh(const IngestParams &P, uint32_t wave, uint32_t waves) {
-  if (!P.lb_n) return;
-  const uint32_t total = min(P.lb_n, gridDim.x * waves), gi = blockIdx.x * waves + wave;
-  if (gi >= total) return;
-  const uint32_t sb = (uint32_t)(((uint64_t)P.lb_seq * total + gi) % P.lb_n);
-  const uint32_t lane = threadIdx.x & 63u, quads = (1u << P.lb_shift) / 16;
-  const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
-  uint32_t mn = 0xFFu;
-  for (uint32_t o = lane; o < quads; o += 64) mn = min(mn, min_bytes(src[o]));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
-  if (lane == 0) P.hll_lb[sb] = (uint8_t)mn;
-}
-
 // Round-synchronous scatter.  The workgroup takes its span range in rounds of
 // 2,048 spans (one 128-span tile per wave, two rounds of tiles in flight);
 // every span claims a slot of its bin's 4-record LDS stage with one LDS
@@ -903,9 +877,9 @@ __host__ __device__ inline uint32_t bt_agg2_off_err(uint32_t sb) { return (sb * 
 __host__ __device__ inline uint32_t bt_agg2_off_reg(uint32_t sb) { return bt_agg2_off_err(sb) + kBtAgg2Err * 8; }
 
 // MODE (ablation): 1 = no records aggregated, 2 = no key / row write-back;
-// MAXPER = key slots per thread (sb <= MAXPER * 512)
-template <int MODE = 0, int MAXPER = 2>
-__global__ __launch_bounds__(kBtAgg2Block) void bt_aggregate2_kernel(IngestParams P) {
+// MAXPER = key slots per thread (sb <= MAXPER * BLOCK)
+template <int MODE = 0, int MAXPER = 2, int BLOCK = 512>
+__global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t log2sb = P.log2sb, sb = 1u << log2sb, smask = sb - 1;
   const uint32_t G = P.bt_grid, bin = blockIdx.x, region = P.bt_region;
@@ -925,21 +899,21 @@ __global__ __launch_bounds__(kBtAgg2Block) void bt_aggregate2_kernel(IngestParam
   unsigned long long orig[kMaxPer];
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
-    const uint32_t s = tid + u * kBtAgg2Block;
+    const uint32_t s = tid + u * BLOCK;
     orig[u] = s < sb ? gk[s] : 0ULL;
   }
-  for (uint32_t g = tid; g < G; g += kBtAgg2Block) rcnt[g] = P.bt_cnt[(uint64_t)bin * G + g];
+  for (uint32_t g = tid; g < G; g += BLOCK) rcnt[g] = P.bt_cnt[(uint64_t)bin * G + g];
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
-    const uint32_t s = tid + u * kBtAgg2Block;
+    const uint32_t s = tid + u * BLOCK;
     if (s < sb) {
       lkeys[s] = orig[u];
       lsum[s] = 0;
     }
   }
   const uint32_t cw = bt_agg2_cnt_words(sb);
-  for (uint32_t i = tid; i < cw; i += kBtAgg2Block) lcnt[i] = 0;
-  for (uint32_t i = tid; i < kBtAgg2Err; i += kBtAgg2Block) etab[i] = make_uint2(0, 0);
+  for (uint32_t i = tid; i < cw; i += BLOCK) lcnt[i] = 0;
+  for (uint32_t i = tid; i < kBtAgg2Err; i += BLOCK) etab[i] = make_uint2(0, 0);
   if (tid == 0) misc[0] = 0;
   __syncthreads();
   bt_stamp(P, (uint64_t)bin * 8, 1);
@@ -1003,7 +977,7 @@ __global__ __launch_bounds__(kBtAgg2Block) void bt_aggregate2_kernel(IngestParam
     }
   };
   if (!(MODE & 1)) {
-    constexpr uint32_t kWaves = kBtAgg2Block / 64, B = 8;
+    constexpr uint32_t kWaves = BLOCK / 64, B = 8;
     const uint32_t pairs = (G + 1) / 2;
     for (uint32_t p0 = wave; p0 < pairs; p0 += kWaves * B) {
       ulonglong2 v[B];
@@ -1046,7 +1020,7 @@ __global__ __launch_bounds__(kBtAgg2Block) void bt_aggregate2_kernel(IngestParam
   bool touched[kMaxPer];
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
-    const uint32_t s = tid + u * kBtAgg2Block;
+    const uint32_t s = tid + u * BLOCK;
     touched[u] = s < sb && lsum[s] != 0;
     if (s < sb && !touched[u]) {  // a zero ns sum: look at the counts
       uint32_t any = 0;
@@ -1062,7 +1036,7 @@ __global__ __launch_bounds__(kBtAgg2Block) void bt_aggregate2_kernel(IngestParam
   }
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
-    const uint32_t s = tid + u * kBtAgg2Block;
+    const uint32_t s = tid + u * BLOCK;
     if (s >= sb) continue;
     const unsigned long long k = lkeys[s];
     if (k != orig[u]) gk[s] = k;
@@ -1088,7 +1062,7 @@ __global__ __launch_bounds__(kBtAgg2Block) void bt_aggregate2_kernel(IngestParam
     for (uint32_t q = 0; q < 5; ++q)
       if (q < nq) row[q] = make_uint4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
   }
-  for (uint32_t i = tid; i < kBtAgg2Err; i += kBtAgg2Block) {
+  for (uint32_t i = tid; i < kBtAgg2Err; i += BLOCK) {
     const uint2 e = etab[i];
     if (e.x == 0) continue;
     const uint32_t ek = e.x - 1, ws = ek >> log2sb, s = ek & smask;
@@ -1206,7 +1180,8 @@ hipError_t launch_ingest_bt(const IngestParams &P, size_t agg_lds, hipStream_t s
   }
   if (P.diag & kDiagBtNoAgg) return hipSuccess;
   const uint32_t diag = P.diag | (P.log2sb > 10 ? kDiagBtAggWide : 0u);
-  return hipLaunchKernel(bt_agg_fn(diag), dim3(kPartBins), dim3((P.diag & kDiagBtAgg1) ? kBtAggBlock : kBtAgg2Block),
+  const uint32_t blk = (P.diag & kDiagBtAgg1) ? kBtAggBlock : kBtAgg2Block;
+  return hipLaunchKernel(bt_agg_fn(diag), dim3(kPartBins), dim3(blk),
                          args, (P.diag & kDiagBtAgg1) ? agg_lds : bt_agg2_lds_bytes(P.log2sb, P.bt_grid), s);
 }
 

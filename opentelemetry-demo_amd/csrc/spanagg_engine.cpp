@@ -613,7 +613,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.dbg = e->dbg;
   P.hll_lb = e->hll_lb;
   P.lb_shift = e->lb_shift;
-  P.lb_n = e->bt ? e->lb_n : 0;  // the kernels that read the bounds
+  P.lb_n = e->lb_n;  // read (and refreshed) by the v2 and binned kernels; the others ignore it
   P.lb_seq = e->lb_seq++;
   hipError_t st;
   if (e->small) {

@@ -425,7 +425,9 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   uint32_t *hq_n = reinterpret_cast<uint32_t *>(hq + kHllQueue);
   BinEntry *lbins = reinterpret_cast<BinEntry *>(hq_n + 4);
   uint32_t *etab = reinterpret_cast<uint32_t *>(lbins + kBins);  // [kErrTab]: (key+1) << 16 | count
+  uint8_t *llb = reinterpret_cast<uint8_t *>(etab + kErrTab);       // [kLbMaxSub] HLL lower bounds
   const bool err_lds = P.errslab != nullptr;
+  const bool lb_on = P.lb_n != 0 && !(diag & 2u);
 
   uint64_t lo, hi;
   wg_range_p(P, lo, hi);
@@ -470,6 +472,8 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   }
   uint4 bv = make_uint4(0, 0, 0, 0);
   if (threadIdx.x < kBins * 2) bv = reinterpret_cast<const uint4 *>(P.bintab)[threadIdx.x];
+  uint32_t lbw = 0;
+  if (lb_on && threadIdx.x * 4 < P.lb_n) lbw = *reinterpret_cast<const uint32_t *>(P.hll_lb + threadIdx.x * 4);
   if constexpr (DYN && (OPT & 1)) {
     // no wait here (gfx950 barriers do not drain vmcnt): only the issue order
     __builtin_amdgcn_sched_barrier(0);
@@ -508,6 +512,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     hq_n[1] = (kTileClaims ? 2u * NBUF : 2u) * kWaves;  // DYN: next unclaimed chunk of this workgroup's range
   }
   etab[threadIdx.x] = 0;  // kErrTab == kLdsBlock
+  if (lb_on && threadIdx.x * 4 < P.lb_n) reinterpret_cast<uint32_t *>(llb)[threadIdx.x] = lbw;
   __syncthreads();
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 1] = __builtin_amdgcn_s_memrealtime();
 
@@ -526,6 +531,9 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   };
   stamp(-1);
   const __amdgpu_buffer_rsrc_t hll_rsrc = rsrc(P.hll, 0xFFFFFFFFu);
+  constexpr uint32_t kHotUnset = 0xFFFFFFFEu;
+  uint32_t hot_slot = kHotUnset;  // wave-uniform (see step 5b)
+  unsigned long long hot_sum = 0;
   // wave-uniform event counts (scalar registers)
   uint32_t n_zero = 0, n_badsvc = 0, n_oor = 0, n_drop = 0;
 #pragma unroll
@@ -580,8 +588,11 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
         // diag 16384: one 64-bit multiply instead of xxh64 (prices the hash's VALU)
         const uint64_t x = (DIAG && (diag & 16384u)) ? (T.a[j] ^ T.b[j]) * XP1 : xxh64_16(T.a[j], T.b[j]);
         const uint32_t r = (uint32_t)__clzll((long long)((x << hp) | (1ULL << (hp - 1)))) + 1;
-        rho[j] = sk ? r : 0u;
-        hoff[j] = sk ? ((ws[j] * P.n_services + svc) << hp) + (uint32_t)(x >> (64 - hp)) : 0u;
+        const uint32_t ho = sk ? ((ws[j] * P.n_services + svc) << hp) + (uint32_t)(x >> (64 - hp)) : 0u;
+        // a rho at or below the register sub-block's lower bound cannot raise it
+        const bool up = sk && !(lb_on && r <= llb[ho >> P.lb_shift]);
+        rho[j] = up ? r : 0u;
+        hoff[j] = up ? ho : 0u;
       }
     }
     stamp(0);
@@ -645,6 +656,23 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
       }
     }
     stamp(2);
+    // wave-level key dedup (first step only): the wave's hot series is the
+    // most common slot among four candidate lanes (ballot); its ns sum then
+    // accumulates in a lane register instead of the LDS atomic that every lane
+    // of that series would otherwise serialise on (summed once at the end)
+    if (hot_slot == kHotUnset) {
+      uint32_t best = kNotFound, nbest = 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const uint32_t cand = (uint32_t)__builtin_amdgcn_readlane((int)found[0], c * 16);
+        const uint32_t n = wave_count(found[0] == cand);
+        if (cand != kNotFound && n > nbest) {
+          best = cand;
+          nbest = n;
+        }
+      }
+      hot_slot = best;
+    }
     // 6. ERROR spans: exact per-(window, slot) counter (one no-return atomic);
     //    spans without a slot update the count-min cells directly
 #pragma unroll
@@ -669,7 +697,8 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
         const uint32_t fs = (DIAG && (diag & 4096u)) ? (found[j] + (threadIdx.x & 63u) * 29u) & (cap - 1u)
                                                      : found[j];
         atomicAdd(&lcnt[fs * nw + (b >> 1)], 1u << ((b & 1) * 16));
-        atomicAdd(&lsum[fs], (unsigned long long)dur[j]);
+        if (found[j] == hot_slot) hot_sum += dur[j];
+        else atomicAdd(&lsum[fs], (unsigned long long)dur[j]);
       }
     }
     stamp(3);
@@ -728,6 +757,13 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     }
   }
   hll_settle(pend);
+  if (hot_slot < cap) {  // the hot series' ns sum: one add per wave
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+      hot_sum += (unsigned long long)(uint32_t)__shfl_xor((int)(uint32_t)hot_sum, o, 64) |
+                 ((unsigned long long)(uint32_t)__shfl_xor((int)(uint32_t)(hot_sum >> 32), o, 64) << 32);
+    if ((threadIdx.x & 63u) == 0 && hot_sum) atomicAdd(&lsum[hot_slot], hot_sum);
+  }
   const uint64_t wave_loop_end = DIAG && P.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 2] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
@@ -741,6 +777,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   }
   const uint32_t nq = *hq_n < kHllQueue ? *hq_n : kHllQueue;
   for (uint32_t i = threadIdx.x; i < nq; i += kLdsBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
+  hll_lb_refresh(P, threadIdx.x >> 6, kWaves);
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 3] = __builtin_amdgcn_s_memrealtime();
   if (DIAG && P.dbg && (threadIdx.x & 63) == 0) {
     for (int i = 0; i < 6; ++i) P.dbg[blockIdx.x * kDbgPerWg + 8 + (threadIdx.x >> 6) * 8 + i] = seg[i];
