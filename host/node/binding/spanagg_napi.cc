@@ -51,15 +51,33 @@ napi_value throw_type(napi_env env, const std::string &msg) {
     return nullptr;
 }
 
-// Engine handle: a JS object wrapping the sa_engine*, destroyed by destroy()
-// or, failing that, by the GC finalizer.
+// Engine handle: a JS object wrapping one sa_engine* or one sa_group* (an
+// engine per GPU behind the same calls), destroyed by destroy() or, failing
+// that, by the GC finalizer.  The ops below dispatch on which one it holds.
 struct Handle {
     sa_engine *e = nullptr;
+    sa_group *g = nullptr;
+    bool live() const { return e || g; }
+    void destroy() {
+        if (e) sa_destroy(e);
+        if (g) sa_group_destroy(g);
+        e = nullptr;
+        g = nullptr;
+    }
+    const char *last_error() const { return g ? sa_group_last_error(g) : e ? sa_last_error(e) : ""; }
+    int ingest(const sa_span_batch *b) { return g ? sa_group_ingest(g, b) : sa_ingest(e, b); }
+    int sync() { return g ? sa_group_sync(g) : sa_sync(e); }
+    int flush(sa_red_result **r) { return g ? sa_group_flush(g, r) : sa_flush(e, r); }
+    int window_read(uint64_t w, sa_sketch_result **r) {
+        return g ? sa_group_window_read(g, w, r) : sa_window_read(e, w, r);
+    }
+    int window_advance(uint64_t b) { return g ? sa_group_window_advance(g, b) : sa_window_advance(e, b); }
+    int stats(sa_stats *s) { return g ? sa_group_get_stats(g, s) : sa_get_stats(e, s); }
 };
 
 void finalize_handle(napi_env, void *data, void *) {
     auto *h = static_cast<Handle *>(data);
-    if (h->e) sa_destroy(h->e);
+    h->destroy();
     delete h;
 }
 
@@ -77,7 +95,7 @@ Handle *get_handle(napi_env env, napi_value v) {
         return nullptr;
     }
     auto *h = static_cast<Handle *>(p);
-    if (!h->e) {
+    if (!h->live()) {
         throw_status(env, SA_ESTATE, "engine already destroyed");
         return nullptr;
     }
@@ -85,7 +103,7 @@ Handle *get_handle(napi_env env, napi_value v) {
 }
 
 napi_value engine_error(napi_env env, Handle *h, int rc, const char *what) {
-    std::string msg = std::string(what) + ": " + (h && h->e ? sa_last_error(h->e) : "");
+    std::string msg = std::string(what) + ": " + (h ? h->last_error() : "");
     return throw_status(env, rc, msg);
 }
 
@@ -321,16 +339,36 @@ napi_value Create(napi_env env, napi_callback_info info) {
     }
     c.bounds = bounds.data();
     c.n_bounds = static_cast<uint32_t>(bounds.size());
-    sa_engine *e = nullptr;
-    int rc = sa_create(&c, &e);
-    if (rc != SA_OK || !e)
+    // devices: [d0, d1, ...] -> an engine group (one engine per entry, spans
+    // sharded by trace id, merged at flush / window read)
+    std::vector<int32_t> devs;
+    if (!is_undefined(env, v = prop(env, cfg, "devices"))) {
+        bool arr = false;
+        napi_is_array(env, v, &arr);
+        uint32_t len = 0;
+        if (!arr || napi_get_array_length(env, v, &len) != napi_ok || len == 0)
+            return throw_type(env, "devices: expected a non-empty array of device ordinals");
+        for (uint32_t i = 0; i < len; ++i) {
+            napi_value x;
+            uint32_t d = 0;
+            napi_get_element(env, v, i, &x);
+            if (!to_u32(env, x, &d, "devices[]")) return nullptr;
+            devs.push_back(static_cast<int32_t>(d));
+        }
+    }
+    auto *h = new Handle();
+    int rc = devs.empty() ? sa_create(&c, &h->e)
+                          : sa_group_create(&c, devs.data(), static_cast<uint32_t>(devs.size()), &h->g);
+    if (rc != SA_OK || !h->live()) {
+        delete h;
         return throw_status(env, rc ? rc : SA_EDEVICE,
-                            "sa_create failed (invalid config, or no gfx950 GPU visible)");
+                            devs.empty() ? "sa_create failed (invalid config, or no gfx950 GPU visible)"
+                                         : "sa_group_create failed (invalid config, or no gfx950 GPU visible)");
+    }
     napi_value obj;
-    auto *h = new Handle{e};
     if (napi_create_object(env, &obj) != napi_ok ||
         napi_wrap(env, obj, h, finalize_handle, nullptr, nullptr) != napi_ok) {
-        sa_destroy(e);
+        h->destroy();
         delete h;
         return throw_napi(env, "napi_wrap");
     }
@@ -342,9 +380,7 @@ napi_value Destroy(napi_env env, napi_callback_info info) {
     if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
     void *p = nullptr;
     if (napi_unwrap(env, argv[0], &p) == napi_ok && p) {
-        auto *h = static_cast<Handle *>(p);
-        if (h->e) sa_destroy(h->e);
-        h->e = nullptr;
+        static_cast<Handle *>(p)->destroy();
     }
     return nullptr;
 }
@@ -355,7 +391,7 @@ napi_value LastError(napi_env env, napi_callback_info info) {
     Handle *h = get_handle(env, argv[0]);
     if (!h) return nullptr;
     napi_value s;
-    napi_create_string_utf8(env, sa_last_error(h->e), NAPI_AUTO_LENGTH, &s);
+    napi_create_string_utf8(env, h->last_error(), NAPI_AUTO_LENGTH, &s);
     return s;
 }
 
@@ -384,7 +420,7 @@ napi_value Ingest(napi_env env, napi_callback_info info) {
     if (!typed(env, prop(env, argv[1], "meta"), napi_uint32_array, &md, &mlen, "meta")) return nullptr;
     if (mlen != n) return throw_status(env, SA_EINVAL, "ingest: ragged SoA batch");
     sa_span_batch b{p64[0], p64[1], p64[2], p64[3], p64[4], static_cast<const uint32_t *>(md), n};
-    int rc = sa_ingest(h->e, &b);
+    int rc = h->ingest(&b);
     if (rc != SA_OK) return engine_error(env, h, rc, "sa_ingest");
     return nullptr;
 }
@@ -394,7 +430,7 @@ napi_value Sync(napi_env env, napi_callback_info info) {
     if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
     Handle *h = get_handle(env, argv[0]);
     if (!h) return nullptr;
-    int rc = sa_sync(h->e);
+    int rc = h->sync();
     if (rc != SA_OK) return engine_error(env, h, rc, "sa_sync");
     return nullptr;
 }
@@ -406,7 +442,7 @@ napi_value Flush(napi_env env, napi_callback_info info) {
     Handle *h = get_handle(env, argv[0]);
     if (!h) return nullptr;
     sa_red_result *r = nullptr;
-    int rc = sa_flush(h->e, &r);
+    int rc = h->flush(&r);
     if ((rc != SA_OK && rc != SA_EFULL) || !r) {
         if (r) sa_red_result_free(r);
         return engine_error(env, h, rc ? rc : SA_ESTATE, "sa_flush");
@@ -437,7 +473,7 @@ napi_value WindowRead(napi_env env, napi_callback_info info) {
     uint64_t wid;
     if (!h || !to_u64(env, argv[1], &wid, "windowId")) return nullptr;
     sa_sketch_result *r = nullptr;
-    int rc = sa_window_read(h->e, wid, &r);
+    int rc = h->window_read(wid, &r);
     if (rc != SA_OK || !r) {
         if (r) sa_sketch_result_free(r);
         return engine_error(env, h, rc ? rc : SA_ESTATE, "sa_window_read");
@@ -465,7 +501,7 @@ napi_value WindowAdvance(napi_env env, napi_callback_info info) {
     Handle *h = get_handle(env, argv[0]);
     uint64_t base;
     if (!h || !to_u64(env, argv[1], &base, "newBase")) return nullptr;
-    int rc = sa_window_advance(h->e, base);
+    int rc = h->window_advance(base);
     if (rc != SA_OK) return engine_error(env, h, rc, "sa_window_advance");
     return nullptr;
 }
@@ -476,7 +512,7 @@ napi_value Stats(napi_env env, napi_callback_info info) {
     Handle *h = get_handle(env, argv[0]);
     if (!h) return nullptr;
     sa_stats s;
-    int rc = sa_get_stats(h->e, &s);
+    int rc = h->stats(&s);
     if (rc != SA_OK) return engine_error(env, h, rc, "sa_get_stats");
     napi_value o, b;
     if (napi_create_object(env, &o) != napi_ok) return throw_napi(env, "napi_create_object");
@@ -490,6 +526,9 @@ napi_value Stats(napi_env env, napi_callback_info info) {
     set(env, o, "windowBase", big(env, s.window_base));
     napi_get_boolean(env, s.small_table != 0, &b);
     set(env, o, "smallTable", b);
+    set(env, o, "engines", num(env, h->g ? sa_group_size(h->g) : 1));
+    napi_get_boolean(env, h->g && sa_group_uses_rccl(h->g), &b);
+    set(env, o, "rccl", b);
     return o;
 }
 
@@ -683,11 +722,11 @@ napi_value ColumnizerIngest(napi_env env, napi_callback_info info) {
   if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
   ColHandle *c = get_col(env, argv[0]);
   if (!c) return nullptr;
-  if (!c->engine || !c->engine->e) return throw_status(env, SA_ESTATE, "the columnizer has no live engine");
+  if (!c->engine || !c->engine->live()) return throw_status(env, SA_ESTATE, "the columnizer has no live engine");
   const size_t n = c->col.buffered();
   if (n) {
     sa_span_batch b{c->col.key(), c->col.start(), c->col.end(), c->col.w0(), c->col.w1(), c->col.meta(), n};
-    const int rc = sa_ingest(c->engine->e, &b);
+    const int rc = c->engine->ingest(&b);
     if (rc != SA_OK) return engine_error(env, c->engine, rc, "sa_ingest");
   }
   c->col.clear_buffer();

@@ -74,7 +74,9 @@ const TEMPORALITY = {
 /**
  * Config with the spanmetrics YAML field names; defaults = createDefaultConfig
  * (the reference declares `spanmetrics:` with an empty body, SURVEY.md a1).
- * `sketches`, `key_capacity`, `device`, `batch_size` are this build's own.
+ * `sketches`, `key_capacity`, `device`, `devices`, `batch_size` are this
+ * build's own; `devices: [0, 1, ...]` runs one engine per listed GPU behind the
+ * connector (spans sharded by trace id, merged at every flush and window read).
  * Histogram buckets: duration strings ("2ms") as in YAML, or numbers already
  * in the histogram unit.
  */
@@ -116,6 +118,7 @@ function normalizeConfig(cfg = {}, addon) {
       default: x.default === undefined || x.default === null ? undefined : String(x.default) })),
     keyCapacity: cfg.key_capacity || d.keyCapacity,
     device: cfg.device || 0,
+    devices: Array.isArray(cfg.devices) && cfg.devices.length ? cfg.devices.map(Number) : null,
     batchSize: cfg.batch_size || 1 << 16,
   };
 }
@@ -158,7 +161,7 @@ class SpanMetricsConnector {
     const c = this.cfg;
     this.handle = this.addon.create({ bounds: c.bounds, unit: c.unit, hllP: c.hllP, cmsD: c.cmsD,
       cmsW: c.cmsW, windowNs: c.windowNs, nWindows: c.nWindows, nServices: c.nServices,
-      keyCapacity: c.keyCapacity, device: c.device });
+      keyCapacity: c.keyCapacity, device: c.device, ...(c.devices ? { devices: c.devices } : {}) });
     this.cols = new Columns(c.batchSize);
     // native OTLP columnizer (binding/otlp_columnizer.cc) for request bytes, when
     // every enabled option is one it implements; otherwise the JS path below

@@ -181,6 +181,46 @@ int sa_gather_dense(sa_engine *e, const uint64_t *d_keys, uint64_t n, uint64_t *
 int sa_window_export(sa_engine *e, uint64_t window_id, uint8_t *d_hll, uint64_t *d_cms,
                      void *stream);
 
+/* ---- engine groups: one engine per GPU behind one handle ----
+ * The connector's single ConsumeTraces/exportMetrics pair over several GPUs.
+ * Spans shard by trace id (engine = trace_w1 % n), so every trace's spans land
+ * on one engine and the per-engine sketches stay exact partials; the group's
+ * flush / window read return the merge:
+ *   RED: key union across engines (a series seen on several engines is one
+ *        row), bucket counts and ns sums added;
+ *   HLL: registers max-merged (exact and idempotent);
+ *   count-min: cells added, then saturated to u32.
+ * Merge transport: when every member has its own device the group owns an
+ * RCCL communicator over them (ncclAllGather of the key lists, ncclAllReduce
+ * sum u64 of the dense rows and count-min cells, max u8 of the HLL
+ * registers, over xGMI); members that share a device (or SPANAGG_GROUP_RCCL=0)
+ * merge through device-to-device copies onto member 0's device and a reduce
+ * kernel there.  Results are identical either way (integer sums and maxima).
+ * Threading: as an engine (single producer); sa_group_ingest fans the shards
+ * out to one host thread per member. */
+typedef struct sa_group sa_group;
+/* devices[i] = HIP ordinal of member i (repeats allowed); cfg->device is ignored. */
+int sa_group_create(const sa_config *cfg, const int32_t *devices, uint32_t n, sa_group **out);
+void sa_group_destroy(sa_group *g);
+const char *sa_group_last_error(const sa_group *g);
+uint32_t sa_group_size(const sa_group *g);
+/* 1 when the group merges over RCCL, 0 when through device copies */
+int sa_group_uses_rccl(const sa_group *g);
+/* Member engine i (for device-resident ingest of a shard the caller made). */
+sa_engine *sa_group_member(sa_group *g, uint32_t i);
+/* Host batch: split by trace_w1 % n, each shard ingested by its member. */
+int sa_group_ingest(sa_group *g, const sa_span_batch *batch);
+int sa_group_sync(sa_group *g);
+/* Merged delta since the previous group flush (members reset); SA_EFULL as
+ * sa_flush when any member dropped spans. Free with sa_red_result_free. */
+int sa_group_flush(sa_group *g, sa_red_result **out);
+/* Merged sketches of one resident window. Free with sa_sketch_result_free. */
+int sa_group_window_read(sa_group *g, uint64_t window_id, sa_sketch_result **out);
+int sa_group_window_advance(sa_group *g, uint64_t new_base);
+/* Counters summed over members (n_keys and table_capacity too; window_base and
+ * small_table from member 0). */
+int sa_group_get_stats(sa_group *g, sa_stats *out);
+
 /* Diagnostic only: per-workgroup s_memrealtime stamps (100 MHz) of the last
  * small-table ingest launch, [G][136] = {start, after LDS setup, after the span
  * loop, after the slab flush, 0 x 4, then per wave 8 segment cycle sums};

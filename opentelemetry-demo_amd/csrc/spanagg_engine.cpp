@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "sa_internal.h"
+#include "sa_results.h"
 #include "spanagg.h"
 
 using sa::IngestParams;
@@ -735,12 +736,6 @@ static int read_stats(sa_engine *e, uint64_t out[sa::kNumStats]) {
   return SA_OK;
 }
 
-struct red_holder {
-  sa_red_result r;
-  std::vector<uint64_t> keys, counts, calls, sum_ns;
-  std::vector<double> sum;
-};
-
 int sa_flush(sa_engine *e, sa_red_result **out) {
   if (!e || !out) return SA_EINVAL;
   *out = nullptr;
@@ -802,12 +797,6 @@ int sa_flush(sa_engine *e, sa_red_result **out) {
 }
 
 void sa_red_result_free(sa_red_result *r) { delete reinterpret_cast<red_holder *>(r); }
-
-struct sketch_holder {
-  sa_sketch_result r;
-  std::vector<uint8_t> hll;
-  std::vector<uint32_t> cms;
-};
 
 static bool resident(const sa_engine *e, uint64_t w) {
   return w >= e->win_base && w - e->win_base < e->cfg.n_windows;

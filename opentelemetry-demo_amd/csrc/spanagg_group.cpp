@@ -1,0 +1,452 @@
+// spanagg_group.cpp -- engine groups (include/spanagg.h, sa_group_*): the
+// spanmetrics connector's ConsumeTraces / exportMetrics over several GPUs of
+// one node behind one handle.  Spans shard by trace id,
+// so each member aggregates whole traces; at flush and window read the group
+// merges the members' partials:
+//   - key union: the members' non-zero series ids (sa_export_keys), gathered
+//     with ncclAllGather (or device copies) and made a sorted dense index;
+//   - RED rows densified against it (sa_gather_dense), summed (ncclAllReduce
+//     sum u64, or copies onto member 0's device + a reduce kernel);
+//   - HLL registers max-merged (ncclAllReduce max u8), count-min cells summed.
+// Every merge is integer sums and maxima, so both transports give the same
+// bits as one engine fed the whole stream.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "sa_results.h"
+#include "spanagg.h"
+
+namespace {
+
+__global__ void sum_slices_u64(unsigned long long *dst, const unsigned long long *src, uint32_t n, uint64_t len) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < len; i += (uint64_t)gridDim.x * blockDim.x) {
+    unsigned long long acc = 0;
+    for (uint32_t k = 0; k < n; ++k) acc += src[k * len + i];
+    dst[i] = acc;
+  }
+}
+
+__global__ void max_slices_u8(uint8_t *dst, const uint8_t *src, uint32_t n, uint64_t len) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < len; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint8_t m = 0;
+    for (uint32_t k = 0; k < n; ++k) m = src[k * len + i] > m ? src[k * len + i] : m;
+    dst[i] = m;
+  }
+}
+
+uint32_t grid_for(uint64_t len) { return (uint32_t)std::min<uint64_t>((len + 255) / 256, 4096); }
+
+// Device buffer on one member's device, grown on demand.
+struct Buf {
+  void *p = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace
+
+struct sa_group {
+  sa_config cfg{};
+  std::vector<double> bounds;
+  std::vector<sa_engine *> eng;
+  std::vector<int> dev;
+  std::vector<hipStream_t> st;  // one merge stream per member, on its device
+  bool rccl = false;
+  std::vector<ncclComm_t> comm;
+  std::vector<Buf> keys, gath, uni, rows, hll, cms;
+  Buf stack;  // member 0's device: every member's slice for the copy-path reduce
+  std::vector<uint64_t> dropped_seen;
+  uint32_t nbk = 0;
+  size_t hll_bytes = 0, cms_elems = 0;
+  std::string err;
+};
+
+namespace {
+
+int gfail(sa_group *g, int code, const std::string &msg) {
+  if (g) g->err = msg;
+  return code;
+}
+
+#define SG_HIP(g, call)                                                                  \
+  do {                                                                                   \
+    hipError_t _s = (call);                                                              \
+    if (_s != hipSuccess)                                                                \
+      return gfail((g), SA_EDEVICE, std::string(#call) + ": " + hipGetErrorString(_s)); \
+  } while (0)
+
+#define SG_NCCL(g, call)                                                                   \
+  do {                                                                                     \
+    ncclResult_t _r = (call);                                                              \
+    if (_r != ncclSuccess)                                                                 \
+      return gfail((g), SA_EDEVICE, std::string(#call) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
+
+int ensure(sa_group *g, int dev, Buf &b, size_t bytes) {
+  if (b.bytes >= bytes) return SA_OK;
+  SG_HIP(g, hipSetDevice(dev));
+  if (b.p) SG_HIP(g, hipFree(b.p));
+  b.p = nullptr;
+  b.bytes = 0;
+  if (hipMalloc(&b.p, bytes) != hipSuccess) return gfail(g, SA_ENOMEM, "group buffer hipMalloc failed");
+  b.bytes = bytes;
+  return SA_OK;
+}
+
+int member_error(sa_group *g, uint32_t i, int rc, const char *what) {
+  return gfail(g, rc, std::string(what) + " (member " + std::to_string(i) + "): " + sa_last_error(g->eng[i]));
+}
+
+// Copy-path reduction: every member's `len` elements of `bufs` onto member 0's
+// device (stacked), then one kernel writes the sum (u64) or max (u8) into
+// bufs[0].  Member streams are drained first; the result is ordered on st[0].
+int copy_reduce(sa_group *g, std::vector<Buf> &bufs, uint64_t len, bool max_u8) {
+  const uint32_t n = (uint32_t)g->eng.size();
+  const size_t esz = max_u8 ? 1 : 8, bytes = len * esz;
+  if (n == 1 || len == 0) return SA_OK;
+  if (int rc = ensure(g, g->dev[0], g->stack, bytes * n)) return rc;
+  for (uint32_t i = 0; i < n; ++i) {
+    SG_HIP(g, hipSetDevice(g->dev[i]));
+    SG_HIP(g, hipStreamSynchronize(g->st[i]));
+  }
+  SG_HIP(g, hipSetDevice(g->dev[0]));
+  char *dst = static_cast<char *>(g->stack.p);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (g->dev[i] == g->dev[0])
+      SG_HIP(g, hipMemcpyAsync(dst + i * bytes, bufs[i].p, bytes, hipMemcpyDeviceToDevice, g->st[0]));
+    else
+      SG_HIP(g, hipMemcpyPeerAsync(dst + i * bytes, g->dev[0], bufs[i].p, g->dev[i], bytes, g->st[0]));
+  }
+  if (max_u8)
+    hipLaunchKernelGGL(max_slices_u8, dim3(grid_for(len)), dim3(256), 0, g->st[0], static_cast<uint8_t *>(bufs[0].p),
+                       static_cast<const uint8_t *>(g->stack.p), n, len);
+  else
+    hipLaunchKernelGGL(sum_slices_u64, dim3(grid_for(len)), dim3(256), 0, g->st[0],
+                       static_cast<unsigned long long *>(bufs[0].p),
+                       static_cast<const unsigned long long *>(g->stack.p), n, len);
+  SG_HIP(g, hipGetLastError());
+  return SA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sa_group_create(const sa_config *cfg, const int32_t *devices, uint32_t n, sa_group **out) {
+  if (!out) return SA_EINVAL;
+  *out = nullptr;
+  if (!cfg || !devices || n == 0 || n > 64) return SA_EINVAL;
+  auto *g = new sa_group();
+  g->cfg = *cfg;
+  g->bounds.assign(cfg->bounds, cfg->bounds + cfg->n_bounds);
+  g->cfg.bounds = g->bounds.data();
+  g->nbk = cfg->n_bounds + 1;
+  g->hll_bytes = (size_t)cfg->n_services << cfg->hll_p;
+  g->cms_elems = (size_t)cfg->cms_d * cfg->cms_w;
+  for (uint32_t i = 0; i < n; ++i) {
+    sa_config c = g->cfg;
+    c.device = devices[i];
+    sa_engine *e = nullptr;
+    const int rc = sa_create(&c, &e);
+    if (rc != SA_OK || !e) {
+      sa_group_destroy(g);
+      return rc ? rc : SA_EDEVICE;
+    }
+    g->eng.push_back(e);
+    g->dev.push_back(devices[i]);
+    hipStream_t s = nullptr;
+    if (hipSetDevice(devices[i]) != hipSuccess || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+      sa_group_destroy(g);
+      return SA_EDEVICE;
+    }
+    g->st.push_back(s);
+  }
+  g->keys.resize(n);
+  g->gath.resize(n);
+  g->uni.resize(n);
+  g->rows.resize(n);
+  g->hll.resize(n);
+  g->cms.resize(n);
+  g->dropped_seen.assign(n, 0);
+  // RCCL over distinct devices (a communicator cannot hold two ranks of one
+  // device); a group of one uses it only when SPANAGG_GROUP_RCCL=1 asks
+  std::vector<int> sorted(g->dev);
+  std::sort(sorted.begin(), sorted.end());
+  const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+  const char *rv = std::getenv("SPANAGG_GROUP_RCCL");
+  const bool want = rv ? std::atoi(rv) != 0 : n > 1;
+  if (distinct && want) {
+    g->comm.resize(n);
+    if (ncclCommInitAll(g->comm.data(), (int)n, g->dev.data()) == ncclSuccess) {
+      g->rccl = true;
+    } else {
+      g->comm.clear();
+      g->err = "ncclCommInitAll failed: merging through device copies";
+    }
+  }
+  *out = g;
+  return SA_OK;
+}
+
+void sa_group_destroy(sa_group *g) {
+  if (!g) return;
+  for (ncclComm_t c : g->comm)
+    if (c) (void)ncclCommDestroy(c);
+  for (size_t i = 0; i < g->eng.size(); ++i) {
+    (void)hipSetDevice(g->dev[i]);
+    if (i < g->st.size() && g->st[i]) {
+      (void)hipStreamSynchronize(g->st[i]);
+      (void)hipStreamDestroy(g->st[i]);
+    }
+    for (std::vector<Buf> *v : {&g->keys, &g->gath, &g->uni, &g->rows, &g->hll, &g->cms})
+      if (i < v->size() && (*v)[i].p) (void)hipFree((*v)[i].p);
+    if (i == 0 && g->stack.p) (void)hipFree(g->stack.p);
+    sa_destroy(g->eng[i]);
+  }
+  delete g;
+}
+
+const char *sa_group_last_error(const sa_group *g) { return g ? g->err.c_str() : "null group"; }
+uint32_t sa_group_size(const sa_group *g) { return g ? (uint32_t)g->eng.size() : 0; }
+int sa_group_uses_rccl(const sa_group *g) { return g && g->rccl ? 1 : 0; }
+sa_engine *sa_group_member(sa_group *g, uint32_t i) { return g && i < g->eng.size() ? g->eng[i] : nullptr; }
+
+int sa_group_ingest(sa_group *g, const sa_span_batch *b) {
+  if (!g || !b) return SA_EINVAL;
+  const uint32_t n = (uint32_t)g->eng.size();
+  if (n == 1 || b->n == 0) {
+    const int rc = sa_ingest(g->eng[0], b);
+    return rc ? member_error(g, 0, rc, "sa_ingest") : SA_OK;
+  }
+  if (!b->key_hash || !b->start_ns || !b->end_ns || !b->trace_w0 || !b->trace_w1 || !b->meta)
+    return gfail(g, SA_EINVAL, "null batch column");
+  // one host thread per member: it scans the batch for its trace-id shard
+  // (trace_w1 % n), packs the shard's columns and ingests them
+  std::vector<int> rcs(n, SA_OK);
+  std::vector<std::thread> th;
+  for (uint32_t i = 0; i < n; ++i) {
+    th.emplace_back([&, i]() {
+      std::vector<uint64_t> k, s, e, a, c;
+      std::vector<uint32_t> m;
+      const size_t guess = b->n / n + b->n / (4 * n) + 64;
+      k.reserve(guess), s.reserve(guess), e.reserve(guess), a.reserve(guess), c.reserve(guess), m.reserve(guess);
+      for (uint64_t j = 0; j < b->n; ++j) {
+        if (b->trace_w1[j] % n != i) continue;
+        k.push_back(b->key_hash[j]);
+        s.push_back(b->start_ns[j]);
+        e.push_back(b->end_ns[j]);
+        a.push_back(b->trace_w0[j]);
+        c.push_back(b->trace_w1[j]);
+        m.push_back(b->meta[j]);
+      }
+      const sa_span_batch sh{k.data(), s.data(), e.data(), a.data(), c.data(), m.data(), k.size()};
+      rcs[i] = sh.n ? sa_ingest(g->eng[i], &sh) : SA_OK;
+    });
+  }
+  for (auto &t : th) t.join();
+  for (uint32_t i = 0; i < n; ++i)
+    if (rcs[i] != SA_OK) return member_error(g, i, rcs[i], "sa_ingest");
+  return SA_OK;
+}
+
+int sa_group_sync(sa_group *g) {
+  if (!g) return SA_EINVAL;
+  for (uint32_t i = 0; i < g->eng.size(); ++i)
+    if (int rc = sa_sync(g->eng[i])) return member_error(g, i, rc, "sa_sync");
+  return SA_OK;
+}
+
+int sa_group_flush(sa_group *g, sa_red_result **out) {
+  if (!g || !out) return SA_EINVAL;
+  *out = nullptr;
+  const uint32_t n = (uint32_t)g->eng.size(), stride = g->nbk + 1;
+  // 1. each member's non-zero series ids (and its drop counter)
+  std::vector<uint64_t> cnt(n, 0), dropped(n, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    sa_stats s;
+    if (int rc = sa_get_stats(g->eng[i], &s)) return member_error(g, i, rc, "sa_get_stats");
+    dropped[i] = s.dropped_table_full;
+    if (int rc = ensure(g, g->dev[i], g->keys[i], s.table_capacity * 8)) return rc;
+    if (int rc = sa_export_keys(g->eng[i], static_cast<uint64_t *>(g->keys[i].p), s.table_capacity, &cnt[i], g->st[i]))
+      return member_error(g, i, rc, "sa_export_keys");
+  }
+  // 2. the sorted key union (the dense index every member densifies against)
+  std::vector<uint64_t> all;
+  if (g->rccl) {
+    const uint64_t nmax = *std::max_element(cnt.begin(), cnt.end());
+    if (nmax) {
+      for (uint32_t i = 0; i < n; ++i) {
+        SG_HIP(g, hipSetDevice(g->dev[i]));
+        if (cnt[i] < nmax)  // pad with 0, the reserved id
+          SG_HIP(g, hipMemsetAsync(static_cast<uint64_t *>(g->keys[i].p) + cnt[i], 0, (nmax - cnt[i]) * 8, g->st[i]));
+        if (int rc = ensure(g, g->dev[i], g->gath[i], nmax * n * 8)) return rc;
+      }
+      SG_NCCL(g, ncclGroupStart());
+      for (uint32_t i = 0; i < n; ++i)
+        SG_NCCL(g, ncclAllGather(g->keys[i].p, g->gath[i].p, nmax, ncclUint64, g->comm[i], g->st[i]));
+      SG_NCCL(g, ncclGroupEnd());
+      all.resize(nmax * n);
+      SG_HIP(g, hipSetDevice(g->dev[0]));
+      SG_HIP(g, hipMemcpyAsync(all.data(), g->gath[0].p, all.size() * 8, hipMemcpyDeviceToHost, g->st[0]));
+      SG_HIP(g, hipStreamSynchronize(g->st[0]));
+    }
+  } else {
+    for (uint32_t i = 0; i < n; ++i) {
+      if (!cnt[i]) continue;
+      const size_t at = all.size();
+      all.resize(at + cnt[i]);
+      SG_HIP(g, hipSetDevice(g->dev[i]));
+      SG_HIP(g, hipMemcpy(all.data() + at, g->keys[i].p, cnt[i] * 8, hipMemcpyDeviceToHost));
+    }
+  }
+  all.erase(std::remove(all.begin(), all.end(), 0ULL), all.end());
+  std::sort(all.begin(), all.end());
+  all.erase(std::unique(all.begin(), all.end()), all.end());
+  const uint64_t nu = all.size(), len = nu * stride;
+  // 3. dense rows per member (and its counters reset), 4. their sum
+  std::vector<uint64_t> merged(len);
+  if (nu) {
+    for (uint32_t i = 0; i < n; ++i) {
+      if (int rc = ensure(g, g->dev[i], g->uni[i], nu * 8)) return rc;
+      if (int rc = ensure(g, g->dev[i], g->rows[i], len * 8)) return rc;
+      SG_HIP(g, hipSetDevice(g->dev[i]));
+      SG_HIP(g, hipMemcpyAsync(g->uni[i].p, all.data(), nu * 8, hipMemcpyHostToDevice, g->st[i]));
+      if (int rc = sa_gather_dense(g->eng[i], static_cast<const uint64_t *>(g->uni[i].p), nu,
+                                   static_cast<uint64_t *>(g->rows[i].p), 1, g->st[i]))
+        return member_error(g, i, rc, "sa_gather_dense");
+    }
+    if (g->rccl) {
+      SG_NCCL(g, ncclGroupStart());
+      for (uint32_t i = 0; i < n; ++i)
+        SG_NCCL(g, ncclAllReduce(g->rows[i].p, g->rows[i].p, len, ncclUint64, ncclSum, g->comm[i], g->st[i]));
+      SG_NCCL(g, ncclGroupEnd());
+    } else if (int rc = copy_reduce(g, g->rows, len, false)) {
+      return rc;
+    }
+    SG_HIP(g, hipSetDevice(g->dev[0]));
+    SG_HIP(g, hipMemcpyAsync(merged.data(), g->rows[0].p, len * 8, hipMemcpyDeviceToHost, g->st[0]));
+    SG_HIP(g, hipStreamSynchronize(g->st[0]));
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    SG_HIP(g, hipSetDevice(g->dev[i]));
+    SG_HIP(g, hipStreamSynchronize(g->st[i]));
+  }
+  // 5. the result, in key order (the union is sorted)
+  auto *h = new red_holder();
+  h->keys = all;
+  h->counts.resize(nu * g->nbk);
+  h->calls.resize(nu);
+  h->sum_ns.resize(nu);
+  h->sum.resize(nu);
+  const double div = g->cfg.unit == SA_UNIT_S ? 1e9 : 1e6;
+  for (uint64_t r = 0; r < nu; ++r) {
+    uint64_t c = 0;
+    for (uint32_t b = 0; b < g->nbk; ++b) {
+      h->counts[r * g->nbk + b] = merged[r * stride + b];
+      c += merged[r * stride + b];
+    }
+    h->calls[r] = c;
+    h->sum_ns[r] = merged[r * stride + g->nbk];
+    h->sum[r] = (double)h->sum_ns[r] / div;
+  }
+  h->r.n_series = nu;
+  h->r.n_buckets = g->nbk;
+  h->r.key_hash = h->keys.data();
+  h->r.bucket_counts = h->counts.data();
+  h->r.calls = h->calls.data();
+  h->r.sum_ns = h->sum_ns.data();
+  h->r.sum = h->sum.data();
+  *out = &h->r;
+  bool full = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    full = full || dropped[i] != g->dropped_seen[i];
+    g->dropped_seen[i] = dropped[i];
+  }
+  return full ? gfail(g, SA_EFULL, "key table full: spans were dropped since the previous flush") : SA_OK;
+}
+
+int sa_group_window_read(sa_group *g, uint64_t window_id, sa_sketch_result **out) {
+  if (!g || !out) return SA_EINVAL;
+  *out = nullptr;
+  const uint32_t n = (uint32_t)g->eng.size();
+  for (uint32_t i = 0; i < n; ++i) {
+    if (int rc = ensure(g, g->dev[i], g->hll[i], g->hll_bytes)) return rc;
+    if (int rc = ensure(g, g->dev[i], g->cms[i], g->cms_elems * 8)) return rc;
+    if (int rc = sa_window_export(g->eng[i], window_id, static_cast<uint8_t *>(g->hll[i].p),
+                                  static_cast<uint64_t *>(g->cms[i].p), g->st[i]))
+      return member_error(g, i, rc, "sa_window_export");
+  }
+  if (g->rccl) {
+    SG_NCCL(g, ncclGroupStart());
+    for (uint32_t i = 0; i < n; ++i) {
+      SG_NCCL(g, ncclAllReduce(g->hll[i].p, g->hll[i].p, g->hll_bytes, ncclUint8, ncclMax, g->comm[i], g->st[i]));
+      SG_NCCL(g, ncclAllReduce(g->cms[i].p, g->cms[i].p, g->cms_elems, ncclUint64, ncclSum, g->comm[i], g->st[i]));
+    }
+    SG_NCCL(g, ncclGroupEnd());
+  } else {
+    if (int rc = copy_reduce(g, g->hll, g->hll_bytes, true)) return rc;
+    if (int rc = copy_reduce(g, g->cms, g->cms_elems, false)) return rc;
+  }
+  auto *h = new sketch_holder();
+  h->hll.resize(g->hll_bytes);
+  std::vector<uint64_t> c64(g->cms_elems);
+  (void)hipSetDevice(g->dev[0]);
+  hipError_t a = hipMemcpyAsync(h->hll.data(), g->hll[0].p, g->hll_bytes, hipMemcpyDeviceToHost, g->st[0]);
+  hipError_t b = hipMemcpyAsync(c64.data(), g->cms[0].p, g->cms_elems * 8, hipMemcpyDeviceToHost, g->st[0]);
+  hipError_t c = hipStreamSynchronize(g->st[0]);
+  for (uint32_t i = 1; i < n && c == hipSuccess; ++i) {
+    (void)hipSetDevice(g->dev[i]);
+    c = hipStreamSynchronize(g->st[i]);
+  }
+  if (a != hipSuccess || b != hipSuccess || c != hipSuccess) {
+    delete h;
+    return gfail(g, SA_EDEVICE, "group window read failed");
+  }
+  h->cms.resize(g->cms_elems);
+  for (size_t i = 0; i < c64.size(); ++i) h->cms[i] = c64[i] > UINT32_MAX ? UINT32_MAX : (uint32_t)c64[i];
+  h->r.window_id = window_id;
+  h->r.n_services = g->cfg.n_services;
+  h->r.hll_p = g->cfg.hll_p;
+  h->r.hll = h->hll.data();
+  h->r.cms_d = g->cfg.cms_d;
+  h->r.cms_w = g->cfg.cms_w;
+  h->r.cms = h->cms.data();
+  *out = &h->r;
+  return SA_OK;
+}
+
+int sa_group_window_advance(sa_group *g, uint64_t new_base) {
+  if (!g) return SA_EINVAL;
+  for (uint32_t i = 0; i < g->eng.size(); ++i)
+    if (int rc = sa_window_advance(g->eng[i], new_base)) return member_error(g, i, rc, "sa_window_advance");
+  return SA_OK;
+}
+
+int sa_group_get_stats(sa_group *g, sa_stats *o) {
+  if (!g || !o) return SA_EINVAL;
+  std::memset(o, 0, sizeof *o);
+  for (uint32_t i = 0; i < g->eng.size(); ++i) {
+    sa_stats s;
+    if (int rc = sa_get_stats(g->eng[i], &s)) return member_error(g, i, rc, "sa_get_stats");
+    o->spans += s.spans;
+    o->zero_key += s.zero_key;
+    o->invalid_service += s.invalid_service;
+    o->window_out_of_range += s.window_out_of_range;
+    o->dropped_table_full += s.dropped_table_full;
+    o->n_keys += s.n_keys;
+    o->table_capacity += s.table_capacity;
+    if (i == 0) {
+      o->window_base = s.window_base;
+      o->small_table = s.small_table;
+    }
+  }
+  return SA_OK;
+}
+
+}  // extern "C"

@@ -87,6 +87,19 @@ SIGNATURES = [
     ("sa_export_keys", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, u64p, C.c_void_p]),
     ("sa_gather_dense", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int, C.c_void_p]),
     ("sa_window_export", C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("sa_group_create", C.c_int, [C.POINTER(sa_config), C.POINTER(C.c_int32), C.c_uint32,
+                                  C.POINTER(C.c_void_p)]),
+    ("sa_group_destroy", None, [C.c_void_p]),
+    ("sa_group_last_error", C.c_char_p, [C.c_void_p]),
+    ("sa_group_size", C.c_uint32, [C.c_void_p]),
+    ("sa_group_uses_rccl", C.c_int, [C.c_void_p]),
+    ("sa_group_member", C.c_void_p, [C.c_void_p, C.c_uint32]),
+    ("sa_group_ingest", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch)]),
+    ("sa_group_sync", C.c_int, [C.c_void_p]),
+    ("sa_group_flush", C.c_int, [C.c_void_p, C.POINTER(C.POINTER(sa_red_result))]),
+    ("sa_group_window_read", C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.POINTER(sa_sketch_result))]),
+    ("sa_group_window_advance", C.c_int, [C.c_void_p, C.c_uint64]),
+    ("sa_group_get_stats", C.c_int, [C.c_void_p, C.POINTER(sa_stats)]),
     ("sa_debug_stamps", C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p]),
     ("sa_bucket_thresholds", C.c_int, [f64p, C.c_uint32, C.c_uint32, u64p, u32p]),
     ("sa_hll_estimate", C.c_double, [u8p, C.c_uint32]),

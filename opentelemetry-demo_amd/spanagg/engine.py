@@ -136,6 +136,40 @@ def bucket_thresholds(bounds, unit: str = "ms"):
     return thr[: len(b) - nneg.value], nneg.value
 
 
+def _red_result(owner, rc: int, out, allow_drops: bool, what: str, _fn=None) -> RedResult:
+    """Copies an sa_red_result into numpy arrays and frees it."""
+    lib = owner.lib
+    if rc not in (0, _lib.SA_EFULL) or not out:
+        owner._check(rc if rc else _lib.SA_ESTATE, what)
+    try:
+        r = out.contents
+        n, nb = int(r.n_series), int(r.n_buckets)
+
+        def arr(p, shape, dt):
+            if n == 0:
+                return np.zeros(shape, dtype=dt)
+            return np.ctypeslib.as_array(p, shape=shape).copy()
+
+        res = RedResult(arr(r.key_hash, (n,), np.uint64), arr(r.bucket_counts, (n, nb), np.uint64),
+                        arr(r.calls, (n,), np.uint64), arr(r.sum_ns, (n,), np.uint64),
+                        arr(r.sum, (n,), np.float64), rc)
+    finally:
+        lib.sa_red_result_free(out)
+    if rc == _lib.SA_EFULL and not allow_drops:
+        raise SpanAggError(rc, f"{what}: spans dropped (key table full); stats={owner.stats()}")
+    return res
+
+
+def _sketch_result(lib, out) -> SketchResult:
+    try:
+        r = out.contents
+        hll = np.ctypeslib.as_array(r.hll, shape=(r.n_services, 1 << r.hll_p)).copy()
+        cms = np.ctypeslib.as_array(r.cms, shape=(r.cms_d, r.cms_w)).copy()
+        return SketchResult(int(r.window_id), hll, cms, int(r.hll_p))
+    finally:
+        lib.sa_sketch_result_free(out)
+
+
 def _ptr(x) -> int:
     """Device pointer of a torch tensor, or an int passthrough."""
     if isinstance(x, int):
@@ -199,37 +233,12 @@ class Engine:
     def flush(self, allow_drops: bool = False) -> RedResult:
         out = C.POINTER(_lib.sa_red_result)()
         rc = self.lib.sa_flush(self._h, C.byref(out))
-        if rc not in (0, _lib.SA_EFULL) or not out:
-            self._check(rc, "sa_flush")
-        try:
-            r = out.contents
-            n, nb = int(r.n_series), int(r.n_buckets)
-
-            def arr(p, shape, dt):
-                if n == 0:
-                    return np.zeros(shape, dtype=dt)
-                return np.ctypeslib.as_array(p, shape=shape).copy()
-
-            res = RedResult(arr(r.key_hash, (n,), np.uint64),
-                            arr(r.bucket_counts, (n, nb), np.uint64),
-                            arr(r.calls, (n,), np.uint64), arr(r.sum_ns, (n,), np.uint64),
-                            arr(r.sum, (n,), np.float64), rc)
-        finally:
-            self.lib.sa_red_result_free(out)
-        if rc == _lib.SA_EFULL and not allow_drops:
-            raise SpanAggError(rc, f"sa_flush: spans dropped (key table full); stats={self.stats()}")
-        return res
+        return _red_result(self, rc, out, allow_drops, "sa_flush", self.lib.sa_flush)
 
     def window_read(self, window_id: int) -> SketchResult:
         out = C.POINTER(_lib.sa_sketch_result)()
         self._check(self.lib.sa_window_read(self._h, window_id, C.byref(out)), "sa_window_read")
-        try:
-            r = out.contents
-            hll = np.ctypeslib.as_array(r.hll, shape=(r.n_services, 1 << r.hll_p)).copy()
-            cms = np.ctypeslib.as_array(r.cms, shape=(r.cms_d, r.cms_w)).copy()
-            return SketchResult(int(r.window_id), hll, cms, int(r.hll_p))
-        finally:
-            self.lib.sa_sketch_result_free(out)
+        return _sketch_result(self.lib, out)
 
     def window_advance(self, new_base: int):
         self._check(self.lib.sa_window_advance(self._h, int(new_base)), "sa_window_advance")
@@ -255,3 +264,75 @@ class Engine:
         self._check(self.lib.sa_window_export(self._h, window_id, C.c_void_p(_ptr(d_hll)),
                                               C.c_void_p(_ptr(d_cms)), C.c_void_p(stream or 0)),
                     "sa_window_export")
+
+
+class Group:
+    """One engine per GPU behind one handle (include/spanagg.h sa_group_*):
+    host batches shard by trace id (trace_w1 % n), flush and window reads
+    return the merge (RCCL over distinct devices, device copies otherwise)."""
+
+    def __init__(self, devices: Sequence[int], config: Optional[Config] = None, **kw):
+        self.lib = _lib.load()
+        self.config = config or Config(**kw)
+        c, self._bounds_keepalive = self.config.to_c()
+        devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+        h = C.c_void_p()
+        rc = self.lib.sa_group_create(C.byref(c), devs, len(devices), C.byref(h))
+        if rc != 0:
+            raise SpanAggError(rc, "sa_group_create failed (are the gfx950 GPUs visible?)")
+        self._h = h
+        self.n_buckets = len(self.config.bounds) + 1
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.sa_group_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str):
+        if rc != 0:
+            raise SpanAggError(rc, f"{what}: {self.lib.sa_group_last_error(self._h).decode()}")
+
+    @property
+    def size(self) -> int:
+        return int(self.lib.sa_group_size(self._h))
+
+    @property
+    def uses_rccl(self) -> bool:
+        return bool(self.lib.sa_group_uses_rccl(self._h))
+
+    def ingest(self, batch: SpanBatch):
+        b = _lib.sa_span_batch(*[c.ctypes.data for c in batch.columns()], len(batch))
+        self._check(self.lib.sa_group_ingest(self._h, C.byref(b)), "sa_group_ingest")
+
+    def sync(self):
+        self._check(self.lib.sa_group_sync(self._h), "sa_group_sync")
+
+    def flush(self, allow_drops: bool = False) -> RedResult:
+        out = C.POINTER(_lib.sa_red_result)()
+        rc = self.lib.sa_group_flush(self._h, C.byref(out))
+        return _red_result(self, rc, out, allow_drops, "sa_group_flush")
+
+    def window_read(self, window_id: int) -> SketchResult:
+        out = C.POINTER(_lib.sa_sketch_result)()
+        self._check(self.lib.sa_group_window_read(self._h, window_id, C.byref(out)), "sa_group_window_read")
+        return _sketch_result(self.lib, out)
+
+    def window_advance(self, new_base: int):
+        self._check(self.lib.sa_group_window_advance(self._h, int(new_base)), "sa_group_window_advance")
+
+    def stats(self) -> dict:
+        s = _lib.sa_stats()
+        self._check(self.lib.sa_group_get_stats(self._h, C.byref(s)), "sa_group_get_stats")
+        return {name: int(getattr(s, name)) for name, _ in _lib.sa_stats._fields_ if name != "pad"}

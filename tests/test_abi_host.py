@@ -108,3 +108,15 @@ def test_engine_rejects_bad_config():
     assert ei.value.code == _lib.SA_EINVAL
     with pytest.raises(_lib.SpanAggError):
         Engine(Config(bounds=(5, 1)))
+
+
+def test_group_fails_loudly_without_gpu(has_gpu):
+    from spanagg import Group
+    if has_gpu:
+        pytest.skip("GPU present")
+    with pytest.raises(_lib.SpanAggError) as ei:
+        Group([0, 0], Config())
+    assert ei.value.code == _lib.SA_EDEVICE
+    with pytest.raises(_lib.SpanAggError) as ei:
+        Group([], Config())
+    assert ei.value.code == _lib.SA_EINVAL

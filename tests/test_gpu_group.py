@@ -1,0 +1,83 @@
+"""Engine groups (include/spanagg.h sa_group_*): several engines behind one
+handle, spans sharded by trace id, merged at flush / window read.  On the
+one-GPU lease both transports run: two members on device 0 merge through
+device copies + a reduce kernel, a group of one with SPANAGG_GROUP_RCCL=1
+merges over a one-rank RCCL communicator.  Bar: the merge equals the CPU
+oracle fed the whole stream (bucket counts, calls, ns sums, HLL registers and
+count-min cells bit-exact; duration sums within 1e-9 relative)."""
+import numpy as np
+import pytest
+
+import pyoracle
+from parity_util import assert_red_equal
+from spanagg import Config, Engine, Group
+from spanagg.synth import generate_c2, generate_highcard
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_windows(g, o):
+    for wid in o.window_ids():
+        sk = g.window_read(wid)
+        hll, cms = o.window(wid)
+        assert np.array_equal(sk.hll, hll), wid
+        assert np.array_equal(sk.cms, cms), wid
+
+
+@pytest.mark.parametrize("devices,rccl", [([0, 0], "0"), ([0, 0, 0], "0"), ([0], "1")])
+def test_group_matches_oracle_c2(devices, rccl, monkeypatch):
+    monkeypatch.setenv("SPANAGG_GROUP_RCCL", rccl)
+    wl = generate_c2(400_003, seed=21)
+    with Group(devices, Config(n_services=wl.n_services, n_windows=16)) as g:
+        assert g.size == len(devices)
+        assert g.uses_rccl == (rccl == "1")
+        g.window_advance(wl.first_window)
+        g.ingest(wl.batch)
+        res = g.flush()
+        o = pyoracle.Oracle(n_services=wl.n_services)
+        o.ingest(wl.batch)
+        assert_red_equal(res, o.series())
+        _check_windows(g, o)
+        st = g.stats()
+        assert st["spans"] == len(wl.batch)
+        # every member saw only its own shard
+        assert st["n_keys"] >= len(res.key_hash)
+
+
+def test_group_delta_flushes_and_equals_one_engine(monkeypatch):
+    monkeypatch.setenv("SPANAGG_GROUP_RCCL", "0")
+    wl = generate_c2(300_000, seed=5)
+    a, b = wl.batch.slice(0, 170_000), wl.batch.slice(170_000, 300_000)
+    cfg = Config(n_services=wl.n_services, n_windows=16)
+    with Group([0, 0], cfg) as g, Engine(cfg) as e:
+        for x in (g, e):
+            x.window_advance(wl.first_window)
+        for part in (a, b):
+            g.ingest(part)
+            e.ingest(part)
+            rg, re_ = g.flush(), e.flush()
+            assert np.array_equal(rg.key_hash, re_.key_hash)
+            assert np.array_equal(rg.bucket_counts, re_.bucket_counts)
+            assert np.array_equal(rg.sum_ns, re_.sum_ns)
+        empty = g.flush()  # nothing since the last flush
+        assert len(empty.key_hash) == 0
+
+
+def test_group_high_cardinality_binned_members(monkeypatch):
+    """Members on the binned HBM-table path (1 M keys): the key union spans
+    series seen by one member only and by both."""
+    monkeypatch.setenv("SPANAGG_GROUP_RCCL", "0")
+    batch, _, first = generate_highcard(1_500_000, seed=3)
+    with Group([0, 0], Config(n_services=1, n_windows=16, key_capacity=1_200_000)) as g:
+        g.window_advance(first)
+        g.ingest(batch)
+        res = g.flush()
+        o = pyoracle.Oracle(n_services=1)
+        o.ingest(batch)
+        assert_red_equal(res, o.series())
+        _check_windows(g, o)
+
+
+def test_group_rejects_bad_arguments():
+    with pytest.raises(Exception):
+        Group([], Config())

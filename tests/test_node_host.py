@@ -330,14 +330,21 @@ def synth_requests(seed, n_requests=12, per_request=2500):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("native", [True, False], ids=["native-columnizer", "js-columnizer"])
-def test_node_host_end_to_end_matches_oracle(native):
+@pytest.mark.parametrize("native,devices", [(True, None), (False, None), (True, [0, 0]), (False, [0, 0])],
+                         ids=["native-columnizer", "js-columnizer", "native-group2", "js-group2"])
+def test_node_host_end_to_end_matches_oracle(native, devices):
+    """devices=[0, 0]: the connector drives an engine group (two engines on the
+    lease's one GPU, spans sharded by trace id, merged through device copies
+    at every flush and window read) through the same N-API calls."""
     import pyoracle
     from spanagg.engine import SpanBatch
 
     requests, facts = synth_requests(seed=11)
     env = dict(os.environ, SPANAGG_NODE_GPU="1")
-    out = node("e2e.js", {"requests": requests, "config": {"batch_size": 4096, "key_capacity": 4096},
+    config = {"batch_size": 4096, "key_capacity": 4096}
+    if devices:
+        config["devices"] = devices
+    out = node("e2e.js", {"requests": requests, "config": config,
                           "exports_after": [3, 7], "native": native}, timeout=300, env=env)
     n = len(facts)
 
@@ -422,6 +429,7 @@ def test_node_host_end_to_end_matches_oracle(native):
             assert not hll.any() and not cms.any()
     st = out["stats"]
     assert int(st["spans"]) == n and int(st["windowOutOfRange"]) == 0 and int(st["droppedTableFull"]) == 0
+    assert int(st["engines"]) == (len(devices) if devices else 1)
 
 
 def test_receiver_interoperates_with_grpcio_and_http_clients():
