@@ -537,12 +537,29 @@ uint32_t Columnizer::service_id(const std::string &name, bool *is_new) {
   return id;
 }
 
+void Columnizer::learn(uint64_t rhash, const std::string &key, uint64_t sid) {
+  res_keys_[rhash][key] = sid;
+  owner_[sid] = std::make_pair(rhash, key);
+}
+
+void Columnizer::remap(uint64_t from, uint64_t to) {
+  for (uint64_t &k : key_)
+    if (k == from) k = to;
+  auto o = owner_.find(from);
+  if (o == owner_.end()) return;
+  const auto who = o->second;
+  owner_.erase(o);
+  owner_[to] = who;
+  res_keys_[who.first][who.second] = to;
+}
+
 Result Columnizer::columnize(const uint8_t *buf, size_t len) {
   Result res;
   const size_t n0 = key_.size();
   const uint64_t max0 = max_end_;
   // dictionary entries made by this call: committed only on success
   std::vector<std::pair<uint64_t, std::string>> added_keys;
+  std::vector<uint64_t> added_sids;
   std::vector<std::string> added_services;
   std::vector<uint64_t> added_resources;
 
@@ -554,6 +571,7 @@ Result Columnizer::columnize(const uint8_t *buf, size_t len) {
       if (it != res_keys_.end()) it->second.erase(k.second);
     }
     for (uint64_t h : added_resources) res_keys_.erase(h);
+    for (uint64_t sid : added_sids) owner_.erase(sid);
     for (auto &s : added_services) services_.erase(s);
     Result r;
     r.status = st;
@@ -745,8 +763,18 @@ Result Columnizer::columnize(const uint8_t *buf, size_t len) {
           hbuf.resize(8 + keystr.size());
           std::memcpy(hbuf.data(), &rhash, 8);
           std::memcpy(hbuf.data() + 8, keystr.data(), keystr.size());
-          sid = xxh64(hbuf.data(), hbuf.size(), 0);
-          if (sid == 0) sid = xxh64(hbuf.data(), hbuf.size(), 1);
+          // seed 0, 1, ... until the id is neither 0 (reserved) nor another series'
+          for (uint64_t seed = 0;; ++seed) {
+            sid = (opt_.test_collide_seed0 && seed == 0) ? 42 : xxh64(hbuf.data(), hbuf.size(), seed);
+            if (sid == 0) continue;
+            auto o = owner_.find(sid);
+            if (o == owner_.end()) {
+              owner_.emplace(sid, std::make_pair(rhash, keystr));
+              added_sids.push_back(sid);
+              break;
+            }
+            if (o->second.first == rhash && o->second.second == keystr) break;
+          }
           keys.emplace(keystr, sid);
           added_keys.emplace_back(rhash, keystr);
           res.new_series.push_back({sid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});

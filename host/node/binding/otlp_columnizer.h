@@ -44,6 +44,7 @@ struct Options {
   bool ex_service = false, ex_name = false, ex_kind = false, ex_status = false;
   std::vector<Rule> rules;
   std::vector<std::string> key_attributes;  // resource_metrics_key_attributes (empty = all)
+  bool test_collide_seed0 = false;          // tests only: every seed-0 series id is 42
 };
 
 struct NewSeries {
@@ -76,6 +77,11 @@ class Columnizer {
 
   uint32_t service_id(const std::string &name, bool *is_new);
   void forget_resource(uint64_t hash) { res_keys_.erase(hash); }
+  // the host interned (resource, key) as `sid` (a series its JavaScript path saw first)
+  void learn(uint64_t rhash, const std::string &key, uint64_t sid);
+  // the host's id for a series this columnizer reported as `from` is `to`:
+  // buffered spans and the dictionary follow (the host's dictionary decides)
+  void remap(uint64_t from, uint64_t to);
   void clear_buffer() {
     key_.clear(); start_.clear(); end_.clear(); w0_.clear(); w1_.clear(); meta_.clear();
     max_end_ = 0;
@@ -97,6 +103,10 @@ class Columnizer {
   uint64_t max_end_ = 0;
   std::unordered_map<std::string, uint32_t> services_;
   std::unordered_map<uint64_t, std::unordered_map<std::string, uint64_t>> res_keys_;
+  // every id handed out -> its (resource, key): an id held by another series
+  // is re-salted (seed + 1) instead of shared; kept after a resource is
+  // forgotten, so the same series gets the same id when it comes back
+  std::unordered_map<uint64_t, std::pair<uint64_t, std::string>> owner_;
 };
 
 // exposed for tests of the building blocks

@@ -650,6 +650,12 @@ napi_value CreateColumnizer(napi_env env, napi_callback_info info) {
     if (!get_string(env, x, &k, "keyAttributes[]")) return nullptr;
     o.key_attributes.push_back(std::move(k));
   }
+  {
+    napi_value tc = prop(env, argv[1], "testCollideSeed0");
+    bool b = false;
+    if (!is_undefined(env, tc)) napi_get_value_bool(env, tc, &b);
+    o.test_collide_seed0 = b;
+  }
   auto *c = new ColHandle(std::move(o));
   c->engine = static_cast<Handle *>(hp);
   napi_value obj;
@@ -768,6 +774,32 @@ napi_value ColumnizerServiceId(napi_env env, napi_callback_info info) {
   return arr;
 }
 
+// columnizerLearn(c, resHash, keyBytes, sid): a series the host interned itself
+napi_value ColumnizerLearn(napi_env env, napi_callback_info info) {
+  napi_value argv[4];
+  if (!get_args(env, info, 4, argv)) return throw_napi(env, "args");
+  ColHandle *c = get_col(env, argv[0]);
+  uint64_t rh, sid;
+  void *d;
+  size_t n;
+  if (!c || !to_u64(env, argv[1], &rh, "resHash") || !typed(env, argv[2], napi_uint8_array, &d, &n, "key") ||
+      !to_u64(env, argv[3], &sid, "sid"))
+    return nullptr;
+  c->col.learn(rh, std::string(static_cast<const char *>(d), n), sid);
+  return nullptr;
+}
+
+// columnizerRemap(c, from, to): the host's id for a reported series differs
+napi_value ColumnizerRemap(napi_env env, napi_callback_info info) {
+  napi_value argv[3];
+  if (!get_args(env, info, 3, argv)) return throw_napi(env, "args");
+  ColHandle *c = get_col(env, argv[0]);
+  uint64_t from, to;
+  if (!c || !to_u64(env, argv[1], &from, "from") || !to_u64(env, argv[2], &to, "to")) return nullptr;
+  c->col.remap(from, to);
+  return nullptr;
+}
+
 napi_value ColumnizerForget(napi_env env, napi_callback_info info) {
   napi_value argv[2];
   if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
@@ -825,6 +857,8 @@ napi_value Init(napi_env env, napi_value exports) {
                {"columnizerTake", ColumnizerTake},
                {"columnizerServiceId", ColumnizerServiceId},
                {"columnizerForget", ColumnizerForget},
+               {"columnizerLearn", ColumnizerLearn},
+               {"columnizerRemap", ColumnizerRemap},
                {"columnizerSelfTest", ColumnizerSelfTest}};
     for (auto &f : fns) {
         napi_value v;

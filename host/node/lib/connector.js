@@ -186,6 +186,8 @@ class SpanMetricsConnector {
     this.sketchWatermark = 0n;
     this.closedWindows = [];
     this.droppedFlushes = 0;
+    this.collisions = 0;          // series ids re-salted after a 64-bit collision
+    this._verifyingNative = false;
     this.eventRecords = 0;
     this.ticker = null;
   }
@@ -270,10 +272,17 @@ class SpanMetricsConnector {
     let sid = res.byKey.get(keyStr);
     if (sid !== undefined) return sid;
     const keyBuf = Buffer.from(keyStr, 'utf8');
-    sid = keys.seriesHash(res.hash, keyBuf);
+    // a 64-bit collision with another series is re-salted (ConsumeTraces never fails)
+    let seed;
+    [sid, seed] = keys.assignSeriesId(res.hash, keyBuf, (h) => {
+      const s = this.series.get(h);
+      return s === undefined ? undefined : s.res.hash === res.hash && s.keyStr === keyStr;
+    });
+    if (seed > 0n) this.collisions += 1;
     const cur = this.series.get(sid);
-    if (cur !== undefined && (cur.res.hash !== res.hash || cur.keyStr !== keyStr)) {
-      throw new Error('64-bit series id collision; re-salt required');
+    // the native columnizer learns series the JavaScript path saw first
+    if (cur === undefined && this.col && !this._verifyingNative) {
+      this.addon.columnizerLearn(this.col, res.hash, keyBuf, sid);
     }
     if (cur === undefined) {
       this.series.set(sid, { sid, res, keyStr, dpAttrs: mkAttrs(), status, kind,
@@ -400,8 +409,16 @@ class SpanMetricsConnector {
       const svc = res.attributes.get(keys.SERVICE_NAME_KEY);
       const service = svc && svc.type === 'string' ? svc.value : '';
       const spanAttrs = this.cfg.dims.length ? keys.attrMap(span.attributes) : undefined;
-      const sid = this._seriesId(res, service, span, res.attributes, spanAttrs);
-      if (sid !== ns.sid) throw new Error('native/JS series id mismatch');
+      this._verifyingNative = true;
+      let sid;
+      try {
+        sid = this._seriesId(res, service, span, res.attributes, spanAttrs);
+      } finally {
+        this._verifyingNative = false;
+      }
+      // the host dictionary decides: after a collision the two sides can differ
+      // (the native side does not see series interned by a JavaScript-path request)
+      if (sid !== ns.sid) this.addon.columnizerRemap(this.col, ns.sid, sid);
     }
     if (r.spans) {
       if (r.maxEnd > this.nativeMaxEnd) this.nativeMaxEnd = r.maxEnd;
@@ -622,7 +639,7 @@ class SpanMetricsConnector {
   stats() {
     const s = this.addon.stats(this.handle);
     return Object.assign(s, { resources: this.resources.size, series: this.series.size,
-      services: this.services.size, droppedFlushes: this.droppedFlushes,
+      services: this.services.size, droppedFlushes: this.droppedFlushes, collisions: this.collisions,
       eventRecords: this.eventRecords, nativeRequests: this.nativeRequests, jsRequests: this.jsRequests });
   }
 }

@@ -143,31 +143,53 @@ function resourceHash(resourceAttrs) {
   return xxh64(Buffer.concat(chunks), 0n);
 }
 
-/** Device series id = xxh64(resource hash LE || key); 0 is reserved -> re-salted (seed 1). */
-function seriesHash(resHash, key) {
+/** xxh64(resource hash LE || key) with one seed. */
+function seriesHashSeeded(resHash, key, seed) {
   const b = Buffer.alloc(8 + key.length);
   b.writeBigUInt64LE(resHash, 0);
   key.copy(b, 8);
-  let h = xxh64(b, 0n);
-  if (h === 0n) h = xxh64(b, 1n);
-  return h;
+  return xxh64(b, seed);
+}
+
+/**
+ * Device series id of (resource, key): xxh64 with seed 0, 1, 2, ... until the
+ * id is neither 0 (reserved by the engine) nor held by another series (a
+ * 64-bit collision is re-salted, never shared).  owner(id) -> undefined
+ * (free), true (this series already) or false (another series).  Returns
+ * [id, seed].  Looks the hash up through module.exports so tests can force
+ * collisions.
+ */
+function assignSeriesId(resHash, key, owner) {
+  for (let seed = 0n; ; seed += 1n) {
+    const h = module.exports.seriesHashSeeded(resHash, key, seed);
+    if (h === 0n) continue;
+    if (owner(h) !== false) return [h, seed];
+  }
+}
+
+/** The id of a series with nothing else interned: seed 0 (seed 1 if that is 0). */
+function seriesHash(resHash, key) {
+  return assignSeriesId(resHash, key, () => undefined)[0];
 }
 
 /**
  * Series id -> {resHash, key, resourceAttrs, dpAttrs}; the first span seen
- * for an id fixes its datapoint attributes (A5/A6).  Distinct (resource, key)
- * with one id is a 64-bit collision and throws.
+ * for an id fixes its datapoint attributes (A5/A6).  A distinct (resource,
+ * key) whose id is taken is re-salted (counted in `collisions`).
  */
 class KeyDictionary {
-  constructor() { this.byId = new Map(); this.collisions = 0; }
+  constructor() { this.byId = new Map(); this.byKey = new Map(); this.collisions = 0; }
   intern(resHash, key, resourceAttrs, dpAttrs) {
-    const sid = seriesHash(resHash, key);
-    const cur = this.byId.get(sid);
-    if (cur === undefined) this.byId.set(sid, { resHash, key, resourceAttrs, dpAttrs });
-    else if (cur.resHash !== resHash || Buffer.compare(cur.key, key) !== 0) {
-      this.collisions += 1;
-      throw new Error('64-bit series id collision; re-salt required');
-    }
+    const name = `${resHash}:${key.toString('latin1')}`;
+    const known = this.byKey.get(name);
+    if (known !== undefined) return known;
+    const [sid, seed] = assignSeriesId(resHash, key, (h) => {
+      const cur = this.byId.get(h);
+      return cur === undefined ? undefined : cur.resHash === resHash && Buffer.compare(cur.key, key) === 0;
+    });
+    if (seed > 0n) this.collisions += 1;
+    if (!this.byId.has(sid)) this.byId.set(sid, { resHash, key, resourceAttrs, dpAttrs });
+    this.byKey.set(name, sid);
     return sid;
   }
   get(sid) { return this.byId.get(sid); }
@@ -175,4 +197,5 @@ class KeyDictionary {
 }
 
 module.exports = { SPAN_KIND_STR, STATUS_CODE_STR, SERVICE_NAME_KEY, spanKindStr, statusCodeStr,
-  formatFloat, asString, attrMap, buildKey, buildKeyString, buildAttributes, resourceHash, seriesHash, KeyDictionary };
+  formatFloat, asString, attrMap, buildKey, buildKeyString, buildAttributes, resourceHash, seriesHash,
+  seriesHashSeeded, assignSeriesId, KeyDictionary };

@@ -135,10 +135,14 @@ class NativeColumnizerFakeAddon extends FakeAddon {
     super();
     this.real = require('../lib/addon').load();
   }
-  createColumnizer(h, opts) { return this.real.createColumnizer(null, opts); }
+  createColumnizer(h, opts) {
+    return this.real.createColumnizer(null, Object.assign({}, opts, this.collide ? { testCollideSeed0: true } : {}));
+  }
   columnize(c, bytes) { return this.real.columnize(c, bytes); }
   columnizerServiceId(c, name) { return this.real.columnizerServiceId(c, name); }
   columnizerForget(c, h) { return this.real.columnizerForget(c, h); }
+  columnizerLearn(c, h, key, sid) { return this.real.columnizerLearn(c, h, key, sid); }
+  columnizerRemap(c, from, to) { return this.real.columnizerRemap(c, from, to); }
   columnizerIngest(c) {
     const b = this.real.columnizerTake(c);
     this.ingest(null, b);

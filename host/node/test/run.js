@@ -377,10 +377,11 @@ function mixedRequests() {
   return reqs;
 }
 
-function runBoth(cfg, rules, reqs) {
+function runBoth(cfg, rules, reqs, collide = false) {
   const out = [];
   for (const native of [true, false]) {
     const addon = native ? new NativeColumnizerFakeAddon() : new FakeAddon();
+    addon.collide = collide;
     const t = { now: 1000n };
     const conn = new SpanMetricsConnector(Object.assign({ batch_size: 16 }, cfg),
       { addon, rules, native, clock: () => (t.now += 1n) });
@@ -414,6 +415,41 @@ test('native columnizer: same columns and same OTLP metrics as the JavaScript pa
     assert.deepStrictEqual(nat.cols, js.cols, JSON.stringify(cfg));
     assert.deepStrictEqual(nat.exports, js.exports, JSON.stringify(cfg));
     assert.deepStrictEqual(nat.services, js.services);
+  }
+});
+
+test('series ids: a 64-bit collision is re-salted on both paths (never thrown), outputs unchanged', () => {
+  const reqs = mixedRequests();
+  const [natRef, jsRef] = runBoth({}, DEMO_SPAN_NAME_RULES, reqs);
+  // every seed-0 id is 42: each new series after the first collides and is re-salted
+  const real = keys.seriesHashSeeded;
+  keys.seriesHashSeeded = (rh, k, seed) => (seed === 0n ? 42n : real(rh, k, seed));
+  let nat, js;
+  try {
+    [nat, js] = runBoth({}, DEMO_SPAN_NAME_RULES, reqs, true);
+  } finally {
+    keys.seriesHashSeeded = real;
+  }
+  assert.ok(nat.stats.nativeRequests > 0 && js.stats.collisions > 0);
+  assert.deepStrictEqual(nat.cols, js.cols);
+  assert.deepStrictEqual(nat.exports, js.exports);
+  // the same series, the same spans per series: only the ids moved
+  const perId = (cols) => {
+    const m = new Map();
+    cols.keyHash.forEach((k, i) => m.set(k, (m.get(k) || 0) + 1));
+    return [...m.values()].sort((a, b) => a - b);
+  };
+  assert.deepStrictEqual(perId(js.cols), perId(jsRef.cols));
+  assert.strictEqual(new Set(js.cols.keyHash).size, new Set(natRef.cols.keyHash).size);
+  // the dictionary: two keys on one seed-0 id get distinct ids
+  keys.seriesHashSeeded = (rh, k, seed) => (seed === 0n ? 42n : real(rh, k, seed));
+  try {
+    const d = new keys.KeyDictionary();
+    const a = d.intern(1n, Buffer.from('a'), {}, {}), b = d.intern(1n, Buffer.from('b'), {}, {});
+    assert.ok(a === 42n && b !== 42n && b !== 0n && d.collisions === 1);
+    assert.strictEqual(d.intern(1n, Buffer.from('b'), {}, {}), b);
+  } finally {
+    keys.seriesHashSeeded = real;
   }
 });
 

@@ -108,31 +108,46 @@ def resource_hash(attrs: Mapping) -> int:
     return h.intdigest()
 
 
+def series_hash_seeded(res_hash: int, key: bytes, seed: int) -> int:
+    return xxhash.xxh64_intdigest(res_hash.to_bytes(8, "little") + key, seed=seed)
+
+
+def assign_series_id(res_hash: int, key: bytes, owner) -> tuple:
+    """Series id of (resource, key): xxh64 with seed 0, 1, ... until the id is
+    neither 0 (reserved by the engine) nor held by another series (owner(id)
+    -> None free, True this series, False another).  Returns (id, seed)."""
+    seed = 0
+    while True:
+        h = series_hash_seeded(res_hash, key, seed)
+        if h != 0 and owner(h) is not False:
+            return h, seed
+        seed += 1
+
+
 def series_hash(res_hash: int, key: bytes) -> int:
-    """Device series id. 0 is reserved by the engine, so a zero hash is re-salted."""
-    h = xxhash.xxh64_intdigest(res_hash.to_bytes(8, "little") + key, seed=0)
-    if h == 0:
-        h = xxhash.xxh64_intdigest(res_hash.to_bytes(8, "little") + key, seed=1)
-    return h
+    """Device series id with nothing else interned (seed 0; seed 1 if that is 0)."""
+    return assign_series_id(res_hash, key, lambda h: None)[0]
 
 
 class KeyDictionary:
     """Host dictionary series id -> (resource attrs, key bytes, datapoint attrs).
-    Detects 64-bit collisions (distinct (resource, key) with the same id)."""
+    A 64-bit collision (a distinct (resource, key) on a taken id) is re-salted."""
 
     def __init__(self):
         self._by_id: dict[int, tuple] = {}
         self.collisions = 0
 
     def intern(self, res_hash: int, key: bytes, resource_attrs: Mapping, dp_attrs: Mapping) -> int:
-        sid = series_hash(res_hash, key)
-        cur = self._by_id.get(sid)
-        if cur is None:
+        """A distinct (resource, key) whose id is taken is re-salted (counted)."""
+        def owner(h):
+            cur = self._by_id.get(h)
+            return None if cur is None else (cur[0] == res_hash and cur[1] == key)
+
+        sid, seed = assign_series_id(res_hash, key, owner)
+        if sid not in self._by_id:
+            self.collisions += seed > 0
             # attributes are taken from the first span seen for the key (A5/A6)
             self._by_id[sid] = (res_hash, key, dict(resource_attrs), dict(dp_attrs))
-        elif cur[0] != res_hash or cur[1] != key:
-            self.collisions += 1
-            raise RuntimeError("64-bit series id collision; re-salt required")
         return sid
 
     def __getitem__(self, sid: int):

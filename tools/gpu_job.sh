@@ -2,11 +2,14 @@
 # One GPU-box job made of named steps, each under its own time limit.
 #   usage (inside gpurun): TAG=name bash tools/gpu_job.sh STEP [STEP ...]
 # Steps:
+#   smoke            __graft_entry__.smoke() (one small hot-path run vs the oracle)
 #   tests            every -m gpu test (pytest, per-test timeout)
 #   tests:<file>     one test file, e.g. tests:tests/test_gpu_binned.py
 #   bench            the default bench line (C2 + C4 sub-objects, CPU baselines)
 #   bench_<wl>       a short bench of one workload (c2, c4, c4zipf), no baselines
-#   ablate_<wl>      tools/ablate.py over the ABL_FLAGS variant set for <wl>
+#   ablate_<wl>      tools/ablate.py over the ABL_FLAGS / ABL_ENVS variant set for <wl>
+#   stamps_<wl>      tools/bt_stamps.py: per-workgroup phase timeline (c4, c4zipf)
+#   sweep            C2 kernel time vs batch size (SIZES="1000000 5000000 ...")
 #   trace_<wl>       rocprofv3 --kernel-trace --stats of a short bench of <wl>
 #   pmc_<wl>_<set>   one rocprofv3 --pmc pass (set: fetch, write, lds, sq) over
 #                    tools/prof_driver.py for <wl>
@@ -34,11 +37,15 @@ run() {  # name, seconds, command...
 BQ="--no-cpu-baseline --host-otlp-spans 0 --h2d-reps 0"
 for step in "$@"; do
   case $step in
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    sweep) for N in ${SIZES:-1000000 2500000 5000000 10000000 15000000}; do
+        run "sweep_n$N" 200 python bench.py --sub "" --spans "$N" --steps 30 --warmup 3 $BQ; done ;;
+    stamps_*) wl=${step#stamps_}; WL=$wl run "stamps_$wl" 300 python tools/bt_stamps.py ;;
     tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     tests:*) f=${step#tests:}; run "tests_$(basename "$f" .py)" 600 python -u -m pytest "$f" -m gpu -x -v --timeout 300 --timeout-method thread ;;
     bench) run bench 500 python bench.py ;;
     bench_*) wl=${step#bench_}; run "bench_$wl" 300 python bench.py --workload "$wl" --sub "" --steps 20 $BQ ;;
-    ablate_*) wl=${step#ablate_}; ABL_WORKLOAD=$wl ABL_VARS= run "ablate_$wl" 400 python tools/ablate.py ;;
+    ablate_*) wl=${step#ablate_}; ABL_WORKLOAD=$wl ABL_VARS=${ABL_VARS:-} run "ablate_$wl" 400 python tools/ablate.py ;;
     trace_*) wl=${step#trace_}
       (cd /tmp && run "trace_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$wl" -o run \
          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 10 --warmup 2 --streams 1 $BQ) || exit $? ;;
