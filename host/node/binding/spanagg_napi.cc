@@ -324,7 +324,8 @@ napi_value Create(napi_env env, napi_callback_info info) {
         uint32_t *dst;
     } u32s[] = {{"hllP", &c.hll_p},         {"cmsD", &c.cms_d},
                 {"cmsW", &c.cms_w},         {"nWindows", &c.n_windows},
-                {"nServices", &c.n_services}, {"flags", &c.flags}};
+                {"nServices", &c.n_services}, {"flags", &c.flags},
+                {"expMaxSize", &c.exp_max_size}};
     for (auto &f : u32s)
         if (!is_undefined(env, v = prop(env, cfg, f.k)) && !to_u32(env, v, f.dst, f.k)) return nullptr;
     if (!is_undefined(env, v = prop(env, cfg, "windowNs")) && !to_u64(env, v, &c.window_ns, "windowNs"))
@@ -462,6 +463,42 @@ napi_value Flush(napi_env env, napi_callback_info info) {
     set(env, o, "sumNs", make_typed(env, napi_biguint64_array, 8, r->sum_ns, n));
     set(env, o, "sum", make_typed(env, napi_float64_array, 8, r->sum, n));
     sa_red_result_free(r);
+    return o;
+}
+
+// flushExp(h) -> {status, nSeries, maxSize, keyHash, count, zeroCount, sumNs,
+// sum, min, max, scale, offset, nBuckets, bucketCounts [n*maxSize]}
+// (exponential-histogram engines; groups merge explicit buckets only)
+napi_value FlushExp(napi_env env, napi_callback_info info) {
+    napi_value argv[1];
+    if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
+    Handle *h = get_handle(env, argv[0]);
+    if (!h) return nullptr;
+    if (!h->e) return throw_status(env, SA_ESTATE, "flushExp: engine groups merge explicit buckets only");
+    sa_exp_result *r = nullptr;
+    int rc = sa_flush_exp(h->e, &r);
+    if ((rc != SA_OK && rc != SA_EFULL) || !r) {
+        if (r) sa_exp_result_free(r);
+        return engine_error(env, h, rc ? rc : SA_ESTATE, "sa_flush_exp");
+    }
+    const size_t n = r->n_series, m = r->max_size;
+    napi_value o;
+    napi_create_object(env, &o);
+    set(env, o, "status", num(env, rc));
+    set(env, o, "nSeries", num(env, static_cast<double>(n)));
+    set(env, o, "maxSize", num(env, static_cast<double>(m)));
+    set(env, o, "keyHash", make_typed(env, napi_biguint64_array, 8, r->key_hash, n));
+    set(env, o, "count", make_typed(env, napi_biguint64_array, 8, r->count, n));
+    set(env, o, "zeroCount", make_typed(env, napi_biguint64_array, 8, r->zero_count, n));
+    set(env, o, "sumNs", make_typed(env, napi_biguint64_array, 8, r->sum_ns, n));
+    set(env, o, "sum", make_typed(env, napi_float64_array, 8, r->sum, n));
+    set(env, o, "min", make_typed(env, napi_float64_array, 8, r->min, n));
+    set(env, o, "max", make_typed(env, napi_float64_array, 8, r->max, n));
+    set(env, o, "scale", make_typed(env, napi_int32_array, 4, r->scale, n));
+    set(env, o, "offset", make_typed(env, napi_int32_array, 4, r->offset, n));
+    set(env, o, "nBuckets", make_typed(env, napi_uint32_array, 4, r->n_buckets, n));
+    set(env, o, "bucketCounts", make_typed(env, napi_biguint64_array, 8, r->bucket_counts, n * m));
+    sa_exp_result_free(r);
     return o;
 }
 
@@ -848,6 +885,7 @@ napi_value Init(napi_env env, napi_value exports) {
                {"ingest", Ingest},
                {"sync", Sync},
                {"flush", Flush},
+               {"flushExp", FlushExp},
                {"windowRead", WindowRead},
                {"windowAdvance", WindowAdvance},
                {"stats", Stats},

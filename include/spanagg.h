@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SA_ABI_VERSION 1
+#define SA_ABI_VERSION 2
 #define SA_MAX_BOUNDS 62
 
 typedef enum {
@@ -86,6 +86,10 @@ typedef struct {
     int32_t device;         /* HIP device ordinal (one engine per GPU / rank) */
     uint32_t flags;         /* 0 for production; SA_DIAG_* bits are profiling-only
                                ablations that skip work and make results WRONG */
+    /* histogram.exponential.max_size: 0 = explicit buckets (the default);
+     * 2..4096 = exponential histograms (bounds unused; read with sa_flush_exp) */
+    uint32_t exp_max_size;
+    uint32_t reserved;
 } sa_config;
 
 typedef struct {
@@ -105,6 +109,26 @@ typedef struct {
     const uint64_t *sum_ns;        /* [n_series] exact sum of durations in ns */
     const double *sum;             /* [n_series] sum_ns / unit divisor (ms or s) */
 } sa_red_result;
+
+/* Exponential histograms (sa_config.exp_max_size > 0): the delta since the
+ * previous sa_flush_exp, one row per series with any span, sorted by
+ * key_hash.  Each row is go-expohisto's Histogram[float64] of the series'
+ * durations (float64(end-start)/unit): positive bucket i at `scale` counts
+ * values in (2^(i/2^scale), 2^((i+1)/2^scale)]; bucket_counts[r][j] is bucket
+ * offset[r] + j for j < n_buckets[r]. */
+typedef struct {
+    uint64_t n_series;
+    uint32_t max_size;             /* row stride of bucket_counts */
+    uint32_t unit;                 /* sa_unit of sum/min/max */
+    const uint64_t *key_hash;      /* [n_series] */
+    const uint64_t *count;         /* [n_series] spans (== calls) */
+    const uint64_t *zero_count;    /* [n_series] zero durations */
+    const uint64_t *sum_ns;        /* [n_series] exact */
+    const double *sum, *min, *max; /* [n_series] in the unit */
+    const int32_t *scale, *offset; /* [n_series] */
+    const uint32_t *n_buckets;     /* [n_series] */
+    const uint64_t *bucket_counts; /* [n_series][max_size] */
+} sa_exp_result;
 
 typedef struct {
     uint64_t window_id;
@@ -155,6 +179,14 @@ int sa_sync(sa_engine *e);
  * if spans were dropped since the previous flush. */
 int sa_flush(sa_engine *e, sa_red_result **out);
 void sa_red_result_free(sa_red_result *r);
+/* exportMetrics of an exponential-histogram engine (sa_flush returns
+ * SA_ESTATE there, and sa_flush_exp does on an explicit-bucket engine). */
+int sa_flush_exp(sa_engine *e, sa_exp_result **out);
+void sa_exp_result_free(sa_exp_result *r);
+/* Diagnostic: out[i] = the exponential bucket index of v[i] at scale[i] and
+ * logs[i] = Go's math.Log(v[i]), both computed on the engine's GPU
+ * (host arrays; n <= 2^20). */
+int sa_expo_probe(sa_engine *e, const double *v, const int32_t *scale, uint64_t n, int32_t *out, double *logs);
 
 /* Sketches of one resident window (not cleared). */
 int sa_window_read(sa_engine *e, uint64_t window_id, sa_sketch_result **out);

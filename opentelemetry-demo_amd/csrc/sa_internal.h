@@ -93,6 +93,35 @@ struct IngestParams {
   uint32_t lb_shift, lb_n, lb_seq;
 };
 
+// Exponential-histogram mode (spanagg_expo.hip): per key slot a header and
+// max_size u32 buckets kept circularly (index mod max_size), two buffers so a
+// downscale can merge from one into the other.
+struct ExpoHdr {
+  unsigned long long count, zero, sum_ns, min_ns, max_ns, minpos_ns, maxpos_ns;
+  int32_t scale, lo, hi;  // the kept buckets' scale and positive index range (lo = INT32_MAX: none)
+  uint32_t cur;           // which bucket buffer holds them
+};
+struct ExpoRow {  // one flushed series
+  unsigned long long count, zero, sum_ns, min_ns, max_ns;
+  int32_t scale, offset;
+  uint32_t n, pad;
+};
+struct ExpoParams {
+  const uint64_t *key, *start, *end;
+  uint64_t n;
+  unsigned long long *gkeys;
+  uint32_t log2cap, max_probe;
+  uint64_t cap;
+  ExpoHdr *hdr;
+  uint32_t *buckets;  // [2][cap][max_size]
+  uint32_t max_size;
+  double div;         // 1e6 (ms) or 1e9 (s)
+  uint32_t *slot_of;  // [n] key slot of each span (pass 1 -> pass 3)
+  unsigned long long *dropped;
+};
+__host__ __device__ ExpoHdr expo_hdr_empty();
+constexpr uint32_t kExpoMaxSize = 4096;
+
 // HLL bound sub-blocks: 2^kLbMinShift registers or more, at most kLbMaxSub of
 // them per engine (the kernels keep the bounds in LDS)
 constexpr uint32_t kLbMinShift = 10;
@@ -305,5 +334,12 @@ hipError_t launch_reduce_errslab(uint32_t *errslab, uint32_t G, uint64_t per_wg,
                                  uint32_t log2cap, unsigned long long *errcnt_ws, hipStream_t s);
 hipError_t launch_count_keys(const unsigned long long *gkeys, uint64_t cap,
                              unsigned long long *out, hipStream_t s);
+// exponential histograms (spanagg_expo.hip)
+hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s);
+hipError_t launch_expo_compact(const ExpoParams &E, unsigned long long *out_keys, ExpoRow *out_rows,
+                               uint32_t *out_buckets, unsigned long long *out_n, hipStream_t s);
+hipError_t launch_expo_init(ExpoHdr *hdr, uint64_t cap, hipStream_t s);
+hipError_t launch_expo_probe(const double *v, const int32_t *scale, int32_t *idx_out, double *log_out, uint64_t n,
+                             hipStream_t s);
 
 }  // namespace sa

@@ -12,6 +12,14 @@ struct red_holder {
   std::vector<double> sum;
 };
 
+struct exp_holder {
+  sa_exp_result r;
+  std::vector<uint64_t> keys, count, zero, sum_ns, buckets;
+  std::vector<double> sum, min, max;
+  std::vector<int32_t> scale, offset;
+  std::vector<uint32_t> nb;
+};
+
 struct sketch_holder {
   sa_sketch_result r;
   std::vector<uint8_t> hll;

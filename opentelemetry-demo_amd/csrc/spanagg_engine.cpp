@@ -84,6 +84,15 @@ struct sa_engine {
   // HLL lower bounds per sub-block of 2^lb_shift registers (IngestParams::hll_lb)
   uint8_t *hll_lb = nullptr;
   uint32_t lb_shift = 0, lb_n = 0, lb_seq = 0;
+  // exponential-histogram mode (cfg.exp_max_size > 0): the HBM-table path
+  // runs the sketches, spanagg_expo.hip the histograms
+  bool expo = false;
+  sa::ExpoHdr *expo_hdr = nullptr;
+  uint32_t *expo_buckets = nullptr, *expo_slot = nullptr;
+  uint64_t expo_slot_cap = 0;
+  unsigned long long *expo_out_keys = nullptr;
+  sa::ExpoRow *expo_out_rows = nullptr;
+  uint32_t *expo_out_buckets = nullptr;
   bool bt_scatter1 = false;  // SPANAGG_BT_SCATTER=1: round-1 scatter kernel (A/B runs)
   bool bt_agg1 = false;      // SPANAGG_BT_AGG=1: first aggregate kernel (A/B runs)
   // partitioned HBM-table path (lazily allocated on the first launch)
@@ -147,6 +156,8 @@ int validate_config(const sa_config *c, std::string &why) {
     return why = "n_windows * window_ns must stay below 2^63 ns", SA_EINVAL;
   if (((uint64_t)c->n_windows * c->n_services << c->hll_p) >= (1ULL << 32))
     return why = "n_windows * n_services * 2^hll_p must stay below 2^32 registers", SA_EINVAL;
+  if (c->exp_max_size == 1 || c->exp_max_size > sa::kExpoMaxSize)
+    return why = "exp_max_size must be 0 (explicit buckets) or 2..4096", SA_EINVAL;
   return SA_OK;
 }
 
@@ -323,7 +334,8 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   const uint32_t nw = (e->nbk + 1) / 2;
   // lkeys + lsum + lcnt + deferred-HLL queue (+ its counter), see ingest_lds_kernel
   e->lds_bytes = (size_t)e->cap * 16 + (size_t)e->cap * nw * 4 + sa::kLdsExtraBytes;
-  e->small = e->lds_bytes <= kLdsBudget;
+  e->expo = cfg->exp_max_size != 0;
+  e->small = e->lds_bytes <= kLdsBudget && !e->expo;
   e->variant = e->small ? kDefaultVariant : 0;
   if (const char *v = std::getenv("SPANAGG_VARIANT"))  // tuning knob for A/B runs
     e->variant = std::max(0, std::min((e->small ? sa::kNumLdsVariants : sa::kNumVariants) - 1,
@@ -343,7 +355,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     // partitioned path unless the LDS counter row is too small for the
     // buckets (SPANAGG_HBM_PART=0: per-span atomics, for A/B runs)
     const char *pv = std::getenv("SPANAGG_HBM_PART");
-    e->part = e->nbk <= sa::kPartMaxBk && !(pv && std::atoi(pv) == 0);
+    e->part = e->nbk <= sa::kPartMaxBk && !(pv && std::atoi(pv) == 0) && !e->expo;
     if (e->part)
       if (hipError_t st = sa::prepare_ingest_part(); st != hipSuccess)
         return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
@@ -386,6 +398,13 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       e->lb_n = (uint32_t)(regs >> sh);
       if ((rc = alloc((void **)&e->hll_lb, ((size_t)e->lb_n + 15) & ~(size_t)15))) return bail(rc);
     }
+  }
+  if (e->expo) {
+    if ((rc = alloc((void **)&e->expo_hdr, (size_t)e->cap * sizeof(sa::ExpoHdr))) ||
+        (rc = alloc((void **)&e->expo_buckets, (size_t)2 * e->cap * cfg->exp_max_size * 4)))
+      return bail(rc);
+    if (sa::launch_expo_init(e->expo_hdr, e->cap, nullptr) != hipSuccess)
+      return bail(fail(e, SA_EDEVICE, "expo state init failed"));
   }
   if (std::getenv("SPANAGG_STAMPS") && (rc = alloc((void **)&e->dbg, (size_t)e->G * sa::kDbgPerWg * 8)))
     return bail(rc);
@@ -454,6 +473,8 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->slab_cnt, (void *)e->hll, (void *)e->errcnt, (void *)e->d_seeds,
                   (void *)e->dbg, (void *)e->d_bins, (void *)e->errslab, (void *)e->part_rec,
                   (void *)e->part_fill, (void *)e->bt_rec, (void *)e->bt_cnt, (void *)e->base64, (void *)e->hll_lb,
+                  (void *)e->expo_hdr, (void *)e->expo_buckets, (void *)e->expo_slot, (void *)e->expo_out_keys,
+                  (void *)e->expo_out_rows, (void *)e->expo_out_buckets,
                   e->stage})
     if (p) (void)hipFree(p);
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
@@ -541,6 +562,27 @@ static int bt_prepare_launch(sa_engine *e, uint64_t n, IngestParams &P, hipStrea
   P.bt_rec = e->bt_rec;
   P.bt_cnt = e->bt_cnt;
   return SA_OK;
+}
+
+static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
+  sa::ExpoParams E{};
+  if (b) {
+    E.key = b->key_hash;
+    E.start = b->start_ns;
+    E.end = b->end_ns;
+    E.n = b->n;
+  }
+  E.gkeys = e->gkeys;
+  E.log2cap = e->log2cap;
+  E.max_probe = sa::max_probe_of(e->log2cap);
+  E.cap = e->cap;
+  E.hdr = e->expo_hdr;
+  E.buckets = e->expo_buckets;
+  E.max_size = e->cfg.exp_max_size;
+  E.div = e->cfg.unit == SA_UNIT_S ? 1e9 : 1e6;
+  E.slot_of = e->expo_slot;
+  E.dropped = e->stats + sa::kStatDropped;
+  return E;
 }
 
 static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
@@ -639,6 +681,19 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
         per_bin_max, ((b->n + sa::kPartBins - 1) / sa::kPartBins * 5 / 4 + 64 + sa::kPartStage - 1) &
                          ~(uint64_t)(sa::kPartStage - 1));
     st = sa::launch_ingest_part(P, s);
+  } else if (e->expo) {
+    // sketches (and the zero-key / service / window counters) through the
+    // HBM-table kernel with its RED part off, then the histogram kernels
+    P.diag |= SA_DIAG_NO_RED;
+    st = sa::launch_ingest_hbm(P, grid, s, e->variant);
+    if (st == hipSuccess && e->expo_slot_cap < b->n) {
+      if (e->expo_slot) (void)hipFree(e->expo_slot);
+      e->expo_slot = nullptr;
+      e->expo_slot_cap = 0;
+      if (hipMalloc((void **)&e->expo_slot, b->n * 4) != hipSuccess) return fail(e, SA_ENOMEM, "expo slot buffer");
+      e->expo_slot_cap = b->n;
+    }
+    if (st == hipSuccess) st = sa::launch_expo_ingest(expo_params(e, b), s);
   } else {
     st = sa::launch_ingest_hbm(P, grid, s, e->variant);
   }
@@ -739,6 +794,7 @@ static int read_stats(sa_engine *e, uint64_t out[sa::kNumStats]) {
 int sa_flush(sa_engine *e, sa_red_result **out) {
   if (!e || !out) return SA_EINVAL;
   *out = nullptr;
+  if (e->expo) return fail(e, SA_ESTATE, "exponential-histogram engine: use sa_flush_exp");
   if (int rc = set_dev(e)) return rc;
   join_sets(e);
   if (int rc = ensure_out(e)) return rc;
@@ -797,6 +853,109 @@ int sa_flush(sa_engine *e, sa_red_result **out) {
 }
 
 void sa_red_result_free(sa_red_result *r) { delete reinterpret_cast<red_holder *>(r); }
+
+int sa_flush_exp(sa_engine *e, sa_exp_result **out) {
+  if (!e || !out) return SA_EINVAL;
+  *out = nullptr;
+  if (!e->expo) return fail(e, SA_ESTATE, "explicit-bucket engine: use sa_flush");
+  if (int rc = set_dev(e)) return rc;
+  join_sets(e);
+  const uint32_t M = e->cfg.exp_max_size;
+  if (!e->expo_out_keys &&
+      (hipMalloc((void **)&e->expo_out_keys, e->cap * 8) != hipSuccess ||
+       hipMalloc((void **)&e->expo_out_rows, e->cap * sizeof(sa::ExpoRow)) != hipSuccess ||
+       hipMalloc((void **)&e->expo_out_buckets, e->cap * (size_t)M * 4) != hipSuccess))
+    return fail(e, SA_ENOMEM, "expo flush buffers hipMalloc failed");
+  SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, e->stream));
+  SA_HIP(e, sa::launch_expo_compact(expo_params(e, nullptr), e->expo_out_keys, e->expo_out_rows,
+                                    e->expo_out_buckets, e->scratch, e->stream));
+  uint64_t n = 0;
+  SA_HIP(e, hipMemcpyAsync(&n, e->scratch, 8, hipMemcpyDeviceToHost, e->stream));
+  SA_HIP(e, hipStreamSynchronize(e->stream));
+  std::vector<uint64_t> k(n);
+  std::vector<sa::ExpoRow> rows(n);
+  std::vector<uint32_t> bk(n * M);
+  if (n) {
+    SA_HIP(e, hipMemcpyAsync(k.data(), e->expo_out_keys, n * 8, hipMemcpyDeviceToHost, e->stream));
+    SA_HIP(e, hipMemcpyAsync(rows.data(), e->expo_out_rows, n * sizeof(sa::ExpoRow), hipMemcpyDeviceToHost, e->stream));
+    SA_HIP(e, hipMemcpyAsync(bk.data(), e->expo_out_buckets, n * (size_t)M * 4, hipMemcpyDeviceToHost, e->stream));
+    SA_HIP(e, hipStreamSynchronize(e->stream));
+  }
+  std::vector<uint64_t> ord(n);
+  std::iota(ord.begin(), ord.end(), 0);
+  std::sort(ord.begin(), ord.end(), [&](uint64_t a, uint64_t b) { return k[a] < k[b]; });
+  auto *h = new exp_holder();
+  h->keys.resize(n);
+  h->count.resize(n);
+  h->zero.resize(n);
+  h->sum_ns.resize(n);
+  h->sum.resize(n);
+  h->min.resize(n);
+  h->max.resize(n);
+  h->scale.resize(n);
+  h->offset.resize(n);
+  h->nb.resize(n);
+  h->buckets.assign(n * M, 0);
+  const double div = e->cfg.unit == SA_UNIT_S ? 1e9 : 1e6;
+  for (uint64_t r = 0; r < n; ++r) {
+    const uint64_t i = ord[r];
+    const sa::ExpoRow &x = rows[i];
+    h->keys[r] = k[i];
+    h->count[r] = x.count;
+    h->zero[r] = x.zero;
+    h->sum_ns[r] = x.sum_ns;
+    h->sum[r] = (double)x.sum_ns / div;
+    h->min[r] = (double)x.min_ns / div;
+    h->max[r] = (double)x.max_ns / div;
+    h->scale[r] = x.scale;
+    h->offset[r] = x.offset;
+    h->nb[r] = x.n;
+    for (uint32_t j = 0; j < x.n && j < M; ++j) h->buckets[r * M + j] = bk[i * M + j];
+  }
+  h->r.n_series = n;
+  h->r.max_size = M;
+  h->r.unit = e->cfg.unit;
+  h->r.key_hash = h->keys.data();
+  h->r.count = h->count.data();
+  h->r.zero_count = h->zero.data();
+  h->r.sum_ns = h->sum_ns.data();
+  h->r.sum = h->sum.data();
+  h->r.min = h->min.data();
+  h->r.max = h->max.data();
+  h->r.scale = h->scale.data();
+  h->r.offset = h->offset.data();
+  h->r.n_buckets = h->nb.data();
+  h->r.bucket_counts = h->buckets.data();
+  *out = &h->r;
+  uint64_t st[sa::kNumStats];
+  if (int rc = read_stats(e, st)) return rc;
+  if (st[sa::kStatDropped] != e->dropped_seen) {
+    e->dropped_seen = st[sa::kStatDropped];
+    return fail(e, SA_EFULL, "key table full: spans were dropped since the previous flush");
+  }
+  return SA_OK;
+}
+
+void sa_exp_result_free(sa_exp_result *r) { delete reinterpret_cast<exp_holder *>(r); }
+
+int sa_expo_probe(sa_engine *e, const double *v, const int32_t *scale, uint64_t n, int32_t *out, double *logs) {
+  if (!e || (n && (!v || !scale || !out || !logs)) || n > (1ULL << 20)) return SA_EINVAL;
+  if (n == 0) return SA_OK;
+  if (int rc = set_dev(e)) return rc;
+  join_sets(e);
+  void *buf = nullptr;
+  if (hipMalloc(&buf, n * 24) != hipSuccess) return fail(e, SA_ENOMEM, "probe buffer");
+  double *dv = static_cast<double *>(buf), *dl = dv + n;
+  int32_t *ds = reinterpret_cast<int32_t *>(dl + n), *di = ds + n;
+  hipError_t st = hipMemcpyAsync(dv, v, n * 8, hipMemcpyHostToDevice, e->stream);
+  if (st == hipSuccess) st = hipMemcpyAsync(ds, scale, n * 4, hipMemcpyHostToDevice, e->stream);
+  if (st == hipSuccess) st = sa::launch_expo_probe(dv, ds, di, dl, n, e->stream);
+  if (st == hipSuccess) st = hipMemcpyAsync(out, di, n * 4, hipMemcpyDeviceToHost, e->stream);
+  if (st == hipSuccess) st = hipMemcpyAsync(logs, dl, n * 8, hipMemcpyDeviceToHost, e->stream);
+  if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+  (void)hipFree(buf);
+  return st == hipSuccess ? SA_OK : fail(e, SA_EDEVICE, std::string("expo probe: ") + hipGetErrorString(st));
+}
 
 static bool resident(const sa_engine *e, uint64_t w) {
   return w >= e->win_base && w - e->win_base < e->cfg.n_windows;
@@ -914,6 +1073,7 @@ int sa_get_stats(sa_engine *e, sa_stats *o) {
 
 int sa_export_keys(sa_engine *e, uint64_t *d_keys, uint64_t cap, uint64_t *n_out, void *stream) {
   if (!e || !n_out || (cap && !d_keys)) return SA_EINVAL;
+  if (e->expo) return fail(e, SA_ESTATE, "merge hooks cover explicit-bucket engines only");
   if (int rc = set_dev(e)) return rc;
   join_sets(e);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
@@ -934,6 +1094,7 @@ int sa_export_keys(sa_engine *e, uint64_t *d_keys, uint64_t cap, uint64_t *n_out
 int sa_gather_dense(sa_engine *e, const uint64_t *d_keys, uint64_t n, uint64_t *d_rows, int reset,
                     void *stream) {
   if (!e || (n && (!d_keys || !d_rows))) return SA_EINVAL;
+  if (e->expo) return fail(e, SA_ESTATE, "merge hooks cover explicit-bucket engines only");
   if (int rc = set_dev(e)) return rc;
   join_sets(e);
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;

@@ -142,6 +142,7 @@ int sa_group_create(const sa_config *cfg, const int32_t *devices, uint32_t n, sa
   if (!out) return SA_EINVAL;
   *out = nullptr;
   if (!cfg || !devices || n == 0 || n > 64) return SA_EINVAL;
+  if (cfg->exp_max_size) return SA_EINVAL;  // groups merge explicit-bucket engines
   auto *g = new sa_group();
   g->cfg = *cfg;
   g->bounds.assign(cfg->bounds, cfg->bounds + cfg->n_bounds);

@@ -33,6 +33,7 @@ class sa_config(C.Structure):
         ("hll_p", C.c_uint32), ("cms_d", C.c_uint32), ("cms_w", C.c_uint32),
         ("window_ns", C.c_uint64), ("n_windows", C.c_uint32), ("n_services", C.c_uint32),
         ("key_capacity", C.c_uint64), ("device", C.c_int32), ("flags", C.c_uint32),
+        ("exp_max_size", C.c_uint32), ("reserved", C.c_uint32),
     ]
 
 
@@ -49,6 +50,16 @@ class sa_red_result(C.Structure):
         ("n_series", C.c_uint64), ("n_buckets", C.c_uint32),
         ("key_hash", u64p), ("bucket_counts", u64p), ("calls", u64p),
         ("sum_ns", u64p), ("sum", f64p),
+    ]
+
+
+class sa_exp_result(C.Structure):
+    _fields_ = [
+        ("n_series", C.c_uint64), ("max_size", C.c_uint32), ("unit", C.c_uint32),
+        ("key_hash", u64p), ("count", u64p), ("zero_count", u64p), ("sum_ns", u64p),
+        ("sum", f64p), ("min", f64p), ("max", f64p),
+        ("scale", C.POINTER(C.c_int32)), ("offset", C.POINTER(C.c_int32)), ("n_buckets", u32p),
+        ("bucket_counts", u64p),
     ]
 
 
@@ -80,6 +91,9 @@ SIGNATURES = [
     ("sa_sync", C.c_int, [C.c_void_p]),
     ("sa_flush", C.c_int, [C.c_void_p, C.POINTER(C.POINTER(sa_red_result))]),
     ("sa_red_result_free", None, [C.POINTER(sa_red_result)]),
+    ("sa_flush_exp", C.c_int, [C.c_void_p, C.POINTER(C.POINTER(sa_exp_result))]),
+    ("sa_exp_result_free", None, [C.POINTER(sa_exp_result)]),
+    ("sa_expo_probe", C.c_int, [C.c_void_p, f64p, C.POINTER(C.c_int32), C.c_uint64, C.POINTER(C.c_int32), f64p]),
     ("sa_window_read", C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.POINTER(sa_sketch_result))]),
     ("sa_window_advance", C.c_int, [C.c_void_p, C.c_uint64]),
     ("sa_sketch_result_free", None, [C.POINTER(sa_sketch_result)]),
@@ -133,7 +147,7 @@ def load() -> C.CDLL:
                 raise RuntimeError(f"libspanagg.so does not export {name}")
             fn.restype = res
             fn.argtypes = args
-        if lib.sa_abi_version() != 1:
+        if lib.sa_abi_version() != 2:
             raise RuntimeError("libspanagg ABI version mismatch")
         _lib = lib
     return _lib

@@ -54,6 +54,7 @@ class Config:
     key_capacity: int = 1000
     device: int = 0
     flags: int = 0  # SA_DIAG_* profiling ablations only (results are wrong when set)
+    exp_max_size: int = 0  # histogram.exponential.max_size (0: explicit buckets)
 
     def to_c(self):
         arr = (C.c_double * max(1, len(self.bounds)))(*[float(b) for b in self.bounds])
@@ -64,6 +65,7 @@ class Config:
         c.hll_p, c.cms_d, c.cms_w = self.hll_p, self.cms_d, self.cms_w
         c.window_ns, c.n_windows, c.n_services = self.window_ns, self.n_windows, self.n_services
         c.key_capacity, c.device, c.flags = self.key_capacity, self.device, self.flags
+        c.exp_max_size = self.exp_max_size
         return c, arr
 
 
@@ -103,6 +105,22 @@ class RedResult:
     calls: np.ndarray             # [n] u64
     sum_ns: np.ndarray            # [n] u64
     sum: np.ndarray               # [n] f64 (ms or s)
+    status: int = 0
+
+
+@dataclass
+class ExpoResult:
+    """sa_exp_result: per series go-expohisto histograms (delta since the last flush)."""
+    key_hash: np.ndarray     # [n] u64, ascending
+    count: np.ndarray        # [n] u64
+    zero_count: np.ndarray   # [n] u64
+    sum_ns: np.ndarray       # [n] u64
+    sum: np.ndarray          # [n] f64 (unit)
+    min: np.ndarray
+    max: np.ndarray
+    scale: np.ndarray        # [n] i32
+    offset: np.ndarray       # [n] i32
+    buckets: list            # [n] u64 arrays (positive buckets offset .. offset + len - 1)
     status: int = 0
 
 
@@ -239,6 +257,41 @@ class Engine:
         out = C.POINTER(_lib.sa_sketch_result)()
         self._check(self.lib.sa_window_read(self._h, window_id, C.byref(out)), "sa_window_read")
         return _sketch_result(self.lib, out)
+
+    def flush_exp(self, allow_drops: bool = False) -> ExpoResult:
+        out = C.POINTER(_lib.sa_exp_result)()
+        rc = self.lib.sa_flush_exp(self._h, C.byref(out))
+        if rc not in (0, _lib.SA_EFULL) or not out:
+            self._check(rc if rc else _lib.SA_ESTATE, "sa_flush_exp")
+        try:
+            r = out.contents
+            n, M = int(r.n_series), int(r.max_size)
+
+            def arr(p, dt):
+                return np.zeros(0, dtype=dt) if n == 0 else np.ctypeslib.as_array(p, shape=(n,)).copy()
+
+            bk = np.zeros((0, M), np.uint64) if n == 0 else np.ctypeslib.as_array(r.bucket_counts, shape=(n, M))
+            nb = arr(r.n_buckets, np.uint32)
+            res = ExpoResult(arr(r.key_hash, np.uint64), arr(r.count, np.uint64), arr(r.zero_count, np.uint64),
+                             arr(r.sum_ns, np.uint64), arr(r.sum, np.float64), arr(r.min, np.float64),
+                             arr(r.max, np.float64), arr(r.scale, np.int32), arr(r.offset, np.int32),
+                             [bk[i, : int(nb[i])].copy() for i in range(n)], rc)
+        finally:
+            self.lib.sa_exp_result_free(out)
+        if rc == _lib.SA_EFULL and not allow_drops:
+            raise SpanAggError(rc, f"sa_flush_exp: spans dropped (key table full); stats={self.stats()}")
+        return res
+
+    def expo_probe(self, values, scales):
+        """GPU bucket index and Go math.Log of each value (diagnostic)."""
+        v = np.ascontiguousarray(values, dtype=np.float64)
+        s = np.ascontiguousarray(scales, dtype=np.int32)
+        idx = np.zeros(len(v), dtype=np.int32)
+        logs = np.zeros(len(v), dtype=np.float64)
+        self._check(self.lib.sa_expo_probe(self._h, v.ctypes.data_as(_lib.f64p), s.ctypes.data_as(C.POINTER(C.c_int32)),
+                                           len(v), idx.ctypes.data_as(C.POINTER(C.c_int32)),
+                                           logs.ctypes.data_as(_lib.f64p)), "sa_expo_probe")
+        return idx, logs
 
     def window_advance(self, new_base: int):
         self._check(self.lib.sa_window_advance(self._h, int(new_base)), "sa_window_advance")

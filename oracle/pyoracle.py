@@ -56,6 +56,11 @@ def load():
         L.or_window.restype = C.c_int
         L.or_window.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
         L.or_stats.argtypes = [C.c_void_p, C.c_void_p]
+        L.or_go_log.restype = C.c_double
+        L.or_go_log.argtypes = [C.c_double]
+        L.or_expo_index.restype = C.c_int32
+        L.or_expo_index.argtypes = [C.c_double, C.c_int32]
+        L.or_expo_series.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32] + [C.c_void_p] * 9
         L.or_aggregate_strings.restype = C.c_uint64
         L.or_aggregate_strings.argtypes = [C.c_void_p] + [C.c_void_p] * 6 + [
             C.c_uint64, _f64p, C.c_uint32, _u64p]
@@ -83,6 +88,45 @@ def splitmix64(x: int) -> int:
 def hll_estimate(regs, p: int) -> float:
     r = np.ascontiguousarray(regs, dtype=np.uint8)
     return float(load().or_hll_estimate(r.ctypes.data_as(_u8p), p))
+
+
+def go_log(x: float) -> float:
+    return float(load().or_go_log(float(x)))
+
+
+def expo_index(v: float, scale: int) -> int:
+    return int(load().or_expo_index(float(v), int(scale)))
+
+
+def expo_series(start, end, max_size: int = 160, unit_seconds: bool = False) -> dict:
+    """One series' exponential histogram, values observed in the given order."""
+    st = np.ascontiguousarray(start, dtype=np.uint64)
+    en = np.ascontiguousarray(end, dtype=np.uint64)
+    cnt, zero = C.c_uint64(), C.c_uint64()
+    sm, mn, mx = C.c_double(), C.c_double(), C.c_double()
+    sc, off, nb = C.c_int32(), C.c_int32(), C.c_uint32()
+    counts = np.zeros(max(1, max_size), dtype=np.uint64)
+    load().or_expo_series(st.ctypes.data, en.ctypes.data, len(st), max_size, int(unit_seconds), C.byref(cnt),
+                          C.byref(zero), C.byref(sm), C.byref(mn), C.byref(mx), C.byref(sc), C.byref(off),
+                          C.byref(nb), counts.ctypes.data)
+    return dict(count=cnt.value, zero_count=zero.value, sum=sm.value, min=mn.value, max=mx.value,
+                scale=sc.value, offset=off.value, counts=counts[: nb.value].copy())
+
+
+def expo_aggregate(batch, max_size: int = 160, unit_seconds: bool = False) -> dict:
+    """Exponential histograms of every non-zero series of a batch (spans of
+    one series in arrival order), keyed by series id."""
+    key = np.asarray(batch.key_hash)
+    order = np.argsort(key, kind="stable")
+    k_sorted = key[order]
+    bounds = np.flatnonzero(np.diff(k_sorted)) + 1
+    out = {}
+    for grp in np.split(order, bounds):
+        k = int(key[grp[0]])
+        if k == 0:
+            continue
+        out[k] = expo_series(np.asarray(batch.start_ns)[grp], np.asarray(batch.end_ns)[grp], max_size, unit_seconds)
+    return out
 
 
 class Oracle:

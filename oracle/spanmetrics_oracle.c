@@ -501,3 +501,115 @@ uint64_t or_aggregate_strings(const char *const *strings, const uint32_t *svc_id
     if (checksum_out) *checksum_out = cs;
     return cnt;
 }
+
+/* ------------------------------------------------------------------------
+ * Exponential histogram: [UPSTREAM] spanmetricsconnector internal/metrics
+ * exponentialHistogram.Observe -> github.com/lightstep/go-expohisto
+ * structure.Histogram[float64].Update, restated value by value.  The log is
+ * Go's math.Log (src/math/log.go) with the same operations in the same order;
+ * the Makefile builds this file with -ffp-contract=off so no multiply-add is
+ * fused (Go does not fuse them on amd64).
+ * ---------------------------------------------------------------------- */
+double or_go_log(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+               L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  int ki;
+  double f1 = frexp(x, &ki);
+  if (f1 < 1.4142135623730951 / 2) {
+    f1 *= 2;
+    ki--;
+  }
+  const double f = f1 - 1, k = (double)ki;
+  const double s = f / (2 + f), s2 = s * s, s4 = s2 * s2;
+  const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  const double R = t1 + t2, hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
+int32_t or_expo_index(double v, int32_t scale) {
+  uint64_t b;
+  memcpy(&b, &v, 8);
+  int64_t raw_exp = (int64_t)((b >> 52) & 0x7FF);
+  const uint64_t sig = b & ((1ULL << 52) - 1);
+  if (scale > 0) {
+    if (v <= 0x1p-1022) return (int32_t)(-1022 * (1LL << scale));
+    if (sig == 0) return (int32_t)((raw_exp - 1023) * (1LL << scale) - 1);
+    const double x = floor(or_go_log(v) * ldexp(1.4426950408889634, scale));
+    const int64_t max_index = (1024LL << scale) - 1;
+    return x >= (double)max_index ? (int32_t)max_index : (int32_t)x;
+  }
+  if (raw_exp == 0) raw_exp -= (int64_t)__builtin_clzll(sig) - 12;
+  const int32_t exp = (int32_t)(raw_exp - 1023);
+  return (exp + (sig == 0 ? -1 : 0)) >> (-scale);
+}
+
+void or_expo_series(const uint64_t *start_ns, const uint64_t *end_ns, uint64_t n, uint32_t max_size,
+                    uint32_t unit_seconds, uint64_t *count, uint64_t *zero_count, double *sum, double *min,
+                    double *max, int32_t *scale, int32_t *offset, uint32_t *n_out, uint64_t *counts) {
+  /* positive buckets: counts[i - start] for index i in [start, end] */
+  uint64_t *tmp = (uint64_t *)calloc(max_size ? max_size : 1, 8);
+  int32_t sc = 20, start = 0, end = -1;
+  int have = 0;
+  *count = *zero_count = 0;
+  *sum = *min = *max = 0.0;
+  memset(counts, 0, (size_t)max_size * 8);
+  for (uint64_t j = 0; j < n; ++j) {
+    const double v = or_duration(start_ns[j], end_ns[j], unit_seconds);
+    if (*count == 0) *min = *max = v;
+    else {
+      if (v < *min) *min = v;
+      if (v > *max) *max = v;
+    }
+    *count += 1;
+    if (v == 0) {
+      *zero_count += 1;
+      continue;
+    }
+    *sum += v;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      const int32_t idx = or_expo_index(v, sc);
+      int32_t hi = 0, lo = 0, fits = 1;
+      if (!have) {
+        start = end = idx;
+        have = 1;
+      } else if (idx < start) {
+        if (end - idx >= (int32_t)max_size) {
+          fits = 0, hi = end, lo = idx;
+        } else {
+          const int32_t shift = start - idx; /* make room below */
+          memmove(counts + shift, counts, (size_t)(end - start + 1) * 8);
+          memset(counts, 0, (size_t)shift * 8);
+          start = idx;
+        }
+      } else if (idx > end) {
+        if (idx - start >= (int32_t)max_size) fits = 0, hi = idx, lo = start;
+        else end = idx;
+      }
+      if (fits) {
+        counts[idx - start] += 1;
+        break;
+      }
+      /* changeScale, then merge the buckets pairwise `change` times */
+      int32_t change = 0;
+      while (hi - lo >= (int32_t)max_size) {
+        hi >>= 1;
+        lo >>= 1;
+        change++;
+      }
+      const int32_t ns = start >> change, ne = end >> change;
+      memset(tmp, 0, (size_t)max_size * 8);
+      for (int32_t i = start; i <= end; ++i) tmp[(i >> change) - ns] += counts[i - start];
+      memcpy(counts, tmp, (size_t)max_size * 8);
+      start = ns;
+      end = ne;
+      sc -= change;
+    }
+  }
+  free(tmp);
+  *scale = sc;
+  *offset = have ? start : 0;
+  *n_out = have ? (uint32_t)(end - start + 1) : 0;
+}

@@ -69,6 +69,22 @@ int or_window(const or_engine *e, uint64_t window_id, uint8_t *hll, uint32_t *cm
 /* counters: [0]=spans, [1]=invalid_service, [2]=zero_key */
 void or_stats(const or_engine *e, uint64_t *out3);
 
+/* ---- exponential histogram (histogram.exponential.max_size) ------------ */
+/* Go's math.Log (src/math/log.go: Frexp reduction + the fdlibm polynomial),
+ * operation for operation (build with -ffp-contract=off). */
+double or_go_log(double x);
+/* go-expohisto MapToIndex of a positive value at `scale` (logarithm mapping
+ * for scale 1..20, exponent mapping for scale <= 0). */
+int32_t or_expo_index(double v, int32_t scale);
+/* One series' go-expohisto structure.Histogram[float64]: Update of each
+ * duration float64(end-start)/div in arrival order (zeros -> zero_count,
+ * downscale by changeScale when the positive range would reach max_size).
+ * counts receives the positive buckets offset .. offset + *n_out - 1
+ * (capacity max_size).  sum is float64 in arrival order. */
+void or_expo_series(const uint64_t *start_ns, const uint64_t *end_ns, uint64_t n, uint32_t max_size,
+                    uint32_t unit_seconds, uint64_t *count, uint64_t *zero_count, double *sum, double *min,
+                    double *max, int32_t *scale, int32_t *offset, uint32_t *n_out, uint64_t *counts);
+
 /* ---- reference-faithful string-keyed path (CPU baseline) ---------------- */
 /* Spans given as (service string id, span name string id, kind, status) with
  * a string table; the key is built per span exactly as buildKey does

@@ -1,0 +1,110 @@
+"""Exponential histograms on the GPU (sa_config.exp_max_size, the
+spanmetrics `histogram.exponential` option) against the oracle's
+value-by-value go-expohisto restatement (oracle/spanmetrics_oracle.c,
+itself pinned to tests/golden/expo_kat.json).  Bar: count, zero count,
+scale, offset and every bucket bit-exact; min/max exact; sum within 1e-9
+relative (exact ns on the GPU, arrival-order float64 in the oracle); the
+kernel's Go math.Log bit-exact with the oracle's."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+from spanagg import Config, Engine, SpanBatch, pack_meta
+from spanagg import _lib
+from spanagg.synth import generate_c2
+
+pytestmark = pytest.mark.gpu
+KAT = os.path.join(os.path.dirname(__file__), "golden", "expo_kat.json")
+
+
+def _check(res, batch, max_size, unit_s=False):
+    ora = pyoracle.expo_aggregate(batch, max_size, unit_s)
+    assert [int(k) for k in res.key_hash] == sorted(ora)
+    for i, k in enumerate(res.key_hash):
+        o = ora[int(k)]
+        assert (int(res.count[i]), int(res.zero_count[i])) == (o["count"], o["zero_count"]), k
+        assert (int(res.scale[i]), int(res.offset[i])) == (o["scale"], o["offset"]), k
+        assert [int(x) for x in res.buckets[i]] == [int(x) for x in o["counts"]], k
+        assert res.min[i] == o["min"] and res.max[i] == o["max"], k
+        assert abs(res.sum[i] - o["sum"]) <= 1e-9 * max(abs(o["sum"]), 1e-300), k
+
+
+def _engine(wl, **kw):
+    e = Engine(Config(n_services=wl.n_services, n_windows=16, **kw))
+    e.window_advance(wl.first_window)
+    return e
+
+
+def test_gpu_log_and_index_bit_exact():
+    kat = json.load(open(KAT))
+    rng = np.random.default_rng(3)
+    vals = np.concatenate([[float.fromhex(x) for x, _ in kat["go_log"] if float.fromhex(x) > 2.0 ** -1000],
+                           np.exp(rng.uniform(-14, 14, 20000)),
+                           rng.integers(1, 10**11, 20000) / 1e6])
+    scales = rng.integers(-6, 21, len(vals)).astype(np.int32)
+    with Engine(Config(exp_max_size=160)) as e:
+        idx, logs = e.expo_probe(vals, scales)
+    for v, s, i, lg in zip(vals, scales, idx, logs):
+        assert lg.hex() == pyoracle.go_log(v).hex(), v
+        assert int(i) == pyoracle.expo_index(v, int(s)), (v, s)
+    for d, s, i in kat["map_to_index_ms"]:
+        with Engine(Config(exp_max_size=160)) as e:
+            gi, _ = e.expo_probe([d / 1e6], [s])
+        assert int(gi[0]) == i
+
+
+@pytest.mark.parametrize("max_size,unit", [(160, "ms"), (8, "ms"), (20, "s"), (2, "ms")])
+def test_expo_histograms_match_oracle(max_size, unit):
+    wl = generate_c2(200_003, seed=13)
+    with _engine(wl, exp_max_size=max_size, unit=unit) as e:
+        e.ingest(wl.batch)
+        res = e.flush_exp()
+        _check(res, wl.batch, max_size, unit == "s")
+
+
+def test_expo_state_across_launches_and_delta_flushes():
+    """Several ingests before one flush (kept buckets merged down when a later
+    batch widens the range), then a second interval from scratch."""
+    wl = generate_c2(240_000, seed=17)
+    parts = [wl.batch.slice(0, 50_000), wl.batch.slice(50_000, 140_000), wl.batch.slice(140_000, 240_000)]
+    with _engine(wl, exp_max_size=12) as e:
+        e.ingest(parts[0])
+        e.ingest(parts[1])
+        first = SpanBatch(*[np.concatenate([a, b]) for a, b in zip(parts[0].columns(), parts[1].columns())])
+        _check(e.flush_exp(), first, 12)
+        e.ingest(parts[2])
+        _check(e.flush_exp(), parts[2], 12)
+        assert len(e.flush_exp().key_hash) == 0
+
+
+def test_expo_edges_zero_pow2_and_huge():
+    ds = [0, 0, 1, 999_999, 1_000_000, 1_000_001, 2_000_000, 4_000_000, 500_000, 60_000_000_000,
+          3_600_000_000_000, 7]
+    n = len(ds)
+    start = np.full(n, 10**18, dtype=np.uint64)
+    end = start + np.array(ds, dtype=np.uint64)
+    end[1] = start[1] - 5  # end <= start: duration 0 (A2)
+    batch = SpanBatch(np.array([11, 11, 11, 11, 11, 11, 22, 22, 22, 22, 22, 22], dtype=np.uint64), start, end,
+                      np.arange(n, dtype=np.uint64), np.arange(n, dtype=np.uint64), pack_meta([0] * n, 2, 0))
+    with Engine(Config(n_services=1, n_windows=16, exp_max_size=4)) as e:
+        e.window_advance(10**18 // 10**10)
+        e.ingest(batch)
+        _check(e.flush_exp(), batch, 4)
+
+
+def test_expo_sketches_unchanged():
+    wl = generate_c2(150_000, seed=23)
+    with _engine(wl, exp_max_size=160) as e:
+        e.ingest(wl.batch)
+        o = pyoracle.Oracle(n_services=wl.n_services)
+        o.ingest(wl.batch)
+        for wid in o.window_ids():
+            sk = e.window_read(wid)
+            hll, cms = o.window(wid)
+            assert np.array_equal(sk.hll, hll) and np.array_equal(sk.cms, cms), wid
+        with pytest.raises(_lib.SpanAggError) as ei:
+            e.flush()
+        assert ei.value.code == _lib.SA_ESTATE
