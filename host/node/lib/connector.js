@@ -28,6 +28,7 @@
 const addonLoader = require('./addon');
 const keys = require('./keys');
 const otlp = require('./otlp');
+const expohisto = require('./expohisto');
 const { applyRules } = require('./transform');
 
 const M64 = (1n << 64n) - 1n;
@@ -85,7 +86,12 @@ function normalizeConfig(cfg = {}, addon) {
   const hist = cfg.histogram || {};
   const unit = hist.unit || 'ms';
   if (unit !== 'ms' && unit !== 's') throw new Error(`histogram.unit must be ms or s, got ${unit}`);
-  if (hist.exponential) throw new Error('exponential histograms are not supported by this engine');
+  if (hist.exponential && hist.explicit) throw new Error('use either `explicit` or `exponential` buckets histogram');
+  // go-expohisto structure.DefaultMaxSize when max_size is unset; the engine takes 2..4096
+  const expMaxSize = hist.exponential ? (hist.exponential.max_size || 160) : 0;
+  if (hist.exponential && !(Number.isInteger(expMaxSize) && expMaxSize >= 2 && expMaxSize <= 4096)) {
+    throw new Error(`histogram.exponential.max_size must be 2..4096, got ${hist.exponential.max_size}`);
+  }
   const div = unit === 's' ? 1e9 : 1e6;
   let bounds = d.bounds.slice();
   if (hist.explicit && Array.isArray(hist.explicit.buckets)) {
@@ -99,7 +105,7 @@ function normalizeConfig(cfg = {}, addon) {
   const sk = cfg.sketches || {};
   const windowNs = sk.window !== undefined ? BigInt(Math.round(parseDurationNs(sk.window))) : d.windowNs;
   return {
-    unit, bounds, dims,
+    unit, bounds, dims, expMaxSize,
     exclude: new Set(cfg.exclude_dimensions || []),
     temporality: TEMPORALITY[temporality],
     namespace: cfg.namespace === undefined ? 'traces.span.metrics' : cfg.namespace,
@@ -161,7 +167,7 @@ class SpanMetricsConnector {
     const c = this.cfg;
     this.handle = this.addon.create({ bounds: c.bounds, unit: c.unit, hllP: c.hllP, cmsD: c.cmsD,
       cmsW: c.cmsW, windowNs: c.windowNs, nWindows: c.nWindows, nServices: c.nServices,
-      keyCapacity: c.keyCapacity, device: c.device, ...(c.devices ? { devices: c.devices } : {}) });
+      keyCapacity: c.keyCapacity, device: c.device, expMaxSize: c.expMaxSize, ...(c.devices ? { devices: c.devices } : {}) });
     this.cols = new Columns(c.batchSize);
     // native OTLP columnizer (binding/otlp_columnizer.cc) for request bytes, when
     // every enabled option is one it implements; otherwise the JS path below
@@ -497,7 +503,8 @@ class SpanMetricsConnector {
     if (!this.handle) throw new Error('connector is shut down');
     this._drain();
     const now = this.clock();
-    const r = this.addon.flush(this.handle);
+    const expo = this.cfg.expMaxSize !== 0;
+    const r = expo ? this.addon.flushExp(this.handle) : this.addon.flush(this.handle);
     if (r.status === this.addon.status.EFULL) this.droppedFlushes += 1;
     const nb = r.nBuckets;
     const delta = this.cfg.temporality === otlp.AGGREGATION_TEMPORALITY.DELTA;
@@ -505,9 +512,15 @@ class SpanMetricsConnector {
     for (let i = 0; i < r.nSeries; i++) {
       const s = this.series.get(r.keyHash[i]);
       if (s === undefined) continue;  // evicted and dropped since; its delta is discarded
-      if (delta || s.counts === null) { s.counts = new Array(nb).fill(0n); s.sumNs = 0n; }
-      for (let b = 0; b < nb; b++) s.counts[b] += r.bucketCounts[i * nb + b];
-      s.sumNs += r.sumNs[i];
+      if (expo) {
+        // s.counts holds the series' go-expohisto state in this mode
+        if (delta || s.counts === null) s.counts = expohisto.empty();
+        expohisto.fold(s.counts, expohisto.fromResult(r, i), this.cfg.expMaxSize);
+      } else {
+        if (delta || s.counts === null) { s.counts = new Array(nb).fill(0n); s.sumNs = 0n; }
+        for (let b = 0; b < nb; b++) s.counts[b] += r.bucketCounts[i * nb + b];
+        s.sumNs += r.sumNs[i];
+      }
       touched.add(s.sid);
     }
     const resourceMetrics = [];
@@ -551,22 +564,31 @@ class SpanMetricsConnector {
         if (last !== undefined) start = last;
         this.lastDeltaTs.set(sid, now);
       }
+      const e = c.expMaxSize ? s.counts : null;
       let count = 0n;
-      for (const x of s.counts) count += x;
+      if (e) count = e.count;
+      else for (const x of s.counts) count += x;
       if (s.kind === 'event') {
         events.push({ attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, asInt: count });
         continue;
       }
       calls.push({ attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, asInt: count });
-      const h = { attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, count,
-        sum: Number(s.sumNs) / div, bucketCounts: s.counts.slice(), explicitBounds: c.bounds };
+      const h = e
+        ? { attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, count, sum: Number(e.sumNs) / div,
+          scale: e.scale, zeroCount: e.zeroCount, positive: { offset: e.offset, bucketCounts: e.counts.slice() },
+          ...(count ? { min: e.min, max: e.max } : {}) }
+        : { attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, count,
+          sum: Number(s.sumNs) / div, bucketCounts: s.counts.slice(), explicitBounds: c.bounds };
       if (s.exemplars.length) h.exemplars = s.exemplars;
       hists.push(h);
       s.exemplars = [];  // exemplars cover one export interval, both temporalities
     }
     const out = [
       { name: ns + 'calls', sum: { dataPoints: calls, aggregationTemporality: temporality, isMonotonic: true } },
-      { name: ns + 'duration', unit: c.unit, histogram: { dataPoints: hists, aggregationTemporality: temporality } },
+      c.expMaxSize
+        ? { name: ns + 'duration', unit: c.unit,
+          exponentialHistogram: { dataPoints: hists, aggregationTemporality: temporality } }
+        : { name: ns + 'duration', unit: c.unit, histogram: { dataPoints: hists, aggregationTemporality: temporality } },
     ];
     if (c.events) {
       out.push({ name: ns + 'events', sum: { dataPoints: events, aggregationTemporality: temporality,

@@ -287,6 +287,7 @@ class Writer {
   fBool(f, v) { if (v) this.tag(f, WT_VARINT).varint(1); return this; }
   fFixed64(f, v) { if (v) this.tag(f, WT_I64).fixed64(v); return this; }
   fFixed32(f, v) { if (v) this.tag(f, WT_I32).fixed32(v); return this; }
+  fSint32(f, v) { if (v) this.tag(f, WT_VARINT).varint(((v << 1) ^ (v >> 31)) >>> 0); return this; }
   fMsg(f, encodeFn, obj) {
     const w = new Writer();
     encodeFn(w, obj);
@@ -395,6 +396,33 @@ function encodeHistogramDataPoint(w, dp) {
   for (const ex of dp.exemplars || []) w.fMsg(8, encodeExemplar, ex);
 }
 
+function encodeExpoBuckets(w, b) {
+  w.fSint32(1, b.offset || 0);
+  const counts = b.bucketCounts || [];
+  if (counts.length) {
+    const p = new Writer();
+    for (const c of counts) p.varint(BigInt(c));
+    w.tag(2, WT_LEN).bytes(p.finish());
+  }
+}
+
+/** ExponentialHistogramDataPoint (metrics.proto v1); positive/negative always
+ * present, as pdata's non-nullable Buckets marshal. */
+function encodeExpoHistogramDataPoint(w, dp) {
+  for (const kv of dp.attributes || []) w.fMsg(1, encodeKeyValue, kv);
+  w.fFixed64(2, dp.startTimeUnixNano);
+  w.fFixed64(3, dp.timeUnixNano);
+  w.fFixed64(4, dp.count);
+  if (dp.sum !== undefined) w.tag(5, WT_I64).double(dp.sum);
+  w.fSint32(6, dp.scale || 0);
+  w.fFixed64(7, dp.zeroCount);
+  w.fMsg(8, encodeExpoBuckets, dp.positive || {});
+  w.fMsg(9, encodeExpoBuckets, dp.negative || {});
+  for (const ex of dp.exemplars || []) w.fMsg(11, encodeExemplar, ex);
+  if (dp.min !== undefined) w.tag(12, WT_I64).double(dp.min);
+  if (dp.max !== undefined) w.tag(13, WT_I64).double(dp.max);
+}
+
 function encodeExemplar(w, ex) {
   w.fFixed64(2, ex.timeUnixNano);
   if (ex.asInt !== undefined) w.tag(6, WT_I64).fixed64(BigInt.asUintN(64, BigInt(ex.asInt)));
@@ -423,6 +451,11 @@ function encodeMetric(w, m) {
       for (const dp of h.dataPoints || []) ww.fMsg(1, encodeHistogramDataPoint, dp);
       ww.fVarint(2, h.aggregationTemporality);
     }, m.histogram);
+  } else if (m.exponentialHistogram) {
+    w.fMsg(10, (ww, h) => {
+      for (const dp of h.dataPoints || []) ww.fMsg(1, encodeExpoHistogramDataPoint, dp);
+      ww.fVarint(2, h.aggregationTemporality);
+    }, m.exponentialHistogram);
   }
 }
 
@@ -503,12 +536,55 @@ function decodeHistogramDataPoint(r) {
   return dp;
 }
 
+function decodeExpoBuckets(r) {
+  const b = { offset: 0, bucketCounts: [] };
+  r.fields((f, wt) => {
+    if (f === 1 && wt === WT_VARINT) { const z = r.varint(); b.offset = z % 2 ? -(z + 1) / 2 : z / 2; return true; }
+    if (f === 2 && wt === WT_LEN) { const s = r.sub(); while (!s.eof()) b.bucketCounts.push(s.varint64()); return true; }
+    if (f === 2 && wt === WT_VARINT) { b.bucketCounts.push(r.varint64()); return true; }
+    return false;
+  });
+  return b;
+}
+
+function decodeExpoHistogramDataPoint(r) {
+  const dp = { attributes: [], startTimeUnixNano: 0n, timeUnixNano: 0n, count: 0n, scale: 0, zeroCount: 0n,
+    positive: { offset: 0, bucketCounts: [] }, negative: { offset: 0, bucketCounts: [] } };
+  r.fields((f, wt) => {
+    if (f === 1 && wt === WT_LEN) { dp.attributes.push(decodeKeyValue(r.sub())); return true; }
+    if (f === 2 && wt === WT_I64) { dp.startTimeUnixNano = r.fixed64(); return true; }
+    if (f === 3 && wt === WT_I64) { dp.timeUnixNano = r.fixed64(); return true; }
+    if (f === 4 && wt === WT_I64) { dp.count = r.fixed64(); return true; }
+    if (f === 5 && wt === WT_I64) { dp.sum = r.double(); return true; }
+    if (f === 6 && wt === WT_VARINT) { const z = r.varint(); dp.scale = z % 2 ? -(z + 1) / 2 : z / 2; return true; }
+    if (f === 7 && wt === WT_I64) { dp.zeroCount = r.fixed64(); return true; }
+    if (f === 8 && wt === WT_LEN) { dp.positive = decodeExpoBuckets(r.sub()); return true; }
+    if (f === 9 && wt === WT_LEN) { dp.negative = decodeExpoBuckets(r.sub()); return true; }
+    if (f === 11 && wt === WT_LEN) { (dp.exemplars = dp.exemplars || []).push(decodeExemplar(r.sub())); return true; }
+    if (f === 12 && wt === WT_I64) { dp.min = r.double(); return true; }
+    if (f === 13 && wt === WT_I64) { dp.max = r.double(); return true; }
+    return false;
+  });
+  return dp;
+}
+
 function decodeMetric(r) {
   const m = { name: '', description: '', unit: '' };
   r.fields((f, wt) => {
     if (f === 1 && wt === WT_LEN) { m.name = r.string(); return true; }
     if (f === 2 && wt === WT_LEN) { m.description = r.string(); return true; }
     if (f === 3 && wt === WT_LEN) { m.unit = r.string(); return true; }
+    if (f === 10 && wt === WT_LEN) {
+      const body = { dataPoints: [], aggregationTemporality: 0 };
+      const s = r.sub();
+      s.fields((g, wt2) => {
+        if (g === 1 && wt2 === WT_LEN) { body.dataPoints.push(decodeExpoHistogramDataPoint(s.sub())); return true; }
+        if (g === 2 && wt2 === WT_VARINT) { body.aggregationTemporality = s.varint(); return true; }
+        return false;
+      });
+      m.exponentialHistogram = body;
+      return true;
+    }
     if ((f === 5 || f === 7 || f === 9) && wt === WT_LEN) {
       const body = { dataPoints: [] };
       if (f !== 5) body.aggregationTemporality = 0;
@@ -531,7 +607,7 @@ function decodeMetric(r) {
   return m;
 }
 
-/** ExportMetricsServiceRequest bytes -> {resourceMetrics: [...]} (Gauge, Sum and Histogram). */
+/** ExportMetricsServiceRequest bytes -> {resourceMetrics: [...]} (Gauge, Sum, Histogram, ExponentialHistogram). */
 function decodeMetrics(buf) {
   const b = Buffer.isBuffer(buf) ? buf : Buffer.from(buf.buffer, buf.byteOffset, buf.byteLength);
   const r = new Reader(b);

@@ -9,6 +9,7 @@
  */
 const { xxh64 } = require('../lib/xxh64');
 const { splitmix64 } = require('../lib/connector');
+const { Histogram } = require('./expo_ref');
 
 const DEFAULT_BOUNDS = [2, 4, 6, 8, 10, 50, 100, 200, 400, 800, 1000, 1400, 2000, 5000, 10000, 15000];
 const CMS_SEED = [0x9E3779B97F4A7C15n, 0xBF58476D1CE4E5B9n, 0x94D049BB133111EBn,
@@ -68,8 +69,15 @@ class FakeAddon {
       const sid = b.keyHash[i];
       const d = b.endNs[i] > b.startNs[i] ? b.endNs[i] - b.startNs[i] : 0n;
       let r = this.red.get(sid);
-      if (!r) { r = { counts: new Array(nb).fill(0n), sumNs: 0n }; this.red.set(sid, r); }
+      if (!r) {
+        r = { counts: new Array(nb).fill(0n), sumNs: 0n, expo: new Histogram(this.cfg.expMaxSize || 160),
+          minNs: 0n, maxNs: 0n };
+        this.red.set(sid, r);
+      }
       r.counts[this._bucket(Number(d))] += 1n;
+      if (r.expo.count === 0n || d < r.minNs) r.minNs = d;
+      if (r.expo.count === 0n || d > r.maxNs) r.maxNs = d;
+      r.expo.update(Number(d) / this.div);
       r.sumNs += d;
       const svc = b.meta[i] & 0xFFFF, status = (b.meta[i] >>> 19) & 3;
       const wid = b.endNs[i] / this.cfg.windowNs;
@@ -104,6 +112,29 @@ class FakeAddon {
       r.counts.forEach((c, j) => { out.bucketCounts[i * nb + j] = c; out.calls[i] += c; });
       out.sumNs[i] = r.sumNs;
       out.sum[i] = Number(r.sumNs) / this.div;
+    });
+    this.red.clear();
+    return out;
+  }
+  flushExp() {
+    if (!this.cfg.expMaxSize) {
+      const e = new Error('sa_flush_exp: engine built for explicit buckets');
+      e.code = this.status.ESTATE;
+      throw e;
+    }
+    const keysSorted = [...this.red.keys()].sort((a, b) => (a < b ? -1 : a > b ? 1 : 0));
+    const m = this.cfg.expMaxSize, n = keysSorted.length;
+    const out = { status: 0, nSeries: n, maxSize: m, keyHash: new BigUint64Array(keysSorted),
+      count: new BigUint64Array(n), zeroCount: new BigUint64Array(n), sumNs: new BigUint64Array(n),
+      sum: new Float64Array(n), min: new Float64Array(n), max: new Float64Array(n), scale: new Int32Array(n),
+      offset: new Int32Array(n), nBuckets: new Uint32Array(n), bucketCounts: new BigUint64Array(n * m) };
+    keysSorted.forEach((k, i) => {
+      const r = this.red.get(k), h = r.expo, b = h.buckets();
+      out.count[i] = h.count; out.zeroCount[i] = h.zero; out.sumNs[i] = r.sumNs;
+      out.sum[i] = Number(r.sumNs) / this.div;
+      out.min[i] = Number(r.minNs) / this.div; out.max[i] = Number(r.maxNs) / this.div;
+      out.scale[i] = h.scale; out.offset[i] = b.offset; out.nBuckets[i] = b.counts.length;
+      b.counts.forEach((c, j) => { out.bucketCounts[i * m + j] = c; });
     });
     this.red.clear();
     return out;

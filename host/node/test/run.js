@@ -92,6 +92,45 @@ test('otlp metrics encode/decode round trip (sum, histogram, gauge)', () => {
   assert.strictEqual(g.gauge.dataPoints[0].asDouble, 1.5);
 });
 
+test('otlp exponential histogram round trip (negative scale/offset, zero count, min/max)', () => {
+  const dp = { attributes: [{ key: 'span.name', value: str('a') }], startTimeUnixNano: 5n, timeUnixNano: 9n,
+    count: 7n, sum: 12.5, scale: -3, zeroCount: 2n, positive: { offset: -17, bucketCounts: [1n, 0n, 300n] },
+    min: 0, max: 9.75 };
+  const req = { resourceMetrics: [{ resource: { attributes: [] }, scopeMetrics: [{ scope: { name: 's' },
+    metrics: [{ name: 'duration', unit: 'ms', exponentialHistogram: { aggregationTemporality: 2, dataPoints: [dp] } }] }] }] };
+  const m = otlp.decodeMetrics(otlp.encodeMetrics(req)).resourceMetrics[0].scopeMetrics[0].metrics[0];
+  assert.strictEqual(m.exponentialHistogram.aggregationTemporality, 2);
+  const d = m.exponentialHistogram.dataPoints[0];
+  assert.deepStrictEqual([d.count, d.sum, d.scale, d.zeroCount, d.min, d.max], [7n, 12.5, -3, 2n, 0, 9.75]);
+  assert.deepStrictEqual(d.positive, { offset: -17, bucketCounts: [1n, 0n, 300n] });
+  assert.deepStrictEqual(d.negative, { offset: 0, bucketCounts: [] });
+});
+
+test('expo restatement (test/expo_ref.js) matches the golden go-expohisto vectors', () => {
+  const kat = JSON.parse(require('fs').readFileSync(path.join(__dirname, '..', '..', '..', 'tests', 'golden',
+    'expo_kat.json'), 'utf8'));
+  const { goLog, mapToIndex, Histogram } = require('./expo_ref');
+  for (const [x, y] of kat.go_log) assert.strictEqual(goLog(parseHexFloat(x)), parseHexFloat(y), x);
+  for (const [d, sc, i] of kat.map_to_index_ms) assert.strictEqual(mapToIndex(d / 1e6, sc), i, `${d} ${sc}`);
+  for (const c of kat.cases) {
+    const h = new Histogram(c.max_size), div = c.unit === 's' ? 1e9 : 1e6;
+    for (const d of c.durations_ns) h.update(d / div);
+    const b = h.buckets(), e = c.expected;
+    assert.deepStrictEqual([Number(h.count), Number(h.zero), h.scale, b.offset, b.counts.map(Number)],
+      [e.count, e.zero_count, e.scale, e.offset, e.counts], c.name);
+    assert.strictEqual(h.sum, parseHexFloat(e.sum), c.name);
+  }
+});
+
+/** Python float.hex() text -> Number. */
+function parseHexFloat(h) {
+  const m = /^(-?)0x([01])\.([0-9a-f]*)p([+-]\d+)$/.exec(h);
+  if (!m) throw new Error(`bad hex float ${h}`);
+  const frac = m[3] ? Number.parseInt(m[3], 16) / 2 ** (4 * m[3].length) : 0;
+  const v = (Number(m[2]) + frac) * 2 ** Number(m[4]);
+  return m[1] ? -v : v;
+}
+
 // ------------------------------------------------------------- transform
 
 test('demo transform rules (A12)', () => {
@@ -136,6 +175,11 @@ test('config: durations, defaults and validation', () => {
   assert.deepStrictEqual(c2.bounds, [0.1, 1, 2]);
   assert.throws(() => normalizeConfig({ histogram: { unit: 'us' } }, fa));
   assert.throws(() => normalizeConfig({ aggregation_temporality: 'X' }, fa));
+  assert.strictEqual(normalizeConfig({ histogram: { exponential: {} } }, fa).expMaxSize, 160);
+  assert.strictEqual(normalizeConfig({ histogram: { exponential: { max_size: 40 } } }, fa).expMaxSize, 40);
+  assert.strictEqual(c.expMaxSize, 0);
+  assert.throws(() => normalizeConfig({ histogram: { exponential: {}, explicit: { buckets: [1] } } }, fa), /either/);
+  assert.throws(() => normalizeConfig({ histogram: { exponential: { max_size: 1 } } }, fa), /max_size/);
 });
 
 // ------------------------------------------------------------- addon
@@ -345,6 +389,54 @@ test('connector: exemplars carry trace/span ids and the duration, one export int
 });
 
 // ------------------------------------------------- native columnizer vs JavaScript
+
+function expoDps(req) {
+  return req.resourceMetrics.flatMap((rm) => rm.scopeMetrics[0].metrics
+    .filter((m) => m.exponentialHistogram).flatMap((m) => m.exponentialHistogram.dataPoints));
+}
+
+for (const temporality of ['AGGREGATION_TEMPORALITY_CUMULATIVE', 'AGGREGATION_TEMPORALITY_DELTA']) {
+  test(`connector: exponential histograms, ${temporality.slice(24).toLowerCase()} (host fold == one go-expohisto)`, () => {
+    const { Histogram } = require('./expo_ref');
+    const maxSize = 6;
+    const { conn, t } = mkConnector({ aggregation_temporality: temporality, histogram: { exponential: { max_size: maxSize } } });
+    const cumulative = temporality.endsWith('CUMULATIVE');
+    let rng = 12345;
+    const rand = () => { rng = (rng * 1103515245 + 12345) % 2147483648; return rng / 2147483648; };
+    const all = new Map([['x', new Histogram(maxSize)], ['y', new Histogram(maxSize)]]);
+    let mixedScales = 0;  // folds of a delta whose scale differs from the running histogram's
+    for (let round = 0; round < 4; round++) {
+      const interval = new Map([['x', new Histogram(maxSize)], ['y', new Histogram(maxSize)]]);
+      const spans = [];
+      for (let i = 0; i < 40; i++) {
+        const name = i % 3 ? 'x' : 'y';
+        // each round widens the range on a different side, forcing host-side downscales
+        const ns = i === 7 ? 0 : Math.round(Math.exp(rand() * (2 + round) + (round % 2 ? 10 : 16 - round)));
+        spans.push(span(name, { startTimeUnixNano: 1000000000000n, endTimeUnixNano: 1000000000000n + BigInt(ns) }));
+        all.get(name).update(ns / 1e6);
+        interval.get(name).update(ns / 1e6);
+      }
+      for (const [k, h] of interval) mixedScales += round > 0 && h.scale !== all.get(k).scale;
+      conn.consumeTraces(request([[{ 'service.name': 'a' }, spans]]));
+      t.now += 1000n;
+      const out = otlp.decodeMetrics(otlp.encodeMetrics(conn.exportMetrics()));
+      const dps = expoDps(out);
+      assert.strictEqual(dps.length, 2);
+      for (const dp of dps) {
+        const name = attr(dp, 'span.name').value;
+        const h = (cumulative ? all : interval).get(name), b = h.buckets();
+        assert.deepStrictEqual([dp.count, dp.zeroCount, dp.scale, dp.positive.offset, dp.positive.bucketCounts],
+          [h.count, h.zero, h.scale, b.offset, b.counts], `${name} round ${round}`);
+        assert.strictEqual(dp.min, h.min);
+        assert.strictEqual(dp.max, h.max);
+        assert.ok(Math.abs(dp.sum - h.sum) <= 1e-9 * h.sum);
+      }
+      const calls = dpsOf(out, 'traces.span.metrics.calls');
+      assert.deepStrictEqual(calls.map((d) => d.asInt).sort(), dps.map((d) => d.count).sort());
+    }
+    assert.ok(mixedScales >= 3, `fold exercised ${mixedScales} scale changes`);
+  });
+}
 
 const { NativeColumnizerFakeAddon } = require('./fake_addon');
 
