@@ -6,6 +6,11 @@
 #include <cmath>
 #include <cstring>
 #include <string_view>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 
 namespace otlpcol {
 namespace {
@@ -537,14 +542,133 @@ uint32_t Columnizer::service_id(const std::string &name, bool *is_new) {
   return id;
 }
 
+// ---------------------------------------------------------------- columns, caches, threads
+void Cols::truncate(size_t n) {
+  key.resize(n), start.resize(n), end.resize(n), w0.resize(n), w1.resize(n), meta.resize(n);
+}
+
+void Cols::append(const Cols &o, size_t off, size_t n) {
+  key.insert(key.end(), o.key.begin() + off, o.key.begin() + off + n);
+  start.insert(start.end(), o.start.begin() + off, o.start.begin() + off + n);
+  end.insert(end.end(), o.end.begin() + off, o.end.begin() + off + n);
+  w0.insert(w0.end(), o.w0.begin() + off, o.w0.begin() + off + n);
+  w1.insert(w1.end(), o.w1.begin() + off, o.w1.begin() + off + n);
+  meta.insert(meta.end(), o.meta.begin() + off, o.meta.begin() + off + n);
+}
+
+uint64_t SigCache::hash(uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code) {
+  const uint64_t seed = rhash ^ ((uint64_t)svc << 40) ^ ((uint64_t)(uint32_t)kind << 8) ^ (uint32_t)code;
+  return xxh64(name.data(), name.size(), seed) | 1;  // 0 never names a used slot
+}
+
+const uint64_t *SigCache::find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
+                               int32_t code) const {
+  if (t_.empty()) return nullptr;
+  const size_t mask = t_.size() - 1;
+  for (size_t i = h & mask;; i = (i + 1) & mask) {
+    const Entry &e = t_[i];
+    if (!e.used) return nullptr;
+    if (e.h == h && e.rhash == rhash && e.svc == svc && e.kind == kind && e.code == code && e.name == name)
+      return &e.sid;
+  }
+}
+
+void SigCache::insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
+                      int32_t code, uint64_t sid) {
+  if (2 * (n_ + 1) > t_.size()) {  // load <= 1/2
+    std::vector<Entry> old;
+    old.swap(t_);
+    t_.resize(old.empty() ? 256 : old.size() * 2);
+    n_ = 0;
+    for (Entry &e : old)
+      if (e.used) insert(e.h, e.rhash, e.svc, e.name, e.kind, e.code, e.sid);
+  }
+  const size_t mask = t_.size() - 1;
+  size_t i = h & mask;
+  while (t_[i].used) i = (i + 1) & mask;
+  Entry &e = t_[i];
+  e.h = h, e.rhash = rhash, e.sid = sid, e.svc = svc, e.kind = kind, e.code = code, e.used = true;
+  e.name.assign(name);
+  ++n_;
+}
+
+struct Columnizer::Worker {
+  Cols cols;
+  SigCache cache;
+  std::vector<Attr> rattrs, sattrs;
+  std::vector<const Attr *> hv;
+  std::string tmp, keystr, sname, service;
+  std::vector<uint8_t> hbuf;
+};
+
+struct Columnizer::Undo {
+  std::vector<std::pair<uint64_t, std::string>> keys;
+  std::vector<uint64_t> sids, resources;
+  std::vector<std::string> services;
+};
+
+// threads 1..n-1 of a fork-join over one job; thread 0 is the caller
+struct Columnizer::Pool {
+  std::vector<std::thread> th;
+  std::mutex m;
+  std::condition_variable go, done;
+  const std::function<void(unsigned)> *job = nullptr;
+  uint64_t epoch = 0;
+  unsigned active = 0, running = 0;
+  bool stop = false;
+
+  explicit Pool(unsigned n) {
+    for (unsigned i = 1; i < n; ++i) th.emplace_back([this, i] { loop(i); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> l(m);
+      stop = true;
+    }
+    go.notify_all();
+    for (auto &t : th) t.join();
+  }
+  void loop(unsigned id) {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> l(m);
+    for (;;) {
+      go.wait(l, [&] { return stop || epoch != seen; });
+      if (stop) return;
+      seen = epoch;
+      const auto *j = job;
+      const bool mine = id < active;
+      l.unlock();
+      if (mine) (*j)(id);
+      l.lock();
+      if (--running == 0) done.notify_one();
+    }
+  }
+  void run(unsigned n, const std::function<void(unsigned)> &f) {
+    {
+      std::lock_guard<std::mutex> l(m);
+      job = &f, active = n, running = (unsigned)th.size();
+      ++epoch;
+    }
+    go.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> l(m);
+    done.wait(l, [&] { return running == 0; });
+  }
+};
+
+Columnizer::Columnizer(Options o) : opt_(std::move(o)), main_(new Worker) {}
+Columnizer::~Columnizer() = default;
+
 void Columnizer::learn(uint64_t rhash, const std::string &key, uint64_t sid) {
   res_keys_[rhash][key] = sid;
   owner_[sid] = std::make_pair(rhash, key);
+  ++gen_;
 }
 
 void Columnizer::remap(uint64_t from, uint64_t to) {
-  for (uint64_t &k : key_)
+  for (uint64_t &k : buf_.key)
     if (k == from) k = to;
+  ++gen_;
   auto o = owner_.find(from);
   if (o == owner_.end()) return;
   const auto who = o->second;
@@ -553,38 +677,25 @@ void Columnizer::remap(uint64_t from, uint64_t to) {
   res_keys_[who.first][who.second] = to;
 }
 
-Result Columnizer::columnize(const uint8_t *buf, size_t len) {
-  Result res;
-  const size_t n0 = key_.size();
-  const uint64_t max0 = max_end_;
-  // dictionary entries made by this call: committed only on success
-  std::vector<std::pair<uint64_t, std::string>> added_keys;
-  std::vector<uint64_t> added_sids;
-  std::vector<std::string> added_services;
-  std::vector<uint64_t> added_resources;
-
-  auto rollback = [&](Result::Status st, const char *why) {
-    key_.resize(n0); start_.resize(n0); end_.resize(n0); w0_.resize(n0); w1_.resize(n0); meta_.resize(n0);
-    max_end_ = max0;
-    for (auto &k : added_keys) {
-      auto it = res_keys_.find(k.first);
-      if (it != res_keys_.end()) it->second.erase(k.second);
-    }
-    for (uint64_t h : added_resources) res_keys_.erase(h);
-    for (uint64_t sid : added_sids) owner_.erase(sid);
-    for (auto &s : added_services) services_.erase(s);
-    Result r;
-    r.status = st;
-    r.error = why;
-    return r;
+// One request into `out`.  kShared (worker threads): the dictionaries are
+// read-only, and anything not already in them -- a new resource, service or
+// series -- or any failure returns false with nothing reported (the request is
+// redone exclusively).  Exclusive: new entries go into the dictionaries and
+// `undo`; false = res.status / res.error say why (the caller rolls back).
+template <bool kShared>
+bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCache &cache, Result &res,
+                     Undo *undo) {
+  auto fail = [&](Result::Status st, const char *why) {
+    if constexpr (!kShared) res.status = st, res.error = why;
+    return false;
   };
-
+  auto &rattrs = w.rattrs, &sattrs = w.sattrs;
+  std::string &tmp = w.tmp, &keystr = w.keystr, &sname = w.sname, &service = w.service;
+  auto &hbuf = w.hbuf;
+  const bool use_cache = opt_.dims.empty();
   PB req(buf, buf + len);
   uint32_t f;
   int wt;
-  std::vector<Attr> rattrs, sattrs;
-  std::string tmp, keystr, sname;
-  std::vector<uint8_t> hbuf;
   while (req.next(f, wt)) {
     if (f != 1 || wt != 2) {
       req.skip(wt);
@@ -602,7 +713,7 @@ Result Columnizer::columnize(const uint8_t *buf, size_t len) {
         if (g == 1 && wt2 == 2) resource = scan.sub(), has_resource = true;
         else scan.skip(wt2);
       }
-      if (!scan.ok) return rollback(Result::kError, "malformed ResourceSpans");
+      if (!scan.ok) return fail(Result::kError, "malformed ResourceSpans");
     }
     rattrs.clear();
     if (has_resource) {
@@ -612,25 +723,26 @@ Result Columnizer::columnize(const uint8_t *buf, size_t len) {
       while (r.next(g, wt2)) {
         if (g == 1 && wt2 == 2) {
           Attr a;
-          if (!parse_kv(r.sub(), a.key, a.val)) return rollback(Result::kError, "malformed KeyValue");
-          if (!valid_utf8(a.key)) return rollback(Result::kFallback, "non-UTF-8 attribute key");
+          if (!parse_kv(r.sub(), a.key, a.val)) return fail(Result::kError, "malformed KeyValue");
+          if (!valid_utf8(a.key)) return fail(Result::kFallback, "non-UTF-8 attribute key");
           rattrs.push_back(a);
         } else {
           r.skip(wt2);
         }
       }
-      if (!r.ok) return rollback(Result::kError, "malformed Resource");
+      if (!r.ok) return fail(Result::kError, "malformed Resource");
     }
     dedupe_last(rattrs);
     const Any *svc = find_attr(rattrs, "service.name");
     if (!svc) continue;  // A1: a resource without service.name contributes nothing
-    std::string service;
+    service.clear();
     if (svc->type == kStr) {
-      if (!valid_utf8(svc->s)) return rollback(Result::kFallback, "non-UTF-8 service.name");
+      if (!valid_utf8(svc->s)) return fail(Result::kFallback, "non-UTF-8 service.name");
       service.assign(svc->s);
     }
     // resource identity (keys.js resourceHash over the key attributes)
-    std::vector<const Attr *> hv;
+    auto &hv = w.hv;
+    hv.clear();
     for (const Attr &a : rattrs) {
       if (opt_.key_attributes.empty() ||
           std::find(opt_.key_attributes.begin(), opt_.key_attributes.end(), a.key) != opt_.key_attributes.end())
@@ -640,8 +752,8 @@ Result Columnizer::columnize(const uint8_t *buf, size_t len) {
     hbuf.clear();
     for (const Attr *a : hv) {
       if (const Keyable k = as_string(a->val, tmp); k != Keyable::kYes)
-        return k == Keyable::kTooDeep ? rollback(Result::kError, "attribute value nested too deeply")
-                                      : rollback(Result::kFallback, "resource attribute not keyable natively");
+        return k == Keyable::kTooDeep ? fail(Result::kError, "attribute value nested too deeply")
+                                      : fail(Result::kFallback, "resource attribute not keyable natively");
       hbuf.insert(hbuf.end(), a->key.begin(), a->key.end());
       hbuf.push_back(0);
       hbuf.insert(hbuf.end(), tmp.begin(), tmp.end());
@@ -653,18 +765,26 @@ Result Columnizer::columnize(const uint8_t *buf, size_t len) {
     const uint64_t rhash = xxh64(hbuf.data(), hbuf.size(), 0);
     auto rit = res_keys_.find(rhash);
     if (rit == res_keys_.end()) {
+      if constexpr (kShared) return false;
       rit = res_keys_.emplace(rhash, std::unordered_map<std::string, uint64_t>{}).first;
-      added_resources.push_back(rhash);
+      undo->resources.push_back(rhash);
       res.new_resources.push_back({rhash, has_resource ? (int64_t)(resource.p - buf) : -1,
                                    has_resource ? (uint32_t)(resource.end - resource.p) : 0u});
     }
     auto &keys = rit->second;
     res.resources.push_back(rhash);
-    bool svc_new = false;
-    const uint32_t svc_id = service_id(service, &svc_new);
-    if (svc_new) {
-      added_services.push_back(service);
-      res.new_services.emplace_back(service, svc_id);
+    uint32_t svc_id;
+    if constexpr (kShared) {
+      auto it = services_.find(service);
+      if (it == services_.end()) return false;
+      svc_id = it->second;
+    } else {
+      bool svc_new = false;
+      svc_id = service_id(service, &svc_new);
+      if (svc_new) {
+        undo->services.push_back(service);
+        res.new_services.emplace_back(service, svc_id);
+      }
     }
 
     // pass 2: scope_spans -> spans
@@ -709,7 +829,7 @@ Result Columnizer::columnize(const uint8_t *buf, size_t len) {
             en = sp.fixed64();
           } else if (k == 9 && wt4 == 2 && !opt_.dims.empty()) {
             Attr a;
-            if (!parse_kv(sp.sub(), a.key, a.val)) return rollback(Result::kError, "malformed KeyValue");
+            if (!parse_kv(sp.sub(), a.key, a.val)) return fail(Result::kError, "malformed KeyValue");
             sattrs.push_back(a);
           } else if (k == 15 && wt4 == 2) {
             PB stt = sp.sub();
@@ -720,87 +840,224 @@ Result Columnizer::columnize(const uint8_t *buf, size_t len) {
               if (m == 3 && wt5 == 0) code = (int32_t)(uint32_t)stt.varint();
               else stt.skip(wt5);
             }
-            if (!stt.ok) return rollback(Result::kError, "malformed Status");
+            if (!stt.ok) return fail(Result::kError, "malformed Status");
           } else {
             sp.skip(wt4);
           }
         }
-        if (!sp.ok) return rollback(Result::kError, "malformed Span");
-        if (!valid_utf8(name)) return rollback(Result::kFallback, "non-UTF-8 span name");
-        sname = apply_rules(opt_.rules, std::string(name));
-        // key = buildKey
-        keystr.clear();
-        bool first = true;
-        auto part = [&](const std::string &s) {
-          if (!first) keystr += '\0';
-          first = false;
-          keystr += s;
-        };
-        if (!opt_.ex_service) part(service);
-        if (!opt_.ex_name) part(sname);
-        if (!opt_.ex_kind) part(kind >= 0 && kind < 6 ? kKindStr[kind] : "");
-        if (!opt_.ex_status) part(code >= 0 && code < 3 ? kStatusStr[code] : "");
-        for (const Dim &d : opt_.dims) {
-          const Any *v = find_attr(sattrs, d.name);
-          if (!v) v = find_attr(rattrs, d.name);
-          if (v) {
-            if (const Keyable k = as_string(*v, tmp); k != Keyable::kYes)
-              return k == Keyable::kTooDeep ? rollback(Result::kError, "attribute value nested too deeply")
-                                            : rollback(Result::kFallback, "dimension value not keyable natively");
-          } else if (d.has_default) {
-            tmp = d.def;
-          } else {
-            continue;  // A5: missing optional dimension, no separator
-          }
-          keystr += '\0';
-          keystr += tmp;
-        }
+        if (!sp.ok) return fail(Result::kError, "malformed Span");
         uint64_t sid;
-        auto kit = keys.find(keystr);
-        if (kit != keys.end()) {
-          sid = kit->second;
-        } else {
-          hbuf.resize(8 + keystr.size());
-          std::memcpy(hbuf.data(), &rhash, 8);
-          std::memcpy(hbuf.data() + 8, keystr.data(), keystr.size());
-          // seed 0, 1, ... until the id is neither 0 (reserved) nor another series'
-          for (uint64_t seed = 0;; ++seed) {
-            sid = (opt_.test_collide_seed0 && seed == 0) ? 42 : xxh64(hbuf.data(), hbuf.size(), seed);
-            if (sid == 0) continue;
-            auto o = owner_.find(sid);
-            if (o == owner_.end()) {
-              owner_.emplace(sid, std::make_pair(rhash, keystr));
-              added_sids.push_back(sid);
-              break;
-            }
-            if (o->second.first == rhash && o->second.second == keystr) break;
-          }
-          keys.emplace(keystr, sid);
-          added_keys.emplace_back(rhash, keystr);
-          res.new_series.push_back({sid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});
+        uint64_t sig = 0;
+        const uint64_t *hit = nullptr;
+        if (use_cache) {
+          sig = SigCache::hash(rhash, svc_id, name, kind, code);
+          hit = cache.find(sig, rhash, svc_id, name, kind, code);
         }
-        key_.push_back(sid);
-        start_.push_back(st);
-        end_.push_back(en);
-        if (en > max_end_) max_end_ = en;
-        if (tid && tid_len == 16) {
-          w0_.push_back(rd64(tid));
-          w1_.push_back(rd64(tid + 8));
+        if (hit) {
+          sid = *hit;
         } else {
-          w0_.push_back(0);
-          w1_.push_back(0);
+          if (!valid_utf8(name)) return fail(Result::kFallback, "non-UTF-8 span name");
+          sname = apply_rules(opt_.rules, std::string(name));
+          // key = buildKey
+          keystr.clear();
+          bool first = true;
+          auto part = [&](std::string_view s) {
+            if (!first) keystr += '\0';
+            first = false;
+            keystr += s;
+          };
+          if (!opt_.ex_service) part(service);
+          if (!opt_.ex_name) part(sname);
+          if (!opt_.ex_kind) part(kind >= 0 && kind < 6 ? kKindStr[kind] : "");
+          if (!opt_.ex_status) part(code >= 0 && code < 3 ? kStatusStr[code] : "");
+          for (const Dim &d : opt_.dims) {
+            const Any *v = find_attr(sattrs, d.name);
+            if (!v) v = find_attr(rattrs, d.name);
+            if (v) {
+              if (const Keyable kb = as_string(*v, tmp); kb != Keyable::kYes)
+                return kb == Keyable::kTooDeep ? fail(Result::kError, "attribute value nested too deeply")
+                                               : fail(Result::kFallback, "dimension value not keyable natively");
+            } else if (d.has_default) {
+              tmp = d.def;
+            } else {
+              continue;  // A5: missing optional dimension, no separator
+            }
+            keystr += '\0';
+            keystr += tmp;
+          }
+          auto kit = keys.find(keystr);
+          if (kit != keys.end()) {
+            sid = kit->second;
+          } else {
+            if constexpr (kShared) return false;
+            hbuf.resize(8 + keystr.size());
+            std::memcpy(hbuf.data(), &rhash, 8);
+            std::memcpy(hbuf.data() + 8, keystr.data(), keystr.size());
+            // seed 0, 1, ... until the id is neither 0 (reserved) nor another series'
+            for (uint64_t seed = 0;; ++seed) {
+              sid = (opt_.test_collide_seed0 && seed == 0) ? 42 : xxh64(hbuf.data(), hbuf.size(), seed);
+              if (sid == 0) continue;
+              auto o = owner_.find(sid);
+              if (o == owner_.end()) {
+                owner_.emplace(sid, std::make_pair(rhash, keystr));
+                undo->sids.push_back(sid);
+                break;
+              }
+              if (o->second.first == rhash && o->second.second == keystr) break;
+            }
+            keys.emplace(keystr, sid);
+            undo->keys.emplace_back(rhash, keystr);
+            res.new_series.push_back(
+                {sid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});
+          }
+          if (use_cache) cache.insert(sig, rhash, svc_id, name, kind, code, sid);
+        }
+        out.key.push_back(sid);
+        out.start.push_back(st);
+        out.end.push_back(en);
+        if (en > out.max_end) out.max_end = en;
+        if (tid && tid_len == 16) {
+          out.w0.push_back(rd64(tid));
+          out.w1.push_back(rd64(tid + 8));
+        } else {
+          out.w0.push_back(0);
+          out.w1.push_back(0);
         }
         const uint32_t kk = kind >= 0 && kind <= 7 ? (uint32_t)kind : 7u;
         const uint32_t cc = code >= 0 && code <= 3 ? (uint32_t)code : 3u;
-        meta_.push_back(svc_id | (kk << 16) | (cc << 19));
+        out.meta.push_back(svc_id | (kk << 16) | (cc << 19));
         ++res.spans;
       }
-      if (!ss.ok) return rollback(Result::kError, "malformed ScopeSpans");
+      if (!ss.ok) return fail(Result::kError, "malformed ScopeSpans");
     }
-    if (!scan.ok) return rollback(Result::kError, "malformed ResourceSpans");
+    if (!scan.ok) return fail(Result::kError, "malformed ResourceSpans");
   }
-  if (!req.ok) return rollback(Result::kError, "malformed ExportTraceServiceRequest");
-  return res;
+  if (!req.ok) return fail(Result::kError, "malformed ExportTraceServiceRequest");
+  return true;
+}
+
+Result Columnizer::columnize(const uint8_t *buf, size_t len) { return columnize_into(buf, len, buf_); }
+
+Result Columnizer::columnize_into(const uint8_t *buf, size_t len, Cols &out) {
+  if (cache_.gen != gen_) cache_.clear(), cache_.gen = gen_;
+  Result res;
+  Undo undo;
+  const size_t n0 = out.size();
+  const uint64_t max0 = out.max_end;
+  if (run<false>(buf, len, *main_, out, cache_, res, &undo)) return res;
+  // all or nothing: drop this call's columns and dictionary entries
+  out.truncate(n0);
+  out.max_end = max0;
+  for (auto &k : undo.keys) {
+    auto it = res_keys_.find(k.first);
+    if (it != res_keys_.end()) it->second.erase(k.second);
+  }
+  for (uint64_t h : undo.resources) res_keys_.erase(h);
+  for (uint64_t sid : undo.sids) owner_.erase(sid);
+  for (auto &s : undo.services) services_.erase(s);
+  cache_.clear();  // it may name series this call made
+  Result r;
+  r.status = res.status;
+  r.error = res.error;
+  return r;
+}
+
+BatchResult Columnizer::columnize_batch(const uint8_t *const *bufs, const size_t *lens, size_t n) {
+  BatchResult br;
+  const unsigned T = (unsigned)std::min<size_t>(std::max(1u, opt_.threads), n);
+  if (T <= 1) {
+    for (size_t i = 0; i < n; ++i) {
+      br.results.push_back(columnize(bufs[i], lens[i]));
+      if (br.results.back().status == Result::kFallback) {
+        br.done = i + 1;
+        return br;
+      }
+    }
+    br.done = n;
+    return br;
+  }
+  struct Slot {
+    const Cols *src = nullptr;
+    bool ok = false;
+    size_t off = 0, cnt = 0, dst = 0;
+    uint64_t max_end = 0;
+    Result r;
+  };
+  std::vector<Slot> slots(n);
+  while (workers_.size() < opt_.threads) workers_.emplace_back(new Worker);
+  if (!pool_) pool_.reset(new Pool(opt_.threads));
+  for (auto &w : workers_) {
+    w->cols.clear();
+    if (w->cache.gen != gen_) w->cache.clear(), w->cache.gen = gen_;
+  }
+  // phase 1: decode in parallel against the dictionaries as they stand
+  std::atomic<size_t> next{0};
+  const std::function<void(unsigned)> decode = [&](unsigned wid) {
+    Worker &w = *workers_[wid];
+    for (size_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) {
+      Slot &s = slots[i];
+      s.src = &w.cols;
+      s.off = w.cols.size();
+      w.cols.max_end = 0;
+      try {
+        s.ok = run<true>(bufs[i], lens[i], w, w.cols, w.cache, s.r, nullptr);
+      } catch (...) {  // e.g. bad_alloc: redone (and reported) on the caller's thread
+        s.ok = false;
+      }
+      if (!s.ok) {
+        w.cols.truncate(s.off);
+        s.r = Result();
+        continue;
+      }
+      s.cnt = w.cols.size() - s.off;
+      s.max_end = w.cols.max_end;
+    }
+  };
+  pool_->run(T, decode);
+  // phase 2, in request order: what phase 1 could not take is redone exclusively
+  excl_.clear();
+  size_t taken = n, total = 0;
+  for (size_t i = 0; i < n; ++i) {
+    Slot &s = slots[i];
+    if (!s.ok) {
+      s.src = &excl_;
+      s.off = excl_.size();
+      excl_.max_end = 0;
+      s.r = columnize_into(bufs[i], lens[i], excl_);
+      s.cnt = excl_.size() - s.off;
+      s.max_end = excl_.max_end;
+    }
+    s.dst = buf_.size() + total;
+    total += s.cnt;
+    if (s.max_end > buf_.max_end) buf_.max_end = s.max_end;
+    if (s.r.status == Result::kFallback) {
+      taken = i + 1;
+      break;
+    }
+  }
+  // phase 3: every request's columns to its place in the buffer, in parallel
+  const size_t base = buf_.size();
+  buf_.key.resize(base + total), buf_.start.resize(base + total), buf_.end.resize(base + total);
+  buf_.w0.resize(base + total), buf_.w1.resize(base + total), buf_.meta.resize(base + total);
+  next = 0;
+  const std::function<void(unsigned)> place = [&](unsigned) {
+    for (size_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < taken;) {
+      const Slot &s = slots[i];
+      if (!s.cnt) continue;
+      const Cols &c = *s.src;
+      std::memcpy(&buf_.key[s.dst], &c.key[s.off], s.cnt * 8);
+      std::memcpy(&buf_.start[s.dst], &c.start[s.off], s.cnt * 8);
+      std::memcpy(&buf_.end[s.dst], &c.end[s.off], s.cnt * 8);
+      std::memcpy(&buf_.w0[s.dst], &c.w0[s.off], s.cnt * 8);
+      std::memcpy(&buf_.w1[s.dst], &c.w1[s.off], s.cnt * 8);
+      std::memcpy(&buf_.meta[s.dst], &c.meta[s.off], s.cnt * 4);
+    }
+  };
+  pool_->run(T, place);
+  br.results.reserve(taken);
+  for (size_t i = 0; i < taken; ++i) br.results.push_back(std::move(slots[i].r));
+  br.done = taken;
+  return br;
 }
 
 }  // namespace otlpcol

@@ -16,9 +16,17 @@
 // Anything outside that subset (array / kvlist values where a string form is
 // needed) makes columnize() report a fallback and roll back, and the host
 // handles that request in JavaScript.  Decoding errors roll back too.
+//
+// columnize_batch() decodes many requests on `threads` worker threads against
+// a read-only view of the dictionaries, then commits them in request order; a
+// request that meets anything new (resource, service, series) or fails is
+// redone by the calling thread at its place in that order, so the columns,
+// ids and reports are the ones request-at-a-time columnize() would give.
 #pragma once
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <vector>
 
@@ -45,6 +53,7 @@ struct Options {
   std::vector<Rule> rules;
   std::vector<std::string> key_attributes;  // resource_metrics_key_attributes (empty = all)
   bool test_collide_seed0 = false;          // tests only: every seed-0 series id is 42
+  unsigned threads = 1;                     // columnize_batch worker threads (caller included)
 };
 
 struct NewSeries {
@@ -68,39 +77,91 @@ struct Result {
   std::vector<std::pair<std::string, uint32_t>> new_services;
 };
 
+struct BatchResult {
+  std::vector<Result> results;  // one per request taken, in order
+  size_t done = 0;              // requests taken: all, or up to and including the first fallback
+};
+
+// SoA v1 columns under construction
+struct Cols {
+  std::vector<uint64_t> key, start, end, w0, w1;
+  std::vector<uint32_t> meta;
+  uint64_t max_end = 0;
+  size_t size() const { return key.size(); }
+  void truncate(size_t n);
+  void append(const Cols &o, size_t off, size_t n);
+  void clear() { truncate(0), max_end = 0; }
+};
+
+// (resource hash, service id, raw span name, kind, status code) -> series id,
+// for keys without dimensions: a span of a known series skips UTF-8
+// validation, the rename rules and building its key string
+class SigCache {
+ public:
+  static uint64_t hash(uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code);
+  const uint64_t *find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
+                       int32_t code) const;
+  void insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code,
+              uint64_t sid);
+  void clear() { t_.clear(), n_ = 0; }
+  uint64_t gen = 0;  // the dictionary generation the entries belong to
+
+ private:
+  struct Entry {
+    uint64_t h = 0, rhash = 0, sid = 0;
+    uint32_t svc = 0;
+    int32_t kind = 0, code = 0;
+    bool used = false;
+    std::string name;
+  };
+  std::vector<Entry> t_;
+  size_t n_ = 0;
+};
+
 class Columnizer {
  public:
-  explicit Columnizer(Options o) : opt_(std::move(o)) {}
+  explicit Columnizer(Options o);
+  ~Columnizer();
 
   // Appends the request's spans to the column buffer (all or nothing).
   Result columnize(const uint8_t *buf, size_t len);
+  // Many requests (see the header comment); stops after the first fallback,
+  // which the caller handles before passing the rest again.
+  BatchResult columnize_batch(const uint8_t *const *bufs, const size_t *lens, size_t n);
 
   uint32_t service_id(const std::string &name, bool *is_new);
-  void forget_resource(uint64_t hash) { res_keys_.erase(hash); }
+  void forget_resource(uint64_t hash) { res_keys_.erase(hash), ++gen_; }
   // the host interned (resource, key) as `sid` (a series its JavaScript path saw first)
   void learn(uint64_t rhash, const std::string &key, uint64_t sid);
   // the host's id for a series this columnizer reported as `from` is `to`:
   // buffered spans and the dictionary follow (the host's dictionary decides)
   void remap(uint64_t from, uint64_t to);
-  void clear_buffer() {
-    key_.clear(); start_.clear(); end_.clear(); w0_.clear(); w1_.clear(); meta_.clear();
-    max_end_ = 0;
-  }
+  void clear_buffer() { buf_.clear(); }
 
-  size_t buffered() const { return key_.size(); }
-  uint64_t max_end() const { return max_end_; }
-  const uint64_t *key() const { return key_.data(); }
-  const uint64_t *start() const { return start_.data(); }
-  const uint64_t *end() const { return end_.data(); }
-  const uint64_t *w0() const { return w0_.data(); }
-  const uint64_t *w1() const { return w1_.data(); }
-  const uint32_t *meta() const { return meta_.data(); }
+  size_t buffered() const { return buf_.size(); }
+  uint64_t max_end() const { return buf_.max_end; }
+  const uint64_t *key() const { return buf_.key.data(); }
+  const uint64_t *start() const { return buf_.start.data(); }
+  const uint64_t *end() const { return buf_.end.data(); }
+  const uint64_t *w0() const { return buf_.w0.data(); }
+  const uint64_t *w1() const { return buf_.w1.data(); }
+  const uint32_t *meta() const { return buf_.meta.data(); }
 
  private:
+  struct Worker;  // per-thread scratch, columns and signature cache
+  struct Undo;    // dictionary entries made by one exclusive call
+  struct Pool;
+  Result columnize_into(const uint8_t *buf, size_t len, Cols &out);
+  template <bool kShared>
+  bool run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCache &cache, Result &res, Undo *undo);
+
   Options opt_;
-  std::vector<uint64_t> key_, start_, end_, w0_, w1_;
-  std::vector<uint32_t> meta_;
-  uint64_t max_end_ = 0;
+  Cols buf_, excl_;  // excl_: columns of a batch's exclusively redone requests
+  SigCache cache_;
+  uint64_t gen_ = 0;  // bumped whenever an existing dictionary entry may change
+  std::unique_ptr<Worker> main_;
+  std::vector<std::unique_ptr<Worker>> workers_;
+  std::unique_ptr<Pool> pool_;
   std::unordered_map<std::string, uint32_t> services_;
   std::unordered_map<uint64_t, std::unordered_map<std::string, uint64_t>> res_keys_;
   // every id handed out -> its (resource, key): an id held by another series

@@ -693,6 +693,13 @@ napi_value CreateColumnizer(napi_env env, napi_callback_info info) {
     if (!is_undefined(env, tc)) napi_get_value_bool(env, tc, &b);
     o.test_collide_seed0 = b;
   }
+  {
+    napi_value th = prop(env, argv[1], "threads");
+    uint32_t t = 1;
+    if (!is_undefined(env, th) && napi_get_value_uint32(env, th, &t) != napi_ok)
+      return throw_type(env, "threads must be a number");
+    o.threads = std::max(1u, std::min(t, 64u));
+  }
   auto *c = new ColHandle(std::move(o));
   c->engine = static_cast<Handle *>(hp);
   napi_value obj;
@@ -706,6 +713,59 @@ napi_value CreateColumnizer(napi_env env, napi_callback_info info) {
   return obj;
 }
 
+// one columnize result; `lean` (a batch's requests) leaves out empty reports
+napi_value result_obj(napi_env env, const otlpcol::Result &r, bool lean) {
+  napi_value o, arr, s;
+  if (napi_create_object(env, &o) != napi_ok) return nullptr;
+  const char *st = r.status == otlpcol::Result::kOk ? "ok" : r.status == otlpcol::Result::kFallback ? "fallback" : "error";
+  napi_create_string_utf8(env, st, NAPI_AUTO_LENGTH, &s);
+  set(env, o, "status", s);
+  if (!lean || !r.error.empty()) {
+    napi_create_string_utf8(env, r.error.c_str(), NAPI_AUTO_LENGTH, &s);
+    set(env, o, "error", s);
+  }
+  set(env, o, "spans", num(env, (double)r.spans));
+  set(env, o, "resources", make_typed(env, napi_biguint64_array, 8, r.resources.data(), r.resources.size()));
+  if (!lean || !r.new_resources.empty()) {
+    napi_create_array_with_length(env, r.new_resources.size(), &arr);
+    for (size_t i = 0; i < r.new_resources.size(); ++i) {
+      napi_value e;
+      napi_create_object(env, &e);
+      set(env, e, "hash", big(env, r.new_resources[i].hash));
+      set(env, e, "off", num(env, (double)r.new_resources[i].off));
+      set(env, e, "len", num(env, r.new_resources[i].len));
+      napi_set_element(env, arr, (uint32_t)i, e);
+    }
+    set(env, o, "newResources", arr);
+  }
+  if (!lean || !r.new_series.empty()) {
+    napi_create_array_with_length(env, r.new_series.size(), &arr);
+    for (size_t i = 0; i < r.new_series.size(); ++i) {
+      napi_value e;
+      napi_create_object(env, &e);
+      set(env, e, "sid", big(env, r.new_series[i].sid));
+      set(env, e, "resHash", big(env, r.new_series[i].res_hash));
+      set(env, e, "off", num(env, r.new_series[i].span_off));
+      set(env, e, "len", num(env, r.new_series[i].span_len));
+      napi_set_element(env, arr, (uint32_t)i, e);
+    }
+    set(env, o, "newSeries", arr);
+  }
+  if (!lean || !r.new_services.empty()) {
+    napi_create_array_with_length(env, r.new_services.size(), &arr);
+    for (size_t i = 0; i < r.new_services.size(); ++i) {
+      napi_value e, nm;
+      napi_create_array_with_length(env, 2, &e);
+      napi_create_string_utf8(env, r.new_services[i].first.c_str(), r.new_services[i].first.size(), &nm);
+      napi_set_element(env, e, 0, nm);
+      napi_set_element(env, e, 1, num(env, r.new_services[i].second));
+      napi_set_element(env, arr, (uint32_t)i, e);
+    }
+    set(env, o, "newServices", arr);
+  }
+  return o;
+}
+
 napi_value Columnize(napi_env env, napi_callback_info info) {
   napi_value argv[2];
   if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
@@ -715,48 +775,43 @@ napi_value Columnize(napi_env env, napi_callback_info info) {
   size_t len;
   if (!typed(env, argv[1], napi_uint8_array, &data, &len, "request")) return nullptr;
   otlpcol::Result r = c->col.columnize(static_cast<const uint8_t *>(data), len);
-  napi_value o, arr, s;
-  if (napi_create_object(env, &o) != napi_ok) return throw_napi(env, "napi_create_object");
-  const char *st = r.status == otlpcol::Result::kOk ? "ok" : r.status == otlpcol::Result::kFallback ? "fallback" : "error";
-  napi_create_string_utf8(env, st, NAPI_AUTO_LENGTH, &s);
-  set(env, o, "status", s);
-  napi_create_string_utf8(env, r.error.c_str(), NAPI_AUTO_LENGTH, &s);
-  set(env, o, "error", s);
-  set(env, o, "spans", num(env, (double)r.spans));
+  napi_value o = result_obj(env, r, false);
+  if (!o) return throw_napi(env, "napi_create_object");
   set(env, o, "buffered", num(env, (double)c->col.buffered()));
   set(env, o, "maxEnd", big(env, c->col.max_end()));
-  set(env, o, "resources", make_typed(env, napi_biguint64_array, 8, r.resources.data(), r.resources.size()));
-  napi_create_array_with_length(env, r.new_resources.size(), &arr);
-  for (size_t i = 0; i < r.new_resources.size(); ++i) {
-    napi_value e;
-    napi_create_object(env, &e);
-    set(env, e, "hash", big(env, r.new_resources[i].hash));
-    set(env, e, "off", num(env, (double)r.new_resources[i].off));
-    set(env, e, "len", num(env, r.new_resources[i].len));
+  return o;
+}
+
+// columnizeBatch(c, [request bytes...]) -> {done, buffered, maxEnd, results}:
+// the requests decoded on the columnizer's threads, committed in order; it
+// stops after the first fallback (results[done - 1]), the caller passes the rest again
+napi_value ColumnizeBatch(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
+  ColHandle *c = get_col(env, argv[0]);
+  if (!c) return nullptr;
+  std::vector<napi_value> items;
+  if (!array_items(env, argv[1], &items, "requests")) return nullptr;
+  std::vector<const uint8_t *> bufs(items.size());
+  std::vector<size_t> lens(items.size());
+  for (size_t i = 0; i < items.size(); ++i) {
+    void *data;
+    if (!typed(env, items[i], napi_uint8_array, &data, &lens[i], "requests[]")) return nullptr;
+    bufs[i] = static_cast<const uint8_t *>(data);
+  }
+  otlpcol::BatchResult br = c->col.columnize_batch(bufs.data(), lens.data(), items.size());
+  napi_value o, arr;
+  if (napi_create_object(env, &o) != napi_ok) return throw_napi(env, "napi_create_object");
+  set(env, o, "done", num(env, (double)br.done));
+  set(env, o, "buffered", num(env, (double)c->col.buffered()));
+  set(env, o, "maxEnd", big(env, c->col.max_end()));
+  napi_create_array_with_length(env, br.results.size(), &arr);
+  for (size_t i = 0; i < br.results.size(); ++i) {
+    napi_value e = result_obj(env, br.results[i], true);
+    if (!e) return throw_napi(env, "napi_create_object");
     napi_set_element(env, arr, (uint32_t)i, e);
   }
-  set(env, o, "newResources", arr);
-  napi_create_array_with_length(env, r.new_series.size(), &arr);
-  for (size_t i = 0; i < r.new_series.size(); ++i) {
-    napi_value e;
-    napi_create_object(env, &e);
-    set(env, e, "sid", big(env, r.new_series[i].sid));
-    set(env, e, "resHash", big(env, r.new_series[i].res_hash));
-    set(env, e, "off", num(env, r.new_series[i].span_off));
-    set(env, e, "len", num(env, r.new_series[i].span_len));
-    napi_set_element(env, arr, (uint32_t)i, e);
-  }
-  set(env, o, "newSeries", arr);
-  napi_create_array_with_length(env, r.new_services.size(), &arr);
-  for (size_t i = 0; i < r.new_services.size(); ++i) {
-    napi_value e, nm;
-    napi_create_array_with_length(env, 2, &e);
-    napi_create_string_utf8(env, r.new_services[i].first.c_str(), r.new_services[i].first.size(), &nm);
-    napi_set_element(env, e, 0, nm);
-    napi_set_element(env, e, 1, num(env, r.new_services[i].second));
-    napi_set_element(env, arr, (uint32_t)i, e);
-  }
-  set(env, o, "newServices", arr);
+  set(env, o, "results", arr);
   return o;
 }
 
@@ -891,6 +946,7 @@ napi_value Init(napi_env env, napi_value exports) {
                {"stats", Stats},
                {"createColumnizer", CreateColumnizer},
                {"columnize", Columnize},
+               {"columnizeBatch", ColumnizeBatch},
                {"columnizerIngest", ColumnizerIngest},
                {"columnizerTake", ColumnizerTake},
                {"columnizerServiceId", ColumnizerServiceId},

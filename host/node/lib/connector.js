@@ -67,6 +67,9 @@ function parseDurationNs(s) {
 const OVERFLOW_KEY = '\u0001otel.metric.overflow';
 const EVENT_KEY_PREFIX = '\u0002events\u0000';
 
+const NONE = [];
+const asBuffer = (b) => (Buffer.isBuffer(b) ? b : Buffer.from(b.buffer, b.byteOffset, b.byteLength));
+
 const TEMPORALITY = {
   AGGREGATION_TEMPORALITY_CUMULATIVE: otlp.AGGREGATION_TEMPORALITY.CUMULATIVE,
   AGGREGATION_TEMPORALITY_DELTA: otlp.AGGREGATION_TEMPORALITY.DELTA,
@@ -126,6 +129,9 @@ function normalizeConfig(cfg = {}, addon) {
     device: cfg.device || 0,
     devices: Array.isArray(cfg.devices) && cfg.devices.length ? cfg.devices.map(Number) : null,
     batchSize: cfg.batch_size || 1 << 16,
+    // native columnizer worker threads for consumeTracesBatch (this build's own)
+    columnizerThreads: cfg.columnizer_threads !== undefined ? cfg.columnizer_threads
+      : Math.min(8, require('os').cpus().length),
   };
 }
 
@@ -180,7 +186,7 @@ class SpanMetricsConnector {
         !c.events && !c.exemplars && !c.cardinalityLimit && this.rules.every((r) => r.native)) {
       this.col = this.addon.createColumnizer(this.handle, { dims: c.dims,
         exclude: [...c.exclude], rules: this.rules.map((r) => r.native),
-        keyAttributes: c.resourceKeyAttributes });
+        keyAttributes: c.resourceKeyAttributes, threads: c.columnizerThreads });
     }
     this.resources = new Map();   // resHash -> resource record (LRU order: oldest first)
     this.evicted = new Map();     // evicted this flush interval, revivable until export
@@ -340,9 +346,50 @@ class SpanMetricsConnector {
   consumeTraces(req) {
     if (!this.handle) throw new Error('connector is shut down');
     const isBytes = Buffer.isBuffer(req) || req instanceof Uint8Array;
-    if (isBytes && this.col && this._consumeNative(Buffer.isBuffer(req) ? req
-      : Buffer.from(req.buffer, req.byteOffset, req.byteLength))) return;
-    if (isBytes) req = otlp.decodeTraces(req);
+    if (isBytes && this.col && this._consumeNative(asBuffer(req))) return;
+    this._consumeJs(isBytes ? otlp.decodeTraces(req) : req);
+  }
+
+  /**
+   * Many requests at once (what the pipeline's queue hands over): byte
+   * requests are columnised on the native columnizer's worker threads
+   * (columnizer_threads) and committed in order, so the ids, dictionary and
+   * columns are those of consumeTraces called on each in turn.  Returns one
+   * entry per request: null, or the Error consumeTraces would have thrown.
+   */
+  consumeTracesBatch(reqs) {
+    if (!this.handle) throw new Error('connector is shut down');
+    const errs = new Array(reqs.length).fill(null);
+    let i = 0;
+    while (i < reqs.length) {
+      const isBytes = Buffer.isBuffer(reqs[i]) || reqs[i] instanceof Uint8Array;
+      if (!isBytes || !this.col) {
+        try { this.consumeTraces(reqs[i]); } catch (e) { errs[i] = e; }
+        i += 1;
+        continue;
+      }
+      const bufs = [];
+      for (let j = i; j < reqs.length && (Buffer.isBuffer(reqs[j]) || reqs[j] instanceof Uint8Array); j++) {
+        bufs.push(asBuffer(reqs[j]));
+      }
+      const br = this.addon.columnizeBatch(this.col, bufs);
+      for (let k = 0; k < br.done; k++) {
+        try {
+          if (!this._applyNative(br.results[k], bufs[k])) this._consumeJs(otlp.decodeTraces(bufs[k]));
+        } catch (e) {
+          errs[i + k] = e;
+        }
+      }
+      if (br.maxEnd > this.nativeMaxEnd) this.nativeMaxEnd = br.maxEnd;
+      this.nativeBuffered = br.buffered;
+      if (br.buffered >= this.cols.cap) this._drain();
+      i += br.done;
+    }
+    return errs;
+  }
+
+  /** The JavaScript columnizer over a decoded request. */
+  _consumeJs(req) {
     this.jsRequests += 1;
     if (this.rules.length) {
       for (const rs of req.resourceSpans || []) {
@@ -396,18 +443,29 @@ class SpanMetricsConnector {
    */
   _consumeNative(bytes) {
     const r = this.addon.columnize(this.col, bytes);
+    if (!this._applyNative(r, bytes)) return false;
+    if (r.spans) {
+      if (r.maxEnd > this.nativeMaxEnd) this.nativeMaxEnd = r.maxEnd;
+      this.nativeBuffered = r.buffered;
+      if (r.buffered >= this.cols.cap) this._drain();
+    }
+    return true;
+  }
+
+  /** Host bookkeeping of one native columnize result (false: fallback). */
+  _applyNative(r, bytes) {
     if (r.status === 'fallback') return false;
     if (r.status !== 'ok') throw new Error(`OTLP request: ${r.error}`);
     this.nativeRequests += 1;
-    for (const [name, id] of r.newServices) this.services.set(name, id);
-    for (const nr of r.newResources) {
+    for (const [name, id] of r.newServices || NONE) this.services.set(name, id);
+    for (const nr of r.newResources || NONE) {
       if (this._touchResource(nr.hash)) continue;  // known to the host, forgotten natively
       const attrs = nr.off >= 0 ? otlp.decodeResource(new otlp.Reader(bytes, nr.off, nr.off + nr.len)).attributes : [];
       const res = this._resource(keys.attrMap(attrs));
       if (res.hash !== nr.hash) throw new Error('native/JS resource hash mismatch');
     }
     for (const h of r.resources) this._touchResource(h);
-    for (const ns of r.newSeries) {
+    for (const ns of r.newSeries || NONE) {
       const res = this.resources.get(ns.resHash) || this.evicted.get(ns.resHash);
       if (!res) throw new Error('native series for an unknown resource');
       const span = otlp.decodeSpan(new otlp.Reader(bytes, ns.off, ns.off + ns.len));
@@ -425,11 +483,6 @@ class SpanMetricsConnector {
       // the host dictionary decides: after a collision the two sides can differ
       // (the native side does not see series interned by a JavaScript-path request)
       if (sid !== ns.sid) this.addon.columnizerRemap(this.col, ns.sid, sid);
-    }
-    if (r.spans) {
-      if (r.maxEnd > this.nativeMaxEnd) this.nativeMaxEnd = r.maxEnd;
-      this.nativeBuffered = r.buffered;
-      if (r.buffered >= this.cols.cap) this._drain();
     }
     return true;
   }

@@ -26,6 +26,9 @@ class TracesToMetricsPipeline {
    * @param opts.receiver     OtlpReceiver options ({httpPort, grpcPort, host}), or false
    * @param opts.exporter     OtlpHttpExporter options ({endpoint}), or false
    * @param opts.addon, opts.clock  passed to the connector
+   * @param opts.queue        requests received within one event-loop turn are handed to
+   *                          the connector together (consumeTracesBatch: decoded on the
+   *                          native columnizer's threads); default on, false = one at a time
    */
   constructor(opts = {}) {
     this.rules = opts.transform || [];
@@ -35,7 +38,11 @@ class TracesToMetricsPipeline {
     this.connector = new SpanMetricsConnector(opts.spanmetrics || {}, { addon: opts.addon, clock: opts.clock,
       rules: this.rules, native: opts.native, metricsConsumer: (req) => this._export(req) });
     this.receiver = opts.receiver === false ? null
-      : new OtlpReceiver(Object.assign({}, opts.receiver, { onTraces: (b) => this.consumeTraces(b) }));
+      : new OtlpReceiver(Object.assign({}, opts.receiver, {
+        onTraces: (b) => (this.queueOn ? this.consumeTracesQueued(b) : this.consumeTraces(b)) }));
+    this.queueOn = opts.queue !== false;
+    this.queueMax = 256;  // requests per consumeTracesBatch call
+    this.pending = [];
     this.exportErrors = 0;
     this.lastExport = null;
   }
@@ -50,6 +57,33 @@ class TracesToMetricsPipeline {
   consumeTraces(bytes) {
     if (this.limiter) this.limiter.check();
     this.connector.consumeTraces(bytes);
+  }
+
+  /**
+   * Queued ConsumeTraces: resolves (or rejects with what consumeTraces would
+   * have thrown) once the request has been aggregated.  The memory limiter
+   * refuses at enqueue time, as the synchronous path does.
+   */
+  consumeTracesQueued(bytes) {
+    if (this.limiter) this.limiter.check();
+    return new Promise((resolve, reject) => {
+      this.pending.push({ bytes, resolve, reject });
+      if (this.pending.length === 1) setImmediate(() => this._drainQueue());
+      else if (this.pending.length >= this.queueMax) this._drainQueue();
+    });
+  }
+
+  _drainQueue() {
+    while (this.pending.length) {
+      const batch = this.pending.splice(0, this.queueMax);
+      let errs;
+      try {
+        errs = this.connector.consumeTracesBatch(batch.map((p) => p.bytes));
+      } catch (e) {
+        errs = batch.map(() => e);
+      }
+      batch.forEach((p, i) => (errs[i] ? p.reject(errs[i]) : p.resolve()));
+    }
   }
 
   _export(req) {

@@ -136,13 +136,12 @@ class OtlpReceiver {
     const type = (req.headers['content-type'] || '').split(';')[0].trim();
     if (type !== 'application/x-protobuf') return void (req.resume(), reply(415, Buffer.from('only application/x-protobuf is supported'), 'text/plain'));
     readBody(req, this.maxBody).then((raw) => {
-      try {
-        this.onTraces(inflate(raw, req.headers['content-encoding'], this.maxBody));
-        reply(200);  // empty ExportTraceServiceResponse
-      } catch (e) {
-        const code = e.refused ? 503 : e.tooLarge ? 413 : isBadRequest(e) ? 400 : 500;
-        reply(code, Buffer.from(String(e.message)), 'text/plain');
-      }
+      // onTraces may return a promise (the pipeline's queue): reply once it settles
+      Promise.resolve().then(() => this.onTraces(inflate(raw, req.headers['content-encoding'], this.maxBody)))
+        .then(() => reply(200), (e) => {  // 200: empty ExportTraceServiceResponse
+          const code = e.refused ? 503 : e.tooLarge ? 413 : isBadRequest(e) ? 400 : 500;
+          reply(code, Buffer.from(String(e.message)), 'text/plain');
+        });
     }, (e) => reply(e.tooLarge ? 413 : 400, Buffer.from(String(e.message)), 'text/plain'));
   }
 
@@ -168,12 +167,10 @@ class OtlpReceiver {
       } catch (e) {
         return done(e.tooLarge ? GRPC_RESOURCE_EXHAUSTED : GRPC_INVALID_ARGUMENT, e.message);
       }
-      try {
-        for (const m of msgs) this.onTraces(m);
-      } catch (e) {
-        return done(e.refused ? GRPC_UNAVAILABLE : isBadRequest(e) ? GRPC_INVALID_ARGUMENT : GRPC_INTERNAL, e.message);
-      }
-      return done(GRPC_OK, null, grpcFrame(Buffer.alloc(0)));  // empty ExportTraceServiceResponse
+      return (async () => {
+        for (const m of msgs) await this.onTraces(m);
+      })().then(() => done(GRPC_OK, null, grpcFrame(Buffer.alloc(0))),  // empty ExportTraceServiceResponse
+        (e) => done(e.refused ? GRPC_UNAVAILABLE : isBadRequest(e) ? GRPC_INVALID_ARGUMENT : GRPC_INTERNAL, e.message));
     }, (e) => done(GRPC_INVALID_ARGUMENT, e.message));
   }
 }

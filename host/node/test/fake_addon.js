@@ -170,6 +170,7 @@ class NativeColumnizerFakeAddon extends FakeAddon {
     return this.real.createColumnizer(null, Object.assign({}, opts, this.collide ? { testCollideSeed0: true } : {}));
   }
   columnize(c, bytes) { return this.real.columnize(c, bytes); }
+  columnizeBatch(c, bufs) { return this.real.columnizeBatch(c, bufs); }
   columnizerServiceId(c, name) { return this.real.columnizerServiceId(c, name); }
   columnizerForget(c, h) { return this.real.columnizerForget(c, h); }
   columnizerLearn(c, h, key, sid) { return this.real.columnizerLearn(c, h, key, sid); }

@@ -1,11 +1,14 @@
 'use strict';
 /**
- * Host-side rate of the Node path on one core: OTLP/protobuf request bytes ->
- * decode -> transform rules -> keying -> SoA columns -> addon.ingest.
- * SURVEY.md 8(d) asks for the OTLP decode+aggregate rate from protobuf bytes.
+ * Host-side rate of the Node path: OTLP/protobuf request bytes -> decode ->
+ * transform rules -> keying -> SoA columns -> addon.ingest.  SURVEY.md 8(d)
+ * asks for the OTLP decode+aggregate rate from protobuf bytes.
  *
- *   node test/host_rate.js [spans] [--gpu]
+ *   node test/host_rate.js [spans] [--gpu] [--threads T] [--batch B]
  *
+ * --threads T --batch B: requests go through consumeTracesBatch B at a time
+ * (what the pipeline's queue does under load), decoded on T columnizer
+ * threads (the JavaScript thread is one of them); default T=1, one request at a time.
  * Without --gpu the addon's ingest is a no-op stub (host work only); with
  * --gpu the real addon ingests (host memory -> HBM -> kernel) and the result
  * is checked for span count.  Prints one JSON line.
@@ -19,6 +22,8 @@ const { NativeColumnizerFakeAddon } = require('./fake_addon');
 const n = parseInt(process.argv[2] || '200000', 10);
 const gpu = process.argv.includes('--gpu');
 const jsOnly = process.argv.includes('--js');  // force the JavaScript columnizer
+const argOf = (k, d) => { const i = process.argv.indexOf(k); return i > 0 ? parseInt(process.argv[i + 1], 10) : d; };
+const threads = argOf('--threads', 1), batch = argOf('--batch', 0);
 const PER_REQUEST = 512;  // an SDK batch span processor's default export batch
 const SERVICES = 20, NAMES = 25;
 
@@ -59,14 +64,21 @@ if (gpu) {
   addon.columnizerIngest = (c) => addon.real.columnizerTake(c).keyHash.length;
 }
 const p = new TracesToMetricsPipeline({ addon, receiver: false, exporter: false, memoryLimiter: false,
-  native: !jsOnly, spanmetrics: { n_services: 64 } });
+  native: !jsOnly, spanmetrics: { n_services: 64, columnizer_threads: threads } });
+const consumeAll = (list) => {
+  if (!batch) { for (const r of list) p.consumeTraces(r); return; }
+  for (let i = 0; i < list.length; i += batch) {
+    const errs = p.connector.consumeTracesBatch(list.slice(i, i + batch));
+    if (errs.some(Boolean)) throw errs.find(Boolean);
+  }
+};
 // warm-up on a tenth of the requests (JIT), then time the whole set
 const warm = reqs.slice(0, Math.max(1, Math.floor(reqs.length / 10)));
-for (const r of warm) p.consumeTraces(r);
+consumeAll(warm);
 const warmSpans = BigInt(Math.min(n, warm.length * PER_REQUEST));
 p.connector.exportMetrics();
 const t0 = process.hrtime.bigint();
-for (const r of reqs) p.consumeTraces(r);
+consumeAll(reqs);
 p.connector._drain();
 if (gpu) addon.sync(p.connector.handle);
 const secs = Number(process.hrtime.bigint() - t0) / 1e9;
@@ -76,7 +88,7 @@ for (const rm of out.resourceMetrics) for (const dp of rm.scopeMetrics[0].metric
 const native = p.connector.stats().nativeRequests > 0;
 p.shutdown();
 console.log(JSON.stringify({ spans: n, requests: reqs.length, otlp_bytes: bytes, seconds: secs,
-  spans_per_s: n / secs, mb_per_s: bytes / secs / 1e6, cores: 1, gpu,
+  spans_per_s: n / secs, mb_per_s: bytes / secs / 1e6, cores: threads, batch, gpu,
   columnizer: native ? 'native (binding/otlp_columnizer.cc)' : 'javascript',
   calls_check: gpu ? calls === BigInt(n) + warmSpans : null,  // cumulative: warm-up + timed
   path: 'OTLP protobuf decode + transform + keying + SoA columnize' + (gpu ? ' + sa_ingest (H2D + kernel)' : ' (engine ingest stubbed)') }));

@@ -545,6 +545,68 @@ test('series ids: a 64-bit collision is re-salted on both paths (never thrown), 
   }
 });
 
+test('native columnizer: consumeTracesBatch on worker threads == consumeTraces one request at a time', () => {
+  const reqs = mixedRequests().map((r) => otlp.encodeTraces(r));
+  for (let r = 0; r < 12; r++) {  // new series, services and resources appear mid-batch
+    reqs.push(otlp.encodeTraces(request([[{ 'service.name': `svc-${r % 5}`, 'k8s.pod.name': `p-${r % 3}` },
+      [span(`op-${r % 4}`), span(`op-${r}`, { status: { code: 2 } }), span('GET /api/products/X?y=1')]]])));
+  }
+  const fallback = Buffer.from(otlp.encodeTraces(request([[{ 'service.name': 'u' }, [span('GET /x\u00e9')]]])));
+  fallback[fallback.indexOf(0xC3)] = 0xFF;
+  reqs.splice(7, 0, fallback);
+  reqs.splice(11, 0, reqs[3].subarray(0, reqs[3].length - 5));  // truncated: rejected
+  const rowsOf = (addon) => {
+    const rows = [];
+    for (const b of addon.batches) {
+      for (let i = 0; i < b.keyHash.length; i++) rows.push([b.keyHash[i], b.startNs[i], b.endNs[i], b.traceW0[i], b.traceW1[i], b.meta[i]].join(','));
+    }
+    return rows.sort();
+  };
+  for (const cfg of [{}, { dimensions: [{ name: 'http.status_code' }, { name: 'k8s.pod.name' }] },
+    { resource_metrics_cache_size: 2 }]) {
+    const out = [];
+    for (const threads of [1, 4]) {
+      const addon = new NativeColumnizerFakeAddon();
+      const t = { now: 1000n };
+      const conn = new SpanMetricsConnector(Object.assign({ batch_size: 16, columnizer_threads: threads }, cfg),
+        { addon, rules: DEMO_SPAN_NAME_RULES, clock: () => (t.now += 1n) });
+      let errs;
+      if (threads === 1) {
+        errs = reqs.map((r) => { try { conn.consumeTraces(r); return null; } catch (e) { return e; } });
+      } else {
+        errs = conn.consumeTracesBatch(reqs.slice(0, 9)).concat(conn.consumeTracesBatch(reqs.slice(9)));
+      }
+      const exp = otlp.encodeMetrics(conn.exportMetrics()).toString('hex');
+      out.push({ errs: errs.map((e) => (e ? 'error' : null)), rows: rowsOf(addon), exp, services: [...conn.services],
+        stats: conn.stats() });
+    }
+    const [one, batch] = out;
+    assert.strictEqual(one.errs.filter(Boolean).length, 1);
+    assert.deepStrictEqual(batch.errs, one.errs, JSON.stringify(cfg));
+    assert.deepStrictEqual(batch.rows, one.rows, JSON.stringify(cfg));
+    assert.deepStrictEqual(batch.exp, one.exp, JSON.stringify(cfg));
+    assert.deepStrictEqual(batch.services, one.services);
+    assert.strictEqual(batch.stats.jsRequests, 1);  // the non-UTF-8 request
+  }
+});
+
+test('pipeline queue: requests of one event-loop turn go through consumeTracesBatch', async () => {
+  const addon = new NativeColumnizerFakeAddon();
+  let batches = 0;
+  const real = addon.columnizeBatch.bind(addon);
+  addon.columnizeBatch = (c, bufs) => { batches += 1; return real(c, bufs); };
+  const { TracesToMetricsPipeline: P } = require(path.join(lib, 'pipeline'));
+  const p = new P({ addon, receiver: false, exporter: false, memoryLimiter: false, spanmetrics: { columnizer_threads: 2 } });
+  const good = otlp.encodeTraces(request([[{ 'service.name': 'a' }, [span('x'), span('y')]]]));
+  const res = await Promise.allSettled([p.consumeTracesQueued(good), p.consumeTracesQueued(good.subarray(0, 9)),
+    p.consumeTracesQueued(good)]);
+  assert.deepStrictEqual(res.map((r) => r.status), ['fulfilled', 'rejected', 'fulfilled']);
+  assert.strictEqual(batches, 1);
+  const calls = dpsOf(p.connector.exportMetrics(), 'traces.span.metrics.calls');
+  assert.deepStrictEqual(calls.map((d) => d.asInt), [2n, 2n]);
+  p.connector.shutdown();
+});
+
 test('native columnizer: invalid UTF-8 falls back to JavaScript; malformed bytes are rejected', () => {
   const addon = new NativeColumnizerFakeAddon();
   const conn = new SpanMetricsConnector({}, { addon, rules: DEMO_SPAN_NAME_RULES });
