@@ -162,7 +162,11 @@ int sa_create(const sa_config *cfg, sa_engine **out);
 void sa_destroy(sa_engine *e);
 const char *sa_last_error(const sa_engine *e);
 
-/* Host-memory batch: staged to HBM by the library, then aggregated. */
+/* Host-memory batch: packed into one of two pinned staging slots, copied to
+ * HBM and aggregated on the engine stream.  Returns once the batch has been
+ * copied out of the caller's buffers (they may be reused at once); the
+ * aggregation completes asynchronously -- every read (sa_flush*, sa_window_*,
+ * sa_get_stats) and sa_sync wait for it, and a device error surfaces there. */
 int sa_ingest(sa_engine *e, const sa_span_batch *batch);
 /* Device-resident batch (pointers into HBM of this engine's device).
  * `stream` is a hipStream_t (NULL = the engine's own stream). Asynchronous:
@@ -175,10 +179,21 @@ int sa_ingest_device(sa_engine *e, const sa_span_batch *batch, void *stream);
 int sa_sync(sa_engine *e);
 
 /* exportMetrics: delta since the last flush, then the engine's RED counters are
- * reset (keys stay resident). Returns SA_EFULL (with the result still filled)
- * if spans were dropped since the previous flush. */
+ * reset. Keys stay resident as a cache of the series seen, until more than half
+ * the table is taken: then the flush empties it (sa_reclaim_keys), so series
+ * that churn (new resources after evictions or restarts, delta purges) do not
+ * fill it for good. Returns SA_EFULL (with the result still filled) if spans
+ * were dropped since the previous flush: more distinct series within one flush
+ * interval than key_capacity. */
 int sa_flush(sa_engine *e, sa_red_result **out);
 void sa_red_result_free(sa_red_result *r);
+/* Key-table reclamation (what every flush does when the table is more than
+ * half full; force != 0: empty it now).  Only between a flush (or a resetting
+ * sa_gather_dense) and the next ingest: SA_ESTATE otherwise.  Results do not
+ * change: every row is zero then, and a series' next span re-inserts its key.
+ * Replaces nothing in the reference (upstream keys live in a Go LRU map,
+ * spanmetrics connector.go `resourceMetrics` / `dimensionsCache`). */
+int sa_reclaim_keys(sa_engine *e, int force);
 /* exportMetrics of an exponential-histogram engine (sa_flush returns
  * SA_ESTATE there, and sa_flush_exp does on an explicit-bucket engine). */
 int sa_flush_exp(sa_engine *e, sa_exp_result **out);

@@ -124,6 +124,7 @@ constexpr uint32_t kExpoMaxSize = 4096;
 
 // HLL bound sub-blocks: 2^kLbMinShift registers or more, at most kLbMaxSub of
 // them per engine (the kernels keep the bounds in LDS)
+constexpr uint64_t kHostChunkSpans = 1ull << 20;  // sa_ingest pinned slot (44 MiB)
 constexpr uint32_t kLbMinShift = 10;
 constexpr uint32_t kLbMaxSub = 2048;
 

@@ -112,9 +112,15 @@ struct sa_engine {
   unsigned long long *base64 = nullptr;
   uint64_t since_fold = 0, fold_limit = 0xFFFFFFFFULL;
   size_t hll_slot_bytes = 0, cms_slot_elems = 0;
-  void *stage = nullptr;
-  uint64_t stage_spans = 0;
+  // sa_ingest: two pinned host slots and their HBM copies; a slot is refilled
+  // once its event (H2D copy + aggregation of the previous use) has passed
+  void *pin[2] = {nullptr, nullptr}, *dstage[2] = {nullptr, nullptr};
+  hipEvent_t pin_ev[2] = {nullptr, nullptr};
+  bool pin_used[2] = {false, false};
+  int pin_cur = 0;
   uint64_t win_base = 0, spans = 0, slab_load = 0, dropped_seen = 0;
+  bool unflushed = false;   // spans ingested since the RED counters were last reset
+  uint64_t reclaims = 0;    // key-table reclamations (sa_reclaim_keys)
   std::string err;
 };
 
@@ -475,8 +481,12 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->part_fill, (void *)e->bt_rec, (void *)e->bt_cnt, (void *)e->base64, (void *)e->hll_lb,
                   (void *)e->expo_hdr, (void *)e->expo_buckets, (void *)e->expo_slot, (void *)e->expo_out_keys,
                   (void *)e->expo_out_rows, (void *)e->expo_out_buckets,
-                  e->stage})
+                  e->dstage[0], e->dstage[1]})
     if (p) (void)hipFree(p);
+  for (int k = 0; k < 2; ++k) {
+    if (e->pin[k]) (void)hipHostFree(e->pin[k]);
+    if (e->pin_ev[k]) (void)hipEventDestroy(e->pin_ev[k]);
+  }
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
   if (e->ev_b) (void)hipEventDestroy(e->ev_b);
   for (hipEvent_t ev : e->ev_set)
@@ -702,6 +712,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   e->set_stream[set] = s;
   e->set = (set + 1) % e->nsets;
   e->spans += b->n;
+  e->unflushed = true;
   return SA_OK;
 }
 
@@ -731,40 +742,45 @@ int sa_ingest_device(sa_engine *e, const sa_span_batch *b, void *stream) {
   return ingest_on(e, b, s);
 }
 
+// Host batches: each chunk is packed into a pinned slot (CPU copy, 44 B/span),
+// copied to HBM by DMA and aggregated on the engine stream; the call returns
+// once the batch has been copied out of the caller's buffers, so the caller
+// builds the next batch while this one is in flight (two slots).
 int sa_ingest(sa_engine *e, const sa_span_batch *b) {
   if (int rc = check_batch(e, b, false)) return rc;
   if (b->n == 0) return SA_OK;
   if (int rc = set_dev(e)) return rc;
   join_sets(e);
-  const uint64_t chunk = std::min<uint64_t>(b->n, 1ULL << 22);
-  if (e->stage_spans < chunk) {
-    if (e->stage) {
-      SA_HIP(e, hipStreamSynchronize(e->stream));
-      (void)hipFree(e->stage);
-      e->stage = nullptr;
-      e->stage_spans = 0;
+  constexpr uint64_t kChunk = sa::kHostChunkSpans;
+  constexpr size_t kSlotBytes = kChunk * 44 + 256;
+  if (!e->pin[0]) {
+    for (int k = 0; k < 2; ++k) {
+      if (hipHostMalloc(&e->pin[k], kSlotBytes, hipHostMallocDefault) != hipSuccess ||
+          hipMalloc(&e->dstage[k], kSlotBytes) != hipSuccess)
+        return fail(e, SA_ENOMEM, "ingest staging allocation failed");
+      SA_HIP(e, hipEventCreateWithFlags(&e->pin_ev[k], hipEventDisableTiming));
     }
-    if (hipMalloc(&e->stage, chunk * 44 + 256) != hipSuccess)
-      return fail(e, SA_ENOMEM, "staging hipMalloc failed");
-    e->stage_spans = chunk;
   }
-  char *base = static_cast<char *>(e->stage);
-  uint64_t *dk = reinterpret_cast<uint64_t *>(base);
-  uint64_t *ds = dk + e->stage_spans, *de = ds + e->stage_spans, *da = de + e->stage_spans,
-           *db = da + e->stage_spans;
-  uint32_t *dm = reinterpret_cast<uint32_t *>(db + e->stage_spans);
-  for (uint64_t off = 0; off < b->n; off += chunk) {
-    const uint64_t m = std::min(chunk, b->n - off);
-    SA_HIP(e, hipMemcpyAsync(dk, b->key_hash + off, m * 8, hipMemcpyHostToDevice, e->stream));
-    SA_HIP(e, hipMemcpyAsync(ds, b->start_ns + off, m * 8, hipMemcpyHostToDevice, e->stream));
-    SA_HIP(e, hipMemcpyAsync(de, b->end_ns + off, m * 8, hipMemcpyHostToDevice, e->stream));
-    SA_HIP(e, hipMemcpyAsync(da, b->trace_w0 + off, m * 8, hipMemcpyHostToDevice, e->stream));
-    SA_HIP(e, hipMemcpyAsync(db, b->trace_w1 + off, m * 8, hipMemcpyHostToDevice, e->stream));
-    SA_HIP(e, hipMemcpyAsync(dm, b->meta + off, m * 4, hipMemcpyHostToDevice, e->stream));
-    sa_span_batch sub{dk, ds, de, da, db, dm, m};
+  for (uint64_t off = 0; off < b->n; off += kChunk) {
+    const uint64_t m = std::min(kChunk, b->n - off);
+    const uint64_t ms = (m + 1) & ~1ULL;  // column stride: u64 columns stay 16-byte aligned
+    const int k = e->pin_cur;
+    e->pin_cur ^= 1;
+    if (e->pin_used[k]) SA_HIP(e, hipEventSynchronize(e->pin_ev[k]));
+    char *h = static_cast<char *>(e->pin[k]);
+    const uint64_t *src[5] = {b->key_hash + off, b->start_ns + off, b->end_ns + off, b->trace_w0 + off,
+                              b->trace_w1 + off};
+    for (int c = 0; c < 5; ++c) std::memcpy(h + c * ms * 8, src[c], m * 8);
+    std::memcpy(h + 5 * ms * 8, b->meta + off, m * 4);
+    char *d = static_cast<char *>(e->dstage[k]);
+    SA_HIP(e, hipMemcpyAsync(d, h, 5 * ms * 8 + m * 4, hipMemcpyHostToDevice, e->stream));
+    const uint64_t *dc = reinterpret_cast<const uint64_t *>(d);
+    sa_span_batch sub{dc, dc + ms, dc + 2 * ms, dc + 3 * ms, dc + 4 * ms,
+                      reinterpret_cast<const uint32_t *>(d + 5 * ms * 8), m};
     if (int rc = ingest_on(e, &sub, e->stream)) return rc;
+    SA_HIP(e, hipEventRecord(e->pin_ev[k], e->stream));
+    e->pin_used[k] = true;
   }
-  SA_HIP(e, hipStreamSynchronize(e->stream));
   return SA_OK;
 }
 
@@ -787,6 +803,43 @@ static int ensure_out(sa_engine *e) {
 
 static int read_stats(sa_engine *e, uint64_t out[sa::kNumStats]) {
   SA_HIP(e, hipMemcpyAsync(out, e->stats, sa::kNumStats * 8, hipMemcpyDeviceToHost, e->stream));
+  SA_HIP(e, hipStreamSynchronize(e->stream));
+  return SA_OK;
+}
+
+static int fold_window(sa_engine *e, uint64_t ws, hipStream_t s);
+
+// Empties the key table.  Keys are a cache of the series seen: after a flush
+// every row is zero, so a forgotten key costs nothing and is re-inserted by its
+// next span (the delta histograms do not depend on the slot).  Window error
+// counts are kept per slot, so every resident window's are folded into its
+// count-min first.
+static int reclaim_now(sa_engine *e) {
+  for (uint32_t ws = 0; ws < e->cfg.n_windows; ++ws)
+    if (int rc = fold_window(e, ws, e->stream)) return rc;
+  SA_HIP(e, hipMemsetAsync(e->gkeys, 0, e->cap * 8, e->stream));
+  ++e->reclaims;
+  return SA_OK;
+}
+
+// Flush-time policy: reclaim once more than half the table is resident, so a
+// collector whose series churn (new pods, restarts) keeps room for the next
+// interval's series instead of dropping their spans.
+static int reclaim_if_full(sa_engine *e) {
+  SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, e->stream));
+  SA_HIP(e, sa::launch_count_keys(e->gkeys, e->cap, e->scratch, e->stream));
+  uint64_t nk = 0;
+  SA_HIP(e, hipMemcpyAsync(&nk, e->scratch, 8, hipMemcpyDeviceToHost, e->stream));
+  SA_HIP(e, hipStreamSynchronize(e->stream));
+  return 2 * nk > e->cap ? reclaim_now(e) : SA_OK;
+}
+
+int sa_reclaim_keys(sa_engine *e, int force) {
+  if (!e) return SA_EINVAL;
+  if (e->unflushed) return fail(e, SA_ESTATE, "sa_reclaim_keys: spans ingested since the last flush");
+  if (int rc = set_dev(e)) return rc;
+  join_sets(e);
+  if (int rc = force ? reclaim_now(e) : reclaim_if_full(e)) return rc;
   SA_HIP(e, hipStreamSynchronize(e->stream));
   return SA_OK;
 }
@@ -843,6 +896,8 @@ int sa_flush(sa_engine *e, sa_red_result **out) {
   h->r.sum_ns = h->sum_ns.data();
   h->r.sum = h->sum.data();
   *out = &h->r;
+  e->unflushed = false;
+  if (int rc = reclaim_if_full(e)) return rc;
   uint64_t st[sa::kNumStats];
   if (int rc = read_stats(e, st)) return rc;
   if (st[sa::kStatDropped] != e->dropped_seen) {
@@ -927,6 +982,8 @@ int sa_flush_exp(sa_engine *e, sa_exp_result **out) {
   h->r.n_buckets = h->nb.data();
   h->r.bucket_counts = h->buckets.data();
   *out = &h->r;
+  e->unflushed = false;
+  if (int rc = reclaim_if_full(e)) return rc;
   uint64_t st[sa::kNumStats];
   if (int rc = read_stats(e, st)) return rc;
   if (st[sa::kStatDropped] != e->dropped_seen) {
@@ -1105,6 +1162,7 @@ int sa_gather_dense(sa_engine *e, const uint64_t *d_keys, uint64_t n, uint64_t *
   if (int rc = reduce_slabs(e, s)) return rc;
   SA_HIP(e, sa::launch_gather_dense(e->gkeys, e->gcounts, geom(e), d_keys, n, d_rows, s));
   if (reset) {
+    e->unflushed = false;
     SA_HIP(e, hipMemsetAsync(e->gcounts, 0, counts_bytes(e), s));
     if (e->base64) SA_HIP(e, hipMemsetAsync(e->base64, 0, (size_t)e->cap * (e->nbk + 1) * 8, s));
     e->since_fold = 0;

@@ -337,6 +337,12 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
   for (uint32_t i = 0; i < n; ++i) {
     SG_HIP(g, hipSetDevice(g->dev[i]));
     SG_HIP(g, hipStreamSynchronize(g->st[i]));
+    // the members' key tables: the flush-time reclamation sa_flush does
+    // (SA_ESTATE: nothing was gathered, the member's counters were never set)
+    if (nu) {
+      if (int rc = sa_reclaim_keys(g->eng[i], 0); rc != SA_OK && rc != SA_ESTATE)
+        return member_error(g, i, rc, "sa_reclaim_keys");
+    }
   }
   // 5. the result, in key order (the union is sorted)
   auto *h = new red_holder();

@@ -282,6 +282,11 @@ class Engine:
             raise SpanAggError(rc, f"sa_flush_exp: spans dropped (key table full); stats={self.stats()}")
         return res
 
+    def reclaim_keys(self, force: bool = False):
+        """sa_reclaim_keys: empty the key table (force) or do the flush-time
+        policy (more than half full); only right after a flush."""
+        self._check(self.lib.sa_reclaim_keys(self._h, int(force)), "sa_reclaim_keys")
+
     def expo_probe(self, values, scales):
         """GPU bucket index and Go math.Log of each value (diagnostic)."""
         v = np.ascontiguousarray(values, dtype=np.float64)
