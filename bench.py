@@ -346,7 +346,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=None,
                     help="PMC traffic summary of the main workload (default profiles/traffic[_<wl>].json)")
-    ap.add_argument("--host-otlp-spans", type=int, default=500_000,
+    ap.add_argument("--host-otlp-spans", type=int, default=2_000_000,
                     help="spans for the Node host's OTLP->GPU rate (0 = skip)")
     ap.add_argument("--cpu-workers", type=int, default=None,
                     help="processes for the multi-core CPU baseline (default: every usable host core; 0 = skip)")

@@ -40,8 +40,9 @@ def test_group_matches_oracle_c2(devices, rccl, monkeypatch):
         _check_windows(g, o)
         st = g.stats()
         assert st["spans"] == len(wl.batch)
-        # every member saw only its own shard
-        assert st["n_keys"] >= len(res.key_hash)
+        # members keep their keys, or the flush emptied their more than half
+        # full tables (sa_reclaim_keys; 2,048 slots each here)
+        assert st["n_keys"] == 0 or st["n_keys"] >= len(res.key_hash)
 
 
 def test_group_delta_flushes_and_equals_one_engine(monkeypatch):

@@ -198,6 +198,39 @@ def test_device_ingest_two_streams_overlap():
         _check_windows(e, _oracle_run(wl.batch, wl.n_services), wl.first_window, wl.n_services)
 
 
+@pytest.mark.parametrize("zipf,fold", [(0.0, None), (1.1, None), (0.0, "1500000")])
+def test_binned_two_streams_overlap(zipf, fold, monkeypatch):
+    """The binned path with its two launch sets: batch k+1's scatter runs
+    while batch k's aggregate does, and both insert keys first seen in them
+    (CAS write-back; a slot another launch took sends its counts down the probe
+    sequence).  With fold: the u32 rows fold into u64 between launches (the
+    fold waits for every outstanding launch)."""
+    import torch
+    if fold:
+        monkeypatch.setenv("SPANAGG_FOLD_LIMIT", fold)
+    batch, _, w0 = generate_highcard(3_000_000, routes=2000, pods=500, seed=21, zipf_s=zipf)
+    cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).cuda()
+            for c in batch.columns()]
+    cuts = [0, 500_000, 1_000_000, 1_500_000, 2_000_000, 2_500_000, 3_000_000]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    with Engine(Config(n_services=1, n_windows=16, key_capacity=1_000_000)) as e:
+        assert e.stats()["small_table"] == 0
+        e.window_advance(w0)
+        for i in range(len(cuts) - 1):
+            e.ingest_device(*[c[cuts[i]:cuts[i + 1]] for c in cols], n=cuts[i + 1] - cuts[i],
+                            stream=streams[i % 2].cuda_stream)
+        res = e.flush()
+        torch.cuda.synchronize()
+        o = _oracle_run(batch, 1)
+        assert_red_equal(res, o.series())
+        assert e.stats()["dropped_table_full"] == 0
+        for wid in o.window_ids():
+            sk = e.window_read(wid)
+            hll, cms = o.window(wid)
+            assert np.array_equal(sk.hll, hll) and np.array_equal(sk.cms, cms), wid
+
+
 def test_device_ingest_null_stream_orders_with_torch():
     """stream=NULL runs on the engine's stream, which is blocking: batches made
     on torch's legacy default stream and freed right after the call are safe."""
