@@ -83,16 +83,6 @@ struct IngestParams {
   ulonglong2 *bt_rec;
   uint32_t *bt_cnt;
   uint32_t bt_grid;  // scatter workgroups (regions per bin)
-  // the scatter's key-table updates (overflow-table rows, cold spans, ERROR
-  // counts), deferred to the aggregate so that the aggregate is the only
-  // writer of keys and rows while the other launch set's scatter runs: per
-  // bin bt_spill_n[bin] entries in bt_spill [bin][kBtSpillCap], the rest in
-  // bt_fb [kBtFbCap] (bt_fb_n[0] fill, [1] aggregate workgroups done), which
-  // the aggregate's last workgroup applies
-  struct BtSpill *bt_spill;
-  uint32_t *bt_spill_n;
-  struct BtSpill *bt_fb;
-  uint32_t *bt_fb_n;
   // HLL lower bounds: hll_lb[j] <= every register of sub-block j (registers
   // [j << lb_shift, (j + 1) << lb_shift)), so a span whose rho is at most its
   // sub-block's bound cannot raise a register and skips the register read.
@@ -230,16 +220,6 @@ __host__ __device__ inline uint32_t bt_slot(uint64_t m, uint32_t log2sb, uint32_
 // [2, 2 + nbk) = bucket counts, padded to whole 16-B quads (80 B at 17 buckets)
 __host__ __device__ inline uint32_t row32_stride(uint32_t nbk) { return (nbk + 2 + 3) & ~3u; }
 constexpr uint32_t kBtStage = 4;     // records per bin stage: one 64-B chunk per flush
-// a deferred key-table update (64 B): ns sum and u16 bucket-count pairs to add
-// to key m's row, nerr ERROR spans in window slot ws
-struct BtSpill {
-  unsigned long long m, sum;
-  uint32_t cnt[(kPartMaxBk + 1) / 2];
-  uint32_t ws, nerr, pad;
-};
-static_assert(sizeof(BtSpill) == 64, "BtSpill is one 64-B line");
-constexpr uint32_t kBtSpillCap = 512;    // per bin and launch set
-constexpr uint32_t kBtFbCap = 1u << 20;  // fallback list per launch set
 constexpr uint32_t kBtHot = 224;     // scatter overflow table entries
 constexpr uint32_t kBtHq = 256;      // scatter deferred HLL raises
 constexpr uint32_t kBtBlock = 1024;  // scatter workgroup
@@ -349,8 +329,6 @@ hipError_t prepare_ingest_bt(size_t agg_lds);
 size_t bt_agg_lds_bytes(uint32_t log2sb, uint32_t grid);
 size_t bt_agg2_lds_bytes(uint32_t log2sb, uint32_t grid);  // (the larger of the two is agg_lds)
 hipError_t launch_ingest_bt(const IngestParams &P, size_t agg_lds, hipStream_t s);
-hipError_t launch_bt_scatter(const IngestParams &P, hipStream_t s);
-hipError_t launch_bt_aggregate(const IngestParams &P, size_t agg_lds, hipStream_t s);
 hipError_t launch_fold_rows32(unsigned long long *gcounts, unsigned long long *base64, uint64_t cap,
                               uint32_t nbk, hipStream_t s);
 hipError_t launch_reduce_errslab(uint32_t *errslab, uint32_t G, uint64_t per_wg, uint64_t ws,

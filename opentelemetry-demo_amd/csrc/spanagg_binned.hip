@@ -79,67 +79,16 @@ __device__ __forceinline__ void bt_cms_add(KParams Q, uint32_t ws, uint64_t key)
   }
 }
 
-// A deferred key-table update: into its bin's list, else the fallback list,
-// else (both full) the span counts are dropped and its ERROR spans go to the
-// count-min.  Returns the spans dropped.
-__device__ __forceinline__ uint32_t bt_spill_put(KParams Q, const BtSpill &e) {
-  const uint32_t b = (uint32_t)(e.m >> kBinShift);
-  BtSpill *dst = nullptr;
-  const uint32_t i = atomicAdd(Q->bt_spill_n + b, 1u);
-  if (i < kBtSpillCap) {
-    dst = Q->bt_spill + (uint64_t)b * kBtSpillCap + i;
-  } else {
-    const uint32_t j = atomicAdd(Q->bt_fb_n, 1u);
-    if (j < kBtFbCap) dst = Q->bt_fb + j;
-  }
-  if (dst) {
-    const uint4 *src = reinterpret_cast<const uint4 *>(&e);
-    uint4 *d4 = reinterpret_cast<uint4 *>(dst);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) d4[q] = src[q];
-    return 0u;
-  }
-  uint32_t n = 0;
-  for (uint32_t w = 0; w < (kPartMaxBk + 1) / 2; ++w) n += (e.cnt[w] & 0xFFFFu) + (e.cnt[w] >> 16);
-  for (uint32_t c = 0; c < e.nerr; ++c) bt_cms_add(Q, e.ws, e.m * Q->kinv);
-  return n;
-}
-
-__device__ __forceinline__ BtSpill bt_spill_of(uint64_t m, unsigned long long sum, uint32_t ws, uint32_t nerr) {
-  BtSpill e;
-  e.m = m;
-  e.sum = sum;
-#pragma unroll
-  for (uint32_t w = 0; w < (kPartMaxBk + 1) / 2; ++w) e.cnt[w] = 0;
-  e.ws = ws;
-  e.nerr = nerr;
-  e.pad = 0;
-  return e;
-}
-
-// Cold paths of the scatter (deferred: see bt_spill_put).
+// Cold paths of the scatter.
 __device__ __noinline__ void bt_cold_err(KParams Q, uint64_t m, uint32_t ws) {
-  (void)bt_spill_put(Q, bt_spill_of(m, 0, ws, 1u));  // an ERROR-only entry drops no span
-}
-
-// returns 1 when the span was dropped (every deferral list is full)
-__device__ __noinline__ uint32_t bt_cold_direct(KParams Q, uint64_t m, uint64_t d, uint32_t bk, bool err,
-                                                uint32_t ws) {
-  BtSpill e = bt_spill_of(m, d, ws, err ? 1u : 0u);
-  e.cnt[bk >> 1] = 1u << ((bk & 1u) * 16);
-  return bt_spill_put(Q, e);
-}
-
-// Direct forms of the cold paths (the first-generation scatter, A/B runs: its
-// launches never overlap an aggregate)
-__device__ __noinline__ void bt_cold_err_direct(KParams Q, uint64_t m, uint32_t ws) {
   const uint32_t s = bt_find_insert(Q->gkeys, m, Q->log2sb);
   if (s != kNotFound) atomicAdd(Q->errcnt + ((uint64_t)ws << Q->log2cap) + s, 1ULL);
   else bt_cms_add(Q, ws, m * Q->kinv);
 }
 
-__device__ __noinline__ uint32_t bt_cold_direct_rows(KParams Q, uint64_t m, uint64_t d, uint32_t bk, bool err,
-                                                     uint32_t ws) {
+// returns 1 when the span was dropped (its bin is full)
+__device__ __noinline__ uint32_t bt_cold_direct(KParams Q, uint64_t m, uint64_t d, uint32_t bk, bool err,
+                                                uint32_t ws) {
   const uint32_t s = bt_find_insert(Q->gkeys, m, Q->log2sb);
   if (s == kNotFound) {
     if (err) bt_cms_add(Q, ws, m * Q->kinv);
@@ -147,27 +96,6 @@ __device__ __noinline__ uint32_t bt_cold_direct_rows(KParams Q, uint64_t m, uint
   }
   row32_add(Q->gcounts, row32_stride(Q->nbk), s, bk, 1u, d);
   if (err) atomicAdd(Q->errcnt + ((uint64_t)ws << Q->log2cap) + s, 1ULL);
-  return 0u;
-}
-
-// The aggregate's application of one deferred update (its workgroup owns the
-// bin's rows now; updates of one key may come from several entries: atomics).
-// Returns the spans dropped (the bin's sub-table is full).
-__device__ __forceinline__ uint32_t bt_apply_spill(KParams Q, const BtSpill &e) {
-  const uint32_t s = bt_find_insert(Q->gkeys, e.m, Q->log2sb);
-  if (s == kNotFound) {
-    uint32_t n = 0;
-    for (uint32_t w = 0; w < (kPartMaxBk + 1) / 2; ++w) n += (e.cnt[w] & 0xFFFFu) + (e.cnt[w] >> 16);
-    for (uint32_t c = 0; c < e.nerr; ++c) bt_cms_add(Q, e.ws, e.m * Q->kinv);
-    return n;
-  }
-  const uint32_t stride32 = row32_stride(Q->nbk);
-  for (uint32_t b = 0; b < Q->nbk; ++b) {
-    const uint32_t c = (e.cnt[b >> 1] >> ((b & 1u) * 16)) & 0xFFFFu;
-    if (c) row32_add(Q->gcounts, stride32, s, b, c, 0);
-  }
-  if (e.sum) row32_add(Q->gcounts, stride32, s, 0, 0, e.sum);
-  if (e.nerr) atomicAdd(Q->errcnt + ((uint64_t)e.ws << Q->log2cap) + s, (unsigned long long)e.nerr);
   return 0u;
 }
 
@@ -246,12 +174,12 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter_kernel(IngestParams P) {
       if (k == 0 || k == m) {
         atomicAdd(&hcnt[h * kPartWords + (bk >> 1)], 1u << ((bk & 1u) * 16));
         atomicAdd(&hsum[h], (unsigned long long)d);
-        if (err) bt_cold_err_direct(kp, m, ws);
+        if (err) bt_cold_err(kp, m, ws);
         return;
       }
       h = h + 1 == kBtHot ? 0u : h + 1;
     }
-    n_drop += bt_cold_direct_rows(kp, m, d, bk, err, ws);
+    n_drop += bt_cold_direct(kp, m, d, bk, err, ws);
   };
   auto hot_rec = [&](uint32_t b, const ulonglong2 &r) {
     const uint64_t m = ((uint64_t)b << kBinShift) | (r.x & kBinRest);
@@ -698,20 +626,33 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
   for (uint32_t b = threadIdx.x; b < kPartBins; b += kBtBlock)
     P.bt_cnt[(uint64_t)b * P.bt_grid + blockIdx.x] = min((rcnw[b >> 1] >> ((b & 1u) * 16)) & 0xFFFFu, region);
   __syncthreads();
-  // the overflow table and its ERROR counts: deferred updates for the
-  // aggregate (this scatter may run while the other launch set's aggregate
-  // owns the key table)
+  // the overflow table: one row update per entry (atomics: entries of one
+  // key may come from several workgroups)
+  const uint32_t stride32 = row32_stride(P.nbk);
   for (uint32_t h = threadIdx.x; h < kBt2Hot; h += kBtBlock) {
     const unsigned long long m = hkey[h];
     if (m == 0) continue;
-    BtSpill e = bt_spill_of(m, hsum[h], 0, 0);
-#pragma unroll
-    for (uint32_t w = 0; w < kPartWords; ++w) e.cnt[w] = hcnt[h * kPartWords + w];
-    n_drop += bt_spill_put(kp, e);
+    const uint32_t s = bt_find_insert(P.gkeys, m, P.log2sb);
+    if (s == kNotFound) {
+      for (uint32_t b = 0; b < P.nbk; ++b) n_drop += (hcnt[h * kPartWords + (b >> 1)] >> ((b & 1u) * 16)) & 0xFFFFu;
+      continue;
+    }
+    for (uint32_t b = 0; b < P.nbk; ++b) {
+      const uint32_t c = (hcnt[h * kPartWords + (b >> 1)] >> ((b & 1u) * 16)) & 0xFFFFu;
+      if (c) row32_add(P.gcounts, stride32, s, b, c, 0);
+    }
+    row32_add(P.gcounts, stride32, s, 0, 0, hsum[h]);
   }
   if (threadIdx.x < kBt2HotErr) {
     const uint2 e = herr[threadIdx.x];
-    if (e.x) (void)bt_spill_put(kp, bt_spill_of(hkey[(e.x - 1) & 0xFFu], 0, (e.x - 1) >> 8, e.y));
+    if (e.x) {
+      const uint32_t ws = (e.x - 1) >> 8, h = (e.x - 1) & 0xFFu;
+      const uint64_t m = hkey[h];
+      const uint32_t s = bt_find_insert(P.gkeys, m, P.log2sb);
+      if (s != kNotFound) atomicAdd(P.errcnt + ((uint64_t)ws << P.log2cap) + s, (unsigned long long)e.y);
+      else
+        for (uint32_t i = 0; i < e.y; ++i) bt_cms_add(kp, ws, m * P.kinv);
+    }
   }
   const uint32_t nq = min(hq_n[0], kBtHq);
   for (uint32_t i = threadIdx.x; i < nq; i += kBtBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
@@ -761,6 +702,7 @@ __global__ __launch_bounds__(kBtAggBlock) void bt_aggregate_kernel(IngestParams 
     orig[u] = s < sb ? gk[s] : 0ULL;
   }
   for (uint32_t g = tid; g < G; g += kBtAggBlock) pre[g] = P.bt_cnt[(uint64_t)bin * G + g];
+  if (tid < kBins * 2) reinterpret_cast<uint4 *>(lbins)[tid] = reinterpret_cast<const uint4 *>(P.bintab)[tid];
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
     const uint32_t s = tid + u * kBtAggBlock;
@@ -977,8 +919,7 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
   bt_stamp(P, (uint64_t)bin * 8, 1);
 
   // 2. the records (the thresholds live in SGPRs: a runtime-bounded loop over
-  //    P.thr would re-load them from the kernarg segment for every record; an
-  //    LDS bin table would cost the third workgroup per CU)
+  //    P.thr would re-load them from the kernarg segment for every record)
   const ulonglong2 *bin_rec = P.bt_rec + (uint64_t)bin * G * region;
   const __amdgpu_buffer_rsrc_t rrec = rsrc(bin_rec, G * region * 16);
   const uint32_t half = lane >> 5, r0 = lane & 31u;
@@ -993,24 +934,14 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
     uint32_t bk = nneg;
 #pragma unroll
     for (uint32_t i = 0; i < kPartMaxBk - 1; ++i) bk += d > thr[i] ? 1u : 0u;
-    // the key's two buckets: four 16-B reads issued together (the asm keeps
-    // the compiler from sinking them into a chain of dependent branches) and
-    // a branch-free select, first match winning; else the probe sequence (a
-    // new key, or one placed past its two buckets)
+    // the key's two buckets (four independent 16-B reads), else the probe
+    // sequence (a new key, or one placed past its two buckets)
     const BtSeq bq = bt_seq(m, log2sb);
     const ulonglong2 *lk2 = reinterpret_cast<const ulonglong2 *>(lkeys);
-    ulonglong2 a0 = lk2[bq.b1 * 2], a1 = lk2[bq.b1 * 2 + 1], c0 = lk2[bq.b2 * 2], c1 = lk2[bq.b2 * 2 + 1];
-    asm volatile("" : "+v"(a0.x), "+v"(a0.y), "+v"(a1.x), "+v"(a1.y), "+v"(c0.x), "+v"(c0.y), "+v"(c1.x),
-                 "+v"(c1.y));
-    uint32_t s = kNotFound;
-    s = c1.y == m ? bq.b2 * 4 + 3 : s;
-    s = c1.x == m ? bq.b2 * 4 + 2 : s;
-    s = c0.y == m ? bq.b2 * 4 + 1 : s;
-    s = c0.x == m ? bq.b2 * 4 : s;
-    s = a1.y == m ? bq.b1 * 4 + 3 : s;
-    s = a1.x == m ? bq.b1 * 4 + 2 : s;
-    s = a0.y == m ? bq.b1 * 4 + 1 : s;
-    s = a0.x == m ? bq.b1 * 4 : s;
+    const ulonglong2 a0 = lk2[bq.b1 * 2], a1 = lk2[bq.b1 * 2 + 1], c0 = lk2[bq.b2 * 2], c1 = lk2[bq.b2 * 2 + 1];
+    uint32_t s = a0.x == m ? bq.b1 * 4 : a0.y == m ? bq.b1 * 4 + 1 : a1.x == m ? bq.b1 * 4 + 2
+               : a1.y == m ? bq.b1 * 4 + 3 : c0.x == m ? bq.b2 * 4 : c0.y == m ? bq.b2 * 4 + 1
+               : c1.x == m ? bq.b2 * 4 + 2 : c1.y == m ? bq.b2 * 4 + 3 : kNotFound;
     const uint32_t pmax = bt_probe_max(log2sb);
     uint32_t i = 0;
     if (s == kNotFound) {
@@ -1052,15 +983,9 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
       ulonglong2 v[B];
       uint32_t cnt[B];
 #pragma unroll
-      for (uint32_t b = 0; b < B; ++b) {  // the fills: unconditional LDS reads, one wait
-        const uint32_t p = p0 + b * kWaves, g = 2 * p + half;
-        const bool ok = p < pairs && g < G;
-        cnt[b] = rcnt[ok ? g : 0u];
-        cnt[b] = ok ? cnt[b] : 0u;
-      }
-#pragma unroll
       for (uint32_t b = 0; b < B; ++b) {  // unconditional buffer loads (0 past the end)
         const uint32_t p = p0 + b * kWaves, g = 2 * p + half;
+        cnt[b] = p < pairs && g < G ? rcnt[g] : 0u;
         const uint32_t off = r0 < cnt[b] ? (g * region + r0) * 16 : 0xFFFFFFF0u;
         const auto x = __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)off, 0, 2);
         v[b] = make_ulonglong2((uint64_t)x[0] | ((uint64_t)x[1] << 32), (uint64_t)x[2] | ((uint64_t)x[3] << 32));
@@ -1086,10 +1011,8 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
   __syncthreads();
   bt_stamp(P, (uint64_t)bin * 8, 2);
 
-  // 3. new keys and touched rows of the bin.  One owner: plain stores (the
-  //    engine orders the aggregates of its two launch sets, and the scatters
-  //    defer their key-table updates to them); every row read is issued
-  //    before the first row is written.
+  // 3. new keys and touched rows of the bin (one owner: plain stores; every
+  //    row read is issued before the first row is written)
   if (MODE & 2) return;
   const uint32_t nbk = P.nbk, stride32 = row32_stride(nbk), nq = stride32 / 4;
   uint32_t *rows = reinterpret_cast<uint32_t *>(P.gcounts) + ((uint64_t)bin << log2sb) * stride32;
@@ -1146,33 +1069,9 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
     unsigned long long *cell = P.errcnt + ((uint64_t)ws << P.log2cap) + ((uint64_t)bin << log2sb) + s;
     *cell += e.y;
   }
-  // 4. the scatter's deferred updates of this bin, then (last workgroup) the
-  //    fallback list; atomics, as several entries may name one key
-  __threadfence();
-  __syncthreads();
-  uint32_t sp_drop = 0;
-  const uint32_t nsp = min(P.bt_spill_n[bin], kBtSpillCap);
-  for (uint32_t i = tid; i < nsp; i += BLOCK) sp_drop += bt_apply_spill(kernel_params(), P.bt_spill[(uint64_t)bin * kBtSpillCap + i]);
-  __threadfence();
-  __syncthreads();
-  if (tid == 0) {
-    P.bt_spill_n[bin] = 0;  // (this launch set's next scatter starts after this launch)
-    misc[1] = atomicAdd(P.bt_fb_n + 1, 1u) == gridDim.x - 1 ? 1u : 0u;
-  }
-  __syncthreads();
-  if (misc[1]) {
-    __threadfence();
-    const uint32_t nfb = min(atomicAdd(P.bt_fb_n, 0u), kBtFbCap);
-    for (uint32_t i = tid; i < nfb; i += BLOCK) sp_drop += bt_apply_spill(kernel_params(), P.bt_fb[i]);
-    __syncthreads();
-    if (tid == 0) P.bt_fb_n[0] = P.bt_fb_n[1] = 0;
-  }
-  sp_drop = wave_sum(sp_drop);
-  if (lane == 0 && sp_drop) atomicAdd(&P.stats[kStatDropped], (unsigned long long)sp_drop);
   if (tid == 0 && misc[0]) atomicAdd(&P.stats[kStatDropped], (unsigned long long)misc[0]);
   bt_stamp(P, (uint64_t)bin * 8, 3);
 }
-
 
 // u32 count rows -> the u64 fold array (before 2^32 spans can accumulate)
 __global__ void fold_rows32_kernel(uint32_t *rows, unsigned long long *base64, uint64_t cap, uint32_t nbk) {
@@ -1270,26 +1169,20 @@ hipError_t prepare_ingest_bt(size_t agg_lds) {
   return hipSuccess;
 }
 
-hipError_t launch_bt_scatter(const IngestParams &P, hipStream_t s) {
-  if (P.diag & kDiagBtNoScatter) return hipSuccess;
+hipError_t launch_ingest_bt(const IngestParams &P, size_t agg_lds, hipStream_t s) {
   void *args[] = {const_cast<IngestParams *>(&P)};
-  const bool v1 = (P.diag & (kDiagBtScatter1 | kDiagBtDirect)) != 0;
-  return hipLaunchKernel(v1 ? bt_scatter_fn(P.diag) : bt_scatter2_fn(P.diag), dim3(P.bt_grid), dim3(kBtBlock), args,
-                         v1 ? kBtScatterLds : kBt2ScatterLds, s);
-}
-
-hipError_t launch_bt_aggregate(const IngestParams &P, size_t agg_lds, hipStream_t s) {
+  if (!(P.diag & kDiagBtNoScatter)) {
+    const bool v1 = (P.diag & (kDiagBtScatter1 | kDiagBtDirect)) != 0;
+    if (hipError_t e = hipLaunchKernel(v1 ? bt_scatter_fn(P.diag) : bt_scatter2_fn(P.diag), dim3(P.bt_grid),
+                                       dim3(kBtBlock), args, v1 ? kBtScatterLds : kBt2ScatterLds, s);
+        e != hipSuccess)
+      return e;
+  }
   if (P.diag & kDiagBtNoAgg) return hipSuccess;
-  void *args[] = {const_cast<IngestParams *>(&P)};
   const uint32_t diag = P.diag | (P.log2sb > 10 ? kDiagBtAggWide : 0u);
   const uint32_t blk = (P.diag & kDiagBtAgg1) ? kBtAggBlock : kBtAgg2Block;
-  return hipLaunchKernel(bt_agg_fn(diag), dim3(kPartBins), dim3(blk), args,
-                         (P.diag & kDiagBtAgg1) ? agg_lds : bt_agg2_lds_bytes(P.log2sb, P.bt_grid), s);
-}
-
-hipError_t launch_ingest_bt(const IngestParams &P, size_t agg_lds, hipStream_t s) {
-  if (hipError_t e = launch_bt_scatter(P, s); e != hipSuccess) return e;
-  return launch_bt_aggregate(P, agg_lds, s);
+  return hipLaunchKernel(bt_agg_fn(diag), dim3(kPartBins), dim3(blk),
+                         args, (P.diag & kDiagBtAgg1) ? agg_lds : bt_agg2_lds_bytes(P.log2sb, P.bt_grid), s);
 }
 
 hipError_t launch_fold_rows32(unsigned long long *gcounts, unsigned long long *base64, uint64_t cap,

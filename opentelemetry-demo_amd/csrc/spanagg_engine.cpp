@@ -107,12 +107,8 @@ struct sa_engine {
   uint32_t log2sb = 0, bt_grid = 0;
   uint64_t kmul = 1, kinv = 1;
   size_t agg_lds = 0;
-  ulonglong2 *bt_rec[kMaxSlabSets] = {};  // per launch set: a launch's scatter overlaps
-  uint32_t *bt_cnt[kMaxSlabSets] = {};    // the other set's aggregate
-  sa::BtSpill *bt_spill[kMaxSlabSets] = {}, *bt_fb[kMaxSlabSets] = {};
-  uint32_t *bt_spill_n[kMaxSlabSets] = {}, *bt_fb_n[kMaxSlabSets] = {};
-  hipEvent_t ev_agg = nullptr;       // the last binned aggregate (the next one orders after it)
-  hipStream_t agg_stream = nullptr;
+  ulonglong2 *bt_rec = nullptr;
+  uint32_t *bt_cnt = nullptr;
   unsigned long long *base64 = nullptr;
   uint64_t since_fold = 0, fold_limit = 0xFFFFFFFFULL;
   size_t hll_slot_bytes = 0, cms_slot_elems = 0;
@@ -433,7 +429,6 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     e->bt_grid = e->cus;
     if (const char *v = std::getenv("SPANAGG_BT_SCATTER")) e->bt_scatter1 = std::atoi(v) == 1;
     if (const char *v = std::getenv("SPANAGG_BT_AGG")) e->bt_agg1 = std::atoi(v) == 1;
-    if (e->bt_agg1) e->bt_scatter1 = true;  // the first aggregate applies no deferred updates
     e->agg_lds = std::max(sa::bt_agg_lds_bytes(e->log2sb, e->bt_grid), sa::bt_agg2_lds_bytes(e->log2sb, e->bt_grid));
     if (hipError_t st = sa::prepare_ingest_bt(e->agg_lds); st != hipSuccess)
       return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
@@ -451,14 +446,6 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   }
   if (hipMemcpy(e->d_seeds, kCmsSeed, sizeof kCmsSeed, hipMemcpyHostToDevice) != hipSuccess)
     return bail(fail(e, SA_EDEVICE, "seed upload failed"));
-  if (e->bt && !e->bt_scatter1 && !e->bt_agg1) {
-    // two record-buffer sets: a launch's scatter runs while the previous
-    // launch's aggregate does (the aggregate's table writes are atomic; the
-    // first-generation A/B kernels write rows plainly and keep one set)
-    e->nsets = 2;
-    if (const char *v = std::getenv("SPANAGG_BT_SETS"))  // A/B runs
-      e->nsets = std::atoi(v) == 1 ? 1u : 2u;
-  }
   if (e->small) {
     e->nsets = kDefaultSlabSets;
     if (const char *v = std::getenv("SPANAGG_SLAB_SETS"))  // tuning knob for A/B runs
@@ -491,10 +478,7 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->stats, (void *)e->out_keys, (void *)e->out_rows, (void *)e->scratch,
                   (void *)e->slab_cnt, (void *)e->hll, (void *)e->errcnt, (void *)e->d_seeds,
                   (void *)e->dbg, (void *)e->d_bins, (void *)e->errslab, (void *)e->part_rec,
-                  (void *)e->part_fill, (void *)e->bt_rec[0], (void *)e->bt_cnt[0],
-                  (void *)e->bt_rec[1], (void *)e->bt_cnt[1], (void *)e->bt_spill[0], (void *)e->bt_spill[1],
-                  (void *)e->bt_fb[0], (void *)e->bt_fb[1], (void *)e->bt_spill_n[0], (void *)e->bt_spill_n[1],
-                  (void *)e->bt_fb_n[0], (void *)e->bt_fb_n[1], (void *)e->base64, (void *)e->hll_lb,
+                  (void *)e->part_fill, (void *)e->bt_rec, (void *)e->bt_cnt, (void *)e->base64, (void *)e->hll_lb,
                   (void *)e->expo_hdr, (void *)e->expo_buckets, (void *)e->expo_slot, (void *)e->expo_out_keys,
                   (void *)e->expo_out_rows, (void *)e->expo_out_buckets,
                   e->dstage[0], e->dstage[1]})
@@ -508,7 +492,6 @@ void sa_destroy(sa_engine *e) {
   for (hipEvent_t ev : e->ev_set)
     if (ev) (void)hipEventDestroy(ev);
   if (e->ev_ctl) (void)hipEventDestroy(e->ev_ctl);
-  if (e->ev_agg) (void)hipEventDestroy(e->ev_agg);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -561,52 +544,33 @@ static uint32_t bt_region_for(uint64_t wg_chunk) {
   return ((uint32_t)std::ceil(mu + 4.0 * std::sqrt(mu) + 8.0) + sa::kBtStage - 1) & ~(sa::kBtStage - 1);
 }
 
-static int bt_prepare_launch(sa_engine *e, uint64_t n, IngestParams &P, uint32_t set, hipStream_t s) {
+static int bt_prepare_launch(sa_engine *e, uint64_t n, IngestParams &P, hipStream_t s) {
   const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(e->bt_grid, (n + 4095) / 4096));
   P.bt_grid = grid;
   P.wg_chunk = ((n + grid - 1) / grid + 3) / 4 * 4;
   P.bt_region = bt_region_for(P.wg_chunk);
-  if (!e->bt_rec[set]) {
+  if (!e->bt_rec) {
     const size_t recs = (size_t)sa::kPartBins * e->bt_grid * bt_region_for(sa::kBtMaxWgSpans);
-    if (hipMalloc((void **)&e->bt_rec[set], recs * sizeof(ulonglong2)) != hipSuccess ||
-        hipMalloc((void **)&e->bt_cnt[set], (size_t)e->bt_grid * sa::kPartBins * 4) != hipSuccess ||
-        hipMalloc((void **)&e->bt_spill[set], (size_t)sa::kPartBins * sa::kBtSpillCap * sizeof(sa::BtSpill)) !=
-            hipSuccess ||
-        hipMalloc((void **)&e->bt_fb[set], (size_t)sa::kBtFbCap * sizeof(sa::BtSpill)) != hipSuccess ||
-        hipMalloc((void **)&e->bt_spill_n[set], (size_t)sa::kPartBins * 4) != hipSuccess ||
-        hipMalloc((void **)&e->bt_fb_n[set], 16) != hipSuccess)
+    if (hipMalloc((void **)&e->bt_rec, recs * sizeof(ulonglong2)) != hipSuccess ||
+        hipMalloc((void **)&e->bt_cnt, (size_t)e->bt_grid * sa::kPartBins * 4) != hipSuccess)
       return fail(e, SA_ENOMEM, "binned-path record buffers hipMalloc failed");
-    SA_HIP(e, hipMemsetAsync(e->bt_spill_n[set], 0, (size_t)sa::kPartBins * 4, s));
-    SA_HIP(e, hipMemsetAsync(e->bt_fb_n[set], 0, 16, s));
-    if (!e->ev_agg) SA_HIP(e, hipEventCreateWithFlags(&e->ev_agg, hipEventDisableTiming));
   }
-  P.log2sb = e->log2sb;
-  P.kmul = e->kmul;
-  P.kinv = e->kinv;
-  P.bt_rec = e->bt_rec[set];
-  P.bt_cnt = e->bt_cnt[set];
-  P.bt_spill = e->bt_spill[set];
-  P.bt_spill_n = e->bt_spill_n[set];
-  P.bt_fb = e->bt_fb[set];
-  P.bt_fb_n = e->bt_fb_n[set];
-  return SA_OK;
-}
-
-// u32 bucket counts could wrap: fold them into the u64 array first, after
-// every outstanding launch (the fold reads and clears rows the launches add to)
-static int bt_fold_if_due(sa_engine *e, uint64_t n) {
-  if (e->since_fold + n > e->fold_limit) {
-    join_sets(e);
+  if (e->since_fold + n > e->fold_limit) {  // u32 bucket counts could wrap: fold them first
     if (!e->base64) {
       const size_t bytes = (size_t)e->cap * (e->nbk + 1) * 8;
       if (hipMalloc((void **)&e->base64, bytes) != hipSuccess)
         return fail(e, SA_ENOMEM, "fold array hipMalloc failed");
-      SA_HIP(e, hipMemsetAsync(e->base64, 0, bytes, e->stream));
+      SA_HIP(e, hipMemsetAsync(e->base64, 0, bytes, s));
     }
-    SA_HIP(e, sa::launch_fold_rows32(e->gcounts, e->base64, e->cap, e->nbk, e->stream));
+    SA_HIP(e, sa::launch_fold_rows32(e->gcounts, e->base64, e->cap, e->nbk, s));
     e->since_fold = 0;
   }
   e->since_fold += n;
+  P.log2sb = e->log2sb;
+  P.kmul = e->kmul;
+  P.kinv = e->kinv;
+  P.bt_rec = e->bt_rec;
+  P.bt_cnt = e->bt_cnt;
   return SA_OK;
 }
 
@@ -645,8 +609,6 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
     }
     e->slab_load += per_wg;
   }
-  if (e->bt)
-    if (int rc = bt_fold_if_due(e, b->n)) return rc;
   // order: after the engine stream's work so far (ev_ctl, re-recorded after
   // each join) and after the previous launch that used this slab set
   if (e->ctl_dirty) {
@@ -710,15 +672,8 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   if (e->small) {
     st = sa::launch_ingest_small(P, grid, e->lds_bytes, s, e->variant);
   } else if (e->bt) {
-    if (int rc = bt_prepare_launch(e, b->n, P, set, s)) return rc;
-    // scatter, then the aggregate after the previous launch's aggregate (one
-    // writer of the key table at a time; the scatters write records and
-    // deferred updates only, so they overlap the other set's aggregate)
-    st = sa::launch_bt_scatter(P, s);
-    if (st == hipSuccess && e->agg_stream && e->agg_stream != s) st = hipStreamWaitEvent(s, e->ev_agg, 0);
-    if (st == hipSuccess) st = sa::launch_bt_aggregate(P, e->agg_lds, s);
-    if (st == hipSuccess) st = hipEventRecord(e->ev_agg, s);
-    e->agg_stream = s;
+    if (int rc = bt_prepare_launch(e, b->n, P, s)) return rc;
+    st = sa::launch_ingest_bt(P, e->agg_lds, s);
   } else if (e->part) {
     // records per bin: 1.25x the mean plus slack; a fuller bin spills to the
     // direct path, so this bounds memory, not correctness
