@@ -125,6 +125,7 @@ constexpr uint32_t kExpoMaxSize = 4096;
 // HLL bound sub-blocks: 2^kLbMinShift registers or more, at most kLbMaxSub of
 // them per engine (the kernels keep the bounds in LDS)
 constexpr uint64_t kHostChunkSpans = 1ull << 20;  // sa_ingest pinned slot (44 MiB)
+constexpr uint64_t kHostPageableMin = 1ull << 18;  // chunks from here on: the runtime's pageable staging
 constexpr uint32_t kLbMinShift = 10;
 constexpr uint32_t kLbMaxSub = 2048;
 

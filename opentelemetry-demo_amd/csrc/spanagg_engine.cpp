@@ -770,10 +770,19 @@ int sa_ingest(sa_engine *e, const sa_span_batch *b) {
     char *h = static_cast<char *>(e->pin[k]);
     const uint64_t *src[5] = {b->key_hash + off, b->start_ns + off, b->end_ns + off, b->trace_w0 + off,
                               b->trace_w1 + off};
-    for (int c = 0; c < 5; ++c) std::memcpy(h + c * ms * 8, src[c], m * 8);
-    std::memcpy(h + 5 * ms * 8, b->meta + off, m * 4);
     char *d = static_cast<char *>(e->dstage[k]);
-    SA_HIP(e, hipMemcpyAsync(d, h, 5 * ms * 8 + m * 4, hipMemcpyHostToDevice, e->stream));
+    if (m >= sa::kHostPageableMin) {
+      // large chunks: the runtime's own staging of pageable memory copies
+      // faster than one host thread packing the pinned slot (and, as that,
+      // returns once the caller's bytes have been taken)
+      for (int c = 0; c < 5; ++c)
+        SA_HIP(e, hipMemcpyAsync(d + c * ms * 8, src[c], m * 8, hipMemcpyHostToDevice, e->stream));
+      SA_HIP(e, hipMemcpyAsync(d + 5 * ms * 8, b->meta + off, m * 4, hipMemcpyHostToDevice, e->stream));
+    } else {
+      for (int c = 0; c < 5; ++c) std::memcpy(h + c * ms * 8, src[c], m * 8);
+      std::memcpy(h + 5 * ms * 8, b->meta + off, m * 4);
+      SA_HIP(e, hipMemcpyAsync(d, h, 5 * ms * 8 + m * 4, hipMemcpyHostToDevice, e->stream));
+    }
     const uint64_t *dc = reinterpret_cast<const uint64_t *>(d);
     sa_span_batch sub{dc, dc + ms, dc + 2 * ms, dc + 3 * ms, dc + 4 * ms,
                       reinterpret_cast<const uint32_t *>(d + 5 * ms * 8), m};

@@ -1,29 +1,52 @@
 #!/usr/bin/env python3
-"""profiles/traffic.json from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of
-tools/round_profile.sh: per ingest launch (first launch dropped), FETCH_SIZE
-doubled per MI355X_MICROARCH.md's gfx950 correction, KB = 1024 B."""
-import csv, json, sys, collections
+"""profiles/traffic[_<wl>].json from the rocprofv3 FETCH_SIZE / WRITE_SIZE
+passes of tools/gpu_job.sh (pmc_<wl>_fetch, pmc_<wl>_write over
+tools/prof_driver.py): per ingest launch -- the mean over launches (first
+dropped) of each hot-path kernel, summed over the kernels of one launch (C2:
+ingest_v2_kernel; C4: bt_scatter2 + bt_aggregate2) -- FETCH_SIZE doubled per
+MI355X_MICROARCH.md's gfx950 correction, KB = 1024 B.
+
+  python tools/traffic.py <job dir> <workload> <round> <out.json>"""
+import collections
+import csv
+import json
+import sys
+
+HOT = ("ingest", "bt_scatter", "bt_aggregate")
+
 
 def per_launch(path, counter):
-    d = collections.defaultdict(float)
+    d = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(path)):
-        if "ingest" in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            d[int(r["Dispatch_Id"])] += float(r["Counter_Value"])
-    ids = sorted(d)[1:] or sorted(d)
-    return sum(d[i] for i in ids) / len(ids), len(ids)
+        name = r["Kernel_Name"]
+        if r["Counter_Name"] == counter and any(h in name for h in HOT):
+            short = next(h for h in HOT if h in name) + name[name.index(next(h for h in HOT if h in name)):].split("(")[0][len(next(h for h in HOT if h in name)):]
+            d[short][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+    total, kernels = 0.0, {}
+    for name, per in d.items():
+        ids = sorted(per)[1:] or sorted(per)
+        kernels[name] = sum(per[i] for i in ids) / len(ids)
+        total += kernels[name]
+    return total, kernels
 
-root, out, rnd = sys.argv[1], sys.argv[2], sys.argv[3]
-f, nf = per_launch(f"{root}/pmc_fetch/run_counter_collection.csv", "FETCH_SIZE")
-w, nw = per_launch(f"{root}/pmc_write/run_counter_collection.csv", "WRITE_SIZE")
-spans = 10_000_000
-t = {"workload": "c2", "kernel": "ingest_v2_kernel<2,2,2,false,11,9,14,-1,true,1> (variant 16)",
-     "spans_per_launch": spans, "algorithmic_bytes_per_launch": 44 * spans,
-     "fetch_size_kb_per_launch": f, "write_size_kb_per_launch": w,
-     "hbm_bytes_per_launch": int((2 * f + w) * 1024),
-     "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes "
-               "(tools/round_profile.sh, tools/prof_driver.py: 5 launches of the C2 10M-span "
-               f"batch, first launch dropped: {nf} / {nw} launches averaged); FETCH_SIZE doubled "
-               "per MI355X_MICROARCH.md gfx950 correction; KB=1024 B",
-     "round": rnd}
-json.dump(t, open(out, "w"), indent=1)
-print(json.dumps(t, indent=1))
+
+def main():
+    root, wl, rnd, out = sys.argv[1:5]
+    f, fk = per_launch(f"{root}/pmc_{wl}_fetch/run_counter_collection.csv", "FETCH_SIZE")
+    w, wk = per_launch(f"{root}/pmc_{wl}_write/run_counter_collection.csv", "WRITE_SIZE")
+    spans = 10_000_000
+    t = {"workload": wl, "spans_per_launch": spans, "algorithmic_bytes_per_launch": 44 * spans,
+         "fetch_size_kb_per_launch": f, "write_size_kb_per_launch": w,
+         "per_kernel_kb": {"fetch": fk, "write": wk},
+         "hbm_bytes_per_launch": int((2 * f + w) * 1024),
+         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/gpu_job.sh "
+                   "pmc_<wl>_fetch / _write over tools/prof_driver.py: 5 launches of the 10M-span batch, "
+                   "first dropped); FETCH_SIZE doubled per MI355X_MICROARCH.md gfx950 correction; KB=1024 B",
+         "round": rnd}
+    t["traffic_over_algorithmic"] = t["hbm_bytes_per_launch"] / t["algorithmic_bytes_per_launch"]
+    json.dump(t, open(out, "w"), indent=1)
+    print(json.dumps(t, indent=1))
+
+
+if __name__ == "__main__":
+    main()
