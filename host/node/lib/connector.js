@@ -198,6 +198,8 @@ class SpanMetricsConnector {
     this.sketchWatermark = 0n;
     this.closedWindows = [];
     this.droppedFlushes = 0;
+    this.droppedSpans = 0n;       // the engine's dropped_table_full after the last dropping flush
+    this.onDrop = opts.onDrop || null;
     this.collisions = 0;          // series ids re-salted after a 64-bit collision
     this._verifyingNative = false;
     this.eventRecords = 0;
@@ -558,7 +560,7 @@ class SpanMetricsConnector {
     const now = this.clock();
     const expo = this.cfg.expMaxSize !== 0;
     const r = expo ? this.addon.flushExp(this.handle) : this.addon.flush(this.handle);
-    if (r.status === this.addon.status.EFULL) this.droppedFlushes += 1;
+    if (r.status === this.addon.status.EFULL) this._reportDrops();
     const nb = r.nBuckets;
     const delta = this.cfg.temporality === otlp.AGGREGATION_TEMPORALITY.DELTA;
     const touched = new Set();
@@ -601,6 +603,30 @@ class SpanMetricsConnector {
       this.closedWindows = [];
     }
     return { resourceMetrics };
+  }
+
+  /**
+   * More distinct series in one flush interval than key_capacity: the engine
+   * dropped spans (sa_flush returned SA_EFULL).  Counted (droppedFlushes,
+   * droppedSpans in stats()) and reported through `onDrop` (default: a warning
+   * on stderr, at most once a minute) -- never silent.  The engine reclaims
+   * its key table at flush time, so the series of earlier intervals do not
+   * fill it; only one interval's series have to fit.
+   */
+  _reportDrops() {
+    this.droppedFlushes += 1;
+    const st = this.addon.stats(this.handle);
+    const dropped = st.droppedTableFull !== undefined ? BigInt(st.droppedTableFull) : 0n;
+    const info = { droppedSpans: dropped, keyCapacity: this.cfg.keyCapacity, droppedFlushes: this.droppedFlushes };
+    this.droppedSpans = dropped;
+    if (this.onDrop) return this.onDrop(info);
+    const now = Date.now();
+    if (!this._lastDropWarn || now - this._lastDropWarn > 60000) {
+      this._lastDropWarn = now;
+      process.emitWarning(`spanmetrics: ${dropped} spans dropped so far: more series in one flush interval ` +
+        `than key_capacity (${this.cfg.keyCapacity})`, 'SpanMetricsDropWarning');
+    }
+    return undefined;
   }
 
   _buildMetrics(res, sids, now, delta) {
@@ -714,7 +740,8 @@ class SpanMetricsConnector {
   stats() {
     const s = this.addon.stats(this.handle);
     return Object.assign(s, { resources: this.resources.size, series: this.series.size,
-      services: this.services.size, droppedFlushes: this.droppedFlushes, collisions: this.collisions,
+      services: this.services.size, droppedFlushes: this.droppedFlushes, droppedSpans: this.droppedSpans,
+      collisions: this.collisions,
       eventRecords: this.eventRecords, nativeRequests: this.nativeRequests, jsRequests: this.jsRequests });
   }
 }

@@ -153,7 +153,7 @@ class FakeAddon {
     for (const wid of [...this.windows.keys()]) if (wid < base) this.windows.delete(wid);
     this.base = base;
   }
-  stats() { return { spans: 0n }; }
+  stats() { return { spans: 0n, droppedTableFull: this.dropped || 0n }; }
 }
 
 /**

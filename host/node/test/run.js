@@ -277,6 +277,19 @@ test('connector: delta emits only touched series, start = previous export', () =
   assert.strictEqual(dpsOf(conn.exportMetrics(), 'traces.span.metrics.calls').length, 0);
 });
 
+test('connector: engine drops (SA_EFULL) are counted and reported, never silent', () => {
+  const seen = [];
+  const addon = new FakeAddon();
+  const conn = new SpanMetricsConnector({ batch_size: 4 }, { addon, clock: () => 1000n, onDrop: (i) => seen.push(i) });
+  conn.consumeTraces(request([[{ 'service.name': 'a' }, [span('x')]]]));
+  const flush = addon.flush.bind(addon);
+  addon.flush = () => Object.assign(flush(), { status: addon.status.EFULL });
+  addon.dropped = 7n;
+  conn.exportMetrics();
+  assert.deepStrictEqual(seen.map((i) => [i.droppedSpans, i.droppedFlushes]), [[7n, 1]]);
+  assert.strictEqual(conn.stats().droppedSpans, 7n);
+});
+
 test('connector: resource LRU evicts, exports the evicted once, then forgets it', () => {
   const { conn, t } = mkConnector({ resource_metrics_cache_size: 1 });
   conn.consumeTraces(request([[{ 'service.name': 'a' }, [span('x')]],
