@@ -876,7 +876,8 @@ __host__ __device__ inline uint32_t bt_agg2_cnt_words(uint32_t sb) { return (sb 
 __host__ __device__ inline uint32_t bt_agg2_off_err(uint32_t sb) { return (sb * 16 + bt_agg2_cnt_words(sb) * 4 + 7) & ~7u; }
 __host__ __device__ inline uint32_t bt_agg2_off_reg(uint32_t sb) { return bt_agg2_off_err(sb) + kBtAgg2Err * 8; }
 
-// MODE (ablation): 1 = no records aggregated, 2 = no key / row write-back;
+// MODE (ablation): 1 = no records aggregated, 2 = no key / row write-back,
+// 4 = records loaded only;
 // MAXPER = key slots per thread (sb <= MAXPER * BLOCK)
 template <int MODE = 0, int MAXPER = 2, int BLOCK = 512>
 __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
@@ -976,35 +977,61 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
       atomicAdd(P.errcnt + ((uint64_t)ws << P.log2cap) + ((uint64_t)bin << log2sb) + s, 1ULL);
     }
   };
+  // a batch: B region pairs of this wave, one record per lane, loaded with
+  // unconditional buffer loads (0 past a region's fill); the fills are read
+  // from LDS first, all of them before the loads
+  constexpr uint32_t kWaves = BLOCK / 64;
+  constexpr uint32_t B = 8;
+  const uint32_t pairs = (G + 1) / 2;
+  auto issue = [&](uint32_t p0, ulonglong2 (&v)[B], uint32_t (&cnt)[B]) {
+#pragma unroll
+    for (uint32_t b = 0; b < B; ++b) {
+      const uint32_t p = p0 + b * kWaves, g = 2 * p + half;
+      const bool ok = p < pairs && g < G;
+      cnt[b] = rcnt[ok ? g : 0u];
+      cnt[b] = ok ? cnt[b] : 0u;
+    }
+#pragma unroll
+    for (uint32_t b = 0; b < B; ++b) {
+      const uint32_t g = 2 * (p0 + b * kWaves) + half;
+      const uint32_t off = r0 < cnt[b] ? (g * region + r0) * 16 : 0xFFFFFFF0u;
+      const auto x = __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)off, 0, 2);
+      v[b] = make_ulonglong2((uint64_t)x[0] | ((uint64_t)x[1] << 32), (uint64_t)x[2] | ((uint64_t)x[3] << 32));
+    }
+  };
+  auto process = [&](uint32_t p0, const ulonglong2 (&v)[B], const uint32_t (&cnt)[B]) {
+    if (MODE & 4) {  // ablation: records loaded, not aggregated
+#pragma unroll
+      for (uint32_t b = 0; b < B; ++b) n_drop += (r0 < cnt[b] && (v[b].x ^ v[b].y) == 0x12345ULL) ? 1u : 0u;
+      return;
+    }
+#pragma unroll
+    for (uint32_t b = 0; b < B; ++b)
+      if (r0 < cnt[b]) agg(v[b]);
+  };
+  // regions longer than 32 records: the rest, one record per lane, after the
+  // batches (loads inside the batch loop would make the compiler drain every
+  // outstanding load at its head)
+  auto tails = [&]() {
+#pragma unroll 1
+    for (uint32_t p = wave; p < pairs; p += kWaves) {
+      const uint32_t g = 2 * p + half;
+      const uint32_t c = g < G ? rcnt[g] : 0u;
+      for (uint32_t r = 32 + r0; r < c; r += 32) agg(bin_rec[(uint64_t)g * region + r]);
+    }
+  };
   if (!(MODE & 1)) {
-    constexpr uint32_t kWaves = BLOCK / 64, B = 8;
-    const uint32_t pairs = (G + 1) / 2;
+    // one batch of 8 pairs at a time (two batches of 4 in flight, the next
+    // one's loads issued before this one is aggregated, measured 3 % slower:
+    // the conditional ERROR-path atomics make the compiler drain every load at
+    // the loop head, profiles/r2_analysis/c4_agg_pipeline.txt)
     for (uint32_t p0 = wave; p0 < pairs; p0 += kWaves * B) {
       ulonglong2 v[B];
       uint32_t cnt[B];
-#pragma unroll
-      for (uint32_t b = 0; b < B; ++b) {  // unconditional buffer loads (0 past the end)
-        const uint32_t p = p0 + b * kWaves, g = 2 * p + half;
-        cnt[b] = p < pairs && g < G ? rcnt[g] : 0u;
-        const uint32_t off = r0 < cnt[b] ? (g * region + r0) * 16 : 0xFFFFFFF0u;
-        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)off, 0, 2);
-        v[b] = make_ulonglong2((uint64_t)x[0] | ((uint64_t)x[1] << 32), (uint64_t)x[2] | ((uint64_t)x[3] << 32));
-      }
-      if (MODE & 4) {  // ablation: records loaded, not aggregated
-#pragma unroll
-        for (uint32_t b = 0; b < B; ++b) n_drop += (r0 < cnt[b] && (v[b].x ^ v[b].y) == 0x12345ULL) ? 1u : 0u;
-        continue;
-      }
-#pragma unroll
-      for (uint32_t b = 0; b < B; ++b)
-        if (r0 < cnt[b]) agg(v[b]);
-      // regions longer than 32 records: the rest, one record per lane
-#pragma unroll 1
-      for (uint32_t b = 0; b < B; ++b) {
-        const uint32_t p = p0 + b * kWaves, g = 2 * p + half;
-        for (uint32_t r = 32 + r0; r < cnt[b]; r += 32) agg(bin_rec[(uint64_t)g * region + r]);
-      }
+      issue(p0, v, cnt);
+      process(p0, v, cnt);
     }
+    if (!(MODE & 4)) tails();
   }
   n_drop = wave_sum(n_drop);
   if (lane == 0 && n_drop) atomicAdd(&misc[0], n_drop);
