@@ -454,18 +454,24 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
       bt_cold_err(kp, m, ws);
     }
   };
-  // a span the stages cannot take: the overflow table, else the direct path
-  auto hot_add = [&](uint64_t m, uint64_t d, bool err, uint32_t ws) {
+  // the overflow table: false when the key is not in it and its 8 probes
+  // are taken
+  auto hot_try = [&](uint64_t m, uint64_t d, bool err, uint32_t ws) -> bool {
     uint32_t h = hot_home(m);
     for (int pr = 0; pr < 8; ++pr) {
       unsigned long long k = hkey[h];
       if (k == 0) k = atomicCAS(&hkey[h], 0ULL, (unsigned long long)m);
       if (k == 0 || k == m) {
         hot_acc(h, m, d, err, ws);
-        return;
+        return true;
       }
       h = h + 1 == kBt2Hot ? 0u : h + 1;
     }
+    return false;
+  };
+  // a span its region cannot take: the overflow table, else the direct path
+  auto hot_add = [&](uint64_t m, uint64_t d, bool err, uint32_t ws) {
+    if (hot_try(m, d, err, ws)) return;
     const uint32_t bk = bucket_lds<1>(d, lbins, P);
     n_drop += bt_cold_direct(kp, m, d, bk, err, ws);
   };
@@ -502,10 +508,9 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
     uint32_t same = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kBtStage; ++q) same += ((stage[b * kBtStage + q].x ^ rec.x) & kBinRest) == 0 ? 1u : 0u;
-    if (same >= 2) {
-      hot_add(m, d, err, ws);
-      return;
-    }
+    // (a frequent key the full overflow table cannot take stays a record:
+    // the per-span direct path is only for a region that is used up)
+    if (same >= 2 && hot_try(m, d, err, ws)) return;
     const uint32_t at = claim(b, 1);
     if (at < region) my_rec[b * bin_stride + at] = rec;
     else hot_add(m, d, err, ws);
