@@ -474,12 +474,11 @@ napi_value FlushExp(napi_env env, napi_callback_info info) {
     if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
     Handle *h = get_handle(env, argv[0]);
     if (!h) return nullptr;
-    if (!h->e) return throw_status(env, SA_ESTATE, "flushExp: engine groups merge explicit buckets only");
     sa_exp_result *r = nullptr;
-    int rc = sa_flush_exp(h->e, &r);
+    int rc = h->e ? sa_flush_exp(h->e, &r) : sa_group_flush_exp(h->g, &r);
     if ((rc != SA_OK && rc != SA_EFULL) || !r) {
         if (r) sa_exp_result_free(r);
-        return engine_error(env, h, rc ? rc : SA_ESTATE, "sa_flush_exp");
+        return engine_error(env, h, rc ? rc : SA_ESTATE, h->e ? "sa_flush_exp" : "sa_group_flush_exp");
     }
     const size_t n = r->n_series, m = r->max_size;
     napi_value o;

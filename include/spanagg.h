@@ -261,6 +261,10 @@ int sa_group_sync(sa_group *g);
 /* Merged delta since the previous group flush (members reset); SA_EFULL as
  * sa_flush when any member dropped spans. Free with sa_red_result_free. */
 int sa_group_flush(sa_group *g, sa_red_result **out);
+/* exportMetrics of a group built with exp_max_size != 0: the members' delta
+ * exponential histograms folded per series (the histogram one engine fed
+ * every member's spans would hold). Free with sa_exp_result_free. */
+int sa_group_flush_exp(sa_group *g, sa_exp_result **out);
 /* Merged sketches of one resident window. Free with sa_sketch_result_free. */
 int sa_group_window_read(sa_group *g, uint64_t window_id, sa_sketch_result **out);
 int sa_group_window_advance(sa_group *g, uint64_t new_base);

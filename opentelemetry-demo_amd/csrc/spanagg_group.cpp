@@ -14,6 +14,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <map>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -134,6 +135,57 @@ int copy_reduce(sa_group *g, std::vector<Buf> &bufs, uint64_t len, bool max_u8) 
   return SA_OK;
 }
 
+// One series' exponential histogram while members' deltas are folded in.
+struct ExpoAcc {
+  uint64_t count = 0, zero = 0, sum_ns = 0;
+  double min = 0, max = 0;
+  int32_t scale = 20, offset = 0;  // go-expohisto's initial scale
+  std::vector<uint64_t> c;         // positive buckets offset .. offset + size - 1
+};
+
+inline int64_t shr_floor(int64_t v, int k) { return v >= 0 ? v >> k : -((-v - 1) >> k) - 1; }
+
+// Folds one member's histogram into a: go-expohisto's state depends only on
+// the values, and index(v) at scale s is index(v) at scale s + k shifted
+// right by k, so both go to the smaller scale, the index ranges unite and
+// the least further downscale that fits max_size applies (changeScale) --
+// exactly the histogram one engine fed both members' spans would hold.
+void expo_fold(ExpoAcc &a, const sa_exp_result &r, uint64_t j, uint32_t max_size) {
+  if (r.count[j] == 0) return;
+  if (a.count == 0) {
+    a.min = r.min[j];
+    a.max = r.max[j];
+  } else {
+    a.min = std::min(a.min, r.min[j]);
+    a.max = std::max(a.max, r.max[j]);
+  }
+  a.count += r.count[j];
+  a.zero += r.zero_count[j];
+  a.sum_ns += r.sum_ns[j];
+  const uint32_t nb = r.n_buckets[j];
+  const uint64_t *cnt = r.bucket_counts + j * r.max_size;
+  if (nb == 0) return;
+  if (a.c.empty()) {
+    a.scale = r.scale[j];
+    a.offset = r.offset[j];
+    a.c.assign(cnt, cnt + nb);
+    return;
+  }
+  int s = std::min(a.scale, r.scale[j]);
+  const int ka = a.scale - s, kd = r.scale[j] - s;
+  int64_t lo = std::min(shr_floor(a.offset, ka), shr_floor(r.offset[j], kd));
+  int64_t hi = std::max(shr_floor((int64_t)a.offset + (int64_t)a.c.size() - 1, ka),
+                        shr_floor((int64_t)r.offset[j] + nb - 1, kd));
+  int c = 0;
+  while (hi - lo >= (int64_t)max_size) lo = shr_floor(lo, 1), hi = shr_floor(hi, 1), ++c;
+  std::vector<uint64_t> out((size_t)(hi - lo + 1), 0);
+  for (size_t i = 0; i < a.c.size(); ++i) out[(size_t)(shr_floor((int64_t)a.offset + (int64_t)i, ka + c) - lo)] += a.c[i];
+  for (uint32_t i = 0; i < nb; ++i) out[(size_t)(shr_floor((int64_t)r.offset[j] + i, kd + c) - lo)] += cnt[i];
+  a.scale = s - c;
+  a.offset = (int32_t)lo;
+  a.c.swap(out);
+}
+
 }  // namespace
 
 extern "C" {
@@ -142,7 +194,6 @@ int sa_group_create(const sa_config *cfg, const int32_t *devices, uint32_t n, sa
   if (!out) return SA_EINVAL;
   *out = nullptr;
   if (!cfg || !devices || n == 0 || n > 64) return SA_EINVAL;
-  if (cfg->exp_max_size) return SA_EINVAL;  // groups merge explicit-bucket engines
   auto *g = new sa_group();
   g->cfg = *cfg;
   g->bounds.assign(cfg->bounds, cfg->bounds + cfg->n_bounds);
@@ -266,6 +317,7 @@ int sa_group_sync(sa_group *g) {
 int sa_group_flush(sa_group *g, sa_red_result **out) {
   if (!g || !out) return SA_EINVAL;
   *out = nullptr;
+  if (g->cfg.exp_max_size) return gfail(g, SA_ESTATE, "exponential-histogram group: use sa_group_flush_exp");
   const uint32_t n = (uint32_t)g->eng.size(), stride = g->nbk + 1;
   // 1. each member's non-zero series ids (and its drop counter)
   std::vector<uint64_t> cnt(n, 0), dropped(n, 0);
@@ -375,6 +427,71 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
     full = full || dropped[i] != g->dropped_seen[i];
     g->dropped_seen[i] = dropped[i];
   }
+  return full ? gfail(g, SA_EFULL, "key table full: spans were dropped since the previous flush") : SA_OK;
+}
+
+// exportMetrics of an exponential-histogram group: every member's delta
+// histograms (sa_flush_exp, which also reclaims its key table), folded per
+// series on the host (expo_fold).
+int sa_group_flush_exp(sa_group *g, sa_exp_result **out) {
+  if (!g || !out) return SA_EINVAL;
+  *out = nullptr;
+  if (!g->cfg.exp_max_size) return gfail(g, SA_ESTATE, "explicit-bucket group: use sa_group_flush");
+  const uint32_t n = (uint32_t)g->eng.size(), M = g->cfg.exp_max_size;
+  std::vector<sa_exp_result *> rs(n, nullptr);
+  bool full = false;
+  int bad = SA_OK;
+  uint32_t bad_i = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const int rc = sa_flush_exp(g->eng[i], &rs[i]);
+    if (rc == SA_EFULL) full = true;
+    else if (rc != SA_OK && bad == SA_OK) bad = rc, bad_i = i;
+  }
+  std::map<uint64_t, ExpoAcc> acc;
+  if (bad == SA_OK)
+    for (uint32_t i = 0; i < n; ++i)
+      for (uint64_t j = 0; rs[i] && j < rs[i]->n_series; ++j) expo_fold(acc[rs[i]->key_hash[j]], *rs[i], j, M);
+  for (sa_exp_result *r : rs)
+    if (r) sa_exp_result_free(r);
+  if (bad != SA_OK) return member_error(g, bad_i, bad, "sa_flush_exp");
+  const size_t ns = acc.size();
+  auto *h = new exp_holder();
+  h->keys.reserve(ns);
+  h->count.reserve(ns), h->zero.reserve(ns), h->sum_ns.reserve(ns), h->sum.reserve(ns);
+  h->min.reserve(ns), h->max.reserve(ns), h->scale.reserve(ns), h->offset.reserve(ns), h->nb.reserve(ns);
+  h->buckets.assign(ns * M, 0);
+  const double div = g->cfg.unit == SA_UNIT_S ? 1e9 : 1e6;
+  size_t r = 0;
+  for (const auto &kv : acc) {  // ascending keys
+    const ExpoAcc &a = kv.second;
+    h->keys.push_back(kv.first);
+    h->count.push_back(a.count);
+    h->zero.push_back(a.zero);
+    h->sum_ns.push_back(a.sum_ns);
+    h->sum.push_back((double)a.sum_ns / div);
+    h->min.push_back(a.min);
+    h->max.push_back(a.max);
+    h->scale.push_back(a.scale);
+    h->offset.push_back(a.offset);
+    h->nb.push_back((uint32_t)a.c.size());
+    std::copy(a.c.begin(), a.c.end(), h->buckets.begin() + r * M);
+    ++r;
+  }
+  h->r.n_series = ns;
+  h->r.max_size = M;
+  h->r.unit = g->cfg.unit;
+  h->r.key_hash = h->keys.data();
+  h->r.count = h->count.data();
+  h->r.zero_count = h->zero.data();
+  h->r.sum_ns = h->sum_ns.data();
+  h->r.sum = h->sum.data();
+  h->r.min = h->min.data();
+  h->r.max = h->max.data();
+  h->r.scale = h->scale.data();
+  h->r.offset = h->offset.data();
+  h->r.n_buckets = h->nb.data();
+  h->r.bucket_counts = h->buckets.data();
+  *out = &h->r;
   return full ? gfail(g, SA_EFULL, "key table full: spans were dropped since the previous flush") : SA_OK;
 }
 

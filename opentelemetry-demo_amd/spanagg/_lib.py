@@ -112,6 +112,7 @@ SIGNATURES = [
     ("sa_group_ingest", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch)]),
     ("sa_group_sync", C.c_int, [C.c_void_p]),
     ("sa_group_flush", C.c_int, [C.c_void_p, C.POINTER(C.POINTER(sa_red_result))]),
+    ("sa_group_flush_exp", C.c_int, [C.c_void_p, C.POINTER(C.POINTER(sa_exp_result))]),
     ("sa_group_window_read", C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.POINTER(sa_sketch_result))]),
     ("sa_group_window_advance", C.c_int, [C.c_void_p, C.c_uint64]),
     ("sa_group_get_stats", C.c_int, [C.c_void_p, C.POINTER(sa_stats)]),

@@ -195,6 +195,30 @@ def _ptr(x) -> int:
     return int(x.data_ptr())
 
 
+def _expo_result(obj, rc, out, allow_drops, what) -> ExpoResult:
+    """sa_exp_result -> ExpoResult (copies), freeing the library's result."""
+    if rc not in (0, _lib.SA_EFULL) or not out:
+        obj._check(rc if rc else _lib.SA_ESTATE, what)
+    try:
+        r = out.contents
+        n, M = int(r.n_series), int(r.max_size)
+
+        def arr(p, dt):
+            return np.zeros(0, dtype=dt) if n == 0 else np.ctypeslib.as_array(p, shape=(n,)).copy()
+
+        bk = np.zeros((0, M), np.uint64) if n == 0 else np.ctypeslib.as_array(r.bucket_counts, shape=(n, M))
+        nb = arr(r.n_buckets, np.uint32)
+        res = ExpoResult(arr(r.key_hash, np.uint64), arr(r.count, np.uint64), arr(r.zero_count, np.uint64),
+                         arr(r.sum_ns, np.uint64), arr(r.sum, np.float64), arr(r.min, np.float64),
+                         arr(r.max, np.float64), arr(r.scale, np.int32), arr(r.offset, np.int32),
+                         [bk[i, : int(nb[i])].copy() for i in range(n)], rc)
+    finally:
+        obj.lib.sa_exp_result_free(out)
+    if rc == _lib.SA_EFULL and not allow_drops:
+        raise SpanAggError(rc, f"{what}: spans dropped (key table full); stats={obj.stats()}")
+    return res
+
+
 class Engine:
     def __init__(self, config: Optional[Config] = None, **kw):
         self.lib = _lib.load()
@@ -261,26 +285,7 @@ class Engine:
     def flush_exp(self, allow_drops: bool = False) -> ExpoResult:
         out = C.POINTER(_lib.sa_exp_result)()
         rc = self.lib.sa_flush_exp(self._h, C.byref(out))
-        if rc not in (0, _lib.SA_EFULL) or not out:
-            self._check(rc if rc else _lib.SA_ESTATE, "sa_flush_exp")
-        try:
-            r = out.contents
-            n, M = int(r.n_series), int(r.max_size)
-
-            def arr(p, dt):
-                return np.zeros(0, dtype=dt) if n == 0 else np.ctypeslib.as_array(p, shape=(n,)).copy()
-
-            bk = np.zeros((0, M), np.uint64) if n == 0 else np.ctypeslib.as_array(r.bucket_counts, shape=(n, M))
-            nb = arr(r.n_buckets, np.uint32)
-            res = ExpoResult(arr(r.key_hash, np.uint64), arr(r.count, np.uint64), arr(r.zero_count, np.uint64),
-                             arr(r.sum_ns, np.uint64), arr(r.sum, np.float64), arr(r.min, np.float64),
-                             arr(r.max, np.float64), arr(r.scale, np.int32), arr(r.offset, np.int32),
-                             [bk[i, : int(nb[i])].copy() for i in range(n)], rc)
-        finally:
-            self.lib.sa_exp_result_free(out)
-        if rc == _lib.SA_EFULL and not allow_drops:
-            raise SpanAggError(rc, f"sa_flush_exp: spans dropped (key table full); stats={self.stats()}")
-        return res
+        return _expo_result(self, rc, out, allow_drops, "sa_flush_exp")
 
     def reclaim_keys(self, force: bool = False):
         """sa_reclaim_keys: empty the key table (force) or do the flush-time
@@ -381,6 +386,12 @@ class Group:
         out = C.POINTER(_lib.sa_red_result)()
         rc = self.lib.sa_group_flush(self._h, C.byref(out))
         return _red_result(self, rc, out, allow_drops, "sa_group_flush")
+
+    def flush_exp(self, allow_drops: bool = False) -> ExpoResult:
+        """sa_group_flush_exp: the members' exponential histograms, folded."""
+        out = C.POINTER(_lib.sa_exp_result)()
+        rc = self.lib.sa_group_flush_exp(self._h, C.byref(out))
+        return _expo_result(self, rc, out, allow_drops, "sa_group_flush_exp")
 
     def window_read(self, window_id: int) -> SketchResult:
         out = C.POINTER(_lib.sa_sketch_result)()

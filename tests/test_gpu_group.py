@@ -82,3 +82,32 @@ def test_group_high_cardinality_binned_members(monkeypatch):
 def test_group_rejects_bad_arguments():
     with pytest.raises(Exception):
         Group([], Config())
+
+
+@pytest.mark.parametrize("devices,rccl", [([0, 0], "0"), ([0, 0, 0], "0")])
+def test_group_exponential_histograms_fold_to_one_engine(devices, rccl, monkeypatch):
+    """sa_group_flush_exp: each member's delta exponential histograms (its own
+    trace-id shard, so its own scales) folded per series on the host must be
+    the histogram of the whole stream, bit-exact against the go-expohisto
+    restatement, over two flush intervals."""
+    monkeypatch.setenv("SPANAGG_GROUP_RCCL", rccl)
+    wl = generate_c2(300_000, seed=31)
+    parts = [wl.batch.slice(0, 120_000), wl.batch.slice(120_000, 300_000)]
+    with Group(devices, Config(n_services=wl.n_services, n_windows=16, exp_max_size=12)) as g:
+        g.window_advance(wl.first_window)
+        for part in parts:
+            g.ingest(part)
+            res = g.flush_exp()
+            ora = pyoracle.expo_aggregate(part, 12)
+            assert [int(k) for k in res.key_hash] == sorted(ora)
+            for i, k in enumerate(res.key_hash):
+                o = ora[int(k)]
+                assert (int(res.count[i]), int(res.zero_count[i]), int(res.scale[i]), int(res.offset[i])) == \
+                    (o["count"], o["zero_count"], o["scale"], o["offset"]), k
+                assert [int(x) for x in res.buckets[i]] == [int(x) for x in o["counts"]], k
+                assert res.min[i] == o["min"] and res.max[i] == o["max"]
+        with pytest.raises(Exception):
+            g.flush()  # explicit-bucket flush of an exponential group: SA_ESTATE
+        o = pyoracle.Oracle(n_services=wl.n_services)
+        o.ingest(wl.batch)
+        _check_windows(g, o)
