@@ -43,9 +43,18 @@ function main(cmd) {
     rules: DEMO_SPAN_NAME_RULES, native });
   const metrics = [];
   const exportsAfter = new Set(cmd.exports_after || []);
+  // batch: the requests between exports go through consumeTracesBatch together
+  // (the pipeline queue's path: decoded on the columnizer's worker threads)
+  let pending = [];
   cmd.requests.forEach((r, i) => {
     const bytes = Buffer.from(r, 'base64');
-    conn.consumeTraces(native ? bytes : otlp.decodeTraces(bytes));
+    if (cmd.batch) pending.push(bytes);
+    else conn.consumeTraces(native ? bytes : otlp.decodeTraces(bytes));
+    if (cmd.batch && (exportsAfter.has(i) || i === cmd.requests.length - 1)) {
+      const errs = conn.consumeTracesBatch(pending);
+      if (errs.some(Boolean)) throw errs.find(Boolean);
+      pending = [];
+    }
     if (exportsAfter.has(i)) metrics.push(otlp.encodeMetrics(conn.exportMetrics()).toString('base64'));
   });
   metrics.push(otlp.encodeMetrics(conn.exportMetrics()).toString('base64'));

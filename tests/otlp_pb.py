@@ -81,12 +81,31 @@ _MESSAGES = {
             ("is_monotonic", 3, F.TYPE_BOOL, OPT, None, None)],
     "Histogram": [("data_points", 1, F.TYPE_MESSAGE, REP, "HistogramDataPoint", None),
                   ("aggregation_temporality", 2, F.TYPE_INT32, OPT, None, None)],
+    # ExponentialHistogramDataPoint.Buckets (nested upstream; the name is not on the wire)
+    "ExpoBuckets": [("offset", 1, F.TYPE_SINT32, OPT, None, None),
+                    ("bucket_counts", 2, F.TYPE_UINT64, REP, None, None)],
+    "ExponentialHistogramDataPoint": [("attributes", 1, F.TYPE_MESSAGE, REP, "KeyValue", None),
+                                      ("start_time_unix_nano", 2, F.TYPE_FIXED64, OPT, None, None),
+                                      ("time_unix_nano", 3, F.TYPE_FIXED64, OPT, None, None),
+                                      ("count", 4, F.TYPE_FIXED64, OPT, None, None),
+                                      ("sum", 5, F.TYPE_DOUBLE, OPT, None, "proto3_optional"),
+                                      ("scale", 6, F.TYPE_SINT32, OPT, None, None),
+                                      ("zero_count", 7, F.TYPE_FIXED64, OPT, None, None),
+                                      ("positive", 8, F.TYPE_MESSAGE, OPT, "ExpoBuckets", None),
+                                      ("negative", 9, F.TYPE_MESSAGE, OPT, "ExpoBuckets", None),
+                                      ("flags", 10, F.TYPE_UINT32, OPT, None, None),
+                                      ("min", 12, F.TYPE_DOUBLE, OPT, None, "proto3_optional"),
+                                      ("max", 13, F.TYPE_DOUBLE, OPT, None, "proto3_optional"),
+                                      ("zero_threshold", 14, F.TYPE_DOUBLE, OPT, None, None)],
+    "ExponentialHistogram": [("data_points", 1, F.TYPE_MESSAGE, REP, "ExponentialHistogramDataPoint", None),
+                             ("aggregation_temporality", 2, F.TYPE_INT32, OPT, None, None)],
     "Metric": [("name", 1, F.TYPE_STRING, OPT, None, None),
                ("description", 2, F.TYPE_STRING, OPT, None, None),
                ("unit", 3, F.TYPE_STRING, OPT, None, None),
                ("gauge", 5, F.TYPE_MESSAGE, OPT, "Gauge", 0),
                ("sum", 7, F.TYPE_MESSAGE, OPT, "Sum", 0),
-               ("histogram", 9, F.TYPE_MESSAGE, OPT, "Histogram", 0)],
+               ("histogram", 9, F.TYPE_MESSAGE, OPT, "Histogram", 0),
+               ("exponential_histogram", 10, F.TYPE_MESSAGE, OPT, "ExponentialHistogram", 0)],
     "ScopeMetrics": [("scope", 1, F.TYPE_MESSAGE, OPT, "InstrumentationScope", None),
                      ("metrics", 2, F.TYPE_MESSAGE, REP, "Metric", None),
                      ("schema_url", 3, F.TYPE_STRING, OPT, None, None)],

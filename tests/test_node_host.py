@@ -462,3 +462,123 @@ def test_receiver_interoperates_with_grpcio_and_http_clients():
     assert summary["requests"] == 2
     assert summary["spans"] == 2 * sum(len(spans) for _, spans in SPEC)
     assert summary["names"][:2] == [s["name"] for s in SPEC[0][1]]
+
+
+def test_exponential_histograms_through_the_node_connector():
+    """`histogram.exponential` in the Node connector (over the test stand-in
+    engine, host logic only): the OTLP ExponentialHistogram it encodes, parsed
+    by Python protobuf, equals an independent go-expohisto restatement
+    (tests/golden/gen_expo.py) of each series' durations -- scale, offset,
+    buckets, zero count, count, min, max, sum."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_expo", os.path.join(os.path.dirname(__file__), "golden",
+                                                                           "gen_expo.py"))
+    gen_expo = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen_expo)
+    rng = np.random.default_rng(5)
+    req = M["ExportTraceServiceRequest"]()
+    per_series = {}
+    for svc in ("frontend", "cart"):
+        rs = req.resource_spans.add()
+        add_attrs(rs.resource.attributes, {"service.name": svc})
+        ss = rs.scope_spans.add()
+        for i in range(400):
+            name = f"op-{i % 3}"
+            start = T0 + int(rng.integers(0, 5_000_000_000))
+            dur = 0 if i % 37 == 0 else int(np.exp(rng.uniform(8, 24)))
+            ss.spans.add(trace_id=rng.integers(0, 256, 16, dtype=np.uint8).tobytes(), span_id=b"\x01" * 8,
+                         name=name, kind=2, start_time_unix_nano=start, end_time_unix_nano=start + dur)
+            per_series.setdefault((svc, name), []).append(dur)
+    out = node("cli.js", {"cmd": "connector_export", "requests": [base64.b64encode(req.SerializeToString()).decode()],
+                          "spanmetrics": {"histogram": {"exponential": {"max_size": 24}}}})
+    msg = M["ExportMetricsServiceRequest"].FromString(base64.b64decode(out["b64"]))
+    seen = 0
+    for rm in msg.resource_metrics:
+        svc = {kv.key: get_any(kv.value) for kv in rm.resource.attributes}["service.name"]
+        calls, dur = rm.scope_metrics[0].metrics
+        assert dur.WhichOneof("data") == "exponential_histogram" and dur.unit == "ms"
+        assert dur.exponential_histogram.aggregation_temporality == 2
+        for dp in dur.exponential_histogram.data_points:
+            name = {kv.key: get_any(kv.value) for kv in dp.attributes}["span.name"]
+            h = gen_expo.Histogram(24)
+            for d in per_series[(svc, name)]:
+                h.update(d / 1e6)
+            e = h.result()
+            assert (dp.count, dp.zero_count, dp.scale, dp.positive.offset) == \
+                (e["count"], e["zero_count"], e["scale"], e["offset"])
+            assert list(dp.positive.bucket_counts) == e["counts"]
+            assert dp.min == float.fromhex(e["min"]) and dp.max == float.fromhex(e["max"])
+            assert abs(dp.sum - float.fromhex(e["sum"])) <= 1e-9 * float.fromhex(e["sum"])
+            assert not dp.negative.bucket_counts
+            seen += 1
+    assert seen == len(per_series)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [None, [0, 0]], ids=["engine", "group2"])
+def test_node_host_exponential_end_to_end(devices):
+    """histogram.exponential through the real addon: OTLP bytes -> native
+    columnizer (consumeTracesBatch on worker threads) -> GPU exponential
+    histograms (sa_flush_exp / sa_group_flush_exp) -> host fold of the deltas
+    into cumulative histograms -> OTLP.  The last cumulative export, parsed by
+    Python protobuf, equals the go-expohisto restatement of every series'
+    durations (tests/golden/gen_expo.py); the window sketches stay bit-exact."""
+    import importlib.util
+    import pyoracle
+    from spanagg.engine import SpanBatch
+    spec = importlib.util.spec_from_file_location("gen_expo", os.path.join(os.path.dirname(__file__), "golden",
+                                                                           "gen_expo.py"))
+    gen_expo = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen_expo)
+    requests, facts = synth_requests(seed=23)
+    env = dict(os.environ, SPANAGG_NODE_GPU="1")
+    config = {"batch_size": 4096, "key_capacity": 4096, "columnizer_threads": 4,
+              "histogram": {"exponential": {"max_size": 40}}}
+    if devices:
+        config["devices"] = devices
+    out = node("e2e.js", {"requests": requests, "config": config, "exports_after": [3, 7], "native": True,
+                          "batch": True}, timeout=300, env=env)
+    series = {}
+    for ra, nm, k, st, start, end, _ in facts:
+        sid = pykeys.series_hash(pykeys.resource_hash(ra), pykeys.build_key(ra["service.name"], nm, k, st))
+        series.setdefault(sid, []).append(end - start if end > start else 0)
+    msg = M["ExportMetricsServiceRequest"].FromString(base64.b64decode(out["metrics"][-1]))
+    seen = 0
+    for rm in msg.resource_metrics:
+        res_attrs = {kv.key: get_any(kv.value) for kv in rm.resource.attributes}
+        calls, dur = rm.scope_metrics[0].metrics
+        assert dur.WhichOneof("data") == "exponential_histogram"
+        for cdp, dp in zip(calls.sum.data_points, dur.exponential_histogram.data_points):
+            a = {kv.key: get_any(kv.value) for kv in dp.attributes}
+            sid = pykeys.series_hash(pykeys.resource_hash(res_attrs), pykeys.build_key(
+                a["service.name"], a["span.name"], pykeys.SPAN_KIND_STR.index(a["span.kind"]),
+                pykeys.STATUS_CODE_STR.index(a["status.code"])))
+            h = gen_expo.Histogram(40)
+            for d in series[sid]:
+                h.update(d / 1e6)
+            e = h.result()
+            assert (dp.count, dp.zero_count, dp.scale, dp.positive.offset) == \
+                (e["count"], e["zero_count"], e["scale"], e["offset"]), sid
+            assert list(dp.positive.bucket_counts) == e["counts"], sid
+            assert dp.min == float.fromhex(e["min"]) and dp.max == float.fromhex(e["max"])
+            assert cdp.as_int == e["count"]
+            seen += 1
+    assert seen == len(series)
+    tids = np.frombuffer(b"".join(f[6] for f in facts), dtype="<u8").reshape(-1, 2)
+    svc_ids = out["services"]
+    sids = [pykeys.series_hash(pykeys.resource_hash(f[0]), pykeys.build_key(f[0]["service.name"], f[1], f[2], f[3]))
+            for f in facts]
+    batch = SpanBatch(np.array(sids, dtype=np.uint64),
+        np.array([f[4] for f in facts], dtype=np.uint64), np.array([f[5] for f in facts], dtype=np.uint64),
+        tids[:, 0].copy(), tids[:, 1].copy(),
+        np.array([svc_ids[f[0]["service.name"]] | (f[2] << 16) | (f[3] << 19) for f in facts], dtype=np.uint32))
+    o = pyoracle.Oracle(n_services=64)
+    o.ingest(batch)
+    for w in out["windows"]:
+        wid = int(w["window_id"])
+        if wid in set(o.window_ids()):
+            rh, rc = o.window(wid)
+            assert np.array_equal(np.frombuffer(base64.b64decode(w["hll"]), np.uint8).reshape(64, 1 << 14), rh)
+            assert np.array_equal(np.frombuffer(base64.b64decode(w["cms"]), np.uint32).reshape(4, 2048), rc)
+    assert int(out["stats"]["engines"]) == (len(devices) if devices else 1)
+    assert int(out["stats"]["nativeRequests"]) == len(requests)
