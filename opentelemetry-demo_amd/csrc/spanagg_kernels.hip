@@ -75,6 +75,105 @@ __device__ __forceinline__ void flush_lds(const IngestParams &P, uint32_t cap, u
   }
 }
 
+// End-of-launch write-back of ingest_v2_kernel for a compile-time geometry
+// (UPT slab-count pairs and SPT slab-sum pairs per thread): every global read
+// of the epilogue -- touched slab-count pairs, touched slab sums, the ERROR
+// slab cell, the words of the queued HLL raises and the lower-bound
+// sub-block -- is issued before the first dependent store, so the tail of a
+// workgroup is one memory round trip instead of one per phase (count rounds,
+// sums, ERROR cells, HLL CAS, bound refresh: ~7 in a row).  A stale HLL word
+// only makes the CAS retry; a stale register read for the bound can only lower
+// it, which keeps it a lower bound.
+template <int UPT, int SPT>
+__device__ __forceinline__ void v2_epilogue(const IngestParams &P, uint32_t cap, uint32_t nw, uint32_t log2cap,
+                                            const unsigned long long *lsum, const uint32_t *lcnt,
+                                            const uint32_t *etab, bool err_lds, const uint2 *hq,
+                                            uint32_t nq) {
+  constexpr uint32_t B = kLdsBlock;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const bool slabs = !(P.diag & 8u);
+  // 1. reads
+  uint4 *scnt = reinterpret_cast<uint4 *>(P.slab_cnt + (uint64_t)blockIdx.x * cap * 2 * nw);
+  const uint2 *lw = reinterpret_cast<const uint2 *>(lcnt);
+  uint2 w[UPT];
+  uint4 g[UPT];
+#pragma unroll
+  for (int u = 0; u < UPT; ++u) w[u] = slabs ? lw[tid + u * B] : make_uint2(0, 0);
+#pragma unroll
+  for (int u = 0; u < UPT; ++u) g[u] = (w[u].x | w[u].y) ? scnt[tid + u * B] : make_uint4(0, 0, 0, 0);
+  ulonglong2 *ss = reinterpret_cast<ulonglong2 *>(P.slab_sum + (uint64_t)blockIdx.x * cap);
+  const ulonglong2 *ls = reinterpret_cast<const ulonglong2 *>(lsum);
+  ulonglong2 sv[SPT], sg[SPT];
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) sv[u] = slabs ? ls[tid + u * B] : make_ulonglong2(0, 0);
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) sg[u] = (sv[u].x | sv[u].y) ? ss[tid + u * B] : make_ulonglong2(0, 0);
+  const uint32_t e = err_lds ? etab[tid] : 0u;
+  uint32_t *ecell =
+      e ? P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1) : nullptr;
+  const uint32_t ev = e ? *ecell : 0u;
+  constexpr uint32_t kQ = kHllQueue / B;
+  uint2 q[kQ];
+  uint32_t qv[kQ];
+#pragma unroll
+  for (uint32_t i = 0; i < kQ; ++i) {
+    q[i] = tid + i * B < nq ? hq[tid + i * B] : make_uint2(0, 0);
+    qv[i] = q[i].y ? *reinterpret_cast<const uint32_t *>(P.hll + (q[i].x & ~3u)) : 0xFFFFFFFFu;
+  }
+  // the bound sub-block of this wave (as hll_lb_refresh); up to 4 quads per lane
+  const uint32_t lbt = P.lb_n ? min(P.lb_n, gridDim.x * (B / 64)) : 0u, gi = blockIdx.x * (B / 64) + wave;
+  const bool lb = gi < lbt;
+  const uint32_t sb = lb ? (uint32_t)(((uint64_t)P.lb_seq * lbt + gi) % P.lb_n) : 0u;
+  const uint32_t quads = lb ? (1u << P.lb_shift) / 16 : 0u;
+  const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
+  uint4 lv[4];
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i)
+    lv[i] = lane + i * 64 < quads ? src[lane + i * 64] : make_uint4(~0u, ~0u, ~0u, ~0u);
+  // 2. dependent stores
+#pragma unroll
+  for (int u = 0; u < UPT; ++u) {
+    if (w[u].x | w[u].y) {
+      g[u].x += w[u].x & 0xFFFFu;
+      g[u].y += w[u].x >> 16;
+      g[u].z += w[u].y & 0xFFFFu;
+      g[u].w += w[u].y >> 16;
+      scnt[tid + u * B] = g[u];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) {
+    if (sv[u].x | sv[u].y) {
+      sg[u].x += sv[u].x;
+      sg[u].y += sv[u].y;
+      ss[tid + u * B] = sg[u];
+    }
+  }
+  if (e) *ecell = ev + (e & 0xFFFFu);
+#pragma unroll
+  for (uint32_t i = 0; i < kQ; ++i) {
+    if (!q[i].y) continue;
+    SA_GLOBAL uint32_t *word = gbl(reinterpret_cast<uint32_t *>(P.hll + (q[i].x & ~3u)));
+    const uint32_t sh = (q[i].x & 3u) * 8;
+    uint32_t old = qv[i];
+    while (((old >> sh) & 0xFFu) < q[i].y) {  // a failed CAS refreshes `old`
+      const uint32_t nw = (old & ~(0xFFu << sh)) | (q[i].y << sh);
+      if (__hip_atomic_compare_exchange_strong(word, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT))
+        break;
+    }
+  }
+  if (lb) {
+    uint32_t mn = 0xFFu;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) mn = min(mn, min_bytes(lv[i]));
+    for (uint32_t o = lane + 256; o < quads; o += 64) mn = min(mn, min_bytes(src[o]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+    if (lane == 0) P.hll_lb[sb] = (uint8_t)mn;
+  }
+}
+
 // Probe the LDS key mirror along the key's sequence from position i0 (the
 // earlier positions are known not to hold `key`); returns the slot or
 // kNotFound (empty slot reached / probe limit).
@@ -409,7 +508,7 @@ __device__ __forceinline__ bool lds_err_add(uint32_t *etab, uint32_t ek) {
 // wave tile instead of NBUF (a round takes NBUF claims), halving the work a
 // wave can still hold when its neighbours run out.
 template <int S, int NBUF, int AUX, bool DIAG, int LC = 0, int NWC = 0, int PC = 0, int HAUX = -1,
-          bool DYN = false, int OPT = 0>
+          bool DYN = false, int OPT = 0, bool EPI = false>
 __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 0] = __builtin_amdgcn_s_memrealtime();
@@ -423,7 +522,8 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + cap);
   uint2 *hq = reinterpret_cast<uint2 *>(lcnt + cap * nw);
   uint32_t *hq_n = reinterpret_cast<uint32_t *>(hq + kHllQueue);
-  BinEntry *lbins = reinterpret_cast<BinEntry *>(hq_n + 4);
+  uint32_t *lstat = hq_n + 4;  // EPI: [4] event counts (zero key, bad service, out of ring, dropped)
+  BinEntry *lbins = reinterpret_cast<BinEntry *>(hq_n + 8);
   uint32_t *etab = reinterpret_cast<uint32_t *>(lbins + kBins);  // [kErrTab]: (key+1) << 16 | count
   uint8_t *llb = reinterpret_cast<uint8_t *>(etab + kErrTab);       // [kLbMaxSub] HLL lower bounds
   const bool err_lds = P.errslab != nullptr;
@@ -511,6 +611,9 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     hq_n[0] = 0;
     hq_n[1] = (kTileClaims ? 2u * NBUF : 2u) * kWaves;  // DYN: next unclaimed chunk of this workgroup's range
   }
+  if (threadIdx.x < 4) lstat[threadIdx.x] = 0;
+  {
+  }
   etab[threadIdx.x] = 0;  // kErrTab == kLdsBlock
   if (lb_on && threadIdx.x * 4 < P.lb_n) reinterpret_cast<uint32_t *>(llb)[threadIdx.x] = lbw;
   __syncthreads();
@@ -568,7 +671,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
       // used after the tile registers are re-filled, and sharing them would
       // make the allocator rotate the tile ring through copies that wait.
       key[j] = copy_u64(T.key[j]);
-      if (!(diag & 128u)) n_zero += wave_count(valid && key[j] == 0);
+      if (!(diag & 128u) && !EPI) n_zero += wave_count(valid && key[j] == 0);
       dur[j] = T.e[j] > T.s[j] ? T.e[j] - T.s[j] : 0;
       bkt[j] = (diag & 32u) ? (uint32_t)dur[j] & 15u : bucket_lds<1>(dur[j], lbins, P);
       const uint32_t meta = copy_u32(T.meta[j]);  // see key
@@ -577,8 +680,20 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
       ws[j] = (diag & 64u) ? (uint32_t)(T.e[j] >> 34) & 7u : window_slot(P, T.e[j]);
       const bool win_ok = ws[j] != 0xFFFFFFFFu;
       if (!(diag & 128u)) {
-        n_badsvc += wave_count(valid && !svc_ok);
-        n_oor += wave_count(valid && svc_ok && !win_ok);
+        if constexpr (EPI) {
+          // rare events: LDS counters (no wave-uniform accumulators held in
+          // scalar registers across the loop)
+          const uint32_t ev = (valid && key[j] == 0 ? 1u : 0u) | (valid && !svc_ok ? 2u : 0u) |
+                              (valid && svc_ok && !win_ok ? 4u : 0u);
+          if (__builtin_expect(ev != 0, 0)) {
+            if (ev & 1u) atomicAdd(&lstat[0], 1u);
+            if (ev & 2u) atomicAdd(&lstat[1], 1u);
+            if (ev & 4u) atomicAdd(&lstat[2], 1u);
+          }
+        } else {
+          n_badsvc += wave_count(valid && !svc_ok);
+          n_oor += wave_count(valid && svc_ok && !win_ok);
+        }
       }
       const bool sk = valid && svc_ok && win_ok;
       err[j] = sk && ((meta >> 19) & 3u) == 2u && !(diag & 4u);
@@ -645,7 +760,11 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
       for (int j = 0; j < S; ++j) {
         if (__builtin_expect(__ballot(need[j]) != 0, 0)) {
           cold_lookup_wave(lkeys, need[j], key[j], log2cap, found[j]);
-          n_drop += wave_count(need[j] && found[j] == kNotFound);
+          if constexpr (EPI) {
+            if (need[j] && found[j] == kNotFound) atomicAdd(&lstat[3], 1u);
+          } else {
+            n_drop += wave_count(need[j] && found[j] == kNotFound);
+          }
         }
       }
     } else {
@@ -767,21 +886,35 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   const uint64_t wave_loop_end = DIAG && P.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 2] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
-  flush_lds(P, cap, nw, lsum, lcnt);
-  if (err_lds) {  // this workgroup's ERROR counts -> its private slab (plain RMW)
-    const uint32_t e = etab[threadIdx.x];
-    if (e) {
-      uint32_t *cell = P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1);
-      *cell += e & 0xFFFFu;
-    }
-  }
   const uint32_t nq = *hq_n < kHllQueue ? *hq_n : kHllQueue;
-  for (uint32_t i = threadIdx.x; i < nq; i += kLdsBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
-  hll_lb_refresh(P, threadIdx.x >> 6, kWaves);
+  if constexpr (LC != 0 && NWC != 0 && EPI) {
+    // compile-time geometry: the batched epilogue (one round trip)
+    constexpr uint32_t kCap = 1u << LC;
+    static_assert((kCap * NWC / 2) % kLdsBlock == 0 && (kCap / 2) % kLdsBlock == 0, "epilogue geometry");
+    v2_epilogue<kCap * NWC / 2 / kLdsBlock, kCap / 2 / kLdsBlock>(P, cap, nw, log2cap, lsum, lcnt, etab, err_lds,
+                                                                    hq, nq);
+  } else {
+    flush_lds(P, cap, nw, lsum, lcnt);
+    if (err_lds) {  // this workgroup's ERROR counts -> its private slab (plain RMW)
+      const uint32_t e = etab[threadIdx.x];
+      if (e) {
+        uint32_t *cell = P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1);
+        *cell += e & 0xFFFFu;
+      }
+    }
+    for (uint32_t i = threadIdx.x; i < nq; i += kLdsBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
+    hll_lb_refresh(P, threadIdx.x >> 6, kWaves);
+  }
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 3] = __builtin_amdgcn_s_memrealtime();
   if (DIAG && P.dbg && (threadIdx.x & 63) == 0) {
     for (int i = 0; i < 6; ++i) P.dbg[blockIdx.x * kDbgPerWg + 8 + (threadIdx.x >> 6) * 8 + i] = seg[i];
     P.dbg[blockIdx.x * kDbgPerWg + 8 + (threadIdx.x >> 6) * 8 + 6] = wave_loop_end;
+  }
+  if constexpr (EPI) {  // (lstat is final: the epilogue follows a workgroup barrier)
+    if (threadIdx.x < 4 && lstat[threadIdx.x]) {
+      constexpr uint32_t kIdx[4] = {kStatZeroKey, kStatInvalidService, kStatWindowOOR, kStatDropped};
+      atomicAdd(&P.stats[kIdx[threadIdx.x]], (unsigned long long)lstat[threadIdx.x]);
+    }
   }
   if ((threadIdx.x & 63) == 0) {
     if (n_zero) atomicAdd(&P.stats[kStatZeroKey], (unsigned long long)n_zero);
@@ -1424,6 +1557,7 @@ static const void *small_fn(bool bt, int v, bool diag) {
       case 16: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1>;
       case 17: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 3>;
       case 18: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 2>;
+      case 19: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1, true>;
       default: return (const void *)&ingest_v2_kernel<2, 2, 2, false>;
     }
   }
