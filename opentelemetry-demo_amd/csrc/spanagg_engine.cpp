@@ -31,7 +31,7 @@ constexpr size_t kLdsBudget = 144 * 1024;  // small-table path LDS ceiling per w
 constexpr uint64_t kSlabLimit = 1ULL << 31;  // per-workgroup spans between slab reductions
 // small path: ingest_v2_kernel variant 16 (14 + key-table loads issued ahead
 // of every tile load); SPANAGG_VARIANT overrides
-constexpr int kDefaultVariant = 16;
+constexpr int kDefaultVariant = 19;
 constexpr uint32_t kMaxSlabSets = 4;      // per-workgroup slab sets (small path)
 constexpr uint32_t kDefaultSlabSets = 2;  // SPANAGG_SLAB_SETS overrides
 
