@@ -174,19 +174,40 @@ def box_cores():
     return {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "usable": max(1, usable)}
 
 
-def trace_variants(w0, w1, k, seed):
+def to_shard(w1, rank, world):
+    """Trace-id word 1 moved into this rank's shard: w1 - w1 % world + rank, so
+    spanagg.dist.shard_of (trace_w1 % world) sends every span of the batch to
+    this rank, as a collector sharding one stream by trace id would (traces
+    stay distinct up to 64-bit collisions).  w1: int64 tensor (u64 bits)."""
+    if world == 1:
+        return w1
+    import torch
+    u = w1.view(torch.uint64) if hasattr(torch, "uint64") else None
+    if u is not None:
+        try:
+            return (u - u % world + rank).view(torch.int64)
+        except (RuntimeError, TypeError):
+            pass
+    # unsigned remainder from signed int64 arithmetic: 2^64 = q * world + r
+    r64 = (1 << 64) % world
+    rem = torch.remainder(w1, world)                     # (w1 as signed) mod world
+    rem = torch.where(w1 < 0, torch.remainder(rem + r64, world), rem)
+    return w1 - rem + rank
+
+
+def trace_variants(w0, w1, k, seed, rank=0, world=1):
     """k distinct trace-id column pairs from one batch's: every trace id XORed
     with a per-variant random 128-bit constant (a bijection, so the traces of
-    a variant stay distinct and keep their span counts).  Each step of the
-    bench aggregates a variant no launch has seen, so HLL registers keep
-    rising as they would on a live stream."""
+    a variant stay distinct and keep their span counts), then kept in this
+    rank's trace-id shard (to_shard).  Each step of the bench aggregates a
+    variant no launch has seen, so HLL registers keep rising as they would on
+    a live stream."""
     import numpy as np
-    import torch
     rng = np.random.Generator(np.random.PCG64(seed))
-    out = [(w0, w1)]
+    out = [(w0, to_shard(w1, rank, world))]
     for _ in range(k - 1):
         c0, c1 = (int(x) for x in rng.integers(-2**63, 2**63 - 1, 2, dtype=np.int64))
-        out.append((w0 ^ c0, w1 ^ c1))
+        out.append((w0 ^ c0, to_shard(w1 ^ c1, rank, world)))
     return out
 
 
@@ -224,7 +245,11 @@ def run_workload(name, n, args, device, rank, world, barrier):
         cols.append(torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(device))
     n_iso = max(3, args.steps // 5)
     n_var = min(args.variants, 1 + args.warmup + n_iso + args.steps)
-    variants = trace_variants(cols[3], cols[4], n_var, seed=1000 + rank)
+    variants = trace_variants(cols[3], cols[4], n_var, seed=1000 + rank, rank=rank, world=world)
+    if world > 1:  # every span of every variant belongs to this rank's trace-id shard
+        from spanagg.dist import shard_of
+        for _, vw1 in variants[:2]:
+            assert (shard_of(vw1[:4096].cpu().numpy().view(np.uint64), world) == rank).all()
     eng = Engine(Config(n_services=max(n_services, 1), n_windows=16, key_capacity=key_capacity,
                         device=device.index))
     eng.window_advance(first_window)
@@ -420,7 +445,8 @@ def main():
             "metric": METRIC, "value": world * n * args.steps / elapsed, "unit": "spans/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
-            "data": "synthetic (seeded PCG64 generator, spanagg/synth.py; one shard per rank; every launch "
+            "data": "synthetic (seeded PCG64 generator, spanagg/synth.py; each rank's batch in its trace-id shard "
+                    "(trace_w1 % N == rank); every launch "
                     "a distinct trace-id variant of the rank's batch)",
             "config": {"workload": WORKLOADS[args.workload], "spans_per_step_per_gpu": n,
                        "global_spans_per_step": n * world,

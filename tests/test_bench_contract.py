@@ -6,6 +6,7 @@ import os
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -33,3 +34,21 @@ def test_cpu_worker_reports_a_rate():
     assert p.returncode == 0, p.stderr[-2000:]
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["spans"] >= 2_000_000 and r["seconds"] > 0
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_bench_batches_sit_in_their_trace_id_shard(world):
+    """bench.py at N ranks: every span of a rank's batch and of each of its
+    trace-id variants is owned by that rank under spanagg.dist.shard_of, and
+    spans of one trace stay together (equal ids map to equal ids)."""
+    import torch
+    from spanagg.dist import shard_of
+    rng = np.random.default_rng(world)
+    w0 = torch.from_numpy(rng.integers(0, 2**63, 20000, dtype=np.int64))
+    w1 = torch.from_numpy(rng.integers(0, 2**64 - 1, 20000, dtype=np.uint64).view(np.int64))
+    w1[1000:1010] = w1[0]  # one trace with several spans
+    for rank in range(world):
+        for v0, v1 in bench.trace_variants(w0, w1, 3, seed=5, rank=rank, world=world):
+            u = v1.numpy().view(np.uint64)
+            assert (shard_of(u, world) == rank).all()
+            assert (u[1000:1010] == u[0]).all()
