@@ -335,8 +335,8 @@ def roofline(name, n, r, traffic_path=None):
     traffic, tsrc = load_traffic(tpath, name)
     piped = BYTES_PER_SPAN * n / (r["device_ms"] * 1e-3) / 1e9
     kern = {"c2": "ingest_v2_kernel (spanagg_kernels.hip)",
-            "c4": "bt_scatter_kernel + bt_aggregate_kernel (spanagg_binned.hip)",
-            "c4zipf": "bt_scatter_kernel + bt_aggregate_kernel (spanagg_binned.hip)"}[name]
+            "c4": "bt_scatter2_kernel + bt_aggregate2_kernel (spanagg_binned.hip)",
+            "c4zipf": "bt_scatter2_kernel + bt_aggregate2_kernel (spanagg_binned.hip)"}[name]
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kern, "kernel_ms": r["kernel_ms"],
             "bytes_per_span": BYTES_PER_SPAN, "traffic_source": tsrc,
