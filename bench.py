@@ -17,7 +17,11 @@ wall clock of the timed steps.
 
 Every launch aggregates a distinct trace-id variant of the batch (trace ids
 XORed with a per-variant constant), so HLL registers keep rising as on a live
-stream; the cold first launch on a fresh engine is reported on its own.  At
+stream; the cold first launch on a fresh engine is reported on its own, and
+the next `--settle` launches (default 16), while the window's HLL registers
+and their lower bounds settle, are timed one by one as `settle_ms` and kept
+out of `value` and `kernel_ms` (a 10 s window at these rates spans ~10^5
+launches, so the settled launch is the one a collector runs).  At
 N=1 the line also carries `c4` and `c4zipf` sub-objects (BASELINE config 4,
 uniform and Zipf(1.1) over 1 M series) with their own roofline.
 
@@ -244,7 +248,7 @@ def run_workload(name, n, args, device, rank, world, barrier):
     for c in batch.columns():
         cols.append(torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(device))
     n_iso = max(3, args.steps // 5)
-    n_var = min(args.variants, 1 + args.warmup + n_iso + args.steps)
+    n_var = min(args.variants, 1 + args.settle + args.warmup + n_iso + args.steps)
     variants = trace_variants(cols[3], cols[4], n_var, seed=1000 + rank, rank=rank, world=world)
     if world > 1:  # every span of every variant belongs to this rank's trace-id shard
         from spanagg.dist import shard_of
@@ -273,10 +277,20 @@ def run_workload(name, n, args, device, rank, world, barrier):
     c0.record(stream)
     step(0, stream)
     c1.record(stream)
+    # settling launches: the first launches into a window raise many HLL
+    # registers and its lower bounds are still low, so they run longer (a 10 s
+    # window at this rate is ~10^5 launches, all but the first few settled);
+    # timed one by one and reported as settle_ms, never part of value
+    st = [(ev(), ev()) for _ in range(args.settle)]
+    for a, b in st:
+        a.record(stream)
+        step(0, stream)
+        b.record(stream)
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(device)
     cold_ms = c0.elapsed_time(c1)
+    settle_ms = [round(a.elapsed_time(b), 4) for a, b in st]
     # 1) the kernel alone: serial launches on one stream, HIP events around each
     iso = [(ev(), ev()) for _ in range(n_iso)]
     for a, b in iso:
@@ -322,7 +336,8 @@ def run_workload(name, n, args, device, rank, world, barrier):
     st = eng.stats()
     calls_ok = int(red.calls.sum()) == launches[0] * n * world - st["zero_key"] * (1 if world == 1 else world)
     out = {"wl": wl, "batch": batch, "eng": eng, "first_window": first_window, "elapsed": elapsed,
-           "kernel_ms": kernel_ms, "device_ms": device_ms, "cold_ms": cold_ms, "merge_ms": merge_ms,
+           "kernel_ms": kernel_ms, "device_ms": device_ms, "cold_ms": cold_ms, "settle_ms": settle_ms,
+           "merge_ms": merge_ms,
            "calls_ok": calls_ok, "enqueue_s": enqueue_s, "streams": len(streams), "variants": n_var,
            "launches": launches[0], "hll_p": 14}
     del variants, cols
@@ -361,7 +376,9 @@ def main():
     ap.add_argument("--streams", type=int, default=2,
                     help="launch streams the steps alternate over (the engine's two slab sets "
                          "let consecutive launches overlap); 1 = strictly serial launches")
-    ap.add_argument("--variants", type=int, default=64,
+    ap.add_argument("--settle", type=int, default=16,
+                    help="untimed launches after the cold one, before the warm-up (HLL registers settle)")
+    ap.add_argument("--variants", type=int, default=128,
                     help="distinct trace-id variants of the batch (one per launch up to this many)")
     ap.add_argument("--sub", default="c4,c4zipf",
                     help="extra workloads reported as sub-objects of the line at N=1 ('' = none)")
@@ -432,7 +449,7 @@ def main():
             r["eng"].close()
             subs[sub] = {"workload": WORKLOADS[sub], "value": n * args.steps / r["elapsed"], "unit": "spans/s",
                          "ms_per_step": r["elapsed"] * 1e3 / args.steps, "steps": args.steps,
-                         "warmup": args.warmup, "cold_launch_ms": r["cold_ms"],
+                         "warmup": args.warmup, "cold_launch_ms": r["cold_ms"], "settle_ms": r["settle_ms"],
                          "roofline": roofline(sub, n, r), "calls_check": r["calls_ok"],
                          "trace_variants": r["variants"]}
             torch.cuda.empty_cache()
@@ -452,7 +469,8 @@ def main():
                        "global_spans_per_step": n * world,
                        "parallelism": f"trace-id shards x{world}, RCCL merge at flush"},
             "roofline": roofline(args.workload, n, main_r, args.traffic),
-            "cold_launch_ms": main_r["cold_ms"], "trace_variants": main_r["variants"],
+            "cold_launch_ms": main_r["cold_ms"], "settle_ms": main_r["settle_ms"],
+            "trace_variants": main_r["variants"],
             "merge_ms": main_r["merge_ms"], "calls_check": main_r["calls_ok"],
             "host_enqueue_us_per_step": main_r["enqueue_s"] * 1e6 / max(1, args.steps),
         }
