@@ -52,3 +52,19 @@ def test_bench_batches_sit_in_their_trace_id_shard(world):
             u = v1.numpy().view(np.uint64)
             assert (shard_of(u, world) == rank).all()
             assert (u[1000:1010] == u[0]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_bench_trace_id_shards_on_device(world):
+    """The same sharding on device-resident columns (bench.py applies it to
+    cuda tensors): every span of each variant lands on its rank."""
+    import torch
+    from spanagg.dist import shard_of
+    rng = np.random.default_rng(world)
+    w0 = torch.from_numpy(rng.integers(0, 2**63, 50000, dtype=np.int64)).cuda()
+    w1 = torch.from_numpy(rng.integers(0, 2**64 - 1, 50000, dtype=np.uint64).view(np.int64)).cuda()
+    for rank in range(world):
+        for _, v1 in bench.trace_variants(w0, w1, 3, seed=9, rank=rank, world=world):
+            assert v1.is_cuda
+            assert (shard_of(v1.cpu().numpy().view(np.uint64), world) == rank).all()
