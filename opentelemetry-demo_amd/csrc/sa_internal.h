@@ -44,8 +44,10 @@ struct IngestParams {
   // small-table path: per-workgroup slabs [G][cap][nbk] u32 and [G][cap] u64
   uint32_t *slab_cnt;
   unsigned long long *slab_sum;
-  // HBM-table path: counters [cap][nbk+1] u64 (last = sum_ns)
+  // HBM-table path: counters [cap][nbk+1] u64 (last = sum_ns); binned path:
+  // 32-B rows (kRowBytes) plus the u64 spill array base64 [cap][nbk + 1]
   unsigned long long *gcounts;
+  unsigned long long *base64;
   // histogram: bucket(d) = nneg + #{i < npos : d > thr[i]}
   uint64_t thr[kMaxBounds];
   uint32_t npos, nneg, nbk;
@@ -217,21 +219,20 @@ __host__ __device__ inline uint32_t bt_probe_max(uint32_t log2sb) { return (1u <
 __host__ __device__ inline uint32_t bt_slot(uint64_t m, uint32_t log2sb, uint32_t i) {
   return ((uint32_t)(m >> kBinShift) << log2sb) | bt_pos(bt_seq(m, log2sb), i);
 }
-// u32 counter rows of the binned path: words [0, 2) = the u64 ns sum, words
-// [2, 2 + nbk) = bucket counts, padded to whole 16-B quads (80 B at 17 buckets)
-__host__ __device__ inline uint32_t row32_stride(uint32_t nbk) { return (nbk + 2 + 3) & ~3u; }
+// Counter rows of the binned path: 32 B per key slot, the u64 ns sum then one
+// u8 count per bucket (bytes 8 .. 8 + nbk), so two rows share a 64-B half
+// line and the aggregate's row read-modify-write moves 32 B per touched key.
+// A count that would pass 255 leaves the row: the aggregate adds the row's
+// counts to the u64 spill array base64 [cap][nbk + 1] (atomics) and zeroes
+// them; the scatter's direct path and overflow table add to base64 directly
+// (its last cell is their ns sum).  A key's totals are row + base64.
+constexpr uint32_t kRowBytes = 32;
+constexpr uint32_t kRowMaxBk = kRowBytes - 8;
+static_assert(kPartMaxBk <= kRowMaxBk, "binned rows hold every bucket count");
 constexpr uint32_t kBtStage = 4;     // records per bin stage: one 64-B chunk per flush
-constexpr uint32_t kBtHot = 224;     // scatter overflow table entries
 constexpr uint32_t kBtHq = 256;      // scatter deferred HLL raises
 constexpr uint32_t kBtBlock = 1024;  // scatter workgroup
-#ifndef SA_BT_AGG_BLOCK
-#define SA_BT_AGG_BLOCK 512
-#endif
-constexpr uint32_t kBtAggBlock = SA_BT_AGG_BLOCK;
 constexpr uint32_t kBtMaxWgSpans = 65520;  // u16 claim / overflow counters per scatter workgroup
-constexpr size_t kBtScatterLds = (size_t)kPartBins * (8 + kBtStage * 16) + (size_t)kBtHot * (16 + 4 * kPartWords) +
-                                 (size_t)kBtHq * 8 + 16 + (size_t)kBins * sizeof(BinEntry);
-static_assert(kBtScatterLds <= 163840, "binned scatter LDS");
 // round-synchronous scatter (bt_scatter2_kernel): per bin a 4-record stage,
 // a u16 claim count (pairs) and a u16 region fill; per wave a flush list of
 // 128 bins; the overflow table; HLL queue; bin table; HLL bounds
@@ -246,11 +247,11 @@ static_assert(kBt2ScatterLds <= 163840, "binned scatter2 LDS");
 // (compact, gather, count-min fold): both table layouts, both row layouts.
 struct RowGeom {
   uint32_t nbk;
-  uint32_t row32;   // 1: u32 count rows (binned path), 0: u64 segment rows
+  uint32_t row8;    // 1: 32-B u8-count rows + base64 (binned path), 0: u64 segment rows
   uint32_t binned;  // 1: binned key table
   uint32_t log2cap, log2sb, max_probe;
   uint64_t kmul, kinv;            // key <-> stored id (1, 1 unless binned)
-  unsigned long long *base64;     // row32: u64 [cap][nbk + 1] folded counts, or nullptr
+  unsigned long long *base64;     // row8: u64 [cap][nbk + 1] spilled counts and sums
 };
 
 // Key-table layout: cap = 2^log2cap slots in buckets of 4 (log2cap in 4..31).
@@ -328,11 +329,8 @@ hipError_t launch_fold_errcnt(const unsigned long long *gkeys, unsigned long lon
                               uint32_t shift, const uint64_t *seeds, uint64_t kinv, hipStream_t s);
 // binned-table path (spanagg_binned.hip)
 hipError_t prepare_ingest_bt(size_t agg_lds);
-size_t bt_agg_lds_bytes(uint32_t log2sb, uint32_t grid);
-size_t bt_agg2_lds_bytes(uint32_t log2sb, uint32_t grid);  // (the larger of the two is agg_lds)
-hipError_t launch_ingest_bt(const IngestParams &P, size_t agg_lds, hipStream_t s);
-hipError_t launch_fold_rows32(unsigned long long *gcounts, unsigned long long *base64, uint64_t cap,
-                              uint32_t nbk, hipStream_t s);
+size_t bt_agg2_lds_bytes(uint32_t log2sb, uint32_t grid);
+hipError_t launch_ingest_bt(const IngestParams &P, hipStream_t s);
 hipError_t launch_reduce_errslab(uint32_t *errslab, uint32_t G, uint64_t per_wg, uint64_t ws,
                                  uint32_t log2cap, unsigned long long *errcnt_ws, hipStream_t s);
 hipError_t launch_count_keys(const unsigned long long *gkeys, uint64_t cap,

@@ -8,24 +8,22 @@
 // and adds the sketch updates.
 //
 // Two kernels per launch:
-//   bt_scatter_kernel  (one 1,024-thread workgroup per CU, ~160 KiB LDS)
-//     streams the SoA batch once (register tile ring, 16-B nt buffer loads,
-//     dynamic wave chunks: the C2 kernel's skeleton), does the per-span stats
-//     and HLL work, and writes one 16-B record {m's low 53 bits | ERROR flag |
-//     window slot, duration} per span into the region of (its bin, this
-//     workgroup).  Records go through a 4-record LDS stage per bin and leave
-//     as aligned 64-B chunks, written by whichever lane stores a stage's last
-//     record (no workgroup barrier in the loop).  A span whose stage or
-//     region is full is pre-aggregated in a small LDS overflow table; past
-//     that, the direct path (key-table CAS + row atomics).
-//   bt_aggregate_kernel (one 512-thread workgroup per bin)
+//   bt_scatter2_kernel (one 1,024-thread workgroup per CU, ~160 KiB LDS)
+//     streams the SoA batch once (register tile ring, 16-B nt buffer loads:
+//     the C2 kernel's skeleton), does the per-span stats and HLL work, and
+//     writes one 16-B record {m's low 53 bits | ERROR flag | window slot,
+//     duration} per span into the region of (its bin, this workgroup),
+//     through 4-record LDS stages that leave as aligned 64-B chunks.  Hot keys
+//     are pre-aggregated in an LDS overflow table; past that, the direct path
+//     (key-table CAS + atomics into the spill array).
+//   bt_aggregate2_kernel (one 512-thread workgroup per bin)
 //     loads the bin's 2^log2sb key slots into LDS at the same positions,
 //     aggregates the bin's records there (u16 bucket-count pairs, u64 ns
 //     sums, an ERROR table keyed by (window slot, key slot)), then writes the
-//     new keys and read-modify-writes each touched u32 counter row of the bin:
-//     one contiguous block per bin, no atomics, since one workgroup owns it.
-// Bucket counts are u32 in HBM (80-B rows at 17 buckets); the engine folds
-// them into a u64 array before 2^32 spans can accumulate (fold_rows32_kernel).
+//     new keys and read-modify-writes each touched 32-B row of the bin (one
+//     owner, no atomics).
+// Rows hold u8 bucket counts (sa_internal.h kRowBytes); a count that would
+// pass 255 moves the row's counts into the u64 spill array base64.
 #include <algorithm>
 
 #include "sa_device.h"
@@ -53,12 +51,13 @@ __device__ __forceinline__ uint32_t bt_find_insert(unsigned long long *keys, uin
   return kNotFound;
 }
 
-// Adds one span to its u32 counter row with atomics (the direct path).
-__device__ __forceinline__ void row32_add(unsigned long long *gcounts, uint32_t stride32, uint32_t s,
-                                          uint32_t bk, uint32_t cnt, unsigned long long dsum) {
-  uint32_t *row = reinterpret_cast<uint32_t *>(gcounts) + (uint64_t)s * stride32;
-  if (cnt) atomicAdd(row + 2 + bk, cnt);
-  if (dsum) atomicAdd(reinterpret_cast<unsigned long long *>(row), dsum);
+// Adds cnt spans of bucket bk and an ns sum to key slot s in the u64 spill
+// array with atomics (the direct path and the overflow table's rows).
+__device__ __forceinline__ void spill_add(unsigned long long *base64, uint32_t nbk, uint32_t s, uint32_t bk,
+                                          uint32_t cnt, unsigned long long dsum) {
+  unsigned long long *row = base64 + (uint64_t)s * (nbk + 1);
+  if (cnt) atomicAdd(row + bk, (unsigned long long)cnt);
+  if (dsum) atomicAdd(row + nbk, dsum);
 }
 
 // The kernel's parameters in the kernarg segment.  Taken in the kernel body
@@ -94,251 +93,9 @@ __device__ __noinline__ uint32_t bt_cold_direct(KParams Q, uint64_t m, uint64_t 
     if (err) bt_cms_add(Q, ws, m * Q->kinv);
     return 1u;
   }
-  row32_add(Q->gcounts, row32_stride(Q->nbk), s, bk, 1u, d);
+  spill_add(Q->base64, Q->nbk, s, bk, 1u, d);
   if (err) atomicAdd(Q->errcnt + ((uint64_t)ws << Q->log2cap) + s, 1ULL);
   return 0u;
-}
-
-// Ablation modes (diagnostic builds only, selected by SA_DIAG bits: results
-// are wrong by design): MODE 1 = no records (placement skipped), 2 = no HLL,
-// 4 = each record stored on its own (no LDS stage).
-template <int S, int NBUF, int MODE = 0>
-__global__ __launch_bounds__(kBtBlock) void bt_scatter_kernel(IngestParams P) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // LDS: per bin a stage word (claims | done << 16) and the region fill,
-  // the 4-record stages, the overflow table, the HLL queue and the bin table
-  uint32_t *wcl = reinterpret_cast<uint32_t *>(smem);
-  uint32_t *rcn = wcl + kPartBins;
-  ulonglong2 *stage = reinterpret_cast<ulonglong2 *>(rcn + kPartBins);
-  unsigned long long *hkey = reinterpret_cast<unsigned long long *>(stage + kPartBins * kBtStage);
-  unsigned long long *hsum = hkey + kBtHot;
-  uint32_t *hcnt = reinterpret_cast<uint32_t *>(hsum + kBtHot);  // [kBtHot][kPartWords] u16 pairs
-  uint2 *hq = reinterpret_cast<uint2 *>(hcnt + kBtHot * kPartWords);
-  uint32_t *hq_n = reinterpret_cast<uint32_t *>(hq + kBtHq);  // [0] HLL queue fill, [1] next chunk
-  BinEntry *lbins = reinterpret_cast<BinEntry *>(hq_n + 4);
-  const KParams kp = kernel_params();
-
-  uint64_t lo, hi;
-  wg_range_p(P, lo, hi);
-  const uint32_t len = (uint32_t)(hi - lo);
-  constexpr uint32_t tile = 64 * S, chunk = NBUF * tile;
-  constexpr uint32_t kWaves = kBtBlock / 64;
-  const uint32_t lane_off = (threadIdx.x & 63u) * S;
-  const uint32_t n_chunks = (len + chunk - 1) / chunk;
-  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  uint32_t c0 = wave, c1 = wave + kWaves;
-  auto tstart = [&](uint32_t c, int b) -> uint32_t { return c * chunk + (uint32_t)b * tile; };
-  auto tremain = [&](uint32_t t) -> uint32_t { return len > t ? len - t : 0u; };
-
-  // prologue: bin table, then the first tiles, then the LDS setup
-  uint4 bv = make_uint4(0, 0, 0, 0);
-  if (threadIdx.x < kBins * 2) bv = reinterpret_cast<const uint4 *>(P.bintab)[threadIdx.x];
-  SpanTile<S> buf[NBUF];
-  Pending<S> pend;
-#pragma unroll
-  for (int b = 0; b < NBUF; ++b) {
-    const uint32_t t = tstart(c0, b);
-    load_tile_at<S, 2>(P, lo + t, tremain(t), lane_off, buf[b]);
-    if (b == NBUF - 1) {
-      uint32_t z;  // a VGPR zero keeps these vector loads
-      asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-#pragma unroll
-      for (int j = 0; j < S; ++j) pend.hv[j] = *reinterpret_cast<const uint32_t *>(P.hll + z);
-    }
-  }
-  for (uint32_t b = threadIdx.x; b < kPartBins; b += kBtBlock) wcl[b] = rcn[b] = 0;
-  for (uint32_t h = threadIdx.x; h < kBtHot; h += kBtBlock) hkey[h] = hsum[h] = 0;
-  for (uint32_t h = threadIdx.x; h < kBtHot * kPartWords; h += kBtBlock) hcnt[h] = 0;
-  if (threadIdx.x < kBins * 2) reinterpret_cast<uint4 *>(lbins)[threadIdx.x] = bv;
-  if (threadIdx.x == 0) {
-    hq_n[0] = 0;
-    hq_n[1] = 2 * kWaves;
-  }
-  __syncthreads();
-
-  uint32_t n_zero = 0, n_badsvc = 0, n_oor = 0;  // wave-uniform (SGPR)
-  uint32_t n_drop = 0;                           // per lane
-#pragma unroll
-  for (int j = 0; j < S; ++j) pend.hoff[j] = pend.rho[j] = 0;
-  const uint32_t region = P.bt_region;
-  ulonglong2 *my_rec = P.bt_rec + (uint64_t)blockIdx.x * region;  // + bin * grid * region
-  const uint64_t bin_stride = (uint64_t)P.bt_grid * region;
-
-  // a span the stages cannot take: the overflow table, else the direct path
-  auto hot_add = [&](uint64_t m, uint64_t d, bool err, uint32_t ws) {
-    const uint32_t bk = bucket_lds<1>(d, lbins, P);
-    uint32_t h = (uint32_t)(((uint64_t)(uint32_t)(m >> 21) * kBtHot) >> 32);
-    for (int pr = 0; pr < 8; ++pr) {
-      unsigned long long k = hkey[h];
-      if (k == 0) k = atomicCAS(&hkey[h], 0ULL, (unsigned long long)m);
-      if (k == 0 || k == m) {
-        atomicAdd(&hcnt[h * kPartWords + (bk >> 1)], 1u << ((bk & 1u) * 16));
-        atomicAdd(&hsum[h], (unsigned long long)d);
-        if (err) bt_cold_err(kp, m, ws);
-        return;
-      }
-      h = h + 1 == kBtHot ? 0u : h + 1;
-    }
-    n_drop += bt_cold_direct(kp, m, d, bk, err, ws);
-  };
-  auto hot_rec = [&](uint32_t b, const ulonglong2 &r) {
-    const uint64_t m = ((uint64_t)b << kBinShift) | (r.x & kBinRest);
-    hot_add(m, r.y, (r.x >> 63) != 0, (uint32_t)(r.x >> kBinShift) & 1023u);
-  };
-  // the lane that completes a stage writes it out as one 64-B chunk
-  auto flush_stage = [&](uint32_t b) {
-    ulonglong2 r[kBtStage];
-#pragma unroll
-    for (int q = 0; q < (int)kBtStage; ++q) r[q] = stage[b * kBtStage + q];
-    // LDS executes one wave's operations in order: the reads above are
-    // performed before the reset lets new claims overwrite the stage
-    compiler_fence();
-    atomicExch(&wcl[b], 0u);
-    const uint32_t at = atomicAdd(&rcn[b], kBtStage);
-    if (at + kBtStage <= region) {
-      ulonglong2 *dst = my_rec + b * bin_stride + at;
-#pragma unroll
-      for (int q = 0; q < (int)kBtStage; ++q) dst[q] = r[q];
-    } else {
-#pragma unroll
-      for (int q = 0; q < (int)kBtStage; ++q) hot_rec(b, r[q]);
-    }
-  };
-  auto place = [&](uint64_t m, uint64_t d, bool err, uint32_t ws) {
-    const uint32_t b = (uint32_t)(m >> kBinShift);
-    const uint64_t x = (m & kBinRest) | (err ? (1ULL << 63) | ((uint64_t)ws << kBinShift) : 0ULL);
-    const uint32_t c = atomicAdd(&wcl[b], 1u) & 0xFFFFu;
-    if (c < kBtStage) {
-      stage[b * kBtStage + c] = make_ulonglong2(x, d);
-      compiler_fence();  // the record store before the completion count
-      const uint32_t done = atomicAdd(&wcl[b], 1u << 16) >> 16;
-      if (done == kBtStage - 1) flush_stage(b);
-    } else {
-      hot_add(m, d, err, ws);
-    }
-  };
-
-  auto hll_settle = [&](const Pending<S> &q) {
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-      if (((q.hv[j] >> ((q.hoff[j] & 3u) * 8)) & 0xFFu) < q.rho[j]) {
-        const uint32_t slot = atomicAdd(&hq_n[0], 1u);
-        if (slot < kBtHq) hq[slot] = make_uint2(q.hoff[j], q.rho[j]);
-        else hll_raise(kp->hll + q.hoff[j], q.rho[j]);
-      }
-    }
-  };
-
-  const uint32_t hp = P.p;
-  auto step = [&](SpanTile<S> &T, uint32_t toff, uint32_t pf) {
-    uint64_t m[S], d[S];
-    uint32_t ws[S], hoff[S], rho[S];
-    bool err[S];
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-      const bool valid = lane_off + toff + (uint32_t)j < len;
-      const uint64_t key = copy_u64(T.key[j]);  // 0 past the range
-      n_zero += wave_count(valid && key == 0);
-      d[j] = T.e[j] > T.s[j] ? T.e[j] - T.s[j] : 0;
-      const uint32_t meta = copy_u32(T.meta[j]);
-      const uint32_t svc = meta & 0xFFFFu;
-      const bool svc_ok = svc < P.n_services;
-      ws[j] = window_slot(P, T.e[j]);
-      const bool win_ok = ws[j] != 0xFFFFFFFFu;
-      n_badsvc += wave_count(valid && !svc_ok);
-      n_oor += wave_count(valid && svc_ok && !win_ok);
-      const bool sk = valid && svc_ok && win_ok;
-      err[j] = sk && ((meta >> 19) & 3u) == 2u;
-      const uint64_t x = xxh64_16(T.a[j], T.b[j]);
-      const uint32_t r = (uint32_t)__clzll((long long)((x << hp) | (1ULL << (hp - 1)))) + 1;
-      rho[j] = sk && !(MODE & 2) ? r : 0u;
-      hoff[j] = sk && !(MODE & 2) ? ((ws[j] * P.n_services + svc) << hp) + (uint32_t)(x >> (64 - hp)) : 0u;
-      m[j] = key * P.kmul;
-    }
-    uint32_t hv[S];
-#pragma unroll
-    for (int j = 0; j < S; ++j)
-      hv[j] = (MODE & 2) ? 0xFFFFFFFFu : *reinterpret_cast<const uint32_t *>(P.hll + (hoff[j] & ~3u));
-    __builtin_amdgcn_sched_barrier(0);
-    load_tile_at<S, 2>(P, lo + pf, tremain(pf), lane_off, T);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-      if (MODE & 1) {
-        n_drop += (uint32_t)((m[j] ^ d[j]) == 0x123456789ABCULL);  // keep the values live
-      } else if (m[j] != 0) {
-        if (MODE & 4) {
-          const uint32_t b = (uint32_t)(m[j] >> kBinShift);
-          const uint32_t at = atomicAdd(&rcn[b], 1u);
-          if (at < region) my_rec[b * bin_stride + at] = make_ulonglong2(m[j] & kBinRest, d[j]);
-          else hot_add(m[j], d[j], err[j], ws[j]);
-        } else {
-          place(m[j], d[j], err[j], ws[j]);
-        }
-      }
-    }
-    hll_settle(pend);
-#pragma unroll
-    for (int j = 0; j < S; ++j) {
-      pend.hoff[j] = hoff[j];
-      pend.rho[j] = rho[j];
-      pend.hv[j] = hv[j];
-    }
-  };
-
-  while (c0 < n_chunks) {
-    const uint32_t c2 = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)atomicAdd(&hq_n[1], (threadIdx.x & 63u) == 0 ? 1u : 0u));
-#pragma unroll
-    for (int b = 0; b < NBUF; ++b) step(buf[b], tstart(c0, b), tstart(c1, b));
-    c0 = c1;
-    c1 = c2;
-  }
-  hll_settle(pend);
-  __syncthreads();
-  // partial stages, then this workgroup's region fills
-  for (uint32_t b = threadIdx.x; b < kPartBins; b += kBtBlock) {
-    const uint32_t c = min(wcl[b] >> 16, kBtStage - 1);  // written records of the open stage
-    const uint32_t at = rcn[b];
-    uint32_t fill = min(at, region);
-    if (c) {
-      if (at + c <= region) {
-        ulonglong2 *dst = my_rec + b * bin_stride + at;
-        for (uint32_t q = 0; q < c; ++q) dst[q] = stage[b * kBtStage + q];
-        fill = at + c;
-      } else {
-        for (uint32_t q = 0; q < c; ++q) hot_rec(b, stage[b * kBtStage + q]);
-      }
-    }
-    P.bt_cnt[(uint64_t)b * P.bt_grid + blockIdx.x] = fill;
-  }
-  __syncthreads();
-  // the overflow table: one row update per entry (atomics: entries of one
-  // key may come from several workgroups)
-  const uint32_t stride32 = row32_stride(P.nbk);
-  for (uint32_t h = threadIdx.x; h < kBtHot; h += kBtBlock) {
-    const unsigned long long m = hkey[h];
-    if (m == 0) continue;
-    const uint32_t s = bt_find_insert(P.gkeys, m, P.log2sb);
-    if (s == kNotFound) {
-      for (uint32_t b = 0; b < P.nbk; ++b) n_drop += (hcnt[h * kPartWords + (b >> 1)] >> ((b & 1u) * 16)) & 0xFFFFu;
-      continue;
-    }
-    for (uint32_t b = 0; b < P.nbk; ++b) {
-      const uint32_t c = (hcnt[h * kPartWords + (b >> 1)] >> ((b & 1u) * 16)) & 0xFFFFu;
-      if (c) row32_add(P.gcounts, stride32, s, b, c, 0);
-    }
-    row32_add(P.gcounts, stride32, s, 0, 0, hsum[h]);
-  }
-  const uint32_t nq = min(hq_n[0], kBtHq);
-  for (uint32_t i = threadIdx.x; i < nq; i += kBtBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
-  n_drop = wave_sum(n_drop);
-  if ((threadIdx.x & 63) == 0) {
-    if (n_zero) atomicAdd(&P.stats[kStatZeroKey], (unsigned long long)n_zero);
-    if (n_badsvc) atomicAdd(&P.stats[kStatInvalidService], (unsigned long long)n_badsvc);
-    if (n_oor) atomicAdd(&P.stats[kStatWindowOOR], (unsigned long long)n_oor);
-    if (n_drop) atomicAdd(&P.stats[kStatDropped], (unsigned long long)n_drop);
-  }
 }
 
 // Diagnostic per-workgroup timestamps (SPANAGG_STAMPS builds of the engine):
@@ -362,7 +119,7 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
 // a span whose stage is full in its round, or whose region is used up, goes
 // to the overflow table, past that the direct path.  The record layout
 // ({m's low 53 bits | ERROR flag | window slot, duration} per (bin,
-// workgroup) region) is the one bt_aggregate_kernel reads.
+// workgroup) region) is the one bt_aggregate2_kernel reads.
 // MODE (ablation): 1 = no records, 2 = no HLL, 4 = overflow-table adds
 // skipped, 8 = overflow-table ERROR counts skipped.
 template <int MODE = 0>
@@ -633,7 +390,6 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
   __syncthreads();
   // the overflow table: one row update per entry (atomics: entries of one
   // key may come from several workgroups)
-  const uint32_t stride32 = row32_stride(P.nbk);
   for (uint32_t h = threadIdx.x; h < kBt2Hot; h += kBtBlock) {
     const unsigned long long m = hkey[h];
     if (m == 0) continue;
@@ -644,9 +400,9 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
     }
     for (uint32_t b = 0; b < P.nbk; ++b) {
       const uint32_t c = (hcnt[h * kPartWords + (b >> 1)] >> ((b & 1u) * 16)) & 0xFFFFu;
-      if (c) row32_add(P.gcounts, stride32, s, b, c, 0);
+      if (c) spill_add(P.base64, P.nbk, s, b, c, 0);
     }
-    row32_add(P.gcounts, stride32, s, 0, 0, hsum[h]);
+    spill_add(P.base64, P.nbk, s, 0, 0, hsum[h]);
   }
   if (threadIdx.x < kBt2HotErr) {
     const uint2 e = herr[threadIdx.x];
@@ -671,201 +427,6 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
   hll_lb_refresh(P, wave, kWaves);
   bt_stamp(P, sbase, 3);
 }
-
-// LDS layout of bt_aggregate_kernel (bytes): keys [sb] u64 | sums [sb] u64 |
-// counts [sb][kPartWords] u32 | region prefix [grid + 1] u32 (16-B padded) |
-// ERROR table [kBtErr] uint2 | bin table [kBins] | misc [4] u32
-constexpr uint32_t kBtErr = 256;
-__host__ __device__ inline uint32_t bt_agg_off_pre(uint32_t sb) { return sb * (16 + 4 * kPartWords); }
-__host__ __device__ inline uint32_t bt_agg_off_err(uint32_t sb, uint32_t grid) {
-  return (bt_agg_off_pre(sb) + (grid + 1) * 4 + 15) & ~15u;
-}
-
-// MODE (ablation): 1 = no records aggregated, 2 = no key / row write-back
-template <int MODE = 0>
-__global__ __launch_bounds__(kBtAggBlock) void bt_aggregate_kernel(IngestParams P) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t log2sb = P.log2sb, sb = 1u << log2sb, smask = sb - 1;
-  const uint32_t G = P.bt_grid, bin = blockIdx.x, region = P.bt_region;
-  unsigned long long *lkeys = reinterpret_cast<unsigned long long *>(smem);
-  unsigned long long *lsum = lkeys + sb;
-  uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + sb);
-  uint32_t *pre = reinterpret_cast<uint32_t *>(smem + bt_agg_off_pre(sb));
-  uint2 *etab = reinterpret_cast<uint2 *>(smem + bt_agg_off_err(sb, G));
-  BinEntry *lbins = reinterpret_cast<BinEntry *>(etab + kBtErr);
-  uint32_t *misc = reinterpret_cast<uint32_t *>(lbins + kBins);  // [0] dropped
-  const uint32_t tid = threadIdx.x;
-  unsigned long long *gk = P.gkeys + ((uint64_t)bin << log2sb);
-
-  // 1. the bin's key slots (kept in registers to find the new ones later),
-  //    region fills, zeroed counters
-  constexpr int kMaxPer = 2048 / kBtAggBlock;  // sb <= 2048 slots
-  unsigned long long orig[kMaxPer];
-#pragma unroll
-  for (int u = 0; u < kMaxPer; ++u) {
-    const uint32_t s = tid + u * kBtAggBlock;
-    orig[u] = s < sb ? gk[s] : 0ULL;
-  }
-  for (uint32_t g = tid; g < G; g += kBtAggBlock) pre[g] = P.bt_cnt[(uint64_t)bin * G + g];
-  if (tid < kBins * 2) reinterpret_cast<uint4 *>(lbins)[tid] = reinterpret_cast<const uint4 *>(P.bintab)[tid];
-#pragma unroll
-  for (int u = 0; u < kMaxPer; ++u) {
-    const uint32_t s = tid + u * kBtAggBlock;
-    if (s < sb) {
-      lkeys[s] = orig[u];
-      lsum[s] = 0;
-    }
-  }
-  for (uint32_t i = tid; i < sb * kPartWords; i += kBtAggBlock) lcnt[i] = 0;
-  for (uint32_t i = tid; i < kBtErr; i += kBtAggBlock) etab[i] = make_uint2(0, 0);
-  if (tid == 0) misc[0] = 0;
-  __syncthreads();
-  // exclusive prefix of the region fills (wave 0)
-  if (tid < 64) {
-    uint32_t carry = 0;
-    for (uint32_t g0 = 0; g0 < G; g0 += 64) {
-      const uint32_t g = g0 + tid;
-      const uint32_t v = g < G ? pre[g] : 0u;
-      uint32_t incl = v;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
-        if ((int)tid >= o) incl += t;
-      }
-      if (g < G) pre[g] = carry + incl - v;
-      carry += (uint32_t)__shfl((int)incl, 63, 64);
-    }
-    if (tid == 0) pre[G] = carry;
-  }
-  __syncthreads();
-
-  // 2. the records: wave w takes 64-record chunks w, w + 8, ...; a chunk's
-  //    first segment by binary search (uniform), each lane's by walking the
-  //    chunk's segment boundaries (uniform broadcast reads)
-  const uint32_t total = (MODE & 1) ? 0u : pre[G];
-  const uint32_t lane = tid & 63u, wave = tid >> 6;
-  constexpr uint32_t kAggWaves = kBtAggBlock / 64;
-  const ulonglong2 *bin_rec = P.bt_rec + (uint64_t)bin * G * region;
-  uint32_t n_drop = 0;
-  constexpr int U = 4;
-  for (uint32_t k0 = wave; k0 * 64 < total; k0 += U * kAggWaves) {
-    ulonglong2 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t r0 = (k0 + u * kAggWaves) * 64, r = r0 + lane;
-      v[u] = make_ulonglong2(0, 0);
-      if (r0 < total) {
-        uint32_t a = 0, b = G;  // largest s with pre[s] <= r0
-        while (b - a > 1) {
-          const uint32_t mid = (a + b) >> 1;
-          if (pre[mid] <= r0) a = mid;
-          else b = mid;
-        }
-        uint32_t seg = a, sbase = pre[a];
-        for (uint32_t j = a + 1; j < G; ++j) {
-          const uint32_t pj = pre[j];
-          if (pj > r0 + 63) break;
-          if (pj <= r) {
-            seg = j;
-            sbase = pj;
-          }
-        }
-        if (r < total) v[u] = bin_rec[(uint64_t)seg * region + (r - sbase)];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t r = (k0 + u * kAggWaves) * 64 + lane;
-      if (r >= total) continue;
-      const uint64_t m = ((uint64_t)bin << kBinShift) | (v[u].x & kBinRest);
-      const uint64_t d = v[u].y;
-      const uint32_t bk = bucket_lds<1>(d, lbins, P);
-      const BtSeq bq = bt_seq(m, log2sb);
-      const uint32_t pmax = bt_probe_max(log2sb);
-      uint32_t s = 0, i = 0;
-      for (; i < pmax; ++i) {
-        s = bt_pos(bq, i);
-        unsigned long long k = lkeys[s];
-        if (k == 0) k = atomicCAS(&lkeys[s], 0ULL, (unsigned long long)m);
-        if (k == 0 || k == m) break;
-      }
-      if (i == pmax) {  // the bin's sub-table is full: the span is dropped
-        ++n_drop;
-        if (v[u].x >> 63) bt_cms_add(kernel_params(), (uint32_t)(v[u].x >> kBinShift) & 1023u, m * P.kinv);
-        continue;
-      }
-      atomicAdd(&lcnt[s * kPartWords + (bk >> 1)], 1u << ((bk & 1u) * 16));
-      atomicAdd(&lsum[s], (unsigned long long)d);
-      if (v[u].x >> 63) {  // ERROR span: (window slot, key slot) -> count
-        const uint32_t ws = (uint32_t)(v[u].x >> kBinShift) & 1023u;
-        const uint32_t ek = ((ws << log2sb) | s) + 1;
-        uint32_t h = (ek * 0x9E3779B1u) >> 24;  // kBtErr = 256
-        bool done = false;
-        for (int pr = 0; pr < 8 && !done; ++pr, h = (h + 1) & (kBtErr - 1)) {
-          uint32_t kk = etab[h].x;
-          if (kk == 0) kk = atomicCAS(&etab[h].x, 0u, ek);
-          if (kk == 0 || kk == ek) {
-            atomicAdd(&etab[h].y, 1u);
-            done = true;
-          }
-        }
-        if (!done)
-          atomicAdd(P.errcnt + ((uint64_t)ws << P.log2cap) + ((uint64_t)bin << log2sb) + s, 1ULL);
-      }
-    }
-  }
-  n_drop = wave_sum(n_drop);
-  if (lane == 0 && n_drop) atomicAdd(&misc[0], n_drop);
-  __syncthreads();
-
-  // 3. new keys and touched rows of the bin (one owner: plain stores)
-  if (MODE & 2) return;
-  const uint32_t nbk = P.nbk, stride32 = row32_stride(nbk), nq = stride32 / 4;
-  uint32_t *rows = reinterpret_cast<uint32_t *>(P.gcounts) + ((uint64_t)bin << log2sb) * stride32;
-#pragma unroll
-  for (int u = 0; u < kMaxPer; ++u) {
-    const uint32_t s = tid + u * kBtAggBlock;
-    if (s >= sb) continue;
-    const unsigned long long k = lkeys[s];
-    if (k != orig[u]) gk[s] = k;
-    uint32_t w[kPartWords];
-    uint32_t any = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < kPartWords; ++q) {
-      w[q] = lcnt[s * kPartWords + q];
-      any |= w[q];
-    }
-    if (!any) continue;
-    uint4 *row = reinterpret_cast<uint4 *>(rows + (uint64_t)s * stride32);
-    uint32_t c[20];
-#pragma unroll
-    for (uint32_t q = 0; q < 5; ++q) {
-      const uint4 x = q < nq ? row[q] : make_uint4(0, 0, 0, 0);
-      c[4 * q] = x.x;
-      c[4 * q + 1] = x.y;
-      c[4 * q + 2] = x.z;
-      c[4 * q + 3] = x.w;
-    }
-    const unsigned long long sum = ((unsigned long long)c[1] << 32 | c[0]) + lsum[s];
-    c[0] = (uint32_t)sum;
-    c[1] = (uint32_t)(sum >> 32);
-#pragma unroll
-    for (uint32_t b = 0; b < kPartMaxBk; ++b)
-      if (b < nbk) c[2 + b] += (w[b >> 1] >> ((b & 1u) * 16)) & 0xFFFFu;
-#pragma unroll
-    for (uint32_t q = 0; q < 5; ++q)
-      if (q < nq) row[q] = make_uint4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
-  }
-  for (uint32_t i = tid; i < kBtErr; i += kBtAggBlock) {
-    const uint2 e = etab[i];
-    if (e.x == 0) continue;
-    const uint32_t ek = e.x - 1, ws = ek >> log2sb, s = ek & smask;
-    unsigned long long *cell = P.errcnt + ((uint64_t)ws << P.log2cap) + ((uint64_t)bin << log2sb) + s;
-    *cell += e.y;
-  }
-  if (tid == 0 && misc[0]) atomicAdd(&P.stats[kStatDropped], (unsigned long long)misc[0]);
-}
-
 
 // Aggregate, second form (the default).  One 512-thread workgroup per bin;
 // its LDS holds the bin's key slots (mirror), u64 ns sums and u16 bucket
@@ -1046,9 +607,9 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
   // 3. new keys and touched rows of the bin (one owner: plain stores; every
   //    row read is issued before the first row is written)
   if (MODE & 2) return;
-  const uint32_t nbk = P.nbk, stride32 = row32_stride(nbk), nq = stride32 / 4;
-  uint32_t *rows = reinterpret_cast<uint32_t *>(P.gcounts) + ((uint64_t)bin << log2sb) * stride32;
-  uint4 rv[kMaxPer][5];
+  const uint32_t nbk = P.nbk;
+  uint4 *rows = reinterpret_cast<uint4 *>(P.gcounts) + ((uint64_t)bin << log2sb) * (kRowBytes / 16);
+  uint4 rv[kMaxPer][2];
   bool touched[kMaxPer];
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
@@ -1062,9 +623,8 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
       }
       touched[u] = any != 0;
     }
-    const uint4 *row = reinterpret_cast<const uint4 *>(rows + (uint64_t)s * stride32);
 #pragma unroll
-    for (uint32_t q = 0; q < 5; ++q) rv[u][q] = touched[u] && q < nq ? row[q] : make_uint4(0, 0, 0, 0);
+    for (uint32_t q = 0; q < 2; ++q) rv[u][q] = touched[u] ? rows[(uint64_t)s * 2 + q] : make_uint4(0, 0, 0, 0);
   }
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
@@ -1073,26 +633,31 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
     const unsigned long long k = lkeys[s];
     if (k != orig[u]) gk[s] = k;
     if (!touched[u]) continue;
-    uint32_t c[20];
-#pragma unroll
-    for (uint32_t q = 0; q < 5; ++q) {
-      c[4 * q] = rv[u][q].x;
-      c[4 * q + 1] = rv[u][q].y;
-      c[4 * q + 2] = rv[u][q].z;
-      c[4 * q + 3] = rv[u][q].w;
-    }
-    const unsigned long long sum = ((unsigned long long)c[1] << 32 | c[0]) + lsum[s];
-    c[0] = (uint32_t)sum;
-    c[1] = (uint32_t)(sum >> 32);
+    // row: words 0-1 the ns sum, bytes 8 .. 8 + nbk the u8 counts
+    const uint32_t w[8] = {rv[u][0].x, rv[u][0].y, rv[u][0].z, rv[u][0].w,
+                           rv[u][1].x, rv[u][1].y, rv[u][1].z, rv[u][1].w};
+    const unsigned long long sum = ((unsigned long long)w[1] << 32 | w[0]) + lsum[s];
+    uint32_t c[kPartMaxBk];
+    bool spill = false;
 #pragma unroll
     for (uint32_t b = 0; b < kPartMaxBk; ++b) {
       const uint32_t h = s * kPartMaxBk + b;
-      if (b < nbk) c[2 + b] += (lcnt[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu;
+      c[b] = b < nbk ? ((w[2 + b / 4] >> ((b & 3u) * 8)) & 0xFFu) + ((lcnt[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu)
+                     : 0u;
+      spill |= c[b] > 0xFFu;
     }
-    uint4 *row = reinterpret_cast<uint4 *>(rows + (uint64_t)s * stride32);
+    uint32_t o[6] = {0, 0, 0, 0, 0, 0};
+    if (spill) {  // the row's counts move to the spill array (atomics: the scatter adds there too)
+      unsigned long long *sp = P.base64 + ((uint64_t)bin << log2sb | s) * (nbk + 1);
 #pragma unroll
-    for (uint32_t q = 0; q < 5; ++q)
-      if (q < nq) row[q] = make_uint4(c[4 * q], c[4 * q + 1], c[4 * q + 2], c[4 * q + 3]);
+      for (uint32_t b = 0; b < kPartMaxBk; ++b)
+        if (c[b]) atomicAdd(sp + b, (unsigned long long)c[b]);
+    } else {
+#pragma unroll
+      for (uint32_t b = 0; b < kPartMaxBk; ++b) o[b / 4] |= c[b] << ((b & 3u) * 8);
+    }
+    rows[(uint64_t)s * 2] = make_uint4((uint32_t)sum, (uint32_t)(sum >> 32), o[0], o[1]);
+    rows[(uint64_t)s * 2 + 1] = make_uint4(o[2], o[3], o[4], o[5]);
   }
   for (uint32_t i = tid; i < kBtAgg2Err; i += BLOCK) {
     const uint2 e = etab[i];
@@ -1105,40 +670,10 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
   bt_stamp(P, (uint64_t)bin * 8, 3);
 }
 
-// u32 count rows -> the u64 fold array (before 2^32 spans can accumulate)
-__global__ void fold_rows32_kernel(uint32_t *rows, unsigned long long *base64, uint64_t cap, uint32_t nbk) {
-  const uint32_t stride32 = row32_stride(nbk);
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap;
-       s += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t *row = rows + s * stride32;
-    unsigned long long *b64 = base64 + s * (nbk + 1);
-    const unsigned long long sum = (unsigned long long)row[1] << 32 | row[0];
-    if (sum) b64[nbk] += sum;
-    for (uint32_t b = 0; b < nbk; ++b)
-      if (row[2 + b]) b64[b] += row[2 + b];
-    for (uint32_t w = 0; w < stride32; ++w) row[w] = 0;
-  }
-}
-
 }  // namespace
 
 // SA_DIAG bits of the ablation builds (profiling only)
-constexpr uint32_t kDiagBtDirect = 1u << 20, kDiagBtAggNoRows = 1u << 21, kDiagBtNoAgg = 1u << 22,
-                   kDiagBtNoScatter = 1u << 23, kDiagBtScatter1 = 1u << 24;
-
-static const void *bt_scatter_fn(uint32_t diag) {
-  const int mode = ((diag & 1u) ? 1 : 0) | ((diag & 2u) ? 2 : 0) | ((diag & kDiagBtDirect) ? 4 : 0);
-  switch (mode) {
-    case 0: return (const void *)&bt_scatter_kernel<2, 2, 0>;
-    case 1: return (const void *)&bt_scatter_kernel<2, 2, 1>;
-    case 2: return (const void *)&bt_scatter_kernel<2, 2, 2>;
-    case 3: return (const void *)&bt_scatter_kernel<2, 2, 3>;
-    case 4: return (const void *)&bt_scatter_kernel<2, 2, 4>;
-    case 6: return (const void *)&bt_scatter_kernel<2, 2, 6>;
-    default: return (const void *)&bt_scatter_kernel<2, 2, 0>;
-  }
-}
-
+constexpr uint32_t kDiagBtAggNoRows = 1u << 21, kDiagBtNoAgg = 1u << 22, kDiagBtNoScatter = 1u << 23;
 constexpr uint32_t kDiagBtHotAcc = 1u << 25, kDiagBtHotErr = 1u << 26, kDiagBtSeqStore = 1u << 27,
                    kDiagBtNoStore = 1u << 28;
 static const void *bt_scatter2_fn(uint32_t diag) {
@@ -1154,46 +689,32 @@ static const void *bt_scatter2_fn(uint32_t diag) {
   }
 }
 
-constexpr uint32_t kDiagBtAgg1 = 1u << 29, kDiagBtAggWide = 1u << 30, kDiagBtAggLoadOnly = 1u << 31;
+constexpr uint32_t kDiagBtAggWide = 1u << 30, kDiagBtAggLoadOnly = 1u << 31;
 static const void *bt_agg_fn(uint32_t diag) {
   const int mode = ((diag & 1u) ? 1 : 0) | ((diag & kDiagBtAggNoRows) ? 2 : 0);
-  if (!(diag & kDiagBtAgg1)) {
-    if (diag & kDiagBtAggLoadOnly) return (const void *)&bt_aggregate2_kernel<4, 2>;
-    if (diag & kDiagBtAggWide) switch (mode) {  // bins of 2,048 slots
-        case 1: return (const void *)&bt_aggregate2_kernel<1, 4>;
-        case 2: return (const void *)&bt_aggregate2_kernel<2, 4>;
-        case 3: return (const void *)&bt_aggregate2_kernel<3, 4>;
-        default: return (const void *)&bt_aggregate2_kernel<0, 4>;
-      }
-    switch (mode) {
-      case 1: return (const void *)&bt_aggregate2_kernel<1, 2>;
-      case 2: return (const void *)&bt_aggregate2_kernel<2, 2>;
-      case 3: return (const void *)&bt_aggregate2_kernel<3, 2>;
-      default: return (const void *)&bt_aggregate2_kernel<0, 2>;
+  if (diag & kDiagBtAggLoadOnly) return (const void *)&bt_aggregate2_kernel<4, 2>;
+  if (diag & kDiagBtAggWide) switch (mode) {  // bins of 2,048 slots
+      case 1: return (const void *)&bt_aggregate2_kernel<1, 4>;
+      case 2: return (const void *)&bt_aggregate2_kernel<2, 4>;
+      case 3: return (const void *)&bt_aggregate2_kernel<3, 4>;
+      default: return (const void *)&bt_aggregate2_kernel<0, 4>;
     }
-  }
   switch (mode) {
-    case 1: return (const void *)&bt_aggregate_kernel<1>;
-    case 2: return (const void *)&bt_aggregate_kernel<2>;
-    case 3: return (const void *)&bt_aggregate_kernel<3>;
-    default: return (const void *)&bt_aggregate_kernel<0>;
+    case 1: return (const void *)&bt_aggregate2_kernel<1, 2>;
+    case 2: return (const void *)&bt_aggregate2_kernel<2, 2>;
+    case 3: return (const void *)&bt_aggregate2_kernel<3, 2>;
+    default: return (const void *)&bt_aggregate2_kernel<0, 2>;
   }
 }
 
 hipError_t prepare_ingest_bt(size_t agg_lds) {
-  for (uint32_t d : {0u, 1u, 2u, 3u, kDiagBtDirect, kDiagBtDirect | 2u}) {
-    if (hipError_t e = hipFuncSetAttribute(bt_scatter_fn(d), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)kBtScatterLds);
-        e != hipSuccess)
-      return e;
-  }
   for (uint32_t d : {0u, 1u, 2u, 3u, kDiagBtHotAcc, kDiagBtHotErr, kDiagBtSeqStore, kDiagBtNoStore})
     if (hipError_t e = hipFuncSetAttribute(bt_scatter2_fn(d), hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)kBt2ScatterLds);
         e != hipSuccess)
       return e;
   for (uint32_t d : {0u, 1u, kDiagBtAggNoRows, 1u | kDiagBtAggNoRows})
-    for (uint32_t v : {0u, kDiagBtAgg1, kDiagBtAggWide, kDiagBtAggLoadOnly})
+    for (uint32_t v : {0u, kDiagBtAggWide, kDiagBtAggLoadOnly})
       if (hipError_t e =
               hipFuncSetAttribute(bt_agg_fn(d | v), hipFuncAttributeMaxDynamicSharedMemorySize, (int)agg_lds);
           e != hipSuccess)
@@ -1201,36 +722,22 @@ hipError_t prepare_ingest_bt(size_t agg_lds) {
   return hipSuccess;
 }
 
-hipError_t launch_ingest_bt(const IngestParams &P, size_t agg_lds, hipStream_t s) {
+hipError_t launch_ingest_bt(const IngestParams &P, hipStream_t s) {
   void *args[] = {const_cast<IngestParams *>(&P)};
   if (!(P.diag & kDiagBtNoScatter)) {
-    const bool v1 = (P.diag & (kDiagBtScatter1 | kDiagBtDirect)) != 0;
-    if (hipError_t e = hipLaunchKernel(v1 ? bt_scatter_fn(P.diag) : bt_scatter2_fn(P.diag), dim3(P.bt_grid),
-                                       dim3(kBtBlock), args, v1 ? kBtScatterLds : kBt2ScatterLds, s);
+    if (hipError_t e = hipLaunchKernel(bt_scatter2_fn(P.diag), dim3(P.bt_grid), dim3(kBtBlock), args,
+                                       kBt2ScatterLds, s);
         e != hipSuccess)
       return e;
   }
   if (P.diag & kDiagBtNoAgg) return hipSuccess;
   const uint32_t diag = P.diag | (P.log2sb > 10 ? kDiagBtAggWide : 0u);
-  const uint32_t blk = (P.diag & kDiagBtAgg1) ? kBtAggBlock : kBtAgg2Block;
-  return hipLaunchKernel(bt_agg_fn(diag), dim3(kPartBins), dim3(blk),
-                         args, (P.diag & kDiagBtAgg1) ? agg_lds : bt_agg2_lds_bytes(P.log2sb, P.bt_grid), s);
-}
-
-hipError_t launch_fold_rows32(unsigned long long *gcounts, unsigned long long *base64, uint64_t cap,
-                              uint32_t nbk, hipStream_t s) {
-  hipLaunchKernelGGL(fold_rows32_kernel, dim3((uint32_t)std::min<uint64_t>((cap + 255) / 256, 4096)), dim3(256), 0,
-                     s, reinterpret_cast<uint32_t *>(gcounts), base64, cap, nbk);
-  return hipGetLastError();
+  return hipLaunchKernel(bt_agg_fn(diag), dim3(kPartBins), dim3(kBtAgg2Block), args,
+                         bt_agg2_lds_bytes(P.log2sb, P.bt_grid), s);
 }
 
 size_t bt_agg2_lds_bytes(uint32_t log2sb, uint32_t grid) {
   return bt_agg2_off_reg(1u << log2sb) + (size_t)grid * 4 + 16;
-}
-
-size_t bt_agg_lds_bytes(uint32_t log2sb, uint32_t grid) {
-  const uint32_t sb = 1u << log2sb;
-  return bt_agg_off_err(sb, grid) + kBtErr * 8 + kBins * sizeof(BinEntry) + 16;
 }
 
 }  // namespace sa

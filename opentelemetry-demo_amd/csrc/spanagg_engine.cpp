@@ -93,16 +93,14 @@ struct sa_engine {
   unsigned long long *expo_out_keys = nullptr;
   sa::ExpoRow *expo_out_rows = nullptr;
   uint32_t *expo_out_buckets = nullptr;
-  bool bt_scatter1 = false;  // SPANAGG_BT_SCATTER=1: round-1 scatter kernel (A/B runs)
-  bool bt_agg1 = false;      // SPANAGG_BT_AGG=1: first aggregate kernel (A/B runs)
   // partitioned HBM-table path (lazily allocated on the first launch)
   bool part = false;
   ulonglong2 *part_rec = nullptr;
   uint32_t *part_fill = nullptr;
   // binned-table path (spanagg_binned.hip): bin-local key sub-tables of
-  // 2^log2sb slots, stored ids m = key * kmul, u32 count rows folded into
-  // base64 before 2^32 spans accumulate (since_fold), span records in
-  // per-(bin, scatter workgroup) regions (lazily allocated)
+  // 2^log2sb slots, stored ids m = key * kmul, 32-B u8-count rows plus the u64
+  // spill array base64 [cap][nbk + 1], span records in per-(bin, scatter
+  // workgroup) regions (lazily allocated)
   bool bt = false;
   uint32_t log2sb = 0, bt_grid = 0;
   uint64_t kmul = 1, kinv = 1;
@@ -110,7 +108,6 @@ struct sa_engine {
   ulonglong2 *bt_rec = nullptr;
   uint32_t *bt_cnt = nullptr;
   unsigned long long *base64 = nullptr;
-  uint64_t since_fold = 0, fold_limit = 0xFFFFFFFFULL;
   size_t hll_slot_bytes = 0, cms_slot_elems = 0;
   // sa_ingest: two pinned host slots and their HBM copies; a slot is refilled
   // once its event (H2D copy + aggregation of the previous use) has passed
@@ -193,13 +190,13 @@ static bool build_bins(const sa_engine *e, sa::BinEntry (&bins)[sa::kBins]) {
 }
 
 static size_t counts_bytes(const sa_engine *e) {
-  return e->bt ? (size_t)e->cap * sa::row32_stride(e->nbk) * 4 : (size_t)e->cap * sa::row_stride(e->nbk) * 8;
+  return e->bt ? (size_t)e->cap * sa::kRowBytes : (size_t)e->cap * sa::row_stride(e->nbk) * 8;
 }
 
 static sa::RowGeom geom(const sa_engine *e) {
   sa::RowGeom g{};
   g.nbk = e->nbk;
-  g.row32 = e->bt ? 1u : 0u;
+  g.row8 = e->bt ? 1u : 0u;
   g.binned = e->bt ? 1u : 0u;
   g.log2cap = e->log2cap;
   g.log2sb = e->log2sb;
@@ -427,9 +424,9 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     // workgroups sized for the bin's sub-table
     e->log2sb = e->log2cap - sa::kPartBinBits;
     e->bt_grid = e->cus;
-    if (const char *v = std::getenv("SPANAGG_BT_SCATTER")) e->bt_scatter1 = std::atoi(v) == 1;
-    if (const char *v = std::getenv("SPANAGG_BT_AGG")) e->bt_agg1 = std::atoi(v) == 1;
-    e->agg_lds = std::max(sa::bt_agg_lds_bytes(e->log2sb, e->bt_grid), sa::bt_agg2_lds_bytes(e->log2sb, e->bt_grid));
+    e->agg_lds = sa::bt_agg2_lds_bytes(e->log2sb, e->bt_grid);
+    const size_t spill = (size_t)e->cap * (e->nbk + 1) * 8;
+    if ((rc = alloc((void **)&e->base64, spill))) return bail(rc);  // (zeroed)
     if (hipError_t st = sa::prepare_ingest_bt(e->agg_lds); st != hipSuccess)
       return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
     // a random odd multiplier per engine: series ids -> stored ids (bins and
@@ -441,8 +438,6 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     uint64_t x = e->kmul;  // Newton: x = x (2 - a x) doubles the correct low bits
     for (int i = 0; i < 6; ++i) x *= 2 - e->kmul * x;
     e->kinv = x;
-    if (const char *fl = std::getenv("SPANAGG_FOLD_LIMIT"))  // test knob: fold u32 rows sooner
-      e->fold_limit = std::max<uint64_t>(1, std::strtoull(fl, nullptr, 0));
   }
   if (hipMemcpy(e->d_seeds, kCmsSeed, sizeof kCmsSeed, hipMemcpyHostToDevice) != hipSuccess)
     return bail(fail(e, SA_EDEVICE, "seed upload failed"));
@@ -536,7 +531,7 @@ static int ingest_on(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
 }
 
 // Binned path: launch geometry, record regions (allocated once for the
-// largest launch) and the u32 row fold.  Region capacity: the mean records
+// largest launch).  Region capacity: the mean records
 // per (bin, scatter workgroup) plus 4 standard deviations and 8, in whole
 // 4-record chunks; records beyond it take the scatter's overflow table.
 static uint32_t bt_region_for(uint64_t wg_chunk) {
@@ -555,17 +550,6 @@ static int bt_prepare_launch(sa_engine *e, uint64_t n, IngestParams &P, hipStrea
         hipMalloc((void **)&e->bt_cnt, (size_t)e->bt_grid * sa::kPartBins * 4) != hipSuccess)
       return fail(e, SA_ENOMEM, "binned-path record buffers hipMalloc failed");
   }
-  if (e->since_fold + n > e->fold_limit) {  // u32 bucket counts could wrap: fold them first
-    if (!e->base64) {
-      const size_t bytes = (size_t)e->cap * (e->nbk + 1) * 8;
-      if (hipMalloc((void **)&e->base64, bytes) != hipSuccess)
-        return fail(e, SA_ENOMEM, "fold array hipMalloc failed");
-      SA_HIP(e, hipMemsetAsync(e->base64, 0, bytes, s));
-    }
-    SA_HIP(e, sa::launch_fold_rows32(e->gcounts, e->base64, e->cap, e->nbk, s));
-    e->since_fold = 0;
-  }
-  e->since_fold += n;
   P.log2sb = e->log2sb;
   P.kmul = e->kmul;
   P.kinv = e->kinv;
@@ -634,6 +618,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.slab_cnt = e->slab_cnt ? e->slab_cnt + (size_t)set * e->G * e->cap * srow : nullptr;
   P.slab_sum = e->slab_sum ? e->slab_sum + (size_t)set * e->G * e->cap : nullptr;
   P.gcounts = e->gcounts;
+  P.base64 = e->base64;
   std::memcpy(P.thr, e->thr, sizeof e->thr);
   P.npos = e->npos;
   P.nneg = e->nneg;
@@ -661,8 +646,6 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.seeds = e->d_seeds;
   P.stats = e->stats;
   P.diag = e->cfg.flags;
-  if (e->bt_scatter1) P.diag |= 1u << 24;
-  if (e->bt_agg1) P.diag |= 1u << 29;
   P.dbg = e->dbg;
   P.hll_lb = e->hll_lb;
   P.lb_shift = e->lb_shift;
@@ -673,7 +656,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
     st = sa::launch_ingest_small(P, grid, e->lds_bytes, s, e->variant);
   } else if (e->bt) {
     if (int rc = bt_prepare_launch(e, b->n, P, s)) return rc;
-    st = sa::launch_ingest_bt(P, e->agg_lds, s);
+    st = sa::launch_ingest_bt(P, s);
   } else if (e->part) {
     // records per bin: 1.25x the mean plus slack; a fuller bin spills to the
     // direct path, so this bounds memory, not correctness
@@ -865,7 +848,6 @@ int sa_flush(sa_engine *e, sa_red_result **out) {
   SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, e->stream));
   SA_HIP(e, sa::launch_compact(e->gkeys, e->gcounts, e->cap, geom(e), e->out_keys, e->out_rows,
                                e->scratch, e->cap, 1, e->stream));
-  e->since_fold = 0;
   uint64_t n = 0;
   SA_HIP(e, hipMemcpyAsync(&n, e->scratch, 8, hipMemcpyDeviceToHost, e->stream));
   SA_HIP(e, hipStreamSynchronize(e->stream));
@@ -1174,7 +1156,6 @@ int sa_gather_dense(sa_engine *e, const uint64_t *d_keys, uint64_t n, uint64_t *
     e->unflushed = false;
     SA_HIP(e, hipMemsetAsync(e->gcounts, 0, counts_bytes(e), s));
     if (e->base64) SA_HIP(e, hipMemsetAsync(e->base64, 0, (size_t)e->cap * (e->nbk + 1) * 8, s));
-    e->since_fold = 0;
   }
   if (s != e->stream) {
     SA_HIP(e, hipEventRecord(e->ev_b, s));

@@ -1385,17 +1385,15 @@ __global__ void reduce_slabs_kernel(const uint32_t *slab_cnt, const unsigned lon
 }
 
 // One counter row in the external layout [nbk bucket counts, ns sum] (u64),
-// from either row layout (u64 segment rows, or u32 rows + the u64 fold array).
+// from either row layout (u64 segment rows, or the binned path's 32-B u8 rows
+// + the u64 spill array).
 __device__ __forceinline__ bool row_nonzero(const unsigned long long *gcounts, uint64_t s, const RowGeom &g) {
-  if (g.row32) {
-    const uint32_t stride32 = row32_stride(g.nbk);
-    const uint32_t *row = reinterpret_cast<const uint32_t *>(gcounts) + s * stride32;
-    uint32_t any = 0;
-    for (uint32_t w = 0; w < stride32; ++w) any |= row[w];
-    if (any) return true;
-    if (g.base64)
-      for (uint32_t c = 0; c <= g.nbk; ++c)
-        if (g.base64[s * (g.nbk + 1) + c]) return true;
+  if (g.row8) {
+    const uint4 *row = reinterpret_cast<const uint4 *>(gcounts) + s * (kRowBytes / 16);
+    const uint4 a = row[0], b = row[1];
+    if (a.x | a.y | a.z | a.w | b.x | b.y | b.z | b.w) return true;
+    for (uint32_t c = 0; c <= g.nbk; ++c)
+      if (g.base64[s * (g.nbk + 1) + c]) return true;
     return false;
   }
   const uint32_t stride = row_stride(g.nbk);
@@ -1408,11 +1406,12 @@ __device__ __forceinline__ bool row_nonzero(const unsigned long long *gcounts, u
 __device__ __forceinline__ void row_emit(const unsigned long long *gcounts, uint64_t s, const RowGeom &g,
                                          unsigned long long *out) {
   const uint32_t nbk = g.nbk;
-  if (g.row32) {
-    const uint32_t *row = reinterpret_cast<const uint32_t *>(gcounts) + s * row32_stride(nbk);
-    const unsigned long long *b64 = g.base64 ? g.base64 + s * (nbk + 1) : nullptr;
-    for (uint32_t b = 0; b < nbk; ++b) out[b] = row[2 + b] + (b64 ? b64[b] : 0ULL);
-    out[nbk] = ((unsigned long long)row[1] << 32 | row[0]) + (b64 ? b64[nbk] : 0ULL);
+  if (g.row8) {
+    const unsigned long long *row = gcounts + s * (kRowBytes / 8);
+    const uint8_t *cnt = reinterpret_cast<const uint8_t *>(row + 1);
+    const unsigned long long *b64 = g.base64 + s * (nbk + 1);
+    for (uint32_t b = 0; b < nbk; ++b) out[b] = cnt[b] + b64[b];
+    out[nbk] = row[0] + b64[nbk];
     return;
   }
   const uint32_t stride = row_stride(nbk);
@@ -1424,12 +1423,10 @@ __device__ __forceinline__ void row_emit(const unsigned long long *gcounts, uint
 }
 
 __device__ __forceinline__ void row_zero(unsigned long long *gcounts, uint64_t s, const RowGeom &g) {
-  if (g.row32) {
-    const uint32_t stride32 = row32_stride(g.nbk);
-    uint32_t *row = reinterpret_cast<uint32_t *>(gcounts) + s * stride32;
-    for (uint32_t w = 0; w < stride32; ++w) row[w] = 0;
-    if (g.base64)
-      for (uint32_t c = 0; c <= g.nbk; ++c) g.base64[s * (g.nbk + 1) + c] = 0;
+  if (g.row8) {
+    uint4 *row = reinterpret_cast<uint4 *>(gcounts) + s * (kRowBytes / 16);
+    row[0] = row[1] = make_uint4(0, 0, 0, 0);
+    for (uint32_t c = 0; c <= g.nbk; ++c) g.base64[s * (g.nbk + 1) + c] = 0;
     return;
   }
   const uint32_t stride = row_stride(g.nbk);

@@ -1,7 +1,8 @@
 """GPU parity of the binned-table high-cardinality path (spanagg_binned.hip:
-bt_scatter_kernel + bt_aggregate_kernel; tables of 2^19..2^22 slots) against
-the CPU oracle, including the spill paths (stage/region overflow table, the
-direct path), the u32 row fold, full bins and launch splitting.
+bt_scatter2_kernel + bt_aggregate2_kernel; tables of 2^19..2^22 slots)
+against the CPU oracle, including the spill paths (stage/region overflow
+table, the direct path), the u8 rows' spill array, full bins and launch
+splitting.
 
 Bar (north_star): bucket counts, calls, HLL registers and count-min cells
 bit-exact; duration sums within 1e-9 relative (parity_util.SUM_RTOL).
@@ -75,18 +76,24 @@ def test_binned_matches_partitioned_path(zipf, monkeypatch):
             _check(e, batch, o)
 
 
-def test_binned_u32_rows_fold(monkeypatch):
-    """u32 bucket counts are folded into the u64 array before they could
-    wrap; a small fold limit folds between every launch (and after a flush)."""
-    monkeypatch.setenv("SPANAGG_FOLD_LIMIT", "150000")
-    batch, _, w0 = generate_highcard(600_000, seed=17, routes=200, pods=100, zipf_s=1.1)
+def test_binned_u8_rows_spill():
+    """Row counts are u8 (32-B rows): a bucket count that would pass 255 moves
+    the row's counts into the u64 spill array -- within one launch for the hot
+    keys of a Zipf mix, over several launches for the others.  Totals stay
+    exact across launches, and the spill array resets with the rows at flush."""
+    batch, _, w0 = generate_highcard(200_000, seed=17, routes=50, pods=40, zipf_s=1.1)
     with _engine(600_000) as e:
         e.window_advance(w0)
-        for a in range(0, 400_000, 100_000):
-            e.ingest(batch.slice(a, a + 100_000))
-        _check(e, batch.slice(0, 400_000))
-        e.ingest(batch.slice(400_000, 600_000))
-        _check(e, batch.slice(400_000, 600_000), o_windows=_oracle(batch))
+        for rounds in (4, 2):  # the second interval starts from rows and spills reset by the flush
+            o = pyoracle.Oracle(n_services=1)
+            for _ in range(rounds):
+                e.ingest(batch)
+                o.ingest(batch)
+            res = e.flush()
+            assert_red_equal(res, o.series())
+            assert int(res.calls.sum()) == rounds * len(batch)
+            assert int(res.bucket_counts.max()) > 255 * rounds  # the spill path ran
+        assert e.stats()["dropped_table_full"] == 0
 
 
 def test_binned_full_bin_reports_drops(monkeypatch):
