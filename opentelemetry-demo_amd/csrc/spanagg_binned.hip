@@ -360,17 +360,28 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
     }
   };
 
+  // Stage flushes: after every round, or -- once the first two rounds have
+  // put 32 or more keys in the overflow table (a skewed mix, whose hot keys
+  // bypass the stages) -- after every second round, which halves the
+  // barriers (for uniform keys the fuller stages would spill more records).
+  bool sparse = false;  // workgroup-uniform: read from LDS after a barrier
   for (uint32_t r = 0; r < rounds; r += 2) {
     step(buf[0], tstart(r), tstart(r + 2));
-    __syncthreads();
-    if (!(MODE & 1)) flush();
-    __syncthreads();
-    if (r + 1 < rounds) {
-      step(buf[1], tstart(r + 1), tstart(r + 3));
+    if (!sparse) {
       __syncthreads();
       if (!(MODE & 1)) flush();
       __syncthreads();
     }
+    if (r + 1 < rounds) step(buf[1], tstart(r + 1), tstart(r + 3));
+    __syncthreads();
+    if (!(MODE & 1)) flush();
+    if (r == 0 && wave == 0) {
+      uint32_t used = 0;
+      for (uint32_t h = lane; h < kBt2Hot; h += 64) used += wave_count(hkey[h] != 0);
+      if (lane == 0) hq_n[2] = used >= 32 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (r == 0) sparse = (MODE & 64) ? true : hq_n[2] != 0;
   }
   hll_settle(pend2);
   hll_settle(pend);
@@ -676,7 +687,9 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
 constexpr uint32_t kDiagBtAggNoRows = 1u << 21, kDiagBtNoAgg = 1u << 22, kDiagBtNoScatter = 1u << 23;
 constexpr uint32_t kDiagBtHotAcc = 1u << 25, kDiagBtHotErr = 1u << 26, kDiagBtSeqStore = 1u << 27,
                    kDiagBtNoStore = 1u << 28;
+constexpr uint32_t kDiagBtFlush2 = 1u << 14;
 static const void *bt_scatter2_fn(uint32_t diag) {
+  if (diag & kDiagBtFlush2) return (const void *)&bt_scatter2_kernel<64>;
   if (diag & kDiagBtSeqStore) return (const void *)&bt_scatter2_kernel<16>;
   if (diag & kDiagBtNoStore) return (const void *)&bt_scatter2_kernel<32>;
   if (diag & kDiagBtHotAcc) return (const void *)&bt_scatter2_kernel<4>;
@@ -708,7 +721,7 @@ static const void *bt_agg_fn(uint32_t diag) {
 }
 
 hipError_t prepare_ingest_bt(size_t agg_lds) {
-  for (uint32_t d : {0u, 1u, 2u, 3u, kDiagBtHotAcc, kDiagBtHotErr, kDiagBtSeqStore, kDiagBtNoStore})
+  for (uint32_t d : {0u, 1u, 2u, 3u, kDiagBtHotAcc, kDiagBtHotErr, kDiagBtSeqStore, kDiagBtNoStore, kDiagBtFlush2})
     if (hipError_t e = hipFuncSetAttribute(bt_scatter2_fn(d), hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)kBt2ScatterLds);
         e != hipSuccess)
