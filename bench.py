@@ -27,9 +27,10 @@ uniform and Zipf(1.1) over 1 M series) with their own roofline.
 
 Prints ONE JSON line on rank 0. `roofline` prices the ingest kernel against
 HBM (44 algorithmic bytes per span / 8 TB/s).  Its `kernel_ms` is the kernel
-alone: HIP events around each of a set of serial launches on one stream,
-inside the run (overlapping launches would double-count, so these are not
-taken from the timed steps); `roofline.pipelined` prices the timed steps'
+alone: HIP events around a block of back-to-back serial launches on one
+stream, divided by their number (`kernel_ms_bracketed`: events around each
+launch on its own), inside the run (overlapping launches would double-count,
+so these are not taken from the timed steps); `roofline.pipelined` prices the timed steps'
 device time per step (one start event all streams wait on, to the last
 stream's end event).
 `cpu_baseline` times the CPU oracle port (oracle/, RED+HLL+CMS, 1 thread) on
@@ -248,7 +249,7 @@ def run_workload(name, n, args, device, rank, world, barrier):
     for c in batch.columns():
         cols.append(torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(device))
     n_iso = max(3, args.steps // 5)
-    n_var = min(args.variants, 1 + args.settle + args.warmup + n_iso + args.steps)
+    n_var = min(args.variants, 1 + args.settle + args.warmup + 2 * n_iso + args.steps)
     variants = trace_variants(cols[3], cols[4], n_var, seed=1000 + rank, rank=rank, world=world)
     if world > 1:  # every span of every variant belongs to this rank's trace-id shard
         from spanagg.dist import shard_of
@@ -291,14 +292,23 @@ def run_workload(name, n, args, device, rank, world, barrier):
     torch.cuda.synchronize(device)
     cold_ms = c0.elapsed_time(c1)
     settle_ms = [round(a.elapsed_time(b), 4) for a, b in st]
-    # 1) the kernel alone: serial launches on one stream, HIP events around each
+    # 1) the kernel alone: serial launches on one stream.  kernel_ms: HIP events
+    #    around n_iso back-to-back launches, divided by n_iso (each launch's
+    #    duration plus the gap to the next); kernel_ms_bracketed: HIP events
+    #    around each launch on its own (adds the events' own cost per launch)
     iso = [(ev(), ev()) for _ in range(n_iso)]
     for a, b in iso:
         a.record(stream)
         step(0, stream)
         b.record(stream)
+    k0, k1 = ev(), ev()
+    k0.record(stream)
+    for _ in range(n_iso):
+        step(0, stream)
+    k1.record(stream)
     torch.cuda.synchronize(device)
-    kernel_ms = sum(a.elapsed_time(b) for a, b in iso) / len(iso)
+    kernel_ms_bracketed = sum(a.elapsed_time(b) for a, b in iso) / len(iso)
+    kernel_ms = k0.elapsed_time(k1) / n_iso
     # 2) the timed steps, alternating over the streams
     start = ev()
     ends = [ev() for _ in streams]
@@ -318,9 +328,10 @@ def run_workload(name, n, args, device, rank, world, barrier):
     barrier()
     device_ms = max(start.elapsed_time(e_) for e_ in ends) / max(1, args.steps)
     if world > 1:
-        t = torch.tensor([elapsed, kernel_ms, device_ms, cold_ms], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, kernel_ms, kernel_ms_bracketed, device_ms, cold_ms], dtype=torch.float64,
+                         device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms, device_ms, cold_ms = (float(x) for x in t)
+        elapsed, kernel_ms, kernel_ms_bracketed, device_ms, cold_ms = (float(x) for x in t)
     # one flush (+ RCCL merge across ranks) after the timed region
     torch.cuda.synchronize(device)
     tm = time.perf_counter()
@@ -336,7 +347,8 @@ def run_workload(name, n, args, device, rank, world, barrier):
     st = eng.stats()
     calls_ok = int(red.calls.sum()) == launches[0] * n * world - st["zero_key"] * (1 if world == 1 else world)
     out = {"wl": wl, "batch": batch, "eng": eng, "first_window": first_window, "elapsed": elapsed,
-           "kernel_ms": kernel_ms, "device_ms": device_ms, "cold_ms": cold_ms, "settle_ms": settle_ms,
+           "kernel_ms": kernel_ms, "kernel_ms_bracketed": kernel_ms_bracketed, "device_ms": device_ms,
+           "cold_ms": cold_ms, "settle_ms": settle_ms,
            "merge_ms": merge_ms,
            "calls_ok": calls_ok, "enqueue_s": enqueue_s, "streams": len(streams), "variants": n_var,
            "launches": launches[0], "hll_p": 14}
@@ -354,6 +366,7 @@ def roofline(name, n, r, traffic_path=None):
             "c4zipf": "bt_scatter2_kernel + bt_aggregate2_kernel (spanagg_binned.hip)"}[name]
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kern, "kernel_ms": r["kernel_ms"],
+            "kernel_ms_bracketed": r["kernel_ms_bracketed"],
             "bytes_per_span": BYTES_PER_SPAN, "traffic_source": tsrc,
             "pipelined": {"streams": r["streams"], "device_ms_per_step": r["device_ms"], "achieved": piped,
                           "frac": piped / HBM_PEAK_GBS}}
