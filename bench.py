@@ -21,7 +21,9 @@ stream; the cold first launch on a fresh engine is reported on its own, and
 the next `--settle` launches (default 16), while the window's HLL registers
 and their lower bounds settle, are timed one by one as `settle_ms` and kept
 out of `value` and `kernel_ms` (a 10 s window at these rates spans ~10^5
-launches, so the settled launch is the one a collector runs).  At
+launches, so the settled launch is the one a collector runs).  After the
+timed steps, `--soak-s` seconds (default 2) of back-to-back launches give the
+`sustained` rate (trace-id variants repeat there).  At
 N=1 the line also carries `c4` and `c4zipf` sub-objects (BASELINE config 4,
 uniform and Zipf(1.1) over 1 M series) with their own roofline.
 
@@ -327,6 +329,22 @@ def run_workload(name, n, args, device, rank, world, barrier):
     elapsed = time.perf_counter() - t0
     barrier()
     device_ms = max(start.elapsed_time(e_) for e_ in ends) / max(1, args.steps)
+    # 3) sustained: back-to-back launches over the streams for --soak-s seconds
+    #    (after the timed steps, never part of value; trace-id variants repeat
+    #    here, so later HLL reads raise little) -- the rate a collector holds
+    soak = None
+    if args.soak_s > 0:
+        per = max(1, int(args.soak_s / max(device_ms * 1e-3, 1e-5)) // 8)  # launches per host check
+        n_soak, ts = 0, time.perf_counter()
+        while True:
+            for i in range(per):
+                step(i)
+            n_soak += per
+            torch.cuda.synchronize(device)
+            if time.perf_counter() - ts >= args.soak_s:
+                break
+        soak_s = time.perf_counter() - ts
+        soak = {"value": n * n_soak / soak_s, "unit": "spans/s", "launches": n_soak, "seconds": soak_s}
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms, kernel_ms_bracketed, device_ms, cold_ms], dtype=torch.float64,
                          device=device)
@@ -348,7 +366,7 @@ def run_workload(name, n, args, device, rank, world, barrier):
     calls_ok = int(red.calls.sum()) == launches[0] * n * world - st["zero_key"] * (1 if world == 1 else world)
     out = {"wl": wl, "batch": batch, "eng": eng, "first_window": first_window, "elapsed": elapsed,
            "kernel_ms": kernel_ms, "kernel_ms_bracketed": kernel_ms_bracketed, "device_ms": device_ms,
-           "cold_ms": cold_ms, "settle_ms": settle_ms,
+           "cold_ms": cold_ms, "settle_ms": settle_ms, "sustained": soak,
            "merge_ms": merge_ms,
            "calls_ok": calls_ok, "enqueue_s": enqueue_s, "streams": len(streams), "variants": n_var,
            "launches": launches[0], "hll_p": 14}
@@ -389,6 +407,8 @@ def main():
     ap.add_argument("--streams", type=int, default=2,
                     help="launch streams the steps alternate over (the engine's two slab sets "
                          "let consecutive launches overlap); 1 = strictly serial launches")
+    ap.add_argument("--soak-s", type=float, default=2.0,
+                    help="seconds of back-to-back launches after the timed steps (reported as sustained)")
     ap.add_argument("--settle", type=int, default=16,
                     help="untimed launches after the cold one, before the warm-up (HLL registers settle)")
     ap.add_argument("--variants", type=int, default=128,
@@ -463,6 +483,7 @@ def main():
             subs[sub] = {"workload": WORKLOADS[sub], "value": n * args.steps / r["elapsed"], "unit": "spans/s",
                          "ms_per_step": r["elapsed"] * 1e3 / args.steps, "steps": args.steps,
                          "warmup": args.warmup, "cold_launch_ms": r["cold_ms"], "settle_ms": r["settle_ms"],
+                         "sustained": r["sustained"],
                          "roofline": roofline(sub, n, r), "calls_check": r["calls_ok"],
                          "trace_variants": r["variants"]}
             torch.cuda.empty_cache()
@@ -483,6 +504,7 @@ def main():
                        "parallelism": f"trace-id shards x{world}, RCCL merge at flush"},
             "roofline": roofline(args.workload, n, main_r, args.traffic),
             "cold_launch_ms": main_r["cold_ms"], "settle_ms": main_r["settle_ms"],
+            "sustained": main_r["sustained"],
             "trace_variants": main_r["variants"],
             "merge_ms": main_r["merge_ms"], "calls_check": main_r["calls_ok"],
             "host_enqueue_us_per_step": main_r["enqueue_s"] * 1e6 / max(1, args.steps),
