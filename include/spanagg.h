@@ -180,7 +180,8 @@ int sa_sync(sa_engine *e);
 
 /* exportMetrics: delta since the last flush, then the engine's RED counters are
  * reset. Keys stay resident as a cache of the series seen, until more than half
- * the table is taken: then the flush empties it (sa_reclaim_keys), so series
+ * the table is taken (35 % for the binned table of large key capacities): then
+ * the flush empties it (sa_reclaim_keys), so series
  * that churn (new resources after evictions or restarts, delta purges) do not
  * fill it for good. Returns SA_EFULL (with the result still filled) if spans
  * were dropped since the previous flush: more distinct series within one flush
@@ -188,7 +189,7 @@ int sa_sync(sa_engine *e);
 int sa_flush(sa_engine *e, sa_red_result **out);
 void sa_red_result_free(sa_red_result *r);
 /* Key-table reclamation (what every flush does when the table is more than
- * half full; force != 0: empty it now).  Only between a flush (or a resetting
+ * half full, binned tables 35 %; force != 0: empty it now).  Only between a flush (or a resetting
  * sa_gather_dense) and the next ingest: SA_ESTATE otherwise.  Results do not
  * change: every row is zero then, and a series' next span re-inserts its key.
  * Replaces nothing in the reference (upstream keys live in a Go LRU map,

@@ -816,14 +816,18 @@ static int reclaim_now(sa_engine *e) {
 
 // Flush-time policy: reclaim once more than half the table is resident, so a
 // collector whose series churn (new pods, restarts) keeps room for the next
-// interval's series instead of dropping their spans.
+// interval's series instead of dropping their spans.  Binned tables reclaim
+// past 35 %: their bins are as small as 256 slots, and a fully churned next
+// interval doubles the load, which must stay near 70 % for no bin to fill
+// (at 76 % of a 2^19-slot table, 2,048 bins of 256, P(some bin full) = 2.8 %).
 static int reclaim_if_full(sa_engine *e) {
   SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, e->stream));
   SA_HIP(e, sa::launch_count_keys(e->gkeys, e->cap, e->scratch, e->stream));
   uint64_t nk = 0;
   SA_HIP(e, hipMemcpyAsync(&nk, e->scratch, 8, hipMemcpyDeviceToHost, e->stream));
   SA_HIP(e, hipStreamSynchronize(e->stream));
-  return 2 * nk > e->cap ? reclaim_now(e) : SA_OK;
+  const bool over = e->bt ? 20 * nk > 7 * (uint64_t)e->cap : 2 * nk > e->cap;
+  return over ? reclaim_now(e) : SA_OK;
 }
 
 int sa_reclaim_keys(sa_engine *e, int force) {
