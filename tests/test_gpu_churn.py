@@ -2,8 +2,8 @@
 
 A long-running collector keeps meeting new series (new pods, restarts, delta
 purges), many more over its life than key_capacity.  Each flush leaves every
-row at zero, and once the table is more than half full the flush empties it,
-so only the series of ONE flush interval have to fit.  Checked against the
+row at zero, and once the table is more than half full (binned tables: 35 %)
+the flush empties it, so only the series of ONE flush interval have to fit.  Checked against the
 oracle interval by interval (RED bit-exact, no drops) and, for the window
 sketches, over all intervals at once (the per-slot error counts are folded
 into the count-min before the keys go)."""
@@ -56,6 +56,21 @@ def test_churn_beyond_capacity_no_drops(key_capacity, per_interval):
             hll, cms = o.window(wid)
             assert np.array_equal(sk.hll, hll), wid
             assert np.array_equal(sk.cms, cms), wid
+
+
+@pytest.mark.parametrize("n_keys,kept", [(150_000, True), (200_000, False)])
+def test_binned_reclaim_threshold(n_keys, kept):
+    # key_capacity 300,000: the binned table of 2^19 slots in 2,048 bins of
+    # 256; the flush keeps up to 35 % (183,500 keys) resident, so a fully
+    # churned next interval stays near 70 % and fills no bin
+    rng = np.random.default_rng(n_keys)
+    with Engine(Config(n_services=8, n_windows=8, key_capacity=300_000)) as e:
+        e.window_advance(BASE)
+        e.ingest(_interval(rng, n_keys, 1))
+        e.flush()
+        st = e.stats()
+        assert st["table_capacity"] == 1 << 19 and st["small_table"] == 0
+        assert st["n_keys"] == (n_keys if kept else 0)
 
 
 def test_forced_reclaim_changes_nothing_and_needs_a_flush():
