@@ -23,7 +23,12 @@ and their lower bounds settle, are timed one by one as `settle_ms` and kept
 out of `value` and `kernel_ms` (a 10 s window at these rates spans ~10^5
 launches, so the settled launch is the one a collector runs).  After the
 timed steps, `--soak-s` seconds (default 2) of back-to-back launches give the
-`sustained` rate (trace-id variants repeat there).  At
+`sustained` rate (trace-id variants repeat there, so it is the rate of a
+saturated window, never a kernel figure).  `value_incl_settle` prices the
+whole window from its cold start: spans of the cold, settling and timed
+launches over their time (HIP events for the first two, wall clock for the
+timed steps).  `hll_filter_off` is the C2 kernel time of the same launches
+with the HLL lower-bound filter off (every span gathers its register).  At
 N=1 the line also carries `c4` and `c4zipf` sub-objects (BASELINE config 4,
 uniform and Zipf(1.1) over 1 M series) with their own roofline.
 
@@ -344,7 +349,10 @@ def run_workload(name, n, args, device, rank, world, barrier):
             if time.perf_counter() - ts >= args.soak_s:
                 break
         soak_s = time.perf_counter() - ts
-        soak = {"value": n * n_soak / soak_s, "unit": "spans/s", "launches": n_soak, "seconds": soak_s}
+        soak = {"value": n * n_soak / soak_s, "unit": "spans/s", "launches": n_soak, "seconds": soak_s,
+                "note": f"trace-id variants repeat every {len(variants)} launches here, so the window's HLL "
+                        "registers saturate and their raises idle: the rate of a saturated window, not a "
+                        "figure of the kernel on fresh traces (value's timed steps are all fresh variants)"}
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms, kernel_ms_bracketed, device_ms, cold_ms], dtype=torch.float64,
                          device=device)
@@ -364,14 +372,104 @@ def run_workload(name, n, args, device, rank, world, barrier):
     merge_ms = (time.perf_counter() - tm) * 1e3
     st = eng.stats()
     calls_ok = int(red.calls.sum()) == launches[0] * n * world - st["zero_key"] * (1 if world == 1 else world)
-    out = {"wl": wl, "batch": batch, "eng": eng, "first_window": first_window, "elapsed": elapsed,
+    # the whole window from its cold start: cold + settling launches (HIP
+    # events, one by one) + the timed steps (wall clock); the warm-up and the
+    # isolated kernel-time launches in between are left out
+    incl_s = (cold_ms + sum(settle_ms)) * 1e-3 + elapsed
+    out = {"value_incl_settle": world * n * (1 + args.settle + args.steps) / incl_s,
+           "wl": wl, "batch": batch, "eng": eng, "first_window": first_window, "elapsed": elapsed,
            "kernel_ms": kernel_ms, "kernel_ms_bracketed": kernel_ms_bracketed, "device_ms": device_ms,
            "cold_ms": cold_ms, "settle_ms": settle_ms, "sustained": soak,
            "merge_ms": merge_ms,
            "calls_ok": calls_ok, "enqueue_s": enqueue_s, "streams": len(streams), "variants": n_var,
-           "launches": launches[0], "hll_p": 14}
+           "launches": launches[0], "hll_p": 14,
+           "hll_filtered_frac": st["hll_filtered"] / max(1, launches[0] * n)}
     del variants, cols
     return out
+
+
+def kernel_ms_filter_off(n, args, device):
+    """C2 kernel time with the HLL lower-bound filter off (SPANAGG_HLL_LB=0 at
+    engine creation): every span reads its HLL register.  Same launches as the
+    main run's kernel time (fresh variants, after cold + settle + warm-up), so
+    the filter's share of the kernel time is visible beside `value`."""
+    import numpy as np
+    import torch
+
+    from spanagg import Config, Engine
+    from spanagg.synth import generate_c2
+
+    wl = generate_c2(n, seed=42)
+    cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(device)
+            for c in wl.batch.columns()]
+    n_iso = max(3, args.steps // 5)
+    k = 1 + args.settle + args.warmup + n_iso
+    variants = trace_variants(cols[3], cols[4], k, seed=1000)
+    old = os.environ.get("SPANAGG_HLL_LB")
+    os.environ["SPANAGG_HLL_LB"] = "0"
+    try:
+        eng = Engine(Config(n_services=wl.n_services, n_windows=16, key_capacity=1500, device=device.index))
+    finally:
+        if old is None:
+            del os.environ["SPANAGG_HLL_LB"]
+        else:
+            os.environ["SPANAGG_HLL_LB"] = old
+    eng.window_advance(wl.first_window)
+    s = torch.cuda.current_stream(device)
+    for w0, w1 in variants[: k - n_iso]:
+        eng.ingest_device(cols[0], cols[1], cols[2], w0, w1, cols[5], n=n, stream=s.cuda_stream)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for w0, w1 in variants[k - n_iso:]:
+        eng.ingest_device(cols[0], cols[1], cols[2], w0, w1, cols[5], n=n, stream=s.cuda_stream)
+    b.record(s)
+    torch.cuda.synchronize(device)
+    ms = a.elapsed_time(b) / n_iso
+    filt = eng.stats()["hll_filtered"]
+    eng.close()
+    return {"kernel_ms": ms, "hll_filtered": filt,
+            "note": "C2 kernel alone (serial launches after cold + settle + warm-up, fresh trace-id variants) "
+                    "with SPANAGG_HLL_LB=0: every span gathers its HLL register"}
+
+
+def run_group(n, members, args, device):
+    """--group N: N engines of one group on this one device, fed through
+    sa_group_ingest_device (the partition kernel shards each batch by trace id
+    into the members' buffers).  Measures the group's overhead on one GPU
+    (partition + N smaller launches), not multi-GPU scaling."""
+    import numpy as np
+    import torch
+
+    from spanagg import Config, Group
+    from spanagg.synth import generate_c2
+
+    wl = generate_c2(n, seed=42)
+    cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(device)
+            for c in wl.batch.columns()]
+    k = args.warmup + args.steps
+    variants = trace_variants(cols[3], cols[4], min(k, args.variants), seed=1000)
+    g = Group([device.index] * members, Config(n_services=wl.n_services, n_windows=16, key_capacity=1500))
+    g.window_advance(wl.first_window)
+    s = torch.cuda.current_stream(device)
+    for i in range(args.warmup):
+        w0, w1 = variants[i % len(variants)]
+        g.ingest_device(cols[0], cols[1], cols[2], w0, w1, cols[5], n=n, stream=s.cuda_stream)
+    g.sync()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for i in range(args.warmup, k):
+        w0, w1 = variants[i % len(variants)]
+        g.ingest_device(cols[0], cols[1], cols[2], w0, w1, cols[5], n=n, stream=s.cuda_stream)
+    g.sync()
+    torch.cuda.synchronize(device)
+    el = time.perf_counter() - t0
+    calls = int(g.flush().calls.sum())
+    st = g.stats()
+    g.close()
+    return {"members": members, "value": n * args.steps / el, "unit": "spans/s", "ms_per_step": el * 1e3 / args.steps,
+            "calls_check": calls == n * k - st["zero_key"],
+            "note": f"{members} engines of one group on this device, sa_group_ingest_device of {n:,}-span "
+                    "device batches (partition kernel + one launch per member); overhead on one GPU, not scaling"}
 
 
 def roofline(name, n, r, traffic_path=None):
@@ -425,6 +523,10 @@ def main():
                     help="spans for the Node host's OTLP->GPU rate (0 = skip)")
     ap.add_argument("--cpu-workers", type=int, default=None,
                     help="processes for the multi-core CPU baseline (default: every usable host core; 0 = skip)")
+    ap.add_argument("--group", type=int, default=0,
+                    help="also time an N-member engine group on this one device (sa_group_ingest_device)")
+    ap.add_argument("--no-filter-off", action="store_true",
+                    help="skip the C2 kernel time with the HLL lower-bound filter off")
     ap.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_worker is not None:  # child of cpu_baseline_multicore (no GPU use)
@@ -481,6 +583,7 @@ def main():
             r = run_workload(sub, n, args, device, rank, world, barrier)
             r["eng"].close()
             subs[sub] = {"workload": WORKLOADS[sub], "value": n * args.steps / r["elapsed"], "unit": "spans/s",
+                         "value_incl_settle": r["value_incl_settle"],
                          "ms_per_step": r["elapsed"] * 1e3 / args.steps, "steps": args.steps,
                          "warmup": args.warmup, "cold_launch_ms": r["cold_ms"], "settle_ms": r["settle_ms"],
                          "sustained": r["sustained"],
@@ -488,8 +591,17 @@ def main():
                          "trace_variants": r["variants"]}
             torch.cuda.empty_cache()
 
+    extra = {}
+    if world == 1 and args.workload == "c2" and not args.no_filter_off:
+        extra["hll_filter_off"] = kernel_ms_filter_off(n, args, device)
+        torch.cuda.empty_cache()
+    if world == 1 and args.group > 1:
+        extra["group"] = run_group(n, args.group, args, device)
+        torch.cuda.empty_cache()
+
     result = None
-    ok = main_r["calls_ok"] and all(v["calls_check"] for v in subs.values())
+    ok = main_r["calls_ok"] and all(v["calls_check"] for v in subs.values()) and \
+        all(v.get("calls_check", True) for v in extra.values())
     if rank == 0:
         elapsed = main_r["elapsed"]
         result = {
@@ -503,13 +615,16 @@ def main():
                        "global_spans_per_step": n * world,
                        "parallelism": f"trace-id shards x{world}, RCCL merge at flush"},
             "roofline": roofline(args.workload, n, main_r, args.traffic),
+            "value_incl_settle": main_r["value_incl_settle"],
             "cold_launch_ms": main_r["cold_ms"], "settle_ms": main_r["settle_ms"],
             "sustained": main_r["sustained"],
             "trace_variants": main_r["variants"],
+            "hll_filtered_frac": main_r["hll_filtered_frac"],
             "merge_ms": main_r["merge_ms"], "calls_check": main_r["calls_ok"],
             "host_enqueue_us_per_step": main_r["enqueue_s"] * 1e6 / max(1, args.steps),
         }
         result.update(subs)
+        result.update(extra)
         if h2d is not None:
             result["host_buffer_ingest"] = h2d
         wl = main_r["wl"]

@@ -560,6 +560,7 @@ napi_value Stats(napi_env env, napi_callback_info info) {
     set(env, o, "nKeys", big(env, s.n_keys));
     set(env, o, "tableCapacity", big(env, s.table_capacity));
     set(env, o, "windowBase", big(env, s.window_base));
+    set(env, o, "hllFiltered", big(env, s.hll_filtered));
     napi_get_boolean(env, s.small_table != 0, &b);
     set(env, o, "smallTable", b);
     set(env, o, "engines", num(env, h->g ? sa_group_size(h->g) : 1));

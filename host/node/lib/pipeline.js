@@ -16,12 +16,14 @@ const otlp = require('./otlp');
 const collectorConfig = require('./collector_config');
 const { SpanMetricsConnector } = require('./connector');
 const { OtlpReceiver, OtlpHttpExporter, MemoryLimiter } = require('./receiver');
+const { DEMO_SPAN_NAME_RULES } = require('./transform');
 
 class TracesToMetricsPipeline {
   /**
    * @param opts.spanmetrics  connector config (YAML field names)
-   * @param opts.transform    span-name rules (default: none; fromCollectorConfig derives
-   *                          them from the collector config's transform processors)
+   * @param opts.transform    span-name rules (default: the demo collector's two rules,
+   *                          otelcol-config.yml:106-113; [] = none; fromCollectorConfig
+   *                          derives them from the collector config's transform processors)
    * @param opts.memoryLimiter MemoryLimiter options (default: the demo's 80% / 25%), or false
    * @param opts.receiver     OtlpReceiver options ({httpPort, grpcPort, host}), or false
    * @param opts.exporter     OtlpHttpExporter options ({endpoint}), or false
@@ -31,7 +33,7 @@ class TracesToMetricsPipeline {
    *                          native columnizer's threads); default on, false = one at a time
    */
   constructor(opts = {}) {
-    this.rules = opts.transform || [];
+    this.rules = opts.transform !== undefined ? opts.transform : DEMO_SPAN_NAME_RULES;
     this.limiter = opts.memoryLimiter === false ? null
       : new MemoryLimiter(Object.assign({ limit_percentage: 80, spike_limit_percentage: 25 }, opts.memoryLimiter));
     this.exporter = opts.exporter ? new OtlpHttpExporter(opts.exporter) : null;

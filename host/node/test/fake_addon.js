@@ -22,7 +22,7 @@ class FakeAddon {
     this.batches = [];
     this.base = 0n;
   }
-  abiVersion() { return 2; }
+  abiVersion() { return 3; }
   configDefault() {
     return { bounds: DEFAULT_BOUNDS.slice(), unit: 'ms', hllP: 14, cmsD: 4, cmsW: 2048,
       windowNs: 10000000000n, nWindows: 8, nServices: 64, keyCapacity: 1000, device: 0, flags: 0 };

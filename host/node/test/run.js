@@ -186,7 +186,7 @@ test('config: durations, defaults and validation', () => {
 
 test('addon loads; pure helpers work; engine errors carry sa_status codes', () => {
   const addon = require('../lib/addon').load();
-  assert.strictEqual(addon.abiVersion(), 2);
+  assert.strictEqual(addon.abiVersion(), 3);
   const d = addon.configDefault();
   assert.deepStrictEqual(d.bounds, [2, 4, 6, 8, 10, 50, 100, 200, 400, 800, 1000, 1400, 2000, 5000, 10000, 15000]);
   const t = addon.bucketThresholds(d.bounds, 'ms');
@@ -618,6 +618,22 @@ test('pipeline queue: requests of one event-loop turn go through consumeTracesBa
   const calls = dpsOf(p.connector.exportMetrics(), 'traces.span.metrics.calls');
   assert.deepStrictEqual(calls.map((d) => d.asInt), [2n, 2n]);
   p.connector.shutdown();
+});
+
+test('pipeline constructor (README / INTEGRATION demo path) applies the demo transform rules', () => {
+  const { TracesToMetricsPipeline: P } = require(path.join(lib, 'pipeline'));
+  const p = new P({ addon: new FakeAddon(), receiver: false, exporter: false, memoryLimiter: false });
+  assert.deepStrictEqual(p.rules, DEMO_SPAN_NAME_RULES);
+  p.consumeTraces(otlp.encodeTraces(request([[{ 'service.name': 'frontend' }, [
+    span('GET /api/products/0PUK6V6EV0?currency=USD'), span('GET /api/products/66VCHSJNUP'),
+    span('GET /api/cart?sessionId=1')]]])));
+  const names = dpsOf(p.connector.exportMetrics(), 'traces.span.metrics.calls')
+    .map((d) => d.attributes.find((a) => a.key === 'span.name').value.value).sort();
+  assert.deepStrictEqual(names, ['GET /api/cart', 'GET /api/products/{productId}']);
+  p.connector.shutdown();
+  const none = new P({ addon: new FakeAddon(), receiver: false, exporter: false, memoryLimiter: false, transform: [] });
+  assert.deepStrictEqual(none.rules, []);
+  none.connector.shutdown();
 });
 
 test('native columnizer: invalid UTF-8 falls back to JavaScript; malformed bytes are rejected', () => {

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SA_ABI_VERSION 2
+#define SA_ABI_VERSION 3
 #define SA_MAX_BOUNDS 62
 
 typedef enum {
@@ -149,6 +149,11 @@ typedef struct {
     uint64_t window_base;          /* oldest resident window id */
     uint32_t small_table;          /* 1 = LDS-mirrored table path, 0 = HBM path */
     uint32_t pad;
+    /* spans whose HLL update was skipped without reading their register: rho
+     * at or below the lower bound of the register's sub-block, so it could not
+     * raise it (the small-table and binned kernels; 0 on the other paths).
+     * Diagnostic: shows how much of a window runs on the filtered path. */
+    uint64_t hll_filtered;
 } sa_stats;
 
 typedef struct sa_engine sa_engine;
@@ -162,9 +167,11 @@ int sa_create(const sa_config *cfg, sa_engine **out);
 void sa_destroy(sa_engine *e);
 const char *sa_last_error(const sa_engine *e);
 
-/* Host-memory batch: packed into one of two pinned staging slots, copied to
- * HBM and aggregated on the engine stream.  Returns once the batch has been
- * copied out of the caller's buffers (they may be reused at once); the
+/* Host-memory batch: packed into one of two pinned staging slots (chunks of
+ * 2^18 spans or more: copied from the caller's pageable columns by the HIP
+ * runtime, and waited for), copied to HBM and aggregated on the engine
+ * stream.  Returns once the batch has been copied out of the caller's buffers
+ * (they may be reused or freed at once); the
  * aggregation completes asynchronously -- every read (sa_flush*, sa_window_*,
  * sa_get_stats) and sa_sync wait for it, and a device error surfaces there. */
 int sa_ingest(sa_engine *e, const sa_span_batch *batch);
@@ -256,8 +263,21 @@ uint32_t sa_group_size(const sa_group *g);
 int sa_group_uses_rccl(const sa_group *g);
 /* Member engine i (for device-resident ingest of a shard the caller made). */
 sa_engine *sa_group_member(sa_group *g, uint32_t i);
-/* Host batch: split by trace_w1 % n, each shard ingested by its member. */
+/* Host batch: split by trace_w1 % n, each shard ingested by its member.  The
+ * split is one pass over trace_w1 (shard sizes) and one gather of each span
+ * into its member's packed shard, both on worker threads; the call returns
+ * once every member has copied its shard out of the caller's buffers. */
 int sa_group_ingest(sa_group *g, const sa_span_batch *batch);
+/* Device-resident batch in HBM of member `src`'s device (`stream`: a
+ * hipStream_t of that device, NULL = the group's stream there).  A partition
+ * kernel on that device counts the shards (trace_w1 % n; the call waits for
+ * these counts, a few microseconds) and scatters every span into its member's
+ * packed shard; shards of members on other devices are copied there
+ * peer-to-peer (xGMI DMA), and every member ingests its shard on its own
+ * stream.  Asynchronous otherwise: the batch must stay valid until `stream`
+ * reaches this point (the partition has read it); sa_group_sync waits for the
+ * members.  Same results as sa_group_ingest of the same spans. */
+int sa_group_ingest_device(sa_group *g, const sa_span_batch *batch, uint32_t src, void *stream);
 int sa_group_sync(sa_group *g);
 /* Merged delta since the previous group flush (members reset); SA_EFULL as
  * sa_flush when any member dropped spans. Free with sa_red_result_free. */

@@ -30,6 +30,41 @@ __device__ __forceinline__ uint64_t xxh64_16(uint64_t a, uint64_t b) {
   return h;
 }
 
+// The same hash on 32-bit halves (the lean C2 kernel): each 64-bit multiply by
+// a constant is one v_mad_u64_u32 and two v_mul_lo_u32 (three quarter-rate
+// ops, the minimum for a 64 x 64 -> 64 product) and each rotate a pair of
+// v_alignbit.  Written on u64 values, LLVM turns rotl(x * C, 31) into a second
+// multiply by C << 31 (five quarter-rate ops instead of three plus two
+// alignbits) and 64-bit shifts into v_lshlrev_b64.
+struct H64 {
+  uint32_t lo, hi;
+};
+__device__ __forceinline__ H64 h64(uint64_t x) { return H64{(uint32_t)x, (uint32_t)(x >> 32)}; }
+__device__ __forceinline__ H64 h64_mulc(H64 x, uint64_t c) {
+  const uint32_t cl = (uint32_t)c, ch = (uint32_t)(c >> 32);
+  const uint64_t p = (uint64_t)x.lo * cl;
+  return H64{(uint32_t)p, (uint32_t)(p >> 32) + x.lo * ch + x.hi * cl};
+}
+__device__ __forceinline__ H64 h64_rotl(H64 x, int r) {  // 0 < r < 32
+  return H64{__builtin_amdgcn_alignbit(x.lo, x.hi, 32 - r), __builtin_amdgcn_alignbit(x.hi, x.lo, 32 - r)};
+}
+__device__ __forceinline__ H64 h64_xor(H64 a, H64 b) { return H64{a.lo ^ b.lo, a.hi ^ b.hi}; }
+__device__ __forceinline__ H64 h64_addc(H64 a, uint64_t c) {
+  return h64((((uint64_t)a.hi << 32) | a.lo) + c);
+}
+__device__ __forceinline__ H64 xxh64_16_h(uint64_t a, uint64_t b) {
+  H64 h = h64_xor(h64_mulc(h64_rotl(h64_mulc(h64(a), XP2), 31), XP1), h64(XP5 + 16));
+  h = h64_addc(h64_mulc(h64_rotl(h, 27), XP1), XP4);
+  h = h64_xor(h, h64_mulc(h64_rotl(h64_mulc(h64(b), XP2), 31), XP1));
+  h = h64_addc(h64_mulc(h64_rotl(h, 27), XP1), XP4);
+  h.lo ^= h.hi >> 1;  // h ^= h >> 33
+  h = h64_mulc(h, XP2);
+  h = H64{h.lo ^ __builtin_amdgcn_alignbit(h.hi, h.lo, 29), h.hi ^ (h.hi >> 29)};  // h ^= h >> 29
+  h = h64_mulc(h, XP3);
+  h.lo ^= h.hi;  // h ^= h >> 32
+  return h;
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   uint64_t z = x + 0x9E3779B97F4A7C15ULL;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -350,6 +385,28 @@ __device__ __forceinline__ uint32_t window_slot(const IngestParams &P, uint64_t 
   r += lo ? (long long)P.window_ns : 0;
   q += r >= (long long)P.window_ns ? 1u : 0u;
   return delta < P.ring_ns ? ((P.base_slot + q) & P.win_mask) : 0xFFFFFFFFu;
+}
+
+// window_slot on 32-bit pieces (the lean C2 kernel): the float estimate from
+// two v_cvt_f32_u32 (written as a 64-bit conversion LLVM expands a generic
+// normalising sequence with a 64-bit shift), q * window_ns as one
+// v_mad_u64_u32 plus a 24-bit multiply-add for the high word (q < 2^24 inside
+// the ring, window_ns < 2^56 -- checked by the host), and the +-1 correction
+// from the remainder's sign and size.
+__device__ __forceinline__ uint32_t window_slot_lean(const IngestParams &P, uint64_t end) {
+  const uint64_t delta = end - P.base_ns;  // wraps (huge) for end < base
+  float fh, fl;
+  asm("v_cvt_f32_u32 %0, %1" : "=v"(fh) : "v"((uint32_t)(delta >> 32)));
+  asm("v_cvt_f32_u32 %0, %1" : "=v"(fl) : "v"((uint32_t)delta));
+  const uint32_t q = (uint32_t)(__builtin_fmaf(fh, 4294967296.0f, fl) * P.inv_window);
+  const uint64_t lo = (uint64_t)q * (uint32_t)P.window_ns;  // v_mad_u64_u32
+  uint32_t qh;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(qh) : "v"(q), "s"((uint32_t)(P.window_ns >> 32)), "v"((uint32_t)(lo >> 32)));
+  const uint64_t r = delta - (((uint64_t)qh << 32) | (uint32_t)lo);
+  const uint32_t neg = (uint32_t)((int32_t)(r >> 32) >> 31);  // r < 0: q one too high (then r >= W too)
+  const uint32_t big = r >= P.window_ns ? 1u : 0u;            // r >= W: q one too low
+  const uint32_t qq = q + big + (neg << 1);
+  return delta < P.ring_ns ? ((P.base_slot + qq) & P.win_mask) : 0xFFFFFFFFu;
 }
 
 // Bucket via the LDS bin table (BK = 1) or linear thresholds (BK = 0).

@@ -19,6 +19,9 @@ enum : int {
   kStatDropped = 3,
   kNumStats = 4
 };
+// HLL updates skipped by the lower-bound filter (sa_stats.hll_filtered): one
+// u64 slot per workgroup index (mod kFiltSlots), summed when stats are read
+constexpr uint32_t kFiltSlots = 1024;
 
 // Bucket lookup table: bin k = floor(log2 d) (k = 64 for d = 0).  For d in
 // bin k, bucket = base + [d > ta] + [d > tb] (ta/tb = UINT64_MAX when absent);
@@ -93,6 +96,7 @@ struct IngestParams {
   // window's bounds, so a bound read at any time stays a lower bound).
   uint8_t *hll_lb;
   uint32_t lb_shift, lb_n, lb_seq;
+  unsigned long long *hll_filt;  // [kFiltSlots] (sa_stats.hll_filtered)
 };
 
 // Exponential-histogram mode (spanagg_expo.hip): per key slot a header and
@@ -267,7 +271,9 @@ struct ProbeSeq {
 };
 __host__ __device__ inline ProbeSeq probe_seq(uint64_t key, uint32_t log2cap) {
   const uint32_t h1 = ((uint32_t)key ^ (uint32_t)(key >> 32)) * 0x9E3779B1u;
-  const uint32_t h2 = (h1 ^ (h1 >> 16)) * 0x85EBCA6Bu;
+  // second choice from a 24-bit multiply (v_mul_u32_u24, full rate; a 32-bit
+  // multiply is quarter rate): the top bits of its low word mix all 24 inputs
+  const uint32_t h2 = ((h1 ^ (h1 >> 16)) & 0xFFFFFFu) * 0x85EBCAu;
   const uint32_t sh = 34 - log2cap;  // top (log2cap - 2) bits
   return ProbeSeq{h1 >> sh, h2 >> sh, (1u << (log2cap - 2)) - 1};
 }
@@ -296,9 +302,9 @@ constexpr uint32_t kHbmBlock = 256;
 // tiles in flight, 10 four spans per lane, 11 generic (default cache policy),
 // 12 / 13 = 8 / 11 specialised for cap 2048, 17 buckets, HLL p 14; 14 = 12 with
 // dynamic wave chunks; 15 = 14 generic; 16-18 = 14 with OPT 1 / 3 / 2; 19 = 16
-// with the batched end-of-launch write-back (v2_epilogue).
-constexpr int kNumLdsVariants = 20;
-constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2, 2};
+// with the batched end-of-launch write-back (v2_epilogue); 20 = 19 LEAN.
+constexpr int kNumLdsVariants = 21;
+constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
 // v2 kernels keep u16 LDS counters for a whole launch: spans per workgroup per launch
 constexpr uint32_t kMaxWgSpans = 65532;
 constexpr uint32_t kDbgPerWg = 136;  // diagnostic stamps per workgroup: 8 + 16 waves x 8

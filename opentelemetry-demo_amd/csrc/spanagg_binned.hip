@@ -182,6 +182,7 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
 
   uint32_t n_zero = 0, n_badsvc = 0, n_oor = 0;  // wave-uniform (SGPR)
   uint32_t n_drop = 0;                           // per lane
+  uint32_t n_filt = 0;                           // per lane: HLL updates the lower-bound filter skipped
 #pragma unroll
   for (int j = 0; j < 2; ++j) pend.hoff[j] = pend.rho[j] = pend2.hoff[j] = pend2.rho[j] = 0;
   const uint32_t region = P.bt_region;
@@ -307,7 +308,11 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
       const uint32_t r = (uint32_t)__clzll((long long)((x << hp) | (1ULL << (hp - 1)))) + 1;
       const uint32_t ho = sk ? ((ws[j] * P.n_services + svc) << hp) + (uint32_t)(x >> (64 - hp)) : 0u;
       bool up = sk && !(MODE & 2);
-      if (lb_on) up = up && r > llb[ho >> lbs];
+      if (lb_on) {
+        const bool f = r <= llb[ho >> lbs];
+        n_filt += (up && f) ? 1u : 0u;
+        up = up && !f;
+      }
       rho[j] = up ? r : 0u;
       hoff[j] = up ? ho : 0u;
       m[j] = key * P.kmul;
@@ -429,7 +434,11 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
   const uint32_t nq = min(hq_n[0], kBtHq);
   for (uint32_t i = threadIdx.x; i < nq; i += kBtBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
   n_drop = wave_sum(n_drop);
+  n_filt = wave_sum(n_filt);
   if (lane == 0) {
+    // a slot per workgroup (same-address atomics from every wave would
+    // serialise the tail of the launch)
+    if (n_filt) atomicAdd(&P.hll_filt[blockIdx.x & (kFiltSlots - 1)], (unsigned long long)n_filt);
     if (n_zero) atomicAdd(&P.stats[kStatZeroKey], (unsigned long long)n_zero);
     if (n_badsvc) atomicAdd(&P.stats[kStatInvalidService], (unsigned long long)n_badsvc);
     if (n_oor) atomicAdd(&P.stats[kStatWindowOOR], (unsigned long long)n_oor);

@@ -84,6 +84,7 @@ struct sa_engine {
   // HLL lower bounds per sub-block of 2^lb_shift registers (IngestParams::hll_lb)
   uint8_t *hll_lb = nullptr;
   uint32_t lb_shift = 0, lb_n = 0, lb_seq = 0;
+  unsigned long long *hll_filt = nullptr;  // [kFiltSlots] filtered HLL updates per workgroup slot
   // exponential-histogram mode (cfg.exp_max_size > 0): the HBM-table path
   // runs the sketches, spanagg_expo.hip the histograms
   bool expo = false;
@@ -387,7 +388,8 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       (rc = alloc((void **)&e->cms, e->cms_slot_elems * W * 8)) ||
       (rc = alloc((void **)&e->errcnt, (size_t)W * e->cap * 8)) ||
       (rc = alloc((void **)&e->d_seeds, sizeof kCmsSeed)) ||
-      (rc = alloc((void **)&e->stats, 64)) || (rc = alloc((void **)&e->scratch, 64)))
+      (rc = alloc((void **)&e->stats, 64)) || (rc = alloc((void **)&e->scratch, 64)) ||
+      (rc = alloc((void **)&e->hll_filt, sa::kFiltSlots * 8)))
     return bail(rc);
   {
     // bound sub-blocks: as small as kLbMinShift allows within kLbMaxSub of them
@@ -475,7 +477,7 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->dbg, (void *)e->d_bins, (void *)e->errslab, (void *)e->part_rec,
                   (void *)e->part_fill, (void *)e->bt_rec, (void *)e->bt_cnt, (void *)e->base64, (void *)e->hll_lb,
                   (void *)e->expo_hdr, (void *)e->expo_buckets, (void *)e->expo_slot, (void *)e->expo_out_keys,
-                  (void *)e->expo_out_rows, (void *)e->expo_out_buckets,
+                  (void *)e->expo_out_rows, (void *)e->expo_out_buckets, (void *)e->hll_filt,
                   e->dstage[0], e->dstage[1]})
     if (p) (void)hipFree(p);
   for (int k = 0; k < 2; ++k) {
@@ -651,6 +653,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.lb_shift = e->lb_shift;
   P.lb_n = e->lb_n;  // read (and refreshed) by the v2 and binned kernels; the others ignore it
   P.lb_seq = e->lb_seq++;
+  P.hll_filt = e->hll_filt;
   hipError_t st;
   if (e->small) {
     st = sa::launch_ingest_small(P, grid, e->lds_bytes, s, e->variant);
@@ -756,11 +759,15 @@ int sa_ingest(sa_engine *e, const sa_span_batch *b) {
     char *d = static_cast<char *>(e->dstage[k]);
     if (m >= sa::kHostPageableMin) {
       // large chunks: the runtime's own staging of pageable memory copies
-      // faster than one host thread packing the pinned slot (and, as that,
-      // returns once the caller's bytes have been taken)
+      // faster than one host thread packing the pinned slot.  HIP does not
+      // promise that an asynchronous copy from pageable memory has taken the
+      // caller's bytes when it returns, so wait for these copies (not for the
+      // aggregation) before the caller may reuse or free its columns.
       for (int c = 0; c < 5; ++c)
         SA_HIP(e, hipMemcpyAsync(d + c * ms * 8, src[c], m * 8, hipMemcpyHostToDevice, e->stream));
       SA_HIP(e, hipMemcpyAsync(d + 5 * ms * 8, b->meta + off, m * 4, hipMemcpyHostToDevice, e->stream));
+      SA_HIP(e, hipEventRecord(e->ev_b, e->stream));
+      SA_HIP(e, hipEventSynchronize(e->ev_b));
     } else {
       for (int c = 0; c < 5; ++c) std::memcpy(h + c * ms * 8, src[c], m * 8);
       std::memcpy(h + 5 * ms * 8, b->meta + off, m * 4);
@@ -1120,6 +1127,12 @@ int sa_get_stats(sa_engine *e, sa_stats *o) {
   o->table_capacity = e->cap;
   o->window_base = e->win_base;
   o->small_table = e->small ? 1 : 0;
+  {
+    std::vector<uint64_t> f(sa::kFiltSlots);
+    SA_HIP(e, hipMemcpyAsync(f.data(), e->hll_filt, sa::kFiltSlots * 8, hipMemcpyDeviceToHost, e->stream));
+    SA_HIP(e, hipStreamSynchronize(e->stream));
+    o->hll_filtered = std::accumulate(f.begin(), f.end(), (uint64_t)0);
+  }
   return SA_OK;
 }
 

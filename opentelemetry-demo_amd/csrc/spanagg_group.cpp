@@ -44,6 +44,79 @@ __global__ void max_slices_u8(uint8_t *dst, const uint8_t *src, uint32_t n, uint
 
 uint32_t grid_for(uint64_t len) { return (uint32_t)std::min<uint64_t>((len + 255) / 256, 4096); }
 
+// ---- trace-id sharding (engine = trace_w1 % n) ------------------------------
+// trace_w1 % n from 32-bit remainders: w1 = hi * 2^32 + lo, so
+// w1 % n = ((hi % n) * (2^32 % n) + lo % n) % n (< n^2 <= 4096 before the
+// last remainder); no 64-bit division per span.
+__host__ __device__ inline uint32_t shard_of(uint64_t w1, uint32_t n, uint32_t r32) {
+  return (((uint32_t)(w1 >> 32) % n) * r32 + (uint32_t)w1 % n) % n;
+}
+
+constexpr uint32_t kMaxMembers = 64;
+
+// Spans per shard of a device batch (LDS counters, one global atomic per
+// shard per workgroup).
+__global__ __launch_bounds__(256) void shard_count_kernel(const uint64_t *w1, uint64_t n, uint32_t nm, uint32_t r32,
+                                                           unsigned long long *cnt) {
+  __shared__ uint32_t c[kMaxMembers];
+  if (threadIdx.x < kMaxMembers) c[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+    atomicAdd(&c[shard_of(w1[i], nm, r32)], 1u);
+  __syncthreads();
+  if (threadIdx.x < nm && c[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], (unsigned long long)c[threadIdx.x]);
+}
+
+// One member's packed shard (SoA v1 columns) in the partition staging buffer.
+struct ShardCols {
+  uint64_t *k, *s, *e, *a, *b;
+  uint32_t *m;
+};
+struct ShardArgs {  // by value (kernel argument segment): nm <= kMaxMembers
+  ShardCols c[kMaxMembers];
+};
+
+// Scatter: every wave takes 64 spans, and for each shard present among them
+// (a ballot) one lane reserves a run of the shard's positions (one global
+// atomic); the lanes of that shard write their span at consecutive positions.
+// Order inside a shard is not kept: every aggregate is order-independent
+// (integer sums and maxima).
+__global__ __launch_bounds__(256) void shard_scatter_kernel(sa_span_batch in, uint32_t nm, uint32_t r32,
+                                                             ShardArgs out, unsigned long long *cursor) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t n = in.n;
+  for (uint64_t i0 = blockIdx.x * 256ull + (threadIdx.x & ~63u); i0 < n; i0 += (uint64_t)gridDim.x * 256) {
+    const uint64_t i = i0 + lane;
+    const bool ok = i < n;
+    const uint64_t k = ok ? in.key_hash[i] : 0, s = ok ? in.start_ns[i] : 0, e = ok ? in.end_ns[i] : 0;
+    const uint64_t a = ok ? in.trace_w0[i] : 0, b = ok ? in.trace_w1[i] : 0;
+    const uint32_t m = ok ? in.meta[i] : 0;
+    const uint32_t sh = ok ? shard_of(b, nm, r32) : 0xFFFFFFFFu;
+    uint64_t pending = __ballot(ok);
+    while (pending) {
+      const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)sh, __builtin_ctzll(pending));
+      const uint64_t mj = __ballot(sh == j);
+      pending &= ~mj;
+      const int leader = __builtin_ctzll(mj);
+      unsigned long long base = 0;
+      if ((int)lane == leader) base = atomicAdd(&cursor[j], (unsigned long long)__popcll(mj));
+      const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, leader);
+      const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(base >> 32), leader);
+      if (sh == j) {
+        const uint64_t pos = (((uint64_t)bhi << 32) | blo) +
+                             __builtin_amdgcn_mbcnt_hi((uint32_t)(mj >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mj, 0u));
+        const ShardCols &c = out.c[j];
+        c.k[pos] = k;
+        c.s[pos] = s;
+        c.e[pos] = e;
+        c.a[pos] = a;
+        c.b[pos] = b;
+        c.m[pos] = m;
+      }
+    }
+  }
+}
+
 // Device buffer on one member's device, grown on demand.
 struct Buf {
   void *p = nullptr;
@@ -62,6 +135,21 @@ struct sa_group {
   std::vector<ncclComm_t> comm;
   std::vector<Buf> keys, gath, uni, rows, hll, cms;
   Buf stack;  // member 0's device: every member's slice for the copy-path reduce
+  // sa_group_ingest_device: two staging sets (a call waits only for the
+  // members' use of the set two calls back).  part[k][i]: set k's packed
+  // shards on member i's device when that device partitions (the source),
+  // peer[k][i]: member i's shard copied to its own device; ev_scat[k][i]
+  // (device i) marks the partition of set k, ev_done[k][i] member i's ingest
+  // of it.
+  int pset = 0;
+  Buf part[2][kMaxMembers], peer[2][kMaxMembers];
+  hipEvent_t ev_scat[2][kMaxMembers] = {}, ev_done[2][kMaxMembers] = {};
+  bool done_used[2][kMaxMembers] = {};
+  std::vector<Buf> pcnt;                 // [n] shard counters / cursors (2 x nm u64) per source device
+  unsigned long long *hcnt = nullptr;    // pinned host copy of the counts
+  // sa_group_ingest: per-member packed host shards, reused across calls
+  std::vector<std::vector<uint64_t>> hcol;
+  std::vector<std::vector<uint32_t>> hmeta;
   std::vector<uint64_t> dropped_seen;
   uint32_t nbk = 0;
   size_t hll_bytes = 0, cms_elems = 0;
@@ -193,7 +281,7 @@ extern "C" {
 int sa_group_create(const sa_config *cfg, const int32_t *devices, uint32_t n, sa_group **out) {
   if (!out) return SA_EINVAL;
   *out = nullptr;
-  if (!cfg || !devices || n == 0 || n > 64) return SA_EINVAL;
+  if (!cfg || !devices || n == 0 || n > kMaxMembers) return SA_EINVAL;
   auto *g = new sa_group();
   g->cfg = *cfg;
   g->bounds.assign(cfg->bounds, cfg->bounds + cfg->n_bounds);
@@ -226,6 +314,25 @@ int sa_group_create(const sa_config *cfg, const int32_t *devices, uint32_t n, sa
   g->hll.resize(n);
   g->cms.resize(n);
   g->dropped_seen.assign(n, 0);
+  g->pcnt.resize(n);
+  g->hcol.resize(n);
+  g->hmeta.resize(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (hipSetDevice(devices[i]) != hipSuccess) {
+      sa_group_destroy(g);
+      return SA_EDEVICE;
+    }
+    for (int k = 0; k < 2; ++k)
+      if (hipEventCreateWithFlags(&g->ev_scat[k][i], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&g->ev_done[k][i], hipEventDisableTiming) != hipSuccess) {
+        sa_group_destroy(g);
+        return SA_EDEVICE;
+      }
+  }
+  if (hipHostMalloc((void **)&g->hcnt, kMaxMembers * 8, hipHostMallocDefault) != hipSuccess) {
+    sa_group_destroy(g);
+    return SA_ENOMEM;
+  }
   // RCCL over distinct devices (a communicator cannot hold two ranks of one
   // device); a group of one uses it only when SPANAGG_GROUP_RCCL=1 asks
   std::vector<int> sorted(g->dev);
@@ -256,11 +363,18 @@ void sa_group_destroy(sa_group *g) {
       (void)hipStreamSynchronize(g->st[i]);
       (void)hipStreamDestroy(g->st[i]);
     }
-    for (std::vector<Buf> *v : {&g->keys, &g->gath, &g->uni, &g->rows, &g->hll, &g->cms})
+    for (std::vector<Buf> *v : {&g->keys, &g->gath, &g->uni, &g->rows, &g->hll, &g->cms, &g->pcnt})
       if (i < v->size() && (*v)[i].p) (void)hipFree((*v)[i].p);
+    for (int k = 0; k < 2; ++k) {
+      if (i < kMaxMembers && g->part[k][i].p) (void)hipFree(g->part[k][i].p);
+      if (i < kMaxMembers && g->peer[k][i].p) (void)hipFree(g->peer[k][i].p);
+      if (g->ev_scat[k][i]) (void)hipEventDestroy(g->ev_scat[k][i]);
+      if (g->ev_done[k][i]) (void)hipEventDestroy(g->ev_done[k][i]);
+    }
     if (i == 0 && g->stack.p) (void)hipFree(g->stack.p);
     sa_destroy(g->eng[i]);
   }
+  if (g->hcnt) (void)hipHostFree(g->hcnt);
   delete g;
 }
 
@@ -269,6 +383,12 @@ uint32_t sa_group_size(const sa_group *g) { return g ? (uint32_t)g->eng.size() :
 int sa_group_uses_rccl(const sa_group *g) { return g && g->rccl ? 1 : 0; }
 sa_engine *sa_group_member(sa_group *g, uint32_t i) { return g && i < g->eng.size() ? g->eng[i] : nullptr; }
 
+// Host batch.  One pass computes every span's shard (worker threads over
+// contiguous chunks, per-chunk shard counts); the prefix over chunks gives
+// each chunk's write position in every member's packed shard; a second pass
+// gathers the spans there (the same threads); then each member ingests its
+// shard (sa_ingest copies it out before returning, so the shard buffers are
+// reused by the next call).
 int sa_group_ingest(sa_group *g, const sa_span_batch *b) {
   if (!g || !b) return SA_EINVAL;
   const uint32_t n = (uint32_t)g->eng.size();
@@ -278,32 +398,143 @@ int sa_group_ingest(sa_group *g, const sa_span_batch *b) {
   }
   if (!b->key_hash || !b->start_ns || !b->end_ns || !b->trace_w0 || !b->trace_w1 || !b->meta)
     return gfail(g, SA_EINVAL, "null batch column");
-  // one host thread per member: it scans the batch for its trace-id shard
-  // (trace_w1 % n), packs the shard's columns and ingests them
+  const uint64_t N = b->n;
+  const uint32_t r32 = (uint32_t)((1ULL << 32) % n);
+  const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+  const uint32_t T = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)std::min(hw, 16u), N / 65536 + 1}));
+  const uint64_t per = (N + T - 1) / T;
+  std::vector<uint8_t> sid(N);
+  std::vector<uint64_t> cnt((size_t)T * n, 0);
+  auto run = [&](auto &&fn) {
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < T; ++t) th.emplace_back(fn, t);
+    fn(0u);
+    for (auto &x : th) x.join();
+  };
+  run([&](uint32_t t) {  // 1. shard ids and per-chunk counts
+    const uint64_t a = std::min(N, t * per), z = std::min(N, a + per);
+    uint64_t *c = cnt.data() + (size_t)t * n;
+    for (uint64_t j = a; j < z; ++j) {
+      const uint32_t sh = shard_of(b->trace_w1[j], n, r32);
+      sid[j] = (uint8_t)sh;
+      ++c[sh];
+    }
+  });
+  std::vector<uint64_t> total(n, 0), off((size_t)T * n);
+  for (uint32_t i = 0; i < n; ++i)
+    for (uint32_t t = 0; t < T; ++t) {
+      off[(size_t)t * n + i] = total[i];
+      total[i] += cnt[(size_t)t * n + i];
+    }
+  for (uint32_t i = 0; i < n; ++i) {
+    if (g->hcol[i].size() < total[i] * 5) g->hcol[i].resize(total[i] * 5);
+    if (g->hmeta[i].size() < total[i]) g->hmeta[i].resize(total[i]);
+  }
+  run([&](uint32_t t) {  // 2. gather into the packed shards
+    const uint64_t a = std::min(N, t * per), z = std::min(N, a + per);
+    std::vector<uint64_t> o(off.begin() + (size_t)t * n, off.begin() + (size_t)(t + 1) * n);
+    for (uint64_t j = a; j < z; ++j) {
+      const uint32_t i = sid[j];
+      const uint64_t p = o[i]++, cap = total[i];
+      uint64_t *c = g->hcol[i].data();
+      c[p] = b->key_hash[j];
+      c[cap + p] = b->start_ns[j];
+      c[2 * cap + p] = b->end_ns[j];
+      c[3 * cap + p] = b->trace_w0[j];
+      c[4 * cap + p] = b->trace_w1[j];
+      g->hmeta[i][p] = b->meta[j];
+    }
+  });
   std::vector<int> rcs(n, SA_OK);
   std::vector<std::thread> th;
-  for (uint32_t i = 0; i < n; ++i) {
+  for (uint32_t i = 0; i < n; ++i) {  // 3. members ingest their shards
+    if (!total[i]) continue;
     th.emplace_back([&, i]() {
-      std::vector<uint64_t> k, s, e, a, c;
-      std::vector<uint32_t> m;
-      const size_t guess = b->n / n + b->n / (4 * n) + 64;
-      k.reserve(guess), s.reserve(guess), e.reserve(guess), a.reserve(guess), c.reserve(guess), m.reserve(guess);
-      for (uint64_t j = 0; j < b->n; ++j) {
-        if (b->trace_w1[j] % n != i) continue;
-        k.push_back(b->key_hash[j]);
-        s.push_back(b->start_ns[j]);
-        e.push_back(b->end_ns[j]);
-        a.push_back(b->trace_w0[j]);
-        c.push_back(b->trace_w1[j]);
-        m.push_back(b->meta[j]);
-      }
-      const sa_span_batch sh{k.data(), s.data(), e.data(), a.data(), c.data(), m.data(), k.size()};
-      rcs[i] = sh.n ? sa_ingest(g->eng[i], &sh) : SA_OK;
+      const uint64_t cap = total[i];
+      const uint64_t *c = g->hcol[i].data();
+      const sa_span_batch sh{c, c + cap, c + 2 * cap, c + 3 * cap, c + 4 * cap, g->hmeta[i].data(), cap};
+      rcs[i] = sa_ingest(g->eng[i], &sh);
     });
   }
-  for (auto &t : th) t.join();
+  for (auto &x : th) x.join();
   for (uint32_t i = 0; i < n; ++i)
     if (rcs[i] != SA_OK) return member_error(g, i, rcs[i], "sa_ingest");
+  return SA_OK;
+}
+
+int sa_group_ingest_device(sa_group *g, const sa_span_batch *b, uint32_t src, void *stream) {
+  if (!g || !b) return SA_EINVAL;
+  const uint32_t n = (uint32_t)g->eng.size();
+  if (src >= n) return gfail(g, SA_EINVAL, "source member out of range");
+  if (b->n == 0) return SA_OK;
+  if (!b->key_hash || !b->start_ns || !b->end_ns || !b->trace_w0 || !b->trace_w1 || !b->meta)
+    return gfail(g, SA_EINVAL, "null batch column");
+  const int sdev = g->dev[src];
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : g->st[src];
+  if (n == 1) {
+    const int rc = sa_ingest_device(g->eng[0], b, s);
+    return rc ? member_error(g, 0, rc, "sa_ingest_device") : SA_OK;
+  }
+  const uint32_t r32 = (uint32_t)((1ULL << 32) % n);
+  const int k = g->pset;
+  g->pset ^= 1;
+  SG_HIP(g, hipSetDevice(sdev));
+  // the staging set's previous users (each member's ingest of it) are done
+  for (uint32_t i = 0; i < n; ++i)
+    if (g->done_used[k][i]) SG_HIP(g, hipStreamWaitEvent(s, g->ev_done[k][i], 0));
+  // 1. shard sizes
+  if (int rc = ensure(g, sdev, g->pcnt[src], 2 * kMaxMembers * 8)) return rc;
+  unsigned long long *dcnt = static_cast<unsigned long long *>(g->pcnt[src].p), *dcur = dcnt + kMaxMembers;
+  SG_HIP(g, hipMemsetAsync(dcnt, 0, 2 * kMaxMembers * 8, s));
+  hipLaunchKernelGGL(shard_count_kernel, dim3(grid_for(b->n)), dim3(256), 0, s, b->trace_w1, b->n, n, r32, dcnt);
+  SG_HIP(g, hipGetLastError());
+  SG_HIP(g, hipMemcpyAsync(g->hcnt, dcnt, n * 8, hipMemcpyDeviceToHost, s));
+  SG_HIP(g, hipStreamSynchronize(s));
+  std::vector<uint64_t> cnt(g->hcnt, g->hcnt + n), cap(n);
+  size_t bytes = 0;
+  std::vector<size_t> at(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    cap[i] = (cnt[i] + 1) & ~1ULL;  // even: every u64 column stays 16-B aligned
+    at[i] = bytes;
+    bytes += cap[i] * 44 + 64;
+    bytes = (bytes + 255) & ~(size_t)255;
+  }
+  // 2. scatter into the packed shards (set k on the source device)
+  if (int rc = ensure(g, sdev, g->part[k][src], bytes)) return rc;
+  char *base = static_cast<char *>(g->part[k][src].p);
+  ShardArgs args{};
+  for (uint32_t i = 0; i < n; ++i) {
+    uint64_t *c = reinterpret_cast<uint64_t *>(base + at[i]);
+    args.c[i] = ShardCols{c, c + cap[i], c + 2 * cap[i], c + 3 * cap[i], c + 4 * cap[i],
+                          reinterpret_cast<uint32_t *>(c + 5 * cap[i])};
+  }
+  hipLaunchKernelGGL(shard_scatter_kernel, dim3(grid_for(b->n)), dim3(256), 0, s, *b, n, r32, args, dcur);
+  SG_HIP(g, hipGetLastError());
+  SG_HIP(g, hipEventRecord(g->ev_scat[k][src], s));
+  // 3. every member ingests its shard on its own stream (peer copy first when
+  //    it lives on another device)
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!cnt[i]) continue;
+    const int d = g->dev[i];
+    SG_HIP(g, hipSetDevice(d));
+    hipStream_t ms = g->st[i];
+    SG_HIP(g, hipStreamWaitEvent(ms, g->ev_scat[k][src], 0));
+    const ShardCols &c0 = args.c[i];
+    ShardCols c = c0;
+    if (d != sdev) {
+      const size_t sb = cap[i] * 44;
+      if (int rc = ensure(g, d, g->peer[k][i], sb)) return rc;
+      SG_HIP(g, hipMemcpyPeerAsync(g->peer[k][i].p, d, c0.k, sdev, sb, ms));
+      uint64_t *p = static_cast<uint64_t *>(g->peer[k][i].p);
+      c = ShardCols{p, p + cap[i], p + 2 * cap[i], p + 3 * cap[i], p + 4 * cap[i],
+                    reinterpret_cast<uint32_t *>(p + 5 * cap[i])};
+    }
+    const sa_span_batch sh{c.k, c.s, c.e, c.a, c.b, c.m, cnt[i]};
+    if (int rc = sa_ingest_device(g->eng[i], &sh, ms)) return member_error(g, i, rc, "sa_ingest_device");
+    SG_HIP(g, hipSetDevice(d));
+    SG_HIP(g, hipEventRecord(g->ev_done[k][i], ms));
+    g->done_used[k][i] = true;
+  }
   return SA_OK;
 }
 
@@ -565,6 +796,7 @@ int sa_group_get_stats(sa_group *g, sa_stats *o) {
     o->dropped_table_full += s.dropped_table_full;
     o->n_keys += s.n_keys;
     o->table_capacity += s.table_capacity;
+    o->hll_filtered += s.hll_filtered;
     if (i == 0) {
       o->window_base = s.window_base;
       o->small_table = s.small_table;

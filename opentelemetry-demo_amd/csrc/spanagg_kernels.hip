@@ -507,8 +507,10 @@ __device__ __forceinline__ bool lds_err_add(uint32_t *etab, uint32_t ek) {
 // does not wait behind the other waves' first tiles; bit 1 = claims of one
 // wave tile instead of NBUF (a round takes NBUF claims), halving the work a
 // wave can still hold when its neighbours run out.
+// LEAN: the span hash on 32-bit halves (xxh64_16_h), rho / register index
+// without 64-bit shifts, the register row offset by a 24-bit multiply.
 template <int S, int NBUF, int AUX, bool DIAG, int LC = 0, int NWC = 0, int PC = 0, int HAUX = -1,
-          bool DYN = false, int OPT = 0, bool EPI = false>
+          bool DYN = false, int OPT = 0, bool EPI = false, bool LEAN = false>
 __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 0] = __builtin_amdgcn_s_memrealtime();
@@ -610,6 +612,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   if (threadIdx.x == 0) {
     hq_n[0] = 0;
     hq_n[1] = (kTileClaims ? 2u * NBUF : 2u) * kWaves;  // DYN: next unclaimed chunk of this workgroup's range
+    hq_n[2] = 0;  // EPI: HLL updates the lower-bound filter skipped (summed over the waves)
   }
   if (threadIdx.x < 4) lstat[threadIdx.x] = 0;
   {
@@ -639,6 +642,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   unsigned long long hot_sum = 0;
   // wave-uniform event counts (scalar registers)
   uint32_t n_zero = 0, n_badsvc = 0, n_oor = 0, n_drop = 0;
+  uint32_t n_filt = 0;  // per lane: HLL updates the lower-bound filter skipped (EPI builds)
 #pragma unroll
   for (int j = 0; j < S; ++j) pend.hoff[j] = pend.rho[j] = 0;
 
@@ -677,7 +681,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
       const uint32_t meta = copy_u32(T.meta[j]);  // see key
       const uint32_t svc = meta & 0xFFFFu;
       const bool svc_ok = svc < P.n_services;
-      ws[j] = (diag & 64u) ? (uint32_t)(T.e[j] >> 34) & 7u : window_slot(P, T.e[j]);
+      ws[j] = (diag & 64u) ? (uint32_t)(T.e[j] >> 34) & 7u : LEAN ? window_slot_lean(P, T.e[j]) : window_slot(P, T.e[j]);
       const bool win_ok = ws[j] != 0xFFFFFFFFu;
       if (!(diag & 128u)) {
         if constexpr (EPI) {
@@ -700,12 +704,27 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
       rho[j] = 0;
       hoff[j] = 0;
       if (!(diag & 2u)) {
-        // diag 16384: one 64-bit multiply instead of xxh64 (prices the hash's VALU)
-        const uint64_t x = (DIAG && (diag & 16384u)) ? (T.a[j] ^ T.b[j]) * XP1 : xxh64_16(T.a[j], T.b[j]);
-        const uint32_t r = (uint32_t)__clzll((long long)((x << hp) | (1ULL << (hp - 1)))) + 1;
-        const uint32_t ho = sk ? ((ws[j] * P.n_services + svc) << hp) + (uint32_t)(x >> (64 - hp)) : 0u;
+        uint32_t r, idx, row;
+        if constexpr (LEAN) {
+          const H64 x = xxh64_16_h(T.a[j], T.b[j]);
+          const uint32_t yh = __builtin_amdgcn_alignbit(x.hi, x.lo, 32 - hp);  // (x << hp) >> 32
+          const uint32_t yl = (x.lo << hp) | (1u << (hp - 1));
+          r = (uint32_t)__clzll((long long)(((uint64_t)yh << 32) | yl)) + 1;  // 2 x v_ffbh, no 64-bit shift
+          idx = x.hi >> (32 - hp);
+          // ws < 2^12, n_services <= 2^16: a 24-bit multiply-add (LLVM picks
+          // the quarter-rate v_mad_u64_u32 for the plain expression)
+          asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(row) : "v"(ws[j]), "s"(P.n_services), "v"(svc));
+        } else {
+          // diag 16384: one 64-bit multiply instead of xxh64 (prices the hash's VALU)
+          const uint64_t x = (DIAG && (diag & 16384u)) ? (T.a[j] ^ T.b[j]) * XP1 : xxh64_16(T.a[j], T.b[j]);
+          r = (uint32_t)__clzll((long long)((x << hp) | (1ULL << (hp - 1)))) + 1;
+          idx = (uint32_t)(x >> (64 - hp));
+          row = ws[j] * P.n_services + svc;
+        }
+        const uint32_t ho = sk ? (row << hp) + idx : 0u;
         // a rho at or below the register sub-block's lower bound cannot raise it
         const bool up = sk && !(lb_on && r <= llb[ho >> P.lb_shift]);
+        if constexpr (EPI) n_filt += (sk && !up) ? 1u : 0u;
         rho[j] = up ? r : 0u;
         hoff[j] = up ? ho : 0u;
       }
@@ -883,6 +902,10 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
                  ((unsigned long long)(uint32_t)__shfl_xor((int)(uint32_t)(hot_sum >> 32), o, 64) << 32);
     if ((threadIdx.x & 63u) == 0 && hot_sum) atomicAdd(&lsum[hot_slot], hot_sum);
   }
+  if constexpr (EPI) {  // one LDS add per wave; one global add per workgroup after the epilogue
+    n_filt = wave_sum(n_filt);
+    if ((threadIdx.x & 63) == 0 && n_filt) atomicAdd(&hq_n[2], n_filt);
+  }
   const uint64_t wave_loop_end = DIAG && P.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 2] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
@@ -915,6 +938,9 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
       constexpr uint32_t kIdx[4] = {kStatZeroKey, kStatInvalidService, kStatWindowOOR, kStatDropped};
       atomicAdd(&P.stats[kIdx[threadIdx.x]], (unsigned long long)lstat[threadIdx.x]);
     }
+    // (a slot per workgroup: thousands of same-address atomics at the end of
+    // every launch would serialise its tail)
+    if (threadIdx.x == 0 && hq_n[2]) atomicAdd(&P.hll_filt[blockIdx.x & (kFiltSlots - 1)], (unsigned long long)hq_n[2]);
   }
   if ((threadIdx.x & 63) == 0) {
     if (n_zero) atomicAdd(&P.stats[kStatZeroKey], (unsigned long long)n_zero);
@@ -1555,6 +1581,7 @@ static const void *small_fn(bool bt, int v, bool diag) {
       case 17: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 3>;
       case 18: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 2>;
       case 19: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1, true>;
+      case 20: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1, true, true>;
       default: return (const void *)&ingest_v2_kernel<2, 2, 2, false>;
     }
   }
@@ -1602,6 +1629,8 @@ hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_
   if ((variant == 12 || variant == 13 || variant >= 14) &&
       !(P.log2cap == 11 && (P.nbk + 1) / 2 == 9 && P.p == 14))
     variant = variant == 12 ? 8 : variant == 13 ? 11 : 15;
+  // the lean window quotient needs window_ns < 2^56 (its high word is a 24-bit multiplier)
+  if (variant == 20 && (P.window_ns >> 56)) variant = 19;
   const void *fn = small_fn(P.bintab != nullptr, variant, P.diag != 0 || P.dbg != nullptr);
   void *args[] = {const_cast<IngestParams *>(&P)};
   return hipLaunchKernel(fn, dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);

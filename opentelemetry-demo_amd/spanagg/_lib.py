@@ -75,7 +75,7 @@ class sa_stats(C.Structure):
         ("spans", C.c_uint64), ("zero_key", C.c_uint64), ("invalid_service", C.c_uint64),
         ("window_out_of_range", C.c_uint64), ("dropped_table_full", C.c_uint64),
         ("n_keys", C.c_uint64), ("table_capacity", C.c_uint64), ("window_base", C.c_uint64),
-        ("small_table", C.c_uint32), ("pad", C.c_uint32),
+        ("small_table", C.c_uint32), ("pad", C.c_uint32), ("hll_filtered", C.c_uint64),
     ]
 
 
@@ -110,6 +110,7 @@ SIGNATURES = [
     ("sa_group_uses_rccl", C.c_int, [C.c_void_p]),
     ("sa_group_member", C.c_void_p, [C.c_void_p, C.c_uint32]),
     ("sa_group_ingest", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch)]),
+    ("sa_group_ingest_device", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch), C.c_uint32, C.c_void_p]),
     ("sa_group_sync", C.c_int, [C.c_void_p]),
     ("sa_group_flush", C.c_int, [C.c_void_p, C.POINTER(C.POINTER(sa_red_result))]),
     ("sa_group_flush_exp", C.c_int, [C.c_void_p, C.POINTER(C.POINTER(sa_exp_result))]),
@@ -120,6 +121,8 @@ SIGNATURES = [
     ("sa_bucket_thresholds", C.c_int, [f64p, C.c_uint32, C.c_uint32, u64p, u32p]),
     ("sa_hll_estimate", C.c_double, [u8p, C.c_uint32]),
 ]
+
+ABI_VERSION = 3  # include/spanagg.h SA_ABI_VERSION
 
 _lib = None
 
@@ -149,7 +152,7 @@ def load() -> C.CDLL:
                 raise RuntimeError(f"libspanagg.so does not export {name}")
             fn.restype = res
             fn.argtypes = args
-        if lib.sa_abi_version() != 2:
+        if lib.sa_abi_version() != ABI_VERSION:
             raise RuntimeError("libspanagg ABI version mismatch")
         _lib = lib
     return _lib

@@ -379,6 +379,17 @@ class Group:
         b = _lib.sa_span_batch(*[c.ctypes.data for c in batch.columns()], len(batch))
         self._check(self.lib.sa_group_ingest(self._h, C.byref(b)), "sa_group_ingest")
 
+    def ingest_device(self, key, start, end, w0, w1, meta, n: Optional[int] = None, src: int = 0,
+                      stream: Optional[int] = None):
+        """sa_group_ingest_device: a batch in HBM of member `src`'s device
+        (torch tensors or raw device pointers), partitioned by trace id on
+        that device and ingested by every member on its own stream."""
+        if n is None:
+            n = int(key.numel())
+        b = _lib.sa_span_batch(_ptr(key), _ptr(start), _ptr(end), _ptr(w0), _ptr(w1), _ptr(meta), n)
+        self._check(self.lib.sa_group_ingest_device(self._h, C.byref(b), int(src), C.c_void_p(stream or 0)),
+                    "sa_group_ingest_device")
+
     def sync(self):
         self._check(self.lib.sa_group_sync(self._h), "sa_group_sync")
 

@@ -31,7 +31,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _lib.load().sa_abi_version() == 2
+    assert _lib.load().sa_abi_version() == 3
 
 
 def test_config_default_matches_connector_defaults():

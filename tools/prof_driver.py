@@ -1,11 +1,15 @@
 #!/usr/bin/env python3
 """Profiling driver: N ingest launches of the C2 10M-span batch (device-resident)
-with the library / variant selected by SPANAGG_LIB / SPANAGG_VARIANT."""
+with the library / variant selected by SPANAGG_LIB / SPANAGG_VARIANT.  Every
+launch aggregates a distinct trace-id variant of the batch (bench.py's
+trace_variants; PROF_FRESH=0: the same trace ids every launch), so the last
+launches of a long run are in the regime bench.py times."""
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "opentelemetry-demo_amd"))
+sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -26,11 +30,18 @@ else:
 cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).cuda()
         for c in batch.columns()]
 s = torch.cuda.Stream()
+s.wait_stream(torch.cuda.current_stream())
 flags = int(os.environ.get("PROF_FLAGS", 0))
+if os.environ.get("PROF_FRESH", "1") != "0":
+    from bench import trace_variants
+    variants = trace_variants(cols[3], cols[4], reps, seed=1000)
+else:
+    variants = [(cols[3], cols[4])] * reps
+torch.cuda.synchronize()
 with Engine(Config(n_services=n_services, n_windows=16, flags=flags, key_capacity=kcap)) as e:
     e.window_advance(first)
-    for _ in range(reps):
-        e.ingest_device(*cols, n=n, stream=s.cuda_stream)
+    for w0, w1 in variants:
+        e.ingest_device(cols[0], cols[1], cols[2], w0, w1, cols[5], n=n, stream=s.cuda_stream)
     torch.cuda.synchronize()
     r = e.flush()
     print("calls", int(r.calls.sum()), "expected", reps * n)

@@ -10,7 +10,16 @@ MI355X_MICROARCH.md's gfx950 correction, KB = 1024 B.
 import collections
 import csv
 import json
+import os
 import sys
+
+
+def _pick(ids):
+    """Dispatches averaged: the last PMC_LAST of them (the settled regime of a
+    fresh-variant run), else all but the first."""
+    k = int(os.environ.get("PMC_LAST", "0"))
+    return ids[-k:] if k else (ids[1:] or ids)
+
 
 HOT = ("ingest", "bt_scatter", "bt_aggregate")
 
@@ -24,7 +33,7 @@ def per_launch(path, counter):
             d[short][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
     total, kernels = 0.0, {}
     for name, per in d.items():
-        ids = sorted(per)[1:] or sorted(per)
+        ids = _pick(sorted(per))
         kernels[name] = sum(per[i] for i in ids) / len(ids)
         total += kernels[name]
     return total, kernels
