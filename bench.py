@@ -231,6 +231,9 @@ WORKLOADS = {
            "key table, HLL + count-min; a fresh trace-id set every step"),
     "c4zipf": ("C4 Zipf: 1,000,000 series (2,000 http.route x 500 k8s.pod.name), Zipf(s=1.1) over keys, "
                "binned HBM key table, HLL + count-min; a fresh trace-id set every step"),
+    "c2expo": ("C2 with histogram.exponential (max_size 160): the C2 spans, per-series go-expohisto "
+               "histograms (small-table kernel in EXPO mode + slab reduce/rescale + LDS-cached bucket "
+               "counts), HLL + count-min; a fresh trace-id set every step"),
 }
 
 
@@ -246,7 +249,8 @@ def run_workload(name, n, args, device, rank, world, barrier):
     from spanagg import Config, Engine
     from spanagg.synth import generate_c2, generate_highcard
 
-    if name == "c2":
+    exp_max = 160 if name == "c2expo" else 0
+    if name in ("c2", "c2expo"):
         wl = generate_c2(n, seed=42 + rank)
         batch, first_window, n_services, key_capacity = wl.batch, wl.first_window, wl.n_services, 1500
     else:
@@ -263,7 +267,7 @@ def run_workload(name, n, args, device, rank, world, barrier):
         for _, vw1 in variants[:2]:
             assert (shard_of(vw1[:4096].cpu().numpy().view(np.uint64), world) == rank).all()
     eng = Engine(Config(n_services=max(n_services, 1), n_windows=16, key_capacity=key_capacity,
-                        device=device.index))
+                        device=device.index, exp_max_size=exp_max))
     eng.window_advance(first_window)
     streams = [torch.cuda.Stream(device) for _ in range(max(1, args.streams))]
     stream = streams[0]
@@ -367,11 +371,12 @@ def run_workload(name, n, args, device, rank, world, barrier):
         red = merge_red(part, reset=True)
         merge_window(part, first_window + 1)
     else:
-        red = eng.flush()
+        red = eng.flush_exp() if exp_max else eng.flush()
     torch.cuda.synchronize(device)
     merge_ms = (time.perf_counter() - tm) * 1e3
     st = eng.stats()
-    calls_ok = int(red.calls.sum()) == launches[0] * n * world - st["zero_key"] * (1 if world == 1 else world)
+    calls = int(red.count.sum()) if exp_max else int(red.calls.sum())
+    calls_ok = calls == launches[0] * n * world - st["zero_key"] * (1 if world == 1 else world)
     # the whole window from its cold start: cold + settling launches (HIP
     # events, one by one) + the timed steps (wall clock); the warm-up and the
     # isolated kernel-time launches in between are left out
@@ -478,6 +483,7 @@ def roofline(name, n, r, traffic_path=None):
     traffic, tsrc = load_traffic(tpath, name)
     piped = BYTES_PER_SPAN * n / (r["device_ms"] * 1e-3) / 1e9
     kern = {"c2": "ingest_v2_kernel (spanagg_kernels.hip)",
+            "c2expo": "ingest_v2_kernel EXPO mode + expo_reduce_rescale_kernel + expo_count_cached_kernel",
             "c4": "bt_scatter2_kernel + bt_aggregate2_kernel (spanagg_binned.hip)",
             "c4zipf": "bt_scatter2_kernel + bt_aggregate2_kernel (spanagg_binned.hip)"}[name]
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -511,7 +517,7 @@ def main():
                     help="untimed launches after the cold one, before the warm-up (HLL registers settle)")
     ap.add_argument("--variants", type=int, default=128,
                     help="distinct trace-id variants of the batch (one per launch up to this many)")
-    ap.add_argument("--sub", default="c4,c4zipf",
+    ap.add_argument("--sub", default="c4,c4zipf,c2expo",
                     help="extra workloads reported as sub-objects of the line at N=1 ('' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--h2d-reps", type=int, default=5,

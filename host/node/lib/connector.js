@@ -358,11 +358,37 @@ class SpanMetricsConnector {
    * (columnizer_threads) and committed in order, so the ids, dictionary and
    * columns are those of consumeTraces called on each in turn.  Returns one
    * entry per request: null, or the Error consumeTraces would have thrown.
+   * Never throws past the first request: when the columnizer or the engine
+   * fails part-way, the requests already applied keep null and only the rest
+   * get the error (a sender that retries them counts nothing twice).  An
+   * engine error is marked `deferred`: the engine runs asynchronously, so it
+   * may come from columns of earlier requests.
    */
   consumeTracesBatch(reqs) {
     if (!this.handle) throw new Error('connector is shut down');
     const errs = new Array(reqs.length).fill(null);
     let i = 0;
+    try {
+      i = this._consumeBatchFrom(reqs, errs);
+    } catch (e) {
+      i = e.batchAt !== undefined ? e.batchAt : 0;
+      for (let j = i; j < reqs.length; j++) errs[j] = e;
+    }
+    return errs;
+  }
+
+  /**
+   * consumeTracesBatch's loop; a throw carries `batchAt`, the first request
+   * not aggregated: on a columnizer failure the first one not applied, on an
+   * engine failure the first one whose spans were in the failed columns (the
+   * requests since the last successful drain of this batch).
+   */
+  _consumeBatchFrom(reqs, errs) {
+    let i = 0, pendFrom = 0;
+    const at = (e, k) => {
+      if (e && typeof e === 'object' && e.batchAt === undefined) e.batchAt = k;
+      return e;
+    };
     while (i < reqs.length) {
       const isBytes = Buffer.isBuffer(reqs[i]) || reqs[i] instanceof Uint8Array;
       if (!isBytes || !this.col) {
@@ -374,7 +400,12 @@ class SpanMetricsConnector {
       for (let j = i; j < reqs.length && (Buffer.isBuffer(reqs[j]) || reqs[j] instanceof Uint8Array); j++) {
         bufs.push(asBuffer(reqs[j]));
       }
-      const br = this.addon.columnizeBatch(this.col, bufs);
+      let br;
+      try {
+        br = this.addon.columnizeBatch(this.col, bufs);
+      } catch (e) {
+        throw at(e, i);
+      }
       for (let k = 0; k < br.done; k++) {
         try {
           if (!this._applyNative(br.results[k], bufs[k])) this._consumeJs(otlp.decodeTraces(bufs[k]));
@@ -384,10 +415,20 @@ class SpanMetricsConnector {
       }
       if (br.maxEnd > this.nativeMaxEnd) this.nativeMaxEnd = br.maxEnd;
       this.nativeBuffered = br.buffered;
-      if (br.buffered >= this.cols.cap) this._drain();
       i += br.done;
+      if (br.buffered >= this.cols.cap) {
+        try {
+          this._drain();
+        } catch (e) {
+          // the engine runs asynchronously: the error may also concern
+          // columns of earlier batches, already acknowledged
+          e.deferred = true;
+          throw at(e, pendFrom);
+        }
+        pendFrom = i;
+      }
     }
-    return errs;
+    return i;
   }
 
   /** The JavaScript columnizer over a decoded request. */

@@ -636,6 +636,32 @@ test('pipeline constructor (README / INTEGRATION demo path) applies the demo tra
   none.connector.shutdown();
 });
 
+test('consumeTracesBatch: a failure part-way rejects only the requests not yet applied', () => {
+  const addon = new NativeColumnizerFakeAddon();
+  let drains = 0;
+  addon.columnizerIngest = (c) => {  // the engine fails on its second batch of columns
+    drains += 1;
+    const b = addon.real.columnizerTake(c);
+    if (drains === 2) throw new Error('SA_EDEVICE: device lost');
+    return b.keyHash.length;
+  };
+  const conn = new SpanMetricsConnector({ batch_size: 4, columnizer_threads: 1 }, { addon, rules: DEMO_SPAN_NAME_RULES });
+  const req = (k) => otlp.encodeTraces(request([[{ 'service.name': `s${k}` }, [span('a'), span('b'), span('c')]]]));
+  // one drain per batch here (6 spans >= 4); the second batch's drain fails:
+  // its requests (whose spans were in the failed columns) are rejected, the
+  // first batch's stay acknowledged
+  assert.deepStrictEqual(conn.consumeTracesBatch([req(0), req(1)]), [null, null]);
+  const errs = conn.consumeTracesBatch([req(2), req(3)]);
+  assert.ok(errs.every((e) => e instanceof Error && e.deferred === true), String(errs));
+  const addon2 = new NativeColumnizerFakeAddon();
+  addon2.columnizeBatch = () => { throw new Error('columnizer broke'); };
+  const c2 = new SpanMetricsConnector({ columnizer_threads: 2 }, { addon: addon2, rules: DEMO_SPAN_NAME_RULES });
+  const e2 = c2.consumeTracesBatch([req(0), req(1)]);
+  assert.ok(e2.every((e) => e instanceof Error && /columnizer broke/.test(e.message)));
+  conn.shutdown();
+  c2.shutdown();
+});
+
 test('native columnizer: invalid UTF-8 falls back to JavaScript; malformed bytes are rejected', () => {
   const addon = new NativeColumnizerFakeAddon();
   const conn = new SpanMetricsConnector({}, { addon, rules: DEMO_SPAN_NAME_RULES });

@@ -79,7 +79,7 @@ typedef struct {
     uint32_t hll_p;         /* HLL precision, 4..18 (default 14) */
     uint32_t cms_d;         /* count-min rows, 1..8 (default 4) */
     uint32_t cms_w;         /* count-min columns, power of two (default 2048) */
-    uint64_t window_ns;     /* sketch window length (default 10 s) */
+    uint64_t window_ns;     /* sketch window length (default 10 s; < 2^56 ns) */
     uint32_t n_windows;     /* resident window ring, power of two (default 8) */
     uint32_t n_services;    /* service ids 0..n_services-1 get sketches */
     uint64_t key_capacity;  /* expected distinct series; table = next pow2 >= 1.25x */

@@ -32,6 +32,7 @@ struct BinEntry {
 };
 constexpr int kBins = 65;
 
+struct XHdr;
 // Everything the ingest kernels need, passed by value (kernel-argument segment,
 // read through the scalar cache).
 struct IngestParams {
@@ -97,6 +98,19 @@ struct IngestParams {
   uint8_t *hll_lb;
   uint32_t lb_shift, lb_n, lb_seq;
   unsigned long long *hll_filt;  // [kFiltSlots] (sa_stats.hll_filtered)
+  // exponential-histogram engines on the small-table kernel (EXPO): the key
+  // slot of every span (for the bucket-counting pass) and the per-workgroup
+  // header slabs [G][cap] (XHdr) the rescale pass reduces
+  uint32_t *slot_of;
+  XHdr *xslab;
+};
+// One workgroup's exponential-histogram header partial for one key slot
+// (EXPO kernel -> expo_reduce_rescale_kernel): counts, exact ns sum, the
+// largest ~d over positive durations (so the minimum starts from a zeroed
+// slab) and the largest positive duration.
+struct XHdr {
+  uint32_t cnt, zero;
+  unsigned long long sum, minx, max;
 };
 
 // Exponential-histogram mode (spanagg_expo.hip): per key slot a header and
@@ -124,6 +138,8 @@ struct ExpoParams {
   double div;         // 1e6 (ms) or 1e9 (s)
   uint32_t *slot_of;  // [n] key slot of each span (pass 1 -> pass 3)
   unsigned long long *dropped;
+  XHdr *xslab;        // small-table engines: [xG][cap] per-workgroup header partials (nullptr: pass 1 atomics)
+  uint32_t xG;
 };
 __host__ __device__ ExpoHdr expo_hdr_empty();
 constexpr uint32_t kExpoMaxSize = 4096;
@@ -233,6 +249,11 @@ __host__ __device__ inline uint32_t bt_slot(uint64_t m, uint32_t log2sb, uint32_
 constexpr uint32_t kRowBytes = 32;
 constexpr uint32_t kRowMaxBk = kRowBytes - 8;
 static_assert(kPartMaxBk <= kRowMaxBk, "binned rows hold every bucket count");
+// Record duration word: the duration in ns (bits 0-58) and its histogram
+// bucket (bits 59-63, from the scatter's bin table), so the aggregate needs no
+// bucketing; a span of 2^59 ns or longer (18 years) takes the overflow path.
+constexpr uint32_t kRecDurBits = 59;
+constexpr uint64_t kRecDurMask = (1ULL << kRecDurBits) - 1;
 constexpr uint32_t kBtStage = 4;     // records per bin stage: one 64-B chunk per flush
 constexpr uint32_t kBtHq = 256;      // scatter deferred HLL raises
 constexpr uint32_t kBtBlock = 1024;  // scatter workgroup
@@ -320,6 +341,11 @@ hipError_t launch_ingest_hbm(const IngestParams &P, uint32_t grid, hipStream_t s
 hipError_t launch_ingest_part(const IngestParams &P, hipStream_t s);
 hipError_t prepare_ingest_part();
 hipError_t prepare_ingest_small(size_t lds_bytes);
+// exponential-histogram engines with an LDS-sized key table: the small-table
+// kernel in EXPO mode (header partials + per-span slots; spanagg_expo.hip
+// reduces and counts)
+hipError_t prepare_ingest_expo_small(size_t lds_bytes);
+hipError_t launch_ingest_expo_small(const IngestParams &P, uint32_t grid, size_t lds_bytes, hipStream_t s);
 hipError_t launch_reduce_slabs(uint32_t *slab_cnt, unsigned long long *slab_sum,
                                unsigned long long *gcounts, uint32_t G, uint64_t cap,
                                uint32_t nbk, hipStream_t s);
@@ -346,6 +372,8 @@ hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s);
 hipError_t launch_expo_compact(const ExpoParams &E, unsigned long long *out_keys, ExpoRow *out_rows,
                                uint32_t *out_buckets, unsigned long long *out_n, hipStream_t s);
 hipError_t launch_expo_init(ExpoHdr *hdr, uint64_t cap, hipStream_t s);
+size_t expo_count_lds_bytes(uint64_t cap, uint32_t max_size);
+hipError_t prepare_expo_count(size_t lds_bytes);
 hipError_t launch_expo_probe(const double *v, const int32_t *scale, int32_t *idx_out, double *log_out, uint64_t n,
                              hipStream_t s);
 

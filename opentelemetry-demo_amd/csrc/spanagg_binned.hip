@@ -25,6 +25,7 @@
 // Rows hold u8 bucket counts (sa_internal.h kRowBytes); a count that would
 // pass 255 moves the row's counts into the u64 spill array base64.
 #include <algorithm>
+#include <cstdlib>
 
 #include "sa_device.h"
 
@@ -235,7 +236,7 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
   };
   auto hot_rec = [&](uint32_t b, const ulonglong2 &r) {
     const uint64_t m = ((uint64_t)b << kBinShift) | (r.x & kBinRest);
-    hot_add(m, r.y, (r.x >> 63) != 0, (uint32_t)(r.x >> kBinShift) & 1023u);
+    hot_add(m, r.y & kRecDurMask, (r.x >> 63) != 0, (uint32_t)(r.x >> kBinShift) & 1023u);
   };
   // claims n record positions of bin b's region (u16 pairs); positions at or
   // past the region's end take the overflow table instead
@@ -250,10 +251,15 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
       hot_acc(h0 + (hk.x == m ? 0u : 1u), m, d, err, ws);
       return;
     }
+    const uint32_t bk = bucket_lds<1>(d, lbins, P);
+    if (__builtin_expect(d > kRecDurMask, 0)) {  // beyond the record's duration bits: the direct path
+      n_drop += bt_cold_direct(kp, m, d, bk, err, ws);
+      return;
+    }
     const uint32_t b = (uint32_t)(m >> kBinShift), sh = (b & 1u) * 16;
     const uint32_t c = (atomicAdd(&fillw[b >> 1], 1u << sh) >> sh) & 0xFFFFu;
-    const ulonglong2 rec =
-        make_ulonglong2((m & kBinRest) | (err ? (1ULL << 63) | ((uint64_t)ws << kBinShift) : 0ULL), d);
+    const ulonglong2 rec = make_ulonglong2((m & kBinRest) | (err ? (1ULL << 63) | ((uint64_t)ws << kBinShift) : 0ULL),
+                                           d | ((uint64_t)bk << kRecDurBits));
     if (c < kBtStage) {
       stage[b * kBtStage + c] = rec;
       return;
@@ -298,15 +304,20 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
       const uint32_t meta = copy_u32(T.meta[j]);
       const uint32_t svc = meta & 0xFFFFu;
       const bool svc_ok = svc < P.n_services;
-      ws[j] = window_slot(P, T.e[j]);
+      ws[j] = window_slot_lean(P, T.e[j]);
       const bool win_ok = ws[j] != 0xFFFFFFFFu;
       n_badsvc += wave_count(valid && !svc_ok);
       n_oor += wave_count(valid && svc_ok && !win_ok);
       const bool sk = valid && svc_ok && win_ok;
       err[j] = sk && ((meta >> 19) & 3u) == 2u;
-      const uint64_t x = xxh64_16(T.a[j], T.b[j]);
-      const uint32_t r = (uint32_t)__clzll((long long)((x << hp) | (1ULL << (hp - 1)))) + 1;
-      const uint32_t ho = sk ? ((ws[j] * P.n_services + svc) << hp) + (uint32_t)(x >> (64 - hp)) : 0u;
+      // the span hash on 32-bit halves, rho without 64-bit shifts, the
+      // register row by a 24-bit multiply-add (as the lean C2 kernel)
+      const H64 x = xxh64_16_h(T.a[j], T.b[j]);
+      const uint32_t yh = __builtin_amdgcn_alignbit(x.hi, x.lo, 32 - hp), yl = (x.lo << hp) | (1u << (hp - 1));
+      const uint32_t r = (uint32_t)__clzll((long long)(((uint64_t)yh << 32) | yl)) + 1;
+      uint32_t row;
+      asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(row) : "v"(ws[j]), "s"(P.n_services), "v"(svc));
+      const uint32_t ho = sk ? (row << hp) + (x.hi >> (32 - hp)) : 0u;
       bool up = sk && !(MODE & 2);
       if (lb_on) {
         const bool f = r <= llb[ho >> lbs];
@@ -505,22 +516,15 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
   __syncthreads();
   bt_stamp(P, (uint64_t)bin * 8, 1);
 
-  // 2. the records (the thresholds live in SGPRs: a runtime-bounded loop over
-  //    P.thr would re-load them from the kernarg segment for every record)
+  // 2. the records (each carries its bucket: kRecDurBits)
   const ulonglong2 *bin_rec = P.bt_rec + (uint64_t)bin * G * region;
   const __amdgpu_buffer_rsrc_t rrec = rsrc(bin_rec, G * region * 16);
   const uint32_t half = lane >> 5, r0 = lane & 31u;
-  uint64_t thr[kPartMaxBk - 1];
-#pragma unroll
-  for (uint32_t i = 0; i < kPartMaxBk - 1; ++i) thr[i] = i < P.npos ? P.thr[i] : ~0ULL;
-  const uint32_t nneg = P.nneg;
   uint32_t n_drop = 0;
   auto agg = [&](const ulonglong2 &v) {
     const uint64_t m = ((uint64_t)bin << kBinShift) | (v.x & kBinRest);
-    const uint64_t d = v.y;
-    uint32_t bk = nneg;
-#pragma unroll
-    for (uint32_t i = 0; i < kPartMaxBk - 1; ++i) bk += d > thr[i] ? 1u : 0u;
+    const uint64_t d = v.y & kRecDurMask;
+    const uint32_t bk = (uint32_t)(v.y >> kRecDurBits);  // bucketed by the scatter
     // the key's two buckets (four independent 16-B reads), else the probe
     // sequence (a new key, or one placed past its two buckets)
     const BtSeq bq = bt_seq(m, log2sb);
@@ -690,6 +694,236 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
   bt_stamp(P, (uint64_t)bin * 8, 3);
 }
 
+
+// Aggregate, third form (the default).  The layout, phases and row
+// write-back of bt_aggregate2_kernel; the records are aggregated two per lane
+// at a time with every LDS access of the pair issued before the first one is
+// waited for -- both records' two key buckets (4 x ds_read_b128 each), then
+// the compares, then both records' counter atomics -- instead of one record's
+// dependent chain after another (a record costs ~6 LDS round trips in
+// sequence there).  Records carry their bucket (the scatter's bin table), so
+// there is no per-record bucketing.  A key missing from its two buckets (new
+// in the bin, or placed past them) takes the probe loop, rare after the first
+// launches.  ERROR records append (window slot, key slot) to an LDS list,
+// added to errcnt after the records (global atomics past the list's 255).
+template <int MODE = 0, int MAXPER = 2, int BLOCK = 512>
+__global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t log2sb = P.log2sb, sb = 1u << log2sb;
+  const uint32_t G = P.bt_grid, bin = blockIdx.x, region = P.bt_region;
+  unsigned long long *lkeys = reinterpret_cast<unsigned long long *>(smem);
+  unsigned long long *lsum = lkeys + sb;
+  uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + sb);  // u16 [sb][17], packed
+  constexpr uint32_t kErrL = kBtAgg2Err * 2;                  // u32 words in the etab space
+  uint32_t *errl = reinterpret_cast<uint32_t *>(smem + bt_agg2_off_err(sb));  // [0] count, [1..] ek + 1
+  uint32_t *rcnt = reinterpret_cast<uint32_t *>(smem + bt_agg2_off_reg(sb));  // [G] region fills
+  uint32_t *misc = rcnt + G;  // [0] dropped
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  unsigned long long *gk = P.gkeys + ((uint64_t)bin << log2sb);
+  bt_stamp(P, (uint64_t)bin * 8, 0);
+
+  // 1. the bin's key slots (kept in registers to find the new ones later),
+  //    region fills, zeroed counters
+  constexpr int kMaxPer = MAXPER;
+  unsigned long long orig[kMaxPer];
+#pragma unroll
+  for (int u = 0; u < kMaxPer; ++u) {
+    const uint32_t s = tid + u * BLOCK;
+    orig[u] = s < sb ? gk[s] : 0ULL;
+  }
+  for (uint32_t g = tid; g < G; g += BLOCK) rcnt[g] = P.bt_cnt[(uint64_t)bin * G + g];
+#pragma unroll
+  for (int u = 0; u < kMaxPer; ++u) {
+    const uint32_t s = tid + u * BLOCK;
+    if (s < sb) {
+      lkeys[s] = orig[u];
+      lsum[s] = 0;
+    }
+  }
+  const uint32_t cw = bt_agg2_cnt_words(sb);
+  for (uint32_t i = tid; i < cw; i += BLOCK) lcnt[i] = 0;
+  if (tid == 0) errl[0] = misc[0] = 0;
+  __syncthreads();
+  bt_stamp(P, (uint64_t)bin * 8, 1);
+
+  // 2. the records
+  const ulonglong2 *bin_rec = P.bt_rec + (uint64_t)bin * G * region;
+  const __amdgpu_buffer_rsrc_t rrec = rsrc(bin_rec, G * region * 16);
+  const uint32_t half = lane >> 5, r0 = lane & 31u;
+  const uint32_t pmax = bt_probe_max(log2sb);
+  uint32_t n_drop = 0;
+  const ulonglong2 *lk2 = reinterpret_cast<const ulonglong2 *>(lkeys);
+  // two records (ok: valid) through the LDS together
+  auto agg_pair = [&](const ulonglong2 (&v)[2], const bool (&ok)[2]) {
+    uint64_t m[2];
+    BtSeq bq[2];
+    ulonglong2 q[2][4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      m[k] = ok[k] ? (((uint64_t)bin << kBinShift) | (v[k].x & kBinRest)) : 0ULL;
+      bq[k] = bt_seq(m[k], log2sb);
+      q[k][0] = lk2[bq[k].b1 * 2];
+      q[k][1] = lk2[bq[k].b1 * 2 + 1];
+      q[k][2] = lk2[bq[k].b2 * 2];
+      q[k][3] = lk2[bq[k].b2 * 2 + 1];
+    }
+    uint32_t s[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint64_t mm = m[k];
+      uint32_t f = kNotFound;
+      f = q[k][3].y == mm ? bq[k].b2 * 4 + 3 : f;
+      f = q[k][3].x == mm ? bq[k].b2 * 4 + 2 : f;
+      f = q[k][2].y == mm ? bq[k].b2 * 4 + 1 : f;
+      f = q[k][2].x == mm ? bq[k].b2 * 4 : f;
+      f = q[k][1].y == mm ? bq[k].b1 * 4 + 3 : f;
+      f = q[k][1].x == mm ? bq[k].b1 * 4 + 2 : f;
+      f = q[k][0].y == mm ? bq[k].b1 * 4 + 1 : f;
+      f = q[k][0].x == mm ? bq[k].b1 * 4 : f;
+      s[k] = ok[k] ? f : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (__builtin_expect(ok[k] && s[k] == kNotFound, 0)) {  // probe / insert in the mirror
+        uint32_t i = 0, sl = kNotFound;
+        for (; i < pmax; ++i) {
+          sl = bt_pos(bq[k], i);
+          unsigned long long kk = lkeys[sl];
+          if (kk == 0) kk = atomicCAS(&lkeys[sl], 0ULL, (unsigned long long)m[k]);
+          if (kk == 0 || kk == m[k]) break;
+        }
+        s[k] = i == pmax ? kNotFound - 1 : sl;  // kNotFound - 1: the bin's sub-table is full
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (!ok[k]) continue;
+      const bool err = (v[k].x >> 63) != 0;
+      const uint32_t ws = (uint32_t)(v[k].x >> kBinShift) & 1023u;
+      if (__builtin_expect(s[k] == kNotFound - 1, 0)) {  // dropped
+        ++n_drop;
+        if (err) bt_cms_add(kernel_params(), ws, m[k] * P.kinv);
+        continue;
+      }
+      const uint32_t h = s[k] * kPartMaxBk + (uint32_t)(v[k].y >> kRecDurBits);
+      atomicAdd(&lcnt[h >> 1], 1u << ((h & 1u) * 16));
+      atomicAdd(&lsum[s[k]], (unsigned long long)(v[k].y & kRecDurMask));
+      if (err) {
+        const uint32_t ek = (ws << log2sb) | s[k];
+        const uint32_t at = atomicAdd(&errl[0], 1u);
+        if (at + 1 < kErrL) errl[at + 1] = ek;
+        else atomicAdd(P.errcnt + ((uint64_t)ws << P.log2cap) + ((uint64_t)bin << log2sb) + s[k], 1ULL);
+      }
+    }
+  };
+  constexpr uint32_t kWaves = BLOCK / 64;
+  constexpr uint32_t B = 4;
+  const uint32_t pairs = (G + 1) / 2;
+  if (!(MODE & 1)) {
+    for (uint32_t p0 = wave; p0 < pairs; p0 += kWaves * B) {
+      ulonglong2 v[B];
+      uint32_t cnt[B];
+#pragma unroll
+      for (uint32_t b = 0; b < B; ++b) {
+        const uint32_t p = p0 + b * kWaves, g = 2 * p + half;
+        const bool okp = p < pairs && g < G;
+        cnt[b] = rcnt[okp ? g : 0u];
+        cnt[b] = okp ? cnt[b] : 0u;
+      }
+#pragma unroll
+      for (uint32_t b = 0; b < B; ++b) {
+        const uint32_t g = 2 * (p0 + b * kWaves) + half;
+        const uint32_t off = r0 < cnt[b] ? (g * region + r0) * 16 : 0xFFFFFFF0u;
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)off, 0, 2);
+        v[b] = make_ulonglong2((uint64_t)x[0] | ((uint64_t)x[1] << 32), (uint64_t)x[2] | ((uint64_t)x[3] << 32));
+      }
+#pragma unroll
+      for (uint32_t b = 0; b < B; b += 2) {
+        const ulonglong2 vv[2] = {v[b], v[b + 1]};
+        const bool ok[2] = {r0 < cnt[b], r0 < cnt[b + 1]};
+        agg_pair(vv, ok);
+      }
+    }
+    // regions longer than 32 records: the rest, one record per lane
+#pragma unroll 1
+    for (uint32_t p = wave; p < pairs; p += kWaves) {
+      const uint32_t g = 2 * p + half;
+      const uint32_t c = g < G ? rcnt[g] : 0u;
+      for (uint32_t r = 32 + r0; r < c; r += 32) {
+        const ulonglong2 vv[2] = {bin_rec[(uint64_t)g * region + r], make_ulonglong2(0, 0)};
+        const bool ok[2] = {true, false};
+        agg_pair(vv, ok);
+      }
+    }
+  }
+  n_drop = wave_sum(n_drop);
+  if (lane == 0 && n_drop) atomicAdd(&misc[0], n_drop);
+  __syncthreads();
+  bt_stamp(P, (uint64_t)bin * 8, 2);
+
+  // 3. new keys and touched rows of the bin (one owner: plain stores; every
+  //    row read is issued before the first row is written); the ERROR list
+  if (MODE & 2) return;
+  const uint32_t nbk = P.nbk;
+  uint4 *rows = reinterpret_cast<uint4 *>(P.gcounts) + ((uint64_t)bin << log2sb) * (kRowBytes / 16);
+  uint4 rv[kMaxPer][2];
+  bool touched[kMaxPer];
+#pragma unroll
+  for (int u = 0; u < kMaxPer; ++u) {
+    const uint32_t s = tid + u * BLOCK;
+    touched[u] = s < sb && lsum[s] != 0;
+    if (s < sb && !touched[u]) {  // a zero ns sum: look at the counts
+      uint32_t any = 0;
+      for (uint32_t b = 0; b < nbk; ++b) {
+        const uint32_t h = s * kPartMaxBk + b;
+        any |= (lcnt[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu;
+      }
+      touched[u] = any != 0;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 2; ++q) rv[u][q] = touched[u] ? rows[(uint64_t)s * 2 + q] : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int u = 0; u < kMaxPer; ++u) {
+    const uint32_t s = tid + u * BLOCK;
+    if (s >= sb) continue;
+    const unsigned long long k = lkeys[s];
+    if (k != orig[u]) gk[s] = k;
+    if (!touched[u]) continue;
+    const uint32_t w[8] = {rv[u][0].x, rv[u][0].y, rv[u][0].z, rv[u][0].w,
+                           rv[u][1].x, rv[u][1].y, rv[u][1].z, rv[u][1].w};
+    const unsigned long long sum = ((unsigned long long)w[1] << 32 | w[0]) + lsum[s];
+    uint32_t c[kPartMaxBk];
+    bool spill = false;
+#pragma unroll
+    for (uint32_t b = 0; b < kPartMaxBk; ++b) {
+      const uint32_t h = s * kPartMaxBk + b;
+      c[b] = b < nbk ? ((w[2 + b / 4] >> ((b & 3u) * 8)) & 0xFFu) + ((lcnt[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu)
+                     : 0u;
+      spill |= c[b] > 0xFFu;
+    }
+    uint32_t o[6] = {0, 0, 0, 0, 0, 0};
+    if (spill) {  // the row's counts move to the spill array (atomics: the scatter adds there too)
+      unsigned long long *sp = P.base64 + ((uint64_t)bin << log2sb | s) * (nbk + 1);
+#pragma unroll
+      for (uint32_t b = 0; b < kPartMaxBk; ++b)
+        if (c[b]) atomicAdd(sp + b, (unsigned long long)c[b]);
+    } else {
+#pragma unroll
+      for (uint32_t b = 0; b < kPartMaxBk; ++b) o[b / 4] |= c[b] << ((b & 3u) * 8);
+    }
+    rows[(uint64_t)s * 2] = make_uint4((uint32_t)sum, (uint32_t)(sum >> 32), o[0], o[1]);
+    rows[(uint64_t)s * 2 + 1] = make_uint4(o[2], o[3], o[4], o[5]);
+  }
+  const uint32_t ne = min(errl[0], kErrL - 1);
+  for (uint32_t i = tid; i < ne; i += BLOCK) {
+    const uint32_t ek = errl[i + 1], ws = ek >> log2sb, s = ek & (sb - 1);
+    atomicAdd(P.errcnt + ((uint64_t)ws << P.log2cap) + ((uint64_t)bin << log2sb) + s, 1ULL);
+  }
+  if (tid == 0 && misc[0]) atomicAdd(&P.stats[kStatDropped], (unsigned long long)misc[0]);
+  bt_stamp(P, (uint64_t)bin * 8, 3);
+}
+
 }  // namespace
 
 // SA_DIAG bits of the ablation builds (profiling only)
@@ -712,7 +946,33 @@ static const void *bt_scatter2_fn(uint32_t diag) {
 }
 
 constexpr uint32_t kDiagBtAggWide = 1u << 30, kDiagBtAggLoadOnly = 1u << 31;
+static const void *bt_agg2_fn(uint32_t diag);
+static bool bt_agg_v2() {  // SPANAGG_BT_AGG=2: the second-form aggregate (A/B runs)
+  static const bool v2 = [] {
+    const char *v = std::getenv("SPANAGG_BT_AGG");
+    return v && std::atoi(v) == 2;
+  }();
+  return v2;
+}
 static const void *bt_agg_fn(uint32_t diag) {
+  const int mode = ((diag & 1u) ? 1 : 0) | ((diag & kDiagBtAggNoRows) ? 2 : 0);
+  if (!bt_agg_v2() && !(diag & kDiagBtAggLoadOnly)) {
+    if (diag & kDiagBtAggWide) switch (mode) {  // bins of 2,048 slots
+        case 1: return (const void *)&bt_aggregate3_kernel<1, 4>;
+        case 2: return (const void *)&bt_aggregate3_kernel<2, 4>;
+        case 3: return (const void *)&bt_aggregate3_kernel<3, 4>;
+        default: return (const void *)&bt_aggregate3_kernel<0, 4>;
+      }
+    switch (mode) {
+      case 1: return (const void *)&bt_aggregate3_kernel<1, 2>;
+      case 2: return (const void *)&bt_aggregate3_kernel<2, 2>;
+      case 3: return (const void *)&bt_aggregate3_kernel<3, 2>;
+      default: return (const void *)&bt_aggregate3_kernel<0, 2>;
+    }
+  }
+  return bt_agg2_fn(diag);
+}
+static const void *bt_agg2_fn(uint32_t diag) {
   const int mode = ((diag & 1u) ? 1 : 0) | ((diag & kDiagBtAggNoRows) ? 2 : 0);
   if (diag & kDiagBtAggLoadOnly) return (const void *)&bt_aggregate2_kernel<4, 2>;
   if (diag & kDiagBtAggWide) switch (mode) {  // bins of 2,048 slots
@@ -737,10 +997,10 @@ hipError_t prepare_ingest_bt(size_t agg_lds) {
       return e;
   for (uint32_t d : {0u, 1u, kDiagBtAggNoRows, 1u | kDiagBtAggNoRows})
     for (uint32_t v : {0u, kDiagBtAggWide, kDiagBtAggLoadOnly})
-      if (hipError_t e =
-              hipFuncSetAttribute(bt_agg_fn(d | v), hipFuncAttributeMaxDynamicSharedMemorySize, (int)agg_lds);
-          e != hipSuccess)
-        return e;
+      for (const void *fn : {bt_agg_fn(d | v), bt_agg2_fn(d | v)})
+        if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)agg_lds);
+            e != hipSuccess)
+          return e;
   return hipSuccess;
 }
 

@@ -88,6 +88,10 @@ struct sa_engine {
   // exponential-histogram mode (cfg.exp_max_size > 0): the HBM-table path
   // runs the sketches, spanagg_expo.hip the histograms
   bool expo = false;
+  // exponential engines whose key table fits LDS: the small-table kernel in
+  // EXPO mode (per-workgroup header partials in xslab [G][cap], per-span slots)
+  bool expo_small = false;
+  sa::XHdr *xslab = nullptr;
   sa::ExpoHdr *expo_hdr = nullptr;
   uint32_t *expo_buckets = nullptr, *expo_slot = nullptr;
   uint64_t expo_slot_cap = 0;
@@ -150,6 +154,7 @@ int validate_config(const sa_config *c, std::string &why) {
   if (c->cms_d < 1 || c->cms_d > 8) return why = "cms_d must be in 1..8", SA_EINVAL;
   if (c->cms_w < 2 || !is_pow2(c->cms_w)) return why = "cms_w must be a power of two >= 2", SA_EINVAL;
   if (c->window_ns == 0) return why = "window_ns must be > 0", SA_EINVAL;
+  if (c->window_ns >> 56) return why = "window_ns must stay below 2^56 ns (~2.3 years)", SA_EINVAL;
   if (!is_pow2(c->n_windows) || c->n_windows > 4096)
     return why = "n_windows must be a power of two <= 4096", SA_EINVAL;
   if (c->n_services < 1 || c->n_services > 65536)
@@ -340,6 +345,12 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   e->lds_bytes = (size_t)e->cap * 16 + (size_t)e->cap * nw * 4 + sa::kLdsExtraBytes;
   e->expo = cfg->exp_max_size != 0;
   e->small = e->lds_bytes <= kLdsBudget && !e->expo;
+  if (e->expo) {  // key mirror + 32-B header partials per slot (nw = 6 counter words)
+    const size_t xl = (size_t)e->cap * 8 + (size_t)e->cap * 32 + sa::kLdsExtraBytes;
+    const char *xv = std::getenv("SPANAGG_EXPO_SMALL");  // 0: the HBM-table pass-1 path (A/B runs)
+    e->expo_small = xl <= kLdsBudget && !(xv && std::atoi(xv) == 0);
+    if (e->expo_small) e->lds_bytes = xl;
+  }
   e->variant = e->small ? kDefaultVariant : 0;
   if (const char *v = std::getenv("SPANAGG_VARIANT"))  // tuning knob for A/B runs
     e->variant = std::max(0, std::min((e->small ? sa::kNumLdsVariants : sa::kNumVariants) - 1,
@@ -351,6 +362,14 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
         1, std::min<uint32_t>(2048 / e->block, (uint32_t)((160 * 1024) / e->lds_bytes)));
     e->G = e->cus * per_cu;
     if (hipError_t st = sa::prepare_ingest_small(e->lds_bytes); st != hipSuccess)
+      return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
+  } else if (e->expo_small) {
+    e->block = 1024;
+    e->spl = 2;
+    e->G = e->cus * std::max<uint32_t>(1, (uint32_t)((160 * 1024) / e->lds_bytes));
+    if (hipError_t st = sa::prepare_ingest_expo_small(e->lds_bytes); st != hipSuccess)
+      return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
+    if (hipError_t st = sa::prepare_expo_count(sa::expo_count_lds_bytes(e->cap, cfg->exp_max_size)); st != hipSuccess)
       return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
   } else {
     e->block = sa::kHbmBlock;
@@ -410,6 +429,13 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       return bail(rc);
     if (sa::launch_expo_init(e->expo_hdr, e->cap, nullptr) != hipSuccess)
       return bail(fail(e, SA_EDEVICE, "expo state init failed"));
+    if (e->expo_small) {
+      if ((rc = alloc((void **)&e->xslab, (size_t)e->G * e->cap * sizeof(sa::XHdr)))) return bail(rc);
+      // (window, slot) keys of the LDS ERROR table are 16-bit
+      if ((uint64_t)cfg->n_windows * e->cap < 65535 &&
+          (rc = alloc((void **)&e->errslab, (size_t)e->G * cfg->n_windows * e->cap * 4)))
+        return bail(rc);
+    }
   }
   if (std::getenv("SPANAGG_STAMPS") && (rc = alloc((void **)&e->dbg, (size_t)e->G * sa::kDbgPerWg * 8)))
     return bail(rc);
@@ -477,7 +503,7 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->dbg, (void *)e->d_bins, (void *)e->errslab, (void *)e->part_rec,
                   (void *)e->part_fill, (void *)e->bt_rec, (void *)e->bt_cnt, (void *)e->base64, (void *)e->hll_lb,
                   (void *)e->expo_hdr, (void *)e->expo_buckets, (void *)e->expo_slot, (void *)e->expo_out_keys,
-                  (void *)e->expo_out_rows, (void *)e->expo_out_buckets, (void *)e->hll_filt,
+                  (void *)e->expo_out_rows, (void *)e->expo_out_buckets, (void *)e->hll_filt, (void *)e->xslab,
                   e->dstage[0], e->dstage[1]})
     if (p) (void)hipFree(p);
   for (int k = 0; k < 2; ++k) {
@@ -522,7 +548,8 @@ static int ingest_on(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   // 65532 spans per workgroup per launch (ingest_v2_kernel has no epoch flush)
   const uint64_t max_n = e->bt     ? (uint64_t)e->bt_grid * sa::kBtMaxWgSpans
                          : e->part ? sa::kPartMaxSpans
-                                   : (uint64_t)e->G * ((e->small && e->variant >= 8) ? sa::kMaxWgSpans : (1u << 27));
+                                   : (uint64_t)e->G * (((e->small && e->variant >= 8) || e->expo_small) ? sa::kMaxWgSpans
+                                                                                                       : (1u << 27));
   for (uint64_t off = 0; off < b->n; off += max_n) {
     const uint64_t m = std::min(max_n, b->n - off);
     sa_span_batch sub{b->key_hash + off, b->start_ns + off, b->end_ns + off, b->trace_w0 + off,
@@ -578,6 +605,8 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
   E.div = e->cfg.unit == SA_UNIT_S ? 1e9 : 1e6;
   E.slot_of = e->expo_slot;
   E.dropped = e->stats + sa::kStatDropped;
+  E.xslab = e->expo_small ? e->xslab : nullptr;
+  E.xG = e->G;
   return E;
 }
 
@@ -678,17 +707,25 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
                          ~(uint64_t)(sa::kPartStage - 1));
     st = sa::launch_ingest_part(P, s);
   } else if (e->expo) {
-    // sketches (and the zero-key / service / window counters) through the
-    // HBM-table kernel with its RED part off, then the histogram kernels
-    P.diag |= SA_DIAG_NO_RED;
-    st = sa::launch_ingest_hbm(P, grid, s, e->variant);
-    if (st == hipSuccess && e->expo_slot_cap < b->n) {
+    if (e->expo_slot_cap < b->n) {  // (hipFree waits for the device)
       if (e->expo_slot) (void)hipFree(e->expo_slot);
       e->expo_slot = nullptr;
       e->expo_slot_cap = 0;
       if (hipMalloc((void **)&e->expo_slot, b->n * 4) != hipSuccess) return fail(e, SA_ENOMEM, "expo slot buffer");
       e->expo_slot_cap = b->n;
     }
+    if (e->expo_small) {
+      // the small-table kernel in EXPO mode: sketches, key slots, header partials
+      P.slot_of = e->expo_slot;
+      P.xslab = e->xslab;
+      st = sa::launch_ingest_expo_small(P, grid, e->lds_bytes, s);
+    } else {
+      // sketches (and the zero-key / service / window counters) through the
+      // HBM-table kernel with its RED part off
+      P.diag |= SA_DIAG_NO_RED;
+      st = sa::launch_ingest_hbm(P, grid, s, e->variant);
+    }
+    // then the histogram kernels
     if (st == hipSuccess) st = sa::launch_expo_ingest(expo_params(e, b), s);
   } else {
     st = sa::launch_ingest_hbm(P, grid, s, e->variant);
@@ -1126,7 +1163,7 @@ int sa_get_stats(sa_engine *e, sa_stats *o) {
   o->n_keys = nk;
   o->table_capacity = e->cap;
   o->window_base = e->win_base;
-  o->small_table = e->small ? 1 : 0;
+  o->small_table = (e->small || e->expo_small) ? 1 : 0;
   {
     std::vector<uint64_t> f(sa::kFiltSlots);
     SA_HIP(e, hipMemcpyAsync(f.data(), e->hll_filt, sa::kFiltSlots * 8, hipMemcpyDeviceToHost, e->stream));

@@ -111,11 +111,11 @@ __global__ __launch_bounds__(256) void expo_pass1_kernel(ExpoParams E) {
 }
 
 // per series: fix the scale for every positive value seen so far; merge the
-// kept buckets down when it drops (one thread per slot)
-__global__ __launch_bounds__(256) void expo_rescale_kernel(ExpoParams E) {
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < E.cap; s += (uint64_t)gridDim.x * blockDim.x) {
+// kept buckets down when it drops
+__device__ __forceinline__ void rescale_slot(const ExpoParams &E, uint64_t s) {
+  {
     ExpoHdr &h = E.hdr[s];
-    if (h.maxpos_ns == 0) continue;  // no positive value
+    if (h.maxpos_ns == 0) return;  // no positive value
     const double vlo = expo_value(h.minpos_ns, E.div), vhi = expo_value(h.maxpos_ns, E.div);
     int32_t lo = expo_index(vlo, kExpoMaxScale), hi = expo_index(vhi, kExpoMaxScale), change = 0;
     while (hi - lo >= (int32_t)E.max_size) {  // changeScale
@@ -140,6 +140,120 @@ __global__ __launch_bounds__(256) void expo_rescale_kernel(ExpoParams E) {
     h.scale = target;
     h.lo = expo_index(vlo, target);
     h.hi = expo_index(vhi, target);
+  }
+}
+
+// (one thread per slot)
+__global__ __launch_bounds__(256) void expo_rescale_kernel(ExpoParams E) {
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < E.cap; s += (uint64_t)gridDim.x * blockDim.x)
+    rescale_slot(E, s);
+}
+
+// Small-table engines: the ingest kernel (EXPO mode) leaves per-workgroup
+// header partials in slabs [xG][cap].  One block per 64 slots: 16 groups of
+// 64 threads sum every 16th workgroup's partials (coalesced 32-B rows,
+// zeroing what they consumed), LDS combines the groups, then one thread per
+// slot folds the sum into the series header and rescales it.
+__global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E) {
+  __shared__ XHdr part[16][64];
+  const uint32_t sl = threadIdx.x & 63u, gg = threadIdx.x >> 6;
+  const uint64_t s = blockIdx.x * 64ull + sl;
+  XHdr acc{0, 0, 0, 0, 0};
+  if (s < E.cap) {
+    for (uint32_t g = gg; g < E.xG; g += 16) {
+      XHdr *p = E.xslab + (uint64_t)g * E.cap + s;
+      const XHdr x = *p;
+      if (x.cnt) {
+        acc.cnt += x.cnt;
+        acc.zero += x.zero;
+        acc.sum += x.sum;
+        acc.minx = x.minx > acc.minx ? x.minx : acc.minx;
+        acc.max = x.max > acc.max ? x.max : acc.max;
+        *p = XHdr{0, 0, 0, 0, 0};
+      }
+    }
+  }
+  part[gg][sl] = acc;
+  __syncthreads();
+  if (gg != 0 || s >= E.cap) return;
+#pragma unroll
+  for (uint32_t k = 1; k < 16; ++k) {
+    const XHdr x = part[k][sl];
+    acc.cnt += x.cnt;
+    acc.zero += x.zero;
+    acc.sum += x.sum;
+    acc.minx = x.minx > acc.minx ? x.minx : acc.minx;
+    acc.max = x.max > acc.max ? x.max : acc.max;
+  }
+  if (acc.cnt) {
+    ExpoHdr &h = E.hdr[s];
+    const unsigned long long minpos = ~acc.minx;  // UINT64_MAX when no positive duration
+    const unsigned long long mn = acc.zero ? 0ULL : minpos;
+    h.count += acc.cnt;
+    h.zero += acc.zero;
+    h.sum_ns += acc.sum;
+    h.min_ns = mn < h.min_ns ? mn : h.min_ns;
+    h.max_ns = acc.max > h.max_ns ? acc.max : h.max_ns;
+    h.minpos_ns = minpos < h.minpos_ns ? minpos : h.minpos_ns;
+    h.maxpos_ns = acc.max > h.maxpos_ns ? acc.max : h.maxpos_ns;
+  }
+  rescale_slot(E, s);
+}
+
+// Bucket counting with per-workgroup LDS privatisation: the slots' (scale,
+// buffer) in LDS, and a cache of kXcEntries series (claimed first come, four
+// probes from the slot's home, so a mix's frequent series hold them) whose
+// max_size bucket counts are added in LDS and leave once per workgroup; spans
+// of other series add to the HBM buckets directly.
+constexpr uint32_t kXcBlock = 1024;
+// u16 cache counts (a workgroup takes at most 2^16 - 1 spans): 64 KiB, so two
+// workgroups share a CU with the slot table
+constexpr uint32_t kXcLdsBudget = 64 * 1024;
+constexpr uint64_t kXcMaxSpans = 65535;
+__host__ __device__ inline uint32_t xc_entries(uint32_t max_size) {
+  uint32_t e = 256;
+  while (e > 4 && (uint64_t)e * max_size * 2 > kXcLdsBudget) e >>= 1;
+  return e;
+}
+__global__ __launch_bounds__(kXcBlock) void expo_count_cached_kernel(ExpoParams E, uint64_t per_wg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t M = E.max_size, NE = xc_entries(M), cap = (uint32_t)E.cap;
+  int2 *meta = reinterpret_cast<int2 *>(smem);                     // [cap] {scale, cur}
+  uint32_t *tag = reinterpret_cast<uint32_t *>(meta + cap);         // [NE] slot + 1 (0: free)
+  uint32_t *cnt = tag + NE;                                          // [NE][M] u16, packed in pairs
+  for (uint32_t i = threadIdx.x; i < cap; i += kXcBlock) {
+    const ExpoHdr &h = E.hdr[i];
+    meta[i] = make_int2(h.scale, (int)h.cur);
+  }
+  for (uint32_t i = threadIdx.x; i < NE; i += kXcBlock) tag[i] = 0;
+  for (uint32_t i = threadIdx.x; i < (NE * M + 1) / 2; i += kXcBlock) cnt[i] = 0;
+  __syncthreads();
+  const uint64_t lo = blockIdx.x * per_wg, hi = lo + per_wg < E.n ? lo + per_wg : E.n;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += kXcBlock) {
+    const uint32_t slot = E.slot_of[i];
+    const uint64_t st = E.start[i], en = E.end[i];
+    if (slot == kNotFound) continue;
+    const uint64_t d = en > st ? en - st : 0;
+    if (d == 0) continue;
+    const int2 m = meta[slot];
+    const uint32_t at = expo_mod(expo_index(expo_value(d, E.div), m.x), M);
+    uint32_t e = (((slot * 0x9E3779B1u) >> 16) & (NE / 4 - 1)) * 4, hit = kNotFound;  // home group of 4
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      uint32_t t = tag[e + k];
+      if (t == 0) t = atomicCAS(&tag[e + k], 0u, slot + 1);
+      if (t == 0 || t == slot + 1) {
+        hit = e + k;
+        break;
+      }
+    }
+    if (hit != kNotFound) atomicAdd(&cnt[(hit * M + at) >> 1], 1u << (((hit * M + at) & 1u) * 16));
+    else atomicAdd(E.buckets + ((uint64_t)m.y * E.cap + slot) * M + at, 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < NE * M; i += kXcBlock) {
+    const uint32_t c = (cnt[i >> 1] >> ((i & 1u) * 16)) & 0xFFFFu, t = tag[i / M];
+    if (c && t) atomicAdd(E.buckets + ((uint64_t)meta[t - 1].y * E.cap + (t - 1)) * M + i % M, c);
   }
 }
 
@@ -207,8 +321,27 @@ __host__ __device__ ExpoHdr expo_hdr_empty() {
   return h;
 }
 
+size_t expo_count_lds_bytes(uint64_t cap, uint32_t max_size) {
+  const uint32_t ne = xc_entries(max_size);
+  return (size_t)cap * 8 + (size_t)ne * 4 + ((size_t)ne * max_size + 1) / 2 * 4;
+}
+
+hipError_t prepare_expo_count(size_t lds_bytes) {
+  return hipFuncSetAttribute((const void *)&expo_count_cached_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds_bytes);
+}
+
 hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s) {
   if (E.n == 0) return hipSuccess;
+  if (E.xslab) {  // small table: the ingest kernel left header partials and slots
+    hipLaunchKernelGGL(expo_reduce_rescale_kernel, dim3((uint32_t)((E.cap + 63) / 64)), dim3(1024), 0, s, E);
+    // u16 LDS counts: at most kXcMaxSpans spans per workgroup; ~512 workgroups (two per CU)
+    const uint64_t per_wg = std::min<uint64_t>(kXcMaxSpans, std::max<uint64_t>(4096, (E.n + 511) / 512));
+    const uint32_t grid = (uint32_t)((E.n + per_wg - 1) / per_wg);
+    hipLaunchKernelGGL(expo_count_cached_kernel, dim3(grid), dim3(kXcBlock), expo_count_lds_bytes(E.cap, E.max_size),
+                       s, E, per_wg);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(expo_pass1_kernel, dim3(grid_of(E.n)), dim3(256), 0, s, E);
   hipLaunchKernelGGL(expo_rescale_kernel, dim3(grid_of(E.cap)), dim3(256), 0, s, E);
   hipLaunchKernelGGL(expo_count_kernel, dim3(grid_of(E.n)), dim3(256), 0, s, E);

@@ -509,14 +509,20 @@ __device__ __forceinline__ bool lds_err_add(uint32_t *etab, uint32_t ek) {
 // wave can still hold when its neighbours run out.
 // LEAN: the span hash on 32-bit halves (xxh64_16_h), rho / register index
 // without 64-bit shifts, the register row offset by a 24-bit multiply.
+// EXPO: exponential-histogram engines (spanagg_expo.hip does the buckets).
+// The RED update becomes per-slot LDS header partials -- count, zero count,
+// ns sum, max of ~d and max d over positive durations (XHdr) -- in the space
+// of lsum + lcnt (nw = 6: 32 B per slot), written to the workgroup's header
+// slab at the end; every span's key slot goes to P.slot_of for the
+// bucket-counting pass.
 template <int S, int NBUF, int AUX, bool DIAG, int LC = 0, int NWC = 0, int PC = 0, int HAUX = -1,
-          bool DYN = false, int OPT = 0, bool EPI = false, bool LEAN = false>
+          bool DYN = false, int OPT = 0, bool EPI = false, bool LEAN = false, bool EXPO = false>
 __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t log2cap = LC ? (uint32_t)LC : P.log2cap;
   const uint32_t cap = 1u << log2cap;
-  const uint32_t nw = NWC ? (uint32_t)NWC : (P.nbk + 1) >> 1;
+  const uint32_t nw = EXPO ? 6u : NWC ? (uint32_t)NWC : (P.nbk + 1) >> 1;
   const uint32_t hp = PC ? (uint32_t)PC : P.p;
   const uint32_t diag = DIAG ? P.diag : 0u;
   unsigned long long *lkeys = reinterpret_cast<unsigned long long *>(smem);
@@ -530,6 +536,9 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   uint8_t *llb = reinterpret_cast<uint8_t *>(etab + kErrTab);       // [kLbMaxSub] HLL lower bounds
   const bool err_lds = P.errslab != nullptr;
   const bool lb_on = P.lb_n != 0 && !(diag & 2u);
+  // EXPO header partials (zeroed with lsum / lcnt): lsum = ns sums
+  unsigned long long *xminx = lsum + cap, *xmax = lsum + 2 * cap;
+  uint32_t *xcnt = reinterpret_cast<uint32_t *>(lsum + 3 * cap), *xzero = xcnt + cap;
 
   uint64_t lo, hi;
   wg_range_p(P, lo, hi);
@@ -573,7 +582,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
                                       : make_ulonglong2(0, 0);
   }
   uint4 bv = make_uint4(0, 0, 0, 0);
-  if (threadIdx.x < kBins * 2) bv = reinterpret_cast<const uint4 *>(P.bintab)[threadIdx.x];
+  if (!EXPO && threadIdx.x < kBins * 2) bv = reinterpret_cast<const uint4 *>(P.bintab)[threadIdx.x];  // (EXPO: no buckets)
   uint32_t lbw = 0;
   if (lb_on && threadIdx.x * 4 < P.lb_n) lbw = *reinterpret_cast<const uint32_t *>(P.hll_lb + threadIdx.x * 4);
   if constexpr (DYN && (OPT & 1)) {
@@ -677,7 +686,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
       key[j] = copy_u64(T.key[j]);
       if (!(diag & 128u) && !EPI) n_zero += wave_count(valid && key[j] == 0);
       dur[j] = T.e[j] > T.s[j] ? T.e[j] - T.s[j] : 0;
-      bkt[j] = (diag & 32u) ? (uint32_t)dur[j] & 15u : bucket_lds<1>(dur[j], lbins, P);
+      bkt[j] = EXPO ? 0u : (diag & 32u) ? (uint32_t)dur[j] & 15u : bucket_lds<1>(dur[j], lbins, P);
       const uint32_t meta = copy_u32(T.meta[j]);  // see key
       const uint32_t svc = meta & 0xFFFFu;
       const bool svc_ok = svc < P.n_services;
@@ -825,9 +834,52 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
         }
       }
     }
-    // 7. RED update: LDS u16 bucket counter + u64 ns sum
+    // 7. RED update: LDS u16 bucket counter + u64 ns sum.  LEAN: wave-level
+    //    key dedup of the counter adds -- the lanes that hold the same
+    //    (slot, bucket) as the wave's first lane of its hot series (a ballot
+    //    on the readlane'd key) make one LDS add of their count, from the
+    //    first of them; the other lanes add their own span.
+    if constexpr (EXPO) {
 #pragma unroll
-    for (int j = 0; j < S; ++j) {
+      for (int j = 0; j < S; ++j) {
+        const uint32_t f = found[j];
+        if (f != kNotFound) {
+          const unsigned long long d = dur[j];
+          atomicAdd(&xcnt[f], 1u);
+          if (f == hot_slot) hot_sum += d;
+          else atomicAdd(&lsum[f], d);
+          if (d == 0) {
+            atomicAdd(&xzero[f], 1u);
+          } else {
+            atomicMax(&xminx[f], ~d);
+            atomicMax(&xmax[f], d);
+          }
+        }
+        if (lane_off + toff + (uint32_t)j < len) P.slot_of[lo + toff + lane_off + j] = f;
+      }
+    } else if constexpr (LEAN) {
+      const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+      for (int j = 0; j < S; ++j) {
+        const uint32_t key = (found[j] << 6) | bkt[j];  // found < 2^11 or kNotFound, bucket < 64
+        const uint64_t hm = __ballot(found[j] == hot_slot && found[j] != kNotFound);
+        uint32_t lead = 64u, ndup = 0u, kk = 0xFFFFFFFFu;
+        if (hm) {  // wave-uniform
+          lead = (uint32_t)__builtin_ctzll(hm);
+          kk = (uint32_t)__builtin_amdgcn_readlane((int)key, (int)lead);
+          ndup = (uint32_t)__popcll(__ballot(key == kk));
+        }
+        const bool dup = key == kk;
+        if (found[j] != kNotFound && (!dup || lane == lead)) {
+          const uint32_t b = bkt[j];
+          atomicAdd(&lcnt[found[j] * nw + (b >> 1)], (dup ? ndup : 1u) << ((b & 1) * 16));
+        }
+        if (found[j] == hot_slot) hot_sum += dur[j];
+        else if (found[j] != kNotFound) atomicAdd(&lsum[found[j]], (unsigned long long)dur[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < S && !LEAN && !EXPO; ++j) {
       if (found[j] != kNotFound) {
         const uint32_t b = bkt[j];
         // diag 4096: spread the atomics over slots by lane (prices same-address
@@ -910,7 +962,22 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 2] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
   const uint32_t nq = *hq_n < kHllQueue ? *hq_n : kHllQueue;
-  if constexpr (LC != 0 && NWC != 0 && EPI) {
+  if constexpr (EXPO) {
+    // this workgroup's header partials -> its slab (touched slots only; the
+    // reduce pass zeroes what it consumed)
+    XHdr *xs = P.xslab + (uint64_t)blockIdx.x * cap;
+    for (uint32_t sl = threadIdx.x; sl < cap; sl += kLdsBlock)
+      if (const uint32_t c = xcnt[sl]) xs[sl] = XHdr{c, xzero[sl], lsum[sl], xminx[sl], xmax[sl]};
+    if (err_lds) {  // this workgroup's ERROR counts -> its private slab (plain RMW)
+      const uint32_t e = etab[threadIdx.x];
+      if (e) {
+        uint32_t *cell = P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1);
+        *cell += e & 0xFFFFu;
+      }
+    }
+    for (uint32_t i = threadIdx.x; i < nq; i += kLdsBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
+    hll_lb_refresh(P, threadIdx.x >> 6, kWaves);
+  } else if constexpr (LC != 0 && NWC != 0 && EPI) {
     // compile-time geometry: the batched epilogue (one round trip)
     constexpr uint32_t kCap = 1u << LC;
     static_assert((kCap * NWC / 2) % kLdsBlock == 0 && (kCap / 2) % kLdsBlock == 0, "epilogue geometry");
@@ -1634,6 +1701,19 @@ hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_
   const void *fn = small_fn(P.bintab != nullptr, variant, P.diag != 0 || P.dbg != nullptr);
   void *args[] = {const_cast<IngestParams *>(&P)};
   return hipLaunchKernel(fn, dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);
+}
+
+static const void *expo_small_fn() {
+  return (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true, 1, true, true, true>;
+}
+
+hipError_t prepare_ingest_expo_small(size_t lds_bytes) {
+  return hipFuncSetAttribute(expo_small_fn(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+}
+
+hipError_t launch_ingest_expo_small(const IngestParams &P, uint32_t grid, size_t lds_bytes, hipStream_t s) {
+  void *args[] = {const_cast<IngestParams *>(&P)};
+  return hipLaunchKernel(expo_small_fn(), dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);
 }
 
 hipError_t launch_ingest_part(const IngestParams &P, hipStream_t s) {

@@ -56,13 +56,40 @@ def test_gpu_log_and_index_bit_exact():
         assert int(gi[0]) == i
 
 
+@pytest.mark.parametrize("path", ["small", "hbm"])
 @pytest.mark.parametrize("max_size,unit", [(160, "ms"), (8, "ms"), (20, "s"), (2, "ms")])
-def test_expo_histograms_match_oracle(max_size, unit):
+def test_expo_histograms_match_oracle(max_size, unit, path, monkeypatch):
+    """small: the small-table kernel in EXPO mode (LDS header partials, slab
+    reduce, LDS-cached bucket counts); hbm: the pass-1 global-atomic path."""
+    monkeypatch.setenv("SPANAGG_EXPO_SMALL", "1" if path == "small" else "0")
     wl = generate_c2(200_003, seed=13)
     with _engine(wl, exp_max_size=max_size, unit=unit) as e:
+        assert e.stats()["small_table"] == (1 if path == "small" else 0)
         e.ingest(wl.batch)
         res = e.flush_exp()
         _check(res, wl.batch, max_size, unit == "s")
+
+
+@pytest.mark.slow
+def test_expo_small_table_full_size_device_launches():
+    """C2 at its full 10 M spans through sa_ingest_device in two launches
+    (the second one a fresh trace-id variant), the bench's c2expo shape."""
+    import torch
+
+    import bench
+    wl = generate_c2(10_000_000, seed=42)
+    dev = torch.device("cuda", 0)
+    cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(dev)
+            for c in wl.batch.columns()]
+    var = bench.trace_variants(cols[3], cols[4], 2, seed=5)
+    with _engine(wl, exp_max_size=160, key_capacity=1500) as e:
+        assert e.stats()["small_table"] == 1
+        for w0, w1 in var:
+            e.ingest_device(cols[0], cols[1], cols[2], w0, w1, cols[5])
+        res = e.flush_exp()
+        both = SpanBatch(*[np.concatenate([c, c]) for c in wl.batch.columns()])
+        _check(res, both, 160)
+        assert int(res.count.sum()) == 2 * len(wl.batch) - 2 * int((wl.batch.key_hash == 0).sum())
 
 
 def test_expo_state_across_launches_and_delta_flushes():
