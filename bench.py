@@ -646,7 +646,8 @@ def main():
                            "cgroup_quota_cpus": cores["cgroup_quota_cpus"]})
                 result["cpu_baseline_multicore"] = mc
         if world == 1 and args.host_otlp_spans > 0:
-            result["host_otlp"] = host_otlp_rate(args.host_otlp_spans)
+            # the box's usable cores (its cgroup CPU share), at most 16 decode threads
+            result["host_otlp"] = host_otlp_rate(args.host_otlp_spans, threads=max(1, min(16, box_cores()["usable"])))
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

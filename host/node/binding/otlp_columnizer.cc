@@ -543,6 +543,36 @@ uint32_t Columnizer::service_id(const std::string &name, bool *is_new) {
 }
 
 // ---------------------------------------------------------------- columns, caches, threads
+namespace {
+HostAllocFn g_host_alloc = nullptr;
+HostFreeFn g_host_free = nullptr;
+constexpr size_t kColHdr = 64;  // block header: the block's kind (1 = page-locked), keeps 64-B alignment
+}  // namespace
+
+void set_host_allocator(HostAllocFn a, HostFreeFn f) {
+  g_host_alloc = a;
+  g_host_free = f;
+}
+
+void *col_alloc(size_t bytes, bool pinned) {
+  unsigned char *raw = nullptr;
+  uint64_t kind = 0;
+  if (pinned && g_host_alloc) {
+    raw = static_cast<unsigned char *>(g_host_alloc(bytes + kColHdr));
+    kind = raw ? 1 : 0;
+  }
+  if (!raw) raw = static_cast<unsigned char *>(::operator new(bytes + kColHdr, std::align_val_t(kColHdr)));
+  *reinterpret_cast<uint64_t *>(raw) = kind;
+  return raw + kColHdr;
+}
+
+void col_free(void *p) {
+  if (!p) return;
+  unsigned char *raw = static_cast<unsigned char *>(p) - kColHdr;
+  if (*reinterpret_cast<uint64_t *>(raw) == 1 && g_host_free) g_host_free(raw);
+  else ::operator delete(raw, std::align_val_t(kColHdr));
+}
+
 void Cols::truncate(size_t n) {
   key.resize(n), start.resize(n), end.resize(n), w0.resize(n), w1.resize(n), meta.resize(n);
 }
@@ -595,10 +625,12 @@ void SigCache::insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view
 struct Columnizer::Worker {
   Cols cols;
   SigCache cache;
-  std::vector<Attr> rattrs, sattrs;
+  std::vector<Attr> rattrs, sattrs, eattrs;
   std::vector<const Attr *> hv;
-  std::string tmp, keystr, sname, service;
+  std::string tmp, keystr, sname, service, evkey;
   std::vector<uint8_t> hbuf;
+  std::vector<std::pair<const uint8_t *, const uint8_t *>> evs;  // the span's Event messages
+  std::unordered_map<uint64_t, uint32_t> exl;                     // this request's exemplar candidates per series
 };
 
 struct Columnizer::Undo {
@@ -659,10 +691,32 @@ struct Columnizer::Pool {
 Columnizer::Columnizer(Options o) : opt_(std::move(o)), main_(new Worker) {}
 Columnizer::~Columnizer() = default;
 
+namespace {
+// the connector's internal keys (connector.js OVERFLOW_KEY, EVENT_KEY_PREFIX)
+const std::string kOverflowKey = std::string("\x01") + "otel.metric.overflow";
+const std::string kEventKeyPrefix = std::string(1, '\x02') + "events" + std::string(1, '\0');
+bool span_key(const std::string &k) { return k.empty() || (k[0] != '\x01' && k[0] != '\x02'); }
+}  // namespace
+
 void Columnizer::learn(uint64_t rhash, const std::string &key, uint64_t sid) {
-  res_keys_[rhash][key] = sid;
+  auto &keys = res_keys_[rhash];
+  if (keys.emplace(key, sid).second && span_key(key)) ++nspan_[rhash];
+  keys[key] = sid;
   owner_[sid] = std::make_pair(rhash, key);
   ++gen_;
+}
+
+void Columnizer::accept_exemplars(Result &r) {
+  if (r.exemplars.empty()) return;
+  size_t k = 0;
+  for (const SpanRef &x : r.exemplars) {
+    uint32_t &c = ex_count_[x.sid];
+    if (c < opt_.exemplars_max) {
+      ++c;
+      r.exemplars[k++] = x;
+    }
+  }
+  r.exemplars.resize(k);
 }
 
 void Columnizer::remap(uint64_t from, uint64_t to) {
@@ -692,7 +746,9 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
   auto &rattrs = w.rattrs, &sattrs = w.sattrs;
   std::string &tmp = w.tmp, &keystr = w.keystr, &sname = w.sname, &service = w.service;
   auto &hbuf = w.hbuf;
-  const bool use_cache = opt_.dims.empty();
+  // the signature cache skips building the key string, which events need
+  const bool use_cache = opt_.dims.empty() && !opt_.events;
+  w.exl.clear();
   PB req(buf, buf + len);
   uint32_t f;
   int wt;
@@ -773,6 +829,29 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
     }
     auto &keys = rit->second;
     res.resources.push_back(rhash);
+    // a new series id for `key` of this resource (exclusive calls only): seed
+    // 0, 1, ... until the id is neither 0 (reserved) nor another series'
+    auto intern = [&](const std::string &key) -> uint64_t {
+      hbuf.resize(8 + key.size());
+      std::memcpy(hbuf.data(), &rhash, 8);
+      std::memcpy(hbuf.data() + 8, key.data(), key.size());
+      uint64_t id = 0;
+      for (uint64_t seed = 0;; ++seed) {
+        id = (opt_.test_collide_seed0 && seed == 0) ? 42 : xxh64(hbuf.data(), hbuf.size(), seed);
+        if (id == 0) continue;
+        auto o = owner_.find(id);
+        if (o == owner_.end()) {
+          owner_.emplace(id, std::make_pair(rhash, key));
+          undo->sids.push_back(id);
+          break;
+        }
+        if (o->second.first == rhash && o->second.second == key) break;
+      }
+      keys.emplace(key, id);
+      undo->keys.emplace_back(rhash, key);
+      if (span_key(key)) ++nspan_[rhash];
+      return id;
+    };
     uint32_t svc_id;
     if constexpr (kShared) {
       auto it = services_.find(service);
@@ -812,6 +891,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
         int32_t kind = 0, code = 0;
         uint64_t st = 0, en = 0;
         sattrs.clear();
+        if (opt_.events) w.evs.clear();
         uint32_t k;
         int wt4;
         while (sp.next(k, wt4)) {
@@ -831,6 +911,9 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
             Attr a;
             if (!parse_kv(sp.sub(), a.key, a.val)) return fail(Result::kError, "malformed KeyValue");
             sattrs.push_back(a);
+          } else if (k == 11 && wt4 == 2 && opt_.events) {
+            const PB ev = sp.sub();
+            w.evs.emplace_back(ev.p, ev.end);
           } else if (k == 15 && wt4 == 2) {
             PB stt = sp.sub();
             uint32_t m;
@@ -886,31 +969,39 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
             keystr += tmp;
           }
           auto kit = keys.find(keystr);
+          bool overflow = false;
           if (kit != keys.end()) {
             sid = kit->second;
           } else {
             if constexpr (kShared) return false;
-            hbuf.resize(8 + keystr.size());
-            std::memcpy(hbuf.data(), &rhash, 8);
-            std::memcpy(hbuf.data() + 8, keystr.data(), keystr.size());
-            // seed 0, 1, ... until the id is neither 0 (reserved) nor another series'
-            for (uint64_t seed = 0;; ++seed) {
-              sid = (opt_.test_collide_seed0 && seed == 0) ? 42 : xxh64(hbuf.data(), hbuf.size(), seed);
-              if (sid == 0) continue;
-              auto o = owner_.find(sid);
-              if (o == owner_.end()) {
-                owner_.emplace(sid, std::make_pair(rhash, keystr));
-                undo->sids.push_back(sid);
-                break;
+            auto ns = nspan_.find(rhash);
+            if (opt_.card_limit && ns != nspan_.end() && ns->second >= opt_.card_limit) {
+              // aggregation_cardinality_limit: the resource's overflow series
+              overflow = true;
+              auto ov = keys.find(kOverflowKey);
+              if (ov != keys.end()) {
+                sid = ov->second;
+              } else {
+                sid = intern(kOverflowKey);
+                res.new_series.push_back(
+                    {sid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});
               }
-              if (o->second.first == rhash && o->second.second == keystr) break;
+            } else {
+              sid = intern(keystr);
+              res.new_series.push_back(
+                  {sid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});
             }
-            keys.emplace(keystr, sid);
-            undo->keys.emplace_back(rhash, keystr);
-            res.new_series.push_back(
-                {sid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});
           }
-          if (use_cache) cache.insert(sig, rhash, svc_id, name, kind, code, sid);
+          // (an overflowed key is decided again each time: the count it met may change)
+          if (use_cache && !overflow) cache.insert(sig, rhash, svc_id, name, kind, code, sid);
+        }
+        if (opt_.exemplars) {  // candidates; accept_exemplars keeps the interval's first ones
+          auto ex = ex_count_.find(sid);
+          uint32_t &mine = w.exl[sid];
+          if ((ex == ex_count_.end() ? 0u : ex->second) + mine < opt_.exemplars_max) {
+            ++mine;
+            res.exemplars.push_back({sid, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});
+          }
         }
         out.key.push_back(sid);
         out.start.push_back(st);
@@ -927,6 +1018,61 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
         const uint32_t cc = code >= 0 && code <= 3 ? (uint32_t)code : 3u;
         out.meta.push_back(svc_id | (kk << 16) | (cc << 19));
         ++res.spans;
+        // events.enabled: one record per event, keyed by the span key and the
+        // event dimensions (connector.js _eventId), counted as a span of
+        // duration 0 with an out-of-range service id (no sketch)
+        for (uint32_t ei = 0; opt_.events && ei < (uint32_t)w.evs.size(); ++ei) {
+          auto &eattrs = w.eattrs;
+          eattrs.clear();
+          PB ev(w.evs[ei].first, w.evs[ei].second);
+          uint32_t m;
+          int wt5;
+          while (ev.next(m, wt5)) {
+            if (m == 3 && wt5 == 2) {
+              Attr a;
+              if (!parse_kv(ev.sub(), a.key, a.val)) return fail(Result::kError, "malformed KeyValue");
+              eattrs.push_back(a);
+            } else {
+              ev.skip(wt5);
+            }
+          }
+          if (!ev.ok) return fail(Result::kError, "malformed Span.Event");
+          dedupe_last(eattrs);
+          std::string &ek = w.evkey;
+          ek.assign(kEventKeyPrefix);
+          ek += keystr;
+          for (const Dim &d : opt_.event_dims) {
+            const Any *v = find_attr(eattrs, d.name);
+            if (v) {
+              if (const Keyable kb = as_string(*v, tmp); kb != Keyable::kYes)
+                return kb == Keyable::kTooDeep ? fail(Result::kError, "attribute value nested too deeply")
+                                               : fail(Result::kFallback, "event dimension not keyable natively");
+            } else if (d.has_default) {
+              tmp = d.def;
+            } else {
+              continue;
+            }
+            ek += '\0';
+            ek += tmp;
+          }
+          uint64_t esid;
+          auto eit = keys.find(ek);
+          if (eit != keys.end()) {
+            esid = eit->second;
+          } else {
+            if constexpr (kShared) return false;
+            esid = intern(ek);
+            res.new_event_series.push_back(
+                {esid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin), ei});
+          }
+          out.key.push_back(esid);
+          out.start.push_back(0);
+          out.end.push_back(0);
+          out.w0.push_back(0);
+          out.w1.push_back(0);
+          out.meta.push_back(0xFFFFu);
+          ++res.event_records;
+        }
       }
       if (!ss.ok) return fail(Result::kError, "malformed ScopeSpans");
     }
@@ -936,7 +1082,11 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
   return true;
 }
 
-Result Columnizer::columnize(const uint8_t *buf, size_t len) { return columnize_into(buf, len, buf_); }
+Result Columnizer::columnize(const uint8_t *buf, size_t len) {
+  Result r = columnize_into(buf, len, buf_);
+  accept_exemplars(r);
+  return r;
+}
 
 Result Columnizer::columnize_into(const uint8_t *buf, size_t len, Cols &out) {
   if (cache_.gen != gen_) cache_.clear(), cache_.gen = gen_;
@@ -951,6 +1101,10 @@ Result Columnizer::columnize_into(const uint8_t *buf, size_t len, Cols &out) {
   for (auto &k : undo.keys) {
     auto it = res_keys_.find(k.first);
     if (it != res_keys_.end()) it->second.erase(k.second);
+    if (span_key(k.second)) {
+      auto ns = nspan_.find(k.first);
+      if (ns != nspan_.end() && ns->second) --ns->second;
+    }
   }
   for (uint64_t h : undo.resources) res_keys_.erase(h);
   for (uint64_t sid : undo.sids) owner_.erase(sid);
@@ -1027,6 +1181,7 @@ BatchResult Columnizer::columnize_batch(const uint8_t *const *bufs, const size_t
       s.cnt = excl_.size() - s.off;
       s.max_end = excl_.max_end;
     }
+    accept_exemplars(s.r);
     s.dst = buf_.size() + total;
     total += s.cnt;
     if (s.max_end > buf_.max_end) buf_.max_end = s.max_end;

@@ -54,11 +54,33 @@ struct Options {
   std::vector<std::string> key_attributes;  // resource_metrics_key_attributes (empty = all)
   bool test_collide_seed0 = false;          // tests only: every seed-0 series id is 42
   unsigned threads = 1;                     // columnize_batch worker threads (caller included)
+  // aggregation_cardinality_limit: past this many span series in a resource,
+  // new keys share the resource's overflow series (0 = unlimited)
+  uint32_t card_limit = 0;
+  // exemplars.enabled / max_per_data_point: the first `exemplars_max` spans
+  // of every series per export interval are reported (their offsets)
+  bool exemplars = false;
+  uint32_t exemplars_max = 5;
+  // events.enabled / events.dimensions: one record per span event, keyed by
+  // the span's key and the event dimensions
+  bool events = false;
+  std::vector<Dim> event_dims;
 };
 
 struct NewSeries {
   uint64_t sid, res_hash;
   uint32_t span_off, span_len;  // the Span message inside the request bytes
+};
+
+// An exemplar candidate / a new event series: the span (offsets in the
+// request bytes) and, for events, which of its events
+struct SpanRef {
+  uint64_t sid;
+  uint32_t span_off, span_len;
+};
+struct NewEventSeries {
+  uint64_t sid, res_hash;
+  uint32_t span_off, span_len, event;
 };
 
 struct NewResource {
@@ -75,6 +97,9 @@ struct Result {
   std::vector<NewSeries> new_series;
   std::vector<uint64_t> resources;  // resource hash of every ResourceSpans that contributed
   std::vector<std::pair<std::string, uint32_t>> new_services;
+  std::vector<SpanRef> exemplars;                 // accepted exemplar spans, in arrival order
+  std::vector<NewEventSeries> new_event_series;   // event series this request made
+  uint64_t event_records = 0;                     // event records appended to the columns
 };
 
 struct BatchResult {
@@ -82,11 +107,41 @@ struct BatchResult {
   size_t done = 0;              // requests taken: all, or up to and including the first fallback
 };
 
+// Column storage.  The columnizer's output buffer asks for page-locked host
+// memory through hooks the addon installs (libspanagg's sa_host_alloc), so
+// sa_ingest DMAs it to HBM without packing a staging copy on the calling
+// thread; worker scratch and any failed pinned allocation use the heap.
+// Every block carries a 64-B header naming its kind, for deallocation.
+using HostAllocFn = void *(*)(size_t);
+using HostFreeFn = void (*)(void *);
+void set_host_allocator(HostAllocFn a, HostFreeFn f);
+void *col_alloc(size_t bytes, bool pinned);
+void col_free(void *p);
+template <class T>
+struct ColAlloc {
+  using value_type = T;
+  bool pinned = false;
+  ColAlloc() = default;
+  explicit ColAlloc(bool p) : pinned(p) {}
+  template <class U>
+  ColAlloc(const ColAlloc<U> &o) : pinned(o.pinned) {}
+  T *allocate(size_t n) { return static_cast<T *>(col_alloc(n * sizeof(T), pinned)); }
+  void deallocate(T *p, size_t) { col_free(p); }
+  bool operator==(const ColAlloc &o) const { return pinned == o.pinned; }
+  bool operator!=(const ColAlloc &o) const { return pinned != o.pinned; }
+};
+template <class T>
+using ColVec = std::vector<T, ColAlloc<T>>;
+
 // SoA v1 columns under construction
 struct Cols {
-  std::vector<uint64_t> key, start, end, w0, w1;
-  std::vector<uint32_t> meta;
+  ColVec<uint64_t> key, start, end, w0, w1;
+  ColVec<uint32_t> meta;
   uint64_t max_end = 0;
+  Cols() = default;
+  explicit Cols(bool pinned)
+      : key(ColAlloc<uint64_t>(pinned)), start(ColAlloc<uint64_t>(pinned)), end(ColAlloc<uint64_t>(pinned)),
+        w0(ColAlloc<uint64_t>(pinned)), w1(ColAlloc<uint64_t>(pinned)), meta(ColAlloc<uint32_t>(pinned)) {}
   size_t size() const { return key.size(); }
   void truncate(size_t n);
   void append(const Cols &o, size_t off, size_t n);
@@ -130,13 +185,15 @@ class Columnizer {
   BatchResult columnize_batch(const uint8_t *const *bufs, const size_t *lens, size_t n);
 
   uint32_t service_id(const std::string &name, bool *is_new);
-  void forget_resource(uint64_t hash) { res_keys_.erase(hash), ++gen_; }
+  void forget_resource(uint64_t hash) { res_keys_.erase(hash), nspan_.erase(hash), ++gen_; }
   // the host interned (resource, key) as `sid` (a series its JavaScript path saw first)
   void learn(uint64_t rhash, const std::string &key, uint64_t sid);
   // the host's id for a series this columnizer reported as `from` is `to`:
   // buffered spans and the dictionary follow (the host's dictionary decides)
   void remap(uint64_t from, uint64_t to);
   void clear_buffer() { buf_.clear(); }
+  // a new export interval: every series may take exemplars again
+  void reset_exemplars() { ex_count_.clear(); }
 
   size_t buffered() const { return buf_.size(); }
   uint64_t max_end() const { return buf_.max_end; }
@@ -156,7 +213,7 @@ class Columnizer {
   bool run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCache &cache, Result &res, Undo *undo);
 
   Options opt_;
-  Cols buf_, excl_;  // excl_: columns of a batch's exclusively redone requests
+  Cols buf_{true}, excl_;  // buf_: page-locked when possible; excl_: a batch's exclusively redone requests
   SigCache cache_;
   uint64_t gen_ = 0;  // bumped whenever an existing dictionary entry may change
   std::unique_ptr<Worker> main_;
@@ -168,6 +225,12 @@ class Columnizer {
   // is re-salted (seed + 1) instead of shared; kept after a resource is
   // forgotten, so the same series gets the same id when it comes back
   std::unordered_map<uint64_t, std::pair<uint64_t, std::string>> owner_;
+  // span series per resource (aggregation_cardinality_limit)
+  std::unordered_map<uint64_t, uint32_t> nspan_;
+  // exemplars taken per series this export interval (written in request order)
+  std::unordered_map<uint64_t, uint32_t> ex_count_;
+  // keeps the request's exemplar candidates that the interval still wants
+  void accept_exemplars(Result &r);
 };
 
 // exposed for tests of the building blocks

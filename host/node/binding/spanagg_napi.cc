@@ -693,6 +693,40 @@ napi_value CreateColumnizer(napi_env env, napi_callback_info info) {
     if (!is_undefined(env, tc)) napi_get_value_bool(env, tc, &b);
     o.test_collide_seed0 = b;
   }
+  {  // aggregation_cardinality_limit, exemplars, events (connector.js normalizeConfig)
+    napi_value v = prop(env, argv[1], "cardinalityLimit");
+    uint32_t u = 0;
+    if (!is_undefined(env, v) && napi_get_value_uint32(env, v, &u) != napi_ok)
+      return throw_type(env, "cardinalityLimit must be a number");
+    o.card_limit = u;
+    bool b = false;
+    v = prop(env, argv[1], "exemplars");
+    if (!is_undefined(env, v)) napi_get_value_bool(env, v, &b);
+    o.exemplars = b;
+    v = prop(env, argv[1], "exemplarsMax");
+    u = 5;
+    if (!is_undefined(env, v) && napi_get_value_uint32(env, v, &u) != napi_ok)
+      return throw_type(env, "exemplarsMax must be a number");
+    o.exemplars_max = u;
+    b = false;
+    v = prop(env, argv[1], "events");
+    if (!is_undefined(env, v)) napi_get_value_bool(env, v, &b);
+    o.events = b;
+    v = prop(env, argv[1], "eventDims");
+    if (!is_undefined(env, v)) {
+      if (!array_items(env, v, &items, "eventDims")) return nullptr;
+      for (napi_value d : items) {
+        otlpcol::Dim dim;
+        if (!get_string(env, prop(env, d, "name"), &dim.name, "eventDims[].name")) return nullptr;
+        napi_value def = prop(env, d, "default");
+        if (!is_undefined(env, def)) {
+          dim.has_default = true;
+          if (!get_string(env, def, &dim.def, "eventDims[].default")) return nullptr;
+        }
+        o.event_dims.push_back(std::move(dim));
+      }
+    }
+  }
   {
     napi_value th = prop(env, argv[1], "threads");
     uint32_t t = 1;
@@ -751,6 +785,33 @@ napi_value result_obj(napi_env env, const otlpcol::Result &r, bool lean) {
     }
     set(env, o, "newSeries", arr);
   }
+  if (!lean || !r.exemplars.empty()) {
+    napi_create_array_with_length(env, r.exemplars.size(), &arr);
+    for (size_t i = 0; i < r.exemplars.size(); ++i) {
+      napi_value e;
+      napi_create_object(env, &e);
+      set(env, e, "sid", big(env, r.exemplars[i].sid));
+      set(env, e, "off", num(env, r.exemplars[i].span_off));
+      set(env, e, "len", num(env, r.exemplars[i].span_len));
+      napi_set_element(env, arr, (uint32_t)i, e);
+    }
+    set(env, o, "exemplars", arr);
+  }
+  if (!lean || !r.new_event_series.empty()) {
+    napi_create_array_with_length(env, r.new_event_series.size(), &arr);
+    for (size_t i = 0; i < r.new_event_series.size(); ++i) {
+      napi_value e;
+      napi_create_object(env, &e);
+      set(env, e, "sid", big(env, r.new_event_series[i].sid));
+      set(env, e, "resHash", big(env, r.new_event_series[i].res_hash));
+      set(env, e, "off", num(env, r.new_event_series[i].span_off));
+      set(env, e, "len", num(env, r.new_event_series[i].span_len));
+      set(env, e, "event", num(env, r.new_event_series[i].event));
+      napi_set_element(env, arr, (uint32_t)i, e);
+    }
+    set(env, o, "newEventSeries", arr);
+  }
+  if (!lean || r.event_records) set(env, o, "eventRecords", num(env, (double)r.event_records));
   if (!lean || !r.new_services.empty()) {
     napi_create_array_with_length(env, r.new_services.size(), &arr);
     for (size_t i = 0; i < r.new_services.size(); ++i) {
@@ -813,6 +874,17 @@ napi_value ColumnizeBatch(napi_env env, napi_callback_info info) {
   }
   set(env, o, "results", arr);
   return o;
+}
+
+// columnizerResetExemplars(c): a new export interval (every series may take
+// exemplars again)
+napi_value ColumnizerResetExemplars(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
+  ColHandle *c = get_col(env, argv[0]);
+  if (!c) return nullptr;
+  c->col.reset_exemplars();
+  return nullptr;
 }
 
 napi_value ColumnizerIngest(napi_env env, napi_callback_info info) {
@@ -926,7 +998,15 @@ napi_value ColumnizerSelfTest(napi_env env, napi_callback_info info) {
   return throw_status(env, SA_EINVAL, "unknown self-test");
 }
 
+// page-locked column buffers for the native columnizer (sa_ingest then DMAs
+// them without a staging copy); nullptr -> the columnizer uses the heap
+void *host_alloc_hook(size_t bytes) {
+  void *p = nullptr;
+  return sa_host_alloc(bytes, &p) == SA_OK ? p : nullptr;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
+  otlpcol::set_host_allocator(&host_alloc_hook, &sa_host_free);
     struct Fn {
         const char *name;
         napi_callback cb;
@@ -947,6 +1027,7 @@ napi_value Init(napi_env env, napi_value exports) {
                {"createColumnizer", CreateColumnizer},
                {"columnize", Columnize},
                {"columnizeBatch", ColumnizeBatch},
+               {"columnizerResetExemplars", ColumnizerResetExemplars},
                {"columnizerIngest", ColumnizerIngest},
                {"columnizerTake", ColumnizerTake},
                {"columnizerServiceId", ColumnizerServiceId},

@@ -175,18 +175,22 @@ class SpanMetricsConnector {
       cmsW: c.cmsW, windowNs: c.windowNs, nWindows: c.nWindows, nServices: c.nServices,
       keyCapacity: c.keyCapacity, device: c.device, expMaxSize: c.expMaxSize, ...(c.devices ? { devices: c.devices } : {}) });
     this.cols = new Columns(c.batchSize);
-    // native OTLP columnizer (binding/otlp_columnizer.cc) for request bytes, when
-    // every enabled option is one it implements; otherwise the JS path below
+    // native OTLP columnizer (binding/otlp_columnizer.cc) for request bytes
+    // (dimensions, exclusions, rules, resource key attributes, the cardinality
+    // limit, exemplars and events are all native); the JS path below takes the
+    // requests it reports as fallbacks
     this.col = null;
     this.nativeMaxEnd = 0n;
     this.nativeBuffered = 0;
     this.nativeRequests = 0;
     this.jsRequests = 0;
     if (opts.native !== false && typeof this.addon.createColumnizer === 'function' &&
-        !c.events && !c.exemplars && !c.cardinalityLimit && this.rules.every((r) => r.native)) {
+        this.rules.every((r) => r.native)) {
       this.col = this.addon.createColumnizer(this.handle, { dims: c.dims,
         exclude: [...c.exclude], rules: this.rules.map((r) => r.native),
-        keyAttributes: c.resourceKeyAttributes, threads: c.columnizerThreads });
+        keyAttributes: c.resourceKeyAttributes, threads: c.columnizerThreads,
+        cardinalityLimit: c.cardinalityLimit, exemplars: c.exemplars, exemplarsMax: c.exemplarsMax,
+        events: c.events, eventDims: c.eventDims });
     }
     this.resources = new Map();   // resHash -> resource record (LRU order: oldest first)
     this.evicted = new Map();     // evicted this flush interval, revivable until export
@@ -203,6 +207,7 @@ class SpanMetricsConnector {
     this.collisions = 0;          // series ids re-salted after a 64-bit collision
     this._verifyingNative = false;
     this.eventRecords = 0;
+    this.nativeRemaps = 0;  // native series ids the host dictionary replaced (collisions)
     this.ticker = null;
   }
 
@@ -271,8 +276,7 @@ class SpanMetricsConnector {
     if (this.resources.size > this.cfg.resourceCacheSize) {
       const [oldest, rec] = this.resources.entries().next().value;
       this.resources.delete(oldest);
-      this.evicted.set(oldest, rec);
-      if (this.col) this.addon.columnizerForget(this.col, oldest);
+      this.evicted.set(oldest, rec);  // the native side keeps its keys until export drops it
     }
     return r;
   }
@@ -452,9 +456,6 @@ class SpanMetricsConnector {
           const spanAttrs = this.cfg.dims.length ? keys.attrMap(span.attributes) : undefined;
           const sid = this._seriesId(res, service, span, resAttrs, spanAttrs);
           if (this.cfg.exemplars) this._exemplar(sid, span);
-          if (this.cfg.events && span.events && span.events.length) {
-            for (const ev of span.events) this._pushEvent(this._eventId(res, service, span, resAttrs, spanAttrs, ev));
-          }
           const i = cols.n;
           cols.keyHash[i] = sid;
           cols.startNs[i] = BigInt.asUintN(64, BigInt(span.startTimeUnixNano || 0));
@@ -473,6 +474,10 @@ class SpanMetricsConnector {
           cols.meta[i] = (svcId | (kind << 16) | (st << 19)) >>> 0;
           cols.n = i + 1;
           if (cols.n === cols.cap) this._drain();
+          // events.enabled: the span's event records follow it (the native order)
+          if (this.cfg.events && span.events && span.events.length) {
+            for (const ev of span.events) this._pushEvent(this._eventId(res, service, span, resAttrs, spanAttrs, ev));
+          }
         }
       }
     }
@@ -497,6 +502,7 @@ class SpanMetricsConnector {
 
   /** Host bookkeeping of one native columnize result (false: fallback). */
   _applyNative(r, bytes) {
+    let remapped = null;  // native -> host ids of this request's series (64-bit collisions)
     if (r.status === 'fallback') return false;
     if (r.status !== 'ok') throw new Error(`OTLP request: ${r.error}`);
     this.nativeRequests += 1;
@@ -525,7 +531,36 @@ class SpanMetricsConnector {
       }
       // the host dictionary decides: after a collision the two sides can differ
       // (the native side does not see series interned by a JavaScript-path request)
-      if (sid !== ns.sid) this.addon.columnizerRemap(this.col, ns.sid, sid);
+      if (sid !== ns.sid) {
+        this.addon.columnizerRemap(this.col, ns.sid, sid);
+        this.nativeRemaps += 1;
+        (remapped || (remapped = new Map())).set(ns.sid, sid);
+      }
+    }
+    for (const ne of r.newEventSeries || NONE) {  // events.enabled: verified as the JS path keys them
+      const res = this.resources.get(ne.resHash) || this.evicted.get(ne.resHash);
+      if (!res) throw new Error('native event series for an unknown resource');
+      const span = otlp.decodeSpan(new otlp.Reader(bytes, ne.off, ne.off + ne.len));
+      span.name = applyRules(span.name, this.rules);
+      const svc = res.attributes.get(keys.SERVICE_NAME_KEY);
+      const service = svc && svc.type === 'string' ? svc.value : '';
+      const spanAttrs = this.cfg.dims.length ? keys.attrMap(span.attributes) : undefined;
+      this._verifyingNative = true;
+      let sid;
+      try {
+        sid = this._eventId(res, service, span, res.attributes, spanAttrs, span.events[ne.event]);
+      } finally {
+        this._verifyingNative = false;
+      }
+      if (sid !== ne.sid) {
+        this.addon.columnizerRemap(this.col, ne.sid, sid);
+        this.nativeRemaps += 1;
+      }
+    }
+    if (r.eventRecords) this.eventRecords += r.eventRecords;
+    for (const ex of r.exemplars || NONE) {  // exemplars.enabled: the native side's candidates, in order
+      const sid = remapped && remapped.has(ex.sid) ? remapped.get(ex.sid) : ex.sid;
+      if (this.series.has(sid)) this._exemplar(sid, otlp.decodeSpan(new otlp.Reader(bytes, ex.off, ex.off + ex.len)));
     }
     return true;
   }
@@ -632,6 +667,7 @@ class SpanMetricsConnector {
     // resetState: delta purges; cumulative drops what the LRU evicted
     for (const res of this.evicted.values()) {
       for (const sid of res.sids) { this.series.delete(sid); this.lastDeltaTs.delete(sid); }
+      if (this.col) this.addon.columnizerForget(this.col, res.hash);
     }
     this.evicted.clear();
     if (delta) for (const sid of touched) this.series.get(sid) && (this.series.get(sid).counts = null);
@@ -703,6 +739,7 @@ class SpanMetricsConnector {
       hists.push(h);
       s.exemplars = [];  // exemplars cover one export interval, both temporalities
     }
+    if (this.col && c.exemplars && this.addon.columnizerResetExemplars) this.addon.columnizerResetExemplars(this.col);
     const out = [
       { name: ns + 'calls', sum: { dataPoints: calls, aggregationTemporality: temporality, isMonotonic: true } },
       c.expMaxSize
@@ -783,7 +820,8 @@ class SpanMetricsConnector {
     return Object.assign(s, { resources: this.resources.size, series: this.series.size,
       services: this.services.size, droppedFlushes: this.droppedFlushes, droppedSpans: this.droppedSpans,
       collisions: this.collisions,
-      eventRecords: this.eventRecords, nativeRequests: this.nativeRequests, jsRequests: this.jsRequests });
+      eventRecords: this.eventRecords, nativeRequests: this.nativeRequests, jsRequests: this.jsRequests,
+      nativeRemaps: this.nativeRemaps });
   }
 }
 

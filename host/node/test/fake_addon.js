@@ -175,6 +175,7 @@ class NativeColumnizerFakeAddon extends FakeAddon {
   columnizerForget(c, h) { return this.real.columnizerForget(c, h); }
   columnizerLearn(c, h, key, sid) { return this.real.columnizerLearn(c, h, key, sid); }
   columnizerRemap(c, from, to) { return this.real.columnizerRemap(c, from, to); }
+  columnizerResetExemplars(c) { return this.real.columnizerResetExemplars(c); }
   columnizerIngest(c) {
     const b = this.real.columnizerTake(c);
     this.ingest(null, b);

@@ -520,7 +520,55 @@ test('native columnizer: same columns and same OTLP metrics as the JavaScript pa
     assert.deepStrictEqual(nat.cols, js.cols, JSON.stringify(cfg));
     assert.deepStrictEqual(nat.exports, js.exports, JSON.stringify(cfg));
     assert.deepStrictEqual(nat.services, js.services);
+    assert.strictEqual(nat.stats.nativeRemaps, 0, JSON.stringify(cfg));
   }
+});
+
+function eventRequests() {
+  const ev = (t, x) => ({ timeUnixNano: 5n, name: 'exception', attributes: [
+    ...(t ? [{ key: 'exception.type', value: str(t) }] : []), ...(x ? [{ key: 'x', value: { type: 'int', value: x } }] : [])] });
+  const tid = (k) => Uint8Array.from({ length: 16 }, (_, i) => (i * 13 + k) & 255);
+  const reqs = [];
+  for (let r = 0; r < 6; r++) {
+    const spans = [];
+    for (let i = 0; i < 9; i++) {
+      spans.push(span(`op-${(r * 3 + i) % 7}`, { traceId: tid(r * 9 + i), status: { code: i % 4 === 0 ? 2 : 0 },
+        events: i % 3 === 0 ? [] : [ev(i % 2 ? 'IOError' : 'Timeout', BigInt(i % 3)), ...(i === 4 ? [ev(null), ev('IOError')] : [])] }));
+    }
+    reqs.push(request([[{ 'service.name': `svc-${r % 2}`, 'k8s.pod.name': `p-${r % 3}` }, spans],
+      [{ 'service.name': 'other' }, [span('lone', { events: [ev('E', 1n)] })]]]));
+  }
+  return reqs;
+}
+
+test('native columnizer: cardinality limit, exemplars and events == the JavaScript path', () => {
+  const reqs = mixedRequests().concat(eventRequests());
+  for (const [cfg, rules] of [
+    [{ aggregation_cardinality_limit: 3 }, DEMO_SPAN_NAME_RULES],
+    [{ aggregation_cardinality_limit: 2, dimensions: [{ name: 'http.status_code' }], resource_metrics_cache_size: 2 }, []],
+    [{ exemplars: { enabled: true, max_per_data_point: 2 } }, DEMO_SPAN_NAME_RULES],
+    [{ exemplars: { enabled: true, max_per_data_point: 1 }, aggregation_temporality: 'AGGREGATION_TEMPORALITY_DELTA' }, []],
+    [{ events: { enabled: true, dimensions: [{ name: 'exception.type' }, { name: 'x', default: 'none' }] } }, DEMO_SPAN_NAME_RULES],
+    [{ aggregation_cardinality_limit: 4, dimensions: [{ name: 'k8s.pod.name' }] }, DEMO_SPAN_NAME_RULES],
+    [{ events: { enabled: true, dimensions: [{ name: 'exception.type' }] },
+      aggregation_cardinality_limit: 4 }, DEMO_SPAN_NAME_RULES],
+    [{ events: { enabled: true, dimensions: [{ name: 'exception.type' }] }, exemplars: { enabled: true, max_per_data_point: 3 },
+      aggregation_cardinality_limit: 4, dimensions: [{ name: 'k8s.pod.name' }] }, DEMO_SPAN_NAME_RULES],
+  ]) {
+    const [nat, js] = runBoth(cfg, rules, reqs);
+    assert.ok(nat.stats.nativeRequests === reqs.length && nat.stats.jsRequests === 0, `${nat.stats.nativeRequests} ${nat.stats.jsRequests}`);
+    assert.deepStrictEqual(nat.cols, js.cols, JSON.stringify(cfg));
+    assert.deepStrictEqual(nat.exports, js.exports, JSON.stringify(cfg));
+    assert.strictEqual(nat.stats.eventRecords, js.stats.eventRecords);
+    assert.strictEqual(nat.stats.nativeRemaps, 0, JSON.stringify(cfg));  // the native side keyed every series as the host does
+    if (cfg.events) assert.ok(js.stats.eventRecords > 40);
+  }
+  // a limited resource really overflows, and exemplars really appear, on the native path
+  const [nat] = runBoth({ aggregation_cardinality_limit: 2, exemplars: { enabled: true } }, [], eventRequests());
+  const dec = nat.exports.map((h) => otlp.decodeMetrics(Buffer.from(h, 'hex')));
+  const calls = dec.flatMap((d) => dpsOf(d, 'traces.span.metrics.calls'));
+  assert.ok(calls.some((d) => attr(d, 'otel.metric.overflow')));
+  assert.ok(dec.flatMap((d) => dpsOf(d, 'traces.span.metrics.duration')).some((d) => d.exemplars && d.exemplars.length));
 });
 
 test('series ids: a 64-bit collision is re-salted on both paths (never thrown), outputs unchanged', () => {
@@ -575,8 +623,10 @@ test('native columnizer: consumeTracesBatch on worker threads == consumeTraces o
     }
     return rows.sort();
   };
+  for (const r of eventRequests()) reqs.push(otlp.encodeTraces(r));
   for (const cfg of [{}, { dimensions: [{ name: 'http.status_code' }, { name: 'k8s.pod.name' }] },
-    { resource_metrics_cache_size: 2 }]) {
+    { resource_metrics_cache_size: 2 },
+    { aggregation_cardinality_limit: 3, exemplars: { enabled: true }, events: { enabled: true, dimensions: [{ name: 'exception.type' }] } }]) {
     const out = [];
     for (const threads of [1, 4]) {
       const addon = new NativeColumnizerFakeAddon();

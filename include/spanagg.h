@@ -175,6 +175,13 @@ const char *sa_last_error(const sa_engine *e);
  * aggregation completes asynchronously -- every read (sa_flush*, sa_window_*,
  * sa_get_stats) and sa_sync wait for it, and a device error surfaces there. */
 int sa_ingest(sa_engine *e, const sa_span_batch *batch);
+/* Page-locked host memory for batch columns a host builds itself (the Node
+ * host's columnizer does): sa_ingest / sa_group_ingest copy columns that all
+ * lie in such memory to HBM by DMA straight from the caller's arrays, with no
+ * staging copy on the calling thread.  SA_ENOMEM when no GPU runtime can pin
+ * memory (the caller then uses ordinary memory, which sa_ingest stages). */
+int sa_host_alloc(size_t bytes, void **out);
+void sa_host_free(void *p);
 /* Device-resident batch (pointers into HBM of this engine's device).
  * `stream` is a hipStream_t (NULL = the engine's own stream). Asynchronous:
  * the batch must stay valid until the stream reaches this point. Ordered

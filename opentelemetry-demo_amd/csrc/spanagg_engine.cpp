@@ -765,6 +765,35 @@ int sa_ingest_device(sa_engine *e, const sa_span_batch *b, void *stream) {
   return ingest_on(e, b, s);
 }
 
+int sa_host_alloc(size_t bytes, void **out) {
+  if (!out) return SA_EINVAL;
+  *out = nullptr;
+  if (hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    *out = nullptr;
+    return SA_ENOMEM;
+  }
+  return SA_OK;
+}
+
+void sa_host_free(void *p) {
+  if (p) (void)hipHostFree(p);
+}
+
+// true when every column of the batch lies in page-locked host memory
+static bool batch_pinned(const sa_span_batch *b) {
+  const void *cols[6] = {b->key_hash, b->start_ns, b->end_ns, b->trace_w0, b->trace_w1, b->meta};
+  for (const void *c : cols) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, c) != hipSuccess) {
+      (void)hipGetLastError();  // pageable memory: an error the runtime must not keep
+      return false;
+    }
+    if (a.type != hipMemoryTypeHost) return false;
+  }
+  return true;
+}
+
 // Host batches: each chunk is packed into a pinned slot (CPU copy, 44 B/span),
 // copied to HBM by DMA and aggregated on the engine stream; the call returns
 // once the batch has been copied out of the caller's buffers, so the caller
@@ -784,6 +813,7 @@ int sa_ingest(sa_engine *e, const sa_span_batch *b) {
       SA_HIP(e, hipEventCreateWithFlags(&e->pin_ev[k], hipEventDisableTiming));
     }
   }
+  const bool pinned = batch_pinned(b);
   for (uint64_t off = 0; off < b->n; off += kChunk) {
     const uint64_t m = std::min(kChunk, b->n - off);
     const uint64_t ms = (m + 1) & ~1ULL;  // column stride: u64 columns stay 16-byte aligned
@@ -794,7 +824,14 @@ int sa_ingest(sa_engine *e, const sa_span_batch *b) {
     const uint64_t *src[5] = {b->key_hash + off, b->start_ns + off, b->end_ns + off, b->trace_w0 + off,
                               b->trace_w1 + off};
     char *d = static_cast<char *>(e->dstage[k]);
-    if (m >= sa::kHostPageableMin) {
+    if (pinned) {
+      // page-locked columns (sa_host_alloc): DMA straight from them, no
+      // packing; the copies are waited for after the last chunk
+      for (int c = 0; c < 5; ++c)
+        SA_HIP(e, hipMemcpyAsync(d + c * ms * 8, src[c], m * 8, hipMemcpyHostToDevice, e->stream));
+      SA_HIP(e, hipMemcpyAsync(d + 5 * ms * 8, b->meta + off, m * 4, hipMemcpyHostToDevice, e->stream));
+      SA_HIP(e, hipEventRecord(e->ev_b, e->stream));
+    } else if (m >= sa::kHostPageableMin) {
       // large chunks: the runtime's own staging of pageable memory copies
       // faster than one host thread packing the pinned slot.  HIP does not
       // promise that an asynchronous copy from pageable memory has taken the
@@ -817,6 +854,9 @@ int sa_ingest(sa_engine *e, const sa_span_batch *b) {
     SA_HIP(e, hipEventRecord(e->pin_ev[k], e->stream));
     e->pin_used[k] = true;
   }
+  // page-locked columns: every chunk's copies are done (stream order) once
+  // the last chunk's are, before the caller may reuse the arrays
+  if (pinned) SA_HIP(e, hipEventSynchronize(e->ev_b));
   return SA_OK;
 }
 

@@ -88,6 +88,8 @@ SIGNATURES = [
     ("sa_last_error", C.c_char_p, [C.c_void_p]),
     ("sa_ingest", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch)]),
     ("sa_ingest_device", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch), C.c_void_p]),
+    ("sa_host_alloc", C.c_int, [C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("sa_host_free", None, [C.c_void_p]),
     ("sa_sync", C.c_int, [C.c_void_p]),
     ("sa_flush", C.c_int, [C.c_void_p, C.POINTER(C.POINTER(sa_red_result))]),
     ("sa_red_result_free", None, [C.POINTER(sa_red_result)]),
