@@ -746,8 +746,9 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
   auto &rattrs = w.rattrs, &sattrs = w.sattrs;
   std::string &tmp = w.tmp, &keystr = w.keystr, &sname = w.sname, &service = w.service;
   auto &hbuf = w.hbuf;
-  // the signature cache skips building the key string, which events need
-  const bool use_cache = opt_.dims.empty() && !opt_.events;
+  // the signature cache skips building the key string (a span with events
+  // builds it anyway, for the event keys)
+  const bool use_cache = opt_.dims.empty();
   w.exl.clear();
   PB req(buf, buf + len);
   uint32_t f;
@@ -936,12 +937,10 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
           sig = SigCache::hash(rhash, svc_id, name, kind, code);
           hit = cache.find(sig, rhash, svc_id, name, kind, code);
         }
-        if (hit) {
-          sid = *hit;
-        } else {
-          if (!valid_utf8(name)) return fail(Result::kFallback, "non-UTF-8 span name");
+        // key = buildKey, into keystr (0 = built; else the failure to return)
+        auto build_key = [&]() -> int {
+          if (!valid_utf8(name)) return 1;
           sname = apply_rules(opt_.rules, std::string(name));
-          // key = buildKey
           keystr.clear();
           bool first = true;
           auto part = [&](std::string_view s) {
@@ -957,9 +956,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
             const Any *v = find_attr(sattrs, d.name);
             if (!v) v = find_attr(rattrs, d.name);
             if (v) {
-              if (const Keyable kb = as_string(*v, tmp); kb != Keyable::kYes)
-                return kb == Keyable::kTooDeep ? fail(Result::kError, "attribute value nested too deeply")
-                                               : fail(Result::kFallback, "dimension value not keyable natively");
+              if (const Keyable kb = as_string(*v, tmp); kb != Keyable::kYes) return kb == Keyable::kTooDeep ? 2 : 3;
             } else if (d.has_default) {
               tmp = d.def;
             } else {
@@ -968,6 +965,20 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
             keystr += '\0';
             keystr += tmp;
           }
+          return 0;
+        };
+        auto key_fail = [&](int why) {
+          return why == 1   ? fail(Result::kFallback, "non-UTF-8 span name")
+                 : why == 2 ? fail(Result::kError, "attribute value nested too deeply")
+                            : fail(Result::kFallback, "dimension value not keyable natively");
+        };
+        if (hit) {
+          sid = *hit;
+          if (opt_.events && !w.evs.empty()) {
+            if (const int why = build_key()) return key_fail(why);
+          }
+        } else {
+          if (const int why = build_key()) return key_fail(why);
           auto kit = keys.find(keystr);
           bool overflow = false;
           if (kit != keys.end()) {
@@ -997,10 +1008,13 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
         }
         if (opt_.exemplars) {  // candidates; accept_exemplars keeps the interval's first ones
           auto ex = ex_count_.find(sid);
-          uint32_t &mine = w.exl[sid];
-          if ((ex == ex_count_.end() ? 0u : ex->second) + mine < opt_.exemplars_max) {
-            ++mine;
-            res.exemplars.push_back({sid, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});
+          const uint32_t taken = ex == ex_count_.end() ? 0u : ex->second;
+          if (taken < opt_.exemplars_max) {  // (a series already full costs one lookup)
+            uint32_t &mine = w.exl[sid];
+            if (taken + mine < opt_.exemplars_max) {
+              ++mine;
+              res.exemplars.push_back({sid, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});
+            }
           }
         }
         out.key.push_back(sid);

@@ -876,6 +876,22 @@ napi_value ColumnizeBatch(napi_env env, napi_callback_info info) {
   return o;
 }
 
+// columnizerDestroy(c): frees the columnizer now (its buffers, threads and
+// dictionaries) instead of at garbage collection; later calls with `c` throw.
+// Also keeps a finalizer from being pending at environment teardown, which
+// this Node version does not survive.
+napi_value ColumnizerDestroy(napi_env env, napi_callback_info info) {
+  napi_value argv[1];
+  if (!get_args(env, info, 1, argv)) return throw_napi(env, "args");
+  void *p = nullptr;
+  if (napi_remove_wrap(env, argv[0], &p) == napi_ok && p) {
+    auto *c = static_cast<ColHandle *>(p);
+    if (c->engine_ref) napi_delete_reference(env, c->engine_ref);
+    delete c;
+  }
+  return nullptr;
+}
+
 // columnizerResetExemplars(c): a new export interval (every series may take
 // exemplars again)
 napi_value ColumnizerResetExemplars(napi_env env, napi_callback_info info) {
@@ -1028,6 +1044,7 @@ napi_value Init(napi_env env, napi_value exports) {
                {"columnize", Columnize},
                {"columnizeBatch", ColumnizeBatch},
                {"columnizerResetExemplars", ColumnizerResetExemplars},
+               {"columnizerDestroy", ColumnizerDestroy},
                {"columnizerIngest", ColumnizerIngest},
                {"columnizerTake", ColumnizerTake},
                {"columnizerServiceId", ColumnizerServiceId},

@@ -226,6 +226,8 @@ class SpanMetricsConnector {
   shutdown() {
     if (this.ticker) clearInterval(this.ticker);
     this.ticker = null;
+    if (this.col && this.addon.columnizerDestroy) this.addon.columnizerDestroy(this.col);
+    this.col = null;
     if (this.handle) this.addon.destroy(this.handle);
     this.handle = null;
   }

@@ -176,6 +176,7 @@ class NativeColumnizerFakeAddon extends FakeAddon {
   columnizerLearn(c, h, key, sid) { return this.real.columnizerLearn(c, h, key, sid); }
   columnizerRemap(c, from, to) { return this.real.columnizerRemap(c, from, to); }
   columnizerResetExemplars(c) { return this.real.columnizerResetExemplars(c); }
+  columnizerDestroy(c) { return this.real.columnizerDestroy(c); }
   columnizerIngest(c) {
     const b = this.real.columnizerTake(c);
     this.ingest(null, b);

@@ -4,14 +4,16 @@
  * transform rules -> keying -> SoA columns -> addon.ingest.  SURVEY.md 8(d)
  * asks for the OTLP decode+aggregate rate from protobuf bytes.
  *
- *   node test/host_rate.js [spans] [--gpu] [--threads T] [--batch B]
+ *   node test/host_rate.js [spans] [--gpu] [--threads T] [--batch B] [--exemplars] [--events]
  *
  * --threads T --batch B: requests go through consumeTracesBatch B at a time
  * (what the pipeline's queue does under load), decoded on T columnizer
  * threads (the JavaScript thread is one of them); default T=1, one request at a time.
  * Without --gpu the addon's ingest is a no-op stub (host work only); with
  * --gpu the real addon ingests (host memory -> HBM -> kernel) and the result
- * is checked for span count.  Prints one JSON line.
+ * is checked for span count.  --exemplars: exemplars.enabled (5 per data
+ * point); --events: events.enabled on exception.type, with one span in 16
+ * carrying an exception event.  Prints one JSON line.
  */
 const path = require('path');
 const lib = path.join(__dirname, '..', 'lib');
@@ -24,6 +26,7 @@ const gpu = process.argv.includes('--gpu');
 const jsOnly = process.argv.includes('--js');  // force the JavaScript columnizer
 const argOf = (k, d) => { const i = process.argv.indexOf(k); return i > 0 ? parseInt(process.argv[i + 1], 10) : d; };
 const threads = argOf('--threads', 1), batch = argOf('--batch', 0);
+const exemplars = process.argv.includes('--exemplars'), events = process.argv.includes('--events');
 const PER_REQUEST = 512;  // an SDK batch span processor's default export batch
 const SERVICES = 20, NAMES = 25;
 
@@ -43,7 +46,9 @@ function makeRequests() {
       spans.push({ traceId: tid, spanId: tid.subarray(0, 8), name: name % 5 === 0 ? `GET /api/products/${name}?x=1` : `op-${name}`,
         kind: 2, startTimeUnixNano: start, endTimeUnixNano: start + BigInt(Math.floor(rnd() * 2e7)),
         attributes: [{ key: 'http.method', value: { type: 'string', value: 'GET' } }],
-        status: { code: rnd() < 0.02 ? 2 : 0, message: '' } });
+        status: { code: rnd() < 0.02 ? 2 : 0, message: '' },
+        events: events && (i & 15) === 0 ? [{ timeUnixNano: start, name: 'exception',
+          attributes: [{ key: 'exception.type', value: { type: 'string', value: `E${name % 3}` } }] }] : [] });
     }
     reqs.push(otlp.encodeTraces({ resourceSpans: [{ resource: { attributes: [
       { key: 'service.name', value: { type: 'string', value: `svc-${svc}` } },
@@ -64,7 +69,9 @@ if (gpu) {
   addon.columnizerIngest = (c) => addon.real.columnizerTake(c).keyHash.length;
 }
 const p = new TracesToMetricsPipeline({ addon, receiver: false, exporter: false, memoryLimiter: false,
-  native: !jsOnly, spanmetrics: { n_services: 64, columnizer_threads: threads } });
+  native: !jsOnly, spanmetrics: Object.assign({ n_services: 64, columnizer_threads: threads },
+    exemplars ? { exemplars: { enabled: true, max_per_data_point: 5 } } : {},
+    events ? { events: { enabled: true, dimensions: [{ name: 'exception.type' }] } } : {}) });
 const consumeAll = (list) => {
   if (!batch) { for (const r of list) p.consumeTraces(r); return; }
   for (let i = 0; i < list.length; i += batch) {
@@ -84,11 +91,19 @@ if (gpu) addon.sync(p.connector.handle);
 const secs = Number(process.hrtime.bigint() - t0) / 1e9;
 const out = p.connector.exportMetrics();
 let calls = 0n;
-for (const rm of out.resourceMetrics) for (const dp of rm.scopeMetrics[0].metrics[0].sum.dataPoints) calls += dp.asInt;
-const native = p.connector.stats().nativeRequests > 0;
+let nEx = 0;
+for (const rm of out.resourceMetrics) {
+  for (const m of rm.scopeMetrics[0].metrics) {
+    if (m.name === 'traces.span.metrics.calls') for (const dp of m.sum.dataPoints) calls += dp.asInt;
+    if (m.histogram) for (const dp of m.histogram.dataPoints) nEx += (dp.exemplars || []).length;
+  }
+}
+const st = p.connector.stats();
+const native = st.nativeRequests > 0 && st.jsRequests === 0;
 p.shutdown();
 console.log(JSON.stringify({ spans: n, requests: reqs.length, otlp_bytes: bytes, seconds: secs,
   spans_per_s: n / secs, mb_per_s: bytes / secs / 1e6, cores: threads, batch, gpu,
   columnizer: native ? 'native (binding/otlp_columnizer.cc)' : 'javascript',
+  exemplars: exemplars ? nEx : undefined, event_records: events ? Number(st.eventRecords) : undefined,
   calls_check: gpu ? calls === BigInt(n) + warmSpans : null,  // cumulative: warm-up + timed
   path: 'OTLP protobuf decode + transform + keying + SoA columnize' + (gpu ? ' + sa_ingest (H2D + kernel)' : ' (engine ingest stubbed)') }));

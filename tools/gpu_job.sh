@@ -44,6 +44,7 @@ for step in "$@"; do
     tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     tests:*) f=${step#tests:}; run "tests_$(basename "$f" .py)" 600 python -u -m pytest "$f" -m gpu -x -v --timeout 300 --timeout-method thread ;;
     bench) run bench 500 python bench.py ;;
+    hostex_*) t=${step#hostex_}; run "hostex_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 --exemplars --events ;;
     host_*) t=${step#host_}; run "host_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 ;;
     bench_*) wl=${step#bench_}; run "bench_$wl" 300 python bench.py --workload "$wl" --sub "" --steps 20 $BQ ;;
     ablate_*) wl=${step#ablate_}; ABL_WORKLOAD=$wl ABL_VARS=${ABL_VARS:-} run "ablate_$wl" 400 python tools/ablate.py ;;
