@@ -39,6 +39,7 @@ struct PB {
   PB(const uint8_t *a, const uint8_t *b) : p(a), end(b) {}
   void fail() { ok = false; p = end; }
   uint64_t varint() {
+    if (p < end && *p < 0x80) return *p++;  // one byte: tags, kinds, short lengths
     uint64_t x = 0;
     for (int s = 0; s < 64 && p < end; s += 7) {
       const uint8_t b = *p++;
@@ -573,22 +574,35 @@ void col_free(void *p) {
   else ::operator delete(raw, std::align_val_t(kColHdr));
 }
 
-void Cols::truncate(size_t n) {
-  key.resize(n), start.resize(n), end.resize(n), w0.resize(n), w1.resize(n), meta.resize(n);
+void Cols::reserve(size_t cap) {
+  if (cap <= key.size()) return;
+  const size_t c = std::max<size_t>({cap, 2 * key.size(), 4096});
+  key.resize(c), start.resize(c), end.resize(c), w0.resize(c), w1.resize(c), meta.resize(c);
 }
 
-void Cols::append(const Cols &o, size_t off, size_t n) {
-  key.insert(key.end(), o.key.begin() + off, o.key.begin() + off + n);
-  start.insert(start.end(), o.start.begin() + off, o.start.begin() + off + n);
-  end.insert(end.end(), o.end.begin() + off, o.end.begin() + off + n);
-  w0.insert(w0.end(), o.w0.begin() + off, o.w0.begin() + off + n);
-  w1.insert(w1.end(), o.w1.begin() + off, o.w1.begin() + off + n);
-  meta.insert(meta.end(), o.meta.begin() + off, o.meta.begin() + off + n);
-}
-
+// The cache's own hash (any good mix will do; names are compared on a hit):
+// 8-byte words of the name, the last one overlapping, through a multiply-xorshift.
 uint64_t SigCache::hash(uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code) {
-  const uint64_t seed = rhash ^ ((uint64_t)svc << 40) ^ ((uint64_t)(uint32_t)kind << 8) ^ (uint32_t)code;
-  return xxh64(name.data(), name.size(), seed) | 1;  // 0 never names a used slot
+  constexpr uint64_t K = 0x9E3779B97F4A7C15ULL;
+  uint64_t h = rhash ^ ((uint64_t)svc << 40) ^ ((uint64_t)(uint32_t)kind << 8) ^ (uint32_t)code ^
+               ((uint64_t)name.size() << 56);
+  auto mix = [&](uint64_t v) {
+    h = (h ^ v) * K;
+    h ^= h >> 29;
+  };
+  const auto *q = reinterpret_cast<const uint8_t *>(name.data());
+  const size_t n = name.size();
+  if (n >= 8) {
+    size_t i = 0;
+    for (; i + 8 < n; i += 8) mix(rd64(q + i));
+    mix(rd64(q + n - 8));
+  } else if (n >= 4) {
+    mix(((uint64_t)rd32(q) << 32) | rd32(q + n - 4));
+  } else if (n) {
+    mix(((uint64_t)q[0] << 16) | ((uint64_t)q[n / 2] << 8) | q[n - 1]);
+  }
+  h = (h ^ (h >> 32)) * K;
+  return (h ^ (h >> 29)) | 1;  // 0 never names a used slot
 }
 
 const uint64_t *SigCache::find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
@@ -720,8 +734,8 @@ void Columnizer::accept_exemplars(Result &r) {
 }
 
 void Columnizer::remap(uint64_t from, uint64_t to) {
-  for (uint64_t &k : buf_.key)
-    if (k == from) k = to;
+  for (size_t i = 0; i < buf_.n; ++i)
+    if (buf_.key[i] == from) buf_.key[i] = to;
   ++gen_;
   auto o = owner_.find(from);
   if (o == owner_.end()) return;
@@ -1017,20 +1031,11 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
             }
           }
         }
-        out.key.push_back(sid);
-        out.start.push_back(st);
-        out.end.push_back(en);
         if (en > out.max_end) out.max_end = en;
-        if (tid && tid_len == 16) {
-          out.w0.push_back(rd64(tid));
-          out.w1.push_back(rd64(tid + 8));
-        } else {
-          out.w0.push_back(0);
-          out.w1.push_back(0);
-        }
+        const bool has_tid = tid && tid_len == 16;
         const uint32_t kk = kind >= 0 && kind <= 7 ? (uint32_t)kind : 7u;
         const uint32_t cc = code >= 0 && code <= 3 ? (uint32_t)code : 3u;
-        out.meta.push_back(svc_id | (kk << 16) | (cc << 19));
+        out.push(sid, st, en, has_tid ? rd64(tid) : 0, has_tid ? rd64(tid + 8) : 0, svc_id | (kk << 16) | (cc << 19));
         ++res.spans;
         // events.enabled: one record per event, keyed by the span key and the
         // event dimensions (connector.js _eventId), counted as a span of
@@ -1079,12 +1084,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
             res.new_event_series.push_back(
                 {esid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin), ei});
           }
-          out.key.push_back(esid);
-          out.start.push_back(0);
-          out.end.push_back(0);
-          out.w0.push_back(0);
-          out.w1.push_back(0);
-          out.meta.push_back(0xFFFFu);
+          out.push(esid, 0, 0, 0, 0, 0xFFFFu);
           ++res.event_records;
         }
       }
@@ -1206,8 +1206,8 @@ BatchResult Columnizer::columnize_batch(const uint8_t *const *bufs, const size_t
   }
   // phase 3: every request's columns to its place in the buffer, in parallel
   const size_t base = buf_.size();
-  buf_.key.resize(base + total), buf_.start.resize(base + total), buf_.end.resize(base + total);
-  buf_.w0.resize(base + total), buf_.w1.resize(base + total), buf_.meta.resize(base + total);
+  buf_.reserve(base + total);
+  buf_.n = base + total;
   next = 0;
   const std::function<void(unsigned)> place = [&](unsigned) {
     for (size_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < taken;) {

@@ -133,19 +133,27 @@ struct ColAlloc {
 template <class T>
 using ColVec = std::vector<T, ColAlloc<T>>;
 
-// SoA v1 columns under construction
+// SoA v1 columns under construction.  The six arrays share one capacity
+// (their vector size) and one fill count n, so appending a span is one bound
+// check and six stores.
 struct Cols {
   ColVec<uint64_t> key, start, end, w0, w1;
   ColVec<uint32_t> meta;
+  size_t n = 0;
   uint64_t max_end = 0;
   Cols() = default;
   explicit Cols(bool pinned)
       : key(ColAlloc<uint64_t>(pinned)), start(ColAlloc<uint64_t>(pinned)), end(ColAlloc<uint64_t>(pinned)),
         w0(ColAlloc<uint64_t>(pinned)), w1(ColAlloc<uint64_t>(pinned)), meta(ColAlloc<uint32_t>(pinned)) {}
-  size_t size() const { return key.size(); }
-  void truncate(size_t n);
-  void append(const Cols &o, size_t off, size_t n);
-  void clear() { truncate(0), max_end = 0; }
+  size_t size() const { return n; }
+  void reserve(size_t cap);  // capacity for at least cap spans (contents kept)
+  void push(uint64_t k, uint64_t s, uint64_t e, uint64_t a, uint64_t b, uint32_t m) {
+    if (n == key.size()) reserve(n + 1);
+    key[n] = k, start[n] = s, end[n] = e, w0[n] = a, w1[n] = b, meta[n] = m;
+    ++n;
+  }
+  void truncate(size_t m) { n = m; }
+  void clear() { n = 0, max_end = 0; }
 };
 
 // (resource hash, service id, raw span name, kind, status code) -> series id,

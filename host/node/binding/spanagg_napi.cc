@@ -11,6 +11,7 @@
 // Error with .code = the status and the engine's sa_last_error() text, except
 // flush(), which returns SA_EFULL in .status (the result is still valid), as
 // sa_flush does.
+#include <algorithm>
 #include <node_api.h>
 
 #include <cstdint>
@@ -861,13 +862,48 @@ napi_value ColumnizeBatch(napi_env env, napi_callback_info info) {
     bufs[i] = static_cast<const uint8_t *>(data);
   }
   otlpcol::BatchResult br = c->col.columnize_batch(bufs.data(), lens.data(), items.size());
+  // Most requests of a steady stream bring nothing new: status ok, no new
+  // services / resources / series, no exemplars or event series.  Those get
+  // no result object; what the host must still see of them -- the resources
+  // they touched, for its LRU -- comes as one list per gap between the
+  // requests that do get one, each resource once, in order of last touch
+  // (nothing is admitted to the LRU inside a gap, so that order is the one
+  // request-at-a-time touches leave).
+  //   results[i]: the request's result object, or undefined (a plain one)
+  //   touch: resource hashes; touchEnd[k]: the end of the gap before the k-th
+  //   result object (the last gap ends at touch.length)
+  auto plain = [](const otlpcol::Result &r) {
+    return r.status == otlpcol::Result::kOk && r.new_resources.empty() && r.new_series.empty() &&
+           r.new_services.empty() && r.exemplars.empty() && r.new_event_series.empty();
+  };
+  std::vector<uint64_t> touch;
+  std::vector<uint32_t> touch_end;
+  size_t gap0 = 0;  // where the current gap starts in `touch`
+  uint64_t spans = 0;
+  for (const auto &r : br.results) {
+    spans += r.spans;
+    if (!plain(r)) {
+      touch_end.push_back((uint32_t)touch.size());
+      gap0 = touch.size();
+      continue;
+    }
+    for (uint64_t h : r.resources) {  // move to the back of the gap's list
+      auto it = std::find(touch.begin() + gap0, touch.end(), h);
+      if (it != touch.end()) touch.erase(it);
+      touch.push_back(h);
+    }
+  }
   napi_value o, arr;
   if (napi_create_object(env, &o) != napi_ok) return throw_napi(env, "napi_create_object");
   set(env, o, "done", num(env, (double)br.done));
   set(env, o, "buffered", num(env, (double)c->col.buffered()));
   set(env, o, "maxEnd", big(env, c->col.max_end()));
+  set(env, o, "spans", num(env, (double)spans));
+  set(env, o, "touch", make_typed(env, napi_biguint64_array, 8, touch.data(), touch.size()));
+  set(env, o, "touchEnd", make_typed(env, napi_uint32_array, 4, touch_end.data(), touch_end.size()));
   napi_create_array_with_length(env, br.results.size(), &arr);
   for (size_t i = 0; i < br.results.size(); ++i) {
+    if (plain(br.results[i])) continue;
     napi_value e = result_obj(env, br.results[i], true);
     if (!e) return throw_napi(env, "napi_create_object");
     napi_set_element(env, arr, (uint32_t)i, e);

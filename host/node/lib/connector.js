@@ -412,13 +412,22 @@ class SpanMetricsConnector {
       } catch (e) {
         throw at(e, i);
       }
+      // plain requests (nothing new, status ok) have no result object: their
+      // resource touches come per gap between the ones that do (touch/touchEnd)
+      let t = 0, gap = 0, plainN = 0;
+      const touchTo = (end) => { for (; t < end; t++) this._touchResource(br.touch[t]); };
       for (let k = 0; k < br.done; k++) {
+        const r = br.results[k];
+        if (r === undefined) { plainN += 1; continue; }
+        touchTo(br.touchEnd[gap++]);
         try {
-          if (!this._applyNative(br.results[k], bufs[k])) this._consumeJs(otlp.decodeTraces(bufs[k]));
+          if (!this._applyNative(r, bufs[k])) this._consumeJs(otlp.decodeTraces(bufs[k]));
         } catch (e) {
           errs[i + k] = e;
         }
       }
+      touchTo(br.touch.length);
+      this.nativeRequests += plainN;
       if (br.maxEnd > this.nativeMaxEnd) this.nativeMaxEnd = br.maxEnd;
       this.nativeBuffered = br.buffered;
       i += br.done;

@@ -515,6 +515,18 @@ __device__ __forceinline__ bool lds_err_add(uint32_t *etab, uint32_t ek) {
 // of lsum + lcnt (nw = 6: 32 B per slot), written to the workgroup's header
 // slab at the end; every span's key slot goes to P.slot_of for the
 // bucket-counting pass.
+// A wave's claim of the next chunk from an LDS counter kept in units of
+// 1/64 chunk.  Every lane adds the same 1 (no branch: a divergent claim made
+// the compiler wait for it at the join), so the atomic optimizer issues one
+// ds_add_rtn of popcount(exec) = 64 and hands the lanes base + rank; the first
+// lane's base / 64 is the claim.  (A lane-varying addend -- 1 on lane 0, 0
+// elsewhere -- compiled to a 64-iteration readlane/writelane scan loop per
+// claim: ~140 scalar and ~30 vector instructions per span-lane of the C2 loop.)
+// Requires a full wave at the call, which the claim loops have.
+__device__ __forceinline__ uint32_t wave_claim(uint32_t *ctr) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)atomicAdd(ctr, 1u)) >> 6;
+}
+
 template <int S, int NBUF, int AUX, bool DIAG, int LC = 0, int NWC = 0, int PC = 0, int HAUX = -1,
           bool DYN = false, int OPT = 0, bool EPI = false, bool LEAN = false, bool EXPO = false>
 __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
@@ -620,7 +632,8 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     *reinterpret_cast<uint4 *>(lcnt + i) = make_uint4(0, 0, 0, 0);
   if (threadIdx.x == 0) {
     hq_n[0] = 0;
-    hq_n[1] = (kTileClaims ? 2u * NBUF : 2u) * kWaves;  // DYN: next unclaimed chunk of this workgroup's range
+    // DYN: next unclaimed chunk of this workgroup's range, x 64 (see the claims)
+    hq_n[1] = ((kTileClaims ? 2u * NBUF : 2u) * kWaves) << 6;
     hq_n[2] = 0;  // EPI: HLL updates the lower-bound filter skipped (summed over the waves)
   }
   if (threadIdx.x < 4) lstat[threadIdx.x] = 0;
@@ -914,9 +927,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     while (cur[0] * tile < len) {
       uint32_t nw_[NBUF];
 #pragma unroll
-      for (int b = 0; b < NBUF; ++b)
-        nw_[b] = (uint32_t)__builtin_amdgcn_readfirstlane(
-            (int)atomicAdd(&hq_n[1], (threadIdx.x & 63u) == 0 ? 1u : 0u));
+      for (int b = 0; b < NBUF; ++b) nw_[b] = wave_claim(&hq_n[1]);
 #pragma unroll
       for (int b = 0; b < NBUF; ++b) step(buf[b], tstart(cur[b], b), tstart(nxt[b], b));
 #pragma unroll
@@ -930,11 +941,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     // (prefetched during this round), c2: claimed now for the round after.
     // The claim returns while the round runs; its result is read at the end.
     while (c0 < n_chunks) {
-      // every lane runs the atomic (no branch: a divergent claim made the
-      // compiler wait for it at the join); only lane 0 adds, lane 0's return
-      // is the claim
-      const uint32_t c2 = (uint32_t)__builtin_amdgcn_readfirstlane(
-          (int)atomicAdd(&hq_n[1], (threadIdx.x & 63u) == 0 ? 1u : 0u));
+      const uint32_t c2 = wave_claim(&hq_n[1]);
 #pragma unroll
       for (int b = 0; b < NBUF; ++b) step(buf[b], tstart(c0, b), tstart(c1, b));
       c0 = c1;
