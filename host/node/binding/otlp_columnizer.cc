@@ -605,15 +605,15 @@ uint64_t SigCache::hash(uint64_t rhash, uint32_t svc, std::string_view name, int
   return (h ^ (h >> 29)) | 1;  // 0 never names a used slot
 }
 
-const uint64_t *SigCache::find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
-                               int32_t code) const {
+SigCache::Entry *SigCache::find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
+                                int32_t code) {
   if (t_.empty()) return nullptr;
   const size_t mask = t_.size() - 1;
   for (size_t i = h & mask;; i = (i + 1) & mask) {
-    const Entry &e = t_[i];
+    Entry &e = t_[i];
     if (!e.used) return nullptr;
     if (e.h == h && e.rhash == rhash && e.svc == svc && e.kind == kind && e.code == code && e.name == name)
-      return &e.sid;
+      return &e;
   }
 }
 
@@ -631,7 +631,7 @@ void SigCache::insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view
   size_t i = h & mask;
   while (t_[i].used) i = (i + 1) & mask;
   Entry &e = t_[i];
-  e.h = h, e.rhash = rhash, e.sid = sid, e.svc = svc, e.kind = kind, e.code = code, e.used = true;
+  e.h = h, e.rhash = rhash, e.sid = sid, e.svc = svc, e.kind = kind, e.code = code, e.used = true, e.ex_full = 0;
   e.name.assign(name);
   ++n_;
 }
@@ -946,7 +946,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
         if (!sp.ok) return fail(Result::kError, "malformed Span");
         uint64_t sid;
         uint64_t sig = 0;
-        const uint64_t *hit = nullptr;
+        SigCache::Entry *hit = nullptr;
         if (use_cache) {
           sig = SigCache::hash(rhash, svc_id, name, kind, code);
           hit = cache.find(sig, rhash, svc_id, name, kind, code);
@@ -987,7 +987,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
                             : fail(Result::kFallback, "dimension value not keyable natively");
         };
         if (hit) {
-          sid = *hit;
+          sid = hit->sid;
           if (opt_.events && !w.evs.empty()) {
             if (const int why = build_key()) return key_fail(why);
           }
@@ -1020,15 +1020,20 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
           // (an overflowed key is decided again each time: the count it met may change)
           if (use_cache && !overflow) cache.insert(sig, rhash, svc_id, name, kind, code, sid);
         }
-        if (opt_.exemplars) {  // candidates; accept_exemplars keeps the interval's first ones
+        // candidates; accept_exemplars keeps the interval's first ones.  A
+        // series seen full this interval is marked in its signature-cache
+        // entry, so its later spans cost no lookup.
+        if (opt_.exemplars && !(hit && hit->ex_full == ex_gen_)) {
           auto ex = ex_count_.find(sid);
           const uint32_t taken = ex == ex_count_.end() ? 0u : ex->second;
-          if (taken < opt_.exemplars_max) {  // (a series already full costs one lookup)
+          if (taken < opt_.exemplars_max) {
             uint32_t &mine = w.exl[sid];
             if (taken + mine < opt_.exemplars_max) {
               ++mine;
               res.exemplars.push_back({sid, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});
             }
+          } else if (hit) {
+            hit->ex_full = ex_gen_;
           }
         }
         if (en > out.max_end) out.max_end = en;

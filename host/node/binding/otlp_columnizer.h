@@ -162,21 +162,23 @@ struct Cols {
 class SigCache {
  public:
   static uint64_t hash(uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code);
-  const uint64_t *find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
-                       int32_t code) const;
+  struct Entry;
+  Entry *find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code);
   void insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code,
               uint64_t sid);
   void clear() { t_.clear(), n_ = 0; }
   uint64_t gen = 0;  // the dictionary generation the entries belong to
 
- private:
   struct Entry {
     uint64_t h = 0, rhash = 0, sid = 0;
+    uint64_t ex_full = 0;  // the exemplar interval (Columnizer::ex_gen_) in which the series was seen full
     uint32_t svc = 0;
     int32_t kind = 0, code = 0;
     bool used = false;
     std::string name;
   };
+
+ private:
   std::vector<Entry> t_;
   size_t n_ = 0;
 };
@@ -201,7 +203,7 @@ class Columnizer {
   void remap(uint64_t from, uint64_t to);
   void clear_buffer() { buf_.clear(); }
   // a new export interval: every series may take exemplars again
-  void reset_exemplars() { ex_count_.clear(); }
+  void reset_exemplars() { ex_count_.clear(), ++ex_gen_; }
 
   size_t buffered() const { return buf_.size(); }
   uint64_t max_end() const { return buf_.max_end; }
@@ -237,6 +239,7 @@ class Columnizer {
   std::unordered_map<uint64_t, uint32_t> nspan_;
   // exemplars taken per series this export interval (written in request order)
   std::unordered_map<uint64_t, uint32_t> ex_count_;
+  uint64_t ex_gen_ = 1;  // the exemplar interval, for SigCache::Entry::ex_full
   // keeps the request's exemplar candidates that the interval still wants
   void accept_exemplars(Result &r);
 };

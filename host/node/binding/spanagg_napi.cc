@@ -879,9 +879,10 @@ napi_value ColumnizeBatch(napi_env env, napi_callback_info info) {
   std::vector<uint64_t> touch;
   std::vector<uint32_t> touch_end;
   size_t gap0 = 0;  // where the current gap starts in `touch`
-  uint64_t spans = 0;
+  uint64_t spans = 0, plain_events = 0;
   for (const auto &r : br.results) {
     spans += r.spans;
+    if (plain(r)) plain_events += r.event_records;
     if (!plain(r)) {
       touch_end.push_back((uint32_t)touch.size());
       gap0 = touch.size();
@@ -899,6 +900,7 @@ napi_value ColumnizeBatch(napi_env env, napi_callback_info info) {
   set(env, o, "buffered", num(env, (double)c->col.buffered()));
   set(env, o, "maxEnd", big(env, c->col.max_end()));
   set(env, o, "spans", num(env, (double)spans));
+  set(env, o, "plainEventRecords", num(env, (double)plain_events));  // event records of the plain requests
   set(env, o, "touch", make_typed(env, napi_biguint64_array, 8, touch.data(), touch.size()));
   set(env, o, "touchEnd", make_typed(env, napi_uint32_array, 4, touch_end.data(), touch_end.size()));
   napi_create_array_with_length(env, br.results.size(), &arr);

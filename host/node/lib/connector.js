@@ -428,6 +428,7 @@ class SpanMetricsConnector {
       }
       touchTo(br.touch.length);
       this.nativeRequests += plainN;
+      if (br.plainEventRecords) this.eventRecords += br.plainEventRecords;
       if (br.maxEnd > this.nativeMaxEnd) this.nativeMaxEnd = br.maxEnd;
       this.nativeBuffered = br.buffered;
       i += br.done;

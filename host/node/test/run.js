@@ -623,10 +623,11 @@ test('native columnizer: consumeTracesBatch on worker threads == consumeTraces o
     }
     return rows.sort();
   };
-  for (const r of eventRequests()) reqs.push(otlp.encodeTraces(r));
+  for (const r of eventRequests().concat(eventRequests())) reqs.push(otlp.encodeTraces(r));  // the second time: nothing new
   for (const cfg of [{}, { dimensions: [{ name: 'http.status_code' }, { name: 'k8s.pod.name' }] },
     { resource_metrics_cache_size: 2 },
-    { aggregation_cardinality_limit: 3, exemplars: { enabled: true }, events: { enabled: true, dimensions: [{ name: 'exception.type' }] } }]) {
+    { aggregation_cardinality_limit: 3, exemplars: { enabled: true }, events: { enabled: true, dimensions: [{ name: 'exception.type' }] } },
+    { events: { enabled: true, dimensions: [{ name: 'exception.type' }] } }]) {
     const out = [];
     for (const threads of [1, 4]) {
       const addon = new NativeColumnizerFakeAddon();
@@ -650,6 +651,8 @@ test('native columnizer: consumeTracesBatch on worker threads == consumeTraces o
     assert.deepStrictEqual(batch.exp, one.exp, JSON.stringify(cfg));
     assert.deepStrictEqual(batch.services, one.services);
     assert.strictEqual(batch.stats.jsRequests, 1);  // the non-UTF-8 request
+    assert.strictEqual(batch.stats.eventRecords, one.stats.eventRecords);
+    assert.strictEqual(batch.stats.nativeRequests, one.stats.nativeRequests);
   }
 });
 
