@@ -217,6 +217,14 @@ void sa_exp_result_free(sa_exp_result *r);
  * logs[i] = Go's math.Log(v[i]), both computed on the engine's GPU
  * (host arrays; n <= 2^20). */
 int sa_expo_probe(sa_engine *e, const double *v, const int32_t *scale, uint64_t n, int32_t *out, double *logs);
+/* Diagnostic: the bucket-index fast path the counting kernel uses.  For each
+ * duration d_ns[i] > 0 at scale[i]: exact[i] = the Go-exact index of
+ * d_ns / (1e6 or 1e9 by the engine's unit), fast[i] = the fast path's index
+ * or INT32_MIN when it defers to the exact path (host arrays; n <= 2^20).
+ * *log2_err (may be null) = max |v_log_f32(m) - log2(m)| over every float m
+ * in [1, 2), the bound the fast path's margins assume. */
+int sa_expo_fast_probe(sa_engine *e, const uint64_t *d_ns, const int32_t *scale, uint64_t n, int32_t *fast,
+                       int32_t *exact, double *log2_err);
 
 /* Sketches of one resident window (not cleared). */
 int sa_window_read(sa_engine *e, uint64_t window_id, sa_sketch_result **out);

@@ -136,10 +136,19 @@ struct ExpoParams {
   uint32_t *buckets;  // [2][cap][max_size]
   uint32_t max_size;
   double div;         // 1e6 (ms) or 1e9 (s)
+  double log2div;     // log2(div), for the bucket index's fast path
+  uint32_t diag;      // ablation bits (SPANAGG_XC_DIAG, profiling only; results wrong when set):
+                      // 1 no HBM bucket atomics, 2 no LDS cache, 4 exact index path only, 8 no index
   uint32_t *slot_of;  // [n] key slot of each span (pass 1 -> pass 3)
   unsigned long long *dropped;
   XHdr *xslab;        // small-table engines: [xG][cap] per-workgroup header partials (nullptr: pass 1 atomics)
   uint32_t xG;
+  // small-table bucket counting (expo_select / expo_count_slab / expo_fold_slab):
+  uint32_t *lcount;         // [cap] this launch's positive durations per slot (reduce -> select)
+  int32_t *entry_of;        // [cap] the slot's LDS entry in the counting kernel, -1: HBM atomics
+  uint32_t *slot_of_entry;  // [xc_ne] the entry's slot, ~0u: unused
+  uint32_t *xcslab;         // [xG][xc_ne][(max_size + 1) / 2] per-workgroup u16 bucket-count pairs
+  uint32_t xc_ne;           // LDS entries of the counting kernel (0: the cached-probe kernel)
 };
 __host__ __device__ ExpoHdr expo_hdr_empty();
 constexpr uint32_t kExpoMaxSize = 4096;
@@ -373,7 +382,14 @@ hipError_t launch_expo_compact(const ExpoParams &E, unsigned long long *out_keys
                                uint32_t *out_buckets, unsigned long long *out_n, hipStream_t s);
 hipError_t launch_expo_init(ExpoHdr *hdr, uint64_t cap, hipStream_t s);
 size_t expo_count_lds_bytes(uint64_t cap, uint32_t max_size);
+// LDS entries of the slab counting kernel for one workgroup's LDS budget, and its LDS bytes
+uint32_t expo_slab_entries(uint64_t cap, uint32_t max_size, size_t budget);
+size_t expo_slab_lds_bytes(uint64_t cap, uint32_t max_size, uint32_t ne);
+hipError_t prepare_expo_slab(size_t lds_bytes);
 hipError_t prepare_expo_count(size_t lds_bytes);
+hipError_t launch_expo_fast_probe(const uint64_t *d, const int32_t *scale, uint64_t n, double div, int32_t *fast,
+                                  int32_t *exact, hipStream_t s);
+hipError_t launch_log2_err_probe(uint32_t i0, uint32_t n, double *block_max, uint32_t blocks, hipStream_t s);
 hipError_t launch_expo_probe(const double *v, const int32_t *scale, int32_t *idx_out, double *log_out, uint64_t n,
                              hipStream_t s);
 

@@ -92,6 +92,10 @@ struct sa_engine {
   // EXPO mode (per-workgroup header partials in xslab [G][cap], per-span slots)
   bool expo_small = false;
   sa::XHdr *xslab = nullptr;
+  // slab bucket counting of small expo tables (spanagg_expo.hip expo_count_slab_kernel)
+  uint32_t xc_ne = 0;
+  uint32_t *xc_lcount = nullptr, *xc_slot_of_entry = nullptr, *xcslab = nullptr;
+  int32_t *xc_entry_of = nullptr;
   sa::ExpoHdr *expo_hdr = nullptr;
   uint32_t *expo_buckets = nullptr, *expo_slot = nullptr;
   uint64_t expo_slot_cap = 0;
@@ -371,6 +375,15 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
     if (hipError_t st = sa::prepare_expo_count(sa::expo_count_lds_bytes(e->cap, cfg->exp_max_size)); st != hipSuccess)
       return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
+    // slab counting: its workgroups (one per ingest workgroup) share a CU as the
+    // ingest ones do; SPANAGG_XC_SLAB=0 keeps the cached-probe kernel (A/B runs)
+    const char *sv = std::getenv("SPANAGG_XC_SLAB");
+    const size_t budget = (size_t)160 * 1024 * e->cus / e->G - 1024;
+    e->xc_ne = (sv && std::atoi(sv) == 0) ? 0u : sa::expo_slab_entries(e->cap, cfg->exp_max_size, budget);
+    if (e->xc_ne)
+      if (hipError_t st = sa::prepare_expo_slab(sa::expo_slab_lds_bytes(e->cap, cfg->exp_max_size, e->xc_ne));
+          st != hipSuccess)
+        return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
   } else {
     e->block = sa::kHbmBlock;
     e->spl = (uint32_t)sa::kVariants[e->variant].spl;
@@ -431,6 +444,11 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       return bail(fail(e, SA_EDEVICE, "expo state init failed"));
     if (e->expo_small) {
       if ((rc = alloc((void **)&e->xslab, (size_t)e->G * e->cap * sizeof(sa::XHdr)))) return bail(rc);
+      if (e->xc_ne &&
+          ((rc = alloc((void **)&e->xc_lcount, e->cap * 4)) || (rc = alloc((void **)&e->xc_entry_of, e->cap * 4)) ||
+           (rc = alloc((void **)&e->xc_slot_of_entry, (size_t)e->xc_ne * 4)) ||
+           (rc = alloc((void **)&e->xcslab, (size_t)e->G * e->xc_ne * ((cfg->exp_max_size + 1) / 2) * 4))))
+        return bail(rc);
       // (window, slot) keys of the LDS ERROR table are 16-bit
       if ((uint64_t)cfg->n_windows * e->cap < 65535 &&
           (rc = alloc((void **)&e->errslab, (size_t)e->G * cfg->n_windows * e->cap * 4)))
@@ -504,6 +522,7 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->part_fill, (void *)e->bt_rec, (void *)e->bt_cnt, (void *)e->base64, (void *)e->hll_lb,
                   (void *)e->expo_hdr, (void *)e->expo_buckets, (void *)e->expo_slot, (void *)e->expo_out_keys,
                   (void *)e->expo_out_rows, (void *)e->expo_out_buckets, (void *)e->hll_filt, (void *)e->xslab,
+                  (void *)e->xc_lcount, (void *)e->xc_entry_of, (void *)e->xc_slot_of_entry, (void *)e->xcslab,
                   e->dstage[0], e->dstage[1]})
     if (p) (void)hipFree(p);
   for (int k = 0; k < 2; ++k) {
@@ -603,10 +622,23 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
   E.buckets = e->expo_buckets;
   E.max_size = e->cfg.exp_max_size;
   E.div = e->cfg.unit == SA_UNIT_S ? 1e9 : 1e6;
+  E.log2div = std::log2(E.div);
+  {
+    static const uint32_t diag = [] {
+      const char *v = std::getenv("SPANAGG_XC_DIAG");
+      return v ? (uint32_t)std::strtoul(v, nullptr, 0) : 0u;
+    }();
+    E.diag = diag;
+  }
   E.slot_of = e->expo_slot;
   E.dropped = e->stats + sa::kStatDropped;
   E.xslab = e->expo_small ? e->xslab : nullptr;
   E.xG = e->G;
+  E.xc_ne = e->expo_small ? e->xc_ne : 0u;
+  E.lcount = E.xc_ne ? e->xc_lcount : nullptr;
+  E.entry_of = e->xc_entry_of;
+  E.slot_of_entry = e->xc_slot_of_entry;
+  E.xcslab = e->xcslab;
   return E;
 }
 
@@ -1091,6 +1123,38 @@ int sa_expo_probe(sa_engine *e, const double *v, const int32_t *scale, uint64_t 
   if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
   (void)hipFree(buf);
   return st == hipSuccess ? SA_OK : fail(e, SA_EDEVICE, std::string("expo probe: ") + hipGetErrorString(st));
+}
+
+int sa_expo_fast_probe(sa_engine *e, const uint64_t *d_ns, const int32_t *scale, uint64_t n, int32_t *fast,
+                       int32_t *exact, double *log2_err) {
+  if (!e || (n && (!d_ns || !scale || !fast || !exact)) || n > (1ULL << 20)) return SA_EINVAL;
+  if (int rc = set_dev(e)) return rc;
+  join_sets(e);
+  constexpr uint32_t kBlocks = 2048;
+  void *buf = nullptr;
+  if (hipMalloc(&buf, n * 20 + kBlocks * 8) != hipSuccess) return fail(e, SA_ENOMEM, "probe buffer");
+  double *bmax = static_cast<double *>(buf);
+  uint64_t *dd = reinterpret_cast<uint64_t *>(bmax + kBlocks);
+  int32_t *ds = reinterpret_cast<int32_t *>(dd + n), *df = ds + n, *dx = df + n;
+  hipError_t st = hipSuccess;
+  if (n) {
+    st = hipMemcpyAsync(dd, d_ns, n * 8, hipMemcpyHostToDevice, e->stream);
+    if (st == hipSuccess) st = hipMemcpyAsync(ds, scale, n * 4, hipMemcpyHostToDevice, e->stream);
+    if (st == hipSuccess)
+      st = sa::launch_expo_fast_probe(dd, ds, n, e->cfg.unit == SA_UNIT_S ? 1e9 : 1e6, df, dx, e->stream);
+    if (st == hipSuccess) st = hipMemcpyAsync(fast, df, n * 4, hipMemcpyDeviceToHost, e->stream);
+    if (st == hipSuccess) st = hipMemcpyAsync(exact, dx, n * 4, hipMemcpyDeviceToHost, e->stream);
+  }
+  std::vector<double> hm(kBlocks);
+  if (log2_err) {
+    if (st == hipSuccess) st = sa::launch_log2_err_probe(0, 1u << 23, bmax, kBlocks, e->stream);
+    if (st == hipSuccess) st = hipMemcpyAsync(hm.data(), bmax, kBlocks * 8, hipMemcpyDeviceToHost, e->stream);
+  }
+  if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+  (void)hipFree(buf);
+  if (st != hipSuccess) return fail(e, SA_EDEVICE, std::string("expo fast probe: ") + hipGetErrorString(st));
+  if (log2_err) *log2_err = *std::max_element(hm.begin(), hm.end());
+  return SA_OK;
 }
 
 static bool resident(const sa_engine *e, uint64_t w) {

@@ -23,6 +23,9 @@
 //                      shorter than max_size)
 // The sketches of these spans run through the HBM-table ingest kernel.
 #include <algorithm>
+#include <climits>
+#include <cstdlib>
+#include <cmath>
 
 #include "sa_device.h"
 
@@ -72,6 +75,35 @@ __device__ __forceinline__ int32_t expo_index(double v, int32_t scale) {
 
 __device__ __forceinline__ double expo_value(uint64_t d_ns, double div) {
   return (double)d_ns / div;
+}
+
+// Fast path of the bucket index of a duration d > 0 ns at `scale`: log2 of the
+// value from d's exponent, v_log_f32 of its top 24 bits and log2(div), all
+// exact or nearly so -- |error| <= kFastLog2Err (the hardware log2 over every
+// float in [1, 2), measured exhaustively by test_gpu_expo.py's
+// test_fast_log2_error_bound, plus the 24-bit truncation of d).  When the
+// scaled value is farther than its error bound from an integer, its floor is
+// the index Go's math.Log computation gives (that one is within ~1e-9 of the
+// exact value at any scale <= 20); otherwise -- including every power of two
+// and every value near a bucket boundary -- false, and the caller takes the
+// exact path.
+constexpr double kFastLog2Err = 1.0 / (1 << 20) + 1.0 / (1 << 22);
+__device__ __forceinline__ bool expo_index_fast(uint64_t d, double log2div, int32_t scale, int32_t &idx) {
+  const int32_t e = 63 - (int32_t)__clzll((long long)d);
+  const uint32_t top = (uint32_t)((d << (63 - e)) >> 40);  // 24 bits, the leading one at bit 23
+  const float m = (float)top * 0x1p-23f;                    // exact, in [1, 2)
+  const double z = (double)e - log2div + (double)__builtin_amdgcn_logf(m);  // ~ log2(d / div)
+  const double fz = floor(z);
+  if (z - fz <= kFastLog2Err || fz + 1.0 - z <= kFastLog2Err) return false;  // near a power of two
+  if (scale <= 0) {
+    idx = (int32_t)fz >> (-scale);  // Go: exponent >> -scale (z is not an integer)
+    return true;
+  }
+  const double y = ldexp(z, scale), fy = floor(y), err = ldexp(kFastLog2Err, scale);
+  if (y - fy <= err || fy + 1.0 - y <= err) return false;
+  const double max_index = (double)((1024 << scale) - 1);
+  idx = fy >= max_index ? (int32_t)max_index : (int32_t)fy;
+  return true;
 }
 
 constexpr int32_t kExpoMaxScale = 20, kExpoMinScale = -10;
@@ -150,17 +182,20 @@ __global__ __launch_bounds__(256) void expo_rescale_kernel(ExpoParams E) {
 }
 
 // Small-table engines: the ingest kernel (EXPO mode) leaves per-workgroup
-// header partials in slabs [xG][cap].  One block per 64 slots: 16 groups of
-// 64 threads sum every 16th workgroup's partials (coalesced 32-B rows,
-// zeroing what they consumed), LDS combines the groups, then one thread per
-// slot folds the sum into the series header and rescales it.
+// header partials in slabs [xG][cap].  One block per 16 slots: 64 groups of
+// 16 threads sum every 64th workgroup's partials (each wave reads four 512-B
+// runs, zeroing what it consumed), LDS combines the groups, then one thread
+// per slot folds the sum into the series header and rescales it.  (64 slots
+// per block gave cap / 64 = 32 blocks at C2's table: 29 us, latency-bound.)
+template <uint32_t kXrSlots>
 __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E) {
-  __shared__ XHdr part[16][64];
-  const uint32_t sl = threadIdx.x & 63u, gg = threadIdx.x >> 6;
-  const uint64_t s = blockIdx.x * 64ull + sl;
+  constexpr uint32_t kXrGroups = 1024 / kXrSlots;
+  __shared__ XHdr part[kXrGroups][kXrSlots];
+  const uint32_t sl = threadIdx.x % kXrSlots, gg = threadIdx.x / kXrSlots;
+  const uint64_t s = blockIdx.x * (uint64_t)kXrSlots + sl;
   XHdr acc{0, 0, 0, 0, 0};
   if (s < E.cap) {
-    for (uint32_t g = gg; g < E.xG; g += 16) {
+    for (uint32_t g = gg; g < E.xG; g += kXrGroups) {
       XHdr *p = E.xslab + (uint64_t)g * E.cap + s;
       const XHdr x = *p;
       if (x.cnt) {
@@ -176,8 +211,7 @@ __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E)
   part[gg][sl] = acc;
   __syncthreads();
   if (gg != 0 || s >= E.cap) return;
-#pragma unroll
-  for (uint32_t k = 1; k < 16; ++k) {
+  for (uint32_t k = 1; k < kXrGroups; ++k) {
     const XHdr x = part[k][sl];
     acc.cnt += x.cnt;
     acc.zero += x.zero;
@@ -185,6 +219,7 @@ __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E)
     acc.minx = x.minx > acc.minx ? x.minx : acc.minx;
     acc.max = x.max > acc.max ? x.max : acc.max;
   }
+  if (E.lcount) E.lcount[s] = acc.cnt - acc.zero;  // this launch's positive durations (expo_select_kernel)
   if (acc.cnt) {
     ExpoHdr &h = E.hdr[s];
     const unsigned long long minpos = ~acc.minx;  // UINT64_MAX when no positive duration
@@ -200,16 +235,155 @@ __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E)
   rescale_slot(E, s);
 }
 
+constexpr uint32_t kXcBlock = 1024;
+constexpr uint64_t kXcMaxSpans = 65535;  // u16 LDS counts: spans per counting workgroup
+
+// Bucket counting of small tables, three kernels:
+//   expo_select_kernel     one block: the xc_ne series with the most positive
+//                          durations this launch get an LDS entry each (by
+//                          bit length of the count, ties in slot order)
+//   expo_count_slab_kernel per span: bucket index at the series' scale; an
+//                          entry's spans add to LDS u16 counts, which leave
+//                          as plain coalesced stores into the workgroup's slab;
+//                          other spans add to the HBM buckets with an atomic
+//   expo_fold_slab_kernel  per (entry, bucket pair): the sum over the
+//                          workgroups' slabs, added to the series' buckets
+//                          (one owner, no atomics)
+// A launch's C2 mix (10 M spans, ~1.4 k series, Zipf) put ~6 M atomics on
+// HBM with per-workgroup caches flushed by atomics: ~200 us of the ~310 us
+// the counting took.
+__global__ __launch_bounds__(1024) void expo_select_kernel(ExpoParams E) {
+  __shared__ uint32_t hist[33], scan[1024], tb_room[2];
+  const uint32_t t = threadIdx.x, cap = (uint32_t)E.cap, K = E.xc_ne;
+  // cap <= 2048: slots 2t and 2t + 1
+  uint32_t c[2], bl[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t sl = 2 * t + k;
+    c[k] = sl < cap ? E.lcount[sl] : 0u;
+    bl[k] = c[k] ? 32u - (uint32_t)__clz(c[k]) : 0u;
+  }
+  if (t < 33) hist[t] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    if (bl[k]) atomicAdd(&hist[bl[k]], 1u);
+  __syncthreads();
+  if (t == 0) {  // the bit length at which the K entries run out, and the room left there
+    uint32_t acc = 0, tb = 0;
+    for (uint32_t b = 32; b >= 1; --b) {
+      if (acc + hist[b] > K) {
+        tb = b;
+        break;
+      }
+      acc += hist[b];
+    }
+    tb_room[0] = tb;
+    tb_room[1] = K - acc;
+  }
+  __syncthreads();
+  const uint32_t tb = tb_room[0], room = tb_room[1];
+  // inclusive block scan of a per-thread value (two slots per thread)
+  auto block_scan = [&](uint32_t v) -> uint32_t {
+    scan[t] = v;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+      const uint32_t x = t >= o ? scan[t - o] : 0u;
+      __syncthreads();
+      scan[t] += x;
+      __syncthreads();
+    }
+    const uint32_t r = scan[t];
+    __syncthreads();
+    return r;
+  };
+  // boundary-bin slots in slot order take the room left
+  const uint32_t b0 = (tb && bl[0] == tb) ? 1u : 0u, b1 = (tb && bl[1] == tb) ? 1u : 0u;
+  const uint32_t bx = block_scan(b0 + b1) - (b0 + b1);  // exclusive
+  bool sel[2];
+  sel[0] = bl[0] && (bl[0] > tb || (b0 && bx < room));
+  sel[1] = bl[1] && (bl[1] > tb || (b1 && bx + b0 < room));
+  const uint32_t n0 = sel[0] ? 1u : 0u, n1 = sel[1] ? 1u : 0u;
+  const uint32_t ex = block_scan(n0 + n1) - (n0 + n1);
+  if (2 * t < cap) E.entry_of[2 * t] = sel[0] ? (int32_t)ex : -1;
+  if (2 * t + 1 < cap) E.entry_of[2 * t + 1] = sel[1] ? (int32_t)(ex + n0) : -1;
+  if (sel[0]) E.slot_of_entry[ex] = 2 * t;
+  if (sel[1]) E.slot_of_entry[ex + n0] = 2 * t + 1;
+  const uint32_t nsel = scan[1023];  // (the last scan's total, still in LDS)
+  for (uint32_t k = nsel + t; k < K; k += 1024) E.slot_of_entry[k] = ~0u;
+}
+
+__global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uint64_t per_wg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t M = E.max_size, NE = E.xc_ne, cap = (uint32_t)E.cap, wpe = (M + 1) / 2;
+  int2 *meta = reinterpret_cast<int2 *>(smem);                   // [cap] {scale, cur}
+  int32_t *ent = reinterpret_cast<int32_t *>(meta + cap);         // [cap] entry or -1
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(ent + cap);        // [NE][wpe] u16 pairs
+  for (uint32_t i = threadIdx.x; i < cap; i += kXcBlock) {
+    const ExpoHdr &h = E.hdr[i];
+    meta[i] = make_int2(h.scale, (int)h.cur);
+    ent[i] = E.entry_of[i];
+  }
+  for (uint32_t i = threadIdx.x; i < NE * wpe; i += kXcBlock) cnt[i] = 0;
+  __syncthreads();
+  const uint64_t lo = blockIdx.x * per_wg, hi = lo + per_wg < E.n ? lo + per_wg : E.n;
+  for (uint64_t i = lo + threadIdx.x; i < hi; i += kXcBlock) {
+    const uint32_t slot = E.slot_of[i];
+    const uint64_t st = E.start[i], en = E.end[i];
+    if (slot == kNotFound) continue;
+    const uint64_t d = en > st ? en - st : 0;
+    if (d == 0) continue;
+    const int2 m = meta[slot];
+    int32_t ix;
+    if (!expo_index_fast(d, E.log2div, m.x, ix)) ix = expo_index(expo_value(d, E.div), m.x);
+    const uint32_t at = expo_mod(ix, M);
+    const int32_t en_ = ent[slot];
+    if (en_ >= 0) atomicAdd(&cnt[(uint32_t)en_ * wpe + (at >> 1)], 1u << ((at & 1u) * 16));
+    else atomicAdd(E.buckets + ((uint64_t)m.y * E.cap + slot) * M + at, 1u);
+  }
+  __syncthreads();
+  uint32_t *slab = E.xcslab + (uint64_t)blockIdx.x * NE * wpe;
+  for (uint32_t i = threadIdx.x; i < NE * wpe; i += kXcBlock) slab[i] = cnt[i];
+}
+
+// (entry, word) x 16 workgroup groups per block of 1024 threads
+__global__ __launch_bounds__(1024) void expo_fold_slab_kernel(ExpoParams E, uint32_t grid) {
+  __shared__ uint32_t part[16][64][2];
+  const uint32_t M = E.max_size, wpe = (M + 1) / 2, total = E.xc_ne * wpe;
+  const uint32_t wl = threadIdx.x & 63u, gq = threadIdx.x >> 6;
+  const uint32_t w = blockIdx.x * 64u + wl;
+  uint32_t lo = 0, hi = 0;
+  if (w < total) {
+#pragma unroll 8
+    for (uint32_t g = gq; g < grid; g += 16) {
+      const uint32_t v = E.xcslab[(uint64_t)g * total + w];
+      lo += v & 0xFFFFu;
+      hi += v >> 16;
+    }
+  }
+  part[gq][wl][0] = lo;
+  part[gq][wl][1] = hi;
+  __syncthreads();
+  if (gq != 0 || w >= total) return;
+  for (uint32_t k = 1; k < 16; ++k) {
+    lo += part[k][wl][0];
+    hi += part[k][wl][1];
+  }
+  const uint32_t e = w / wpe, q = w % wpe, slot = E.slot_of_entry[e];
+  if (slot == ~0u || (lo | hi) == 0) return;
+  uint32_t *b = E.buckets + ((uint64_t)E.hdr[slot].cur * E.cap + slot) * M;
+  if (lo) b[2 * q] += lo;
+  if (hi && 2 * q + 1 < M) b[2 * q + 1] += hi;
+}
+
 // Bucket counting with per-workgroup LDS privatisation: the slots' (scale,
 // buffer) in LDS, and a cache of kXcEntries series (claimed first come, four
 // probes from the slot's home, so a mix's frequent series hold them) whose
 // max_size bucket counts are added in LDS and leave once per workgroup; spans
 // of other series add to the HBM buckets directly.
-constexpr uint32_t kXcBlock = 1024;
 // u16 cache counts (a workgroup takes at most 2^16 - 1 spans): 64 KiB, so two
 // workgroups share a CU with the slot table
 constexpr uint32_t kXcLdsBudget = 64 * 1024;
-constexpr uint64_t kXcMaxSpans = 65535;
 __host__ __device__ inline uint32_t xc_entries(uint32_t max_size) {
   uint32_t e = 256;
   while (e > 4 && (uint64_t)e * max_size * 2 > kXcLdsBudget) e >>= 1;
@@ -236,10 +410,13 @@ __global__ __launch_bounds__(kXcBlock) void expo_count_cached_kernel(ExpoParams 
     const uint64_t d = en > st ? en - st : 0;
     if (d == 0) continue;
     const int2 m = meta[slot];
-    const uint32_t at = expo_mod(expo_index(expo_value(d, E.div), m.x), M);
+    int32_t ix;
+    if (E.diag & 8u) ix = (int32_t)(d & 127u);
+    else if ((E.diag & 4u) || !expo_index_fast(d, E.log2div, m.x, ix)) ix = expo_index(expo_value(d, E.div), m.x);
+    const uint32_t at = expo_mod(ix, M);
     uint32_t e = (((slot * 0x9E3779B1u) >> 16) & (NE / 4 - 1)) * 4, hit = kNotFound;  // home group of 4
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
+    for (uint32_t k = 0; k < 4 && !(E.diag & 2u); ++k) {
       uint32_t t = tag[e + k];
       if (t == 0) t = atomicCAS(&tag[e + k], 0u, slot + 1);
       if (t == 0 || t == slot + 1) {
@@ -248,7 +425,8 @@ __global__ __launch_bounds__(kXcBlock) void expo_count_cached_kernel(ExpoParams 
       }
     }
     if (hit != kNotFound) atomicAdd(&cnt[(hit * M + at) >> 1], 1u << (((hit * M + at) & 1u) * 16));
-    else atomicAdd(E.buckets + ((uint64_t)m.y * E.cap + slot) * M + at, 1u);
+    else if (!(E.diag & 1u)) atomicAdd(E.buckets + ((uint64_t)m.y * E.cap + slot) * M + at, 1u);
+    else if (at == 0xFFFFFFFFu) E.buckets[0] = 0;  // keeps the index live
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < NE * M; i += kXcBlock) {
@@ -321,6 +499,21 @@ __host__ __device__ ExpoHdr expo_hdr_empty() {
   return h;
 }
 
+uint32_t expo_slab_entries(uint64_t cap, uint32_t max_size, size_t budget) {
+  const size_t fixed = (size_t)cap * 12, per = (size_t)((max_size + 1) / 2) * 4;
+  if (budget <= fixed + per) return 0;
+  return (uint32_t)std::min<size_t>(cap, (budget - fixed) / per);
+}
+
+size_t expo_slab_lds_bytes(uint64_t cap, uint32_t max_size, uint32_t ne) {
+  return (size_t)cap * 12 + (size_t)ne * ((max_size + 1) / 2) * 4;
+}
+
+hipError_t prepare_expo_slab(size_t lds_bytes) {
+  return hipFuncSetAttribute((const void *)&expo_count_slab_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds_bytes);
+}
+
 size_t expo_count_lds_bytes(uint64_t cap, uint32_t max_size) {
   const uint32_t ne = xc_entries(max_size);
   return (size_t)cap * 8 + (size_t)ne * 4 + ((size_t)ne * max_size + 1) / 2 * 4;
@@ -331,10 +524,35 @@ hipError_t prepare_expo_count(size_t lds_bytes) {
                              (int)lds_bytes);
 }
 
+// slots per reduce block (SPANAGG_XR: 16 / 32 / 64, A/B runs)
+void launch_reduce_rescale(const ExpoParams &E, hipStream_t s) {
+  static const uint32_t xr = [] {
+    const char *v = std::getenv("SPANAGG_XR");
+    const uint32_t x = v ? (uint32_t)std::atoi(v) : 64u;
+    return x == 16 || x == 32 ? x : 64u;
+  }();
+  const dim3 g((uint32_t)((E.cap + xr - 1) / xr));
+  if (xr == 16) hipLaunchKernelGGL(expo_reduce_rescale_kernel<16>, g, dim3(1024), 0, s, E);
+  else if (xr == 32) hipLaunchKernelGGL(expo_reduce_rescale_kernel<32>, g, dim3(1024), 0, s, E);
+  else hipLaunchKernelGGL(expo_reduce_rescale_kernel<64>, g, dim3(1024), 0, s, E);
+}
+
 hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s) {
   if (E.n == 0) return hipSuccess;
+  if (E.xslab && E.xc_ne) {  // small table, slab counting (E.xG workgroups, <= kXcMaxSpans spans each)
+    launch_reduce_rescale(E, s);
+    hipLaunchKernelGGL(expo_select_kernel, dim3(1), dim3(1024), 0, s, E);
+    const uint64_t per_wg = (E.n + E.xG - 1) / E.xG;
+    if (per_wg > kXcMaxSpans) return hipErrorInvalidValue;  // (the engine splits batches below this)
+    const uint32_t grid = (uint32_t)((E.n + per_wg - 1) / per_wg);
+    hipLaunchKernelGGL(expo_count_slab_kernel, dim3(grid), dim3(kXcBlock),
+                       expo_slab_lds_bytes(E.cap, E.max_size, E.xc_ne), s, E, per_wg);
+    const uint32_t words = E.xc_ne * ((E.max_size + 1) / 2);
+    hipLaunchKernelGGL(expo_fold_slab_kernel, dim3((words + 63) / 64), dim3(1024), 0, s, E, grid);
+    return hipGetLastError();
+  }
   if (E.xslab) {  // small table: the ingest kernel left header partials and slots
-    hipLaunchKernelGGL(expo_reduce_rescale_kernel, dim3((uint32_t)((E.cap + 63) / 64)), dim3(1024), 0, s, E);
+    launch_reduce_rescale(E, s);
     // u16 LDS counts: at most kXcMaxSpans spans per workgroup; ~512 workgroups (two per CU)
     const uint64_t per_wg = std::min<uint64_t>(kXcMaxSpans, std::max<uint64_t>(4096, (E.n + 511) / 512));
     const uint32_t grid = (uint32_t)((E.n + per_wg - 1) / per_wg);
@@ -369,6 +587,47 @@ __global__ void expo_index_probe_kernel(const double *v, const int32_t *scale, i
 __global__ void go_log_probe_kernel(const double *v, double *out, uint64_t n) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     out[i] = go_log(v[i]);
+}
+
+// (tests) |v_log_f32(m) - log2(m)| over the floats m = 1 + i * 2^-23, i in
+// [i0, i0 + n): the per-block maxima, as doubles
+__global__ __launch_bounds__(256) void log2_err_probe_kernel(uint32_t i0, uint32_t n, double *block_max) {
+  __shared__ double red[256];
+  double mx = 0;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+    const float m = 1.0f + (float)(i0 + i) * 0x1p-23f;
+    const double err = fabs((double)__builtin_amdgcn_logf(m) - log2((double)m));
+    mx = err > mx ? err : mx;
+  }
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  for (uint32_t o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o && red[threadIdx.x + o] > red[threadIdx.x]) red[threadIdx.x] = red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) block_max[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(256) void expo_fast_probe_kernel(const uint64_t *d, const int32_t *scale, uint64_t n,
+                                                             double div, double log2div, int32_t *fast,
+                                                             int32_t *exact) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+    int32_t ix;
+    fast[i] = expo_index_fast(d[i], log2div, scale[i], ix) ? ix : INT32_MIN;
+    exact[i] = expo_index(expo_value(d[i], div), scale[i]);
+  }
+}
+
+hipError_t launch_expo_fast_probe(const uint64_t *d, const int32_t *scale, uint64_t n, double div, int32_t *fast,
+                                  int32_t *exact, hipStream_t s) {
+  hipLaunchKernelGGL(expo_fast_probe_kernel, dim3(grid_of(n)), dim3(256), 0, s, d, scale, n, div, std::log2(div), fast,
+                     exact);
+  return hipGetLastError();
+}
+
+hipError_t launch_log2_err_probe(uint32_t i0, uint32_t n, double *block_max, uint32_t blocks, hipStream_t s) {
+  hipLaunchKernelGGL(log2_err_probe_kernel, dim3(blocks), dim3(256), 0, s, i0, n, block_max);
+  return hipGetLastError();
 }
 
 hipError_t launch_expo_probe(const double *v, const int32_t *scale, int32_t *idx_out, double *log_out, uint64_t n,

@@ -470,21 +470,34 @@ __device__ __forceinline__ void cold_lookup_wave(unsigned long long *lkeys, bool
 }
 
 // Adds one ERROR span of (window slot, key slot) key `ek` (< 65535) to the
-// workgroup's LDS table (open addressing, 4 probes); false when those are taken
-// by other keys (the caller then falls back to a global atomic).
+// workgroup's LDS table: 256 aligned groups of 4 entries {(ek + 1) << 16 |
+// count}; false when the key's group is taken by other keys (the caller then
+// falls back to a global atomic).  The common case -- the key already in its
+// group -- is one ds_read_b128, four compares and one ds_add; the claim loop
+// runs once per key per workgroup.  (A linear 4-probe loop with a CAS per
+// probe compiled to ~100 mostly scalar instructions per wave step: 2 % of
+// spans are ERROR, so nearly every 128-span wave step has one.)
 __device__ __forceinline__ bool lds_err_add(uint32_t *etab, uint32_t ek) {
   const uint32_t tag = (ek + 1) << 16;
-  const uint32_t h = (ek * 0x9E3779B1u) >> (32 - 10);  // kErrTab = 1024
-#pragma unroll
+  uint32_t *grp = etab + ((ek * 0x9E3779B1u) >> (32 - 8)) * 4;  // kErrTab = 1024
+  const uint4 v = *reinterpret_cast<const uint4 *>(grp);
+  const int at = (v.x & 0xFFFF0000u) == tag   ? 0
+                 : (v.y & 0xFFFF0000u) == tag ? 1
+                 : (v.z & 0xFFFF0000u) == tag ? 2
+                 : (v.w & 0xFFFF0000u) == tag ? 3
+                                              : -1;
+  if (__builtin_expect(at >= 0, 1)) {
+    atomicAdd(grp + at, 1u);
+    return true;
+  }
   for (int q = 0; q < 4; ++q) {
-    uint32_t *c = etab + ((h + q) & (kErrTab - 1));
-    uint32_t v = *c;
-    if (v == 0) {
-      v = atomicCAS(c, 0u, tag | 1u);
-      if (v == 0) return true;
+    uint32_t w = grp[q];
+    if (w == 0) {
+      w = atomicCAS(grp + q, 0u, tag | 1u);
+      if (w == 0) return true;
     }
-    if ((v & 0xFFFF0000u) == tag) {
-      atomicAdd(c, 1u);
+    if ((w & 0xFFFF0000u) == tag) {
+      atomicAdd(grp + q, 1u);
       return true;
     }
   }

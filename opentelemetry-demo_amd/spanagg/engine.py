@@ -303,6 +303,22 @@ class Engine:
                                            logs.ctypes.data_as(_lib.f64p)), "sa_expo_probe")
         return idx, logs
 
+    def expo_fast_probe(self, d_ns, scales, log2_err=True):
+        """The counting kernel's bucket-index fast path (diagnostic): (fast,
+        exact, max log2 error) -- fast[i] is INT32_MIN where it defers to the
+        exact path; the error is the hardware log2's over every float in [1, 2)."""
+        d = np.ascontiguousarray(d_ns, dtype=np.uint64)
+        s = np.ascontiguousarray(scales, dtype=np.int32)
+        fast = np.zeros(len(d), dtype=np.int32)
+        exact = np.zeros(len(d), dtype=np.int32)
+        err = C.c_double(0.0)
+        self._check(self.lib.sa_expo_fast_probe(self._h, d.ctypes.data_as(_lib.u64p),
+                                                s.ctypes.data_as(C.POINTER(C.c_int32)), len(d),
+                                                fast.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                exact.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                C.byref(err) if log2_err else None), "sa_expo_fast_probe")
+        return fast, exact, err.value
+
     def window_advance(self, new_base: int):
         self._check(self.lib.sa_window_advance(self._h, int(new_base)), "sa_window_advance")
 

@@ -56,6 +56,49 @@ def test_gpu_log_and_index_bit_exact():
         assert int(gi[0]) == i
 
 
+def test_fast_log2_error_bound():
+    """The counting kernel's fast path assumes |v_log_f32(m) - log2(m)| <=
+    2^-20 over every float m in [1, 2) (kFastLog2Err in spanagg_expo.hip adds
+    the 24-bit truncation of the duration): measured here exhaustively on the
+    device, so a part whose hardware log2 were less accurate fails this test
+    instead of mis-bucketing near bucket boundaries."""
+    with Engine(Config(exp_max_size=160)) as e:
+        _, _, err = e.expo_fast_probe([], [])
+    assert 0 < err <= 2.0 ** -20, err
+
+
+@pytest.mark.parametrize("unit", ["ms", "s"])
+def test_fast_index_agrees_with_exact_path(unit):
+    """Wherever the fast path answers it gives the exact (Go math.Log) index;
+    near bucket boundaries and powers of two it defers.  Durations: random over
+    1 ns .. ~1 day, every power of two, and values straddling bucket
+    boundaries at each scale."""
+    rng = np.random.default_rng(11)
+    div = 1e9 if unit == "s" else 1e6
+    d = np.concatenate([
+        np.exp(rng.uniform(0, np.log(8.64e13), 300000)).astype(np.uint64) + 1,
+        2 ** np.arange(0, 47, dtype=np.uint64),
+        rng.integers(1, 2**20, 50000, dtype=np.uint64)])
+    # boundary straddlers: d near div * 2^(k / 2^s) for a few scales
+    b = []
+    for s in (1, 3, 5, 8, 12):
+        for k in rng.integers(-20 * 2**s, 30 * 2**s, 400):
+            c = div * 2.0 ** (float(k) / 2**s)
+            if 2 <= c < 2**62:
+                b += [int(c) - 1, int(c), int(c) + 1]
+    d = np.concatenate([d, np.array(b, dtype=np.uint64)])
+    scales = rng.integers(-4, 21, len(d)).astype(np.int32)
+    with Engine(Config(exp_max_size=160, unit="s" if unit == "s" else "ms")) as e:
+        fast, exact, _ = e.expo_fast_probe(d, scales, log2_err=False)
+    taken = fast != np.iinfo(np.int32).min
+    assert np.array_equal(fast[taken], exact[taken])
+    # spot-check the exact column against the oracle's restatement
+    for i in rng.integers(0, len(d), 3000):
+        assert int(exact[i]) == pyoracle.expo_index(float(d[i]) / div, int(scales[i])), (int(d[i]), int(scales[i]))
+    low = scales <= 8
+    assert taken[low].mean() > 0.99, taken[low].mean()  # the fast path carries the common case
+
+
 @pytest.mark.parametrize("path", ["small", "hbm"])
 @pytest.mark.parametrize("max_size,unit", [(160, "ms"), (8, "ms"), (20, "s"), (2, "ms")])
 def test_expo_histograms_match_oracle(max_size, unit, path, monkeypatch):
