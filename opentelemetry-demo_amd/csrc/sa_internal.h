@@ -101,7 +101,7 @@ struct IngestParams {
   // exponential-histogram engines on the small-table kernel (EXPO): the key
   // slot of every span (for the bucket-counting pass) and the per-workgroup
   // header slabs [G][cap] (XHdr) the rescale pass reduces
-  uint32_t *slot_of;
+  uint32_t *slot_of;  // EXPO mode: [n] key slot of each span (kNotFound without one)
   XHdr *xslab;
 };
 // One workgroup's exponential-histogram header partial for one key slot
@@ -139,7 +139,7 @@ struct ExpoParams {
   double log2div;     // log2(div), for the bucket index's fast path
   uint32_t diag;      // ablation bits (SPANAGG_XC_DIAG, profiling only; results wrong when set):
                       // 1 no HBM bucket atomics, 2 no LDS cache, 4 exact index path only, 8 no index
-  uint32_t *slot_of;  // [n] key slot of each span (pass 1 -> pass 3)
+  uint32_t *slot_of;  // [n] key slot of each span (pass 1 / the small-table ingest kernel -> counting)
   unsigned long long *dropped;
   XHdr *xslab;        // small-table engines: [xG][cap] per-workgroup header partials (nullptr: pass 1 atomics)
   uint32_t xG;

@@ -182,11 +182,11 @@ __global__ __launch_bounds__(256) void expo_rescale_kernel(ExpoParams E) {
 }
 
 // Small-table engines: the ingest kernel (EXPO mode) leaves per-workgroup
-// header partials in slabs [xG][cap].  One block per 16 slots: 64 groups of
-// 16 threads sum every 64th workgroup's partials (each wave reads four 512-B
-// runs, zeroing what it consumed), LDS combines the groups, then one thread
-// per slot folds the sum into the series header and rescales it.  (64 slots
-// per block gave cap / 64 = 32 blocks at C2's table: 29 us, latency-bound.)
+// header partials in slabs [xG][cap].  One block per kXrSlots slots (32 by
+// default): 1,024 / kXrSlots groups sum a strided share of the workgroups'
+// partials (coalesced runs, zeroing what they consumed), LDS combines the
+// groups, then one thread per slot folds the sum into the series header and
+// rescales it.
 template <uint32_t kXrSlots>
 __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E) {
   constexpr uint32_t kXrGroups = 1024 / kXrSlots;
@@ -524,12 +524,13 @@ hipError_t prepare_expo_count(size_t lds_bytes) {
                              (int)lds_bytes);
 }
 
-// slots per reduce block (SPANAGG_XR: 16 / 32 / 64, A/B runs)
+// slots per reduce block (SPANAGG_XR: 16 / 32 / 64, A/B runs; rocprofv3 medians at
+// C2's table: 38.5 / 21.1 / 29.4 us)
 void launch_reduce_rescale(const ExpoParams &E, hipStream_t s) {
   static const uint32_t xr = [] {
     const char *v = std::getenv("SPANAGG_XR");
-    const uint32_t x = v ? (uint32_t)std::atoi(v) : 64u;
-    return x == 16 || x == 32 ? x : 64u;
+    const uint32_t x = v ? (uint32_t)std::atoi(v) : 32u;
+    return x == 16 || x == 64 ? x : 32u;
   }();
   const dim3 g((uint32_t)((E.cap + xr - 1) / xr));
   if (xr == 16) hipLaunchKernelGGL(expo_reduce_rescale_kernel<16>, g, dim3(1024), 0, s, E);
