@@ -50,7 +50,7 @@ for step in "$@"; do
     ablate_*) wl=${step#ablate_}; ABL_WORKLOAD=$wl ABL_VARS=${ABL_VARS:-} run "ablate_$wl" 400 python tools/ablate.py ;;
     trace_*) wl=${step#trace_}
       (cd /tmp && run "trace_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$wl" -o run \
-         -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 10 --warmup 2 --streams 1 $BQ) || exit $? ;;
+         -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 10 --warmup 2 --streams 1 --soak-s 0 $BQ) || exit $? ;;
     pmc_*) rest=${step#pmc_}; wl=${rest%%_*}; set_=${rest#*_}
       case $set_ in
         fetch) ctr="FETCH_SIZE" ;;
@@ -62,7 +62,7 @@ for step in "$@"; do
         ta) ctr="TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_PENDING_STALL_CYCLES_sum GRBM_GUI_ACTIVE" ;;
         *) echo "unknown pmc set $set_" >> "$OUT/status.txt"; exit 2 ;;
       esac
-      (cd /tmp && PROF_WORKLOAD=$wl run "pmc_${wl}_$set_" 120 rocprofv3 --pmc $ctr --output-format csv \
+      (cd /tmp && PROF_WORKLOAD=$wl PROF_REPS=${PROF_REPS:-24} run "pmc_${wl}_$set_" 120 rocprofv3 --pmc $ctr --output-format csv \
          -d "$OUT/pmc_${wl}_$set_" -o run -- python3 "$ROOTDIR/tools/prof_driver.py") || exit $? ;;
     *) echo "unknown step $step" >> "$OUT/status.txt"; exit 2 ;;
   esac

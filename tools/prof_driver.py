@@ -20,13 +20,15 @@ from spanagg.synth import generate_c2  # noqa: E402
 n = int(os.environ.get("PROF_SPANS", 10_000_000))
 reps = int(os.environ.get("PROF_REPS", 5))
 wk = os.environ.get("PROF_WORKLOAD", "c2")
+exp_max = 0
 if wk in ("c4", "c4zipf"):  # 1 M series, HBM table (binned path)
     from spanagg.synth import generate_highcard
     batch, _, first = generate_highcard(n, seed=7, zipf_s=1.1 if wk == "c4zipf" else 0.0)
     n_services, kcap = 1, 1_200_000
-else:
+else:  # c2, c2expo (exponential histograms, max_size 160)
     wl = generate_c2(n, seed=42)
     batch, first, n_services, kcap = wl.batch, wl.first_window, wl.n_services, 1500
+exp_max = 160 if wk == "c2expo" else 0
 cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).cuda()
         for c in batch.columns()]
 s = torch.cuda.Stream()
@@ -38,10 +40,11 @@ if os.environ.get("PROF_FRESH", "1") != "0":
 else:
     variants = [(cols[3], cols[4])] * reps
 torch.cuda.synchronize()
-with Engine(Config(n_services=n_services, n_windows=16, flags=flags, key_capacity=kcap)) as e:
+with Engine(Config(n_services=n_services, n_windows=16, flags=flags, key_capacity=kcap,
+                   exp_max_size=exp_max)) as e:
     e.window_advance(first)
     for w0, w1 in variants:
         e.ingest_device(cols[0], cols[1], cols[2], w0, w1, cols[5], n=n, stream=s.cuda_stream)
     torch.cuda.synchronize()
-    r = e.flush()
-    print("calls", int(r.calls.sum()), "expected", reps * n)
+    r = e.flush_exp() if exp_max else e.flush()
+    print("calls", int(r.count.sum() if exp_max else r.calls.sum()), "expected", reps * n)

@@ -3,7 +3,8 @@
 passes of tools/gpu_job.sh (pmc_<wl>_fetch, pmc_<wl>_write over
 tools/prof_driver.py): per ingest launch -- the mean over launches (first
 dropped) of each hot-path kernel, summed over the kernels of one launch (C2:
-ingest_v2_kernel; C4: bt_scatter2 + bt_aggregate2) -- FETCH_SIZE doubled per
+ingest_v2_kernel; C4: bt_scatter2 + bt_aggregate3;
+c2expo: ingest_v2 + the expo_* kernels of a launch) -- FETCH_SIZE doubled per
 MI355X_MICROARCH.md's gfx950 correction, KB = 1024 B.
 
   python tools/traffic.py <job dir> <workload> <round> <out.json>"""
@@ -21,7 +22,7 @@ def _pick(ids):
     return ids[-k:] if k else (ids[1:] or ids)
 
 
-HOT = ("ingest", "bt_scatter", "bt_aggregate")
+HOT = ("ingest", "bt_scatter", "bt_aggregate", "expo_")
 
 
 def per_launch(path, counter):
@@ -49,8 +50,8 @@ def main():
          "per_kernel_kb": {"fetch": fk, "write": wk},
          "hbm_bytes_per_launch": int((2 * f + w) * 1024),
          "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (tools/gpu_job.sh "
-                   "pmc_<wl>_fetch / _write over tools/prof_driver.py: 5 launches of the 10M-span batch, "
-                   "first dropped); FETCH_SIZE doubled per MI355X_MICROARCH.md gfx950 correction; KB=1024 B",
+                   "pmc_<wl>_fetch / _write over tools/prof_driver.py: PROF_REPS launches of the 10M-span batch, each "
+                   "a fresh trace-id variant; the last PMC_LAST averaged, else all but the first); FETCH_SIZE doubled per MI355X_MICROARCH.md gfx950 correction; KB=1024 B",
          "round": rnd}
     t["traffic_over_algorithmic"] = t["hbm_bytes_per_launch"] / t["algorithmic_bytes_per_launch"]
     json.dump(t, open(out, "w"), indent=1)
