@@ -415,31 +415,46 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
   for (uint32_t b = threadIdx.x; b < kPartBins; b += kBtBlock)
     P.bt_cnt[(uint64_t)b * P.bt_grid + blockIdx.x] = min((rcnw[b >> 1] >> ((b & 1u) * 16)) & 0xFFFFu, region);
   __syncthreads();
-  // the overflow table: one row update per entry (atomics: entries of one
-  // key may come from several workgroups)
+  // the overflow table: each entry's key slot (find-or-insert, one lane per
+  // entry) into the LDS of the flush lists (the stages are all out) ...
+  uint32_t *hslot = reinterpret_cast<uint32_t *>(flist);  // [kBt2Hot]
   for (uint32_t h = threadIdx.x; h < kBt2Hot; h += kBtBlock) {
     const unsigned long long m = hkey[h];
-    if (m == 0) continue;
-    const uint32_t s = bt_find_insert(P.gkeys, m, P.log2sb);
-    if (s == kNotFound) {
-      for (uint32_t b = 0; b < P.nbk; ++b) n_drop += (hcnt[h * kPartWords + (b >> 1)] >> ((b & 1u) * 16)) & 0xFFFFu;
-      continue;
+    uint32_t s = kNotFound;
+    if (m != 0) {
+      s = bt_find_insert(P.gkeys, m, P.log2sb);
+      if (s == kNotFound)
+        for (uint32_t b = 0; b < P.nbk; ++b) n_drop += (hcnt[h * kPartWords + (b >> 1)] >> ((b & 1u) * 16)) & 0xFFFFu;
     }
-    for (uint32_t b = 0; b < P.nbk; ++b) {
-      const uint32_t c = (hcnt[h * kPartWords + (b >> 1)] >> ((b & 1u) * 16)) & 0xFFFFu;
-      if (c) spill_add(P.base64, P.nbk, s, b, c, 0);
+    hslot[h] = s;
+  }
+  __syncthreads();
+  // ... then its row added to the spill array (atomics: the entries of one key
+  // come from every workgroup), two entries per wave instruction and one cell
+  // per lane: an entry's nbk counts and ns sum are contiguous in base64, so it
+  // leaves as three 64-B atomic requests, where one lane's nbk + 1 serial
+  // atomics made a Zipf mix's epilogue (hundreds of hot keys in every
+  // workgroup's table) the scatter's longest phase
+  {
+    const uint32_t half = lane >> 5, cell = lane & 31u, nc = P.nbk + 1;
+    static_assert(kBt2Hot % 2 == 0 && kPartMaxBk + 1 <= 32, "overflow flush geometry");
+    for (uint32_t h0 = wave * 2; h0 < kBt2Hot; h0 += kWaves * 2) {
+      const uint32_t h = h0 + half;
+      const uint32_t s = hslot[h];
+      if (s == kNotFound || cell >= nc) continue;
+      const unsigned long long v = cell == P.nbk ? hsum[h]
+                                                 : (hcnt[h * kPartWords + (cell >> 1)] >> ((cell & 1u) * 16)) & 0xFFFFu;
+      if (v) atomicAdd(P.base64 + (uint64_t)s * nc + cell, v);
     }
-    spill_add(P.base64, P.nbk, s, 0, 0, hsum[h]);
   }
   if (threadIdx.x < kBt2HotErr) {
     const uint2 e = herr[threadIdx.x];
     if (e.x) {
       const uint32_t ws = (e.x - 1) >> 8, h = (e.x - 1) & 0xFFu;
-      const uint64_t m = hkey[h];
-      const uint32_t s = bt_find_insert(P.gkeys, m, P.log2sb);
+      const uint32_t s = hslot[h];
       if (s != kNotFound) atomicAdd(P.errcnt + ((uint64_t)ws << P.log2cap) + s, (unsigned long long)e.y);
       else
-        for (uint32_t i = 0; i < e.y; ++i) bt_cms_add(kp, ws, m * P.kinv);
+        for (uint32_t i = 0; i < e.y; ++i) bt_cms_add(kp, ws, hkey[h] * P.kinv);
     }
   }
   const uint32_t nq = min(hq_n[0], kBtHq);
@@ -706,7 +721,16 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
 // in the bin, or placed past them) takes the probe loop, rare after the first
 // launches.  ERROR records append (window slot, key slot) to an LDS list,
 // added to errcnt after the records (global atomics past the list's 255).
-template <int MODE = 0, int MAXPER = 2, int BLOCK = 512>
+// NB: record batch (region pairs per wave whose loads are issued together);
+// EARLY: each occupied slot's row is read right after the key slots, so its
+// round trip overlaps the records instead of following them.
+// PF: right after the setup barrier every thread touches one dword of its
+// 128-B lines of the bin's records (by the region fills) and of its rows
+// (one HBM round trip for all of them), so the record batches and the row
+// read-modify-write find their lines in L2 instead of paying an HBM round
+// trip each (the loaded words only feed a never-taken branch, which keeps
+// the loads).
+template <int MODE = 0, int MAXPER = 2, int BLOCK = 512, int NB = 4, bool EARLY = false, bool PF = false>
 __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t log2sb = P.log2sb, sb = 1u << log2sb;
@@ -743,6 +767,17 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
   const uint32_t cw = bt_agg2_cnt_words(sb);
   for (uint32_t i = tid; i < cw; i += BLOCK) lcnt[i] = 0;
   if (tid == 0) errl[0] = misc[0] = 0;
+  uint4 *rows = reinterpret_cast<uint4 *>(P.gcounts) + ((uint64_t)bin << log2sb) * (kRowBytes / 16);
+  uint4 rv[kMaxPer][2];
+  if constexpr (EARLY) {  // rows of the occupied slots (a new key's row is zero)
+#pragma unroll
+    for (int u = 0; u < kMaxPer; ++u) {
+      const uint32_t s = tid + u * BLOCK;
+#pragma unroll
+      for (uint32_t q = 0; q < 2; ++q)
+        rv[u][q] = s < sb && orig[u] != 0 ? rows[(uint64_t)s * 2 + q] : make_uint4(0, 0, 0, 0);
+    }
+  }
   __syncthreads();
   bt_stamp(P, (uint64_t)bin * 8, 1);
 
@@ -751,6 +786,17 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
   const __amdgpu_buffer_rsrc_t rrec = rsrc(bin_rec, G * region * 16);
   const uint32_t half = lane >> 5, r0 = lane & 31u;
   const uint32_t pmax = bt_probe_max(log2sb);
+  uint32_t pfv = 0;
+  if constexpr (PF) {
+    const uint32_t *rw = reinterpret_cast<const uint32_t *>(bin_rec);
+    for (uint32_t g = tid >> 1; g < G; g += BLOCK / 2) {
+      const uint32_t nl = (rcnt[g] * 16 + 127) / 128;  // lines of the region's records
+      for (uint32_t l = tid & 1u; l < nl; l += 2) pfv |= rw[((uint64_t)g * region * 16 + l * 128) / 4];
+    }
+    const uint32_t row_lines = (sb * kRowBytes) / 128;
+    const uint32_t *rr = reinterpret_cast<const uint32_t *>(P.gcounts) + ((uint64_t)bin << log2sb) * (kRowBytes / 4);
+    for (uint32_t l = tid; l < row_lines; l += BLOCK) pfv |= rr[l * 32];
+  }
   uint32_t n_drop = 0;
   const ulonglong2 *lk2 = reinterpret_cast<const ulonglong2 *>(lkeys);
   // two records (ok: valid) through the LDS together
@@ -817,7 +863,8 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
     }
   };
   constexpr uint32_t kWaves = BLOCK / 64;
-  constexpr uint32_t B = 4;
+  constexpr uint32_t B = NB;
+  static_assert(B % 2 == 0, "records go through the LDS in pairs");
   const uint32_t pairs = (G + 1) / 2;
   if (!(MODE & 1)) {
     for (uint32_t p0 = wave; p0 < pairs; p0 += kWaves * B) {
@@ -858,6 +905,9 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
   }
   n_drop = wave_sum(n_drop);
   if (lane == 0 && n_drop) atomicAdd(&misc[0], n_drop);
+  if constexpr (PF) {  // never true (P.n < 2^63): keeps the prefetch loads
+    if (pfv == 0x9E3779B9u && (P.n >> 63)) misc[1] = 1;
+  }
   __syncthreads();
   bt_stamp(P, (uint64_t)bin * 8, 2);
 
@@ -865,8 +915,6 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
   //    row read is issued before the first row is written); the ERROR list
   if (MODE & 2) return;
   const uint32_t nbk = P.nbk;
-  uint4 *rows = reinterpret_cast<uint4 *>(P.gcounts) + ((uint64_t)bin << log2sb) * (kRowBytes / 16);
-  uint4 rv[kMaxPer][2];
   bool touched[kMaxPer];
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
@@ -880,8 +928,10 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
       }
       touched[u] = any != 0;
     }
+    if constexpr (!EARLY) {
 #pragma unroll
-    for (uint32_t q = 0; q < 2; ++q) rv[u][q] = touched[u] ? rows[(uint64_t)s * 2 + q] : make_uint4(0, 0, 0, 0);
+      for (uint32_t q = 0; q < 2; ++q) rv[u][q] = touched[u] ? rows[(uint64_t)s * 2 + q] : make_uint4(0, 0, 0, 0);
+    }
   }
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
@@ -947,15 +997,26 @@ static const void *bt_scatter2_fn(uint32_t diag) {
 
 constexpr uint32_t kDiagBtAggWide = 1u << 30, kDiagBtAggLoadOnly = 1u << 31;
 static const void *bt_agg2_fn(uint32_t diag);
-static bool bt_agg_v2() {  // SPANAGG_BT_AGG=2: the second-form aggregate (A/B runs)
-  static const bool v2 = [] {
+static int bt_agg_form() {  // SPANAGG_BT_AGG (A/B runs): 2 = the second-form aggregate;
+                            // 4/5/6 = the third form with NB 8 + early rows / NB 4 + early rows / NB 8
+  static const int f = [] {
     const char *v = std::getenv("SPANAGG_BT_AGG");
-    return v && std::atoi(v) == 2;
+    return v ? std::atoi(v) : 0;
   }();
-  return v2;
+  return f;
 }
+static bool bt_agg_v2() { return bt_agg_form() == 2; }
 static const void *bt_agg_fn(uint32_t diag) {
   const int mode = ((diag & 1u) ? 1 : 0) | ((diag & kDiagBtAggNoRows) ? 2 : 0);
+  // (diag bits 17-19 pick a form per engine in A/B runs: 1 -> 4, 2 -> 5, 3 -> 6, 4 -> 7)
+  const int form = (diag >> 17) & 7u ? 3 + (int)((diag >> 17) & 7u) : bt_agg_form();
+  if (mode == 0 && !(diag & (kDiagBtAggWide | kDiagBtAggLoadOnly))) switch (form) {
+      case 4: return (const void *)&bt_aggregate3_kernel<0, 2, 512, 8, true>;
+      case 5: return (const void *)&bt_aggregate3_kernel<0, 2, 512, 4, true>;
+      case 6: return (const void *)&bt_aggregate3_kernel<0, 2, 512, 8, false>;
+      case 7: return (const void *)&bt_aggregate3_kernel<0, 2, 512, 4, false, true>;
+      default: break;
+    }
   if (!bt_agg_v2() && !(diag & kDiagBtAggLoadOnly)) {
     if (diag & kDiagBtAggWide) switch (mode) {  // bins of 2,048 slots
         case 1: return (const void *)&bt_aggregate3_kernel<1, 4>;
@@ -997,7 +1058,10 @@ hipError_t prepare_ingest_bt(size_t agg_lds) {
       return e;
   for (uint32_t d : {0u, 1u, kDiagBtAggNoRows, 1u | kDiagBtAggNoRows})
     for (uint32_t v : {0u, kDiagBtAggWide, kDiagBtAggLoadOnly})
-      for (const void *fn : {bt_agg_fn(d | v), bt_agg2_fn(d | v)})
+      for (const void *fn : {bt_agg_fn(d | v), bt_agg2_fn(d | v), (const void *)&bt_aggregate3_kernel<0, 2, 512, 8, true>,
+                             (const void *)&bt_aggregate3_kernel<0, 2, 512, 4, true>,
+                             (const void *)&bt_aggregate3_kernel<0, 2, 512, 8, false>,
+                             (const void *)&bt_aggregate3_kernel<0, 2, 512, 4, false, true>})
         if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)agg_lds);
             e != hipSuccess)
           return e;
