@@ -71,7 +71,8 @@ __device__ __forceinline__ KParams kernel_params() {
 }
 
 // Count-min cells of one ERROR span without a key-table slot (d atomics).
-__device__ __forceinline__ void bt_cms_add(KParams Q, uint32_t ws, uint64_t key) {
+template <typename QP>
+__device__ __forceinline__ void bt_cms_add(QP Q, uint32_t ws, uint64_t key) {
   SA_GLOBAL unsigned long long *row0 = gbl(Q->cms) + (uint64_t)ws * Q->cms_d * Q->cms_w;
   for (uint32_t r = 0; r < Q->cms_d; ++r) {
     const uint64_t col = splitmix64(key ^ Q->seeds[r]) >> Q->cms_shift;
@@ -711,26 +712,25 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
 
 
 // Aggregate, third form (the default).  The layout, phases and row
-// write-back of bt_aggregate2_kernel; the records are aggregated two per lane
-// at a time with every LDS access of the pair issued before the first one is
-// waited for -- both records' two key buckets (4 x ds_read_b128 each), then
-// the compares, then both records' counter atomics -- instead of one record's
-// dependent chain after another (a record costs ~6 LDS round trips in
-// sequence there).  Records carry their bucket (the scatter's bin table), so
-// there is no per-record bucketing.  A key missing from its two buckets (new
-// in the bin, or placed past them) takes the probe loop, rare after the first
-// launches.  ERROR records append (window slot, key slot) to an LDS list,
-// added to errcnt after the records (global atomics past the list's 255).
-// NB: record batch (region pairs per wave whose loads are issued together);
-// EARLY: each occupied slot's row is read right after the key slots, so its
-// round trip overlaps the records instead of following them.
-// PF: right after the setup barrier every thread touches one dword of its
-// 128-B lines of the bin's records (by the region fills) and of its rows
-// (one HBM round trip for all of them), so the record batches and the row
-// read-modify-write find their lines in L2 instead of paying an HBM round
-// trip each (the loaded words only feed a never-taken branch, which keeps
-// the loads).
-template <int MODE = 0, int MAXPER = 2, int BLOCK = 512, int NB = 4, bool EARLY = false, bool PF = false>
+// write-back of bt_aggregate2_kernel; the records go through the LDS two per
+// lane at a time with every LDS access of the pair issued before the first
+// one is waited for -- both records' two key buckets (4 x ds_read_b128 each),
+// then the compares, then both records' counter atomics -- instead of one
+// record's dependent chain after another (a record costs ~6 LDS round trips
+// in sequence there).  Records carry their bucket (the scatter's bin table),
+// so there is no per-record bucketing.  A key missing from its two buckets
+// (new in the bin, or placed past them) takes the probe loop, rare after the
+// first launches.  ERROR records append (window slot, key slot) to an LDS
+// list, added to errcnt after the records (global atomics past the list's
+// 255).  The record loop keeps its VALU lean -- 32-bit key arithmetic
+// (records carry m's low 53 bits, so m's high word is (x.hi & 0x1FFFFF) |
+// bin << 21), load offsets stepped per batch, the in-bucket slot picked as an
+// index 0-7 by inline-constant selects -- and its batches of two region pairs
+// are double-buffered: the next batch's loads are issued before this one goes
+// through the LDS.
+// MODE (ablation): 1 = no records aggregated, 2 = no key / row write-back,
+// 16 = no lookup reads, 32 = no counter atomics.
+template <int MODE = 0, int MAXPER = 2, int BLOCK = 512>
 __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t log2sb = P.log2sb, sb = 1u << log2sb;
@@ -767,17 +767,6 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
   const uint32_t cw = bt_agg2_cnt_words(sb);
   for (uint32_t i = tid; i < cw; i += BLOCK) lcnt[i] = 0;
   if (tid == 0) errl[0] = misc[0] = 0;
-  uint4 *rows = reinterpret_cast<uint4 *>(P.gcounts) + ((uint64_t)bin << log2sb) * (kRowBytes / 16);
-  uint4 rv[kMaxPer][2];
-  if constexpr (EARLY) {  // rows of the occupied slots (a new key's row is zero)
-#pragma unroll
-    for (int u = 0; u < kMaxPer; ++u) {
-      const uint32_t s = tid + u * BLOCK;
-#pragma unroll
-      for (uint32_t q = 0; q < 2; ++q)
-        rv[u][q] = s < sb && orig[u] != 0 ? rows[(uint64_t)s * 2 + q] : make_uint4(0, 0, 0, 0);
-    }
-  }
   __syncthreads();
   bt_stamp(P, (uint64_t)bin * 8, 1);
 
@@ -786,57 +775,61 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
   const __amdgpu_buffer_rsrc_t rrec = rsrc(bin_rec, G * region * 16);
   const uint32_t half = lane >> 5, r0 = lane & 31u;
   const uint32_t pmax = bt_probe_max(log2sb);
-  uint32_t pfv = 0;
-  if constexpr (PF) {
-    const uint32_t *rw = reinterpret_cast<const uint32_t *>(bin_rec);
-    for (uint32_t g = tid >> 1; g < G; g += BLOCK / 2) {
-      const uint32_t nl = (rcnt[g] * 16 + 127) / 128;  // lines of the region's records
-      for (uint32_t l = tid & 1u; l < nl; l += 2) pfv |= rw[((uint64_t)g * region * 16 + l * 128) / 4];
-    }
-    const uint32_t row_lines = (sb * kRowBytes) / 128;
-    const uint32_t *rr = reinterpret_cast<const uint32_t *>(P.gcounts) + ((uint64_t)bin << log2sb) * (kRowBytes / 4);
-    for (uint32_t l = tid; l < row_lines; l += BLOCK) pfv |= rr[l * 32];
-  }
   uint32_t n_drop = 0;
   const ulonglong2 *lk2 = reinterpret_cast<const ulonglong2 *>(lkeys);
+  const uint32_t binhi = bin << (kBinShift - 32);
+  const uint32_t sh = 34 - log2sb;  // bt_seq: the top (log2sb - 2) bits
   // two records (ok: valid) through the LDS together
   auto agg_pair = [&](const ulonglong2 (&v)[2], const bool (&ok)[2]) {
-    uint64_t m[2];
-    BtSeq bq[2];
+    uint32_t mlo[2], mhi[2], b1[2], b2[2];
     ulonglong2 q[2][4];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      m[k] = ok[k] ? (((uint64_t)bin << kBinShift) | (v[k].x & kBinRest)) : 0ULL;
-      bq[k] = bt_seq(m[k], log2sb);
-      q[k][0] = lk2[bq[k].b1 * 2];
-      q[k][1] = lk2[bq[k].b1 * 2 + 1];
-      q[k][2] = lk2[bq[k].b2 * 2];
-      q[k][3] = lk2[bq[k].b2 * 2 + 1];
+      mlo[k] = (uint32_t)v[k].x;
+      mhi[k] = (((uint32_t)(v[k].x >> 32)) & ((1u << (kBinShift - 32)) - 1)) | binhi;
+      // bt_seq on the 32-bit halves
+      const uint32_t h1 = (mlo[k] ^ __builtin_amdgcn_alignbit(mhi[k], mlo[k], 29)) * 0x9E3779B1u;
+      const uint32_t h2 = (h1 ^ (h1 >> 16)) * 0x85EBCA6Bu;
+      b1[k] = h1 >> sh;
+      b2[k] = h2 >> sh;
+      if (MODE & 16) {  // ablation: no lookup reads (every key taken as slot 0 of its first bucket)
+        q[k][0] = make_ulonglong2(((uint64_t)mhi[k] << 32) | mlo[k], 0);
+        q[k][1] = q[k][2] = q[k][3] = make_ulonglong2(0, 0);
+        continue;
+      }
+      q[k][0] = lk2[b1[k] * 2];
+      q[k][1] = lk2[b1[k] * 2 + 1];
+      q[k][2] = lk2[b2[k] * 2];
+      q[k][3] = lk2[b2[k] * 2 + 1];
     }
-    uint32_t s[2];
+    // position in the two buckets (8: not there)
+    uint32_t s[2], j[2] = {8u, 8u};
+    uint64_t mm[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) mm[k] = ((uint64_t)mhi[k] << 32) | mlo[k];
+#pragma unroll
+    for (int i = 7; i >= 0; --i) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const unsigned long long w = (i & 1) ? q[k][i >> 1].y : q[k][i >> 1].x;
+        j[k] = w == mm[k] ? (uint32_t)i : j[k];
+      }
+    }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-      const uint64_t mm = m[k];
-      uint32_t f = kNotFound;
-      f = q[k][3].y == mm ? bq[k].b2 * 4 + 3 : f;
-      f = q[k][3].x == mm ? bq[k].b2 * 4 + 2 : f;
-      f = q[k][2].y == mm ? bq[k].b2 * 4 + 1 : f;
-      f = q[k][2].x == mm ? bq[k].b2 * 4 : f;
-      f = q[k][1].y == mm ? bq[k].b1 * 4 + 3 : f;
-      f = q[k][1].x == mm ? bq[k].b1 * 4 + 2 : f;
-      f = q[k][0].y == mm ? bq[k].b1 * 4 + 1 : f;
-      f = q[k][0].x == mm ? bq[k].b1 * 4 : f;
-      s[k] = ok[k] ? f : 0u;
+      const uint32_t sl = ((j[k] < 4 ? b1[k] : b2[k]) << 2) | (j[k] & 3u);
+      s[k] = j[k] < 8 ? sl : kNotFound;
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       if (__builtin_expect(ok[k] && s[k] == kNotFound, 0)) {  // probe / insert in the mirror
+        const BtSeq bq = bt_seq(mm[k], log2sb);
         uint32_t i = 0, sl = kNotFound;
         for (; i < pmax; ++i) {
-          sl = bt_pos(bq[k], i);
+          sl = bt_pos(bq, i);
           unsigned long long kk = lkeys[sl];
-          if (kk == 0) kk = atomicCAS(&lkeys[sl], 0ULL, (unsigned long long)m[k]);
-          if (kk == 0 || kk == m[k]) break;
+          if (kk == 0) kk = atomicCAS(&lkeys[sl], 0ULL, (unsigned long long)mm[k]);
+          if (kk == 0 || kk == mm[k]) break;
         }
         s[k] = i == pmax ? kNotFound - 1 : sl;  // kNotFound - 1: the bin's sub-table is full
       }
@@ -844,16 +837,23 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       if (!ok[k]) continue;
-      const bool err = (v[k].x >> 63) != 0;
-      const uint32_t ws = (uint32_t)(v[k].x >> kBinShift) & 1023u;
+      const uint32_t xhi = (uint32_t)(v[k].x >> 32);
+      const bool err = (int32_t)xhi < 0;
+      const uint32_t ws = (xhi >> (kBinShift - 32)) & 1023u;
       if (__builtin_expect(s[k] == kNotFound - 1, 0)) {  // dropped
         ++n_drop;
-        if (err) bt_cms_add(kernel_params(), ws, m[k] * P.kinv);
+        if (err) bt_cms_add(kernel_params(), ws, mm[k] * P.kinv);
         continue;
       }
-      const uint32_t h = s[k] * kPartMaxBk + (uint32_t)(v[k].y >> kRecDurBits);
-      atomicAdd(&lcnt[h >> 1], 1u << ((h & 1u) * 16));
-      atomicAdd(&lsum[s[k]], (unsigned long long)(v[k].y & kRecDurMask));
+      const uint32_t yhi = (uint32_t)(v[k].y >> 32);
+      uint32_t h;  // the (slot, bucket) u16 counter: s * 17 + bucket
+      asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(h) : "v"(s[k]), "i"(kPartMaxBk), "v"(yhi >> (kRecDurBits - 32)));
+      if (MODE & 32) {  // ablation: no counter atomics
+        n_drop += (h == 0xFFFFFFFu) ? 1u : 0u;
+      } else {
+        atomicAdd(&lcnt[h >> 1], 1u << ((h & 1u) << 4));
+        atomicAdd(&lsum[s[k]], ((unsigned long long)(yhi & ((1u << (kRecDurBits - 32)) - 1)) << 32) | (uint32_t)v[k].y);
+      }
       if (err) {
         const uint32_t ek = (ws << log2sb) | s[k];
         const uint32_t at = atomicAdd(&errl[0], 1u);
@@ -863,33 +863,36 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
     }
   };
   constexpr uint32_t kWaves = BLOCK / 64;
-  constexpr uint32_t B = NB;
-  static_assert(B % 2 == 0, "records go through the LDS in pairs");
   const uint32_t pairs = (G + 1) / 2;
   if (!(MODE & 1)) {
-    for (uint32_t p0 = wave; p0 < pairs; p0 += kWaves * B) {
-      ulonglong2 v[B];
-      uint32_t cnt[B];
+    // the wave's region pairs p = wave + 8 j; this lane's region g = 2 p +
+    // half, its byte offset stepped by 16 regions per pair.  Batches of two
+    // pairs, double-buffered (a batch past the bin's regions loads nothing
+    // and adds nothing).
+    const uint32_t g0 = 2 * wave + half;
+    const uint32_t rstep = 2 * kWaves * region * 16;
+    uint32_t roff = (g0 * region + r0) * 16;
+    uint32_t goff = g0;
+    auto issue = [&](ulonglong2 (&v)[2], bool (&ok)[2]) {
 #pragma unroll
-      for (uint32_t b = 0; b < B; ++b) {
-        const uint32_t p = p0 + b * kWaves, g = 2 * p + half;
-        const bool okp = p < pairs && g < G;
-        cnt[b] = rcnt[okp ? g : 0u];
-        cnt[b] = okp ? cnt[b] : 0u;
-      }
-#pragma unroll
-      for (uint32_t b = 0; b < B; ++b) {
-        const uint32_t g = 2 * (p0 + b * kWaves) + half;
-        const uint32_t off = r0 < cnt[b] ? (g * region + r0) * 16 : 0xFFFFFFF0u;
-        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)off, 0, 2);
+      for (uint32_t b = 0; b < 2; ++b) {
+        const uint32_t g = goff + b * 2 * kWaves;
+        const uint32_t c = rcnt[g < G ? g : 0u];
+        ok[b] = g < G && r0 < c;
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)(ok[b] ? roff + b * rstep : 0xFFFFFFF0u), 0, 2);
         v[b] = make_ulonglong2((uint64_t)x[0] | ((uint64_t)x[1] << 32), (uint64_t)x[2] | ((uint64_t)x[3] << 32));
       }
-#pragma unroll
-      for (uint32_t b = 0; b < B; b += 2) {
-        const ulonglong2 vv[2] = {v[b], v[b + 1]};
-        const bool ok[2] = {r0 < cnt[b], r0 < cnt[b + 1]};
-        agg_pair(vv, ok);
-      }
+      roff += 2 * rstep;
+      goff += 4 * kWaves;
+    };
+    ulonglong2 va[2], vb[2];
+    bool oka[2], okb[2];
+    issue(va, oka);
+    for (uint32_t p0 = wave; p0 < pairs; p0 += kWaves * 4) {
+      issue(vb, okb);
+      agg_pair(va, oka);
+      issue(va, oka);
+      agg_pair(vb, okb);
     }
     // regions longer than 32 records: the rest, one record per lane
 #pragma unroll 1
@@ -905,9 +908,6 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
   }
   n_drop = wave_sum(n_drop);
   if (lane == 0 && n_drop) atomicAdd(&misc[0], n_drop);
-  if constexpr (PF) {  // never true (P.n < 2^63): keeps the prefetch loads
-    if (pfv == 0x9E3779B9u && (P.n >> 63)) misc[1] = 1;
-  }
   __syncthreads();
   bt_stamp(P, (uint64_t)bin * 8, 2);
 
@@ -915,6 +915,8 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
   //    row read is issued before the first row is written); the ERROR list
   if (MODE & 2) return;
   const uint32_t nbk = P.nbk;
+  uint4 *rows = reinterpret_cast<uint4 *>(P.gcounts) + ((uint64_t)bin << log2sb) * (kRowBytes / 16);
+  uint4 rv[kMaxPer][2];
   bool touched[kMaxPer];
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
@@ -928,10 +930,8 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
       }
       touched[u] = any != 0;
     }
-    if constexpr (!EARLY) {
 #pragma unroll
-      for (uint32_t q = 0; q < 2; ++q) rv[u][q] = touched[u] ? rows[(uint64_t)s * 2 + q] : make_uint4(0, 0, 0, 0);
-    }
+    for (uint32_t q = 0; q < 2; ++q) rv[u][q] = touched[u] ? rows[(uint64_t)s * 2 + q] : make_uint4(0, 0, 0, 0);
   }
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
@@ -996,28 +996,24 @@ static const void *bt_scatter2_fn(uint32_t diag) {
 }
 
 constexpr uint32_t kDiagBtAggWide = 1u << 30, kDiagBtAggLoadOnly = 1u << 31;
+constexpr uint32_t kDiagBtAggNoLookup = 1u << 17, kDiagBtAggNoAtomics = 1u << 18;
 static const void *bt_agg2_fn(uint32_t diag);
-static int bt_agg_form() {  // SPANAGG_BT_AGG (A/B runs): 2 = the second-form aggregate;
-                            // 4/5/6 = the third form with NB 8 + early rows / NB 4 + early rows / NB 8
-  static const int f = [] {
+static bool bt_agg_v2() {  // SPANAGG_BT_AGG=2: the second-form aggregate (A/B runs)
+  static const bool v2 = [] {
     const char *v = std::getenv("SPANAGG_BT_AGG");
-    return v ? std::atoi(v) : 0;
+    return v && std::atoi(v) == 2;
   }();
-  return f;
+  return v2;
 }
-static bool bt_agg_v2() { return bt_agg_form() == 2; }
 static const void *bt_agg_fn(uint32_t diag) {
-  const int mode = ((diag & 1u) ? 1 : 0) | ((diag & kDiagBtAggNoRows) ? 2 : 0);
-  // (diag bits 17-19 pick a form per engine in A/B runs: 1 -> 4, 2 -> 5, 3 -> 6, 4 -> 7)
-  const int form = (diag >> 17) & 7u ? 3 + (int)((diag >> 17) & 7u) : bt_agg_form();
-  if (mode == 0 && !(diag & (kDiagBtAggWide | kDiagBtAggLoadOnly))) switch (form) {
-      case 4: return (const void *)&bt_aggregate3_kernel<0, 2, 512, 8, true>;
-      case 5: return (const void *)&bt_aggregate3_kernel<0, 2, 512, 4, true>;
-      case 6: return (const void *)&bt_aggregate3_kernel<0, 2, 512, 8, false>;
-      case 7: return (const void *)&bt_aggregate3_kernel<0, 2, 512, 4, false, true>;
-      default: break;
-    }
+  const int mode = ((diag & 1u) ? 1 : 0) | ((diag & kDiagBtAggNoRows) ? 2 : 0) |
+                   ((diag & kDiagBtAggNoLookup) ? 16 : 0) | ((diag & kDiagBtAggNoAtomics) ? 32 : 0);
   if (!bt_agg_v2() && !(diag & kDiagBtAggLoadOnly)) {
+    if (mode & 48) switch (mode) {  // ablations of the record loop
+        case 16: return (const void *)&bt_aggregate3_kernel<16, 2>;
+        case 32: return (const void *)&bt_aggregate3_kernel<32, 2>;
+        default: return (const void *)&bt_aggregate3_kernel<48, 2>;
+      }
     if (diag & kDiagBtAggWide) switch (mode) {  // bins of 2,048 slots
         case 1: return (const void *)&bt_aggregate3_kernel<1, 4>;
         case 2: return (const void *)&bt_aggregate3_kernel<2, 4>;
@@ -1056,12 +1052,10 @@ hipError_t prepare_ingest_bt(size_t agg_lds) {
                                            (int)kBt2ScatterLds);
         e != hipSuccess)
       return e;
-  for (uint32_t d : {0u, 1u, kDiagBtAggNoRows, 1u | kDiagBtAggNoRows})
+  for (uint32_t d : {0u, 1u, kDiagBtAggNoRows, 1u | kDiagBtAggNoRows, kDiagBtAggNoLookup, kDiagBtAggNoAtomics,
+                     kDiagBtAggNoLookup | kDiagBtAggNoAtomics})
     for (uint32_t v : {0u, kDiagBtAggWide, kDiagBtAggLoadOnly})
-      for (const void *fn : {bt_agg_fn(d | v), bt_agg2_fn(d | v), (const void *)&bt_aggregate3_kernel<0, 2, 512, 8, true>,
-                             (const void *)&bt_aggregate3_kernel<0, 2, 512, 4, true>,
-                             (const void *)&bt_aggregate3_kernel<0, 2, 512, 8, false>,
-                             (const void *)&bt_aggregate3_kernel<0, 2, 512, 4, false, true>})
+      for (const void *fn : {bt_agg_fn(d | v), bt_agg2_fn(d | v)})
         if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)agg_lds);
             e != hipSuccess)
           return e;

@@ -51,6 +51,14 @@ def main():
                       "records": q(agg[:, 2] - agg[:, 1]), "rows": q(agg[:, 3] - agg[:, 2]),
                       "life": q(agg[:, 3] - agg[:, 0]), "end": q(agg[:, 3] - t0)},
     }
+    # resident aggregate workgroups over time (sweep over start/end stamps):
+    # the peak is the occupancy the LDS / register budget really allows
+    ev = sorted([(int(a), 1) for a in agg[:, 0]] + [(int(z), -1) for z in agg[:, 3]])
+    cur = peak = 0
+    for _, d in ev:
+        cur += d
+        peak = max(peak, cur)
+    out["aggregate"]["peak_resident"] = peak
     print(json.dumps(out, indent=1))
 
 
