@@ -29,9 +29,10 @@ constexpr uint64_t kCmsSeed[8] = {0x9E3779B97F4A7C15ULL, 0xBF58476D1CE4E5B9ULL,
                                   0x8EBC6AF09C88C6E3ULL, 0x589965CC75374CC3ULL};
 constexpr size_t kLdsBudget = 144 * 1024;  // small-table path LDS ceiling per workgroup
 constexpr uint64_t kSlabLimit = 1ULL << 31;  // per-workgroup spans between slab reductions
-// small path: ingest_v2_kernel variant 16 (14 + key-table loads issued ahead
-// of every tile load); SPANAGG_VARIANT overrides
-constexpr int kDefaultVariant = 19;
+// small path: ingest_v2_kernel variant 20 (19 LEAN: the span hash on 32-bit
+// halves and the wave-level (slot, bucket) dedup of the hot series' counter
+// adds); SPANAGG_VARIANT overrides
+constexpr int kDefaultVariant = 20;
 constexpr uint32_t kMaxSlabSets = 4;      // per-workgroup slab sets (small path)
 constexpr uint32_t kDefaultSlabSets = 2;  // SPANAGG_SLAB_SETS overrides
 
