@@ -549,10 +549,16 @@ def main():
         if world == 1 and args.gpus > 1:
             print("run N>1 under torch.distributed.run (one process per GPU)", file=sys.stderr)
             return 2
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # SPANAGG_BENCH_ONE_DEVICE=1 rehearses the N-rank path on a one-GPU box:
+    # every rank on cuda:0, gloo collectives (never for a reported number)
+    one_dev = os.environ.get("SPANAGG_BENCH_ONE_DEVICE") == "1"
+    torch.cuda.set_device(0 if one_dev else local_rank)
+    device = torch.device("cuda", 0 if one_dev else local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if one_dev:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     def barrier():
         if world > 1:
@@ -618,6 +624,7 @@ def main():
                     "(trace_w1 % N == rank); every launch "
                     "a distinct trace-id variant of the rank's batch)",
             "config": {"workload": WORKLOADS[args.workload], "spans_per_step_per_gpu": n,
+                       **({"rehearsal": "all ranks on one device, gloo"} if one_dev else {}),
                        "global_spans_per_step": n * world,
                        "parallelism": f"trace-id shards x{world}, RCCL merge at flush"},
             "roofline": roofline(args.workload, n, main_r, args.traffic),

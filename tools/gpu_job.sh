@@ -6,6 +6,8 @@
 #   tests            every -m gpu test (pytest, per-test timeout)
 #   tests:<file>     one test file, e.g. tests:tests/test_gpu_binned.py
 #   bench            the default bench line (C2 + C4 sub-objects, CPU baselines)
+#   rehearse_<n>     bench.py's n-rank path (torch.distributed.run) with every
+#                    rank on this one GPU and gloo collectives (a rehearsal)
 #   bench_<wl>       a short bench of one workload (c2, c4, c4zipf), no baselines
 #   ablate_<wl>      tools/ablate.py over the ABL_FLAGS / ABL_ENVS variant set for <wl>
 #   stamps_<wl>      tools/bt_stamps.py: per-workgroup phase timeline (c4, c4zipf)
@@ -44,13 +46,16 @@ for step in "$@"; do
     tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     tests:*) f=${step#tests:}; run "tests_$(basename "$f" .py)" 600 python -u -m pytest "$f" -m gpu -x -v --timeout 300 --timeout-method thread ;;
     bench) run bench 500 python bench.py ;;
+    rehearse_*) n=${step#rehearse_}; SPANAGG_BENCH_ONE_DEVICE=1 run "rehearse_n$n" 400 python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus "$n" --steps 10 \
+        --warmup 2 --settle 4 --soak-s 0 ;;
     hostex_*) t=${step#hostex_}; run "hostex_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 --exemplars --events ;;
     host_*) t=${step#host_}; run "host_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 ;;
     bench_*) wl=${step#bench_}; run "bench_$wl" 300 python bench.py --workload "$wl" --sub "" --steps 20 $BQ ;;
     ablate_*) wl=${step#ablate_}; ABL_WORKLOAD=$wl ABL_VARS=${ABL_VARS:-} run "ablate_$wl" 400 python tools/ablate.py ;;
     trace_*) wl=${step#trace_}
       (cd /tmp && run "trace_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$wl" -o run \
-         -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 10 --warmup 2 --streams 1 --soak-s 0 $BQ) || exit $? ;;
+         -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 10 --warmup 2 --streams 1 --soak-s 0 --no-filter-off $BQ) || exit $? ;;
     pmc_*) rest=${step#pmc_}; wl=${rest%%_*}; set_=${rest#*_}
       case $set_ in
         fetch) ctr="FETCH_SIZE" ;;
