@@ -54,17 +54,50 @@ __host__ __device__ inline uint32_t shard_of(uint64_t w1, uint32_t n, uint32_t r
 
 constexpr uint32_t kMaxMembers = 64;
 
-// Spans per shard of a device batch (LDS counters, one global atomic per
-// shard per workgroup).
+// Spans per shard of a device batch: LDS counters per workgroup, written to
+// blk[workgroup][shard], plus one global atomic per shard per workgroup for
+// the totals the host reads.
 __global__ __launch_bounds__(256) void shard_count_kernel(const uint64_t *w1, uint64_t n, uint32_t nm, uint32_t r32,
-                                                           unsigned long long *cnt) {
+                                                           unsigned long long *cnt, uint32_t *blk) {
   __shared__ uint32_t c[kMaxMembers];
   if (threadIdx.x < kMaxMembers) c[threadIdx.x] = 0;
   __syncthreads();
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
     atomicAdd(&c[shard_of(w1[i], nm, r32)], 1u);
   __syncthreads();
-  if (threadIdx.x < nm && c[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], (unsigned long long)c[threadIdx.x]);
+  if (threadIdx.x < nm) {
+    blk[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = c[threadIdx.x];
+    if (c[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], (unsigned long long)c[threadIdx.x]);
+  }
+}
+
+// Exclusive scan of one shard's counts over the workgroups (one block per
+// shard, grid <= 4096: four workgroups per thread): blk[j][b] becomes
+// workgroup b's first position in shard j.
+__global__ __launch_bounds__(1024) void shard_scan_kernel(uint32_t *blk, uint32_t grid) {
+  __shared__ uint32_t part[1024];
+  uint32_t *row = blk + (uint64_t)blockIdx.x * grid;
+  const uint32_t t = threadIdx.x, b0 = 4 * t;
+  uint32_t v[4], sum = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[k] = b0 + k < grid ? row[b0 + k] : 0u;
+    sum += v[k];
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan of the thread sums
+    const uint32_t x = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t acc = part[t] - sum;  // exclusive
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (b0 + k < grid) row[b0 + k] = acc;
+    acc += v[k];
+  }
 }
 
 // One member's packed shard (SoA v1 columns) in the partition staging buffer.
@@ -76,13 +109,20 @@ struct ShardArgs {  // by value (kernel argument segment): nm <= kMaxMembers
   ShardCols c[kMaxMembers];
 };
 
-// Scatter: every wave takes 64 spans, and for each shard present among them
-// (a ballot) one lane reserves a run of the shard's positions (one global
-// atomic); the lanes of that shard write their span at consecutive positions.
-// Order inside a shard is not kept: every aggregate is order-independent
-// (integer sums and maxima).
+// Scatter: a workgroup takes the spans it counted (the same grid and stride
+// as shard_count_kernel), from its own first position in every shard (the
+// scanned counts).  Every wave takes 64 spans, and for each shard present
+// among them (a ballot) one lane reserves a run of the shard's positions from
+// the workgroup's LDS cursor; the lanes of that shard write their span at
+// consecutive positions.  (Reserving from one global cursor per shard put a
+// returning atomic on eight hot addresses per wave and took 15 ms per 10 M
+// spans.)  Order inside a shard is not kept: every aggregate is
+// order-independent (integer sums and maxima).
 __global__ __launch_bounds__(256) void shard_scatter_kernel(sa_span_batch in, uint32_t nm, uint32_t r32,
-                                                             ShardArgs out, unsigned long long *cursor) {
+                                                             ShardArgs out, const uint32_t *first) {
+  __shared__ uint32_t cursor[kMaxMembers];
+  if (threadIdx.x < nm) cursor[threadIdx.x] = first[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t n = in.n;
   for (uint64_t i0 = blockIdx.x * 256ull + (threadIdx.x & ~63u); i0 < n; i0 += (uint64_t)gridDim.x * 256) {
@@ -98,12 +138,11 @@ __global__ __launch_bounds__(256) void shard_scatter_kernel(sa_span_batch in, ui
       const uint64_t mj = __ballot(sh == j);
       pending &= ~mj;
       const int leader = __builtin_ctzll(mj);
-      unsigned long long base = 0;
-      if ((int)lane == leader) base = atomicAdd(&cursor[j], (unsigned long long)__popcll(mj));
-      const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, leader);
-      const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(base >> 32), leader);
+      uint32_t base = 0;
+      if ((int)lane == leader) base = atomicAdd(&cursor[j], (uint32_t)__popcll(mj));
+      const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
       if (sh == j) {
-        const uint64_t pos = (((uint64_t)bhi << 32) | blo) +
+        const uint64_t pos = (uint64_t)b0 +
                              __builtin_amdgcn_mbcnt_hi((uint32_t)(mj >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mj, 0u));
         const ShardCols &c = out.c[j];
         c.k[pos] = k;
@@ -483,10 +522,15 @@ int sa_group_ingest_device(sa_group *g, const sa_span_batch *b, uint32_t src, vo
   for (uint32_t i = 0; i < n; ++i)
     if (g->done_used[k][i]) SG_HIP(g, hipStreamWaitEvent(s, g->ev_done[k][i], 0));
   // 1. shard sizes
-  if (int rc = ensure(g, sdev, g->pcnt[src], 2 * kMaxMembers * 8)) return rc;
-  unsigned long long *dcnt = static_cast<unsigned long long *>(g->pcnt[src].p), *dcur = dcnt + kMaxMembers;
-  SG_HIP(g, hipMemsetAsync(dcnt, 0, 2 * kMaxMembers * 8, s));
-  hipLaunchKernelGGL(shard_count_kernel, dim3(grid_for(b->n)), dim3(256), 0, s, b->trace_w1, b->n, n, r32, dcnt);
+  const uint32_t pgrid = grid_for(b->n);
+  if (int rc = ensure(g, sdev, g->pcnt[src], kMaxMembers * 8 + (size_t)4096 * kMaxMembers * 4)) return rc;
+  unsigned long long *dcnt = static_cast<unsigned long long *>(g->pcnt[src].p);
+  uint32_t *dblk = reinterpret_cast<uint32_t *>(dcnt + kMaxMembers);  // [n][pgrid] counts -> first positions
+  if (b->n > 0xFFFFFFFFull) return gfail(g, SA_EINVAL, "device batch above 2^32 spans (u32 shard positions)");
+  SG_HIP(g, hipMemsetAsync(dcnt, 0, kMaxMembers * 8, s));
+  hipLaunchKernelGGL(shard_count_kernel, dim3(pgrid), dim3(256), 0, s, b->trace_w1, b->n, n, r32, dcnt, dblk);
+  SG_HIP(g, hipGetLastError());
+  hipLaunchKernelGGL(shard_scan_kernel, dim3(n), dim3(1024), 0, s, dblk, pgrid);
   SG_HIP(g, hipGetLastError());
   SG_HIP(g, hipMemcpyAsync(g->hcnt, dcnt, n * 8, hipMemcpyDeviceToHost, s));
   SG_HIP(g, hipStreamSynchronize(s));
@@ -508,7 +552,7 @@ int sa_group_ingest_device(sa_group *g, const sa_span_batch *b, uint32_t src, vo
     args.c[i] = ShardCols{c, c + cap[i], c + 2 * cap[i], c + 3 * cap[i], c + 4 * cap[i],
                           reinterpret_cast<uint32_t *>(c + 5 * cap[i])};
   }
-  hipLaunchKernelGGL(shard_scatter_kernel, dim3(grid_for(b->n)), dim3(256), 0, s, *b, n, r32, args, dcur);
+  hipLaunchKernelGGL(shard_scatter_kernel, dim3(pgrid), dim3(256), 0, s, *b, n, r32, args, dblk);
   SG_HIP(g, hipGetLastError());
   SG_HIP(g, hipEventRecord(g->ev_scat[k][src], s));
   // 3. every member ingests its shard on its own stream (peer copy first when
