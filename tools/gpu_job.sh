@@ -13,6 +13,9 @@
 #   stamps_<wl>      tools/bt_stamps.py: per-workgroup phase timeline (c4, c4zipf)
 #   sweep            C2 kernel time vs batch size (SIZES="1000000 5000000 ...")
 #   trace_<wl>       rocprofv3 --kernel-trace --stats of a short bench of <wl>
+#   ptrace_<wl>      the same over a long timed region (PSTEPS, default 400 steps,
+#                    one stream: overlapping launches would stretch each other's
+#                    traced durations); the bench line is the last line of the log
 #   pmc_<wl>_<set>   one rocprofv3 --pmc pass (set: fetch, write, lds, sq) over
 #                    tools/prof_driver.py for <wl>
 # Outputs go to gpurun_out/$TAG/.  Any failing step ends the job (exit code
@@ -53,6 +56,11 @@ for step in "$@"; do
     host_*) t=${step#host_}; run "host_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 ;;
     bench_*) wl=${step#bench_}; run "bench_$wl" 300 python bench.py --workload "$wl" --sub "" --steps 20 $BQ ;;
     ablate_*) wl=${step#ablate_}; ABL_WORKLOAD=$wl ABL_VARS=${ABL_VARS:-} run "ablate_$wl" 400 python tools/ablate.py ;;
+    ptrace_*) wl=${step#ptrace_}  # the rocprofv3 summary the bench line's kernel_ms is checked against:
+      # a long timed region so the cold and settling launches weigh little in the average
+      (cd /tmp && run "ptrace_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ptrace_$wl" -o run \
+         -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps ${PSTEPS:-400} --streams 1 --soak-s 0 \
+         --no-filter-off $BQ) || exit $? ;;
     trace_*) wl=${step#trace_}
       (cd /tmp && run "trace_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$wl" -o run \
          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 10 --warmup 2 --streams 1 --soak-s 0 --no-filter-off $BQ) || exit $? ;;
