@@ -544,7 +544,7 @@ template <int S, int NBUF, int AUX, bool DIAG, int LC = 0, int NWC = 0, int PC =
           bool DYN = false, int OPT = 0, bool EPI = false, bool LEAN = false, bool EXPO = false>
 __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 0] = __builtin_amdgcn_s_memrealtime();
+  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t log2cap = LC ? (uint32_t)LC : P.log2cap;
   const uint32_t cap = 1u << log2cap;
   const uint32_t nw = EXPO ? 6u : NWC ? (uint32_t)NWC : (P.nbk + 1) >> 1;
@@ -655,7 +655,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   etab[threadIdx.x] = 0;  // kErrTab == kLdsBlock
   if (lb_on && threadIdx.x * 4 < P.lb_n) reinterpret_cast<uint32_t *>(llb)[threadIdx.x] = lbw;
   __syncthreads();
-  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 1] = __builtin_amdgcn_s_memrealtime();
+  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 1] = __builtin_amdgcn_s_memrealtime();
 
   // diagnostic build: per-wave cycle sums of the step's segments (s_memtime;
   // the stamp's lgkmcnt(0) serialises LDS, so read shares, not lengths)
@@ -978,8 +978,8 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     n_filt = wave_sum(n_filt);
     if ((threadIdx.x & 63) == 0 && n_filt) atomicAdd(&hq_n[2], n_filt);
   }
-  const uint64_t wave_loop_end = DIAG && P.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 2] = __builtin_amdgcn_s_memrealtime();
+  const uint64_t wave_loop_end = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 2] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
   const uint32_t nq = *hq_n < kHllQueue ? *hq_n : kHllQueue;
   if constexpr (EXPO) {
@@ -1015,9 +1015,9 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     for (uint32_t i = threadIdx.x; i < nq; i += kLdsBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
     hll_lb_refresh(P, threadIdx.x >> 6, kWaves);
   }
-  if (DIAG && P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 3] = __builtin_amdgcn_s_memrealtime();
-  if (DIAG && P.dbg && (threadIdx.x & 63) == 0) {
-    for (int i = 0; i < 6; ++i) P.dbg[blockIdx.x * kDbgPerWg + 8 + (threadIdx.x >> 6) * 8 + i] = seg[i];
+  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 3] = __builtin_amdgcn_s_memrealtime();
+  if (P.dbg && (threadIdx.x & 63) == 0) {
+    for (int i = 0; i < 6 && DIAG; ++i) P.dbg[blockIdx.x * kDbgPerWg + 8 + (threadIdx.x >> 6) * 8 + i] = seg[i];
     P.dbg[blockIdx.x * kDbgPerWg + 8 + (threadIdx.x >> 6) * 8 + 6] = wave_loop_end;
   }
   if constexpr (EPI) {  // (lstat is final: the epilogue follows a workgroup barrier)
@@ -1718,7 +1718,9 @@ hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_
     variant = variant == 12 ? 8 : variant == 13 ? 11 : 15;
   // the lean window quotient needs window_ns < 2^56 (its high word is a 24-bit multiplier)
   if (variant == 20 && (P.window_ns >> 56)) variant = 19;
-  const void *fn = small_fn(P.bintab != nullptr, variant, P.diag != 0 || P.dbg != nullptr);
+  // (SPANAGG_STAMPS engines keep the production v2 kernels: their workgroup
+  // and wave-end stamps are written whenever P.dbg is set)
+  const void *fn = small_fn(P.bintab != nullptr, variant, P.diag != 0 || (P.dbg != nullptr && variant < 8));
   void *args[] = {const_cast<IngestParams *>(&P)};
   return hipLaunchKernel(fn, dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);
 }

@@ -49,7 +49,8 @@ def main():
             for c in wl.batch.columns()]
     s = torch.cuda.Stream(dev)
     out = {}
-    for name, fl in (("full", 0), ("loads_only", 15), ("no_sketch", 6)):
+    for name, fl in [x for x in (("full", 0), ("loads_only", 15), ("no_sketch", 6))
+                     if x[0] in os.environ.get("STAMP_SETS", "full,loads_only,no_sketch").split(",")]:
         for v in [int(x) for x in os.environ.get("STAMP_VARS", "0,8").split(",")]:
             os.environ["SPANAGG_VARIANT"] = str(v)
             with Engine(Config(n_services=wl.n_services, n_windows=16, flags=fl)) as e:
