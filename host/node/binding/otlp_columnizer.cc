@@ -618,14 +618,14 @@ SigCache::Entry *SigCache::find(uint64_t h, uint64_t rhash, uint32_t svc, std::s
 }
 
 void SigCache::insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
-                      int32_t code, uint64_t sid) {
+                      int32_t code, uint64_t sid, const std::string &key) {
   if (2 * (n_ + 1) > t_.size()) {  // load <= 1/2
     std::vector<Entry> old;
     old.swap(t_);
     t_.resize(old.empty() ? 256 : old.size() * 2);
     n_ = 0;
     for (Entry &e : old)
-      if (e.used) insert(e.h, e.rhash, e.svc, e.name, e.kind, e.code, e.sid);
+      if (e.used) insert(e.h, e.rhash, e.svc, e.name, e.kind, e.code, e.sid, e.key);
   }
   const size_t mask = t_.size() - 1;
   size_t i = h & mask;
@@ -633,6 +633,7 @@ void SigCache::insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view
   Entry &e = t_[i];
   e.h = h, e.rhash = rhash, e.sid = sid, e.svc = svc, e.kind = kind, e.code = code, e.used = true, e.ex_full = 0;
   e.name.assign(name);
+  e.key = key;
   ++n_;
 }
 
@@ -709,6 +710,7 @@ namespace {
 // the connector's internal keys (connector.js OVERFLOW_KEY, EVENT_KEY_PREFIX)
 const std::string kOverflowKey = std::string("\x01") + "otel.metric.overflow";
 const std::string kEventKeyPrefix = std::string(1, '\x02') + "events" + std::string(1, '\0');
+const std::string kNoKey;
 bool span_key(const std::string &k) { return k.empty() || (k[0] != '\x01' && k[0] != '\x02'); }
 }  // namespace
 
@@ -988,8 +990,9 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
         };
         if (hit) {
           sid = hit->sid;
-          if (opt_.events && !w.evs.empty()) {
-            if (const int why = build_key()) return key_fail(why);
+          if (opt_.events && !w.evs.empty()) {  // the event keys extend the span key: kept in the entry
+            if (!hit->key.empty()) keystr = hit->key;
+            else if (const int why = build_key()) return key_fail(why);
           }
         } else {
           if (const int why = build_key()) return key_fail(why);
@@ -1018,7 +1021,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
             }
           }
           // (an overflowed key is decided again each time: the count it met may change)
-          if (use_cache && !overflow) cache.insert(sig, rhash, svc_id, name, kind, code, sid);
+          if (use_cache && !overflow) cache.insert(sig, rhash, svc_id, name, kind, code, sid, opt_.events ? keystr : kNoKey);
         }
         // candidates; accept_exemplars keeps the interval's first ones.  A
         // series seen full this interval is marked in its signature-cache

@@ -164,8 +164,10 @@ class SigCache {
   static uint64_t hash(uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code);
   struct Entry;
   Entry *find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code);
+  // key: the span's key string, kept for events.enabled (its spans' event
+  // keys extend it), empty otherwise
   void insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code,
-              uint64_t sid);
+              uint64_t sid, const std::string &key);
   void clear() { t_.clear(), n_ = 0; }
   uint64_t gen = 0;  // the dictionary generation the entries belong to
 
@@ -176,6 +178,7 @@ class SigCache {
     int32_t kind = 0, code = 0;
     bool used = false;
     std::string name;
+    std::string key;  // events.enabled: the span key string (see insert)
   };
 
  private:
