@@ -572,7 +572,7 @@ class SpanMetricsConnector {
     if (r.eventRecords) this.eventRecords += r.eventRecords;
     for (const ex of r.exemplars || NONE) {  // exemplars.enabled: the native side's candidates, in order
       const sid = remapped && remapped.has(ex.sid) ? remapped.get(ex.sid) : ex.sid;
-      if (this.series.has(sid)) this._exemplar(sid, otlp.decodeSpan(new otlp.Reader(bytes, ex.off, ex.off + ex.len)));
+      if (this.series.has(sid)) this._exemplar(sid, otlp.decodeSpanExemplar(new otlp.Reader(bytes, ex.off, ex.off + ex.len)));
     }
     return true;
   }

@@ -201,6 +201,22 @@ function decodeSpan(r) {
   return s;
 }
 
+/** The fields of a Span an exemplar keeps (trace id, span id, start and end
+ * times); every other field is skipped undecoded. */
+function decodeSpanExemplar(r) {
+  const s = { traceId: new Uint8Array(16), spanId: new Uint8Array(8), startTimeUnixNano: 0n, endTimeUnixNano: 0n };
+  r.fields((f, wt) => {
+    switch (f) {
+      case 1: if (wt !== WT_LEN) return false; s.traceId = Uint8Array.from(r.bytes()); return true;
+      case 2: if (wt !== WT_LEN) return false; s.spanId = Uint8Array.from(r.bytes()); return true;
+      case 7: if (wt !== WT_I64) return false; s.startTimeUnixNano = r.fixed64(); return true;
+      case 8: if (wt !== WT_I64) return false; s.endTimeUnixNano = r.fixed64(); return true;
+      default: return false;
+    }
+  });
+  return s;
+}
+
 function decodeResource(r) {
   const res = { attributes: [] };
   r.fields((f, wt) => {
@@ -637,6 +653,6 @@ function decodeMetrics(buf) {
   return req;
 }
 
-module.exports = { Reader, Writer, decodeAnyValue, decodeKeyValue, decodeSpan, decodeResource, decodeTraces,
+module.exports = { Reader, Writer, decodeAnyValue, decodeKeyValue, decodeSpan, decodeSpanExemplar, decodeResource, decodeTraces,
   encodeAnyValue, encodeKeyValue, encodeSpan, encodeTraces, encodeMetrics, decodeMetrics,
   AGGREGATION_TEMPORALITY };
