@@ -143,36 +143,53 @@ __global__ __launch_bounds__(256) void expo_pass1_kernel(ExpoParams E) {
 }
 
 // per series: fix the scale for every positive value seen so far; merge the
-// kept buckets down when it drops
-__device__ __forceinline__ void rescale_slot(const ExpoParams &E, uint64_t s) {
-  {
-    ExpoHdr &h = E.hdr[s];
-    if (h.maxpos_ns == 0) return;  // no positive value
-    const double vlo = expo_value(h.minpos_ns, E.div), vhi = expo_value(h.maxpos_ns, E.div);
-    int32_t lo = expo_index(vlo, kExpoMaxScale), hi = expo_index(vhi, kExpoMaxScale), change = 0;
-    while (hi - lo >= (int32_t)E.max_size) {  // changeScale
-      hi >>= 1;
-      lo >>= 1;
-      ++change;
+// kept buckets down when it drops.  h is the series header in registers (the
+// caller stores it back).  At a positive target scale the indices of the
+// smallest and largest positive value are their scale-20 indices shifted
+// right: Go's index is floor(Log(v) * Ldexp(Log2E, s)), and the product with
+// an exact power of two rounds the same at every scale, so the scale-s value
+// is the scale-20 value times 2^(s-20) exactly, and floor(y / 2^k) =
+// floor(y) >> k (the max-index clamp and the power-of-two case shift the same
+// way).  Scales <= 0 take Go's exponent formula instead.
+__device__ __forceinline__ void rescale_hdr(const ExpoParams &E, uint64_t s, ExpoHdr &h) {
+  if (h.maxpos_ns == 0) return;  // no positive value
+  const double vlo = expo_value(h.minpos_ns, E.div), vhi = expo_value(h.maxpos_ns, E.div);
+  const int32_t lo20 = expo_index(vlo, kExpoMaxScale), hi20 = expo_index(vhi, kExpoMaxScale);
+  int32_t lo = lo20, hi = hi20, change = 0;
+  while (hi - lo >= (int32_t)E.max_size) {  // changeScale
+    hi >>= 1;
+    lo >>= 1;
+    ++change;
+  }
+  int32_t target = kExpoMaxScale - change;
+  if (target < kExpoMinScale) target = kExpoMinScale;
+  if (h.lo != kExpoEmpty && h.scale < target) target = h.scale;  // scales only go down
+  if (h.lo != kExpoEmpty && target < h.scale) {
+    const uint32_t diff = (uint32_t)(h.scale - target), M = E.max_size;
+    uint32_t *src = E.buckets + ((uint64_t)h.cur * E.cap + s) * M;
+    uint32_t *dst = E.buckets + ((uint64_t)(h.cur ^ 1u) * E.cap + s) * M;
+    for (int32_t i = h.lo; i <= h.hi; ++i) {
+      const uint32_t c = src[expo_mod(i, M)];
+      if (c) dst[expo_mod(i >> diff, M)] += c;
+      src[expo_mod(i, M)] = 0;
     }
-    int32_t target = kExpoMaxScale - change;
-    if (target < kExpoMinScale) target = kExpoMinScale;
-    if (h.lo != kExpoEmpty && h.scale < target) target = h.scale;  // scales only go down
-    if (h.lo != kExpoEmpty && target < h.scale) {
-      const uint32_t diff = (uint32_t)(h.scale - target), M = E.max_size;
-      uint32_t *src = E.buckets + ((uint64_t)h.cur * E.cap + s) * M;
-      uint32_t *dst = E.buckets + ((uint64_t)(h.cur ^ 1u) * E.cap + s) * M;
-      for (int32_t i = h.lo; i <= h.hi; ++i) {
-        const uint32_t c = src[expo_mod(i, M)];
-        if (c) dst[expo_mod(i >> diff, M)] += c;
-        src[expo_mod(i, M)] = 0;
-      }
-      h.cur ^= 1u;
-    }
-    h.scale = target;
+    h.cur ^= 1u;
+  }
+  h.scale = target;
+  if (target > 0) {
+    h.lo = lo20 >> (kExpoMaxScale - target);
+    h.hi = hi20 >> (kExpoMaxScale - target);
+  } else {
     h.lo = expo_index(vlo, target);
     h.hi = expo_index(vhi, target);
   }
+}
+
+__device__ __forceinline__ void rescale_slot(const ExpoParams &E, uint64_t s) {
+  ExpoHdr h = E.hdr[s];
+  if (h.maxpos_ns == 0) return;
+  rescale_hdr(E, s, h);
+  E.hdr[s] = h;
 }
 
 // (one thread per slot)
@@ -182,57 +199,86 @@ __global__ __launch_bounds__(256) void expo_rescale_kernel(ExpoParams E) {
 }
 
 // Small-table engines: the ingest kernel (EXPO mode) leaves per-workgroup
-// header partials in slabs [xG][cap].  One block per kXrSlots slots (32 by
-// default): 1,024 / kXrSlots groups sum a strided share of the workgroups'
-// partials (coalesced runs, zeroing what they consumed), LDS combines the
-// groups, then one thread per slot folds the sum into the series header and
-// rescales it.
+// header partials in slabs [xG][cap].  One block per kXrSlots slots (8 by
+// default, 256 blocks at C2's 2,048 slots): the block's 1,024 / kXrSlots
+// groups sum a strided share of the workgroups' partials (coalesced runs,
+// zeroing what they consumed), the lanes of a wave holding the same slot
+// combine by shuffles and the 16 waves through LDS, then one thread per slot
+// folds the sum into the series header and rescales it.  A thread issues all
+// its partial reads (kXrBatch at a time) and the owner its header read before
+// any is used: a loop with the zeroing store in it kept one round trip per
+// partial in a row, and a 64-block grid left three quarters of the CUs idle.
+constexpr uint32_t kXrBatch = 8;
+__device__ __forceinline__ void xhdr_add(XHdr &acc, const XHdr &x) {
+  acc.cnt += x.cnt;
+  acc.zero += x.zero;
+  acc.sum += x.sum;
+  acc.minx = x.minx > acc.minx ? x.minx : acc.minx;
+  acc.max = x.max > acc.max ? x.max : acc.max;
+}
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int o) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o, 64);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o, 64);
+  return ((unsigned long long)hi << 32) | lo;
+}
 template <uint32_t kXrSlots>
 __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E) {
+  static_assert(kXrSlots >= 1 && kXrSlots <= 64 && (kXrSlots & (kXrSlots - 1)) == 0, "slots per block");
   constexpr uint32_t kXrGroups = 1024 / kXrSlots;
-  __shared__ XHdr part[kXrGroups][kXrSlots];
+  __shared__ XHdr part[16][kXrSlots];
   const uint32_t sl = threadIdx.x % kXrSlots, gg = threadIdx.x / kXrSlots;
   const uint64_t s = blockIdx.x * (uint64_t)kXrSlots + sl;
+  const bool owner = gg == 0 && s < E.cap;
+  ExpoHdr h{};
+  if (owner) h = E.hdr[s];
   XHdr acc{0, 0, 0, 0, 0};
   if (s < E.cap) {
-    for (uint32_t g = gg; g < E.xG; g += kXrGroups) {
-      XHdr *p = E.xslab + (uint64_t)g * E.cap + s;
-      const XHdr x = *p;
-      if (x.cnt) {
-        acc.cnt += x.cnt;
-        acc.zero += x.zero;
-        acc.sum += x.sum;
-        acc.minx = x.minx > acc.minx ? x.minx : acc.minx;
-        acc.max = x.max > acc.max ? x.max : acc.max;
-        *p = XHdr{0, 0, 0, 0, 0};
+    for (uint32_t g0 = gg; g0 < E.xG; g0 += kXrBatch * kXrGroups) {
+      XHdr x[kXrBatch];
+#pragma unroll
+      for (uint32_t u = 0; u < kXrBatch; ++u) {
+        const uint32_t g = g0 + u * kXrGroups;
+        x[u] = g < E.xG ? E.xslab[(uint64_t)g * E.cap + s] : XHdr{0, 0, 0, 0, 0};
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kXrBatch; ++u) {
+        if (x[u].cnt) {
+          xhdr_add(acc, x[u]);
+          E.xslab[(uint64_t)(g0 + u * kXrGroups) * E.cap + s] = XHdr{0, 0, 0, 0, 0};
+        }
       }
     }
   }
-  part[gg][sl] = acc;
+  // lanes l, l ^ kXrSlots, ... of a wave hold the same slot
+#pragma unroll
+  for (int o = kXrSlots; o < 64; o <<= 1) {
+    XHdr y;
+    y.cnt = (uint32_t)__shfl_xor((int)acc.cnt, o, 64);
+    y.zero = (uint32_t)__shfl_xor((int)acc.zero, o, 64);
+    y.sum = shfl_xor_u64(acc.sum, o);
+    y.minx = shfl_xor_u64(acc.minx, o);
+    y.max = shfl_xor_u64(acc.max, o);
+    xhdr_add(acc, y);
+  }
+  if ((threadIdx.x & 63u) < kXrSlots) part[threadIdx.x >> 6][sl] = acc;
   __syncthreads();
-  if (gg != 0 || s >= E.cap) return;
-  for (uint32_t k = 1; k < kXrGroups; ++k) {
-    const XHdr x = part[k][sl];
-    acc.cnt += x.cnt;
-    acc.zero += x.zero;
-    acc.sum += x.sum;
-    acc.minx = x.minx > acc.minx ? x.minx : acc.minx;
-    acc.max = x.max > acc.max ? x.max : acc.max;
-  }
+  if (!owner) return;
+  acc = part[0][sl];
+#pragma unroll
+  for (uint32_t k = 1; k < 16; ++k) xhdr_add(acc, part[k][sl]);
   if (E.lcount) E.lcount[s] = acc.cnt - acc.zero;  // this launch's positive durations (expo_select_kernel)
-  if (acc.cnt) {
-    ExpoHdr &h = E.hdr[s];
-    const unsigned long long minpos = ~acc.minx;  // UINT64_MAX when no positive duration
-    const unsigned long long mn = acc.zero ? 0ULL : minpos;
-    h.count += acc.cnt;
-    h.zero += acc.zero;
-    h.sum_ns += acc.sum;
-    h.min_ns = mn < h.min_ns ? mn : h.min_ns;
-    h.max_ns = acc.max > h.max_ns ? acc.max : h.max_ns;
-    h.minpos_ns = minpos < h.minpos_ns ? minpos : h.minpos_ns;
-    h.maxpos_ns = acc.max > h.maxpos_ns ? acc.max : h.maxpos_ns;
-  }
-  rescale_slot(E, s);
+  if (!acc.cnt) return;  // no new values: the header (scale, range) stays as it is
+  const unsigned long long minpos = ~acc.minx;  // UINT64_MAX when no positive duration
+  const unsigned long long mn = acc.zero ? 0ULL : minpos;
+  h.count += acc.cnt;
+  h.zero += acc.zero;
+  h.sum_ns += acc.sum;
+  h.min_ns = mn < h.min_ns ? mn : h.min_ns;
+  h.max_ns = acc.max > h.max_ns ? acc.max : h.max_ns;
+  h.minpos_ns = minpos < h.minpos_ns ? minpos : h.minpos_ns;
+  h.maxpos_ns = acc.max > h.maxpos_ns ? acc.max : h.maxpos_ns;
+  rescale_hdr(E, s, h);
+  E.hdr[s] = h;
 }
 
 constexpr uint32_t kXcBlock = 1024;
@@ -524,16 +570,16 @@ hipError_t prepare_expo_count(size_t lds_bytes) {
                              (int)lds_bytes);
 }
 
-// slots per reduce block (SPANAGG_XR: 16 / 32 / 64, A/B runs; rocprofv3 medians at
-// C2's table: 38.5 / 21.1 / 29.4 us)
+// slots per reduce block (SPANAGG_XR: 8 / 16 / 32 / 64, A/B runs)
 void launch_reduce_rescale(const ExpoParams &E, hipStream_t s) {
   static const uint32_t xr = [] {
     const char *v = std::getenv("SPANAGG_XR");
-    const uint32_t x = v ? (uint32_t)std::atoi(v) : 32u;
-    return x == 16 || x == 64 ? x : 32u;
+    const uint32_t x = v ? (uint32_t)std::atoi(v) : 8u;
+    return x == 16 || x == 32 || x == 64 ? x : 8u;
   }();
   const dim3 g((uint32_t)((E.cap + xr - 1) / xr));
-  if (xr == 16) hipLaunchKernelGGL(expo_reduce_rescale_kernel<16>, g, dim3(1024), 0, s, E);
+  if (xr == 8) hipLaunchKernelGGL(expo_reduce_rescale_kernel<8>, g, dim3(1024), 0, s, E);
+  else if (xr == 16) hipLaunchKernelGGL(expo_reduce_rescale_kernel<16>, g, dim3(1024), 0, s, E);
   else if (xr == 32) hipLaunchKernelGGL(expo_reduce_rescale_kernel<32>, g, dim3(1024), 0, s, E);
   else hipLaunchKernelGGL(expo_reduce_rescale_kernel<64>, g, dim3(1024), 0, s, E);
 }

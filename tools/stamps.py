@@ -38,7 +38,12 @@ def timeline(e):
             "seg_share": [round(x / max(segs.sum(), 1), 3) for x in segs],
             "wave_loop_end": q(wend.reshape(-1)),
             "wave_skew_in_wg": q(wend.max(axis=1) - wend.min(axis=1)),
-            "loop_end_by_wave_med": [round(us(float(np.median(wend[:, i]))), 1) for i in range(16)]}
+            "loop_end_by_wave_med": [round(us(float(np.median(wend[:, i]))), 1) for i in range(16)],
+            # workgroup i runs on XCD i % 8 (round-robin dispatch): is the end spread per XCD?
+            "end_by_xcd": [q((t[:, 3] - t0)[np.nonzero(keep)[0] % 8 == x]) for x in range(8)],
+            # the launch if every workgroup ended at the mean end / its waves at their mean
+            "end_mean": float(us((t[:, 3] - t0).mean())),
+            "wave_end_mean_minus_max": q(wend.mean(axis=1) - wend.max(axis=1))}
 
 
 def main():
@@ -55,8 +60,11 @@ def main():
             os.environ["SPANAGG_VARIANT"] = str(v)
             with Engine(Config(n_services=wl.n_services, n_windows=16, flags=fl)) as e:
                 e.window_advance(wl.first_window)
-                for _ in range(3):
-                    e.ingest_device(*cols, n=n, stream=s.cuda_stream)
+                for i in range(int(os.environ.get("STAMP_LAUNCHES", "24"))):
+                    # a fresh trace-id variant per launch (as bench.py), so HLL raises do not idle
+                    c = list(cols)
+                    c[3] = cols[3] ^ (0x5DEECE66D * (i + 1))
+                    e.ingest_device(*c, n=n, stream=s.cuda_stream)
                 torch.cuda.synchronize()
                 out[f"{name}/v{v}"] = timeline(e)
     print(json.dumps(out, indent=1))
