@@ -143,9 +143,8 @@ struct ExpoParams {
   unsigned long long *dropped;
   XHdr *xslab;        // small-table engines: [xG][cap] per-workgroup header partials (nullptr: pass 1 atomics)
   uint32_t xG;
-  // small-table bucket counting (expo_select / expo_count_slab / expo_fold_slab):
-  uint32_t *lcount;         // [cap] this launch's positive durations per slot (reduce -> select)
-  int32_t *entry_of;        // [cap] the slot's LDS entry in the counting kernel, -1: HBM atomics
+  // small-table bucket counting (expo_count_slab with its entry selection / expo_fold_slab):
+  uint32_t *lcount;         // [cap] this launch's positive durations per slot (reduce -> selection)
   uint32_t *slot_of_entry;  // [xc_ne] the entry's slot, ~0u: unused
   uint32_t *xcslab;         // [xG][xc_ne][(max_size + 1) / 2] per-workgroup u16 bucket-count pairs
   uint32_t xc_ne;           // LDS entries of the counting kernel (0: the cached-probe kernel)

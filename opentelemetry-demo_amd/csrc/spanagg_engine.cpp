@@ -96,7 +96,6 @@ struct sa_engine {
   // slab bucket counting of small expo tables (spanagg_expo.hip expo_count_slab_kernel)
   uint32_t xc_ne = 0;
   uint32_t *xc_lcount = nullptr, *xc_slot_of_entry = nullptr, *xcslab = nullptr;
-  int32_t *xc_entry_of = nullptr;
   sa::ExpoHdr *expo_hdr = nullptr;
   uint32_t *expo_buckets = nullptr, *expo_slot = nullptr;
   uint64_t expo_slot_cap = 0;
@@ -446,7 +445,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     if (e->expo_small) {
       if ((rc = alloc((void **)&e->xslab, (size_t)e->G * e->cap * sizeof(sa::XHdr)))) return bail(rc);
       if (e->xc_ne &&
-          ((rc = alloc((void **)&e->xc_lcount, e->cap * 4)) || (rc = alloc((void **)&e->xc_entry_of, e->cap * 4)) ||
+          ((rc = alloc((void **)&e->xc_lcount, e->cap * 4)) ||
            (rc = alloc((void **)&e->xc_slot_of_entry, (size_t)e->xc_ne * 4)) ||
            (rc = alloc((void **)&e->xcslab, (size_t)e->G * e->xc_ne * ((cfg->exp_max_size + 1) / 2) * 4))))
         return bail(rc);
@@ -523,7 +522,7 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->part_fill, (void *)e->bt_rec, (void *)e->bt_cnt, (void *)e->base64, (void *)e->hll_lb,
                   (void *)e->expo_hdr, (void *)e->expo_buckets, (void *)e->expo_slot, (void *)e->expo_out_keys,
                   (void *)e->expo_out_rows, (void *)e->expo_out_buckets, (void *)e->hll_filt, (void *)e->xslab,
-                  (void *)e->xc_lcount, (void *)e->xc_entry_of, (void *)e->xc_slot_of_entry, (void *)e->xcslab,
+                  (void *)e->xc_lcount, (void *)e->xc_slot_of_entry, (void *)e->xcslab,
                   e->dstage[0], e->dstage[1]})
     if (p) (void)hipFree(p);
   for (int k = 0; k < 2; ++k) {
@@ -637,7 +636,6 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
   E.xG = e->G;
   E.xc_ne = e->expo_small ? e->xc_ne : 0u;
   E.lcount = E.xc_ne ? e->xc_lcount : nullptr;
-  E.entry_of = e->xc_entry_of;
   E.slot_of_entry = e->xc_slot_of_entry;
   E.xcslab = e->xcslab;
   return E;

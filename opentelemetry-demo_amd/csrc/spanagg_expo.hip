@@ -266,7 +266,7 @@ __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E)
   acc = part[0][sl];
 #pragma unroll
   for (uint32_t k = 1; k < 16; ++k) xhdr_add(acc, part[k][sl]);
-  if (E.lcount) E.lcount[s] = acc.cnt - acc.zero;  // this launch's positive durations (expo_select_kernel)
+  if (E.lcount) E.lcount[s] = acc.cnt - acc.zero;  // this launch's positive durations (the entry selection)
   if (!acc.cnt) return;  // no new values: the header (scale, range) stays as it is
   const unsigned long long minpos = ~acc.minx;  // UINT64_MAX when no positive duration
   const unsigned long long mn = acc.zero ? 0ULL : minpos;
@@ -284,79 +284,105 @@ __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E)
 constexpr uint32_t kXcBlock = 1024;
 constexpr uint64_t kXcMaxSpans = 65535;  // u16 LDS counts: spans per counting workgroup
 
-// Bucket counting of small tables, three kernels:
-//   expo_select_kernel     one block: the xc_ne series with the most positive
-//                          durations this launch get an LDS entry each (by
-//                          bit length of the count, ties in slot order)
-//   expo_count_slab_kernel per span: bucket index at the series' scale; an
-//                          entry's spans add to LDS u16 counts, which leave
-//                          as plain coalesced stores into the workgroup's slab;
-//                          other spans add to the HBM buckets with an atomic
+// Bucket counting of small tables, two kernels:
+//   expo_count_slab_kernel every workgroup first selects the xc_ne series with
+//                          the most positive durations this launch (lcount,
+//                          left by the reduce pass) for its LDS entries: by bit
+//                          length of the count, ties in slot order.  Every
+//                          workgroup computes the same selection; workgroup 0
+//                          also writes it out for the fold.  Then per span:
+//                          bucket index at the series' scale; an entry's spans
+//                          add to LDS u16 counts, which leave as plain
+//                          coalesced stores into the workgroup's slab; other
+//                          spans add to the HBM buckets with an atomic
 //   expo_fold_slab_kernel  per (entry, bucket pair): the sum over the
 //                          workgroups' slabs, added to the series' buckets
 //                          (one owner, no atomics)
 // A launch's C2 mix (10 M spans, ~1.4 k series, Zipf) put ~6 M atomics on
 // HBM with per-workgroup caches flushed by atomics: ~200 us of the ~310 us
-// the counting took.
-__global__ __launch_bounds__(1024) void expo_select_kernel(ExpoParams E) {
-  __shared__ uint32_t hist[33], scan[1024], tb_room[2];
-  const uint32_t t = threadIdx.x, cap = (uint32_t)E.cap, K = E.xc_ne;
-  // cap <= 2048: slots 2t and 2t + 1
-  uint32_t c[2], bl[2];
+// the counting took.  The selection was a one-block kernel of its own, 6 us
+// of block-wide scans plus a launch; in the counting kernel's prologue it is
+// two wave-shuffle scans.  Which series hold entries changes where counts are
+// added, never the counts.
+
+// Exclusive scan of v over a 1,024-thread block (wave shuffles, then the 16
+// wave totals through LDS wsum[16]); total = the block's sum.  Every thread
+// calls it.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *wsum, uint32_t &total) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  uint32_t x = v;
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const uint32_t sl = 2 * t + k;
-    c[k] = sl < cap ? E.lcount[sl] : 0u;
-    bl[k] = c[k] ? 32u - (uint32_t)__clz(c[k]) : 0u;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
+    if (lane >= (uint32_t)o) x += y;
   }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k) {
+    const uint32_t t = wsum[k];
+    base += k < w ? t : 0u;
+    tot += t;
+  }
+  __syncthreads();  // wsum is free again
+  total = tot;
+  return base + x - v;
+}
+
+// The entry selection (cap <= 2,048: slots 2t and 2t + 1 of thread t) into
+// ent[cap] (LDS; -1: no entry).  scratch: 64 LDS words.  Workgroup 0 also
+// writes slot_of_entry (~0u past the selected ones) for expo_fold_slab_kernel.
+// lc: lcount of slots 2t and 2t + 1 (0 past cap), loaded by the caller ahead
+// of its other prologue reads.
+__device__ __forceinline__ void expo_select_lds(const ExpoParams &E, int32_t *ent, uint32_t *scratch,
+                                                const uint32_t (&lc)[2]) {
+  const uint32_t t = threadIdx.x, cap = (uint32_t)E.cap, K = E.xc_ne, lane = t & 63u;
+  uint32_t *hist = scratch, *wsum = scratch + 48;  // hist[33], wsum[16]
+  uint32_t bl[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) bl[k] = lc[k] ? 32u - (uint32_t)__clz(lc[k]) : 0u;
   if (t < 33) hist[t] = 0;
-  __syncthreads();
+  // the wave's count of each bit length by ballots (lane b keeps length b's),
+  // then one conflict-free LDS add per lane: per-slot adds into a few hot
+  // bit lengths serialised on their words (~3 us)
+  uint32_t mine = 0;
 #pragma unroll
-  for (int k = 0; k < 2; ++k)
-    if (bl[k]) atomicAdd(&hist[bl[k]], 1u);
-  __syncthreads();
-  if (t == 0) {  // the bit length at which the K entries run out, and the room left there
-    uint32_t acc = 0, tb = 0;
-    for (uint32_t b = 32; b >= 1; --b) {
-      if (acc + hist[b] > K) {
-        tb = b;
-        break;
-      }
-      acc += hist[b];
-    }
-    tb_room[0] = tb;
-    tb_room[1] = K - acc;
+  for (uint32_t b = 1; b <= 32; ++b) {
+    const uint32_t c = (uint32_t)__popcll(__ballot(bl[0] == b)) + (uint32_t)__popcll(__ballot(bl[1] == b));
+    mine = lane == b ? c : mine;
   }
   __syncthreads();
-  const uint32_t tb = tb_room[0], room = tb_room[1];
-  // inclusive block scan of a per-thread value (two slots per thread)
-  auto block_scan = [&](uint32_t v) -> uint32_t {
-    scan[t] = v;
-    __syncthreads();
-    for (uint32_t o = 1; o < 1024; o <<= 1) {
-      const uint32_t x = t >= o ? scan[t - o] : 0u;
-      __syncthreads();
-      scan[t] += x;
-      __syncthreads();
-    }
-    const uint32_t r = scan[t];
-    __syncthreads();
-    return r;
-  };
+  if (mine) atomicAdd(&hist[lane], mine);
+  __syncthreads();
+  // every wave: suffix sums S[b] = #slots of bit length >= b (lane b); the
+  // boundary bit length tb is the largest b >= 1 with S[b] > K (0: every
+  // series fits), and S[tb + 1] of the entries go above it
+  uint32_t sfx = lane <= 32 ? hist[lane] : 0u;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_down((int)sfx, (unsigned)o, 64);
+    if (lane + (uint32_t)o < 64) sfx += y;
+  }
+  const uint64_t over = __ballot(lane >= 1 && lane <= 32 && sfx > K);
+  const uint32_t tb = over ? 63u - (uint32_t)__clzll((long long)over) : 0u;
+  const uint32_t room = K - (uint32_t)__shfl((int)sfx, (int)(tb + 1), 64);
   // boundary-bin slots in slot order take the room left
   const uint32_t b0 = (tb && bl[0] == tb) ? 1u : 0u, b1 = (tb && bl[1] == tb) ? 1u : 0u;
-  const uint32_t bx = block_scan(b0 + b1) - (b0 + b1);  // exclusive
-  bool sel[2];
-  sel[0] = bl[0] && (bl[0] > tb || (b0 && bx < room));
-  sel[1] = bl[1] && (bl[1] > tb || (b1 && bx + b0 < room));
-  const uint32_t n0 = sel[0] ? 1u : 0u, n1 = sel[1] ? 1u : 0u;
-  const uint32_t ex = block_scan(n0 + n1) - (n0 + n1);
-  if (2 * t < cap) E.entry_of[2 * t] = sel[0] ? (int32_t)ex : -1;
-  if (2 * t + 1 < cap) E.entry_of[2 * t + 1] = sel[1] ? (int32_t)(ex + n0) : -1;
-  if (sel[0]) E.slot_of_entry[ex] = 2 * t;
-  if (sel[1]) E.slot_of_entry[ex + n0] = 2 * t + 1;
-  const uint32_t nsel = scan[1023];  // (the last scan's total, still in LDS)
-  for (uint32_t k = nsel + t; k < K; k += 1024) E.slot_of_entry[k] = ~0u;
+  uint32_t tot;
+  const uint32_t bx = block_excl_scan(b0 + b1, wsum, tot);
+  const bool sel0 = bl[0] && (bl[0] > tb || (b0 && bx < room));
+  const bool sel1 = bl[1] && (bl[1] > tb || (b1 && bx + b0 < room));
+  const uint32_t n0 = sel0 ? 1u : 0u, n1 = sel1 ? 1u : 0u;
+  uint32_t nsel;
+  const uint32_t ex = block_excl_scan(n0 + n1, wsum, nsel);
+  if (2 * t < cap) ent[2 * t] = sel0 ? (int32_t)ex : -1;
+  if (2 * t + 1 < cap) ent[2 * t + 1] = sel1 ? (int32_t)(ex + n0) : -1;
+  if (blockIdx.x == 0) {
+    if (sel0) E.slot_of_entry[ex] = 2 * t;
+    if (sel1) E.slot_of_entry[ex + n0] = 2 * t + 1;
+    for (uint32_t k = nsel + t; k < K; k += 1024) E.slot_of_entry[k] = ~0u;
+  }
 }
 
 __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uint64_t per_wg) {
@@ -365,12 +391,16 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
   int2 *meta = reinterpret_cast<int2 *>(smem);                   // [cap] {scale, cur}
   int32_t *ent = reinterpret_cast<int32_t *>(meta + cap);         // [cap] entry or -1
   uint32_t *cnt = reinterpret_cast<uint32_t *>(ent + cap);        // [NE][wpe] u16 pairs
+  uint32_t *scratch = cnt + NE * wpe;                             // [64] selection scratch
+  uint32_t lc[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) lc[k] = 2 * threadIdx.x + k < cap ? E.lcount[2 * threadIdx.x + k] : 0u;
   for (uint32_t i = threadIdx.x; i < cap; i += kXcBlock) {
     const ExpoHdr &h = E.hdr[i];
     meta[i] = make_int2(h.scale, (int)h.cur);
-    ent[i] = E.entry_of[i];
   }
   for (uint32_t i = threadIdx.x; i < NE * wpe; i += kXcBlock) cnt[i] = 0;
+  expo_select_lds(E, ent, scratch, lc);
   __syncthreads();
   const uint64_t lo = blockIdx.x * per_wg, hi = lo + per_wg < E.n ? lo + per_wg : E.n;
   for (uint64_t i = lo + threadIdx.x; i < hi; i += kXcBlock) {
@@ -385,7 +415,7 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
     const uint32_t at = expo_mod(ix, M);
     const int32_t en_ = ent[slot];
     if (en_ >= 0) atomicAdd(&cnt[(uint32_t)en_ * wpe + (at >> 1)], 1u << ((at & 1u) * 16));
-    else atomicAdd(E.buckets + ((uint64_t)m.y * E.cap + slot) * M + at, 1u);
+    else if (!(E.diag & 1u)) atomicAdd(E.buckets + ((uint64_t)m.y * E.cap + slot) * M + at, 1u);
   }
   __syncthreads();
   uint32_t *slab = E.xcslab + (uint64_t)blockIdx.x * NE * wpe;
@@ -546,13 +576,13 @@ __host__ __device__ ExpoHdr expo_hdr_empty() {
 }
 
 uint32_t expo_slab_entries(uint64_t cap, uint32_t max_size, size_t budget) {
-  const size_t fixed = (size_t)cap * 12, per = (size_t)((max_size + 1) / 2) * 4;
+  const size_t fixed = (size_t)cap * 12 + 256, per = (size_t)((max_size + 1) / 2) * 4;
   if (budget <= fixed + per) return 0;
   return (uint32_t)std::min<size_t>(cap, (budget - fixed) / per);
 }
 
 size_t expo_slab_lds_bytes(uint64_t cap, uint32_t max_size, uint32_t ne) {
-  return (size_t)cap * 12 + (size_t)ne * ((max_size + 1) / 2) * 4;
+  return (size_t)cap * 12 + (size_t)ne * ((max_size + 1) / 2) * 4 + 256;
 }
 
 hipError_t prepare_expo_slab(size_t lds_bytes) {
@@ -587,8 +617,8 @@ void launch_reduce_rescale(const ExpoParams &E, hipStream_t s) {
 hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s) {
   if (E.n == 0) return hipSuccess;
   if (E.xslab && E.xc_ne) {  // small table, slab counting (E.xG workgroups, <= kXcMaxSpans spans each)
+    if (E.cap > 2048) return hipErrorInvalidValue;  // the selection's two slots per thread
     launch_reduce_rescale(E, s);
-    hipLaunchKernelGGL(expo_select_kernel, dim3(1), dim3(1024), 0, s, E);
     const uint64_t per_wg = (E.n + E.xG - 1) / E.xG;
     if (per_wg > kXcMaxSpans) return hipErrorInvalidValue;  // (the engine splits batches below this)
     const uint32_t grid = (uint32_t)((E.n + per_wg - 1) / per_wg);

@@ -165,6 +165,26 @@ def test_expo_edges_zero_pow2_and_huge():
         _check(e.flush_exp(), batch, 4)
 
 
+@pytest.mark.parametrize("path", ["small", "hbm"])
+def test_expo_huge_durations(path, monkeypatch):
+    """Durations around 2^52 ns and up to 9e17 ns (weeks to decades) on both
+    table paths: the fast log2 index path, the exact Go math.Log path and the
+    rescale by shifted scale-20 indices all agree with the oracle."""
+    monkeypatch.setenv("SPANAGG_EXPO_SMALL", "1" if path == "small" else "0")
+    ds = [2**52 - 3, 2**52 - 2, 2**52 - 1, 2**52, 2**52 + 1, 3 * 2**52, 9 * 10**17, 5_000_000, 2**40, 1]
+    n = len(ds)
+    end = np.full(n, 10**18, dtype=np.uint64)
+    start = end - np.array(ds, dtype=np.uint64)
+    batch = SpanBatch(np.array([11, 22] * (n // 2), dtype=np.uint64), start, end,
+                      np.arange(n, dtype=np.uint64), np.arange(n, dtype=np.uint64), pack_meta([0] * n, 2, 0))
+    for max_size in (4, 160):
+        with Engine(Config(n_services=1, n_windows=16, exp_max_size=max_size)) as e:
+            assert e.stats()["small_table"] == (1 if path == "small" else 0)
+            e.window_advance(10**18 // 10**10)
+            e.ingest(batch)
+            _check(e.flush_exp(), batch, max_size)
+
+
 def test_expo_sketches_unchanged():
     wl = generate_c2(150_000, seed=23)
     with _engine(wl, exp_max_size=160) as e:

@@ -67,7 +67,7 @@ def main():
             if "SQ_ACTIVE_INST_VALU" in c and "SQ_WAVE_CYCLES" in c:
                 d["valu_issue_share_per_wave"] = c["SQ_ACTIVE_INST_VALU"] / c["SQ_WAVE_CYCLES"]
             if "SQ_LDS_BANK_CONFLICT" in c and "SQ_LDS_IDX_ACTIVE" in c:
-                d["lds_bank_conflict_share"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
+                d["lds_bank_conflict_share"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"] if c["SQ_LDS_IDX_ACTIVE"] else None
             if "FETCH_SIZE" in c:
                 d["fetch_bytes_corrected"] = 2 * c["FETCH_SIZE"] * 1024
             if "WRITE_SIZE" in c:
