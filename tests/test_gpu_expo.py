@@ -99,15 +99,18 @@ def test_fast_index_agrees_with_exact_path(unit):
     assert taken[low].mean() > 0.99, taken[low].mean()  # the fast path carries the common case
 
 
-@pytest.mark.parametrize("path", ["small", "hbm"])
+@pytest.mark.parametrize("path", ["small", "small_cached", "hbm"])
 @pytest.mark.parametrize("max_size,unit", [(160, "ms"), (8, "ms"), (20, "s"), (2, "ms")])
 def test_expo_histograms_match_oracle(max_size, unit, path, monkeypatch):
     """small: the small-table kernel in EXPO mode (LDS header partials, slab
-    reduce, LDS-cached bucket counts); hbm: the pass-1 global-atomic path."""
-    monkeypatch.setenv("SPANAGG_EXPO_SMALL", "1" if path == "small" else "0")
+    reduce, LDS slab counts for the selected series); small_cached: the same
+    with the cached-probe counting kernel (SPANAGG_XC_SLAB=0); hbm: the
+    pass-1 global-atomic path."""
+    monkeypatch.setenv("SPANAGG_EXPO_SMALL", "0" if path == "hbm" else "1")
+    monkeypatch.setenv("SPANAGG_XC_SLAB", "0" if path == "small_cached" else "1")
     wl = generate_c2(200_003, seed=13)
     with _engine(wl, exp_max_size=max_size, unit=unit) as e:
-        assert e.stats()["small_table"] == (1 if path == "small" else 0)
+        assert e.stats()["small_table"] == (0 if path == "hbm" else 1)
         e.ingest(wl.batch)
         res = e.flush_exp()
         _check(res, wl.batch, max_size, unit == "s")
