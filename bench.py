@@ -483,9 +483,10 @@ def roofline(name, n, r, traffic_path=None):
     traffic, tsrc = load_traffic(tpath, name)
     piped = BYTES_PER_SPAN * n / (r["device_ms"] * 1e-3) / 1e9
     kern = {"c2": "ingest_v2_kernel (spanagg_kernels.hip)",
-            "c2expo": "ingest_v2_kernel EXPO mode + expo_reduce_rescale_kernel + expo_count_cached_kernel",
-            "c4": "bt_scatter2_kernel + bt_aggregate2_kernel (spanagg_binned.hip)",
-            "c4zipf": "bt_scatter2_kernel + bt_aggregate2_kernel (spanagg_binned.hip)"}[name]
+            "c2expo": "ingest_v2_kernel EXPO mode + expo_reduce_rescale_kernel + expo_count_slab_kernel + "
+                      "expo_fold_slab_kernel (spanagg_kernels.hip, spanagg_expo.hip)",
+            "c4": "bt_scatter2_kernel + bt_aggregate3_kernel (spanagg_binned.hip)",
+            "c4zipf": "bt_scatter2_kernel + bt_aggregate3_kernel (spanagg_binned.hip)"}[name]
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kern, "kernel_ms": r["kernel_ms"],
             "kernel_ms_bracketed": r["kernel_ms_bracketed"],

@@ -16,7 +16,8 @@
 //     through 4-record LDS stages that leave as aligned 64-B chunks.  Hot keys
 //     are pre-aggregated in an LDS overflow table; past that, the direct path
 //     (key-table CAS + atomics into the spill array).
-//   bt_aggregate2_kernel (one 512-thread workgroup per bin)
+//   bt_aggregate3_kernel (one 512-thread workgroup per bin; the default, see
+//   bt_agg_fn -- bt_aggregate2_kernel is the earlier form, SPANAGG_BT_AGG=2)
 //     loads the bin's 2^log2sb key slots into LDS at the same positions,
 //     aggregates the bin's records there (u16 bucket-count pairs, u64 ns
 //     sums, an ERROR table keyed by (window slot, key slot)), then writes the

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-workgroup timeline of the binned C4 kernels (bt_scatter2_kernel,
-bt_aggregate2_kernel) from in-kernel s_memrealtime stamps (SPANAGG_STAMPS=1
+bt_aggregate3_kernel, or bt_aggregate2_kernel with SPANAGG_BT_AGG=2) from in-kernel s_memrealtime stamps (SPANAGG_STAMPS=1
 diagnostic engines).  Prints phase durations (us) over workgroups."""
 import ctypes as C
 import json
