@@ -223,6 +223,21 @@ def trace_variants(w0, w1, k, seed, rank=0, world=1):
     return out
 
 
+def n_variants(args, launches, device):
+    """Trace-id variants to build: one per launch before the soak (--variants 0,
+    the default), so every launch `value`, `kernel_ms` and a rocprofv3 trace of
+    the run see is a fresh trace-id set; an explicit --variants caps it.  Each
+    variant is 16 B/span of device memory; the count is bounded by what fits in
+    half the free HBM (a 400-step trace of 10 M-span batches needs ~93 GB)."""
+    want = launches if args.variants <= 0 else min(args.variants, launches)
+    import torch
+    free, _ = torch.cuda.mem_get_info(device)
+    fit = max(2, int(free // 2 // (16 * args.spans)))
+    if want > fit:
+        print(f"bench: {want} trace-id variants do not fit; using {fit} (variants repeat)", file=sys.stderr)
+    return min(want, fit)
+
+
 WORKLOADS = {
     "c2": ("C2: synthetic SoA v1 spans, 20 services x 25 span names (Zipf 1.1) x 3 status codes -> "
            "<=1,500 series, default spanmetrics buckets, lognormal durations, ~10 spans/trace, "
@@ -260,7 +275,7 @@ def run_workload(name, n, args, device, rank, world, barrier):
     for c in batch.columns():
         cols.append(torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(device))
     n_iso = max(3, args.steps // 5)
-    n_var = min(args.variants, 1 + args.settle + args.warmup + 2 * n_iso + args.steps)
+    n_var = n_variants(args, 1 + args.settle + args.warmup + 2 * n_iso + args.steps, device)
     variants = trace_variants(cols[3], cols[4], n_var, seed=1000 + rank, rank=rank, world=world)
     if world > 1:  # every span of every variant belongs to this rank's trace-id shard
         from spanagg.dist import shard_of
@@ -452,7 +467,7 @@ def run_group(n, members, args, device):
     cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(device)
             for c in wl.batch.columns()]
     k = args.warmup + args.steps
-    variants = trace_variants(cols[3], cols[4], min(k, args.variants), seed=1000)
+    variants = trace_variants(cols[3], cols[4], n_variants(args, k, device), seed=1000)
     g = Group([device.index] * members, Config(n_services=wl.n_services, n_windows=16, key_capacity=1500))
     g.window_advance(wl.first_window)
     s = torch.cuda.current_stream(device)
@@ -516,8 +531,9 @@ def main():
                     help="seconds of back-to-back launches after the timed steps (reported as sustained)")
     ap.add_argument("--settle", type=int, default=16,
                     help="untimed launches after the cold one, before the warm-up (HLL registers settle)")
-    ap.add_argument("--variants", type=int, default=128,
-                    help="distinct trace-id variants of the batch (one per launch up to this many)")
+    ap.add_argument("--variants", type=int, default=0,
+                    help="distinct trace-id variants of the batch (0 = one per launch before the soak; "
+                         "N = at most N, repeating after that)")
     ap.add_argument("--sub", default="c4,c4zipf,c2expo",
                     help="extra workloads reported as sub-objects of the line at N=1 ('' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)

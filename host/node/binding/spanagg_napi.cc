@@ -951,6 +951,9 @@ napi_value ColumnizerIngest(napi_env env, napi_callback_info info) {
   if (n) {
     sa_span_batch b{c->col.key(), c->col.start(), c->col.end(), c->col.w0(), c->col.w1(), c->col.meta(), n};
     const int rc = c->engine->ingest(&b);
+    // a failed ingest rejects these columns' requests (the host reports them
+    // to their senders): drop the columns too, so a retry counts nothing twice
+    c->col.clear_buffer();
     if (rc != SA_OK) return engine_error(env, c->engine, rc, "sa_ingest");
   }
   c->col.clear_buffer();

@@ -628,11 +628,21 @@ class SpanMetricsConnector {
       this.windowBase = base;
     }
     if (maxWid > this.maxWindowSeen) this.maxWindowSeen = maxWid;
-    if (cols.n) this.addon.ingest(this.handle, cols.view());
-    cols.n = 0;
-    if (this.nativeBuffered) this.addon.columnizerIngest(this.col);
-    this.nativeBuffered = 0;
-    this.nativeMaxEnd = 0n;
+    let applied = false;
+    try {
+      if (cols.n) this.addon.ingest(this.handle, cols.view());
+      cols.n = 0;
+      if (this.nativeBuffered) this.addon.columnizerIngest(this.col);
+      applied = true;
+    } finally {
+      // a failed ingest rejects the requests these columns hold
+      // (consumeTracesBatch reports them to their senders): drop the columns,
+      // JavaScript and native, so a sender's retry counts nothing twice
+      cols.n = 0;
+      if (!applied && this.nativeBuffered) this.addon.columnizerTake(this.col);
+      this.nativeBuffered = 0;
+      this.nativeMaxEnd = 0n;
+    }
   }
 
   // ------------------------------------------------------------ export

@@ -177,6 +177,7 @@ class NativeColumnizerFakeAddon extends FakeAddon {
   columnizerRemap(c, from, to) { return this.real.columnizerRemap(c, from, to); }
   columnizerResetExemplars(c) { return this.real.columnizerResetExemplars(c); }
   columnizerDestroy(c) { return this.real.columnizerDestroy(c); }
+  columnizerTake(c) { return this.real.columnizerTake(c); }
   columnizerIngest(c) {
     const b = this.real.columnizerTake(c);
     this.ingest(null, b);

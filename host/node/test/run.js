@@ -694,8 +694,11 @@ test('consumeTracesBatch: a failure part-way rejects only the requests not yet a
   let drains = 0;
   addon.columnizerIngest = (c) => {  // the engine fails on its second batch of columns
     drains += 1;
-    const b = addon.real.columnizerTake(c);
+    // a failing ingest that leaves the columns buffered (the worst case: the
+    // connector itself must drop them, advisor r3)
     if (drains === 2) throw new Error('SA_EDEVICE: device lost');
+    const b = addon.real.columnizerTake(c);
+    addon.ingest(null, b);
     return b.keyHash.length;
   };
   const conn = new SpanMetricsConnector({ batch_size: 4, columnizer_threads: 1 }, { addon, rules: DEMO_SPAN_NAME_RULES });
@@ -706,6 +709,11 @@ test('consumeTracesBatch: a failure part-way rejects only the requests not yet a
   assert.deepStrictEqual(conn.consumeTracesBatch([req(0), req(1)]), [null, null]);
   const errs = conn.consumeTracesBatch([req(2), req(3)]);
   assert.ok(errs.every((e) => e instanceof Error && e.deferred === true), String(errs));
+  // the senders retry the rejected requests: each span counts once
+  assert.deepStrictEqual(conn.consumeTracesBatch([req(2), req(3)]), [null, null]);
+  const calls = dpsOf(conn.exportMetrics(), 'traces.span.metrics.calls');
+  assert.strictEqual(calls.length, 12);  // 4 services x 3 span names
+  assert.ok(calls.every((d) => Number(d.asInt) === 1), calls.map((d) => String(d.asInt)).join(","));
   const addon2 = new NativeColumnizerFakeAddon();
   addon2.columnizeBatch = () => { throw new Error('columnizer broke'); };
   const c2 = new SpanMetricsConnector({ columnizer_threads: 2 }, { addon: addon2, rules: DEMO_SPAN_NAME_RULES });

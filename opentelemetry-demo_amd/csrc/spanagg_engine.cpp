@@ -845,6 +845,16 @@ int sa_ingest(sa_engine *e, const sa_span_batch *b) {
     }
   }
   const bool pinned = batch_pinned(b);
+  // page-locked columns are copied asynchronously: an error return after the
+  // first copy still waits for the copies in flight (the caller may reuse or
+  // free its columns as soon as the call returns, whatever it returned)
+  struct CopyGuard {
+    hipStream_t s;
+    bool armed;
+    ~CopyGuard() {
+      if (armed) (void)hipStreamSynchronize(s);
+    }
+  } guard{e->stream, pinned};
   for (uint64_t off = 0; off < b->n; off += kChunk) {
     const uint64_t m = std::min(kChunk, b->n - off);
     const uint64_t ms = (m + 1) & ~1ULL;  // column stride: u64 columns stay 16-byte aligned
@@ -888,6 +898,7 @@ int sa_ingest(sa_engine *e, const sa_span_batch *b) {
   // page-locked columns: every chunk's copies are done (stream order) once
   // the last chunk's are, before the caller may reuse the arrays
   if (pinned) SA_HIP(e, hipEventSynchronize(e->ev_b));
+  guard.armed = false;
   return SA_OK;
 }
 

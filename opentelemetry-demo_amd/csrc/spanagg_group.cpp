@@ -184,7 +184,10 @@ struct sa_group {
   Buf part[2][kMaxMembers], peer[2][kMaxMembers];
   hipEvent_t ev_scat[2][kMaxMembers] = {}, ev_done[2][kMaxMembers] = {};
   bool done_used[2][kMaxMembers] = {};
-  std::vector<Buf> pcnt;                 // [n] shard counters / cursors (2 x nm u64) per source device
+  // [2][n] shard counters + per-workgroup cursors, per staging set and source
+  // device: a call's count/scan may overlap the scatter of the call before it
+  // (when the caller alternates streams), never the one of the same set
+  std::vector<Buf> pcnt;
   unsigned long long *hcnt = nullptr;    // pinned host copy of the counts
   // sa_group_ingest: per-member packed host shards, reused across calls
   std::vector<std::vector<uint64_t>> hcol;
@@ -353,7 +356,7 @@ int sa_group_create(const sa_config *cfg, const int32_t *devices, uint32_t n, sa
   g->hll.resize(n);
   g->cms.resize(n);
   g->dropped_seen.assign(n, 0);
-  g->pcnt.resize(n);
+  g->pcnt.resize(2 * n);
   g->hcol.resize(n);
   g->hmeta.resize(n);
   for (uint32_t i = 0; i < n; ++i) {
@@ -402,8 +405,11 @@ void sa_group_destroy(sa_group *g) {
       (void)hipStreamSynchronize(g->st[i]);
       (void)hipStreamDestroy(g->st[i]);
     }
-    for (std::vector<Buf> *v : {&g->keys, &g->gath, &g->uni, &g->rows, &g->hll, &g->cms, &g->pcnt})
+    for (std::vector<Buf> *v : {&g->keys, &g->gath, &g->uni, &g->rows, &g->hll, &g->cms})
       if (i < v->size() && (*v)[i].p) (void)hipFree((*v)[i].p);
+    for (size_t k = 0; k < 2; ++k)
+      if (k * g->eng.size() + i < g->pcnt.size() && g->pcnt[k * g->eng.size() + i].p)
+        (void)hipFree(g->pcnt[k * g->eng.size() + i].p);
     for (int k = 0; k < 2; ++k) {
       if (i < kMaxMembers && g->part[k][i].p) (void)hipFree(g->part[k][i].p);
       if (i < kMaxMembers && g->peer[k][i].p) (void)hipFree(g->peer[k][i].p);
@@ -523,8 +529,9 @@ int sa_group_ingest_device(sa_group *g, const sa_span_batch *b, uint32_t src, vo
     if (g->done_used[k][i]) SG_HIP(g, hipStreamWaitEvent(s, g->ev_done[k][i], 0));
   // 1. shard sizes
   const uint32_t pgrid = grid_for(b->n);
-  if (int rc = ensure(g, sdev, g->pcnt[src], kMaxMembers * 8 + (size_t)4096 * kMaxMembers * 4)) return rc;
-  unsigned long long *dcnt = static_cast<unsigned long long *>(g->pcnt[src].p);
+  Buf &pc = g->pcnt[(size_t)k * n + src];  // this set's: the previous call's scatter may still read the other
+  if (int rc = ensure(g, sdev, pc, kMaxMembers * 8 + (size_t)4096 * kMaxMembers * 4)) return rc;
+  unsigned long long *dcnt = static_cast<unsigned long long *>(pc.p);
   uint32_t *dblk = reinterpret_cast<uint32_t *>(dcnt + kMaxMembers);  // [n][pgrid] counts -> first positions
   if (b->n > 0xFFFFFFFFull) return gfail(g, SA_EINVAL, "device batch above 2^32 spans (u32 shard positions)");
   SG_HIP(g, hipMemsetAsync(dcnt, 0, kMaxMembers * 8, s));

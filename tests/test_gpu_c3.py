@@ -122,6 +122,65 @@ def test_group_device_ingest_matches_oracle(members, n):
         assert st["zero_key"] == 2 * int((key == 0).sum())
 
 
+def test_group_device_ingest_alternating_streams():
+    """Advisor r3: consecutive sa_group_ingest_device calls on two different
+    caller streams.  Each staging set has its own shard counters and cursors,
+    so a call's count/scan never rewrites the cursors the previous call's
+    partition kernel (on the other stream) may still be reading."""
+    import torch
+    dev = torch.device("cuda", 0)
+    n = 2_000_003
+    wl = generate_c2(n, seed=21)
+    cols = _device_cols(wl.batch, dev)
+    variants = bench.trace_variants(cols[3], cols[4], 6, seed=4000)
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    for s in streams:
+        s.wait_stream(torch.cuda.current_stream(dev))
+    o = pyoracle.Oracle(n_services=wl.n_services)
+    with Group([0] * 4, Config(n_services=wl.n_services, n_windows=16, key_capacity=1500)) as g:
+        g.window_advance(wl.first_window)
+        for i, (w0, w1) in enumerate(variants):
+            g.ingest_device(cols[0], cols[1], cols[2], w0, w1, cols[5], n=n, src=0,
+                            stream=streams[i % 2].cuda_stream)
+            o.ingest(SpanBatch(wl.batch.key_hash, wl.batch.start_ns, wl.batch.end_ns,
+                               w0.cpu().numpy().view(np.uint64), w1.cpu().numpy().view(np.uint64), wl.batch.meta))
+        g.sync()
+        torch.cuda.synchronize(dev)
+        assert g.stats()["spans"] == 6 * n
+        _check(g, o)
+
+
+def test_group_device_ingest_cross_device_matches_host_split():
+    """Advisor r3: the cross-device branch of sa_group_ingest_device (peer
+    staging buffers, hipMemcpyPeerAsync of each packed shard, cross-device
+    event waits) against the host split (sa_group_ingest) of the same spans.
+    Needs two GPUs: the round's GPU boxes have one, so this runs only where a
+    multi-GPU box is available (unverified until then)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one GPU: the cross-device branch needs two devices")
+    devs = list(range(min(4, torch.cuda.device_count())))
+    n = 3_000_001
+    wl = generate_c2(n, seed=31)
+    cols = _device_cols(wl.batch, torch.device("cuda", 0))
+    cfg = Config(n_services=wl.n_services, n_windows=16, key_capacity=1500)
+    with Group(devs, cfg) as gd, Group(devs, cfg) as gh:
+        gd.window_advance(wl.first_window)
+        gh.window_advance(wl.first_window)
+        for _ in range(3):  # both staging sets, then the first again
+            gd.ingest_device(*cols, n=n, src=0)
+            gh.ingest(wl.batch)
+        gd.sync()
+        a, b = gd.flush(), gh.flush()
+        assert np.array_equal(a.key_hash, b.key_hash)
+        assert np.array_equal(a.bucket_counts, b.bucket_counts)
+        assert np.array_equal(a.sum_ns, b.sum_ns)
+        o = pyoracle.Oracle(n_services=wl.n_services)
+        for _ in range(3):
+            o.ingest(wl.batch)
+        assert_red_equal(a, o.series())
+
+
 def test_group_device_ingest_binned_members():
     import torch
     dev = torch.device("cuda", 0)
