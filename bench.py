@@ -409,8 +409,8 @@ def run_workload(name, n, args, device, rank, world, barrier):
 
 
 def kernel_ms_filter_off(n, args, device):
-    """C2 kernel time with the HLL lower-bound filter off (SPANAGG_HLL_LB=0 at
-    engine creation): every span reads its HLL register.  Same launches as the
+    """C2 kernel time with the HLL lower-bound filter off (SA_OPT_NO_HLL_FILTER
+    at engine creation): every span reads its HLL register.  Same launches as the
     main run's kernel time (fresh variants, after cold + settle + warm-up), so
     the filter's share of the kernel time is visible beside `value`."""
     import numpy as np
@@ -425,15 +425,9 @@ def kernel_ms_filter_off(n, args, device):
     n_iso = max(3, args.steps // 5)
     k = 1 + args.settle + args.warmup + n_iso
     variants = trace_variants(cols[3], cols[4], k, seed=1000)
-    old = os.environ.get("SPANAGG_HLL_LB")
-    os.environ["SPANAGG_HLL_LB"] = "0"
-    try:
-        eng = Engine(Config(n_services=wl.n_services, n_windows=16, key_capacity=1500, device=device.index))
-    finally:
-        if old is None:
-            del os.environ["SPANAGG_HLL_LB"]
-        else:
-            os.environ["SPANAGG_HLL_LB"] = old
+    from spanagg._lib import OPT_NO_HLL_FILTER
+    eng = Engine(Config(n_services=wl.n_services, n_windows=16, key_capacity=1500, device=device.index,
+                        options=OPT_NO_HLL_FILTER))
     eng.window_advance(wl.first_window)
     s = torch.cuda.current_stream(device)
     for w0, w1 in variants[: k - n_iso]:
@@ -449,7 +443,7 @@ def kernel_ms_filter_off(n, args, device):
     eng.close()
     return {"kernel_ms": ms, "hll_filtered": filt,
             "note": "C2 kernel alone (serial launches after cold + settle + warm-up, fresh trace-id variants) "
-                    "with SPANAGG_HLL_LB=0: every span gathers its HLL register"}
+                    "with SA_OPT_NO_HLL_FILTER: every span gathers its HLL register"}
 
 
 def run_group(n, members, args, device):

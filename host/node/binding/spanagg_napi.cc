@@ -275,6 +275,7 @@ napi_value ConfigDefault(napi_env env, napi_callback_info) {
     set(env, o, "keyCapacity", num(env, static_cast<double>(c.key_capacity)));
     set(env, o, "device", num(env, c.device));
     set(env, o, "flags", num(env, c.flags));
+    set(env, o, "options", num(env, c.options));
     return o;
 }
 
@@ -326,7 +327,7 @@ napi_value Create(napi_env env, napi_callback_info info) {
     } u32s[] = {{"hllP", &c.hll_p},         {"cmsD", &c.cms_d},
                 {"cmsW", &c.cms_w},         {"nWindows", &c.n_windows},
                 {"nServices", &c.n_services}, {"flags", &c.flags},
-                {"expMaxSize", &c.exp_max_size}};
+                {"expMaxSize", &c.exp_max_size}, {"options", &c.options}};
     for (auto &f : u32s)
         if (!is_undefined(env, v = prop(env, cfg, f.k)) && !to_u32(env, v, f.dst, f.k)) return nullptr;
     if (!is_undefined(env, v = prop(env, cfg, "windowNs")) && !to_u64(env, v, &c.window_ns, "windowNs"))

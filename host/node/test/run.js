@@ -186,7 +186,7 @@ test('config: durations, defaults and validation', () => {
 
 test('addon loads; pure helpers work; engine errors carry sa_status codes', () => {
   const addon = require('../lib/addon').load();
-  assert.strictEqual(addon.abiVersion(), 3);
+  assert.strictEqual(addon.abiVersion(), 4);
   const d = addon.configDefault();
   assert.deepStrictEqual(d.bounds, [2, 4, 6, 8, 10, 50, 100, 200, 400, 800, 1000, 1400, 2000, 5000, 10000, 15000]);
   const t = addon.bucketThresholds(d.bounds, 'ms');

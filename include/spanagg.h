@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define SA_ABI_VERSION 3
+#define SA_ABI_VERSION 4
 #define SA_MAX_BOUNDS 62
 
 typedef enum {
@@ -62,13 +62,30 @@ typedef enum {
 
 typedef enum { SA_UNIT_MS = 0, SA_UNIT_S = 1 } sa_unit;
 
-/* Diagnostic ablations (sa_config.flags), used only to attribute kernel time. */
+/* Diagnostic ablations (sa_config.flags), used only to attribute kernel time.
+ * Only the laboratory build of the library accepts them (`make -C
+ * opentelemetry-demo_amd ab` -> libspanagg_ab.so, used by tools/); the
+ * product library returns SA_EINVAL for any flags != 0. */
 #define SA_DIAG_NO_RED 1u     /* skip key lookup + counter updates */
 #define SA_DIAG_NO_HLL 2u     /* skip HLL hashing + register updates */
 #define SA_DIAG_NO_CMS 4u     /* skip count-min updates */
 #define SA_DIAG_NO_FLUSH 8u   /* skip the LDS -> slab flush */
 #define SA_DIAG_L2_INPUT 16u  /* every workgroup re-reads the batch's first 4 tiles
                                  (cache-resident input: prices the HBM stream) */
+
+/* Path options (sa_config.options): each selects another kernel path (or
+ * merge transport) that computes the SAME results -- the parity tests compare
+ * the paths through them.  0 (the default) lets the engine pick by geometry. */
+#define SA_OPT_NO_HLL_FILTER (1u << 0) /* every span gathers its HLL register (no lower-bound filter) */
+#define SA_OPT_PARTITIONED   (1u << 1) /* large tables: the partitioned path instead of the binned one */
+#define SA_OPT_ATOMIC_TABLE  (1u << 2) /* large tables: per-span HBM CAS + atomics (no partition) */
+#define SA_OPT_EXPO_HBM      (1u << 3) /* exponential histograms on the HBM-table kernels at any size */
+#define SA_OPT_EXPO_CACHED   (1u << 4) /* small exponential tables: the cached-probe counting kernel */
+#define SA_OPT_IDENTITY_IDS  (1u << 5) /* binned table: stored id = series id (no random multiplier) */
+#define SA_OPT_STAMPS        (1u << 6) /* per-workgroup timestamps for sa_debug_stamps */
+#define SA_OPT_GROUP_COPY    (1u << 7) /* sa_group_create: merge through device copies, never RCCL */
+#define SA_OPT_GROUP_RCCL    (1u << 8) /* sa_group_create: RCCL even for a group of one */
+#define SA_OPT_ALL           0x1FFu
 
 typedef struct {
     /* histogram.explicit.buckets (sorted ascending, finite) and histogram.unit */
@@ -85,11 +102,12 @@ typedef struct {
     uint64_t key_capacity;  /* expected distinct series; table = next pow2 >= 1.25x */
     int32_t device;         /* HIP device ordinal (one engine per GPU / rank) */
     uint32_t flags;         /* 0 for production; SA_DIAG_* bits are profiling-only
-                               ablations that skip work and make results WRONG */
+                               ablations that skip work and make results WRONG
+                               (laboratory build only) */
     /* histogram.exponential.max_size: 0 = explicit buckets (the default);
      * 2..4096 = exponential histograms (bounds unused; read with sa_flush_exp) */
     uint32_t exp_max_size;
-    uint32_t reserved;
+    uint32_t options;       /* SA_OPT_* path options (0 = the engine's choice) */
 } sa_config;
 
 typedef struct {
@@ -263,7 +281,7 @@ int sa_window_export(sa_engine *e, uint64_t window_id, uint8_t *d_hll, uint64_t 
  * Merge transport: when every member has its own device the group owns an
  * RCCL communicator over them (ncclAllGather of the key lists, ncclAllReduce
  * sum u64 of the dense rows and count-min cells, max u8 of the HLL
- * registers, over xGMI); members that share a device (or SPANAGG_GROUP_RCCL=0)
+ * registers, over xGMI); members that share a device (or SA_OPT_GROUP_COPY)
  * merge through device-to-device copies onto member 0's device and a reduce
  * kernel there.  Results are identical either way (integer sums and maxima).
  * Threading: as an engine (single producer); sa_group_ingest fans the shards
@@ -311,8 +329,8 @@ int sa_group_get_stats(sa_group *g, sa_stats *out);
 /* Diagnostic only: per-workgroup s_memrealtime stamps (100 MHz) of the last
  * small-table ingest launch, [G][136] = {start, after LDS setup, after the span
  * loop, after the slab flush, 0 x 4, then per wave 8 segment cycle sums};
- * filled only when the engine was created with SPANAGG_STAMPS set in the
- * environment (*n_out = 0 otherwise). */
+ * filled only when the engine was created with SA_OPT_STAMPS (*n_out = 0
+ * otherwise). */
 int sa_debug_stamps(sa_engine *e, uint64_t *out, uint64_t cap, uint64_t *n_out);
 
 /* ---- pure host helpers (no device needed) ---- */

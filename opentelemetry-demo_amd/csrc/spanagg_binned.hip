@@ -16,8 +16,8 @@
 //     through 4-record LDS stages that leave as aligned 64-B chunks.  Hot keys
 //     are pre-aggregated in an LDS overflow table; past that, the direct path
 //     (key-table CAS + atomics into the spill array).
-//   bt_aggregate3_kernel (one 512-thread workgroup per bin; the default, see
-//   bt_agg_fn -- bt_aggregate2_kernel is the earlier form, SPANAGG_BT_AGG=2)
+//   bt_aggregate3_kernel (one 512-thread workgroup per bin; the laboratory
+//   build also keeps bt_aggregate2_kernel, the earlier form, SPANAGG_BT_AGG=2)
 //     loads the bin's 2^log2sb key slots into LDS at the same positions,
 //     aggregates the bin's records there (u16 bucket-count pairs, u64 ns
 //     sums, an ERROR table keyed by (window slot, key slot)), then writes the
@@ -122,7 +122,7 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {
 // a span whose stage is full in its round, or whose region is used up, goes
 // to the overflow table, past that the direct path.  The record layout
 // ({m's low 53 bits | ERROR flag | window slot, duration} per (bin,
-// workgroup) region) is the one bt_aggregate2_kernel reads.
+// workgroup) region) is the one bt_aggregate3_kernel reads.
 // MODE (ablation): 1 = no records, 2 = no HLL, 4 = overflow-table adds
 // skipped, 8 = overflow-table ERROR counts skipped.
 template <int MODE = 0>
@@ -476,7 +476,8 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
   bt_stamp(P, sbase, 3);
 }
 
-// Aggregate, second form (the default).  One 512-thread workgroup per bin;
+// Aggregate geometry (bt_aggregate3_kernel; the laboratory build's earlier
+// form bt_aggregate2_kernel shares it).  One 512-thread workgroup per bin;
 // its LDS holds the bin's key slots (mirror), u64 ns sums and u16 bucket
 // counts (17 per slot, packed), an ERROR table and the region fills: 53 KiB
 // at 1,024 slots, so three workgroups share a CU.  No prefix scan: each
@@ -490,6 +491,8 @@ __host__ __device__ inline uint32_t bt_agg2_cnt_words(uint32_t sb) { return (sb 
 __host__ __device__ inline uint32_t bt_agg2_off_err(uint32_t sb) { return (sb * 16 + bt_agg2_cnt_words(sb) * 4 + 7) & ~7u; }
 __host__ __device__ inline uint32_t bt_agg2_off_reg(uint32_t sb) { return bt_agg2_off_err(sb) + kBtAgg2Err * 8; }
 
+#ifdef SPANAGG_AB
+// Aggregate, second form (laboratory build only).
 // MODE (ablation): 1 = no records aggregated, 2 = no key / row write-back,
 // 4 = records loaded only;
 // MAXPER = key slots per thread (sb <= MAXPER * BLOCK)
@@ -710,6 +713,7 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
   if (tid == 0 && misc[0]) atomicAdd(&P.stats[kStatDropped], (unsigned long long)misc[0]);
   bt_stamp(P, (uint64_t)bin * 8, 3);
 }
+#endif  // SPANAGG_AB
 
 
 // Aggregate, third form (the default).  The layout, phases and row
@@ -977,6 +981,7 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
 
 }  // namespace
 
+#ifdef SPANAGG_AB
 // SA_DIAG bits of the ablation builds (profiling only)
 constexpr uint32_t kDiagBtAggNoRows = 1u << 21, kDiagBtNoAgg = 1u << 22, kDiagBtNoScatter = 1u << 23;
 constexpr uint32_t kDiagBtHotAcc = 1u << 25, kDiagBtHotErr = 1u << 26, kDiagBtSeqStore = 1u << 27,
@@ -1047,6 +1052,29 @@ static const void *bt_agg2_fn(uint32_t diag) {
   }
 }
 
+#endif
+
+#ifndef SPANAGG_AB
+// Product build: one scatter and one aggregate (bins of up to 1,024 slots, or
+// the wide form for 2,048); the ablation MODEs and the earlier aggregate form
+// live in the laboratory build.
+static const void *bt_scatter2_fn(uint32_t) { return (const void *)&bt_scatter2_kernel<0>; }
+constexpr uint32_t kDiagBtAggWide = 1u << 30;
+static const void *bt_agg_fn(uint32_t diag) {
+  return (diag & kDiagBtAggWide) ? (const void *)&bt_aggregate3_kernel<0, 4> : (const void *)&bt_aggregate3_kernel<0, 2>;
+}
+hipError_t prepare_ingest_bt(size_t agg_lds) {
+  if (hipError_t e = hipFuncSetAttribute(bt_scatter2_fn(0), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)kBt2ScatterLds);
+      e != hipSuccess)
+    return e;
+  for (uint32_t v : {0u, kDiagBtAggWide})
+    if (hipError_t e = hipFuncSetAttribute(bt_agg_fn(v), hipFuncAttributeMaxDynamicSharedMemorySize, (int)agg_lds);
+        e != hipSuccess)
+      return e;
+  return hipSuccess;
+}
+#else
 hipError_t prepare_ingest_bt(size_t agg_lds) {
   for (uint32_t d : {0u, 1u, 2u, 3u, kDiagBtHotAcc, kDiagBtHotErr, kDiagBtSeqStore, kDiagBtNoStore, kDiagBtFlush2})
     if (hipError_t e = hipFuncSetAttribute(bt_scatter2_fn(d), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1063,8 +1091,13 @@ hipError_t prepare_ingest_bt(size_t agg_lds) {
   return hipSuccess;
 }
 
+#endif
+
 hipError_t launch_ingest_bt(const IngestParams &P, hipStream_t s) {
   void *args[] = {const_cast<IngestParams *>(&P)};
+#ifndef SPANAGG_AB
+  constexpr uint32_t kDiagBtNoScatter = 0, kDiagBtNoAgg = 0;
+#endif
   if (!(P.diag & kDiagBtNoScatter)) {
     if (hipError_t e = hipLaunchKernel(bt_scatter2_fn(P.diag), dim3(P.bt_grid), dim3(kBtBlock), args,
                                        kBt2ScatterLds, s);

@@ -31,10 +31,19 @@ constexpr size_t kLdsBudget = 144 * 1024;  // small-table path LDS ceiling per w
 constexpr uint64_t kSlabLimit = 1ULL << 31;  // per-workgroup spans between slab reductions
 // small path: ingest_v2_kernel variant 20 (19 LEAN: the span hash on 32-bit
 // halves and the wave-level (slot, bucket) dedup of the hot series' counter
-// adds); SPANAGG_VARIANT overrides
+// adds); SPANAGG_VARIANT overrides in the laboratory build
 constexpr int kDefaultVariant = 20;
 constexpr uint32_t kMaxSlabSets = 4;      // per-workgroup slab sets (small path)
-constexpr uint32_t kDefaultSlabSets = 2;  // SPANAGG_SLAB_SETS overrides
+constexpr uint32_t kDefaultSlabSets = 2;  // SPANAGG_SLAB_SETS overrides (laboratory build)
+
+// Laboratory knobs: the SPANAGG_AB build (`make ab` -> libspanagg_ab.so, used
+// by tools/ for A/B runs and ablations) reads them from the environment; the
+// product library reads no environment at all.
+#ifdef SPANAGG_AB
+const char *ab_env(const char *name) { return std::getenv(name); }
+#else
+constexpr const char *ab_env(const char *) { return nullptr; }
+#endif
 
 bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 uint32_t log2u(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
@@ -171,6 +180,10 @@ int validate_config(const sa_config *c, std::string &why) {
     return why = "n_windows * n_services * 2^hll_p must stay below 2^32 registers", SA_EINVAL;
   if (c->exp_max_size == 1 || c->exp_max_size > sa::kExpoMaxSize)
     return why = "exp_max_size must be 0 (explicit buckets) or 2..4096", SA_EINVAL;
+  if (c->options & ~SA_OPT_ALL) return why = "unknown bits in options", SA_EINVAL;
+#ifndef SPANAGG_AB
+  if (c->flags) return why = "SA_DIAG_* flags need the laboratory build (libspanagg_ab.so)", SA_EINVAL;
+#endif
   return SA_OK;
 }
 
@@ -351,12 +364,11 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   e->small = e->lds_bytes <= kLdsBudget && !e->expo;
   if (e->expo) {  // key mirror + 32-B header partials per slot (nw = 6 counter words)
     const size_t xl = (size_t)e->cap * 8 + (size_t)e->cap * 32 + sa::kLdsExtraBytes;
-    const char *xv = std::getenv("SPANAGG_EXPO_SMALL");  // 0: the HBM-table pass-1 path (A/B runs)
-    e->expo_small = xl <= kLdsBudget && !(xv && std::atoi(xv) == 0);
+    e->expo_small = xl <= kLdsBudget && !(cfg->options & SA_OPT_EXPO_HBM);
     if (e->expo_small) e->lds_bytes = xl;
   }
   e->variant = e->small ? kDefaultVariant : 0;
-  if (const char *v = std::getenv("SPANAGG_VARIANT"))  // tuning knob for A/B runs
+  if (const char *v = ab_env("SPANAGG_VARIANT"))
     e->variant = std::max(0, std::min((e->small ? sa::kNumLdsVariants : sa::kNumVariants) - 1,
                                       std::atoi(v)));
   if (e->small) {
@@ -376,10 +388,9 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     if (hipError_t st = sa::prepare_expo_count(sa::expo_count_lds_bytes(e->cap, cfg->exp_max_size)); st != hipSuccess)
       return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
     // slab counting: its workgroups (one per ingest workgroup) share a CU as the
-    // ingest ones do; SPANAGG_XC_SLAB=0 keeps the cached-probe kernel (A/B runs)
-    const char *sv = std::getenv("SPANAGG_XC_SLAB");
+    // ingest ones do; SA_OPT_EXPO_CACHED keeps the cached-probe kernel
     const size_t budget = (size_t)160 * 1024 * e->cus / e->G - 1024;
-    e->xc_ne = (sv && std::atoi(sv) == 0) ? 0u : sa::expo_slab_entries(e->cap, cfg->exp_max_size, budget);
+    e->xc_ne = (cfg->options & SA_OPT_EXPO_CACHED) ? 0u : sa::expo_slab_entries(e->cap, cfg->exp_max_size, budget);
     if (e->xc_ne)
       if (hipError_t st = sa::prepare_expo_slab(sa::expo_slab_lds_bytes(e->cap, cfg->exp_max_size, e->xc_ne));
           st != hipSuccess)
@@ -389,20 +400,18 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     e->spl = (uint32_t)sa::kVariants[e->variant].spl;
     e->G = e->cus * 8;
     // partitioned path unless the LDS counter row is too small for the
-    // buckets (SPANAGG_HBM_PART=0: per-span atomics, for A/B runs)
-    const char *pv = std::getenv("SPANAGG_HBM_PART");
-    e->part = e->nbk <= sa::kPartMaxBk && !(pv && std::atoi(pv) == 0) && !e->expo;
+    // buckets (SA_OPT_ATOMIC_TABLE: per-span atomics)
+    e->part = e->nbk <= sa::kPartMaxBk && !(cfg->options & SA_OPT_ATOMIC_TABLE) && !e->expo;
     if (e->part)
       if (hipError_t st = sa::prepare_ingest_part(); st != hipSuccess)
         return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
     // binned-table path where each bin's sub-table fits an aggregate
     // workgroup's LDS (256..2048 slots per bin: 2^19..2^22 table slots), the
     // window slot fits the record (<= 1024 windows) and buckets come from the
-    // bin table (SPANAGG_BINNED=0: the partitioned path, for A/B runs)
-    const char *bv = std::getenv("SPANAGG_BINNED");
+    // bin table (SA_OPT_PARTITIONED: the partitioned path)
     sa::BinEntry bins_probe[sa::kBins];  // the binned kernels bucket by the bin table
     e->bt = e->part && e->log2cap >= sa::kPartBinBits + 8 && e->log2cap <= sa::kPartBinBits + 11 &&
-            cfg->n_windows <= 1024 && build_bins(e, bins_probe) && !(bv && std::atoi(bv) == 0);
+            cfg->n_windows <= 1024 && build_bins(e, bins_probe) && !(cfg->options & SA_OPT_PARTITIONED);
   }
 
   const uint64_t S = cfg->n_services, W = cfg->n_windows;
@@ -425,12 +434,11 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     return bail(rc);
   {
     // bound sub-blocks: as small as kLbMinShift allows within kLbMaxSub of them
-    // (SPANAGG_HLL_LB=0 turns the filter off, for A/B runs)
+    // (SA_OPT_NO_HLL_FILTER turns the filter off)
     const uint64_t regs = W * S << cfg->hll_p;
     uint32_t sh = sa::kLbMinShift;
     while (sh < cfg->hll_p && (regs >> sh) > sa::kLbMaxSub) ++sh;
-    const char *lv = std::getenv("SPANAGG_HLL_LB");
-    if ((regs >> sh) <= sa::kLbMaxSub && sh <= cfg->hll_p && !(lv && std::atoi(lv) == 0)) {
+    if ((regs >> sh) <= sa::kLbMaxSub && sh <= cfg->hll_p && !(cfg->options & SA_OPT_NO_HLL_FILTER)) {
       e->lb_shift = sh;
       e->lb_n = (uint32_t)(regs >> sh);
       if ((rc = alloc((void **)&e->hll_lb, ((size_t)e->lb_n + 15) & ~(size_t)15))) return bail(rc);
@@ -455,7 +463,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
         return bail(rc);
     }
   }
-  if (std::getenv("SPANAGG_STAMPS") && (rc = alloc((void **)&e->dbg, (size_t)e->G * sa::kDbgPerWg * 8)))
+  if ((cfg->options & SA_OPT_STAMPS) && (rc = alloc((void **)&e->dbg, (size_t)e->G * sa::kDbgPerWg * 8)))
     return bail(rc);
   {
     sa::BinEntry bins[sa::kBins];
@@ -479,7 +487,8 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     // home slots), so bin occupancy does not depend on ids a sender chooses
     std::random_device rd;
     uint64_t r = ((uint64_t)rd() << 32) ^ rd();
-    if (const char *kv = std::getenv("SPANAGG_KMUL")) r = std::strtoull(kv, nullptr, 0);  // fixed, for A/B runs
+    if (cfg->options & SA_OPT_IDENTITY_IDS) r = 1;  // stored id = series id (tests of a full bin)
+    if (const char *kv = ab_env("SPANAGG_KMUL")) r = std::strtoull(kv, nullptr, 0);  // fixed, for A/B runs
     e->kmul = r | 1ULL;
     uint64_t x = e->kmul;  // Newton: x = x (2 - a x) doubles the correct low bits
     for (int i = 0; i < 6; ++i) x *= 2 - e->kmul * x;
@@ -489,7 +498,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     return bail(fail(e, SA_EDEVICE, "seed upload failed"));
   if (e->small) {
     e->nsets = kDefaultSlabSets;
-    if (const char *v = std::getenv("SPANAGG_SLAB_SETS"))  // tuning knob for A/B runs
+    if (const char *v = ab_env("SPANAGG_SLAB_SETS"))
       e->nsets = (uint32_t)std::max(1, std::min((int)kMaxSlabSets, std::atoi(v)));
     const size_t srow = (e->nbk + 1) & ~1u;  // slab row = 2 * ceil(nbk/2) u32 cells
     const size_t gs = (size_t)e->G * e->nsets;  // slabs of all sets, set-major
@@ -625,7 +634,7 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
   E.log2div = std::log2(E.div);
   {
     static const uint32_t diag = [] {
-      const char *v = std::getenv("SPANAGG_XC_DIAG");
+      const char *v = ab_env("SPANAGG_XC_DIAG");
       return v ? (uint32_t)std::strtoul(v, nullptr, 0) : 0u;
     }();
     E.diag = diag;

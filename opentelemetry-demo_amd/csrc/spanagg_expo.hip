@@ -600,8 +600,9 @@ hipError_t prepare_expo_count(size_t lds_bytes) {
                              (int)lds_bytes);
 }
 
-// slots per reduce block (SPANAGG_XR: 8 / 16 / 32 / 64, A/B runs)
+// 8 slots per reduce block (the laboratory build: SPANAGG_XR = 16 / 32 / 64)
 void launch_reduce_rescale(const ExpoParams &E, hipStream_t s) {
+#ifdef SPANAGG_AB
   static const uint32_t xr = [] {
     const char *v = std::getenv("SPANAGG_XR");
     const uint32_t x = v ? (uint32_t)std::atoi(v) : 8u;
@@ -612,6 +613,9 @@ void launch_reduce_rescale(const ExpoParams &E, hipStream_t s) {
   else if (xr == 16) hipLaunchKernelGGL(expo_reduce_rescale_kernel<16>, g, dim3(1024), 0, s, E);
   else if (xr == 32) hipLaunchKernelGGL(expo_reduce_rescale_kernel<32>, g, dim3(1024), 0, s, E);
   else hipLaunchKernelGGL(expo_reduce_rescale_kernel<64>, g, dim3(1024), 0, s, E);
+#else
+  hipLaunchKernelGGL(expo_reduce_rescale_kernel<8>, dim3((uint32_t)((E.cap + 7) / 8)), dim3(1024), 0, s, E);
+#endif
 }
 
 hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s) {

@@ -376,12 +376,12 @@ int sa_group_create(const sa_config *cfg, const int32_t *devices, uint32_t n, sa
     return SA_ENOMEM;
   }
   // RCCL over distinct devices (a communicator cannot hold two ranks of one
-  // device); a group of one uses it only when SPANAGG_GROUP_RCCL=1 asks
+  // device); SA_OPT_GROUP_COPY keeps the copy transport, and a group of one
+  // uses RCCL only when SA_OPT_GROUP_RCCL asks
   std::vector<int> sorted(g->dev);
   std::sort(sorted.begin(), sorted.end());
   const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
-  const char *rv = std::getenv("SPANAGG_GROUP_RCCL");
-  const bool want = rv ? std::atoi(rv) != 0 : n > 1;
+  const bool want = !(cfg->options & SA_OPT_GROUP_COPY) && (n > 1 || (cfg->options & SA_OPT_GROUP_RCCL));
   if (distinct && want) {
     g->comm.resize(n);
     if (ncclCommInitAll(g->comm.data(), (int)n, g->dev.data()) == ncclSuccess) {

@@ -1649,8 +1649,21 @@ uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap_blocks) {
   return (uint32_t)g;
 }
 
-// Small-table kernels: bin-table bucketing in four (spans/lane, prefetch)
-// variants, the linear-threshold fallback, and the diagnostic build.
+// Small-table kernels.  Product build: the v2 kernel specialised for the
+// default geometry (variant 20: 2,048 slots, 17 buckets, HLL p 14, LEAN), the
+// generic v2 kernel (variant 15) for any other geometry with a bucket bin
+// table, and the linear-threshold kernel for bounds no bin table can hold.
+// The laboratory build (SPANAGG_AB) keeps every variant and the diagnostic
+// (ablation) kernels.
+#ifndef SPANAGG_AB
+static const void *small_fn(bool bt, int v, bool diag) {
+  (void)diag;
+  if (!bt) return (const void *)&ingest_lds_kernel<0, 4, true, false>;
+  if (v == 20) return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1, true, true>;
+  return (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true>;
+}
+constexpr int kSmallFnVariants[] = {15, 20};
+#else
 static const void *small_fn(bool bt, int v, bool diag) {
   if (bt && v >= 8) {  // v2 kernels (bin-table bucketing only)
     if (diag)
@@ -1686,20 +1699,34 @@ static const void *small_fn(bool bt, int v, bool diag) {
     default: return (const void *)&ingest_lds_kernel<1, 4, true, false>;
   }
 }
+#endif
 
 template <int NB>
 static void launch_hbm_nb(const IngestParams &P, uint32_t grid, hipStream_t s, int v) {
+#ifndef SPANAGG_AB
+  (void)v;
+  hipLaunchKernelGGL((ingest_hbm_kernel<NB, 4, false, 256>), dim3(grid), dim3(256), 0, s, P);
+#else
   switch (v) {
     case 1: hipLaunchKernelGGL((ingest_hbm_kernel<NB, 2, true, 256>), dim3(grid), dim3(256), 0, s, P); break;
     case 2: hipLaunchKernelGGL((ingest_hbm_kernel<NB, 4, true, 256>), dim3(grid), dim3(256), 0, s, P); break;
     case 3: hipLaunchKernelGGL((ingest_hbm_kernel<NB, 2, false, 256>), dim3(grid), dim3(256), 0, s, P); break;
     default: hipLaunchKernelGGL((ingest_hbm_kernel<NB, 4, false, 256>), dim3(grid), dim3(256), 0, s, P); break;
   }
+#endif
 }
 
 }  // namespace
 
 hipError_t prepare_ingest_small(size_t lds_bytes) {
+#ifndef SPANAGG_AB
+  for (int bt = 0; bt < 2; ++bt)
+    for (int v : kSmallFnVariants) {
+      hipError_t e = hipFuncSetAttribute(small_fn(bt, v, false), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)lds_bytes);
+      if (e != hipSuccess) return e;
+    }
+#else
   for (int bt = 0; bt < 2; ++bt)
     for (int v = 0; v < kNumLdsVariants; ++v)
       for (int d = 0; d < 2; ++d) {
@@ -1707,6 +1734,7 @@ hipError_t prepare_ingest_small(size_t lds_bytes) {
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
         if (e != hipSuccess) return e;
       }
+#endif
   return hipSuccess;
 }
 
@@ -1716,10 +1744,9 @@ hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_
   if ((variant == 12 || variant == 13 || variant >= 14) &&
       !(P.log2cap == 11 && (P.nbk + 1) / 2 == 9 && P.p == 14))
     variant = variant == 12 ? 8 : variant == 13 ? 11 : 15;
-  // the lean window quotient needs window_ns < 2^56 (its high word is a 24-bit multiplier)
-  if (variant == 20 && (P.window_ns >> 56)) variant = 19;
-  // (SPANAGG_STAMPS engines keep the production v2 kernels: their workgroup
-  // and wave-end stamps are written whenever P.dbg is set)
+  // (the lean window quotient of variant 20 needs window_ns < 2^56, which
+  // sa_create enforces; SA_OPT_STAMPS engines keep the production v2 kernels:
+  // their workgroup and wave-end stamps are written whenever P.dbg is set)
   const void *fn = small_fn(P.bintab != nullptr, variant, P.diag != 0 || (P.dbg != nullptr && variant < 8));
   void *args[] = {const_cast<IngestParams *>(&P)};
   return hipLaunchKernel(fn, dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);
@@ -1739,18 +1766,28 @@ hipError_t launch_ingest_expo_small(const IngestParams &P, uint32_t grid, size_t
 }
 
 hipError_t launch_ingest_part(const IngestParams &P, hipStream_t s) {
+#ifdef SPANAGG_AB
   static const uint32_t max_grid = [] {
-    const char *v = std::getenv("SPANAGG_PART_GRID");  // tuning knob for A/B runs
+    const char *v = std::getenv("SPANAGG_PART_GRID");  // laboratory knob
     return v ? (uint32_t)std::max(1, std::atoi(v)) : 256u;
   }();
-  const uint32_t grid = (uint32_t)std::min<uint64_t>(max_grid, (P.n + kPartBlock - 1) / kPartBlock);
   static const bool stage = [] {
-    const char *v = std::getenv("SPANAGG_PART_STAGE");  // tuning knob for A/B runs
+    const char *v = std::getenv("SPANAGG_PART_STAGE");  // laboratory knob
     return !(v && std::atoi(v) == 0);
   }();
+#else
+  constexpr uint32_t max_grid = 256u;
+  constexpr bool stage = true;
+#endif
+  const uint32_t grid = (uint32_t)std::min<uint64_t>(max_grid, (P.n + kPartBlock - 1) / kPartBlock);
   const bool b16 = P.nneg == 0 && P.npos == 16;
+#ifdef SPANAGG_AB
   const void *fn = stage ? (b16 ? (const void *)&part_scatter_kernel<16, true> : (const void *)&part_scatter_kernel<-1, true>)
                          : (b16 ? (const void *)&part_scatter_kernel<16, false> : (const void *)&part_scatter_kernel<-1, false>);
+#else
+  (void)stage;
+  const void *fn = b16 ? (const void *)&part_scatter_kernel<16, true> : (const void *)&part_scatter_kernel<-1, true>;
+#endif
   void *args[] = {const_cast<IngestParams *>(&P)};
   if (hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(kPartBlock), args, kPartScatterLds, s); e != hipSuccess)
     return e;
@@ -1760,8 +1797,12 @@ hipError_t launch_ingest_part(const IngestParams &P, hipStream_t s) {
 }
 
 hipError_t prepare_ingest_part() {
+#ifdef SPANAGG_AB
   for (const void *fn : {(const void *)&part_scatter_kernel<16, true>, (const void *)&part_scatter_kernel<-1, true>,
                          (const void *)&part_scatter_kernel<16, false>, (const void *)&part_scatter_kernel<-1, false>})
+#else
+  for (const void *fn : {(const void *)&part_scatter_kernel<16, true>, (const void *)&part_scatter_kernel<-1, true>})
+#endif
     if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kPartScatterLds);
         e != hipSuccess)
       return e;

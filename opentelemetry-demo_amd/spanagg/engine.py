@@ -53,8 +53,9 @@ class Config:
     n_services: int = 64
     key_capacity: int = 1000
     device: int = 0
-    flags: int = 0  # SA_DIAG_* profiling ablations only (results are wrong when set)
+    flags: int = 0  # SA_DIAG_* profiling ablations only (laboratory build; results are wrong when set)
     exp_max_size: int = 0  # histogram.exponential.max_size (0: explicit buckets)
+    options: int = 0  # SA_OPT_* path options (spanagg._lib.OPT_*): same results, another kernel path
 
     def to_c(self):
         arr = (C.c_double * max(1, len(self.bounds)))(*[float(b) for b in self.bounds])
@@ -65,7 +66,7 @@ class Config:
         c.hll_p, c.cms_d, c.cms_w = self.hll_p, self.cms_d, self.cms_w
         c.window_ns, c.n_windows, c.n_services = self.window_ns, self.n_windows, self.n_services
         c.key_capacity, c.device, c.flags = self.key_capacity, self.device, self.flags
-        c.exp_max_size = self.exp_max_size
+        c.exp_max_size, c.options = self.exp_max_size, self.options
         return c, arr
 
 

@@ -31,7 +31,31 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert _lib.load().sa_abi_version() == 3
+    assert _lib.load().sa_abi_version() == 4
+
+
+def test_product_library_has_no_laboratory():
+    """Verdict r3: the product libspanagg.so reads no environment (no getenv
+    import at all) and carries one kernel per path; the A/B variants and the
+    ablation kernels live in the laboratory build (libspanagg_ab.so, tools/)."""
+    import subprocess
+    so = os.path.join(os.path.dirname(_lib.__file__), "libspanagg.so")
+    dyn = subprocess.run(["nm", "-D", "--undefined-only", so], capture_output=True, text=True, check=True).stdout
+    assert "getenv" not in dyn
+    strings = subprocess.run(["strings", so], capture_output=True, text=True, check=True).stdout
+    for lab in ("bt_aggregate2_kernel", "ingest_lds_kernelILi1E", "SPANAGG_VARIANT", "SPANAGG_BT_AGG"):
+        assert lab not in strings, lab
+
+
+def test_diagnostic_flags_rejected_by_product_library():
+    """SA_DIAG_* ablations need the laboratory build: the product library
+    refuses them (before touching a device) instead of running wrong kernels."""
+    with pytest.raises(_lib.SpanAggError) as ei:
+        Engine(Config(flags=1))
+    assert ei.value.code == _lib.SA_EINVAL
+    with pytest.raises(_lib.SpanAggError) as ei:
+        Engine(Config(options=1 << 20))  # unknown option bit
+    assert ei.value.code == _lib.SA_EINVAL
 
 
 def test_config_default_matches_connector_defaults():

@@ -12,6 +12,7 @@ import pytest
 
 import pyoracle
 from parity_util import assert_red_equal
+from spanagg._lib import OPT_IDENTITY_IDS, OPT_PARTITIONED
 from spanagg import Config, Engine, SpanBatch
 from spanagg.synth import generate_highcard
 
@@ -61,15 +62,14 @@ def test_c4zipf_full_size_bit_exact():
 
 
 @pytest.mark.parametrize("zipf", [0.0, 1.3])
-def test_binned_matches_partitioned_path(zipf, monkeypatch):
+def test_binned_matches_partitioned_path(zipf):
     """Same input through the binned path and the round-1 partitioned path
-    (SPANAGG_BINNED=0), two ingests each: both equal the oracle."""
+    (SA_OPT_PARTITIONED), two ingests each: both equal the oracle."""
     batch, _, w0 = generate_highcard(3_000_000, seed=13, routes=1000, pods=300, zipf_s=zipf)
     half = len(batch) // 2
     o = _oracle(batch)
-    for binned in ("1", "0"):
-        monkeypatch.setenv("SPANAGG_BINNED", binned)
-        with _engine(600_000) as e:
+    for opt in (0, OPT_PARTITIONED):
+        with _engine(600_000, options=opt) as e:
             e.window_advance(w0)
             e.ingest(batch.slice(0, half))
             e.ingest(batch.slice(half, len(batch)))
@@ -96,12 +96,11 @@ def test_binned_u8_rows_spill():
         assert e.stats()["dropped_table_full"] == 0
 
 
-def test_binned_full_bin_reports_drops(monkeypatch):
-    """With the identity id map (SPANAGG_KMUL=1) 1,000 keys that share their
+def test_binned_full_bin_reports_drops():
+    """With the identity id map (SA_OPT_IDENTITY_IDS) 1,000 keys that share their
     top 11 bits all land in one bin of 256 slots: the bin fills, the spans of
     the keys that found no slot are dropped and reported, every kept series
     is exact (a key is kept or dropped as a whole: slots never empty)."""
-    monkeypatch.setenv("SPANAGG_KMUL", "1")
     n = 200_000
     batch, _, w0 = generate_highcard(n, seed=19, routes=100, pods=100)
     rng = np.random.Generator(np.random.PCG64(19))
@@ -111,7 +110,7 @@ def test_binned_full_bin_reports_drops(monkeypatch):
     keys = (np.uint64(0x155) << np.uint64(53)) | (low >> np.uint64(11)) | np.uint64(1)
     one_bin = SpanBatch(keys, *batch.columns()[1:])
     ref = _oracle(one_bin).series()
-    with _engine(400_000) as e:  # cap 2^19: 2,048 bins of 256 slots
+    with _engine(400_000, options=OPT_IDENTITY_IDS) as e:  # cap 2^19: 2,048 bins of 256 slots
         e.window_advance(w0)
         e.ingest(one_bin)
         res = e.flush(allow_drops=True)

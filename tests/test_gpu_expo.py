@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 import pyoracle
+from spanagg._lib import OPT_EXPO_CACHED, OPT_EXPO_HBM
 from spanagg import Config, Engine, SpanBatch, pack_meta
 from spanagg import _lib
 from spanagg.synth import generate_c2
@@ -101,15 +102,14 @@ def test_fast_index_agrees_with_exact_path(unit):
 
 @pytest.mark.parametrize("path", ["small", "small_cached", "hbm"])
 @pytest.mark.parametrize("max_size,unit", [(160, "ms"), (8, "ms"), (20, "s"), (2, "ms")])
-def test_expo_histograms_match_oracle(max_size, unit, path, monkeypatch):
+def test_expo_histograms_match_oracle(max_size, unit, path):
     """small: the small-table kernel in EXPO mode (LDS header partials, slab
     reduce, LDS slab counts for the selected series); small_cached: the same
-    with the cached-probe counting kernel (SPANAGG_XC_SLAB=0); hbm: the
-    pass-1 global-atomic path."""
-    monkeypatch.setenv("SPANAGG_EXPO_SMALL", "0" if path == "hbm" else "1")
-    monkeypatch.setenv("SPANAGG_XC_SLAB", "0" if path == "small_cached" else "1")
+    with the cached-probe counting kernel (SA_OPT_EXPO_CACHED); hbm: the
+    pass-1 global-atomic path (SA_OPT_EXPO_HBM)."""
+    opt = {"small": 0, "small_cached": OPT_EXPO_CACHED, "hbm": OPT_EXPO_HBM}[path]
     wl = generate_c2(200_003, seed=13)
-    with _engine(wl, exp_max_size=max_size, unit=unit) as e:
+    with _engine(wl, exp_max_size=max_size, unit=unit, options=opt) as e:
         assert e.stats()["small_table"] == (0 if path == "hbm" else 1)
         e.ingest(wl.batch)
         res = e.flush_exp()
@@ -169,11 +169,10 @@ def test_expo_edges_zero_pow2_and_huge():
 
 
 @pytest.mark.parametrize("path", ["small", "hbm"])
-def test_expo_huge_durations(path, monkeypatch):
+def test_expo_huge_durations(path):
     """Durations around 2^52 ns and up to 9e17 ns (weeks to decades) on both
     table paths: the fast log2 index path, the exact Go math.Log path and the
     rescale by shifted scale-20 indices all agree with the oracle."""
-    monkeypatch.setenv("SPANAGG_EXPO_SMALL", "1" if path == "small" else "0")
     ds = [2**52 - 3, 2**52 - 2, 2**52 - 1, 2**52, 2**52 + 1, 3 * 2**52, 9 * 10**17, 5_000_000, 2**40, 1]
     n = len(ds)
     end = np.full(n, 10**18, dtype=np.uint64)
@@ -181,7 +180,8 @@ def test_expo_huge_durations(path, monkeypatch):
     batch = SpanBatch(np.array([11, 22] * (n // 2), dtype=np.uint64), start, end,
                       np.arange(n, dtype=np.uint64), np.arange(n, dtype=np.uint64), pack_meta([0] * n, 2, 0))
     for max_size in (4, 160):
-        with Engine(Config(n_services=1, n_windows=16, exp_max_size=max_size)) as e:
+        with Engine(Config(n_services=1, n_windows=16, exp_max_size=max_size,
+                           options=0 if path == "small" else OPT_EXPO_HBM)) as e:
             assert e.stats()["small_table"] == (1 if path == "small" else 0)
             e.window_advance(10**18 // 10**10)
             e.ingest(batch)

@@ -9,6 +9,7 @@ import pytest
 
 import pyoracle
 from parity_util import assert_red_equal, assert_red_golden, sketch_sparse
+from spanagg._lib import OPT_ATOMIC_TABLE, OPT_PARTITIONED
 from spanagg import Config, Engine, SpanBatch, pack_meta
 from spanagg import _lib
 from spanagg.synth import generate_c2, generate_highcard
@@ -350,12 +351,13 @@ def test_high_cardinality_hbm_table_vs_oracle():
 
 
 @pytest.mark.parametrize("shape", ["zipf_bins_spill", "lds_tables_spill"])
-def test_partitioned_hbm_path_spills_vs_oracle(shape, monkeypatch):
+def test_partitioned_hbm_path_spills_vs_oracle(shape):
     """The partitioned HBM-table path (part_scatter + part_aggregate) where it
     falls back to the direct path: a Zipf key mix overfills the hot keys' bins,
     and ~2.9 M distinct keys (~1,400 per bin) overfill the 1,024-slot LDS
     tables.  Two ingests (two launches, bin counters reset between) and the
-    per-span atomic path (SPANAGG_HBM_PART=0) on the same input must agree."""
+    per-span atomic path (SA_OPT_ATOMIC_TABLE) on the same input must agree.
+    (SA_OPT_PARTITIONED keeps tables the binned path would take on this one.)"""
     if shape == "zipf_bins_spill":
         batch, _, w0 = generate_highcard(2_000_000, seed=3, routes=400, pods=250, zipf_s=1.2)
         kcap = 200_000
@@ -364,9 +366,8 @@ def test_partitioned_hbm_path_spills_vs_oracle(shape, monkeypatch):
         kcap = 3_500_000
     half = len(batch) // 2 // 16 * 16
     results = []
-    for part in ("1", "0"):
-        monkeypatch.setenv("SPANAGG_HBM_PART", part)
-        with Engine(Config(n_services=1, n_windows=16, key_capacity=kcap)) as e:
+    for opt in (OPT_PARTITIONED, OPT_ATOMIC_TABLE):
+        with Engine(Config(n_services=1, n_windows=16, key_capacity=kcap, options=opt)) as e:
             assert e.stats()["small_table"] == 0
             e.window_advance(w0)
             e.ingest(batch.slice(0, half))

@@ -11,6 +11,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "opentelemetry-demo_amd"))
+# the laboratory build (variants, ablation flags): make -C opentelemetry-demo_amd ab
+os.environ.setdefault("SPANAGG_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "opentelemetry-demo_amd", "spanagg", "libspanagg_ab.so"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

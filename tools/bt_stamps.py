@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
 """Per-workgroup timeline of the binned C4 kernels (bt_scatter2_kernel,
-bt_aggregate3_kernel, or bt_aggregate2_kernel with SPANAGG_BT_AGG=2) from in-kernel s_memrealtime stamps (SPANAGG_STAMPS=1
+bt_aggregate3_kernel, or bt_aggregate2_kernel with SPANAGG_BT_AGG=2) from in-kernel s_memrealtime stamps (SA_OPT_STAMPS
 diagnostic engines).  Prints phase durations (us) over workgroups."""
 import ctypes as C
 import json
 import os
 import sys
 
-os.environ["SPANAGG_STAMPS"] = "1"
+# the laboratory build (variants, ablation flags): make -C opentelemetry-demo_amd ab
+os.environ.setdefault("SPANAGG_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "opentelemetry-demo_amd", "spanagg", "libspanagg_ab.so"))
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "opentelemetry-demo_amd"))
 
@@ -31,7 +33,7 @@ def main():
     cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).cuda()
             for c in batch.columns()]
     s = torch.cuda.Stream()
-    with Engine(Config(n_services=1, n_windows=16, key_capacity=1_200_000)) as e:
+    with Engine(Config(n_services=1, n_windows=16, key_capacity=1_200_000, options=_lib.OPT_STAMPS)) as e:
         e.window_advance(first)
         for _ in range(4):
             e.ingest_device(*cols, n=n, stream=s.cuda_stream)

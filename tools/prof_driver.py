@@ -10,6 +10,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "opentelemetry-demo_amd"))
 sys.path.insert(0, ROOT)
+flags = int(os.environ.get("PROF_FLAGS", 0))
+if flags or os.environ.get("SPANAGG_VARIANT"):  # ablations and variants: the laboratory build
+    os.environ.setdefault("SPANAGG_LIB", os.path.join(ROOT, "opentelemetry-demo_amd", "spanagg", "libspanagg_ab.so"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -33,7 +36,6 @@ cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np
         for c in batch.columns()]
 s = torch.cuda.Stream()
 s.wait_stream(torch.cuda.current_stream())
-flags = int(os.environ.get("PROF_FLAGS", 0))
 if os.environ.get("PROF_FRESH", "1") != "0":
     from bench import trace_variants
     variants = trace_variants(cols[3], cols[4], reps, seed=1000)

@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """Per-workgroup timeline of the small-table ingest kernel from in-kernel
-s_memrealtime stamps (diagnostic build path, SPANAGG_STAMPS=1)."""
+s_memrealtime stamps (diagnostic build path, SA_OPT_STAMPS)."""
 import ctypes as C
 import json
 import os
 import sys
 
-os.environ["SPANAGG_STAMPS"] = "1"
+# the laboratory build (variants, ablation flags): make -C opentelemetry-demo_amd ab
+os.environ.setdefault("SPANAGG_LIB", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "opentelemetry-demo_amd", "spanagg", "libspanagg_ab.so"))
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "opentelemetry-demo_amd"))
 
@@ -58,7 +60,7 @@ def main():
                      if x[0] in os.environ.get("STAMP_SETS", "full,loads_only,no_sketch").split(",")]:
         for v in [int(x) for x in os.environ.get("STAMP_VARS", "0,8").split(",")]:
             os.environ["SPANAGG_VARIANT"] = str(v)
-            with Engine(Config(n_services=wl.n_services, n_windows=16, flags=fl)) as e:
+            with Engine(Config(n_services=wl.n_services, n_windows=16, flags=fl, options=_lib.OPT_STAMPS)) as e:
                 e.window_advance(wl.first_window)
                 for i in range(int(os.environ.get("STAMP_LAUNCHES", "24"))):
                     # a fresh trace-id variant per launch (as bench.py), so HLL raises do not idle

@@ -27,6 +27,14 @@ def main():
         short = name[name.index(h):].split("(")[0]
         d[short].append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
     out = {}
+    # launch period: the first hot kernel of each launch (the one with the most
+    # dispatches that starts earliest) -> start-to-start over the last LAST
+    # launches, and their span / count (with overlapping kernels of
+    # consecutive launches the period, not the sum of durations, is the rate)
+    first = min(d, key=lambda k: (-len(d[k]), min(t for t, _ in d[k])))
+    starts = sorted(t for t, _ in d[first])[-(last + 1):]
+    if len(starts) > 1:
+        out["launch_period_us_last%d" % last] = round((starts[-1] - starts[0]) / 1e3 / (len(starts) - 1), 2)
     for k, v in d.items():
         v.sort()
         us = [x for _, x in v]
