@@ -449,21 +449,29 @@ def kernel_ms_filter_off(n, args, device):
 def run_group(n, members, args, device):
     """--group N: N engines of one group on this one device, fed through
     sa_group_ingest_device (the partition kernel shards each batch by trace id
-    into the members' buffers).  Measures the group's overhead on one GPU
-    (partition + N smaller launches), not multi-GPU scaling."""
+    into the members' buffers), then one group flush (device key union, dense
+    rows summed on the device).  Measures the group's overhead on one GPU
+    (partition + N smaller launches) and the flush at the workload's
+    cardinality (--workload c4: ~1 M series, every member holding most of
+    them), not multi-GPU scaling."""
     import numpy as np
     import torch
 
     from spanagg import Config, Group
-    from spanagg.synth import generate_c2
+    from spanagg.synth import generate_c2, generate_highcard
 
-    wl = generate_c2(n, seed=42)
+    if args.workload in ("c4", "c4zipf"):
+        batch, _, first = generate_highcard(n, seed=7, zipf_s=1.1 if args.workload == "c4zipf" else 0.0)
+        n_services, kcap = 1, 1_200_000
+    else:
+        wl = generate_c2(n, seed=42)
+        batch, first, n_services, kcap = wl.batch, wl.first_window, wl.n_services, 1500
     cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(device)
-            for c in wl.batch.columns()]
+            for c in batch.columns()]
     k = args.warmup + args.steps
     variants = trace_variants(cols[3], cols[4], n_variants(args, k, device), seed=1000)
-    g = Group([device.index] * members, Config(n_services=wl.n_services, n_windows=16, key_capacity=1500))
-    g.window_advance(wl.first_window)
+    g = Group([device.index] * members, Config(n_services=n_services, n_windows=16, key_capacity=kcap))
+    g.window_advance(first)
     s = torch.cuda.current_stream(device)
     for i in range(args.warmup):
         w0, w1 = variants[i % len(variants)]
@@ -477,13 +485,18 @@ def run_group(n, members, args, device):
     g.sync()
     torch.cuda.synchronize(device)
     el = time.perf_counter() - t0
-    calls = int(g.flush().calls.sum())
+    tf = time.perf_counter()
+    red = g.flush()
+    flush_ms = (time.perf_counter() - tf) * 1e3
+    calls = int(red.calls.sum())
     st = g.stats()
     g.close()
-    return {"members": members, "value": n * args.steps / el, "unit": "spans/s", "ms_per_step": el * 1e3 / args.steps,
+    return {"members": members, "workload": args.workload, "value": n * args.steps / el, "unit": "spans/s",
+            "ms_per_step": el * 1e3 / args.steps, "flush_ms": flush_ms, "flush_series": len(red.key_hash),
             "calls_check": calls == n * k - st["zero_key"],
             "note": f"{members} engines of one group on this device, sa_group_ingest_device of {n:,}-span "
-                    "device batches (partition kernel + one launch per member); overhead on one GPU, not scaling"}
+                    "device batches (partition kernel + one launch per member); flush_ms: one sa_group_flush "
+                    "(device key union, dense rows summed on the device); overhead on one GPU, not scaling"}
 
 
 def roofline(name, n, r, traffic_path=None):

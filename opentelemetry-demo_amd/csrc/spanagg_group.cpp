@@ -12,9 +12,12 @@
 // bits as one engine fed the whole stream.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_select.hpp>
 
 #include <algorithm>
 #include <map>
+#include <memory>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -44,6 +47,41 @@ __global__ void max_slices_u8(uint8_t *dst, const uint8_t *src, uint32_t n, uint
 
 uint32_t grid_for(uint64_t len) { return (uint32_t)std::min<uint64_t>((len + 255) / 256, 4096); }
 
+constexpr uint32_t kMaxMembers = 64;
+
+// Sum of members' dense rows that live on one device: dst[i] = sum_k src[k][i]
+// straight from each member's buffer (no stacking copy).
+struct SrcPtrs {
+  const unsigned long long *p[kMaxMembers];
+};
+__global__ void sum_ptrs_u64(unsigned long long *dst, SrcPtrs src, uint32_t n, uint64_t len) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < len; i += (uint64_t)gridDim.x * blockDim.x) {
+    unsigned long long acc = 0;
+    for (uint32_t k = 0; k < n; ++k) acc += src.p[k][i];
+    dst[i] = acc;
+  }
+}
+
+// The merged dense rows [nu][nbk + 1] (bucket counts, ns sum) -> the result's
+// columns on the device: counts [nu][nbk], calls = sum of counts (A8),
+// sum_ns, and sum = sum_ns / div (IEEE division, as the host's).
+__global__ void finalize_rows_kernel(const unsigned long long *rows, uint64_t nu, uint32_t nbk,
+                                     unsigned long long *counts, unsigned long long *calls,
+                                     unsigned long long *sum_ns, double *sum, double div) {
+  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < nu; r += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long *row = rows + r * (nbk + 1);
+    unsigned long long c = 0;
+    for (uint32_t b = 0; b < nbk; ++b) {
+      const unsigned long long v = row[b];
+      counts[r * nbk + b] = v;
+      c += v;
+    }
+    calls[r] = c;
+    sum_ns[r] = row[nbk];
+    sum[r] = (double)row[nbk] / div;
+  }
+}
+
 // ---- trace-id sharding (engine = trace_w1 % n) ------------------------------
 // trace_w1 % n from 32-bit remainders: w1 = hi * 2^32 + lo, so
 // w1 % n = ((hi % n) * (2^32 % n) + lo % n) % n (< n^2 <= 4096 before the
@@ -51,8 +89,6 @@ uint32_t grid_for(uint64_t len) { return (uint32_t)std::min<uint64_t>((len + 255
 __host__ __device__ inline uint32_t shard_of(uint64_t w1, uint32_t n, uint32_t r32) {
   return (((uint32_t)(w1 >> 32) % n) * r32 + (uint32_t)w1 % n) % n;
 }
-
-constexpr uint32_t kMaxMembers = 64;
 
 // Spans per shard of a device batch: LDS counters per workgroup, written to
 // blk[workgroup][shard], plus one global atomic per shard per workgroup for
@@ -173,6 +209,8 @@ struct sa_group {
   bool rccl = false;
   std::vector<ncclComm_t> comm;
   std::vector<Buf> keys, gath, uni, rows, hll, cms;
+  std::vector<Buf> srt, sort_tmp, ucnt;  // device key union: sorted keys, rocPRIM scratch, unique count
+  Buf fin;                               // member 0's device: the result's columns (finalize_rows_kernel)
   Buf stack;  // member 0's device: every member's slice for the copy-path reduce
   // sa_group_ingest_device: two staging sets (a call waits only for the
   // members' use of the set two calls back).  part[k][i]: set k's packed
@@ -265,6 +303,45 @@ int copy_reduce(sa_group *g, std::vector<Buf> &bufs, uint64_t len, bool max_u8) 
   return SA_OK;
 }
 
+// The sorted union of `n_in` series ids in `in` (member i's device, stream
+// st[i]; ids may repeat, 0 = padding): rocPRIM radix sort, then unique, into
+// uni[i]; *first = 1 when the union's first id is the padding 0 (skipped by
+// the caller), *nu = distinct ids including it.  Asynchronous: the counts
+// land in ucnt[i] (device) and are read by union_count.
+int device_union(sa_group *g, uint32_t i, const uint64_t *in, uint64_t n_in) {
+  const int dev = g->dev[i];
+  hipStream_t s = g->st[i];
+  if (int rc = ensure(g, dev, g->srt[i], std::max<uint64_t>(1, n_in) * 8)) return rc;
+  if (int rc = ensure(g, dev, g->uni[i], std::max<uint64_t>(1, n_in) * 8)) return rc;
+  if (int rc = ensure(g, dev, g->ucnt[i], 64)) return rc;
+  SG_HIP(g, hipSetDevice(dev));
+  auto *srt = static_cast<uint64_t *>(g->srt[i].p), *uni = static_cast<uint64_t *>(g->uni[i].p);
+  auto *cnt = static_cast<uint64_t *>(g->ucnt[i].p);
+  size_t tb_sort = 0, tb_uniq = 0;
+  SG_HIP(g, rocprim::radix_sort_keys(nullptr, tb_sort, in, srt, (size_t)n_in, 0, 64, s));
+  SG_HIP(g, rocprim::unique(nullptr, tb_uniq, srt, uni, cnt, (size_t)n_in, rocprim::equal_to<uint64_t>(), s));
+  if (int rc = ensure(g, dev, g->sort_tmp[i], std::max<size_t>({tb_sort, tb_uniq, (size_t)256}))) return rc;
+  size_t tb = g->sort_tmp[i].bytes;
+  SG_HIP(g, rocprim::radix_sort_keys(g->sort_tmp[i].p, tb, in, srt, (size_t)n_in, 0, 64, s));
+  tb = g->sort_tmp[i].bytes;
+  SG_HIP(g, rocprim::unique(g->sort_tmp[i].p, tb, srt, uni, cnt, (size_t)n_in, rocprim::equal_to<uint64_t>(), s));
+  // the first id (0 when padding or the reserved id sorted first) next to the count
+  SG_HIP(g, hipMemcpyAsync(cnt + 1, uni, 8, hipMemcpyDeviceToDevice, s));
+  return SA_OK;
+}
+
+// Reads member i's union size (waits for its stream): distinct non-zero ids
+// and whether the union starts with the padding 0.
+int union_count(sa_group *g, uint32_t i, uint64_t *nu, bool *skip0) {
+  uint64_t h[2] = {0, 0};
+  SG_HIP(g, hipSetDevice(g->dev[i]));
+  SG_HIP(g, hipMemcpyAsync(h, g->ucnt[i].p, 16, hipMemcpyDeviceToHost, g->st[i]));
+  SG_HIP(g, hipStreamSynchronize(g->st[i]));
+  *skip0 = h[0] > 0 && h[1] == 0;
+  *nu = h[0] - (*skip0 ? 1 : 0);
+  return SA_OK;
+}
+
 // One series' exponential histogram while members' deltas are folded in.
 struct ExpoAcc {
   uint64_t count = 0, zero = 0, sum_ns = 0;
@@ -350,6 +427,9 @@ int sa_group_create(const sa_config *cfg, const int32_t *devices, uint32_t n, sa
     g->st.push_back(s);
   }
   g->keys.resize(n);
+  g->srt.resize(n);
+  g->sort_tmp.resize(n);
+  g->ucnt.resize(n);
   g->gath.resize(n);
   g->uni.resize(n);
   g->rows.resize(n);
@@ -405,7 +485,8 @@ void sa_group_destroy(sa_group *g) {
       (void)hipStreamSynchronize(g->st[i]);
       (void)hipStreamDestroy(g->st[i]);
     }
-    for (std::vector<Buf> *v : {&g->keys, &g->gath, &g->uni, &g->rows, &g->hll, &g->cms})
+    for (std::vector<Buf> *v : {&g->keys, &g->gath, &g->uni, &g->rows, &g->hll, &g->cms, &g->srt, &g->sort_tmp,
+                                &g->ucnt})
       if (i < v->size() && (*v)[i].p) (void)hipFree((*v)[i].p);
     for (size_t k = 0; k < 2; ++k)
       if (k * g->eng.size() + i < g->pcnt.size() && g->pcnt[k * g->eng.size() + i].p)
@@ -417,6 +498,7 @@ void sa_group_destroy(sa_group *g) {
       if (g->ev_done[k][i]) (void)hipEventDestroy(g->ev_done[k][i]);
     }
     if (i == 0 && g->stack.p) (void)hipFree(g->stack.p);
+    if (i == 0 && g->fin.p) (void)hipFree(g->fin.p);
     sa_destroy(g->eng[i]);
   }
   if (g->hcnt) (void)hipHostFree(g->hcnt);
@@ -611,11 +693,16 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
     if (int rc = sa_export_keys(g->eng[i], static_cast<uint64_t *>(g->keys[i].p), s.table_capacity, &cnt[i], g->st[i]))
       return member_error(g, i, rc, "sa_export_keys");
   }
-  // 2. the sorted key union (the dense index every member densifies against)
-  std::vector<uint64_t> all;
-  if (g->rccl) {
-    const uint64_t nmax = *std::max_element(cnt.begin(), cnt.end());
-    if (nmax) {
+  // 2. the sorted key union (the dense index every member densifies against),
+  //    built on the devices: RCCL gathers every member's list onto every
+  //    member, and each sorts / uniques its copy (identical bits everywhere,
+  //    no broadcast); the copy transport gathers the lists onto member 0's
+  //    device, builds the union there and copies it to the others.
+  const uint64_t nmax = *std::max_element(cnt.begin(), cnt.end());
+  uint64_t nu = 0;
+  bool skip0 = false;
+  if (nmax) {
+    if (g->rccl) {
       for (uint32_t i = 0; i < n; ++i) {
         SG_HIP(g, hipSetDevice(g->dev[i]));
         if (cnt[i] < nmax)  // pad with 0, the reserved id
@@ -626,46 +713,110 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
       for (uint32_t i = 0; i < n; ++i)
         SG_NCCL(g, ncclAllGather(g->keys[i].p, g->gath[i].p, nmax, ncclUint64, g->comm[i], g->st[i]));
       SG_NCCL(g, ncclGroupEnd());
-      all.resize(nmax * n);
+      for (uint32_t i = 0; i < n; ++i)
+        if (int rc = device_union(g, i, static_cast<const uint64_t *>(g->gath[i].p), nmax * n)) return rc;
+      if (int rc = union_count(g, 0, &nu, &skip0)) return rc;
+      for (uint32_t i = 1; i < n; ++i) {
+        uint64_t nu_i = 0;
+        bool s0 = false;
+        if (int rc = union_count(g, i, &nu_i, &s0)) return rc;
+        if (nu_i != nu || s0 != skip0) return gfail(g, SA_EDEVICE, "members disagree on the key union");
+      }
+    } else {
+      uint64_t total = 0;
+      for (uint32_t i = 0; i < n; ++i) total += cnt[i];
+      if (int rc = ensure(g, g->dev[0], g->gath[0], total * 8)) return rc;
+      for (uint32_t i = 1; i < n; ++i) {  // member 0's stream orders after every member's export
+        SG_HIP(g, hipSetDevice(g->dev[i]));
+        SG_HIP(g, hipStreamSynchronize(g->st[i]));
+      }
       SG_HIP(g, hipSetDevice(g->dev[0]));
-      SG_HIP(g, hipMemcpyAsync(all.data(), g->gath[0].p, all.size() * 8, hipMemcpyDeviceToHost, g->st[0]));
-      SG_HIP(g, hipStreamSynchronize(g->st[0]));
-    }
-  } else {
-    for (uint32_t i = 0; i < n; ++i) {
-      if (!cnt[i]) continue;
-      const size_t at = all.size();
-      all.resize(at + cnt[i]);
-      SG_HIP(g, hipSetDevice(g->dev[i]));
-      SG_HIP(g, hipMemcpy(all.data() + at, g->keys[i].p, cnt[i] * 8, hipMemcpyDeviceToHost));
+      uint64_t at = 0;
+      for (uint32_t i = 0; i < n; ++i) {
+        uint64_t *dst = static_cast<uint64_t *>(g->gath[0].p) + at;
+        if (cnt[i] && g->dev[i] == g->dev[0])
+          SG_HIP(g, hipMemcpyAsync(dst, g->keys[i].p, cnt[i] * 8, hipMemcpyDeviceToDevice, g->st[0]));
+        else if (cnt[i])
+          SG_HIP(g, hipMemcpyPeerAsync(dst, g->dev[0], g->keys[i].p, g->dev[i], cnt[i] * 8, g->st[0]));
+        at += cnt[i];
+      }
+      if (int rc = device_union(g, 0, static_cast<const uint64_t *>(g->gath[0].p), total)) return rc;
+      if (int rc = union_count(g, 0, &nu, &skip0)) return rc;
+      const uint64_t *u0 = static_cast<const uint64_t *>(g->uni[0].p) + (skip0 ? 1 : 0);
+      for (uint32_t i = 1; i < n && nu; ++i) {
+        if (int rc = ensure(g, g->dev[i], g->uni[i], nu * 8)) return rc;
+        SG_HIP(g, hipSetDevice(g->dev[i]));
+        if (g->dev[i] == g->dev[0])
+          SG_HIP(g, hipMemcpyAsync(g->uni[i].p, u0, nu * 8, hipMemcpyDeviceToDevice, g->st[0]));
+        else
+          SG_HIP(g, hipMemcpyPeerAsync(g->uni[i].p, g->dev[i], u0, g->dev[0], nu * 8, g->st[0]));
+      }
+      if (nu) {  // the members' streams wait for the union copies on st[0]
+        SG_HIP(g, hipSetDevice(g->dev[0]));
+        SG_HIP(g, hipStreamSynchronize(g->st[0]));
+      }
     }
   }
-  all.erase(std::remove(all.begin(), all.end(), 0ULL), all.end());
-  std::sort(all.begin(), all.end());
-  all.erase(std::unique(all.begin(), all.end()), all.end());
-  const uint64_t nu = all.size(), len = nu * stride;
-  // 3. dense rows per member (and its counters reset), 4. their sum
-  std::vector<uint64_t> merged(len);
+  auto union_of = [&](uint32_t i) -> const uint64_t * {
+    // the copy transport's members other than 0 hold the union without the padding 0
+    const bool own = g->rccl || i == 0;
+    return static_cast<const uint64_t *>(g->uni[i].p) + (own && skip0 ? 1 : 0);
+  };
+  const uint64_t len = nu * stride;
+  // 3. dense rows per member (and its counters reset), 4. their sum, 5. the
+  //    result's columns on member 0's device
+  std::unique_ptr<red_holder> h(new red_holder());
+  h->keys.resize(nu);
+  h->counts.resize(nu * g->nbk);
+  h->calls.resize(nu);
+  h->sum_ns.resize(nu);
+  h->sum.resize(nu);
+  auto drop = [](int rc) { return rc; };
   if (nu) {
     for (uint32_t i = 0; i < n; ++i) {
-      if (int rc = ensure(g, g->dev[i], g->uni[i], nu * 8)) return rc;
-      if (int rc = ensure(g, g->dev[i], g->rows[i], len * 8)) return rc;
-      SG_HIP(g, hipSetDevice(g->dev[i]));
-      SG_HIP(g, hipMemcpyAsync(g->uni[i].p, all.data(), nu * 8, hipMemcpyHostToDevice, g->st[i]));
-      if (int rc = sa_gather_dense(g->eng[i], static_cast<const uint64_t *>(g->uni[i].p), nu,
-                                   static_cast<uint64_t *>(g->rows[i].p), 1, g->st[i]))
-        return member_error(g, i, rc, "sa_gather_dense");
+      if (int rc = ensure(g, g->dev[i], g->rows[i], len * 8)) return drop(rc);
+      if (int rc = sa_gather_dense(g->eng[i], union_of(i), nu, static_cast<uint64_t *>(g->rows[i].p), 1, g->st[i]))
+        return drop(member_error(g, i, rc, "sa_gather_dense"));
     }
+    bool one_device = true;
+    for (uint32_t i = 1; i < n; ++i) one_device = one_device && g->dev[i] == g->dev[0];
     if (g->rccl) {
       SG_NCCL(g, ncclGroupStart());
       for (uint32_t i = 0; i < n; ++i)
         SG_NCCL(g, ncclAllReduce(g->rows[i].p, g->rows[i].p, len, ncclUint64, ncclSum, g->comm[i], g->st[i]));
       SG_NCCL(g, ncclGroupEnd());
+    } else if (one_device && n > 1) {
+      // every member's rows on one device: summed from their buffers into
+      // member 0's (each element read from every member before its one write)
+      for (uint32_t i = 1; i < n; ++i) {
+        SG_HIP(g, hipSetDevice(g->dev[i]));
+        SG_HIP(g, hipStreamSynchronize(g->st[i]));
+      }
+      SG_HIP(g, hipSetDevice(g->dev[0]));
+      SrcPtrs src{};
+      for (uint32_t i = 0; i < n; ++i) src.p[i] = static_cast<const unsigned long long *>(g->rows[i].p);
+      hipLaunchKernelGGL(sum_ptrs_u64, dim3(grid_for(len)), dim3(256), 0, g->st[0],
+                         static_cast<unsigned long long *>(g->rows[0].p), src, n, len);
+      SG_HIP(g, hipGetLastError());
     } else if (int rc = copy_reduce(g, g->rows, len, false)) {
-      return rc;
+      return drop(rc);
     }
+    const size_t fin_bytes = (size_t)nu * (g->nbk + 3) * 8;
+    if (int rc = ensure(g, g->dev[0], g->fin, fin_bytes)) return drop(rc);
     SG_HIP(g, hipSetDevice(g->dev[0]));
-    SG_HIP(g, hipMemcpyAsync(merged.data(), g->rows[0].p, len * 8, hipMemcpyDeviceToHost, g->st[0]));
+    auto *fin = static_cast<unsigned long long *>(g->fin.p);
+    unsigned long long *d_counts = fin, *d_calls = fin + nu * g->nbk, *d_sum_ns = d_calls + nu;
+    double *d_sum = reinterpret_cast<double *>(d_sum_ns + nu);
+    const double div = g->cfg.unit == SA_UNIT_S ? 1e9 : 1e6;
+    hipLaunchKernelGGL(finalize_rows_kernel, dim3(grid_for(nu)), dim3(256), 0, g->st[0],
+                       static_cast<const unsigned long long *>(g->rows[0].p), nu, g->nbk, d_counts, d_calls,
+                       d_sum_ns, d_sum, div);
+    SG_HIP(g, hipGetLastError());
+    SG_HIP(g, hipMemcpyAsync(h->keys.data(), union_of(0), nu * 8, hipMemcpyDeviceToHost, g->st[0]));
+    SG_HIP(g, hipMemcpyAsync(h->counts.data(), d_counts, nu * g->nbk * 8, hipMemcpyDeviceToHost, g->st[0]));
+    SG_HIP(g, hipMemcpyAsync(h->calls.data(), d_calls, nu * 8, hipMemcpyDeviceToHost, g->st[0]));
+    SG_HIP(g, hipMemcpyAsync(h->sum_ns.data(), d_sum_ns, nu * 8, hipMemcpyDeviceToHost, g->st[0]));
+    SG_HIP(g, hipMemcpyAsync(h->sum.data(), d_sum, nu * 8, hipMemcpyDeviceToHost, g->st[0]));
     SG_HIP(g, hipStreamSynchronize(g->st[0]));
   }
   for (uint32_t i = 0; i < n; ++i) {
@@ -675,26 +826,8 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
     // (SA_ESTATE: nothing was gathered, the member's counters were never set)
     if (nu) {
       if (int rc = sa_reclaim_keys(g->eng[i], 0); rc != SA_OK && rc != SA_ESTATE)
-        return member_error(g, i, rc, "sa_reclaim_keys");
+        return drop(member_error(g, i, rc, "sa_reclaim_keys"));
     }
-  }
-  // 5. the result, in key order (the union is sorted)
-  auto *h = new red_holder();
-  h->keys = all;
-  h->counts.resize(nu * g->nbk);
-  h->calls.resize(nu);
-  h->sum_ns.resize(nu);
-  h->sum.resize(nu);
-  const double div = g->cfg.unit == SA_UNIT_S ? 1e9 : 1e6;
-  for (uint64_t r = 0; r < nu; ++r) {
-    uint64_t c = 0;
-    for (uint32_t b = 0; b < g->nbk; ++b) {
-      h->counts[r * g->nbk + b] = merged[r * stride + b];
-      c += merged[r * stride + b];
-    }
-    h->calls[r] = c;
-    h->sum_ns[r] = merged[r * stride + g->nbk];
-    h->sum[r] = (double)h->sum_ns[r] / div;
   }
   h->r.n_series = nu;
   h->r.n_buckets = g->nbk;
@@ -703,7 +836,7 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
   h->r.calls = h->calls.data();
   h->r.sum_ns = h->sum_ns.data();
   h->r.sum = h->sum.data();
-  *out = &h->r;
+  *out = &h.release()->r;
   bool full = false;
   for (uint32_t i = 0; i < n; ++i) {
     full = full || dropped[i] != g->dropped_seen[i];
