@@ -244,6 +244,12 @@ int sa_expo_probe(sa_engine *e, const double *v, const int32_t *scale, uint64_t 
 int sa_expo_fast_probe(sa_engine *e, const uint64_t *d_ns, const int32_t *scale, uint64_t n, int32_t *fast,
                        int32_t *exact, double *log2_err);
 
+/* Diagnostic: the device key union the group flush builds (sa::key_union:
+ * bucket sort by the top bits, bitonic per bucket, repeats and 0 dropped) on
+ * the engine's GPU.  out[0 .. *n_out) = the distinct non-zero ids of
+ * in[0 .. n) ascending (host arrays; out holds n; n <= 2^28). */
+int sa_key_union_probe(sa_engine *e, const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *n_out);
+
 /* Sketches of one resident window (not cleared). */
 int sa_window_read(sa_engine *e, uint64_t window_id, sa_sketch_result **out);
 /* Retire every window < new_base (clears their ring slots); spans whose window

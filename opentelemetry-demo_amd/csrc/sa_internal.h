@@ -375,6 +375,14 @@ hipError_t launch_reduce_errslab(uint32_t *errslab, uint32_t G, uint64_t per_wg,
                                  uint32_t log2cap, unsigned long long *errcnt_ws, hipStream_t s);
 hipError_t launch_count_keys(const unsigned long long *gkeys, uint64_t cap,
                              unsigned long long *out, hipStream_t s);
+// sorted union of series ids on the device (spanagg_union.hip): out = the
+// distinct non-zero ids of in[0..n) ascending, *d_total (device u32) their
+// count; scratch >= key_union_scratch_bytes(n); big_scratch / big_bytes: a
+// grown-on-demand buffer for buckets the LDS sort cannot hold.  Synchronises
+// `s` once (the largest bucket decides the sort's form).
+size_t key_union_scratch_bytes(uint64_t n);
+hipError_t key_union(const uint64_t *in, uint64_t n, uint64_t *out, uint32_t *d_total, void *scratch,
+                     uint64_t **big_scratch, size_t *big_bytes, hipStream_t s);
 // exponential histograms (spanagg_expo.hip)
 hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s);
 hipError_t launch_expo_compact(const ExpoParams &E, unsigned long long *out_keys, ExpoRow *out_rows,

@@ -1144,6 +1144,33 @@ int sa_expo_probe(sa_engine *e, const double *v, const int32_t *scale, uint64_t 
   return st == hipSuccess ? SA_OK : fail(e, SA_EDEVICE, std::string("expo probe: ") + hipGetErrorString(st));
 }
 
+int sa_key_union_probe(sa_engine *e, const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *n_out) {
+  if (!e || !n_out || (n && (!in || !out)) || n > (1ULL << 28)) return SA_EINVAL;
+  *n_out = 0;
+  if (n == 0) return SA_OK;
+  if (int rc = set_dev(e)) return rc;
+  join_sets(e);
+  void *buf = nullptr;
+  const size_t scratch = sa::key_union_scratch_bytes(n);
+  if (hipMalloc(&buf, n * 16 + scratch + 64) != hipSuccess) return fail(e, SA_ENOMEM, "probe buffer");
+  auto *din = static_cast<uint64_t *>(buf), *dout = din + n;
+  auto *dtot = reinterpret_cast<uint32_t *>(dout + n);
+  void *dscr = reinterpret_cast<char *>(dtot) + 64;
+  uint64_t *big = nullptr;
+  size_t big_bytes = 0;
+  uint32_t tot = 0;
+  hipError_t st = hipMemcpyAsync(din, in, n * 8, hipMemcpyHostToDevice, e->stream);
+  if (st == hipSuccess) st = sa::key_union(din, n, dout, dtot, dscr, &big, &big_bytes, e->stream);
+  if (st == hipSuccess) st = hipMemcpyAsync(&tot, dtot, 4, hipMemcpyDeviceToHost, e->stream);
+  if (st == hipSuccess) st = hipStreamSynchronize(e->stream);
+  if (st == hipSuccess && tot) st = hipMemcpy(out, dout, (size_t)tot * 8, hipMemcpyDeviceToHost);
+  if (big) (void)hipFree(big);
+  (void)hipFree(buf);
+  if (st != hipSuccess) return fail(e, SA_EDEVICE, std::string("key union probe: ") + hipGetErrorString(st));
+  *n_out = tot;
+  return SA_OK;
+}
+
 int sa_expo_fast_probe(sa_engine *e, const uint64_t *d_ns, const int32_t *scale, uint64_t n, int32_t *fast,
                        int32_t *exact, double *log2_err) {
   if (!e || (n && (!d_ns || !scale || !fast || !exact)) || n > (1ULL << 20)) return SA_EINVAL;

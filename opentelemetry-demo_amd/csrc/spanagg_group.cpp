@@ -12,8 +12,6 @@
 // bits as one engine fed the whole stream.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_select.hpp>
 
 #include <algorithm>
 #include <map>
@@ -24,6 +22,7 @@
 #include <thread>
 #include <vector>
 
+#include "sa_internal.h"
 #include "sa_results.h"
 #include "spanagg.h"
 
@@ -90,20 +89,40 @@ __host__ __device__ inline uint32_t shard_of(uint64_t w1, uint32_t n, uint32_t r
   return (((uint32_t)(w1 >> 32) % n) * r32 + (uint32_t)w1 % n) % n;
 }
 
-// Spans per shard of a device batch: LDS counters per workgroup, written to
-// blk[workgroup][shard], plus one global atomic per shard per workgroup for
-// the totals the host reads.
-__global__ __launch_bounds__(256) void shard_count_kernel(const uint64_t *w1, uint64_t n, uint32_t nm, uint32_t r32,
-                                                           unsigned long long *cnt, uint32_t *blk) {
-  __shared__ uint32_t c[kMaxMembers];
-  if (threadIdx.x < kMaxMembers) c[threadIdx.x] = 0;
+// ---- device partition (sa_group_ingest_device) -------------------------------
+// Workgroup b of the partition owns the contiguous span range [b * per,
+// (b + 1) * per) and walks it in chunks of kPartChunk spans.
+constexpr uint32_t kShardBlock = 256;
+constexpr uint32_t kPartChunk = 1024;  // spans staged in LDS per round (44 KiB)
+
+// Spans per shard and workgroup: per-wave LDS counters, written to
+// blk[shard][workgroup]; the totals (one global add per shard and workgroup)
+// are what the host reads to size the shards.
+__global__ __launch_bounds__(kShardBlock) void shard_count_kernel(const uint64_t *w1, uint64_t n, uint64_t per,
+                                                                   uint32_t nm, uint32_t r32,
+                                                                   unsigned long long *cnt, uint32_t *blk) {
+  __shared__ uint32_t c[kShardBlock / 64][kMaxMembers];
+  const uint32_t wave = threadIdx.x >> 6;
+  for (uint32_t i = threadIdx.x; i < (kShardBlock / 64) * kMaxMembers; i += kShardBlock) (&c[0][0])[i] = 0;
   __syncthreads();
-  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
-    atomicAdd(&c[shard_of(w1[i], nm, r32)], 1u);
+  const uint64_t lo = blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+  // two spans per lane per step (16-B loads: lo and per are even and the
+  // columns 16-B aligned; a last odd span is read on its own)
+  for (uint64_t i = lo + 2 * threadIdx.x; i < hi; i += 2 * kShardBlock) {
+    if (i + 1 < hi) {
+      const ulonglong2 v = *reinterpret_cast<const ulonglong2 *>(w1 + i);
+      atomicAdd(&c[wave][shard_of(v.x, nm, r32)], 1u);
+      atomicAdd(&c[wave][shard_of(v.y, nm, r32)], 1u);
+    } else {
+      atomicAdd(&c[wave][shard_of(w1[i], nm, r32)], 1u);
+    }
+  }
   __syncthreads();
   if (threadIdx.x < nm) {
-    blk[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = c[threadIdx.x];
-    if (c[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], (unsigned long long)c[threadIdx.x]);
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < kShardBlock / 64; ++w) t += c[w][threadIdx.x];
+    blk[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x] = t;
+    if (t) atomicAdd(&cnt[threadIdx.x], (unsigned long long)t);
   }
 }
 
@@ -145,50 +164,111 @@ struct ShardArgs {  // by value (kernel argument segment): nm <= kMaxMembers
   ShardCols c[kMaxMembers];
 };
 
-// Scatter: a workgroup takes the spans it counted (the same grid and stride
-// as shard_count_kernel), from its own first position in every shard (the
-// scanned counts).  Every wave takes 64 spans, and for each shard present
-// among them (a ballot) one lane reserves a run of the shard's positions from
-// the workgroup's LDS cursor; the lanes of that shard write their span at
-// consecutive positions.  (Reserving from one global cursor per shard put a
-// returning atomic on eight hot addresses per wave and took 15 ms per 10 M
-// spans.)  Order inside a shard is not kept: every aggregate is
+// Scatter, LDS-staged: per chunk of 1,024 spans, every span takes a position
+// in its shard's run of the chunk (a ballot per shard present in the wave,
+// one LDS add per shard and wave), the chunk is written into LDS in shard
+// order (SoA), and then each column leaves as the shards' contiguous runs
+// (~128 spans = 1 KiB per u64 column at 8 members), so the stores coalesce.
+// (Round 3 wrote every wave's 64 spans straight to their shards: runs of ~8
+// spans, 2.2 TB/s.)  Order inside a shard is not kept: every aggregate is
 // order-independent (integer sums and maxima).
-__global__ __launch_bounds__(256) void shard_scatter_kernel(sa_span_batch in, uint32_t nm, uint32_t r32,
-                                                             ShardArgs out, const uint32_t *first) {
-  __shared__ uint32_t cursor[kMaxMembers];
-  if (threadIdx.x < nm) cursor[threadIdx.x] = first[(uint64_t)threadIdx.x * gridDim.x + blockIdx.x];
+__global__ __launch_bounds__(kShardBlock) void shard_scatter_kernel(sa_span_batch in, uint64_t per, uint32_t nm,
+                                                                     uint32_t r32, ShardArgs out,
+                                                                     const uint32_t *first) {
+  __shared__ uint64_t sk[kPartChunk], ss[kPartChunk], se[kPartChunk], sa_[kPartChunk], sb[kPartChunk];
+  __shared__ uint32_t sm[kPartChunk];
+  __shared__ uint8_t sid[kPartChunk];
+  __shared__ uint32_t ccnt[kMaxMembers], coff[kMaxMembers], cur[kMaxMembers];
+  __shared__ ShardCols cols[kMaxMembers];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  if (tid < nm) {
+    cur[tid] = first[(uint64_t)tid * gridDim.x + blockIdx.x];
+    ccnt[tid] = 0;
+    cols[tid] = out.c[tid];
+  }
   __syncthreads();
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t n = in.n;
-  for (uint64_t i0 = blockIdx.x * 256ull + (threadIdx.x & ~63u); i0 < n; i0 += (uint64_t)gridDim.x * 256) {
-    const uint64_t i = i0 + lane;
-    const bool ok = i < n;
-    const uint64_t k = ok ? in.key_hash[i] : 0, s = ok ? in.start_ns[i] : 0, e = ok ? in.end_ns[i] : 0;
-    const uint64_t a = ok ? in.trace_w0[i] : 0, b = ok ? in.trace_w1[i] : 0;
-    const uint32_t m = ok ? in.meta[i] : 0;
-    const uint32_t sh = ok ? shard_of(b, nm, r32) : 0xFFFFFFFFu;
-    uint64_t pending = __ballot(ok);
-    while (pending) {
-      const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)sh, __builtin_ctzll(pending));
-      const uint64_t mj = __ballot(sh == j);
-      pending &= ~mj;
-      const int leader = __builtin_ctzll(mj);
-      uint32_t base = 0;
-      if ((int)lane == leader) base = atomicAdd(&cursor[j], (uint32_t)__popcll(mj));
-      const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
-      if (sh == j) {
-        const uint64_t pos = (uint64_t)b0 +
-                             __builtin_amdgcn_mbcnt_hi((uint32_t)(mj >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mj, 0u));
-        const ShardCols &c = out.c[j];
-        c.k[pos] = k;
-        c.s[pos] = s;
-        c.e[pos] = e;
-        c.a[pos] = a;
-        c.b[pos] = b;
-        c.m[pos] = m;
+  const uint64_t lo = blockIdx.x * per, hi = lo + per < in.n ? lo + per : in.n;
+  constexpr uint32_t kPer = kPartChunk / kShardBlock;  // spans per thread per chunk
+  for (uint64_t c0 = lo; c0 < hi; c0 += kPartChunk) {
+    // 1. loads (span c0 + tid + u * 256) and positions within the shards' runs
+    uint64_t k[kPer], s[kPer], e[kPer], a[kPer], b[kPer];
+    uint32_t m[kPer], sh[kPer], rk[kPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u) {
+      const uint64_t i = c0 + tid + u * kShardBlock;
+      const bool ok = i < hi;
+      k[u] = ok ? in.key_hash[i] : 0;
+      s[u] = ok ? in.start_ns[i] : 0;
+      e[u] = ok ? in.end_ns[i] : 0;
+      a[u] = ok ? in.trace_w0[i] : 0;
+      b[u] = ok ? in.trace_w1[i] : 0;
+      m[u] = ok ? in.meta[i] : 0;
+      sh[u] = ok ? shard_of(b[u], nm, r32) : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u) {
+      uint64_t pending = __ballot(sh[u] != 0xFFFFFFFFu);
+      rk[u] = 0;
+      while (pending) {  // wave-uniform: one round per shard present among the wave's spans
+        const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)sh[u], __builtin_ctzll(pending));
+        const uint64_t mj = __ballot(sh[u] == j);
+        pending &= ~mj;
+        const int leader = __builtin_ctzll(mj);
+        uint32_t base = 0;
+        if ((int)lane == leader) base = atomicAdd(&ccnt[j], (uint32_t)__popcll(mj));
+        base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);
+        if (sh[u] == j)
+          rk[u] = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mj >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mj, 0u));
       }
     }
+    __syncthreads();
+    if (tid < 64) {  // the shards' runs within the chunk (nm <= 64: one wave scan)
+      const uint32_t v = tid < nm ? ccnt[tid] : 0u;
+      uint32_t x = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if ((int)lane >= o) x += y;
+      }
+      if (tid < nm) coff[tid] = x - v;
+    }
+    __syncthreads();
+    // 2. the chunk into LDS in shard order
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u) {
+      if (sh[u] == 0xFFFFFFFFu) continue;
+      const uint32_t p = coff[sh[u]] + rk[u];
+      sk[p] = k[u];
+      ss[p] = s[u];
+      se[p] = e[u];
+      sa_[p] = a[u];
+      sb[p] = b[u];
+      sm[p] = m[u];
+      sid[p] = (uint8_t)sh[u];
+    }
+    __syncthreads();
+    // 3. out as runs: position p of shard j goes to cur[j] + p - coff[j]
+    const uint32_t nchunk = (uint32_t)(hi - c0 < kPartChunk ? hi - c0 : kPartChunk);
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u) {
+      const uint32_t p = tid + u * kShardBlock;
+      if (p >= nchunk) continue;
+      const uint32_t j = sid[p];
+      const uint64_t g = (uint64_t)cur[j] + p - coff[j];
+      const ShardCols &c = cols[j];
+      c.k[g] = sk[p];
+      c.s[g] = ss[p];
+      c.e[g] = se[p];
+      c.a[g] = sa_[p];
+      c.b[g] = sb[p];
+      c.m[g] = sm[p];
+    }
+    __syncthreads();
+    if (tid < nm) {
+      cur[tid] += ccnt[tid];
+      ccnt[tid] = 0;
+    }
+    __syncthreads();
   }
 }
 
@@ -209,7 +289,9 @@ struct sa_group {
   bool rccl = false;
   std::vector<ncclComm_t> comm;
   std::vector<Buf> keys, gath, uni, rows, hll, cms;
-  std::vector<Buf> srt, sort_tmp, ucnt;  // device key union: sorted keys, rocPRIM scratch, unique count
+  std::vector<Buf> srt, ucnt;  // device key union (sa::key_union): its scratch and the distinct count
+  std::vector<uint64_t *> big;  // key_union's scratch for oversized buckets (per member)
+  std::vector<size_t> big_bytes;
   Buf fin;                               // member 0's device: the result's columns (finalize_rows_kernel)
   Buf stack;  // member 0's device: every member's slice for the copy-path reduce
   // sa_group_ingest_device: two staging sets (a call waits only for the
@@ -304,41 +386,27 @@ int copy_reduce(sa_group *g, std::vector<Buf> &bufs, uint64_t len, bool max_u8) 
 }
 
 // The sorted union of `n_in` series ids in `in` (member i's device, stream
-// st[i]; ids may repeat, 0 = padding): rocPRIM radix sort, then unique, into
-// uni[i]; *first = 1 when the union's first id is the padding 0 (skipped by
-// the caller), *nu = distinct ids including it.  Asynchronous: the counts
-// land in ucnt[i] (device) and are read by union_count.
+// st[i]; ids may repeat, 0 = padding) into uni[i]: sa::key_union (bucket
+// sort by the top bits, bitonic per bucket in LDS, repeats and 0 dropped).
+// Its distinct count lands in ucnt[i] (device u32), read by union_count.
 int device_union(sa_group *g, uint32_t i, const uint64_t *in, uint64_t n_in) {
   const int dev = g->dev[i];
-  hipStream_t s = g->st[i];
-  if (int rc = ensure(g, dev, g->srt[i], std::max<uint64_t>(1, n_in) * 8)) return rc;
+  if (int rc = ensure(g, dev, g->srt[i], sa::key_union_scratch_bytes(n_in))) return rc;
   if (int rc = ensure(g, dev, g->uni[i], std::max<uint64_t>(1, n_in) * 8)) return rc;
   if (int rc = ensure(g, dev, g->ucnt[i], 64)) return rc;
   SG_HIP(g, hipSetDevice(dev));
-  auto *srt = static_cast<uint64_t *>(g->srt[i].p), *uni = static_cast<uint64_t *>(g->uni[i].p);
-  auto *cnt = static_cast<uint64_t *>(g->ucnt[i].p);
-  size_t tb_sort = 0, tb_uniq = 0;
-  SG_HIP(g, rocprim::radix_sort_keys(nullptr, tb_sort, in, srt, (size_t)n_in, 0, 64, s));
-  SG_HIP(g, rocprim::unique(nullptr, tb_uniq, srt, uni, cnt, (size_t)n_in, rocprim::equal_to<uint64_t>(), s));
-  if (int rc = ensure(g, dev, g->sort_tmp[i], std::max<size_t>({tb_sort, tb_uniq, (size_t)256}))) return rc;
-  size_t tb = g->sort_tmp[i].bytes;
-  SG_HIP(g, rocprim::radix_sort_keys(g->sort_tmp[i].p, tb, in, srt, (size_t)n_in, 0, 64, s));
-  tb = g->sort_tmp[i].bytes;
-  SG_HIP(g, rocprim::unique(g->sort_tmp[i].p, tb, srt, uni, cnt, (size_t)n_in, rocprim::equal_to<uint64_t>(), s));
-  // the first id (0 when padding or the reserved id sorted first) next to the count
-  SG_HIP(g, hipMemcpyAsync(cnt + 1, uni, 8, hipMemcpyDeviceToDevice, s));
+  SG_HIP(g, sa::key_union(in, n_in, static_cast<uint64_t *>(g->uni[i].p), static_cast<uint32_t *>(g->ucnt[i].p),
+                          g->srt[i].p, &g->big[i], &g->big_bytes[i], g->st[i]));
   return SA_OK;
 }
 
-// Reads member i's union size (waits for its stream): distinct non-zero ids
-// and whether the union starts with the padding 0.
-int union_count(sa_group *g, uint32_t i, uint64_t *nu, bool *skip0) {
-  uint64_t h[2] = {0, 0};
+// Reads member i's union size (waits for its stream).
+int union_count(sa_group *g, uint32_t i, uint64_t *nu) {
+  uint32_t h = 0;
   SG_HIP(g, hipSetDevice(g->dev[i]));
-  SG_HIP(g, hipMemcpyAsync(h, g->ucnt[i].p, 16, hipMemcpyDeviceToHost, g->st[i]));
+  SG_HIP(g, hipMemcpyAsync(&h, g->ucnt[i].p, 4, hipMemcpyDeviceToHost, g->st[i]));
   SG_HIP(g, hipStreamSynchronize(g->st[i]));
-  *skip0 = h[0] > 0 && h[1] == 0;
-  *nu = h[0] - (*skip0 ? 1 : 0);
+  *nu = h;
   return SA_OK;
 }
 
@@ -428,8 +496,9 @@ int sa_group_create(const sa_config *cfg, const int32_t *devices, uint32_t n, sa
   }
   g->keys.resize(n);
   g->srt.resize(n);
-  g->sort_tmp.resize(n);
   g->ucnt.resize(n);
+  g->big.assign(n, nullptr);
+  g->big_bytes.assign(n, 0);
   g->gath.resize(n);
   g->uni.resize(n);
   g->rows.resize(n);
@@ -485,9 +554,9 @@ void sa_group_destroy(sa_group *g) {
       (void)hipStreamSynchronize(g->st[i]);
       (void)hipStreamDestroy(g->st[i]);
     }
-    for (std::vector<Buf> *v : {&g->keys, &g->gath, &g->uni, &g->rows, &g->hll, &g->cms, &g->srt, &g->sort_tmp,
-                                &g->ucnt})
+    for (std::vector<Buf> *v : {&g->keys, &g->gath, &g->uni, &g->rows, &g->hll, &g->cms, &g->srt, &g->ucnt})
       if (i < v->size() && (*v)[i].p) (void)hipFree((*v)[i].p);
+    if (i < g->big.size() && g->big[i]) (void)hipFree(g->big[i]);
     for (size_t k = 0; k < 2; ++k)
       if (k * g->eng.size() + i < g->pcnt.size() && g->pcnt[k * g->eng.size() + i].p)
         (void)hipFree(g->pcnt[k * g->eng.size() + i].p);
@@ -596,6 +665,10 @@ int sa_group_ingest_device(sa_group *g, const sa_span_batch *b, uint32_t src, vo
   if (b->n == 0) return SA_OK;
   if (!b->key_hash || !b->start_ns || !b->end_ns || !b->trace_w0 || !b->trace_w1 || !b->meta)
     return gfail(g, SA_EINVAL, "null batch column");
+  for (const void *c : {(const void *)b->key_hash, (const void *)b->start_ns, (const void *)b->end_ns,
+                        (const void *)b->trace_w0, (const void *)b->trace_w1})
+    if (reinterpret_cast<uintptr_t>(c) & 15) return gfail(g, SA_EINVAL, "device batch u64 columns must be 16-byte aligned");
+  if (reinterpret_cast<uintptr_t>(b->meta) & 7) return gfail(g, SA_EINVAL, "device batch meta column must be 8-byte aligned");
   const int sdev = g->dev[src];
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : g->st[src];
   if (n == 1) {
@@ -609,19 +682,21 @@ int sa_group_ingest_device(sa_group *g, const sa_span_batch *b, uint32_t src, vo
   // the staging set's previous users (each member's ingest of it) are done
   for (uint32_t i = 0; i < n; ++i)
     if (g->done_used[k][i]) SG_HIP(g, hipStreamWaitEvent(s, g->ev_done[k][i], 0));
-  // 1. shard sizes
-  const uint32_t pgrid = grid_for(b->n);
+  // 1. shard sizes (workgroup b of the partition owns spans [b * per, (b + 1) * per))
+  const uint64_t per = std::max<uint64_t>(kPartChunk, (b->n + 2047) / 2048 + kPartChunk - 1) / kPartChunk * kPartChunk;
+  const uint32_t pgrid = (uint32_t)((b->n + per - 1) / per);  // <= 2048
   Buf &pc = g->pcnt[(size_t)k * n + src];  // this set's: the previous call's scatter may still read the other
   if (int rc = ensure(g, sdev, pc, kMaxMembers * 8 + (size_t)4096 * kMaxMembers * 4)) return rc;
   unsigned long long *dcnt = static_cast<unsigned long long *>(pc.p);
   uint32_t *dblk = reinterpret_cast<uint32_t *>(dcnt + kMaxMembers);  // [n][pgrid] counts -> first positions
   if (b->n > 0xFFFFFFFFull) return gfail(g, SA_EINVAL, "device batch above 2^32 spans (u32 shard positions)");
   SG_HIP(g, hipMemsetAsync(dcnt, 0, kMaxMembers * 8, s));
-  hipLaunchKernelGGL(shard_count_kernel, dim3(pgrid), dim3(256), 0, s, b->trace_w1, b->n, n, r32, dcnt, dblk);
-  SG_HIP(g, hipGetLastError());
-  hipLaunchKernelGGL(shard_scan_kernel, dim3(n), dim3(1024), 0, s, dblk, pgrid);
+  hipLaunchKernelGGL(shard_count_kernel, dim3(pgrid), dim3(kShardBlock), 0, s, b->trace_w1, b->n, per, n, r32, dcnt,
+                     dblk);
   SG_HIP(g, hipGetLastError());
   SG_HIP(g, hipMemcpyAsync(g->hcnt, dcnt, n * 8, hipMemcpyDeviceToHost, s));
+  hipLaunchKernelGGL(shard_scan_kernel, dim3(n), dim3(1024), 0, s, dblk, pgrid);  // (while the host reads the counts)
+  SG_HIP(g, hipGetLastError());
   SG_HIP(g, hipStreamSynchronize(s));
   std::vector<uint64_t> cnt(g->hcnt, g->hcnt + n), cap(n);
   size_t bytes = 0;
@@ -641,7 +716,7 @@ int sa_group_ingest_device(sa_group *g, const sa_span_batch *b, uint32_t src, vo
     args.c[i] = ShardCols{c, c + cap[i], c + 2 * cap[i], c + 3 * cap[i], c + 4 * cap[i],
                           reinterpret_cast<uint32_t *>(c + 5 * cap[i])};
   }
-  hipLaunchKernelGGL(shard_scatter_kernel, dim3(pgrid), dim3(256), 0, s, *b, n, r32, args, dblk);
+  hipLaunchKernelGGL(shard_scatter_kernel, dim3(pgrid), dim3(kShardBlock), 0, s, *b, per, n, r32, args, dblk);
   SG_HIP(g, hipGetLastError());
   SG_HIP(g, hipEventRecord(g->ev_scat[k][src], s));
   // 3. every member ingests its shard on its own stream (peer copy first when
@@ -700,7 +775,6 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
   //    device, builds the union there and copies it to the others.
   const uint64_t nmax = *std::max_element(cnt.begin(), cnt.end());
   uint64_t nu = 0;
-  bool skip0 = false;
   if (nmax) {
     if (g->rccl) {
       for (uint32_t i = 0; i < n; ++i) {
@@ -715,12 +789,11 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
       SG_NCCL(g, ncclGroupEnd());
       for (uint32_t i = 0; i < n; ++i)
         if (int rc = device_union(g, i, static_cast<const uint64_t *>(g->gath[i].p), nmax * n)) return rc;
-      if (int rc = union_count(g, 0, &nu, &skip0)) return rc;
+      if (int rc = union_count(g, 0, &nu)) return rc;
       for (uint32_t i = 1; i < n; ++i) {
         uint64_t nu_i = 0;
-        bool s0 = false;
-        if (int rc = union_count(g, i, &nu_i, &s0)) return rc;
-        if (nu_i != nu || s0 != skip0) return gfail(g, SA_EDEVICE, "members disagree on the key union");
+        if (int rc = union_count(g, i, &nu_i)) return rc;
+        if (nu_i != nu) return gfail(g, SA_EDEVICE, "members disagree on the key union");
       }
     } else {
       uint64_t total = 0;
@@ -741,8 +814,8 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
         at += cnt[i];
       }
       if (int rc = device_union(g, 0, static_cast<const uint64_t *>(g->gath[0].p), total)) return rc;
-      if (int rc = union_count(g, 0, &nu, &skip0)) return rc;
-      const uint64_t *u0 = static_cast<const uint64_t *>(g->uni[0].p) + (skip0 ? 1 : 0);
+      if (int rc = union_count(g, 0, &nu)) return rc;
+      const uint64_t *u0 = static_cast<const uint64_t *>(g->uni[0].p);
       for (uint32_t i = 1; i < n && nu; ++i) {
         if (int rc = ensure(g, g->dev[i], g->uni[i], nu * 8)) return rc;
         SG_HIP(g, hipSetDevice(g->dev[i]));
@@ -757,11 +830,7 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
       }
     }
   }
-  auto union_of = [&](uint32_t i) -> const uint64_t * {
-    // the copy transport's members other than 0 hold the union without the padding 0
-    const bool own = g->rccl || i == 0;
-    return static_cast<const uint64_t *>(g->uni[i].p) + (own && skip0 ? 1 : 0);
-  };
+  auto union_of = [&](uint32_t i) -> const uint64_t * { return static_cast<const uint64_t *>(g->uni[i].p); };
   const uint64_t len = nu * stride;
   // 3. dense rows per member (and its counters reset), 4. their sum, 5. the
   //    result's columns on member 0's device

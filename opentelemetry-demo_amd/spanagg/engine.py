@@ -293,6 +293,16 @@ class Engine:
         policy (more than half full); only right after a flush."""
         self._check(self.lib.sa_reclaim_keys(self._h, int(force)), "sa_reclaim_keys")
 
+    def key_union_probe(self, ids) -> np.ndarray:
+        """Diagnostic: the group flush's device key union (sa_key_union_probe)
+        of `ids` -- their distinct non-zero values, ascending."""
+        a = np.ascontiguousarray(ids, dtype=np.uint64)
+        out = np.empty(max(1, len(a)), dtype=np.uint64)
+        n = C.c_uint64(0)
+        self._check(self.lib.sa_key_union_probe(self._h, a.ctypes.data_as(_lib.u64p), len(a),
+                                                out.ctypes.data_as(_lib.u64p), C.byref(n)), "sa_key_union_probe")
+        return out[: n.value].copy()
+
     def expo_probe(self, values, scales):
         """GPU bucket index and Go math.Log of each value (diagnostic)."""
         v = np.ascontiguousarray(values, dtype=np.float64)

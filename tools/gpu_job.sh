@@ -12,6 +12,8 @@
 #   ablate_<wl>      tools/ablate.py over the ABL_FLAGS / ABL_ENVS variant set for <wl>
 #   stamps_<wl>      tools/bt_stamps.py: per-workgroup phase timeline (c4, c4zipf)
 #   sweep            C2 kernel time vs batch size (SIZES="1000000 5000000 ...")
+#   group_<wl>       rocprofv3 --kernel-trace --stats of bench.py --group 8 (an
+#                    8-member group on this device: partition + group flush)
 #   trace_<wl>       rocprofv3 --kernel-trace --stats of a short bench of <wl>
 #   ptrace_<wl>      the same over a long timed region (PSTEPS, default 400 steps,
 #                    one stream: overlapping launches would stretch each other's
@@ -60,6 +62,10 @@ for step in "$@"; do
       # a long timed region so the cold and settling launches weigh little in the average
       (cd /tmp && run "ptrace_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ptrace_$wl" -o run \
          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps ${PSTEPS:-400} --streams 1 --soak-s 0 \
+         --no-filter-off $BQ) || exit $? ;;
+    group_*) wl=${step#group_}  # an 8-member group on this device: partition kernels + group flush
+      (cd /tmp && run "group_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/group_$wl" -o run \
+         -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --group 8 --steps 20 --warmup 3 --soak-s 0 \
          --no-filter-off $BQ) || exit $? ;;
     trace_*) wl=${step#trace_}
       (cd /tmp && run "trace_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$wl" -o run \
