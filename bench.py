@@ -303,6 +303,7 @@ def run_workload(name, n, args, device, rank, world, barrier):
     c0, c1 = ev(), ev()
     c0.record(stream)
     step(0, stream)
+    eng.join(stream.cuda_stream)
     c1.record(stream)
     # settling launches: the first launches into a window raise many HLL
     # registers and its lower bounds are still low, so they run longer (a 10 s
@@ -310,8 +311,10 @@ def run_workload(name, n, args, device, rank, world, barrier):
     # timed one by one and reported as settle_ms, never part of value
     st = [(ev(), ev()) for _ in range(args.settle)]
     for a, b in st:
+        eng.join(stream.cuda_stream)
         a.record(stream)
         step(0, stream)
+        eng.join(stream.cuda_stream)
         b.record(stream)
     for i in range(args.warmup):
         step(i)
@@ -324,13 +327,17 @@ def run_workload(name, n, args, device, rank, world, barrier):
     #    around each launch on its own (adds the events' own cost per launch)
     iso = [(ev(), ev()) for _ in range(n_iso)]
     for a, b in iso:
+        eng.join(stream.cuda_stream)
         a.record(stream)
         step(0, stream)
+        eng.join(stream.cuda_stream)
         b.record(stream)
     k0, k1 = ev(), ev()
+    eng.join(stream.cuda_stream)
     k0.record(stream)
     for _ in range(n_iso):
         step(0, stream)
+    eng.join(stream.cuda_stream)  # (the binned path aggregates on an engine stream)
     k1.record(stream)
     torch.cuda.synchronize(device)
     kernel_ms_bracketed = sum(a.elapsed_time(b) for a, b in iso) / len(iso)
@@ -348,6 +355,7 @@ def run_workload(name, n, args, device, rank, world, barrier):
         step(i)
     enqueue_s = time.perf_counter() - t0
     for s, e_ in zip(streams, ends):
+        eng.join(s.cuda_stream)
         e_.record(s)
     torch.cuda.synchronize(device)
     elapsed = time.perf_counter() - t0

@@ -208,6 +208,14 @@ void sa_host_free(void *p);
  * may run concurrently on the device (the engine orders them only where they
  * share state), which is how consecutive batches overlap. */
 int sa_ingest_device(sa_engine *e, const sa_span_batch *batch, void *stream);
+/* Orders `stream` (NULL = the engine's stream) after every launch the engine
+ * has enqueued so far, including work it runs on its own streams: the
+ * high-cardinality (binned) path aggregates launch k on an engine stream
+ * while launch k + 1 reads its batch, so the caller's stream passes an
+ * ingest once the batch is consumed, not once it is aggregated.  Engine reads
+ * (sa_flush*, sa_window_*, sa_get_stats) and sa_sync join by themselves; a
+ * caller timing the aggregation with events on its own stream joins first. */
+int sa_join(sa_engine *e, void *stream);
 int sa_sync(sa_engine *e);
 
 /* exportMetrics: delta since the last flush, then the engine's RED counters are

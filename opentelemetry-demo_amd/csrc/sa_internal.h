@@ -370,7 +370,10 @@ hipError_t launch_fold_errcnt(const unsigned long long *gkeys, unsigned long lon
 // binned-table path (spanagg_binned.hip)
 hipError_t prepare_ingest_bt(size_t agg_lds);
 size_t bt_agg2_lds_bytes(uint32_t log2sb, uint32_t grid);
-hipError_t launch_ingest_bt(const IngestParams &P, hipStream_t s);
+// the binned launch's two kernels (the engine runs the aggregate on its own
+// stream, beside the next launch's scatter)
+hipError_t launch_bt_scatter(const IngestParams &P, hipStream_t s);
+hipError_t launch_bt_aggregate(const IngestParams &P, hipStream_t s);
 hipError_t launch_reduce_errslab(uint32_t *errslab, uint32_t G, uint64_t per_wg, uint64_t ws,
                                  uint32_t log2cap, unsigned long long *errcnt_ws, hipStream_t s);
 hipError_t launch_count_keys(const unsigned long long *gkeys, uint64_t cap,

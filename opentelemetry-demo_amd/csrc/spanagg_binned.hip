@@ -863,7 +863,9 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
         const uint32_t ek = (ws << log2sb) | s[k];
         const uint32_t at = atomicAdd(&errl[0], 1u);
         if (at + 1 < kErrL) errl[at + 1] = ek;
-        else atomicAdd(P.errcnt + ((uint64_t)ws << P.log2cap) + ((uint64_t)bin << log2sb) + s[k], 1ULL);
+        // past the LDS list: the key's canonical HBM slot (find-or-insert), so
+        // the count stays right if the write-back relocates the key
+        else bt_cold_err(kernel_params(), mm[k], ws);
       }
     }
   };
@@ -917,15 +919,32 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
   bt_stamp(P, (uint64_t)bin * 8, 2);
 
   // 3. new keys and touched rows of the bin (one owner: plain stores; every
-  //    row read is issued before the first row is written); the ERROR list
+  //    row read is issued before the first row is written); the ERROR list.
+  //    The next launch's scatter may run beside this aggregate (the engine
+  //    overlaps them, section "launch pipeline" of spanagg_engine.cpp) and
+  //    CAS-insert keys into this bin's HBM sub-table meanwhile, so a key this
+  //    aggregate added to its LDS mirror is inserted into HBM by the same
+  //    find-or-insert the scatter uses: slots never empty and every inserter
+  //    probes one sequence, so the HBM table stays free of duplicates.  When
+  //    the key lands in another slot than its LDS one (a concurrent insert
+  //    took that slot or an earlier one of the key's sequence), its counts go
+  //    to that slot's spill-array cells by atomics and the LDS slot's row is
+  //    left alone; lsum[s] then carries the relocated slot for the ERROR list.
   if (MODE & 2) return;
   const uint32_t nbk = P.nbk;
   uint4 *rows = reinterpret_cast<uint4 *>(P.gcounts) + ((uint64_t)bin << log2sb) * (kRowBytes / 16);
+  constexpr unsigned long long kMoved = 1ULL << 63;  // lsum[s] after the write-back: kMoved | new slot (or kNotFound)
   uint4 rv[kMaxPer][2];
   bool touched[kMaxPer];
+  uint32_t hs[kMaxPer];  // the HBM slot (in the whole table) holding lkeys[s]
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
     const uint32_t s = tid + u * BLOCK;
+    hs[u] = (bin << log2sb) | s;
+    if (s < sb && lkeys[s] != orig[u]) {
+      const uint32_t f = bt_find_insert(P.gkeys, lkeys[s], log2sb);
+      hs[u] = f;  // kNotFound: the bin's HBM sub-table filled meanwhile
+    }
     touched[u] = s < sb && lsum[s] != 0;
     if (s < sb && !touched[u]) {  // a zero ns sum: look at the counts
       uint32_t any = 0;
@@ -935,16 +954,30 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
       }
       touched[u] = any != 0;
     }
+    const bool own = hs[u] == ((bin << log2sb) | s);
 #pragma unroll
-    for (uint32_t q = 0; q < 2; ++q) rv[u][q] = touched[u] ? rows[(uint64_t)s * 2 + q] : make_uint4(0, 0, 0, 0);
+    for (uint32_t q = 0; q < 2; ++q)
+      rv[u][q] = touched[u] && own ? rows[(uint64_t)s * 2 + q] : make_uint4(0, 0, 0, 0);
   }
+  uint32_t n_lost = 0;
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
     const uint32_t s = tid + u * BLOCK;
     if (s >= sb) continue;
-    const unsigned long long k = lkeys[s];
-    if (k != orig[u]) gk[s] = k;
+    const bool own = hs[u] == ((bin << log2sb) | s);
+    const unsigned long long ls = lsum[s];
+    lsum[s] = own ? 0ULL : kMoved | hs[u];
     if (!touched[u]) continue;
+    if (!own) {  // relocated (or lost): the counts by atomics into the spill array
+      for (uint32_t b = 0; b < nbk; ++b) {
+        const uint32_t h = s * kPartMaxBk + b;
+        const uint32_t c = (lcnt[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu;
+        if (hs[u] == kNotFound) n_lost += c;
+        else if (c) atomicAdd(P.base64 + (uint64_t)hs[u] * (nbk + 1) + b, (unsigned long long)c);
+      }
+      if (hs[u] != kNotFound && ls) atomicAdd(P.base64 + (uint64_t)hs[u] * (nbk + 1) + nbk, ls);
+      continue;
+    }
     const uint32_t w[8] = {rv[u][0].x, rv[u][0].y, rv[u][0].z, rv[u][0].w,
                            rv[u][1].x, rv[u][1].y, rv[u][1].z, rv[u][1].w};
     const unsigned long long sum = ((unsigned long long)w[1] << 32 | w[0]) + lsum[s];
@@ -970,10 +1003,16 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
     rows[(uint64_t)s * 2] = make_uint4((uint32_t)sum, (uint32_t)(sum >> 32), o[0], o[1]);
     rows[(uint64_t)s * 2 + 1] = make_uint4(o[2], o[3], o[4], o[5]);
   }
+  n_lost = wave_sum(n_lost);
+  if (lane == 0 && n_lost) atomicAdd(&misc[0], n_lost);
+  __syncthreads();  // lsum carries the relocations for the ERROR list
   const uint32_t ne = min(errl[0], kErrL - 1);
   for (uint32_t i = tid; i < ne; i += BLOCK) {
     const uint32_t ek = errl[i + 1], ws = ek >> log2sb, s = ek & (sb - 1);
-    atomicAdd(P.errcnt + ((uint64_t)ws << P.log2cap) + ((uint64_t)bin << log2sb) + s, 1ULL);
+    const unsigned long long mv = lsum[s];
+    const uint32_t slot = (mv & kMoved) ? (uint32_t)mv : ((bin << log2sb) | s);
+    if (slot != kNotFound) atomicAdd(P.errcnt + ((uint64_t)ws << P.log2cap) + slot, 1ULL);
+    else bt_cms_add(kernel_params(), ws, lkeys[s] * P.kinv);
   }
   if (tid == 0 && misc[0]) atomicAdd(&P.stats[kStatDropped], (unsigned long long)misc[0]);
   bt_stamp(P, (uint64_t)bin * 8, 3);
@@ -1093,18 +1132,19 @@ hipError_t prepare_ingest_bt(size_t agg_lds) {
 
 #endif
 
-hipError_t launch_ingest_bt(const IngestParams &P, hipStream_t s) {
-  void *args[] = {const_cast<IngestParams *>(&P)};
 #ifndef SPANAGG_AB
-  constexpr uint32_t kDiagBtNoScatter = 0, kDiagBtNoAgg = 0;
+constexpr uint32_t kDiagBtNoScatter = 0, kDiagBtNoAgg = 0;
 #endif
-  if (!(P.diag & kDiagBtNoScatter)) {
-    if (hipError_t e = hipLaunchKernel(bt_scatter2_fn(P.diag), dim3(P.bt_grid), dim3(kBtBlock), args,
-                                       kBt2ScatterLds, s);
-        e != hipSuccess)
-      return e;
-  }
+
+hipError_t launch_bt_scatter(const IngestParams &P, hipStream_t s) {
+  if (P.diag & kDiagBtNoScatter) return hipSuccess;
+  void *args[] = {const_cast<IngestParams *>(&P)};
+  return hipLaunchKernel(bt_scatter2_fn(P.diag), dim3(P.bt_grid), dim3(kBtBlock), args, kBt2ScatterLds, s);
+}
+
+hipError_t launch_bt_aggregate(const IngestParams &P, hipStream_t s) {
   if (P.diag & kDiagBtNoAgg) return hipSuccess;
+  void *args[] = {const_cast<IngestParams *>(&P)};
   const uint32_t diag = P.diag | (P.log2sb > 10 ? kDiagBtAggWide : 0u);
   return hipLaunchKernel(bt_agg_fn(diag), dim3(kPartBins), dim3(kBtAgg2Block), args,
                          bt_agg2_lds_bytes(P.log2sb, P.bt_grid), s);

@@ -123,8 +123,19 @@ struct sa_engine {
   uint32_t log2sb = 0, bt_grid = 0;
   uint64_t kmul = 1, kinv = 1;
   size_t agg_lds = 0;
-  ulonglong2 *bt_rec = nullptr;
-  uint32_t *bt_cnt = nullptr;
+  // Launch pipeline of the binned path: launch k's scatter runs on the
+  // caller's stream and its aggregate on agg_stream (after ev_scat[k % 2]),
+  // so launch k + 1's scatter overlaps launch k's aggregate.  Two record sets
+  // (records + region fills): a scatter waits only for the aggregate that
+  // last read its set (ev_agg, two launches back).  The aggregate's key
+  // write-back is safe against the concurrent scatter's key inserts
+  // (spanagg_binned.hip bt_aggregate3_kernel step 3).
+  ulonglong2 *bt_rec[2] = {nullptr, nullptr};
+  uint32_t *bt_cnt[2] = {nullptr, nullptr};
+  hipStream_t agg_stream = nullptr;
+  hipEvent_t ev_scat[2] = {nullptr, nullptr}, ev_agg[2] = {nullptr, nullptr};
+  bool agg_used[2] = {false, false};
+  uint32_t bt_set = 0;
   unsigned long long *base64 = nullptr;
   size_t hll_slot_bytes = 0, cms_slot_elems = 0;
   // sa_ingest: two pinned host slots and their HBM copies; a slot is refilled
@@ -483,6 +494,13 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     if ((rc = alloc((void **)&e->base64, spill))) return bail(rc);  // (zeroed)
     if (hipError_t st = sa::prepare_ingest_bt(e->agg_lds); st != hipSuccess)
       return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
+    // the aggregate stream of the launch pipeline (ordered by events only)
+    if (hipStreamCreateWithFlags(&e->agg_stream, hipStreamNonBlocking) != hipSuccess)
+      return bail(fail(e, SA_EDEVICE, "aggregate stream creation failed"));
+    for (int k = 0; k < 2; ++k)
+      if (hipEventCreateWithFlags(&e->ev_scat[k], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&e->ev_agg[k], hipEventDisableTiming) != hipSuccess)
+        return bail(fail(e, SA_EDEVICE, "event creation failed"));
     // a random odd multiplier per engine: series ids -> stored ids (bins and
     // home slots), so bin occupancy does not depend on ids a sender chooses
     std::random_device rd;
@@ -528,7 +546,8 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->stats, (void *)e->out_keys, (void *)e->out_rows, (void *)e->scratch,
                   (void *)e->slab_cnt, (void *)e->hll, (void *)e->errcnt, (void *)e->d_seeds,
                   (void *)e->dbg, (void *)e->d_bins, (void *)e->errslab, (void *)e->part_rec,
-                  (void *)e->part_fill, (void *)e->bt_rec, (void *)e->bt_cnt, (void *)e->base64, (void *)e->hll_lb,
+                  (void *)e->part_fill, (void *)e->bt_rec[0], (void *)e->bt_cnt[0], (void *)e->bt_rec[1],
+                  (void *)e->bt_cnt[1], (void *)e->base64, (void *)e->hll_lb,
                   (void *)e->expo_hdr, (void *)e->expo_buckets, (void *)e->expo_slot, (void *)e->expo_out_keys,
                   (void *)e->expo_out_rows, (void *)e->expo_out_buckets, (void *)e->hll_filt, (void *)e->xslab,
                   (void *)e->xc_lcount, (void *)e->xc_slot_of_entry, (void *)e->xcslab,
@@ -543,6 +562,14 @@ void sa_destroy(sa_engine *e) {
   for (hipEvent_t ev : e->ev_set)
     if (ev) (void)hipEventDestroy(ev);
   if (e->ev_ctl) (void)hipEventDestroy(e->ev_ctl);
+  for (int k = 0; k < 2; ++k) {
+    if (e->ev_scat[k]) (void)hipEventDestroy(e->ev_scat[k]);
+    if (e->ev_agg[k]) (void)hipEventDestroy(e->ev_agg[k]);
+  }
+  if (e->agg_stream) {
+    (void)hipStreamSynchronize(e->agg_stream);
+    (void)hipStreamDestroy(e->agg_stream);
+  }
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -556,6 +583,8 @@ static void join_sets(sa_engine *e) {
   for (uint32_t i = 0; i < e->nsets; ++i)
     if (e->set_stream[i] && e->set_stream[i] != e->stream)
       (void)hipStreamWaitEvent(e->stream, e->ev_set[i], 0);
+  for (int k = 0; k < 2; ++k)  // the binned path's aggregates
+    if (e->agg_used[k]) (void)hipStreamWaitEvent(e->stream, e->ev_agg[k], 0);
   e->ctl_dirty = true;
 }
 
@@ -601,17 +630,18 @@ static int bt_prepare_launch(sa_engine *e, uint64_t n, IngestParams &P, hipStrea
   P.bt_grid = grid;
   P.wg_chunk = ((n + grid - 1) / grid + 3) / 4 * 4;
   P.bt_region = bt_region_for(P.wg_chunk);
-  if (!e->bt_rec) {
+  if (!e->bt_rec[0]) {
     const size_t recs = (size_t)sa::kPartBins * e->bt_grid * bt_region_for(sa::kBtMaxWgSpans);
-    if (hipMalloc((void **)&e->bt_rec, recs * sizeof(ulonglong2)) != hipSuccess ||
-        hipMalloc((void **)&e->bt_cnt, (size_t)e->bt_grid * sa::kPartBins * 4) != hipSuccess)
-      return fail(e, SA_ENOMEM, "binned-path record buffers hipMalloc failed");
+    for (int k = 0; k < 2; ++k)
+      if (hipMalloc((void **)&e->bt_rec[k], recs * sizeof(ulonglong2)) != hipSuccess ||
+          hipMalloc((void **)&e->bt_cnt[k], (size_t)e->bt_grid * sa::kPartBins * 4) != hipSuccess)
+        return fail(e, SA_ENOMEM, "binned-path record buffers hipMalloc failed");
   }
   P.log2sb = e->log2sb;
   P.kmul = e->kmul;
   P.kinv = e->kinv;
-  P.bt_rec = e->bt_rec;
-  P.bt_cnt = e->bt_cnt;
+  P.bt_rec = e->bt_rec[e->bt_set];
+  P.bt_cnt = e->bt_cnt[e->bt_set];
   return SA_OK;
 }
 
@@ -728,7 +758,16 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
     st = sa::launch_ingest_small(P, grid, e->lds_bytes, s, e->variant);
   } else if (e->bt) {
     if (int rc = bt_prepare_launch(e, b->n, P, s)) return rc;
-    st = sa::launch_ingest_bt(P, s);
+    // the pipeline (sa_engine::bt_rec): scatter here, aggregate on agg_stream
+    const uint32_t k = e->bt_set;
+    if (e->agg_used[k]) SA_HIP(e, hipStreamWaitEvent(s, e->ev_agg[k], 0));  // set k's last reader
+    st = sa::launch_bt_scatter(P, s);
+    if (st == hipSuccess) st = hipEventRecord(e->ev_scat[k], s);
+    if (st == hipSuccess) st = hipStreamWaitEvent(e->agg_stream, e->ev_scat[k], 0);
+    if (st == hipSuccess) st = sa::launch_bt_aggregate(P, e->agg_stream);
+    if (st == hipSuccess) st = hipEventRecord(e->ev_agg[k], e->agg_stream);
+    e->agg_used[k] = true;
+    e->bt_set ^= 1;
   } else if (e->part) {
     // records per bin: 1.25x the mean plus slack; a fuller bin spills to the
     // direct path, so this bounds memory, not correctness
@@ -908,6 +947,17 @@ int sa_ingest(sa_engine *e, const sa_span_batch *b) {
   // the last chunk's are, before the caller may reuse the arrays
   if (pinned) SA_HIP(e, hipEventSynchronize(e->ev_b));
   guard.armed = false;
+  return SA_OK;
+}
+
+int sa_join(sa_engine *e, void *stream) {
+  if (!e) return SA_EINVAL;
+  if (int rc = set_dev(e)) return rc;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+  for (uint32_t i = 0; i < e->nsets; ++i)
+    if (e->set_stream[i] && e->set_stream[i] != s) SA_HIP(e, hipStreamWaitEvent(s, e->ev_set[i], 0));
+  for (int k = 0; k < 2; ++k)
+    if (e->agg_used[k]) SA_HIP(e, hipStreamWaitEvent(s, e->ev_agg[k], 0));
   return SA_OK;
 }
 

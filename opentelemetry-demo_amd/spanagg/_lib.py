@@ -103,6 +103,7 @@ SIGNATURES = [
     ("sa_exp_result_free", None, [C.POINTER(sa_exp_result)]),
     ("sa_expo_probe", C.c_int, [C.c_void_p, f64p, C.POINTER(C.c_int32), C.c_uint64, C.POINTER(C.c_int32), f64p]),
     ("sa_key_union_probe", C.c_int, [C.c_void_p, u64p, C.c_uint64, u64p, u64p]),
+    ("sa_join", C.c_int, [C.c_void_p, C.c_void_p]),
     ("sa_expo_fast_probe", C.c_int, [C.c_void_p, u64p, C.POINTER(C.c_int32), C.c_uint64, C.POINTER(C.c_int32),
                                      C.POINTER(C.c_int32), f64p]),
     ("sa_window_read", C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.POINTER(sa_sketch_result))]),

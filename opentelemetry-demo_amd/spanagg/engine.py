@@ -269,6 +269,12 @@ class Engine:
         self._check(self.lib.sa_ingest_device(self._h, C.byref(b), C.c_void_p(stream or 0)),
                     "sa_ingest_device")
 
+    def join(self, stream: Optional[int] = None):
+        """sa_join: order `stream` (a hipStream_t handle, None = the engine's)
+        after every launch enqueued so far, the binned path's aggregates on
+        the engine's own stream included (before timing events on `stream`)."""
+        self._check(self.lib.sa_join(self._h, C.c_void_p(stream or 0)), "sa_join")
+
     def sync(self):
         self._check(self.lib.sa_sync(self._h), "sa_sync")
 

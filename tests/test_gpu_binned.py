@@ -1,5 +1,5 @@
 """GPU parity of the binned-table high-cardinality path (spanagg_binned.hip:
-bt_scatter2_kernel + bt_aggregate2_kernel; tables of 2^19..2^22 slots)
+bt_scatter2_kernel + bt_aggregate3_kernel; tables of 2^19..2^22 slots)
 against the CPU oracle, including the spill paths (stage/region overflow
 table, the direct path), the u8 rows' spill array, full bins and launch
 splitting.
@@ -74,6 +74,48 @@ def test_binned_matches_partitioned_path(zipf):
             e.ingest(batch.slice(0, half))
             e.ingest(batch.slice(half, len(batch)))
             _check(e, batch, o)
+
+
+@pytest.mark.parametrize("zipf", [0.0, 1.2])
+def test_binned_pipeline_new_keys_every_launch(zipf):
+    """The launch pipeline (spanagg_engine.cpp sa_engine::bt_rec): launch k's
+    aggregate runs on the engine's stream beside launch k + 1's scatter.  Every
+    launch brings a key set no launch had (the series ids XORed with a
+    per-launch constant), so launch k's aggregate inserts its keys into the
+    HBM sub-tables while launch k + 1's scatter inserts the hot keys of its
+    own mix (overflow table, direct path) into the same bins: the write-back
+    must find-or-insert and relocate, never duplicate or overwrite a key.
+    Launches alternate over two caller streams, device-resident."""
+    import torch
+    dev = torch.device("cuda", 0)
+    n = 2_000_000
+    batch, _, w0 = generate_highcard(n, seed=41, routes=1000, pods=400, zipf_s=zipf)
+    cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(dev)
+            for c in batch.columns()]
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream(dev))
+    o = pyoracle.Oracle(n_services=1)
+    rng = np.random.Generator(np.random.PCG64(43))
+    with _engine(1_200_000) as e:
+        e.window_advance(w0)
+        keep = []
+        for i in range(6):
+            c = int(rng.integers(1, 2**63 - 1))
+            kx = cols[0] ^ c
+            keep.append(kx)
+            e.ingest_device(kx, cols[1], cols[2], cols[3], cols[4], cols[5], n=n, stream=streams[i % 2].cuda_stream)
+            o.ingest(SpanBatch(batch.key_hash ^ np.uint64(c), batch.start_ns, batch.end_ns, batch.trace_w0,
+                               batch.trace_w1, batch.meta))
+        torch.cuda.synchronize(dev)
+        res = e.flush()
+        assert_red_equal(res, o.series())
+        assert len(np.unique(res.key_hash)) == len(res.key_hash)
+        for wid in o.window_ids():
+            sk = e.window_read(wid)
+            hll, cms = o.window(wid)
+            assert np.array_equal(sk.hll, hll) and np.array_equal(sk.cms, cms), wid
+        assert e.stats()["dropped_table_full"] == 0
 
 
 def test_binned_u8_rows_spill():
