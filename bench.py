@@ -138,7 +138,7 @@ def load_traffic(path, workload):
     return None, None
 
 
-def host_otlp_rate(spans: int, threads: int = 8, batch: int = 128):
+def host_otlp_rate(spans: int, threads: int = 8, batch: int = 128, extra=()):
     """the OTLP decode+aggregate rate from protobuf bytes -- the
     Node host (native columnizer in the N-API addon, `threads` decode threads
     with the JavaScript thread one of them, `batch` requests per
@@ -150,12 +150,14 @@ def host_otlp_rate(spans: int, threads: int = 8, batch: int = 128):
         return None
     try:
         p = subprocess.run([node, "--max-old-space-size=16000", script, str(spans), "--gpu", "--threads",
-                            str(threads), "--batch", str(batch)], capture_output=True, text=True, timeout=180)
+                            str(threads), "--batch", str(batch), *extra], capture_output=True, text=True, timeout=180)
         r = json.loads(p.stdout.strip().splitlines()[-1])
     except Exception as e:  # reported, never fatal for the bench line
         return {"error": str(e)[:200]}
     return {"value": r["spans_per_s"], "unit": "spans/s", "cores": r["cores"], "mb_per_s": r["mb_per_s"],
             "calls_check": r["calls_check"], "columnizer": r["columnizer"],
+            "seconds_in": r.get("seconds_in"), "options": list(extra),
+            **({"exemplars": r["exemplars"], "event_records": r["event_records"]} if extra else {}),
             "sample": f"{r['spans']:,} spans in {r['requests']} OTLP requests of 512 spans, "
                       f"{batch} requests per batch, 20 services x 25 names, decode + transform rules + "
                       "keying + columnise + sa_ingest (pinned staging, H2D + kernel)"}
@@ -686,7 +688,11 @@ def main():
                 result["cpu_baseline_multicore"] = mc
         if world == 1 and args.host_otlp_spans > 0:
             # the box's usable cores (its cgroup CPU share), at most 16 decode threads
-            result["host_otlp"] = host_otlp_rate(args.host_otlp_spans, threads=max(1, min(16, box_cores()["usable"])))
+            hthreads = max(1, min(16, box_cores()["usable"]))
+            result["host_otlp"] = host_otlp_rate(args.host_otlp_spans, threads=hthreads)
+            # the same with exemplars (5 per data point) and span events (exception.type) on
+            result["host_otlp_exemplars_events"] = host_otlp_rate(args.host_otlp_spans, threads=hthreads,
+                                                                  extra=("--exemplars", "--events"))
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -980,7 +980,7 @@ __global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P)
     }
     const uint32_t w[8] = {rv[u][0].x, rv[u][0].y, rv[u][0].z, rv[u][0].w,
                            rv[u][1].x, rv[u][1].y, rv[u][1].z, rv[u][1].w};
-    const unsigned long long sum = ((unsigned long long)w[1] << 32 | w[0]) + lsum[s];
+    const unsigned long long sum = ((unsigned long long)w[1] << 32 | w[0]) + ls;  // (lsum[s] now holds the relocation mark)
     uint32_t c[kPartMaxBk];
     bool spill = false;
 #pragma unroll
