@@ -453,6 +453,10 @@ struct Pending {  // one step's HLL reads, compared one step later
   uint32_t hoff[S], rho[S], hv[S];
 };
 
+// 32-bit tag of a series id in the small-table LDS mirror (TAG kernels); the
+// same fold probe_seq hashes, so the two share the XOR
+__device__ __forceinline__ uint32_t key_tag(uint64_t k) { return (uint32_t)k ^ (uint32_t)(k >> 32); }
+
 __device__ __forceinline__ uint64_t copy_u64(uint64_t x) {
   uint32_t lo, hi;
   asm volatile("v_mov_b32 %0, %1" : "=v"(lo) : "v"((uint32_t)x));

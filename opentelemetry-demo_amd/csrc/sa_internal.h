@@ -331,16 +331,20 @@ constexpr uint32_t kHbmBlock = 256;
 // tiles in flight, 10 four spans per lane, 11 generic (default cache policy),
 // 12 / 13 = 8 / 11 specialised for cap 2048, 17 buckets, HLL p 14; 14 = 12 with
 // dynamic wave chunks; 15 = 14 generic; 16-18 = 14 with OPT 1 / 3 / 2; 19 = 16
-// with the batched end-of-launch write-back (v2_epilogue); 20 = 19 LEAN.
-constexpr int kNumLdsVariants = 21;
-constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
+// with the batched end-of-launch write-back (v2_epilogue); 20 = 19 LEAN; 21 =
+// 20 with the TAG key lookup.
+constexpr int kNumLdsVariants = 22;
+constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
 // v2 kernels keep u16 LDS counters for a whole launch: spans per workgroup per launch
 constexpr uint32_t kMaxWgSpans = 65532;
 constexpr uint32_t kDbgPerWg = 136;  // diagnostic stamps per workgroup: 8 + 16 waves x 8
 constexpr uint32_t kHllQueue = 2048;  // deferred HLL raises per workgroup (8 B each)
 constexpr uint32_t kErrTab = 1024;    // LDS (window, slot) -> ERROR count table per workgroup (4 B each)
 // ingest_lds_kernel LDS beyond the table: HLL queue + its count + bin table
+// (+ the ERROR table and HLL bounds of the v2 kernels; their TAG forms add
+// cap u32 key tags, see kLdsTagBytes)
 constexpr size_t kLdsExtraBytes = kHllQueue * 8 + 32 + kBins * sizeof(BinEntry) + kErrTab * 4 + kLbMaxSub;
+constexpr size_t kLdsTagBytesPerSlot = 4;
 
 // launchers (spanagg_kernels.hip)
 hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,

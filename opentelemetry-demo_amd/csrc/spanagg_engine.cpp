@@ -370,7 +370,8 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   e->log2cap = log2u(e->cap);
   const uint32_t nw = (e->nbk + 1) / 2;
   // lkeys + lsum + lcnt + deferred-HLL queue (+ its counter), see ingest_lds_kernel
-  e->lds_bytes = (size_t)e->cap * 16 + (size_t)e->cap * nw * 4 + sa::kLdsExtraBytes;
+  e->lds_bytes = (size_t)e->cap * 16 + (size_t)e->cap * nw * 4 + sa::kLdsExtraBytes +
+                 (size_t)e->cap * sa::kLdsTagBytesPerSlot;  // (the TAG kernels' key tags)
   e->expo = cfg->exp_max_size != 0;
   e->small = e->lds_bytes <= kLdsBudget && !e->expo;
   if (e->expo) {  // key mirror + 32-B header partials per slot (nw = 6 counter words)

@@ -455,7 +455,7 @@ __device__ __forceinline__ uint32_t wave_find_insert(unsigned long long *lkeys, 
 // Resolves the lanes with `need` one distinct key at a time (lanes sharing a
 // key are resolved together); call with all lanes active.
 __device__ __forceinline__ void cold_lookup_wave(unsigned long long *lkeys, bool need, uint64_t key,
-                                                 uint32_t log2cap, uint32_t &found) {
+                                                 uint32_t log2cap, uint32_t &found, uint32_t *ltag = nullptr) {
   uint64_t m = __ballot(need);
   while (m) {
     const int l = __builtin_ctzll(m);
@@ -463,6 +463,7 @@ __device__ __forceinline__ void cold_lookup_wave(unsigned long long *lkeys, bool
     const uint32_t khi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(key >> 32), l);
     const uint64_t k = ((uint64_t)khi << 32) | klo;
     const uint32_t f = wave_find_insert(lkeys, k, log2cap);
+    if (ltag && f != kNotFound && (threadIdx.x & 63u) == 0) ltag[f] = key_tag(k);  // (the mirror's tag of the slot)
     const bool same = need && key == k;
     found = same ? f : found;
     m &= ~__ballot(same);
@@ -540,8 +541,13 @@ __device__ __forceinline__ uint32_t wave_claim(uint32_t *ctr) {
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)atomicAdd(ctr, 1u)) >> 6;
 }
 
+// TAG: the key lookup reads 32-bit tags (key_tag) of the two candidate
+// buckets -- one ds_read_b128 per bucket instead of two -- and verifies the
+// matching slot's full key with one ds_read_b64 (a tag match on another key,
+// or on an empty slot for a key whose tag is 0, fails the check and takes the
+// cold path, which probes full keys): 40 B of LDS per span instead of 64.
 template <int S, int NBUF, int AUX, bool DIAG, int LC = 0, int NWC = 0, int PC = 0, int HAUX = -1,
-          bool DYN = false, int OPT = 0, bool EPI = false, bool LEAN = false, bool EXPO = false>
+          bool DYN = false, int OPT = 0, bool EPI = false, bool LEAN = false, bool EXPO = false, bool TAG = false>
 __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 0] = __builtin_amdgcn_s_memrealtime();
@@ -559,6 +565,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   BinEntry *lbins = reinterpret_cast<BinEntry *>(hq_n + 8);
   uint32_t *etab = reinterpret_cast<uint32_t *>(lbins + kBins);  // [kErrTab]: (key+1) << 16 | count
   uint8_t *llb = reinterpret_cast<uint8_t *>(etab + kErrTab);       // [kLbMaxSub] HLL lower bounds
+  uint32_t *ltag = reinterpret_cast<uint32_t *>(llb + kLbMaxSub);    // TAG: [cap] key_tag of each slot's key
   const bool err_lds = P.errslab != nullptr;
   const bool lb_on = P.lb_n != 0 && !(diag & 2u);
   // EXPO header partials (zeroed with lsum / lcnt): lsum = ns sums
@@ -638,6 +645,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     if (u < (int)per && i < cap) {
       reinterpret_cast<ulonglong2 *>(lkeys)[i / 2] = kv[u];
       reinterpret_cast<ulonglong2 *>(lsum)[i / 2] = make_ulonglong2(0, 0);
+      if constexpr (TAG) reinterpret_cast<uint2 *>(ltag)[i / 2] = make_uint2(key_tag(kv[u].x), key_tag(kv[u].y));
     }
   }
   if (threadIdx.x < kBins * 2) reinterpret_cast<uint4 *>(lbins)[threadIdx.x] = bv;
@@ -789,6 +797,33 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     uint32_t found[S];
     if (!(diag & 1u)) {
       bool need[S];
+      if constexpr (TAG) {
+        uint32_t f[S];
+#pragma unroll
+        for (int j = 0; j < S; ++j) {  // both spans' tag reads first, then both verifies
+          const ProbeSeq pr = probe_seq(key[j], log2cap);
+          const uint4 t1 = *reinterpret_cast<const uint4 *>(ltag + pr.b1 * 4);
+          const uint4 t2 = *reinterpret_cast<const uint4 *>(ltag + pr.b2 * 4);
+          const uint32_t tg = key_tag(key[j]);
+          uint32_t g = kNotFound;
+          g = t2.w == tg ? pr.b2 * 4 + 3 : g;
+          g = t2.z == tg ? pr.b2 * 4 + 2 : g;
+          g = t2.y == tg ? pr.b2 * 4 + 1 : g;
+          g = t2.x == tg ? pr.b2 * 4 + 0 : g;
+          g = t1.w == tg ? pr.b1 * 4 + 3 : g;
+          g = t1.z == tg ? pr.b1 * 4 + 2 : g;
+          g = t1.y == tg ? pr.b1 * 4 + 1 : g;
+          g = t1.x == tg ? pr.b1 * 4 + 0 : g;
+          f[j] = g;
+        }
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+          const unsigned long long kk = lkeys[f[j] != kNotFound ? f[j] : 0u];
+          const bool hit = key[j] != 0 && f[j] != kNotFound && kk == key[j];
+          found[j] = hit ? f[j] : kNotFound;
+          need[j] = key[j] != 0 && !hit;
+        }
+      } else {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         const ProbeSeq pr = probe_seq(key[j], log2cap);
@@ -808,12 +843,13 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
         found[j] = k != 0 ? f : kNotFound;
         need[j] = k != 0 && f == kNotFound;
       }
+      }
       // 5. cold path (wave-uniform): keys outside their two buckets or not yet
       //    in this workgroup's mirror
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         if (__builtin_expect(__ballot(need[j]) != 0, 0)) {
-          cold_lookup_wave(lkeys, need[j], key[j], log2cap, found[j]);
+          cold_lookup_wave(lkeys, need[j], key[j], log2cap, found[j], TAG ? ltag : nullptr);
           if constexpr (EPI) {
             if (need[j] && found[j] == kNotFound) atomicAdd(&lstat[3], 1u);
           } else {
@@ -1682,6 +1718,7 @@ static const void *small_fn(bool bt, int v, bool diag) {
       case 18: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 2>;
       case 19: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1, true>;
       case 20: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1, true, true>;
+      case 21: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1, true, true, false, true>;
       default: return (const void *)&ingest_v2_kernel<2, 2, 2, false>;
     }
   }

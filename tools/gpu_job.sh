@@ -9,6 +9,9 @@
 #   rehearse_<n>     bench.py's n-rank path (torch.distributed.run) with every
 #                    rank on this one GPU and gloo collectives (a rehearsal)
 #   bench_<wl>       a short bench of one workload (c2, c4, c4zipf), no baselines
+#   abvar_<a>_<b>..  C2 bench of laboratory-build kernel variants a, b, ... (3 rounds)
+#   streams_<wl>     bench of <wl> with 1 and with 2 launch streams (2 rounds)
+#   labtests_<v>     the small-table parity suites on laboratory-build variant v
 #   ablate_<wl>      tools/ablate.py over the ABL_FLAGS / ABL_ENVS variant set for <wl>
 #   stamps_<wl>      tools/bt_stamps.py: per-workgroup phase timeline (c4, c4zipf)
 #   sweep            C2 kernel time vs batch size (SIZES="1000000 5000000 ...")
@@ -57,6 +60,19 @@ for step in "$@"; do
     hostex_*) t=${step#hostex_}; run "hostex_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 --exemplars --events ;;
     host_*) t=${step#host_}; run "host_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 ;;
     bench_*) wl=${step#bench_}; run "bench_$wl" 300 python bench.py --workload "$wl" --sub "" --steps 20 $BQ ;;
+    abvar_*) vs=${step#abvar_}  # A/B of small-table kernel variants (laboratory build), rounds interleaved
+      for r in 1 2 3; do for v in ${vs//_/ }; do
+        SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_VARIANT=$v \
+          run "abvar_v${v}_r$r" 200 python bench.py --workload c2 --sub "" --steps 50 --soak-s 0 --no-filter-off $BQ
+      done; done ;;
+    labtests_*) v=${step#labtests_}  # small-table parity suites on a laboratory-build variant
+      SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_VARIANT=$v \
+        run "labtests_v$v" 600 python -u -m pytest tests/test_gpu_parity.py tests/test_c5_windows.py tests/test_gpu_churn.py \
+        "tests/test_gpu_regime.py::test_c2_bench_regime_40_variants_bit_exact" -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    streams_*) wl=${step#streams_}  # one launch stream against two, rounds interleaved
+      for r in 1 2; do for n in 1 2; do
+        run "streams_${wl}_s${n}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 50 --streams $n --soak-s 0 --no-filter-off $BQ
+      done; done ;;
     ablate_*) wl=${step#ablate_}; ABL_WORKLOAD=$wl ABL_VARS=${ABL_VARS:-} run "ablate_$wl" 400 python tools/ablate.py ;;
     ptrace_*) wl=${step#ptrace_}  # the rocprofv3 summary the bench line's kernel_ms is checked against:
       # a long timed region so the cold and settling launches weigh little in the average
