@@ -762,11 +762,17 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
     // the pipeline (sa_engine::bt_rec): scatter here, aggregate on agg_stream
     const uint32_t k = e->bt_set;
     if (e->agg_used[k]) SA_HIP(e, hipStreamWaitEvent(s, e->ev_agg[k], 0));  // set k's last reader
+    // (laboratory build: SPANAGG_BT_PIPE=0 runs the aggregate on the caller's stream)
+    static const bool pipe = [] {
+      const char *v = ab_env("SPANAGG_BT_PIPE");
+      return !(v && std::atoi(v) == 0);
+    }();
+    hipStream_t as = pipe ? e->agg_stream : s;
     st = sa::launch_bt_scatter(P, s);
     if (st == hipSuccess) st = hipEventRecord(e->ev_scat[k], s);
-    if (st == hipSuccess) st = hipStreamWaitEvent(e->agg_stream, e->ev_scat[k], 0);
-    if (st == hipSuccess) st = sa::launch_bt_aggregate(P, e->agg_stream);
-    if (st == hipSuccess) st = hipEventRecord(e->ev_agg[k], e->agg_stream);
+    if (st == hipSuccess && as != s) st = hipStreamWaitEvent(as, e->ev_scat[k], 0);
+    if (st == hipSuccess) st = sa::launch_bt_aggregate(P, as);
+    if (st == hipSuccess) st = hipEventRecord(e->ev_agg[k], as);
     e->agg_used[k] = true;
     e->bt_set ^= 1;
   } else if (e->part) {

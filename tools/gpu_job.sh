@@ -12,7 +12,9 @@
 #   abvar_<a>_<b>..  C2 bench of laboratory-build kernel variants a, b, ... (3 rounds)
 #   streams_<wl>     bench of <wl> with 1 and with 2 launch streams (2 rounds)
 #   labtests_<v>     the small-table parity suites on laboratory-build variant v
+#   btpipe_<wl>      bench of <wl> with the binned launch pipeline on and off (2 rounds)
 #   ablate_<wl>      tools/ablate.py over the ABL_FLAGS / ABL_ENVS variant set for <wl>
+#   c2stamps         tools/stamps.py: per-workgroup phases of the C2 kernel (STAMP_VARS variants)
 #   stamps_<wl>      tools/bt_stamps.py: per-workgroup phase timeline (c4, c4zipf)
 #   sweep            C2 kernel time vs batch size (SIZES="1000000 5000000 ...")
 #   group_<wl>       rocprofv3 --kernel-trace --stats of bench.py --group 8 (an
@@ -50,6 +52,7 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     sweep) for N in ${SIZES:-1000000 2500000 5000000 10000000 15000000}; do
         run "sweep_n$N" 200 python bench.py --sub "" --spans "$N" --steps 30 --warmup 3 $BQ; done ;;
+    c2stamps) STAMP_SETS=${STAMP_SETS:-full} STAMP_VARS=${STAMP_VARS:-20,21} run c2stamps 300 python tools/stamps.py ;;
     stamps_*) wl=${step#stamps_}; WL=$wl run "stamps_$wl" 300 python tools/bt_stamps.py ;;
     tests) run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
     tests:*) f=${step#tests:}; run "tests_$(basename "$f" .py)" 600 python -u -m pytest "$f" -m gpu -x -v --timeout 300 --timeout-method thread ;;
@@ -64,6 +67,11 @@ for step in "$@"; do
       for r in 1 2 3; do for v in ${vs//_/ }; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_VARIANT=$v \
           run "abvar_v${v}_r$r" 200 python bench.py --workload c2 --sub "" --steps 50 --soak-s 0 --no-filter-off $BQ
+      done; done ;;
+    btpipe_*) wl=${step#btpipe_}  # the binned launch pipeline on / off (laboratory build), rounds interleaved
+      for r in 1 2; do for pp in 1 0; do
+        SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_BT_PIPE=$pp \
+          run "btpipe_${wl}_p${pp}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $BQ
       done; done ;;
     labtests_*) v=${step#labtests_}  # small-table parity suites on a laboratory-build variant
       SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_VARIANT=$v \
