@@ -64,20 +64,30 @@ __global__ void sum_ptrs_u64(unsigned long long *dst, SrcPtrs src, uint32_t n, u
 // The merged dense rows [nu][nbk + 1] (bucket counts, ns sum) -> the result's
 // columns on the device: counts [nu][nbk], calls = sum of counts (A8),
 // sum_ns, and sum = sum_ns / div (IEEE division, as the host's).
+// One 32-lane half wave per row: lane b moves bucket b (b, b + 32, ...), the
+// calls are a half-wave sum (coalesced rows in and out).
 __global__ void finalize_rows_kernel(const unsigned long long *rows, uint64_t nu, uint32_t nbk,
                                      unsigned long long *counts, unsigned long long *calls,
                                      unsigned long long *sum_ns, double *sum, double div) {
-  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < nu; r += (uint64_t)gridDim.x * blockDim.x) {
+  const uint32_t b0 = threadIdx.x & 31u;
+  for (uint64_t r = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 5; r < nu;
+       r += ((uint64_t)gridDim.x * blockDim.x) >> 5) {
     const unsigned long long *row = rows + r * (nbk + 1);
     unsigned long long c = 0;
-    for (uint32_t b = 0; b < nbk; ++b) {
+    for (uint32_t b = b0; b < nbk; b += 32) {
       const unsigned long long v = row[b];
       counts[r * nbk + b] = v;
       c += v;
     }
-    calls[r] = c;
-    sum_ns[r] = row[nbk];
-    sum[r] = (double)row[nbk] / div;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1)  // (xor offsets < 32 stay inside the half wave)
+      c += (unsigned long long)(uint32_t)__shfl_xor((int)(uint32_t)c, o, 64) |
+           ((unsigned long long)(uint32_t)__shfl_xor((int)(uint32_t)(c >> 32), o, 64) << 32);
+    if (b0 == 0) {
+      calls[r] = c;
+      sum_ns[r] = row[nbk];
+      sum[r] = (double)row[nbk] / div;
+    }
   }
 }
 
@@ -190,20 +200,31 @@ __global__ __launch_bounds__(kShardBlock) void shard_scatter_kernel(sa_span_batc
   const uint64_t lo = blockIdx.x * per, hi = lo + per < in.n ? lo + per : in.n;
   constexpr uint32_t kPer = kPartChunk / kShardBlock;  // spans per thread per chunk
   for (uint64_t c0 = lo; c0 < hi; c0 += kPartChunk) {
-    // 1. loads (span c0 + tid + u * 256) and positions within the shards' runs
+    // 1. loads (spans c0 + 2 tid + {0, 1} + 512 h: 16-B loads of two spans per
+    //    u64 column, 8 B of meta) and positions within the shards' runs
     uint64_t k[kPer], s[kPer], e[kPer], a[kPer], b[kPer];
     uint32_t m[kPer], sh[kPer], rk[kPer];
 #pragma unroll
-    for (uint32_t u = 0; u < kPer; ++u) {
-      const uint64_t i = c0 + tid + u * kShardBlock;
-      const bool ok = i < hi;
-      k[u] = ok ? in.key_hash[i] : 0;
-      s[u] = ok ? in.start_ns[i] : 0;
-      e[u] = ok ? in.end_ns[i] : 0;
-      a[u] = ok ? in.trace_w0[i] : 0;
-      b[u] = ok ? in.trace_w1[i] : 0;
-      m[u] = ok ? in.meta[i] : 0;
-      sh[u] = ok ? shard_of(b[u], nm, r32) : 0xFFFFFFFFu;
+    for (uint32_t h = 0; h < kPer / 2; ++h) {
+      const uint64_t i = c0 + 2 * tid + h * 2 * kShardBlock;
+      const uint32_t u = 2 * h;
+      if (i + 1 < hi) {
+        const ulonglong2 kk = *reinterpret_cast<const ulonglong2 *>(in.key_hash + i);
+        const ulonglong2 ss = *reinterpret_cast<const ulonglong2 *>(in.start_ns + i);
+        const ulonglong2 ee = *reinterpret_cast<const ulonglong2 *>(in.end_ns + i);
+        const ulonglong2 aa = *reinterpret_cast<const ulonglong2 *>(in.trace_w0 + i);
+        const ulonglong2 bb = *reinterpret_cast<const ulonglong2 *>(in.trace_w1 + i);
+        const uint2 mm = *reinterpret_cast<const uint2 *>(in.meta + i);
+        k[u] = kk.x, k[u + 1] = kk.y, s[u] = ss.x, s[u + 1] = ss.y, e[u] = ee.x, e[u + 1] = ee.y;
+        a[u] = aa.x, a[u + 1] = aa.y, b[u] = bb.x, b[u + 1] = bb.y, m[u] = mm.x, m[u + 1] = mm.y;
+      } else {  // the range's last odd span, or nothing
+        const bool ok = i < hi;
+        k[u] = ok ? in.key_hash[i] : 0, s[u] = ok ? in.start_ns[i] : 0, e[u] = ok ? in.end_ns[i] : 0;
+        a[u] = ok ? in.trace_w0[i] : 0, b[u] = ok ? in.trace_w1[i] : 0, m[u] = ok ? in.meta[i] : 0;
+        k[u + 1] = s[u + 1] = e[u + 1] = a[u + 1] = b[u + 1] = 0, m[u + 1] = 0;
+      }
+      sh[u] = i < hi ? shard_of(b[u], nm, r32) : 0xFFFFFFFFu;
+      sh[u + 1] = i + 1 < hi ? shard_of(b[u + 1], nm, r32) : 0xFFFFFFFFu;
     }
 #pragma unroll
     for (uint32_t u = 0; u < kPer; ++u) {
@@ -877,7 +898,7 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
     unsigned long long *d_counts = fin, *d_calls = fin + nu * g->nbk, *d_sum_ns = d_calls + nu;
     double *d_sum = reinterpret_cast<double *>(d_sum_ns + nu);
     const double div = g->cfg.unit == SA_UNIT_S ? 1e9 : 1e6;
-    hipLaunchKernelGGL(finalize_rows_kernel, dim3(grid_for(nu)), dim3(256), 0, g->st[0],
+    hipLaunchKernelGGL(finalize_rows_kernel, dim3(grid_for(nu * 32)), dim3(256), 0, g->st[0],
                        static_cast<const unsigned long long *>(g->rows[0].p), nu, g->nbk, d_counts, d_calls,
                        d_sum_ns, d_sum, div);
     SG_HIP(g, hipGetLastError());

@@ -1595,7 +1595,16 @@ __global__ void compact_kernel(const unsigned long long *gkeys, unsigned long lo
     const unsigned long long k = gkeys[s];
     if (!k) continue;
     if (!row_nonzero(gcounts, s, g)) continue;
-    const unsigned long long pos = atomicAdd(out_n, 1ULL);
+    // one returning atomic per wave for its emitting lanes (a million lanes
+    // on one counter serialised the compaction of a 1 M-series table)
+    const uint64_t m = __ballot(true);
+    const int leader = __builtin_ctzll(m);
+    unsigned long long base = 0;
+    if ((int)(threadIdx.x & 63u) == leader) base = atomicAdd(out_n, (unsigned long long)__popcll(m));
+    base = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(base >> 32), leader) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, leader);
+    const unsigned long long pos =
+        base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     if (pos < out_cap) {
       if (out_keys) out_keys[pos] = k * g.kinv;
       if (out_rows) row_emit(gcounts, s, g, out_rows + pos * ostride);
@@ -1619,19 +1628,36 @@ __device__ __forceinline__ uint32_t geom_find(const unsigned long long *gkeys, u
   return g_find(gkeys, m, g.log2cap, g.max_probe);
 }
 
-// rows[i] = [nbk bucket counts, ns sum] of keys[i] (zeros if absent).
+// rows[i] = [nbk bucket counts, ns sum] of keys[i] (zeros if absent).  One
+// 32-lane half wave per key: every lane probes the same key (one broadcast
+// load per probe), then lane c moves cells c, c + 32, ... so a row's reads
+// and its dense output row are contiguous across the lanes.
 __global__ void gather_dense_kernel(const unsigned long long *gkeys, const unsigned long long *gcounts,
                                     RowGeom g, const uint64_t *keys, uint64_t n, uint64_t *rows) {
-  const uint32_t ostride = g.nbk + 1;
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
-       i += (uint64_t)gridDim.x * blockDim.x) {
+  const uint32_t nbk = g.nbk, ostride = nbk + 1, c0 = threadIdx.x & 31u;
+  for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 5; i < n;
+       i += ((uint64_t)gridDim.x * blockDim.x) >> 5) {
     const uint64_t k = keys[i];
     const uint32_t s = k ? geom_find(gkeys, k * g.kmul, g) : kNotFound;
     unsigned long long *out = reinterpret_cast<unsigned long long *>(rows) + i * ostride;
-    if (s != kNotFound) {
-      row_emit(gcounts, s, g, out);
-    } else {
-      for (uint32_t c = 0; c < ostride; ++c) out[c] = 0;
+    for (uint32_t c = c0; c < ostride; c += 32) {
+      unsigned long long v = 0;
+      if (s != kNotFound) {
+        if (g.row8) {
+          const unsigned long long *row = gcounts + (uint64_t)s * (kRowBytes / 8);
+          v = g.base64[(uint64_t)s * ostride + c] +
+              (c < nbk ? (unsigned long long)reinterpret_cast<const uint8_t *>(row + 1)[c] : row[0]);
+        } else {
+          const uint32_t stride = row_stride(nbk);
+          const unsigned long long *row = gcounts + (uint64_t)s * stride;
+          if (c < nbk) {
+            v = row[row_count_cell(c)];
+          } else {
+            for (uint32_t q = 0; q < stride; q += 8) v += row[q];
+          }
+        }
+      }
+      out[c] = v;
     }
   }
 }
@@ -1883,7 +1909,7 @@ hipError_t launch_gather_dense(const unsigned long long *gkeys, const unsigned l
                                hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint32_t block = 256;
-  hipLaunchKernelGGL(gather_dense_kernel, dim3(grid_for(n, block, 4096)), dim3(block), 0, s,
+  hipLaunchKernelGGL(gather_dense_kernel, dim3(grid_for(n * 32, block, 8192)), dim3(block), 0, s,  // (32 lanes a key)
                      gkeys, gcounts, g, keys, n, rows);
   return hipGetLastError();
 }
