@@ -45,6 +45,20 @@ const char *ab_env(const char *name) { return std::getenv(name); }
 constexpr const char *ab_env(const char *) { return nullptr; }
 #endif
 
+// The engine's ordering events only order its own launches, copies and
+// reads on this device (cross-stream waits, slab-set and record-set reuse),
+// so they release at device scope: a default event ends with a system-scope
+// fence (L2 write-back and invalidate) that the next launch on the stream
+// waits behind and starts cold after.  (Laboratory build: SPANAGG_EV_SYS=1
+// restores the default for A/B runs.)
+unsigned ev_flags() {
+  static const unsigned f = [] {
+    const char *v = ab_env("SPANAGG_EV_SYS");
+    return (v && std::atoi(v) != 0) ? hipEventDisableTiming : (hipEventDisableTiming | hipEventReleaseToDevice);
+  }();
+  return f;
+}
+
 bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
 uint32_t log2u(uint64_t x) { return 63u - (uint32_t)__builtin_clzll(x); }
 uint64_t next_pow2(uint64_t x) {
@@ -356,12 +370,12 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   // A blocking stream: it orders against the legacy null stream, so callers
   // that produce batches on the null stream (stream == NULL) stay race-free.
   if (hipStreamCreateWithFlags(&e->stream, hipStreamDefault) != hipSuccess ||
-      hipEventCreateWithFlags(&e->ev_a, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&e->ev_b, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&e->ev_ctl, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&e->ev_a, ev_flags()) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_b, ev_flags()) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_ctl, ev_flags()) != hipSuccess)
     return bail(fail(e, SA_EDEVICE, "stream/event creation failed"));
   for (hipEvent_t &ev : e->ev_set)
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)
+    if (hipEventCreateWithFlags(&ev, ev_flags()) != hipSuccess)
       return bail(fail(e, SA_EDEVICE, "event creation failed"));
 
   // buckets of 4 slots with two choices stay well-behaved up to ~90% load:
@@ -499,8 +513,8 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     if (hipStreamCreateWithFlags(&e->agg_stream, hipStreamNonBlocking) != hipSuccess)
       return bail(fail(e, SA_EDEVICE, "aggregate stream creation failed"));
     for (int k = 0; k < 2; ++k)
-      if (hipEventCreateWithFlags(&e->ev_scat[k], hipEventDisableTiming) != hipSuccess ||
-          hipEventCreateWithFlags(&e->ev_agg[k], hipEventDisableTiming) != hipSuccess)
+      if (hipEventCreateWithFlags(&e->ev_scat[k], ev_flags()) != hipSuccess ||
+          hipEventCreateWithFlags(&e->ev_agg[k], ev_flags()) != hipSuccess)
         return bail(fail(e, SA_EDEVICE, "event creation failed"));
     // a random odd multiplier per engine: series ids -> stored ids (bins and
     // home slots), so bin occupancy does not depend on ids a sender chooses

@@ -12,6 +12,7 @@
 #   abvar_<a>_<b>..  C2 bench of laboratory-build kernel variants a, b, ... (3 rounds)
 #   streams_<wl>     bench of <wl> with 1 and with 2 launch streams (2 rounds)
 #   labtests_<v>     the small-table parity suites on laboratory-build variant v
+#   evscope_<wl>     bench of <wl> with the engine's events at device / system scope (2 rounds)
 #   btpipe_<wl>      bench of <wl> with the binned launch pipeline on and off (2 rounds)
 #   ablate_<wl>      tools/ablate.py over the ABL_FLAGS / ABL_ENVS variant set for <wl>
 #   c2stamps         tools/stamps.py: per-workgroup phases of the C2 kernel (STAMP_VARS variants)
@@ -72,6 +73,11 @@ for step in "$@"; do
       for r in 1 2; do for pp in 1 0; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_BT_PIPE=$pp \
           run "btpipe_${wl}_p${pp}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $BQ
+      done; done ;;
+    evscope_*) wl=${step#evscope_}  # engine events at device scope (default) / system scope (laboratory build)
+      for r in 1 2; do for es in 0 1; do
+        SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_EV_SYS=$es \
+          run "evscope_${wl}_sys${es}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 50 --soak-s 0 --no-filter-off $BQ
       done; done ;;
     labtests_*) v=${step#labtests_}  # small-table parity suites on a laboratory-build variant
       SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_VARIANT=$v \
