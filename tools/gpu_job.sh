@@ -13,6 +13,7 @@
 #   streams_<wl>     bench of <wl> with 1 and with 2 launch streams (2 rounds)
 #   labtests_<v>     the small-table parity suites on laboratory-build variant v
 #   evscope_<wl>     bench of <wl> with the engine's events at device / system scope (2 rounds)
+#   labtrace_<wl>_<VAR=v>  rocprofv3 trace of a 100-step bench of <wl> on the laboratory build with VAR=v
 #   btpipe_<wl>      bench of <wl> with the binned launch pipeline on and off (2 rounds)
 #   ablate_<wl>      tools/ablate.py over the ABL_FLAGS / ABL_ENVS variant set for <wl>
 #   c2stamps         tools/stamps.py: per-workgroup phases of the C2 kernel (STAMP_VARS variants)
@@ -97,6 +98,11 @@ for step in "$@"; do
       (cd /tmp && run "group_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/group_$wl" -o run \
          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --group 8 --steps 20 --warmup 3 --soak-s 0 \
          --no-filter-off $BQ) || exit $? ;;
+    labtrace_*) rest=${step#labtrace_}; wl=${rest%%_*}; knob=${rest#*_}  # e.g. labtrace_c4_SPANAGG_BT_PIPE=0
+      (export SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so; export "$knob"; cd /tmp && \
+       run "labtrace_${wl}_${knob//=/}" 300 rocprofv3 --kernel-trace --stats --output-format csv \
+         -d "$OUT/labtrace_${wl}_${knob//=/}" -o run \
+         -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 100 --streams 1 --soak-s 0 --no-filter-off $BQ) || exit $? ;;
     trace_*) wl=${step#trace_}
       (cd /tmp && run "trace_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$wl" -o run \
          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 10 --warmup 2 --streams 1 --soak-s 0 --no-filter-off $BQ) || exit $? ;;
