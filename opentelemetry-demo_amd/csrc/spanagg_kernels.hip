@@ -84,8 +84,8 @@ __device__ __forceinline__ void flush_lds(const IngestParams &P, uint32_t cap, u
 // sums, ERROR cells, HLL CAS, bound refresh: ~7 in a row).  A stale HLL word
 // only makes the CAS retry; a stale register read for the bound can only lower
 // it, which keeps it a lower bound.
-template <int UPT, int SPT>
-__device__ __forceinline__ void v2_epilogue(const IngestParams &P, uint32_t cap, uint32_t nw, uint32_t log2cap,
+template <int UPT, int SPT, typename PT>
+__device__ __forceinline__ void v2_epilogue(const PT &P, uint32_t cap, uint32_t nw, uint32_t log2cap,
                                             const unsigned long long *lsum, const uint32_t *lcnt,
                                             const uint32_t *etab, bool err_lds, const uint2 *hq,
                                             uint32_t nq) {
@@ -661,7 +661,9 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   {
   }
   etab[threadIdx.x] = 0;  // kErrTab == kLdsBlock
-  if (lb_on && threadIdx.x * 4 < P.lb_n) reinterpret_cast<uint32_t *>(llb)[threadIdx.x] = lbw;
+  // (filter off: the first bound word stays 0, and every span's sub-block
+  // index is 0 or 1 below, so no rho can be at or below it)
+  if (threadIdx.x * 4 < (lb_on ? P.lb_n : 4u)) reinterpret_cast<uint32_t *>(llb)[threadIdx.x] = lbw;
   __syncthreads();
   if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 1] = __builtin_amdgcn_s_memrealtime();
 
@@ -680,6 +682,10 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   };
   stamp(-1);
   const __amdgpu_buffer_rsrc_t hll_rsrc = rsrc(P.hll, 0xFFFFFFFFu);
+  // the bound's shift as a VGPR operand (31 with the filter off): a loop-long
+  // scalar here was one of the kernel's SGPR spills, read back by a
+  // v_readlane on every span
+  const uint32_t lbs_v = copy_u32(lb_on ? P.lb_shift : 31u);
   constexpr uint32_t kHotUnset = 0xFFFFFFFEu;
   uint32_t hot_slot = kHotUnset;  // wave-uniform (see step 5b)
   unsigned long long hot_sum = 0;
@@ -766,7 +772,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
         }
         const uint32_t ho = sk ? (row << hp) + idx : 0u;
         // a rho at or below the register sub-block's lower bound cannot raise it
-        const bool up = sk && !(lb_on && r <= llb[ho >> P.lb_shift]);
+        const bool up = sk && !(r <= llb[ho >> lbs_v]);
         if constexpr (EPI) n_filt += (sk && !up) ? 1u : 0u;
         rho[j] = up ? r : 0u;
         hoff[j] = up ? ho : 0u;
@@ -892,7 +898,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
         } else {
           const uint32_t ek = (ws[j] << log2cap) | found[j];
           if (!(err_lds && lds_err_add(etab, ek)))
-            atomicAdd(P.errcnt + ((uint64_t)ws[j] << log2cap) + found[j], 1ULL);
+            atomicAdd(cold_params().errcnt + ((uint64_t)ws[j] << log2cap) + found[j], 1ULL);
         }
       }
     }
@@ -1014,8 +1020,11 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     n_filt = wave_sum(n_filt);
     if ((threadIdx.x & 63) == 0 && n_filt) atomicAdd(&hq_n[2], n_filt);
   }
-  const uint64_t wave_loop_end = P.dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 2] = __builtin_amdgcn_s_memrealtime();
+  // (parameters used only after the loop are read through the laundered
+  // kernarg pointer, so they do not hold SGPRs across it)
+  unsigned long long *const dbg = cold_params().dbg;
+  const uint64_t wave_loop_end = dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+  if (dbg && threadIdx.x == 0) dbg[blockIdx.x * kDbgPerWg + 2] = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
   const uint32_t nq = *hq_n < kHllQueue ? *hq_n : kHllQueue;
   if constexpr (EXPO) {
@@ -1037,8 +1046,8 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     // compile-time geometry: the batched epilogue (one round trip)
     constexpr uint32_t kCap = 1u << LC;
     static_assert((kCap * NWC / 2) % kLdsBlock == 0 && (kCap / 2) % kLdsBlock == 0, "epilogue geometry");
-    v2_epilogue<kCap * NWC / 2 / kLdsBlock, kCap / 2 / kLdsBlock>(P, cap, nw, log2cap, lsum, lcnt, etab, err_lds,
-                                                                    hq, nq);
+    v2_epilogue<kCap * NWC / 2 / kLdsBlock, kCap / 2 / kLdsBlock>(cold_params(), cap, nw, log2cap, lsum, lcnt, etab,
+                                                                    err_lds, hq, nq);
   } else {
     flush_lds(P, cap, nw, lsum, lcnt);
     if (err_lds) {  // this workgroup's ERROR counts -> its private slab (plain RMW)
@@ -1051,25 +1060,27 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     for (uint32_t i = threadIdx.x; i < nq; i += kLdsBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
     hll_lb_refresh(P, threadIdx.x >> 6, kWaves);
   }
-  if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 3] = __builtin_amdgcn_s_memrealtime();
-  if (P.dbg && (threadIdx.x & 63) == 0) {
-    for (int i = 0; i < 6 && DIAG; ++i) P.dbg[blockIdx.x * kDbgPerWg + 8 + (threadIdx.x >> 6) * 8 + i] = seg[i];
-    P.dbg[blockIdx.x * kDbgPerWg + 8 + (threadIdx.x >> 6) * 8 + 6] = wave_loop_end;
+  if (dbg && threadIdx.x == 0) dbg[blockIdx.x * kDbgPerWg + 3] = __builtin_amdgcn_s_memrealtime();
+  if (dbg && (threadIdx.x & 63) == 0) {
+    for (int i = 0; i < 6 && DIAG; ++i) dbg[blockIdx.x * kDbgPerWg + 8 + (threadIdx.x >> 6) * 8 + i] = seg[i];
+    dbg[blockIdx.x * kDbgPerWg + 8 + (threadIdx.x >> 6) * 8 + 6] = wave_loop_end;
   }
   if constexpr (EPI) {  // (lstat is final: the epilogue follows a workgroup barrier)
     if (threadIdx.x < 4 && lstat[threadIdx.x]) {
       constexpr uint32_t kIdx[4] = {kStatZeroKey, kStatInvalidService, kStatWindowOOR, kStatDropped};
-      atomicAdd(&P.stats[kIdx[threadIdx.x]], (unsigned long long)lstat[threadIdx.x]);
+      atomicAdd(&cold_params().stats[kIdx[threadIdx.x]], (unsigned long long)lstat[threadIdx.x]);
     }
     // (a slot per workgroup: thousands of same-address atomics at the end of
     // every launch would serialise its tail)
-    if (threadIdx.x == 0 && hq_n[2]) atomicAdd(&P.hll_filt[blockIdx.x & (kFiltSlots - 1)], (unsigned long long)hq_n[2]);
+    if (threadIdx.x == 0 && hq_n[2])
+      atomicAdd(&cold_params().hll_filt[blockIdx.x & (kFiltSlots - 1)], (unsigned long long)hq_n[2]);
   }
   if ((threadIdx.x & 63) == 0) {
-    if (n_zero) atomicAdd(&P.stats[kStatZeroKey], (unsigned long long)n_zero);
-    if (n_badsvc) atomicAdd(&P.stats[kStatInvalidService], (unsigned long long)n_badsvc);
-    if (n_oor) atomicAdd(&P.stats[kStatWindowOOR], (unsigned long long)n_oor);
-    if (n_drop) atomicAdd(&P.stats[kStatDropped], (unsigned long long)n_drop);
+    unsigned long long *const stats = cold_params().stats;
+    if (n_zero) atomicAdd(&stats[kStatZeroKey], (unsigned long long)n_zero);
+    if (n_badsvc) atomicAdd(&stats[kStatInvalidService], (unsigned long long)n_badsvc);
+    if (n_oor) atomicAdd(&stats[kStatWindowOOR], (unsigned long long)n_oor);
+    if (n_drop) atomicAdd(&stats[kStatDropped], (unsigned long long)n_drop);
   }
 }
 
