@@ -393,7 +393,7 @@ __device__ __forceinline__ uint32_t window_slot(const IngestParams &P, uint64_t 
 // v_mad_u64_u32 plus a 24-bit multiply-add for the high word (q < 2^24 inside
 // the ring, window_ns < 2^56 -- checked by the host), and the +-1 correction
 // from the remainder's sign and size.
-__device__ __forceinline__ uint32_t window_slot_lean(const IngestParams &P, uint64_t end) {
+__device__ __forceinline__ uint32_t window_slot_lean(const IngestParams &P, uint64_t end, uint32_t win_mask) {
   const uint64_t delta = end - P.base_ns;  // wraps (huge) for end < base
   float fh, fl;
   asm("v_cvt_f32_u32 %0, %1" : "=v"(fh) : "v"((uint32_t)(delta >> 32)));
@@ -406,7 +406,10 @@ __device__ __forceinline__ uint32_t window_slot_lean(const IngestParams &P, uint
   const uint32_t neg = (uint32_t)((int32_t)(r >> 32) >> 31);  // r < 0: q one too high (then r >= W too)
   const uint32_t big = r >= P.window_ns ? 1u : 0u;            // r >= W: q one too low
   const uint32_t qq = q + big + (neg << 1);
-  return delta < P.ring_ns ? ((P.base_slot + qq) & P.win_mask) : 0xFFFFFFFFu;
+  return delta < P.ring_ns ? ((P.base_slot + qq) & win_mask) : 0xFFFFFFFFu;
+}
+__device__ __forceinline__ uint32_t window_slot_lean(const IngestParams &P, uint64_t end) {
+  return window_slot_lean(P, end, P.win_mask);
 }
 
 // Bucket via the LDS bin table (BK = 1) or linear thresholds (BK = 0).

@@ -686,6 +686,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   // scalar here was one of the kernel's SGPR spills, read back by a
   // v_readlane on every span
   const uint32_t lbs_v = copy_u32(lb_on ? P.lb_shift : 31u);
+  const uint32_t wmask_v = copy_u32(P.win_mask);  // (likewise the ring mask of every span's window slot)
   constexpr uint32_t kHotUnset = 0xFFFFFFFEu;
   uint32_t hot_slot = kHotUnset;  // wave-uniform (see step 5b)
   unsigned long long hot_sum = 0;
@@ -730,7 +731,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
       const uint32_t meta = copy_u32(T.meta[j]);  // see key
       const uint32_t svc = meta & 0xFFFFu;
       const bool svc_ok = svc < P.n_services;
-      ws[j] = (diag & 64u) ? (uint32_t)(T.e[j] >> 34) & 7u : LEAN ? window_slot_lean(P, T.e[j]) : window_slot(P, T.e[j]);
+      ws[j] = (diag & 64u) ? (uint32_t)(T.e[j] >> 34) & 7u : LEAN ? window_slot_lean(P, T.e[j], wmask_v) : window_slot(P, T.e[j]);
       const bool win_ok = ws[j] != 0xFFFFFFFFu;
       if (!(diag & 128u)) {
         if constexpr (EPI) {
