@@ -736,7 +736,7 @@ __global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
 // MODE (ablation): 1 = no records aggregated, 2 = no key / row write-back,
 // 16 = no lookup reads, 32 = no counter atomics.
 template <int MODE = 0, int MAXPER = 2, int BLOCK = 512>
-__global__ __launch_bounds__(BLOCK, 6) void bt_aggregate3_kernel(IngestParams P) {
+__global__ __launch_bounds__(BLOCK, BLOCK == 1024 ? 8 : 6) void bt_aggregate3_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t log2sb = P.log2sb, sb = 1u << log2sb;
   const uint32_t G = P.bt_grid, bin = blockIdx.x, region = P.bt_region;
@@ -1050,9 +1050,21 @@ static bool bt_agg_v2() {  // SPANAGG_BT_AGG=2: the second-form aggregate (A/B r
   }();
   return v2;
 }
+// SPANAGG_BT_AGG_BLOCK=1024: 1,024-thread aggregate workgroups, two per CU
+// (512 resident bins: the 2,048 bins in four full rounds instead of 2.67)
+static uint32_t bt_agg_block() {
+  static const uint32_t b = [] {
+    const char *v = std::getenv("SPANAGG_BT_AGG_BLOCK");
+    return v && std::atoi(v) == 1024 ? 1024u : kBtAgg2Block;
+  }();
+  return b;
+}
 static const void *bt_agg_fn(uint32_t diag) {
   const int mode = ((diag & 1u) ? 1 : 0) | ((diag & kDiagBtAggNoRows) ? 2 : 0) |
                    ((diag & kDiagBtAggNoLookup) ? 16 : 0) | ((diag & kDiagBtAggNoAtomics) ? 32 : 0);
+  if (bt_agg_block() == 1024 && mode == 0 && !(diag & kDiagBtAggLoadOnly) && !bt_agg_v2())
+    return (diag & kDiagBtAggWide) ? (const void *)&bt_aggregate3_kernel<0, 2, 1024>
+                                   : (const void *)&bt_aggregate3_kernel<0, 1, 1024>;
   if (!bt_agg_v2() && !(diag & kDiagBtAggLoadOnly)) {
     if (mode & 48) switch (mode) {  // ablations of the record loop
         case 16: return (const void *)&bt_aggregate3_kernel<16, 2>;
@@ -1123,7 +1135,8 @@ hipError_t prepare_ingest_bt(size_t agg_lds) {
   for (uint32_t d : {0u, 1u, kDiagBtAggNoRows, 1u | kDiagBtAggNoRows, kDiagBtAggNoLookup, kDiagBtAggNoAtomics,
                      kDiagBtAggNoLookup | kDiagBtAggNoAtomics})
     for (uint32_t v : {0u, kDiagBtAggWide, kDiagBtAggLoadOnly})
-      for (const void *fn : {bt_agg_fn(d | v), bt_agg2_fn(d | v)})
+      for (const void *fn : {bt_agg_fn(d | v), bt_agg2_fn(d | v), (const void *)&bt_aggregate3_kernel<0, 1, 1024>,
+                             (const void *)&bt_aggregate3_kernel<0, 2, 1024>})
         if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)agg_lds);
             e != hipSuccess)
           return e;
@@ -1134,6 +1147,7 @@ hipError_t prepare_ingest_bt(size_t agg_lds) {
 
 #ifndef SPANAGG_AB
 constexpr uint32_t kDiagBtNoScatter = 0, kDiagBtNoAgg = 0;
+static uint32_t bt_agg_block() { return kBtAgg2Block; }
 #endif
 
 hipError_t launch_bt_scatter(const IngestParams &P, hipStream_t s) {
@@ -1146,7 +1160,7 @@ hipError_t launch_bt_aggregate(const IngestParams &P, hipStream_t s) {
   if (P.diag & kDiagBtNoAgg) return hipSuccess;
   void *args[] = {const_cast<IngestParams *>(&P)};
   const uint32_t diag = P.diag | (P.log2sb > 10 ? kDiagBtAggWide : 0u);
-  return hipLaunchKernel(bt_agg_fn(diag), dim3(kPartBins), dim3(kBtAgg2Block), args,
+  return hipLaunchKernel(bt_agg_fn(diag), dim3(kPartBins), dim3(bt_agg_block()), args,
                          bt_agg2_lds_bytes(P.log2sb, P.bt_grid), s);
 }
 

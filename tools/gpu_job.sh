@@ -12,6 +12,8 @@
 #   abvar_<a>_<b>..  C2 bench of laboratory-build kernel variants a, b, ... (3 rounds)
 #   streams_<wl>     bench of <wl> with 1 and with 2 launch streams (2 rounds)
 #   labtests_<v>     the small-table parity suites on laboratory-build variant v
+#   btagg_<wl>       bench of <wl> with 512- and 1,024-thread aggregate workgroups (2 rounds)
+#   labbin_<KNOB=v>  the binned parity suites on the laboratory build with KNOB=v
 #   evscope_<wl>     bench of <wl> with the engine's events at device / system scope (2 rounds)
 #   labtrace_<wl>_<VAR=v>  rocprofv3 trace of a 100-step bench of <wl> on the laboratory build with VAR=v
 #   btpipe_<wl>      bench of <wl> with the binned launch pipeline on and off (2 rounds)
@@ -75,6 +77,15 @@ for step in "$@"; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_BT_PIPE=$pp \
           run "btpipe_${wl}_p${pp}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $BQ
       done; done ;;
+    btagg_*) wl=${step#btagg_}  # aggregate workgroups of 512 / 1,024 threads (laboratory build), rounds interleaved
+      for r in 1 2; do for bb in 512 1024; do
+        SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_BT_AGG_BLOCK=$bb \
+          run "btagg_${wl}_b${bb}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $BQ
+      done; done ;;
+    labbin_*) knob=${step#labbin_}  # the binned parity suite on the laboratory build with one knob, e.g. labbin_SPANAGG_BT_AGG_BLOCK=1024
+      (export SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so; export "$knob"; \
+       run "labbin_${knob//=/}" 600 python -u -m pytest tests/test_gpu_binned.py "tests/test_gpu_regime.py" -m gpu -x -v \
+         --timeout 300 --timeout-method thread) || exit $? ;;
     evscope_*) wl=${step#evscope_}  # engine events at device scope (default) / system scope (laboratory build)
       for r in 1 2; do for es in 0 1; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_EV_SYS=$es \
