@@ -9,6 +9,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <functional>
+#include <chrono>
 #include <mutex>
 #include <thread>
 
@@ -1166,6 +1167,11 @@ BatchResult Columnizer::columnize_batch(const uint8_t *const *bufs, const size_t
     w->cols.clear();
     if (w->cache.gen != gen_) w->cache.clear(), w->cache.gen = gen_;
   }
+  using clk = std::chrono::steady_clock;
+  const auto ns_since = [](clk::time_point t) {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t).count();
+  };
+  auto t_ph = clk::now();
   // phase 1: decode in parallel against the dictionaries as they stand
   std::atomic<size_t> next{0};
   const std::function<void(unsigned)> decode = [&](unsigned wid) {
@@ -1190,6 +1196,8 @@ BatchResult Columnizer::columnize_batch(const uint8_t *const *bufs, const size_t
     }
   };
   pool_->run(T, decode);
+  br.ns_decode = ns_since(t_ph);
+  t_ph = clk::now();
   // phase 2, in request order: what phase 1 could not take is redone exclusively
   excl_.clear();
   size_t taken = n, total = 0;
@@ -1212,6 +1220,8 @@ BatchResult Columnizer::columnize_batch(const uint8_t *const *bufs, const size_t
       break;
     }
   }
+  br.ns_commit = ns_since(t_ph);
+  t_ph = clk::now();
   // phase 3: every request's columns to its place in the buffer, in parallel
   const size_t base = buf_.size();
   buf_.reserve(base + total);
@@ -1231,6 +1241,7 @@ BatchResult Columnizer::columnize_batch(const uint8_t *const *bufs, const size_t
     }
   };
   pool_->run(T, place);
+  br.ns_place = ns_since(t_ph);
   br.results.reserve(taken);
   for (size_t i = 0; i < taken; ++i) br.results.push_back(std::move(slots[i].r));
   br.done = taken;

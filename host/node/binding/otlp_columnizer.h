@@ -105,6 +105,10 @@ struct Result {
 struct BatchResult {
   std::vector<Result> results;  // one per request taken, in order
   size_t done = 0;              // requests taken: all, or up to and including the first fallback
+  // wall time of the three phases (threaded calls): the parallel decode, the
+  // in-order commit (exclusive redos, exemplar acceptance) and the parallel
+  // copy into the column buffer
+  uint64_t ns_decode = 0, ns_commit = 0, ns_place = 0;
 };
 
 // Column storage.  The columnizer's output buffer asks for page-locked host

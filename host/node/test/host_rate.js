@@ -4,7 +4,7 @@
  * transform rules -> keying -> SoA columns -> addon.ingest.  SURVEY.md 8(d)
  * asks for the OTLP decode+aggregate rate from protobuf bytes.
  *
- *   node test/host_rate.js [spans] [--gpu] [--threads T] [--batch B] [--exemplars] [--events]
+ *   node test/host_rate.js [spans] [--gpu] [--threads T] [--batch B] [--exemplars] [--events] [--dump FILE]
  *
  * --threads T --batch B: requests go through consumeTracesBatch B at a time
  * (what the pipeline's queue does under load), decoded on T columnizer
@@ -60,6 +60,21 @@ function makeRequests() {
 
 const reqs = makeRequests();
 const bytes = reqs.reduce((a, b) => a + b.length, 0);
+// --dump FILE: write the requests (u32 little-endian length + bytes each) for
+// tools/colbench (the columnizer alone, profiled natively) and exit
+const dumpAt = process.argv.indexOf('--dump');
+if (dumpAt > 0) {
+  const fs = require('fs');
+  const parts = [];
+  for (const r of reqs) {
+    const len = Buffer.alloc(4);
+    len.writeUInt32LE(r.length, 0);
+    parts.push(len, Buffer.from(r.buffer, r.byteOffset, r.length));
+  }
+  fs.writeFileSync(process.argv[dumpAt + 1], Buffer.concat(parts));
+  console.log(JSON.stringify({ dumped: reqs.length, spans: n, otlp_bytes: bytes }));
+  process.exit(0);
+}
 let addon;
 if (gpu) {
   addon = require(path.join(lib, 'addon')).load();

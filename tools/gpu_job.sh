@@ -14,6 +14,7 @@
 #   labtests_<v>     the small-table parity suites on laboratory-build variant v
 #   btagg_<wl>       bench of <wl> with 512- and 1,024-thread aggregate workgroups (2 rounds)
 #   labbin_<KNOB=v>  the binned parity suites on the laboratory build with KNOB=v
+#   colbench         the native columnizer alone (host/node/build/colbench) at 1-16 threads
 #   evscope_<wl>     bench of <wl> with the engine's events at device / system scope (2 rounds)
 #   labtrace_<wl>_<VAR=v>  rocprofv3 trace of a 100-step bench of <wl> on the laboratory build with VAR=v
 #   btpipe_<wl>      bench of <wl> with the binned launch pipeline on and off (2 rounds)
@@ -64,6 +65,10 @@ for step in "$@"; do
     rehearse_*) n=${step#rehearse_}; SPANAGG_BENCH_ONE_DEVICE=1 run "rehearse_n$n" 400 python -m torch.distributed.run \
         --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus "$n" --steps 10 \
         --warmup 2 --settle 4 --soak-s 0 ;;
+    colbench) (cd host/node && node test/host_rate.js 2000000 --dump /tmp/req_plain.bin > /dev/null && \
+        node test/host_rate.js 2000000 --events --dump /tmp/req_ev.bin > /dev/null) || exit 1
+      for t in ${COL_THREADS:-1 4 8 16}; do run "colbench_t$t" 120 host/node/build/colbench /tmp/req_plain.bin --threads "$t"; done
+      run colbench_ex_t16 120 host/node/build/colbench /tmp/req_ev.bin --threads 16 --exemplars --events ;;
     hostex_*) t=${step#hostex_}; run "hostex_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 --exemplars --events ;;
     host_*) t=${step#host_}; run "host_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 ;;
     bench_*) wl=${step#bench_}; run "bench_$wl" 300 python bench.py --workload "$wl" --sub "" --steps 20 $BQ ;;
