@@ -903,8 +903,8 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
         }
         PB sp = ss.sub();
         const uint8_t *span_begin = sp.p, *span_end = sp.end;
-        const uint8_t *tid = nullptr;
-        size_t tid_len = 0;
+        const uint8_t *tid = nullptr, *spid = nullptr;
+        size_t tid_len = 0, spid_len = 0;
         std::string_view name;
         int32_t kind = 0, code = 0;
         uint64_t st = 0, en = 0;
@@ -917,6 +917,10 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
             const std::string_view t = sp.str();
             tid = reinterpret_cast<const uint8_t *>(t.data());
             tid_len = t.size();
+          } else if (k == 2 && wt4 == 2 && opt_.exemplars) {
+            const std::string_view t = sp.str();
+            spid = reinterpret_cast<const uint8_t *>(t.data());
+            spid_len = t.size();
           } else if (k == 5 && wt4 == 2) {
             name = sp.str();
           } else if (k == 6 && wt4 == 0) {
@@ -1034,7 +1038,14 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
             uint32_t &mine = w.exl[sid];
             if (taken + mine < opt_.exemplars_max) {
               ++mine;
-              res.exemplars.push_back({sid, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});
+              SpanRef x{sid, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)};
+              if (tid && tid_len == 16 && spid && spid_len == 8) {
+                x.ids_ok = true;
+                std::memcpy(x.ids, tid, 16);
+                std::memcpy(x.ids + 16, spid, 8);
+                x.start = st, x.end = en;
+              }
+              res.exemplars.push_back(x);
             }
           } else if (hit) {
             hit->ex_full = ex_gen_;

@@ -77,6 +77,11 @@ struct NewSeries {
 struct SpanRef {
   uint64_t sid;
   uint32_t span_off, span_len;
+  // exemplars: the span's fields an exemplar carries, when its trace id is 16
+  // bytes and its span id 8 (ids_ok; else the host decodes the span itself)
+  bool ids_ok = false;
+  uint8_t ids[24] = {};  // trace id, then span id
+  uint64_t start = 0, end = 0;
 };
 struct NewEventSeries {
   uint64_t sid, res_hash;

@@ -789,12 +789,27 @@ napi_value result_obj(napi_env env, const otlpcol::Result &r, bool lean) {
   }
   if (!lean || !r.exemplars.empty()) {
     napi_create_array_with_length(env, r.exemplars.size(), &arr);
+    // the exemplars' ids as views of one buffer (the host keeps them as is)
+    napi_value ab = nullptr;
+    uint8_t *abd = nullptr;
+    if (!r.exemplars.empty()) napi_create_arraybuffer(env, 24 * r.exemplars.size(), (void **)&abd, &ab);
     for (size_t i = 0; i < r.exemplars.size(); ++i) {
+      const otlpcol::SpanRef &x = r.exemplars[i];
       napi_value e;
       napi_create_object(env, &e);
-      set(env, e, "sid", big(env, r.exemplars[i].sid));
-      set(env, e, "off", num(env, r.exemplars[i].span_off));
-      set(env, e, "len", num(env, r.exemplars[i].span_len));
+      set(env, e, "sid", big(env, x.sid));
+      set(env, e, "off", num(env, x.span_off));
+      set(env, e, "len", num(env, x.span_len));
+      if (x.ids_ok && abd) {  // else the host decodes the span from off / len
+        std::memcpy(abd + 24 * i, x.ids, 24);
+        napi_value tv, sv;
+        napi_create_typedarray(env, napi_uint8_array, 16, ab, 24 * i, &tv);
+        napi_create_typedarray(env, napi_uint8_array, 8, ab, 24 * i + 16, &sv);
+        set(env, e, "traceId", tv);
+        set(env, e, "spanId", sv);
+        set(env, e, "start", big(env, x.start));
+        set(env, e, "end", big(env, x.end));
+      }
       napi_set_element(env, arr, (uint32_t)i, e);
     }
     set(env, o, "exemplars", arr);
@@ -1056,6 +1071,20 @@ napi_value ColumnizerSelfTest(napi_env env, napi_callback_info info) {
   return throw_status(env, SA_EINVAL, "unknown self-test");
 }
 
+// xxh64(bytes, seed) -> BigInt: the host's series and resource ids (keys.js
+// uses it once the addon is loaded; its BigInt restatement costs tens of
+// microseconds per key, which made the discovery of new series the host's
+// main JavaScript cost)
+napi_value Xxh64(napi_env env, napi_callback_info info) {
+  napi_value argv[2];
+  if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
+  void *d;
+  size_t n;
+  uint64_t seed;
+  if (!typed(env, argv[0], napi_uint8_array, &d, &n, "data") || !to_u64(env, argv[1], &seed, "seed")) return nullptr;
+  return big(env, otlpcol::xxh64(d, n, seed));
+}
+
 // page-locked column buffers for the native columnizer (sa_ingest then DMAs
 // them without a staging copy); nullptr -> the columnizer uses the heap
 void *host_alloc_hook(size_t bytes) {
@@ -1093,7 +1122,8 @@ napi_value Init(napi_env env, napi_value exports) {
                {"columnizerForget", ColumnizerForget},
                {"columnizerLearn", ColumnizerLearn},
                {"columnizerRemap", ColumnizerRemap},
-               {"columnizerSelfTest", ColumnizerSelfTest}};
+               {"columnizerSelfTest", ColumnizerSelfTest},
+               {"xxh64", Xxh64}};
     for (auto &f : fns) {
         napi_value v;
         if (napi_create_function(env, f.name, NAPI_AUTO_LENGTH, f.cb, nullptr, &v) != napi_ok ||

@@ -19,6 +19,7 @@ function load() {
     e.cause = err;
     throw e;
   }
+  if (typeof cached.xxh64 === 'function') require('./keys').useNativeXxh64(cached.xxh64);
   return cached;
 }
 

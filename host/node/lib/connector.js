@@ -572,7 +572,10 @@ class SpanMetricsConnector {
     if (r.eventRecords) this.eventRecords += r.eventRecords;
     for (const ex of r.exemplars || NONE) {  // exemplars.enabled: the native side's candidates, in order
       const sid = remapped && remapped.has(ex.sid) ? remapped.get(ex.sid) : ex.sid;
-      if (this.series.has(sid)) this._exemplar(sid, otlp.decodeSpanExemplar(new otlp.Reader(bytes, ex.off, ex.off + ex.len)));
+      if (!this.series.has(sid)) continue;
+      // the native side reports the fields of a span with 16-B trace and 8-B span ids
+      this._exemplar(sid, ex.traceId ? { traceId: ex.traceId, spanId: ex.spanId, startTimeUnixNano: ex.start,
+        endTimeUnixNano: ex.end } : otlp.decodeSpanExemplar(new otlp.Reader(bytes, ex.off, ex.off + ex.len)));
     }
     return true;
   }

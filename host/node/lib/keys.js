@@ -12,7 +12,13 @@
  * 'string' | 'bool' | 'int' (BigInt) | 'double' | 'bytes' (Uint8Array) |
  * 'array' (AnyValue[]) | 'kvlist' ({key, value}[]) | 'empty'.
  */
-const { xxh64 } = require('./xxh64');
+const xxh64js = require('./xxh64').xxh64;
+
+// The addon's native xxh64 once addon.js has loaded it (same function: the
+// addon's self-test checks the two against each other); the JavaScript BigInt
+// restatement stays for hosts without the addon (the fake-addon tests).
+let xxh64 = xxh64js;
+function useNativeXxh64(fn) { xxh64 = fn || xxh64js; }
 
 const SPAN_KIND_STR = ['SPAN_KIND_UNSPECIFIED', 'SPAN_KIND_INTERNAL', 'SPAN_KIND_SERVER',
   'SPAN_KIND_CLIENT', 'SPAN_KIND_PRODUCER', 'SPAN_KIND_CONSUMER'];
@@ -198,4 +204,4 @@ class KeyDictionary {
 
 module.exports = { SPAN_KIND_STR, STATUS_CODE_STR, SERVICE_NAME_KEY, spanKindStr, statusCodeStr,
   formatFloat, asString, attrMap, buildKey, buildKeyString, buildAttributes, resourceHash, seriesHash,
-  seriesHashSeeded, assignSeriesId, KeyDictionary };
+  seriesHashSeeded, assignSeriesId, KeyDictionary, useNativeXxh64 };

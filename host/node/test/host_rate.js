@@ -85,18 +85,22 @@ if (gpu) {
 }
 // time spent inside the addon's batch columnizer and its ingest (the rest of
 // the timed region is the JavaScript thread's own work)
-const spent = { columnize: 0n, ingest: 0n };
-for (const [fn, k] of [['columnizeBatch', 'columnize'], ['columnizerIngest', 'ingest']]) {
-  const orig = addon[fn].bind(addon);
-  addon[fn] = (...a) => {
+const spent = { columnize: 0n, ingest: 0n, sync: 0n, apply: 0n };
+const timed = (obj, fn, k) => {
+  const orig = obj[fn].bind(obj);
+  obj[fn] = (...a) => {
     const t = process.hrtime.bigint();
     try { return orig(...a); } finally { spent[k] += process.hrtime.bigint() - t; }
   };
+};
+for (const [fn, k] of [['columnizeBatch', 'columnize'], ['columnizerIngest', 'ingest'], ['sync', 'sync']]) {
+  if (addon[fn]) timed(addon, fn, k);
 }
 const p = new TracesToMetricsPipeline({ addon, receiver: false, exporter: false, memoryLimiter: false,
   native: !jsOnly, spanmetrics: Object.assign({ n_services: 64, columnizer_threads: threads },
     exemplars ? { exemplars: { enabled: true, max_per_data_point: 5 } } : {},
     events ? { events: { enabled: true, dimensions: [{ name: 'exception.type' }] } } : {}) });
+timed(p.connector, '_applyNative', 'apply');  // the host bookkeeping of the non-plain results
 const consumeAll = (list) => {
   if (!batch) { for (const r of list) p.consumeTraces(r); return; }
   for (let i = 0; i < list.length; i += batch) {
@@ -109,7 +113,7 @@ const warm = reqs.slice(0, Math.max(1, Math.floor(reqs.length / 10)));
 consumeAll(warm);
 const warmSpans = BigInt(Math.min(n, warm.length * PER_REQUEST));
 p.connector.exportMetrics();
-spent.columnize = spent.ingest = 0n;
+spent.columnize = spent.ingest = spent.sync = spent.apply = 0n;
 const t0 = process.hrtime.bigint();
 consumeAll(reqs);
 p.connector._drain();
@@ -129,7 +133,8 @@ const native = st.nativeRequests > 0 && st.jsRequests === 0;
 p.shutdown();
 console.log(JSON.stringify({ spans: n, requests: reqs.length, otlp_bytes: bytes, seconds: secs,
   spans_per_s: n / secs, mb_per_s: bytes / secs / 1e6, cores: threads, batch, gpu,
-  seconds_in: { columnize_batch: Number(spent.columnize) / 1e9, ingest: Number(spent.ingest) / 1e9 },
+  seconds_in: { columnize_batch: Number(spent.columnize) / 1e9, ingest: Number(spent.ingest) / 1e9,
+    sync: Number(spent.sync) / 1e9, apply_native: Number(spent.apply) / 1e9 },
   columnizer: native ? 'native (binding/otlp_columnizer.cc)' : 'javascript',
   exemplars: exemplars ? nEx : undefined, event_records: events ? Number(st.eventRecords) : undefined,
   calls_check: gpu ? calls === BigInt(n) + warmSpans : null,  // cumulative: warm-up + timed
