@@ -12,6 +12,7 @@
 #   abvar_<a>_<b>..  C2 bench of laboratory-build kernel variants a, b, ... (3 rounds)
 #   streams_<wl>     bench of <wl> with 1 and with 2 launch streams (2 rounds)
 #   labtests_<v>     the small-table parity suites on laboratory-build variant v
+#   libab_<wl>_<name>  bench of <wl> on the product library and on spanagg/lib<name>.so (3 rounds)
 #   btagg_<wl>       bench of <wl> with 512- and 1,024-thread aggregate workgroups (2 rounds)
 #   labbin_<KNOB=v>  the binned parity suites on the laboratory build with KNOB=v
 #   colbench         the native columnizer alone (host/node/build/colbench) at 1-16 threads
@@ -81,6 +82,11 @@ for step in "$@"; do
       for r in 1 2; do for pp in 1 0; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_BT_PIPE=$pp \
           run "btpipe_${wl}_p${pp}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $BQ
+      done; done ;;
+    libab_*) rest=${step#libab_}; wl=${rest%%_*}; other=${rest#*_}  # product library against spanagg/lib<other>.so, e.g. libab_c2_spanagg_prediet
+      for r in 1 2 3; do for lib in libspanagg "lib$other"; do
+        SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/$lib.so \
+          run "libab_${wl}_${lib}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 50 --soak-s 0 --no-filter-off $BQ
       done; done ;;
     btagg_*) wl=${step#btagg_}  # aggregate workgroups of 512 / 1,024 threads (laboratory build), rounds interleaved
       for r in 1 2; do for bb in 512 1024; do
