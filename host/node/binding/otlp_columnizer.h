@@ -28,6 +28,7 @@
 #include <string>
 #include <string_view>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 namespace otlpcol {
@@ -214,6 +215,14 @@ class Columnizer {
   // buffered spans and the dictionary follow (the host's dictionary decides)
   void remap(uint64_t from, uint64_t to);
   void clear_buffer() { buf_.clear(); }
+  // The buffer just handed to the engine's asynchronous DMA (sa_ingest_async)
+  // becomes the spare and columnizing continues into the other one; the
+  // engine returns from its next sa_ingest_async only once the spare has been
+  // read, so the two alternate.
+  void swap_buffers() {
+    std::swap(buf_, spare_);
+    buf_.clear();
+  }
   // a new export interval: every series may take exemplars again
   void reset_exemplars() { ex_count_.clear(), ++ex_gen_; }
 
@@ -236,6 +245,7 @@ class Columnizer {
 
   Options opt_;
   Cols buf_{true}, excl_;  // buf_: page-locked when possible; excl_: a batch's exclusively redone requests
+  Cols spare_{true};       // the other page-locked buffer (swap_buffers)
   SigCache cache_;
   uint64_t gen_ = 0;  // bumped whenever an existing dictionary entry may change
   std::unique_ptr<Worker> main_;

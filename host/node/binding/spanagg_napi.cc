@@ -67,6 +67,9 @@ struct Handle {
     }
     const char *last_error() const { return g ? sa_group_last_error(g) : e ? sa_last_error(e) : ""; }
     int ingest(const sa_span_batch *b) { return g ? sa_group_ingest(g, b) : sa_ingest(e, b); }
+    // the columnizer's buffers: an engine reads them by DMA after returning
+    // (sa_ingest_async); a group copies them out before returning
+    int ingest_async(const sa_span_batch *b) { return g ? sa_group_ingest(g, b) : sa_ingest_async(e, b); }
     int sync() { return g ? sa_group_sync(g) : sa_sync(e); }
     int flush(sa_red_result **r) { return g ? sa_group_flush(g, r) : sa_flush(e, r); }
     int window_read(uint64_t w, sa_sketch_result **r) {
@@ -940,6 +943,8 @@ napi_value ColumnizerDestroy(napi_env env, napi_callback_info info) {
   void *p = nullptr;
   if (napi_remove_wrap(env, argv[0], &p) == napi_ok && p) {
     auto *c = static_cast<ColHandle *>(p);
+    // its buffers may still be read by the engine's DMA (sa_ingest_async)
+    if (c->engine && c->engine->live()) (void)c->engine->sync();
     if (c->engine_ref) napi_delete_reference(env, c->engine_ref);
     delete c;
   }
@@ -966,11 +971,18 @@ napi_value ColumnizerIngest(napi_env env, napi_callback_info info) {
   const size_t n = c->col.buffered();
   if (n) {
     sa_span_batch b{c->col.key(), c->col.start(), c->col.end(), c->col.w0(), c->col.w1(), c->col.meta(), n};
-    const int rc = c->engine->ingest(&b);
-    // a failed ingest rejects these columns' requests (the host reports them
-    // to their senders): drop the columns too, so a retry counts nothing twice
-    c->col.clear_buffer();
-    if (rc != SA_OK) return engine_error(env, c->engine, rc, "sa_ingest");
+    const int rc = c->engine->ingest_async(&b);
+    if (rc != SA_OK) {
+      // a failed ingest rejects these columns' requests (the host reports them
+      // to their senders): drop the columns too, so a retry counts nothing
+      // twice (an error return has read the columns, as sa_ingest does)
+      c->col.clear_buffer();
+      return engine_error(env, c->engine, rc, "sa_ingest_async");
+    }
+    // the engine's DMA may still read this buffer: columnize into the other
+    // one (the next ingest returns once this one has been read)
+    c->col.swap_buffers();
+    return num(env, (double)n);
   }
   c->col.clear_buffer();
   return num(env, (double)n);

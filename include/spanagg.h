@@ -193,6 +193,15 @@ const char *sa_last_error(const sa_engine *e);
  * aggregation completes asynchronously -- every read (sa_flush*, sa_window_*,
  * sa_get_stats) and sa_sync wait for it, and a device error surfaces there. */
 int sa_ingest(sa_engine *e, const sa_span_batch *batch);
+/* sa_ingest for a host that alternates two page-locked column buffers (the
+ * Node host's columnizer): when every column lies in sa_host_alloc memory the
+ * DMA reads them after the call returns, and the call returns once the
+ * columns of this engine's previous sa_ingest_async call have been read -- so
+ * the caller may refill the other buffer while this one is copied, and must
+ * leave this one alone until its next sa_ingest_async (or sa_sync /
+ * sa_destroy) returns.  Any other columns, and any error return: as
+ * sa_ingest (read before the call returns). */
+int sa_ingest_async(sa_engine *e, const sa_span_batch *batch);
 /* Page-locked host memory for batch columns a host builds itself (the Node
  * host's columnizer does): sa_ingest / sa_group_ingest copy columns that all
  * lie in such memory to HBM by DMA straight from the caller's arrays, with no

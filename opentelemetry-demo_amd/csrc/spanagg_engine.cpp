@@ -157,6 +157,10 @@ struct sa_engine {
   void *pin[2] = {nullptr, nullptr}, *dstage[2] = {nullptr, nullptr};
   hipEvent_t pin_ev[2] = {nullptr, nullptr};
   bool pin_used[2] = {false, false};
+  // sa_ingest_async: the event after the last async call's copies (its
+  // columns are the caller's until that event completes)
+  hipEvent_t ev_async = nullptr;
+  bool async_pending = false;
   int pin_cur = 0;
   uint64_t win_base = 0, spans = 0, slab_load = 0, dropped_seen = 0;
   bool unflushed = false;   // spans ingested since the RED counters were last reset
@@ -571,6 +575,7 @@ void sa_destroy(sa_engine *e) {
   for (int k = 0; k < 2; ++k) {
     if (e->pin[k]) (void)hipHostFree(e->pin[k]);
     if (e->pin_ev[k]) (void)hipEventDestroy(e->pin_ev[k]);
+  if (e->ev_async) (void)hipEventDestroy(e->ev_async);
   }
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
   if (e->ev_b) (void)hipEventDestroy(e->ev_b);
@@ -898,11 +903,12 @@ static bool batch_pinned(const sa_span_batch *b) {
 // copied to HBM by DMA and aggregated on the engine stream; the call returns
 // once the batch has been copied out of the caller's buffers, so the caller
 // builds the next batch while this one is in flight (two slots).
-int sa_ingest(sa_engine *e, const sa_span_batch *b) {
+static int ingest_host(sa_engine *e, const sa_span_batch *b, bool async) {
   if (int rc = check_batch(e, b, false)) return rc;
   if (b->n == 0) return SA_OK;
   if (int rc = set_dev(e)) return rc;
   join_sets(e);
+  if (!e->ev_async) SA_HIP(e, hipEventCreateWithFlags(&e->ev_async, hipEventDisableTiming));
   constexpr uint64_t kChunk = sa::kHostChunkSpans;
   constexpr size_t kSlotBytes = kChunk * 44 + 256;
   if (!e->pin[0]) {
@@ -929,7 +935,10 @@ int sa_ingest(sa_engine *e, const sa_span_batch *b) {
     const uint64_t ms = (m + 1) & ~1ULL;  // column stride: u64 columns stay 16-byte aligned
     const int k = e->pin_cur;
     e->pin_cur ^= 1;
-    if (e->pin_used[k]) SA_HIP(e, hipEventSynchronize(e->pin_ev[k]));
+    // the packing path rewrites the pinned slot: its last reader (the copy of
+    // two chunks back) must be done.  The other paths only reuse the device
+    // slot, which stream order protects.
+    if (e->pin_used[k] && !pinned && m < sa::kHostPageableMin) SA_HIP(e, hipEventSynchronize(e->pin_ev[k]));
     char *h = static_cast<char *>(e->pin[k]);
     const uint64_t *src[5] = {b->key_hash + off, b->start_ns + off, b->end_ns + off, b->trace_w0 + off,
                               b->trace_w1 + off};
@@ -965,11 +974,21 @@ int sa_ingest(sa_engine *e, const sa_span_batch *b) {
     e->pin_used[k] = true;
   }
   // page-locked columns: every chunk's copies are done (stream order) once
-  // the last chunk's are, before the caller may reuse the arrays
-  if (pinned) SA_HIP(e, hipEventSynchronize(e->ev_b));
+  // the last chunk's are, before the caller may reuse the arrays -- or, for
+  // sa_ingest_async, the previous async call's copies (earlier on the stream)
+  if (pinned && async) {
+    if (e->async_pending) SA_HIP(e, hipEventSynchronize(e->ev_async));
+    SA_HIP(e, hipEventRecord(e->ev_async, e->stream));
+    e->async_pending = true;
+  } else if (pinned) {
+    SA_HIP(e, hipEventSynchronize(e->ev_b));
+  }
   guard.armed = false;
   return SA_OK;
 }
+
+int sa_ingest(sa_engine *e, const sa_span_batch *b) { return ingest_host(e, b, false); }
+int sa_ingest_async(sa_engine *e, const sa_span_batch *b) { return ingest_host(e, b, true); }
 
 int sa_join(sa_engine *e, void *stream) {
   if (!e) return SA_EINVAL;

@@ -92,6 +92,7 @@ SIGNATURES = [
     ("sa_destroy", None, [C.c_void_p]),
     ("sa_last_error", C.c_char_p, [C.c_void_p]),
     ("sa_ingest", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch)]),
+    ("sa_ingest_async", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch)]),
     ("sa_ingest_device", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch), C.c_void_p]),
     ("sa_host_alloc", C.c_int, [C.c_size_t, C.POINTER(C.c_void_p)]),
     ("sa_host_free", None, [C.c_void_p]),

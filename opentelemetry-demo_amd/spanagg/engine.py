@@ -259,6 +259,12 @@ class Engine:
         b = _lib.sa_span_batch(*[c.ctypes.data for c in batch.columns()], len(batch))
         self._check(self.lib.sa_ingest(self._h, C.byref(b)), "sa_ingest")
 
+    def ingest_async(self, batch: SpanBatch):
+        """sa_ingest_async: columns in sa_host_alloc memory stay the engine's
+        until the next ingest_async (or sync) returns."""
+        b = _lib.sa_span_batch(*[c.ctypes.data for c in batch.columns()], len(batch))
+        self._check(self.lib.sa_ingest_async(self._h, C.byref(b)), "sa_ingest_async")
+
     def ingest_device(self, key, start, end, w0, w1, meta, n: Optional[int] = None,
                       stream: Optional[int] = None):
         """Device-resident batch: torch tensors (or raw device pointers)."""

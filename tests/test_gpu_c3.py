@@ -15,6 +15,8 @@ spanmetrics connector at src/otel-collector/otelcol-config.yml:116).  The
     nothing.
 Bar: bucket counts, calls, ns sums, HLL registers and count-min cells
 bit-exact with the oracle fed the same spans; duration sums within 1e-9."""
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -264,4 +266,48 @@ def test_ingest_columns_reusable_at_return(n):
         del b
         o = pyoracle.Oracle(n_services=wl.n_services)
         o.ingest(keep)
+        _check(e, o)
+
+
+def _pinned_batch(lib, n):
+    """A SpanBatch whose columns lie in sa_host_alloc (page-locked) memory."""
+    p = C.c_void_p()
+    assert lib.sa_host_alloc(n * 44 + 64, C.byref(p)) == 0
+    raw = (C.c_uint8 * (n * 44 + 64)).from_address(p.value)
+    buf = np.frombuffer(raw, dtype=np.uint8)
+    cols = [buf[i * n * 8:(i + 1) * n * 8].view(np.uint64) for i in range(5)]
+    meta = buf[5 * n * 8:5 * n * 8 + n * 4].view(np.uint32)
+    return p, cols, meta
+
+
+def test_ingest_async_double_buffered_pinned_columns():
+    """sa_ingest_async (the Node host's columnizer path): two page-locked
+    column buffers alternate; after each call the previous buffer is
+    overwritten with the next chunk at once, and the buffer just passed is
+    left alone until the following call returns.  Any early reuse would
+    count garbage."""
+    wl = generate_c2(2_400_000, seed=29)
+    b = wl.batch
+    chunks = [slice(i, min(i + 300_000, len(b))) for i in range(0, len(b), 300_000)]
+    with Engine(Config(n_services=wl.n_services, n_windows=16)) as e:
+        e.window_advance(wl.first_window)
+        bufs = [_pinned_batch(e.lib, 300_000) for _ in range(2)]
+        try:
+            for i, sl in enumerate(chunks):
+                p, cols, meta = bufs[i % 2]
+                m = sl.stop - sl.start
+                for c, src in zip(cols, b.columns()[:5]):
+                    c[:m] = src[sl]
+                meta[:m] = b.meta[sl]
+                e.ingest_async(SpanBatch(*[c[:m] for c in cols], meta[:m]))
+                # the other buffer (the previous call's) is free now: poison it
+                pp, pcols, pmeta = bufs[(i + 1) % 2]
+                for c in pcols:
+                    c[:] = 0xAB
+            e.sync()
+        finally:
+            for p, _, _ in bufs:
+                e.lib.sa_host_free(p)
+        o = pyoracle.Oracle(n_services=wl.n_services)
+        o.ingest(b)
         _check(e, o)
