@@ -160,7 +160,7 @@ def host_otlp_rate(spans: int, threads: int = 8, batch: int = 128, extra=()):
             **({"exemplars": r["exemplars"], "event_records": r["event_records"]} if extra else {}),
             "sample": f"{r['spans']:,} spans in {r['requests']} OTLP requests of 512 spans, "
                       f"{batch} requests per batch, 20 services x 25 names, decode + transform rules + "
-                      "keying + columnise + sa_ingest (pinned staging, H2D + kernel)"}
+                      "keying + columnise + sa_ingest_async (two pinned column buffers, H2D + kernel)"}
 
 
 def box_cores():
@@ -693,6 +693,8 @@ def main():
             # the same with exemplars (5 per data point) and span events (exception.type) on
             result["host_otlp_exemplars_events"] = host_otlp_rate(args.host_otlp_spans, threads=hthreads,
                                                                   extra=("--exemplars", "--events"))
+            # SURVEY 8(d) also asks for the decode + aggregate rate on one core
+            result["host_otlp_1core"] = host_otlp_rate(args.host_otlp_spans, threads=1)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
