@@ -15,6 +15,7 @@
 #include <node_api.h>
 
 #include <cstdint>
+#include <array>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -920,6 +921,10 @@ napi_value ColumnizeBatch(napi_env env, napi_callback_info info) {
   set(env, o, "maxEnd", big(env, c->col.max_end()));
   set(env, o, "spans", num(env, (double)spans));
   set(env, o, "plainEventRecords", num(env, (double)plain_events));  // event records of the plain requests
+  // wall ns of columnize_batch's phases (threaded calls): decode, commit, place
+  set(env, o, "phaseNs", make_typed(env, napi_float64_array, 8,
+                                    std::array<double, 3>{(double)br.ns_decode, (double)br.ns_commit,
+                                                          (double)br.ns_place}.data(), 3));
   set(env, o, "touch", make_typed(env, napi_biguint64_array, 8, touch.data(), touch.size()));
   set(env, o, "touchEnd", make_typed(env, napi_uint32_array, 4, touch_end.data(), touch_end.size()));
   napi_create_array_with_length(env, br.results.size(), &arr);

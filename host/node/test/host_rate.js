@@ -96,6 +96,16 @@ const timed = (obj, fn, k) => {
 for (const [fn, k] of [['columnizeBatch', 'columnize'], ['columnizerIngest', 'ingest'], ['sync', 'sync']]) {
   if (addon[fn]) timed(addon, fn, k);
 }
+// columnize_batch's own phases (decode / commit / place), summed over the calls
+const phases = [0, 0, 0];
+{
+  const cb = addon.columnizeBatch;
+  addon.columnizeBatch = (...a) => {
+    const r = cb(...a);
+    if (r && r.phaseNs) for (let i = 0; i < 3; i++) phases[i] += r.phaseNs[i];
+    return r;
+  };
+}
 const p = new TracesToMetricsPipeline({ addon, receiver: false, exporter: false, memoryLimiter: false,
   native: !jsOnly, spanmetrics: Object.assign({ n_services: 64, columnizer_threads: threads },
     exemplars ? { exemplars: { enabled: true, max_per_data_point: 5 } } : {},
@@ -114,6 +124,7 @@ consumeAll(warm);
 const warmSpans = BigInt(Math.min(n, warm.length * PER_REQUEST));
 p.connector.exportMetrics();
 spent.columnize = spent.ingest = spent.sync = spent.apply = 0n;
+phases.fill(0);
 const t0 = process.hrtime.bigint();
 consumeAll(reqs);
 p.connector._drain();
@@ -134,7 +145,8 @@ p.shutdown();
 console.log(JSON.stringify({ spans: n, requests: reqs.length, otlp_bytes: bytes, seconds: secs,
   spans_per_s: n / secs, mb_per_s: bytes / secs / 1e6, cores: threads, batch, gpu,
   seconds_in: { columnize_batch: Number(spent.columnize) / 1e9, ingest: Number(spent.ingest) / 1e9,
-    sync: Number(spent.sync) / 1e9, apply_native: Number(spent.apply) / 1e9 },
+    sync: Number(spent.sync) / 1e9, apply_native: Number(spent.apply) / 1e9,
+    columnize_phases: { decode: phases[0] / 1e9, commit: phases[1] / 1e9, place: phases[2] / 1e9 } },
   columnizer: native ? 'native (binding/otlp_columnizer.cc)' : 'javascript',
   exemplars: exemplars ? nEx : undefined, event_records: events ? Number(st.eventRecords) : undefined,
   calls_check: gpu ? calls === BigInt(n) + warmSpans : null,  // cumulative: warm-up + timed
