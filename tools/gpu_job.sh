@@ -15,6 +15,7 @@
 #   libab_<wl>_<name>  bench of <wl> on the product library and on spanagg/lib<name>.so (3 rounds)
 #   btagg_<wl>       bench of <wl> with 512- and 1,024-thread aggregate workgroups (2 rounds)
 #   labbin_<KNOB=v>  the binned parity suites on the laboratory build with KNOB=v
+#   colab            colbench against host/node/build/$COL_OTHER (3 rounds, 16 and 8 threads)
 #   colbench         the native columnizer alone (host/node/build/colbench) at 1-16 threads
 #   evscope_<wl>     bench of <wl> with the engine's events at device / system scope (2 rounds)
 #   labtrace_<wl>_<VAR=v>  rocprofv3 trace of a 100-step bench of <wl> on the laboratory build with VAR=v
@@ -70,6 +71,9 @@ for step in "$@"; do
         node test/host_rate.js 2000000 --events --dump /tmp/req_ev.bin > /dev/null) || exit 1
       for t in ${COL_THREADS:-1 4 8 16}; do run "colbench_t$t" 120 host/node/build/colbench /tmp/req_plain.bin --threads "$t"; done
       run colbench_ex_t16 120 host/node/build/colbench /tmp/req_ev.bin --threads 16 --exemplars --events ;;
+    colab) (cd host/node && node test/host_rate.js 2000000 --dump /tmp/req_plain.bin > /dev/null) || exit 1  # colbench against build/colbench_<other>
+      for r in 1 2 3; do for t in 16 8; do for b in colbench ${COL_OTHER:-colbench_condvar}; do
+        run "colab_${b}_t${t}_r$r" 120 host/node/build/$b /tmp/req_plain.bin --threads "$t"; done; done; done ;;
     hostex_*) t=${step#hostex_}; run "hostex_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 --exemplars --events ;;
     host_*) t=${step#host_}; run "host_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 ;;
     bench_*) wl=${step#bench_}; run "bench_$wl" 300 python bench.py --workload "$wl" --sub "" --steps 20 $BQ ;;
