@@ -13,15 +13,16 @@
  *   ----------------------------------------------  -------------------------------
  *   createDefaultConfig / Config                    sa_config + sa_config_default
  *   createTracesToMetricsConnector, Start           sa_create
- *   ConsumeTraces -> aggregateMetrics (per span)    sa_ingest / sa_ingest_device
+ *   ConsumeTraces -> aggregateMetrics (per span)    sa_ingest / sa_ingest_async / sa_ingest_device
  *   exportMetrics -> buildMetrics + resetState      sa_flush (+ host-side encoding)
  *   Shutdown                                        sa_destroy
  *   (new) per-service HLL + error count-min         sa_window_read / sa_window_advance
  *
  * Boundary rules (mirroring the connector's contracts):
- *  - Ownership: batches are borrowed for the duration of the call; results are
- *    owned by the library and released with sa_red_result_free /
- *    sa_sketch_result_free.
+ *  - Ownership: batches are borrowed for the duration of the call (page-locked
+ *    columns passed to sa_ingest_async: until the next sa_ingest_async or
+ *    sa_sync returns); results are owned by the library and released with
+ *    sa_red_result_free / sa_sketch_result_free.
  *  - Errors: every call returns an sa_status (0 ok, <0 error); nothing throws
  *    or aborts across the ABI; sa_last_error() gives the message.
  *  - Threading: one engine is single-producer (the connector serialises
