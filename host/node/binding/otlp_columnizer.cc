@@ -662,7 +662,7 @@ struct Columnizer::Undo {
 // the same way on the workers' completion: a blocked hand-over costs a futex
 // wake per thread and per fork (~tens of microseconds for 15 threads).
 struct Columnizer::Pool {
-  static constexpr int64_t kSpinNs = 200000;
+  static constexpr int64_t kSpinNs = 50000;
   std::vector<std::thread> th;
   std::mutex m;
   std::condition_variable go, done;
