@@ -593,6 +593,9 @@ struct ColHandle {
 };
 
 void finalize_col(napi_env env, void *data, void *) {
+  // (its pinned column buffers may still be read by an sa_ingest_async DMA:
+  // sa_host_free -> hipHostFree synchronizes the device before freeing; the
+  // engine handle itself may already be finalized here, so it is not used)
   auto *c = static_cast<ColHandle *>(data);
   if (c->engine_ref) napi_delete_reference(env, c->engine_ref);
   delete c;
