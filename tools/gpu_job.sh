@@ -15,6 +15,7 @@
 #   libab_<wl>_<name>  bench of <wl> on the product library and on spanagg/lib<name>.so (3 rounds)
 #   btagg_<wl>       bench of <wl> with 512- and 1,024-thread aggregate workgroups (2 rounds)
 #   labbin_<KNOB=v>  the binned parity suites on the laboratory build with KNOB=v
+#   hostprof_<t>     host_rate.js (GPU ingest, t threads) under node --cpu-prof
 #   colab            colbench against host/node/build/$COL_OTHER (3 rounds, 16 and 8 threads)
 #   colbench         the native columnizer alone (host/node/build/colbench) at 1-16 threads
 #   evscope_<wl>     bench of <wl> with the engine's events at device / system scope (2 rounds)
@@ -74,6 +75,8 @@ for step in "$@"; do
     colab) (cd host/node && node test/host_rate.js 2000000 --dump /tmp/req_plain.bin > /dev/null) || exit 1  # colbench against build/colbench_<other>
       for r in 1 2 3; do for t in 16 8; do for b in colbench ${COL_OTHER:-colbench_condvar}; do
         run "colab_${b}_t${t}_r$r" 120 host/node/build/$b /tmp/req_plain.bin --threads "$t"; done; done; done ;;
+    hostprof_*) t=${step#hostprof_}; run "hostprof_t$t" 200 node --cpu-prof --cpu-prof-dir="$OUT/hostprof_t$t" \
+        --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 ;;
     hostex_*) t=${step#hostex_}; run "hostex_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 --exemplars --events ;;
     host_*) t=${step#host_}; run "host_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 ;;
     bench_*) wl=${step#bench_}; run "bench_$wl" 300 python bench.py --workload "$wl" --sub "" --steps 20 $BQ ;;
