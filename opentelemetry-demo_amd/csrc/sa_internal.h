@@ -89,6 +89,11 @@ struct IngestParams {
   ulonglong2 *bt_rec;
   uint32_t *bt_cnt;
   uint32_t bt_grid;  // scatter workgroups (regions per bin)
+  // the aggregate's second record set (nullptr: one): the next launch's
+  // scatter output, aggregated with this one (sa_engine::bt_pend)
+  ulonglong2 *bt_rec2;
+  uint32_t *bt_cnt2;
+  uint32_t bt_grid2, bt_region2;
   // HLL lower bounds: hll_lb[j] <= every register of sub-block j (registers
   // [j << lb_shift, (j + 1) << lb_shift)), so a span whose rho is at most its
   // sub-block's bound cannot raise a register and skips the register read.

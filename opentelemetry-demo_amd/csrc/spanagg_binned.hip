@@ -739,14 +739,18 @@ template <int MODE = 0, int MAXPER = 2, int BLOCK = 512>
 __global__ __launch_bounds__(BLOCK, BLOCK == 1024 ? 8 : 6) void bt_aggregate3_kernel(IngestParams P) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t log2sb = P.log2sb, sb = 1u << log2sb;
-  const uint32_t G = P.bt_grid, bin = blockIdx.x, region = P.bt_region;
+  // record sets: one, or two (P.bt_rec2: two launches' scatters aggregated
+  // together, so the bin's setup and row write-back serve both)
+  const uint32_t nrs = cold_params().bt_rec2 ? 2u : 1u;
+  const uint32_t Gmax = nrs == 2 && cold_params().bt_grid2 > P.bt_grid ? cold_params().bt_grid2 : P.bt_grid;
+  const uint32_t bin = blockIdx.x;
   unsigned long long *lkeys = reinterpret_cast<unsigned long long *>(smem);
   unsigned long long *lsum = lkeys + sb;
   uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + sb);  // u16 [sb][17], packed
   constexpr uint32_t kErrL = kBtAgg2Err * 2;                  // u32 words in the etab space
   uint32_t *errl = reinterpret_cast<uint32_t *>(smem + bt_agg2_off_err(sb));  // [0] count, [1..] ek + 1
-  uint32_t *rcnt = reinterpret_cast<uint32_t *>(smem + bt_agg2_off_reg(sb));  // [G] region fills
-  uint32_t *misc = rcnt + G;  // [0] dropped
+  uint32_t *rcnt = reinterpret_cast<uint32_t *>(smem + bt_agg2_off_reg(sb));  // [G] region fills (the set's)
+  uint32_t *misc = rcnt + Gmax;  // [0] dropped
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   unsigned long long *gk = P.gkeys + ((uint64_t)bin << log2sb);
   bt_stamp(P, (uint64_t)bin * 8, 0);
@@ -760,7 +764,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 1024 ? 8 : 6) void bt_aggregate3_ke
     const uint32_t s = tid + u * BLOCK;
     orig[u] = s < sb ? gk[s] : 0ULL;
   }
-  for (uint32_t g = tid; g < G; g += BLOCK) rcnt[g] = P.bt_cnt[(uint64_t)bin * G + g];
+  for (uint32_t g = tid; g < P.bt_grid; g += BLOCK) rcnt[g] = P.bt_cnt[(uint64_t)bin * P.bt_grid + g];
 #pragma unroll
   for (int u = 0; u < kMaxPer; ++u) {
     const uint32_t s = tid + u * BLOCK;
@@ -775,9 +779,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 1024 ? 8 : 6) void bt_aggregate3_ke
   __syncthreads();
   bt_stamp(P, (uint64_t)bin * 8, 1);
 
-  // 2. the records
-  const ulonglong2 *bin_rec = P.bt_rec + (uint64_t)bin * G * region;
-  const __amdgpu_buffer_rsrc_t rrec = rsrc(bin_rec, G * region * 16);
+  // 2. the records, set by set
   const uint32_t half = lane >> 5, r0 = lane & 31u;
   const uint32_t pmax = bt_probe_max(log2sb);
   uint32_t n_drop = 0;
@@ -870,46 +872,60 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 1024 ? 8 : 6) void bt_aggregate3_ke
     }
   };
   constexpr uint32_t kWaves = BLOCK / 64;
-  const uint32_t pairs = (G + 1) / 2;
-  if (!(MODE & 1)) {
-    // the wave's region pairs p = wave + 8 j; this lane's region g = 2 p +
-    // half, its byte offset stepped by 16 regions per pair.  Batches of two
-    // pairs, double-buffered (a batch past the bin's regions loads nothing
-    // and adds nothing).
-    const uint32_t g0 = 2 * wave + half;
-    const uint32_t rstep = 2 * kWaves * region * 16;
-    uint32_t roff = (g0 * region + r0) * 16;
-    uint32_t goff = g0;
-    auto issue = [&](ulonglong2 (&v)[2], bool (&ok)[2]) {
-#pragma unroll
-      for (uint32_t b = 0; b < 2; ++b) {
-        const uint32_t g = goff + b * 2 * kWaves;
-        const uint32_t c = rcnt[g < G ? g : 0u];
-        ok[b] = g < G && r0 < c;
-        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)(ok[b] ? roff + b * rstep : 0xFFFFFFF0u), 0, 2);
-        v[b] = make_ulonglong2((uint64_t)x[0] | ((uint64_t)x[1] << 32), (uint64_t)x[2] | ((uint64_t)x[3] << 32));
-      }
-      roff += 2 * rstep;
-      goff += 4 * kWaves;
-    };
-    ulonglong2 va[2], vb[2];
-    bool oka[2], okb[2];
-    issue(va, oka);
-    for (uint32_t p0 = wave; p0 < pairs; p0 += kWaves * 4) {
-      issue(vb, okb);
-      agg_pair(va, oka);
-      issue(va, oka);
-      agg_pair(vb, okb);
-    }
-    // regions longer than 32 records: the rest, one record per lane
 #pragma unroll 1
-    for (uint32_t p = wave; p < pairs; p += kWaves) {
-      const uint32_t g = 2 * p + half;
-      const uint32_t c = g < G ? rcnt[g] : 0u;
-      for (uint32_t r = 32 + r0; r < c; r += 32) {
-        const ulonglong2 vv[2] = {bin_rec[(uint64_t)g * region + r], make_ulonglong2(0, 0)};
-        const bool ok[2] = {true, false};
-        agg_pair(vv, ok);
+  for (uint32_t rs = 0; rs < nrs; ++rs) {
+    // (the second set's parameters through the kernarg pointer: read where
+    // they are used, so they hold no scalar registers across the first set)
+    SA_CONST const IngestParams &Q = cold_params();
+    const uint32_t G = rs ? Q.bt_grid2 : P.bt_grid, region = rs ? Q.bt_region2 : P.bt_region;
+    if (rs) {  // the second set's region fills (every wave is past the first set's records)
+      __syncthreads();
+      for (uint32_t g = tid; g < G; g += BLOCK) rcnt[g] = Q.bt_cnt2[(uint64_t)bin * G + g];
+      __syncthreads();
+    }
+    const ulonglong2 *bin_rec = (rs ? Q.bt_rec2 : P.bt_rec) + (uint64_t)bin * G * region;
+    const __amdgpu_buffer_rsrc_t rrec = rsrc(bin_rec, G * region * 16);
+    const uint32_t pairs = (G + 1) / 2;
+    if (!(MODE & 1)) {
+      // the wave's region pairs p = wave + 8 j; this lane's region g = 2 p +
+      // half, its byte offset stepped by 16 regions per pair.  Batches of two
+      // pairs, double-buffered (a batch past the bin's regions loads nothing
+      // and adds nothing).
+      const uint32_t g0 = 2 * wave + half;
+      const uint32_t rstep = 2 * kWaves * region * 16;
+      uint32_t roff = (g0 * region + r0) * 16;
+      uint32_t goff = g0;
+      auto issue = [&](ulonglong2 (&v)[2], bool (&ok)[2]) {
+#pragma unroll
+        for (uint32_t b = 0; b < 2; ++b) {
+          const uint32_t g = goff + b * 2 * kWaves;
+          const uint32_t c = rcnt[g < G ? g : 0u];
+          ok[b] = g < G && r0 < c;
+          const auto x = __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)(ok[b] ? roff + b * rstep : 0xFFFFFFF0u), 0, 2);
+          v[b] = make_ulonglong2((uint64_t)x[0] | ((uint64_t)x[1] << 32), (uint64_t)x[2] | ((uint64_t)x[3] << 32));
+        }
+        roff += 2 * rstep;
+        goff += 4 * kWaves;
+      };
+      ulonglong2 va[2], vb[2];
+      bool oka[2], okb[2];
+      issue(va, oka);
+      for (uint32_t p0 = wave; p0 < pairs; p0 += kWaves * 4) {
+        issue(vb, okb);
+        agg_pair(va, oka);
+        issue(va, oka);
+        agg_pair(vb, okb);
+      }
+      // regions longer than 32 records: the rest, one record per lane
+#pragma unroll 1
+      for (uint32_t p = wave; p < pairs; p += kWaves) {
+        const uint32_t g = 2 * p + half;
+        const uint32_t c = g < G ? rcnt[g] : 0u;
+        for (uint32_t r = 32 + r0; r < c; r += 32) {
+          const ulonglong2 vv[2] = {bin_rec[(uint64_t)g * region + r], make_ulonglong2(0, 0)};
+          const bool ok[2] = {true, false};
+          agg_pair(vv, ok);
+        }
       }
     }
   }
@@ -1160,8 +1176,10 @@ hipError_t launch_bt_aggregate(const IngestParams &P, hipStream_t s) {
   if (P.diag & kDiagBtNoAgg) return hipSuccess;
   void *args[] = {const_cast<IngestParams *>(&P)};
   const uint32_t diag = P.diag | (P.log2sb > 10 ? kDiagBtAggWide : 0u);
-  return hipLaunchKernel(bt_agg_fn(diag), dim3(kPartBins), dim3(bt_agg_block()), args,
-                         bt_agg2_lds_bytes(P.log2sb, P.bt_grid), s);
+  // (two record sets: the region-fill array holds the larger set's)
+  const uint32_t g = P.bt_rec2 && P.bt_grid2 > P.bt_grid ? P.bt_grid2 : P.bt_grid;
+  return hipLaunchKernel(bt_agg_fn(diag), dim3(kPartBins), dim3(bt_agg_block()), args, bt_agg2_lds_bytes(P.log2sb, g),
+                         s);
 }
 
 size_t bt_agg2_lds_bytes(uint32_t log2sb, uint32_t grid) {

@@ -138,18 +138,24 @@ struct sa_engine {
   uint64_t kmul = 1, kinv = 1;
   size_t agg_lds = 0;
   // Launch pipeline of the binned path: launch k's scatter runs on the
-  // caller's stream and its aggregate on agg_stream (after ev_scat[k % 2]),
-  // so launch k + 1's scatter overlaps launch k's aggregate.  Two record sets
-  // (records + region fills): a scatter waits only for the aggregate that
-  // last read its set (ev_agg, two launches back).  The aggregate's key
-  // write-back is safe against the concurrent scatter's key inserts
-  // (spanagg_binned.hip bt_aggregate3_kernel step 3).
-  ulonglong2 *bt_rec[2] = {nullptr, nullptr};
-  uint32_t *bt_cnt[2] = {nullptr, nullptr};
+  // caller's stream; the aggregate runs on agg_stream (after the scatters'
+  // events), so later scatters overlap it.  Launches are aggregated in pairs:
+  // launch k's records wait (bt_pend) until launch k + 1's scatter, then one
+  // aggregate takes both record sets -- a bin's setup and row write-back
+  // serve two launches.  A pending set is aggregated alone before anything
+  // reads (join_sets, sa_join).  Four record sets (records + region fills):
+  // a scatter waits only for the aggregate that last read its set.  The
+  // aggregate's key write-back is safe against the concurrent scatters' key
+  // inserts (spanagg_binned.hip bt_aggregate3_kernel step 3).
+  static constexpr int kBtSets = 4;
+  ulonglong2 *bt_rec[kBtSets] = {};
+  uint32_t *bt_cnt[kBtSets] = {};
   hipStream_t agg_stream = nullptr;
-  hipEvent_t ev_scat[2] = {nullptr, nullptr}, ev_agg[2] = {nullptr, nullptr};
-  bool agg_used[2] = {false, false};
+  hipEvent_t ev_scat[kBtSets] = {}, ev_agg[kBtSets] = {};
+  bool agg_used[kBtSets] = {};
   uint32_t bt_set = 0;
+  int bt_pend = -1;              // the set whose records await the next launch's (or a join)
+  sa::IngestParams bt_pend_P{};  // its launch parameters
   unsigned long long *base64 = nullptr;
   size_t hll_slot_bytes = 0, cms_slot_elems = 0;
   // sa_ingest: two pinned host slots and their HBM copies; a slot is refilled
@@ -516,7 +522,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     // the aggregate stream of the launch pipeline (ordered by events only)
     if (hipStreamCreateWithFlags(&e->agg_stream, hipStreamNonBlocking) != hipSuccess)
       return bail(fail(e, SA_EDEVICE, "aggregate stream creation failed"));
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < sa_engine::kBtSets; ++k)
       if (hipEventCreateWithFlags(&e->ev_scat[k], ev_flags()) != hipSuccess ||
           hipEventCreateWithFlags(&e->ev_agg[k], ev_flags()) != hipSuccess)
         return bail(fail(e, SA_EDEVICE, "event creation failed"));
@@ -565,13 +571,15 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->stats, (void *)e->out_keys, (void *)e->out_rows, (void *)e->scratch,
                   (void *)e->slab_cnt, (void *)e->hll, (void *)e->errcnt, (void *)e->d_seeds,
                   (void *)e->dbg, (void *)e->d_bins, (void *)e->errslab, (void *)e->part_rec,
-                  (void *)e->part_fill, (void *)e->bt_rec[0], (void *)e->bt_cnt[0], (void *)e->bt_rec[1],
-                  (void *)e->bt_cnt[1], (void *)e->base64, (void *)e->hll_lb,
+                  (void *)e->part_fill, (void *)e->base64, (void *)e->hll_lb,
                   (void *)e->expo_hdr, (void *)e->expo_buckets, (void *)e->expo_slot, (void *)e->expo_out_keys,
                   (void *)e->expo_out_rows, (void *)e->expo_out_buckets, (void *)e->hll_filt, (void *)e->xslab,
                   (void *)e->xc_lcount, (void *)e->xc_slot_of_entry, (void *)e->xcslab,
                   e->dstage[0], e->dstage[1]})
     if (p) (void)hipFree(p);
+  for (int k = 0; k < sa_engine::kBtSets; ++k)
+    for (void *p : {(void *)e->bt_rec[k], (void *)e->bt_cnt[k]})
+      if (p) (void)hipFree(p);
   for (int k = 0; k < 2; ++k) {
     if (e->pin[k]) (void)hipHostFree(e->pin[k]);
     if (e->pin_ev[k]) (void)hipEventDestroy(e->pin_ev[k]);
@@ -582,7 +590,7 @@ void sa_destroy(sa_engine *e) {
   for (hipEvent_t ev : e->ev_set)
     if (ev) (void)hipEventDestroy(ev);
   if (e->ev_ctl) (void)hipEventDestroy(e->ev_ctl);
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < sa_engine::kBtSets; ++k) {
     if (e->ev_scat[k]) (void)hipEventDestroy(e->ev_scat[k]);
     if (e->ev_agg[k]) (void)hipEventDestroy(e->ev_agg[k]);
   }
@@ -599,11 +607,13 @@ const char *sa_last_error(const sa_engine *e) { return e ? e->err.c_str() : "nul
 // Orders the engine stream after every outstanding launch (each set's last
 // user); the next launch then orders after whatever the caller enqueues on the
 // engine stream now (ev_ctl, recorded lazily by that launch).
+static int bt_aggregate_pending(sa_engine *e);
 static void join_sets(sa_engine *e) {
+  (void)bt_aggregate_pending(e);  // (a failed launch is in e->err; the device error surfaces at the read)
   for (uint32_t i = 0; i < e->nsets; ++i)
     if (e->set_stream[i] && e->set_stream[i] != e->stream)
       (void)hipStreamWaitEvent(e->stream, e->ev_set[i], 0);
-  for (int k = 0; k < 2; ++k)  // the binned path's aggregates
+  for (int k = 0; k < sa_engine::kBtSets; ++k)  // the binned path's aggregates
     if (e->agg_used[k]) (void)hipStreamWaitEvent(e->stream, e->ev_agg[k], 0);
   e->ctl_dirty = true;
 }
@@ -652,7 +662,7 @@ static int bt_prepare_launch(sa_engine *e, uint64_t n, IngestParams &P, hipStrea
   P.bt_region = bt_region_for(P.wg_chunk);
   if (!e->bt_rec[0]) {
     const size_t recs = (size_t)sa::kPartBins * e->bt_grid * bt_region_for(sa::kBtMaxWgSpans);
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < sa_engine::kBtSets; ++k)
       if (hipMalloc((void **)&e->bt_rec[k], recs * sizeof(ulonglong2)) != hipSuccess ||
           hipMalloc((void **)&e->bt_cnt[k], (size_t)e->bt_grid * sa::kPartBins * 4) != hipSuccess)
         return fail(e, SA_ENOMEM, "binned-path record buffers hipMalloc failed");
@@ -662,7 +672,39 @@ static int bt_prepare_launch(sa_engine *e, uint64_t n, IngestParams &P, hipStrea
   P.kinv = e->kinv;
   P.bt_rec = e->bt_rec[e->bt_set];
   P.bt_cnt = e->bt_cnt[e->bt_set];
+  P.bt_rec2 = nullptr;
+  P.bt_cnt2 = nullptr;
   return SA_OK;
+}
+
+// The aggregate of record set k alone (pend < 0), or of the pending set and k
+// together (the pending set's records first), on `as` after both scatters.
+static int bt_launch_aggregate(sa_engine *e, int pend, const sa::IngestParams &Pp, int k,
+                               const sa::IngestParams &Pk, hipStream_t as) {
+  sa::IngestParams A = pend >= 0 ? Pp : Pk;
+  if (pend >= 0) {
+    A.bt_rec2 = Pk.bt_rec;
+    A.bt_cnt2 = Pk.bt_cnt;
+    A.bt_grid2 = Pk.bt_grid;
+    A.bt_region2 = Pk.bt_region;
+  }
+  for (int j : {pend, k})
+    if (j >= 0) SA_HIP(e, hipStreamWaitEvent(as, e->ev_scat[j], 0));
+  if (hipError_t st = sa::launch_bt_aggregate(A, as); st != hipSuccess)
+    return fail(e, SA_EDEVICE, std::string("aggregate launch: ") + hipGetErrorString(st));
+  for (int j : {pend, k})
+    if (j >= 0) {
+      SA_HIP(e, hipEventRecord(e->ev_agg[j], as));
+      e->agg_used[j] = true;
+    }
+  return SA_OK;
+}
+
+static int bt_aggregate_pending(sa_engine *e) {
+  if (!e->bt || e->bt_pend < 0) return SA_OK;
+  const int k = e->bt_pend;
+  e->bt_pend = -1;
+  return bt_launch_aggregate(e, -1, e->bt_pend_P, k, e->bt_pend_P, e->agg_stream);
 }
 
 static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
@@ -779,21 +821,33 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   } else if (e->bt) {
     if (int rc = bt_prepare_launch(e, b->n, P, s)) return rc;
     // the pipeline (sa_engine::bt_rec): scatter here, aggregate on agg_stream
-    const uint32_t k = e->bt_set;
+    const int k = (int)e->bt_set;
     if (e->agg_used[k]) SA_HIP(e, hipStreamWaitEvent(s, e->ev_agg[k], 0));  // set k's last reader
-    // (laboratory build: SPANAGG_BT_PIPE=0 runs the aggregate on the caller's stream)
+    // (laboratory build: SPANAGG_BT_PIPE=0 runs each launch's aggregate right
+    // after its scatter on the caller's stream; SPANAGG_BT_PAIR=0 aggregates
+    // every launch alone on the aggregate stream)
     static const bool pipe = [] {
       const char *v = ab_env("SPANAGG_BT_PIPE");
       return !(v && std::atoi(v) == 0);
     }();
-    hipStream_t as = pipe ? e->agg_stream : s;
+    static const bool pair = [] {
+      const char *v = ab_env("SPANAGG_BT_PAIR");
+      return !(v && std::atoi(v) == 0);
+    }();
     st = sa::launch_bt_scatter(P, s);
     if (st == hipSuccess) st = hipEventRecord(e->ev_scat[k], s);
-    if (st == hipSuccess && as != s) st = hipStreamWaitEvent(as, e->ev_scat[k], 0);
-    if (st == hipSuccess) st = sa::launch_bt_aggregate(P, as);
-    if (st == hipSuccess) st = hipEventRecord(e->ev_agg[k], as);
-    e->agg_used[k] = true;
-    e->bt_set ^= 1;
+    if (st != hipSuccess) return fail(e, SA_EDEVICE, std::string("ingest launch: ") + hipGetErrorString(st));
+    if (!pipe) {
+      if (int rc = bt_launch_aggregate(e, -1, P, k, P, s)) return rc;
+    } else if (pair && e->bt_pend < 0) {
+      e->bt_pend = k;  // aggregated with the next launch's records, or at the next join
+      e->bt_pend_P = P;
+    } else {
+      const int pend = e->bt_pend;
+      e->bt_pend = -1;
+      if (int rc = bt_launch_aggregate(e, pend, e->bt_pend_P, k, P, e->agg_stream)) return rc;
+    }
+    e->bt_set = (e->bt_set + 1) % sa_engine::kBtSets;
   } else if (e->part) {
     // records per bin: 1.25x the mean plus slack; a fuller bin spills to the
     // direct path, so this bounds memory, not correctness
@@ -994,9 +1048,10 @@ int sa_join(sa_engine *e, void *stream) {
   if (!e) return SA_EINVAL;
   if (int rc = set_dev(e)) return rc;
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+  if (int rc = bt_aggregate_pending(e)) return rc;
   for (uint32_t i = 0; i < e->nsets; ++i)
     if (e->set_stream[i] && e->set_stream[i] != s) SA_HIP(e, hipStreamWaitEvent(s, e->ev_set[i], 0));
-  for (int k = 0; k < 2; ++k)
+  for (int k = 0; k < sa_engine::kBtSets; ++k)
     if (e->agg_used[k]) SA_HIP(e, hipStreamWaitEvent(s, e->ev_agg[k], 0));
   return SA_OK;
 }

@@ -13,6 +13,7 @@
 #   streams_<wl>     bench of <wl> with 1 and with 2 launch streams (2 rounds)
 #   labtests_<v>     the small-table parity suites on laboratory-build variant v
 #   libab_<wl>_<name>  bench of <wl> on the product library and on spanagg/lib<name>.so (3 rounds)
+#   btpair_<wl>      bench of <wl> with binned aggregates in pairs / one per launch (3 rounds)
 #   btagg_<wl>       bench of <wl> with 512- and 1,024-thread aggregate workgroups (2 rounds)
 #   labbin_<KNOB=v>  the binned parity suites on the laboratory build with KNOB=v
 #   hostprof_<t>     host_rate.js (GPU ingest, t threads) under node --cpu-prof
@@ -94,6 +95,11 @@ for step in "$@"; do
       for r in 1 2 3; do for lib in libspanagg "lib$other"; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/$lib.so \
           run "libab_${wl}_${lib}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 50 --soak-s 0 --no-filter-off $BQ
+      done; done ;;
+    btpair_*) wl=${step#btpair_}  # binned launches aggregated in pairs / alone (laboratory build), rounds interleaved
+      for r in 1 2 3; do for pp in 1 0; do
+        SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_BT_PAIR=$pp \
+          run "btpair_${wl}_p${pp}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $BQ
       done; done ;;
     btagg_*) wl=${step#btagg_}  # aggregate workgroups of 512 / 1,024 threads (laboratory build), rounds interleaved
       for r in 1 2; do for bb in 512 1024; do
