@@ -119,6 +119,53 @@ def test_binned_pipeline_new_keys_every_launch(zipf):
         assert e.stats()["dropped_table_full"] == 0
 
 
+def test_binned_paired_aggregates_with_reads_between():
+    """Launches are aggregated in pairs (sa_engine::bt_pend): a launch's
+    records wait for the next launch's, unless something reads first.  Five
+    launches over two streams with a flush and a window read after the first
+    (a pending set aggregated alone), a stats read after the fourth (a pair
+    just done), a window advance after the third, and a flush at the end
+    (the fifth launch pending): every flush and window equal to the oracle
+    fed the same spans."""
+    import torch
+    dev = torch.device("cuda", 0)
+    n = 1_500_000
+    batch, _, w0 = generate_highcard(n, seed=47, routes=800, pods=400, zipf_s=1.1)
+    cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(dev)
+            for c in batch.columns()]
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream(dev))
+    o_all = pyoracle.Oracle(n_services=1)  # the sketches: every launch
+    o_red = pyoracle.Oracle(n_services=1)  # RED since the last flush
+    with _engine(1_200_000) as e:
+        e.window_advance(w0)
+        for i in range(5):
+            c = np.uint64(0x9E3779B97F4A7C15 * (i + 1) & (2**64 - 1))
+            tw = cols[4] ^ int(c.view(np.int64))
+            e.ingest_device(cols[0], cols[1], cols[2], cols[3], tw, cols[5], n=n, stream=streams[i % 2].cuda_stream)
+            b = SpanBatch(batch.key_hash, batch.start_ns, batch.end_ns, batch.trace_w0, batch.trace_w1 ^ c, batch.meta)
+            o_all.ingest(b)
+            o_red.ingest(b)
+            if i == 0:  # the first launch's records are pending here
+                assert_red_equal(e.flush(), o_red.series())
+                o_red = pyoracle.Oracle(n_services=1)
+                wid = o_all.window_ids()[0]
+                sk = e.window_read(wid)
+                hll, cms = o_all.window(wid)
+                assert np.array_equal(sk.hll, hll) and np.array_equal(sk.cms, cms)
+            if i == 2:  # pending again (launch 2): a window advance joins it
+                e.window_advance(w0)
+            if i == 3:
+                assert e.stats()["dropped_table_full"] == 0
+        torch.cuda.synchronize(dev)
+        assert_red_equal(e.flush(), o_red.series())
+        for wid in o_all.window_ids():
+            sk = e.window_read(wid)
+            hll, cms = o_all.window(wid)
+            assert np.array_equal(sk.hll, hll) and np.array_equal(sk.cms, cms), wid
+
+
 def test_binned_u8_rows_spill():
     """Row counts are u8 (32-B rows): a bucket count that would pass 255 moves
     the row's counts into the u64 spill array -- within one launch for the hot
