@@ -311,3 +311,20 @@ def test_ingest_async_double_buffered_pinned_columns():
         o = pyoracle.Oracle(n_services=wl.n_services)
         o.ingest(b)
         _check(e, o)
+
+
+def test_ingest_async_pageable_columns_read_before_return():
+    """sa_ingest_async with ordinary (pageable) columns behaves as sa_ingest:
+    the columns are read before the call returns, so overwriting them at
+    once changes nothing."""
+    wl = generate_c2(600_000, seed=31)
+    b = wl.batch
+    keep = SpanBatch(*[c.copy() for c in b.columns()])
+    with Engine(Config(n_services=wl.n_services, n_windows=16)) as e:
+        e.window_advance(wl.first_window)
+        e.ingest_async(b)
+        for c in b.columns():
+            c[:] = 0xAB
+        o = pyoracle.Oracle(n_services=wl.n_services)
+        o.ingest(keep)
+        _check(e, o)
