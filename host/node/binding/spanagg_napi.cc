@@ -16,6 +16,7 @@
 
 #include <cstdint>
 #include <array>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -875,6 +876,8 @@ napi_value ColumnizeBatch(napi_env env, napi_callback_info info) {
   if (!get_args(env, info, 2, argv)) return throw_napi(env, "args");
   ColHandle *c = get_col(env, argv[0]);
   if (!c) return nullptr;
+  using clk = std::chrono::steady_clock;
+  const auto t_in = clk::now();
   std::vector<napi_value> items;
   if (!array_items(env, argv[1], &items, "requests")) return nullptr;
   std::vector<const uint8_t *> bufs(items.size());
@@ -884,7 +887,9 @@ napi_value ColumnizeBatch(napi_env env, napi_callback_info info) {
     if (!typed(env, items[i], napi_uint8_array, &data, &lens[i], "requests[]")) return nullptr;
     bufs[i] = static_cast<const uint8_t *>(data);
   }
+  const auto t_cb = clk::now();
   otlpcol::BatchResult br = c->col.columnize_batch(bufs.data(), lens.data(), items.size());
+  const auto t_out = clk::now();
   // Most requests of a steady stream bring nothing new: status ok, no new
   // services / resources / series, no exemplars or event series.  Those get
   // no result object; what the host must still see of them -- the resources
@@ -924,10 +929,13 @@ napi_value ColumnizeBatch(napi_env env, napi_callback_info info) {
   set(env, o, "maxEnd", big(env, c->col.max_end()));
   set(env, o, "spans", num(env, (double)spans));
   set(env, o, "plainEventRecords", num(env, (double)plain_events));  // event records of the plain requests
-  // wall ns of columnize_batch's phases (threaded calls): decode, commit, place
+  // wall ns of columnize_batch's phases (threaded calls): decode, commit,
+  // place; then this call's own argument unpacking and (so far) result building
+  const auto ns = [](clk::duration d) { return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count(); };
   set(env, o, "phaseNs", make_typed(env, napi_float64_array, 8,
-                                    std::array<double, 3>{(double)br.ns_decode, (double)br.ns_commit,
-                                                          (double)br.ns_place}.data(), 3));
+                                    std::array<double, 5>{(double)br.ns_decode, (double)br.ns_commit,
+                                                          (double)br.ns_place, ns(t_cb - t_in),
+                                                          ns(clk::now() - t_out)}.data(), 5));
   set(env, o, "touch", make_typed(env, napi_biguint64_array, 8, touch.data(), touch.size()));
   set(env, o, "touchEnd", make_typed(env, napi_uint32_array, 4, touch_end.data(), touch_end.size()));
   napi_create_array_with_length(env, br.results.size(), &arr);

@@ -97,12 +97,12 @@ for (const [fn, k] of [['columnizeBatch', 'columnize'], ['columnizerIngest', 'in
   if (addon[fn]) timed(addon, fn, k);
 }
 // columnize_batch's own phases (decode / commit / place), summed over the calls
-const phases = [0, 0, 0];
+const phases = [0, 0, 0, 0, 0];
 {
   const cb = addon.columnizeBatch;
   addon.columnizeBatch = (...a) => {
     const r = cb(...a);
-    if (r && r.phaseNs) for (let i = 0; i < 3; i++) phases[i] += r.phaseNs[i];
+    if (r && r.phaseNs) for (let i = 0; i < r.phaseNs.length; i++) phases[i] += r.phaseNs[i];
     return r;
   };
 }
@@ -146,7 +146,8 @@ console.log(JSON.stringify({ spans: n, requests: reqs.length, otlp_bytes: bytes,
   spans_per_s: n / secs, mb_per_s: bytes / secs / 1e6, cores: threads, batch, gpu,
   seconds_in: { columnize_batch: Number(spent.columnize) / 1e9, ingest: Number(spent.ingest) / 1e9,
     sync: Number(spent.sync) / 1e9, apply_native: Number(spent.apply) / 1e9,
-    columnize_phases: { decode: phases[0] / 1e9, commit: phases[1] / 1e9, place: phases[2] / 1e9 } },
+    columnize_phases: { decode: phases[0] / 1e9, commit: phases[1] / 1e9, place: phases[2] / 1e9,
+      napi_args: phases[3] / 1e9, napi_results: phases[4] / 1e9 } },
   columnizer: native ? 'native (binding/otlp_columnizer.cc)' : 'javascript',
   exemplars: exemplars ? nEx : undefined, event_records: events ? Number(st.eventRecords) : undefined,
   calls_check: gpu ? calls === BigInt(n) + warmSpans : null,  // cumulative: warm-up + timed
