@@ -155,6 +155,7 @@ struct sa_engine {
   bool agg_used[kBtSets] = {};
   uint32_t bt_set = 0;
   int bt_pend = -1;              // the set whose records await the next launch's (or a join)
+  int sticky_rc = 0;             // a pending aggregate that failed to launch (join_checked)
   sa::IngestParams bt_pend_P{};  // its launch parameters
   unsigned long long *base64 = nullptr;
   size_t hll_slot_bytes = 0, cms_slot_elems = 0;
@@ -609,13 +610,22 @@ const char *sa_last_error(const sa_engine *e) { return e ? e->err.c_str() : "nul
 // engine stream now (ev_ctl, recorded lazily by that launch).
 static int bt_aggregate_pending(sa_engine *e);
 static void join_sets(sa_engine *e) {
-  (void)bt_aggregate_pending(e);  // (a failed launch is in e->err; the device error surfaces at the read)
+  // a pending binned record set is aggregated first; a failed launch is
+  // kept (sticky_rc) and returned by join_checked, so no read goes on without it
+  if (int rc = bt_aggregate_pending(e)) e->sticky_rc = rc;
   for (uint32_t i = 0; i < e->nsets; ++i)
     if (e->set_stream[i] && e->set_stream[i] != e->stream)
       (void)hipStreamWaitEvent(e->stream, e->ev_set[i], 0);
   for (int k = 0; k < sa_engine::kBtSets; ++k)  // the binned path's aggregates
     if (e->agg_used[k]) (void)hipStreamWaitEvent(e->stream, e->ev_agg[k], 0);
   e->ctl_dirty = true;
+}
+
+// join_sets for the calls that read or reorder: SA_EDEVICE (with e->err) when
+// a pending aggregate could not be launched
+static int join_checked(sa_engine *e) {
+  join_sets(e);
+  return e->sticky_rc;
 }
 
 static int reduce_slabs(sa_engine *e, hipStream_t s) {
@@ -751,7 +761,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   if (e->small) {
     const uint64_t per_wg = ((b->n + grid - 1) / grid + 3) / 4 * 4;
     if (e->slab_load + per_wg > kSlabLimit) {  // fold every set into the counters first
-      join_sets(e);
+      if (int rc = join_checked(e)) return rc;
       if (int rc = reduce_slabs(e, e->stream)) return rc;
     }
     e->slab_load += per_wg;
@@ -961,7 +971,7 @@ static int ingest_host(sa_engine *e, const sa_span_batch *b, bool async) {
   if (int rc = check_batch(e, b, false)) return rc;
   if (b->n == 0) return SA_OK;
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   if (!e->ev_async) SA_HIP(e, hipEventCreateWithFlags(&e->ev_async, hipEventDisableTiming));
   constexpr uint64_t kChunk = sa::kHostChunkSpans;
   constexpr size_t kSlotBytes = kChunk * 44 + 256;
@@ -1059,7 +1069,7 @@ int sa_join(sa_engine *e, void *stream) {
 int sa_sync(sa_engine *e) {
   if (!e) return SA_EINVAL;
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   SA_HIP(e, hipStreamSynchronize(e->stream));
   return SA_OK;
 }
@@ -1114,7 +1124,7 @@ int sa_reclaim_keys(sa_engine *e, int force) {
   if (!e) return SA_EINVAL;
   if (e->unflushed) return fail(e, SA_ESTATE, "sa_reclaim_keys: spans ingested since the last flush");
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   if (int rc = force ? reclaim_now(e) : reclaim_if_full(e)) return rc;
   SA_HIP(e, hipStreamSynchronize(e->stream));
   return SA_OK;
@@ -1125,7 +1135,7 @@ int sa_flush(sa_engine *e, sa_red_result **out) {
   *out = nullptr;
   if (e->expo) return fail(e, SA_ESTATE, "exponential-histogram engine: use sa_flush_exp");
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   if (int rc = ensure_out(e)) return rc;
   if (int rc = reduce_slabs(e, e->stream)) return rc;
   const uint32_t stride = e->nbk + 1;
@@ -1189,7 +1199,7 @@ int sa_flush_exp(sa_engine *e, sa_exp_result **out) {
   *out = nullptr;
   if (!e->expo) return fail(e, SA_ESTATE, "explicit-bucket engine: use sa_flush");
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   const uint32_t M = e->cfg.exp_max_size;
   if (!e->expo_out_keys &&
       (hipMalloc((void **)&e->expo_out_keys, e->cap * 8) != hipSuccess ||
@@ -1274,7 +1284,7 @@ int sa_expo_probe(sa_engine *e, const double *v, const int32_t *scale, uint64_t 
   if (!e || (n && (!v || !scale || !out || !logs)) || n > (1ULL << 20)) return SA_EINVAL;
   if (n == 0) return SA_OK;
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   void *buf = nullptr;
   if (hipMalloc(&buf, n * 24) != hipSuccess) return fail(e, SA_ENOMEM, "probe buffer");
   double *dv = static_cast<double *>(buf), *dl = dv + n;
@@ -1294,7 +1304,7 @@ int sa_key_union_probe(sa_engine *e, const uint64_t *in, uint64_t n, uint64_t *o
   *n_out = 0;
   if (n == 0) return SA_OK;
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   void *buf = nullptr;
   const size_t scratch = sa::key_union_scratch_bytes(n);
   if (hipMalloc(&buf, n * 16 + scratch + 64) != hipSuccess) return fail(e, SA_ENOMEM, "probe buffer");
@@ -1320,7 +1330,7 @@ int sa_expo_fast_probe(sa_engine *e, const uint64_t *d_ns, const int32_t *scale,
                        int32_t *exact, double *log2_err) {
   if (!e || (n && (!d_ns || !scale || !fast || !exact)) || n > (1ULL << 20)) return SA_EINVAL;
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   constexpr uint32_t kBlocks = 2048;
   void *buf = nullptr;
   if (hipMalloc(&buf, n * 20 + kBlocks * 8) != hipSuccess) return fail(e, SA_ENOMEM, "probe buffer");
@@ -1374,7 +1384,7 @@ int sa_window_read(sa_engine *e, uint64_t window_id, sa_sketch_result **out) {
   *out = nullptr;
   if (!resident(e, window_id)) return fail(e, SA_ERANGE, "window not resident");
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   const uint64_t ws = window_id & (e->cfg.n_windows - 1);
   if (int rc = fold_window(e, ws, e->stream)) return rc;
   auto *h = new sketch_holder();
@@ -1411,7 +1421,7 @@ int sa_window_advance(sa_engine *e, uint64_t new_base) {
   if (new_base > UINT64_MAX / e->cfg.window_ns)
     return fail(e, SA_EINVAL, "window base beyond the u64 nanosecond range");
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   const uint64_t n = std::min<uint64_t>(new_base - e->win_base, e->cfg.n_windows);
   for (uint64_t k = 0; k < n; ++k) {
     const uint64_t ws = (e->win_base + k) & (e->cfg.n_windows - 1);
@@ -1433,7 +1443,7 @@ int sa_debug_stamps(sa_engine *e, uint64_t *out, uint64_t cap, uint64_t *n_out) 
   *n_out = e->dbg ? (uint64_t)e->G * sa::kDbgPerWg : 0;
   if (!e->dbg || !out) return SA_OK;
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   SA_HIP(e, hipStreamSynchronize(e->stream));
   SA_HIP(e, hipMemcpy(out, e->dbg, std::min<uint64_t>(cap, *n_out) * 8, hipMemcpyDeviceToHost));
   return SA_OK;
@@ -1442,7 +1452,7 @@ int sa_debug_stamps(sa_engine *e, uint64_t *out, uint64_t cap, uint64_t *n_out) 
 int sa_get_stats(sa_engine *e, sa_stats *o) {
   if (!e || !o) return SA_EINVAL;
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   uint64_t st[sa::kNumStats];
   SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, e->stream));
   SA_HIP(e, sa::launch_count_keys(e->gkeys, e->cap, e->scratch, e->stream));
@@ -1472,7 +1482,7 @@ int sa_export_keys(sa_engine *e, uint64_t *d_keys, uint64_t cap, uint64_t *n_out
   if (!e || !n_out || (cap && !d_keys)) return SA_EINVAL;
   if (e->expo) return fail(e, SA_ESTATE, "merge hooks cover explicit-bucket engines only");
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
   if (s != e->stream) {
     SA_HIP(e, hipEventRecord(e->ev_a, e->stream));
@@ -1493,7 +1503,7 @@ int sa_gather_dense(sa_engine *e, const uint64_t *d_keys, uint64_t n, uint64_t *
   if (!e || (n && (!d_keys || !d_rows))) return SA_EINVAL;
   if (e->expo) return fail(e, SA_ESTATE, "merge hooks cover explicit-bucket engines only");
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
   if (s != e->stream) {
     SA_HIP(e, hipEventRecord(e->ev_a, e->stream));
@@ -1518,7 +1528,7 @@ int sa_window_export(sa_engine *e, uint64_t window_id, uint8_t *d_hll, uint64_t 
   if (!e) return SA_EINVAL;
   if (!resident(e, window_id)) return fail(e, SA_ERANGE, "window not resident");
   if (int rc = set_dev(e)) return rc;
-  join_sets(e);
+  if (int rc = join_checked(e)) return rc;
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
   if (s != e->stream) {
     SA_HIP(e, hipEventRecord(e->ev_a, e->stream));
