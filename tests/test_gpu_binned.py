@@ -166,6 +166,40 @@ def test_binned_paired_aggregates_with_reads_between():
             assert np.array_equal(sk.hll, hll) and np.array_equal(sk.cms, cms), wid
 
 
+def test_binned_pairing_across_host_and_device_ingest():
+    """Host-buffer and device-resident ingests interleaved on the binned path:
+    a device launch leaves its records pending, the host sa_ingest that
+    follows joins first (the pending set is aggregated alone) and leaves its
+    own launch pending, and the next device launch pairs with it.  The window
+    equals the oracle fed all three batches."""
+    import torch
+    dev = torch.device("cuda", 0)
+    n = 1_000_000
+    batch, _, w0 = generate_highcard(n, seed=53, routes=600, pods=300)
+    cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(dev)
+            for c in batch.columns()]
+    o = pyoracle.Oracle(n_services=1)
+    with _engine(1_200_000) as e:
+        e.window_advance(w0)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        for i in range(3):
+            c = np.uint64((0xD1B54A32D192ED03 * (i + 1)) & (2**64 - 1))
+            b = SpanBatch(batch.key_hash, batch.start_ns, batch.end_ns, batch.trace_w0, batch.trace_w1 ^ c, batch.meta)
+            if i == 1:
+                e.ingest(b)  # host buffers
+            else:
+                tw = cols[4] ^ int(c.view(np.int64))
+                e.ingest_device(cols[0], cols[1], cols[2], cols[3], tw, cols[5], n=n, stream=s.cuda_stream)
+            o.ingest(b)
+        torch.cuda.synchronize(dev)
+        assert_red_equal(e.flush(), o.series())
+        for wid in o.window_ids():
+            sk = e.window_read(wid)
+            hll, cms = o.window(wid)
+            assert np.array_equal(sk.hll, hll) and np.array_equal(sk.cms, cms), wid
+
+
 def test_binned_u8_rows_spill():
     """Row counts are u8 (32-B rows): a bucket count that would pass 255 moves
     the row's counts into the u64 spill array -- within one launch for the hot
