@@ -350,6 +350,7 @@ constexpr uint32_t kErrTab = 1024;    // LDS (window, slot) -> ERROR count table
 // cap u32 key tags, see kLdsTagBytes)
 constexpr size_t kLdsExtraBytes = kHllQueue * 8 + 32 + kBins * sizeof(BinEntry) + kErrTab * 4 + kLbMaxSub;
 constexpr size_t kLdsTagBytesPerSlot = 4;
+constexpr int kLdsTagVariant = 21;  // the only small-table variant with LDS key tags
 
 // launchers (spanagg_kernels.hip)
 hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,

@@ -395,8 +395,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   e->log2cap = log2u(e->cap);
   const uint32_t nw = (e->nbk + 1) / 2;
   // lkeys + lsum + lcnt + deferred-HLL queue (+ its counter), see ingest_lds_kernel
-  e->lds_bytes = (size_t)e->cap * 16 + (size_t)e->cap * nw * 4 + sa::kLdsExtraBytes +
-                 (size_t)e->cap * sa::kLdsTagBytesPerSlot;  // (the TAG kernels' key tags)
+  e->lds_bytes = (size_t)e->cap * 16 + (size_t)e->cap * nw * 4 + sa::kLdsExtraBytes;
   e->expo = cfg->exp_max_size != 0;
   e->small = e->lds_bytes <= kLdsBudget && !e->expo;
   if (e->expo) {  // key mirror + 32-B header partials per slot (nw = 6 counter words)
@@ -408,6 +407,14 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   if (const char *v = ab_env("SPANAGG_VARIANT"))
     e->variant = std::max(0, std::min((e->small ? sa::kNumLdsVariants : sa::kNumVariants) - 1,
                                       std::atoi(v)));
+  // the laboratory TAG variant also keeps a u32 key tag per slot in LDS; a
+  // table whose tags do not fit stays on the default variant
+  if (e->small && e->variant == sa::kLdsTagVariant) {
+    if (e->lds_bytes + (size_t)e->cap * sa::kLdsTagBytesPerSlot <= kLdsBudget)
+      e->lds_bytes += (size_t)e->cap * sa::kLdsTagBytesPerSlot;
+    else
+      e->variant = kDefaultVariant;
+  }
   if (e->small) {
     e->spl = (uint32_t)sa::kLdsSpl[e->variant];
     e->block = 1024;
@@ -584,8 +591,8 @@ void sa_destroy(sa_engine *e) {
   for (int k = 0; k < 2; ++k) {
     if (e->pin[k]) (void)hipHostFree(e->pin[k]);
     if (e->pin_ev[k]) (void)hipEventDestroy(e->pin_ev[k]);
-  if (e->ev_async) (void)hipEventDestroy(e->ev_async);
   }
+  if (e->ev_async) (void)hipEventDestroy(e->ev_async);
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
   if (e->ev_b) (void)hipEventDestroy(e->ev_b);
   for (hipEvent_t ev : e->ev_set)
@@ -611,8 +618,9 @@ const char *sa_last_error(const sa_engine *e) { return e ? e->err.c_str() : "nul
 static int bt_aggregate_pending(sa_engine *e);
 static void join_sets(sa_engine *e) {
   // a pending binned record set is aggregated first; a failed launch is
-  // kept (sticky_rc) and returned by join_checked, so no read goes on without it
-  if (int rc = bt_aggregate_pending(e)) e->sticky_rc = rc;
+  // kept (sticky_rc, bt_aggregate_pending) and returned by join_checked, so
+  // no read goes on without it
+  (void)bt_aggregate_pending(e);
   for (uint32_t i = 0; i < e->nsets; ++i)
     if (e->set_stream[i] && e->set_stream[i] != e->stream)
       (void)hipStreamWaitEvent(e->stream, e->ev_set[i], 0);
@@ -700,6 +708,16 @@ static int bt_launch_aggregate(sa_engine *e, int pend, const sa::IngestParams &P
   }
   for (int j : {pend, k})
     if (j >= 0) SA_HIP(e, hipStreamWaitEvent(as, e->ev_scat[j], 0));
+  {
+    // laboratory build: SPANAGG_FAIL_AGG=n fails the n-th aggregate launch of
+    // the process (tests of the pending-set error path)
+    static const long fail_at = [] {
+      const char *v = ab_env("SPANAGG_FAIL_AGG");
+      return v ? std::atol(v) : 0L;
+    }();
+    static long n_agg = 0;
+    if (fail_at > 0 && ++n_agg == fail_at) return fail(e, SA_EDEVICE, "aggregate launch: injected failure");
+  }
   if (hipError_t st = sa::launch_bt_aggregate(A, as); st != hipSuccess)
     return fail(e, SA_EDEVICE, std::string("aggregate launch: ") + hipGetErrorString(st));
   for (int j : {pend, k})
@@ -710,11 +728,25 @@ static int bt_launch_aggregate(sa_engine *e, int pend, const sa::IngestParams &P
   return SA_OK;
 }
 
+// Every launch of an aggregate that takes a pending record set goes through
+// here: the pending set belongs to an ingest that already returned SA_OK, so a
+// failure is kept (sticky_rc) and returned by every later read instead of
+// results without those records.
+static int bt_launch_with_pending(sa_engine *e, const sa::IngestParams &Pk, int k, hipStream_t as) {
+  const int pend = e->bt_pend;
+  e->bt_pend = -1;
+  const int rc = bt_launch_aggregate(e, pend, e->bt_pend_P, k, Pk, as);
+  if (rc && pend >= 0 && !e->sticky_rc) e->sticky_rc = rc;
+  return rc;
+}
+
 static int bt_aggregate_pending(sa_engine *e) {
   if (!e->bt || e->bt_pend < 0) return SA_OK;
   const int k = e->bt_pend;
   e->bt_pend = -1;
-  return bt_launch_aggregate(e, -1, e->bt_pend_P, k, e->bt_pend_P, e->agg_stream);
+  const int rc = bt_launch_aggregate(e, -1, e->bt_pend_P, k, e->bt_pend_P, e->agg_stream);
+  if (rc && !e->sticky_rc) e->sticky_rc = rc;
+  return rc;
 }
 
 static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
@@ -853,9 +885,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
       e->bt_pend = k;  // aggregated with the next launch's records, or at the next join
       e->bt_pend_P = P;
     } else {
-      const int pend = e->bt_pend;
-      e->bt_pend = -1;
-      if (int rc = bt_launch_aggregate(e, pend, e->bt_pend_P, k, P, e->agg_stream)) return rc;
+      if (int rc = bt_launch_with_pending(e, P, k, e->agg_stream)) return rc;
     }
     e->bt_set = (e->bt_set + 1) % sa_engine::kBtSets;
   } else if (e->part) {
@@ -900,7 +930,10 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
     st = sa::launch_ingest_hbm(P, grid, s, e->variant);
   }
   if (st != hipSuccess) return fail(e, SA_EDEVICE, std::string("ingest launch: ") + hipGetErrorString(st));
-  SA_HIP(e, hipEventRecord(e->ev_set[set], s));
+  // (laboratory build: SPANAGG_NO_SETEV=1 skips the slab-set event -- only
+  // valid when every launch uses one stream; it prices the event's cost)
+  static const bool no_setev = ab_env("SPANAGG_NO_SETEV") != nullptr;
+  if (!no_setev) SA_HIP(e, hipEventRecord(e->ev_set[set], s));
   e->set_stream[set] = s;
   e->set = (set + 1) % e->nsets;
   e->spans += b->n;
@@ -971,7 +1004,12 @@ static int ingest_host(sa_engine *e, const sa_span_batch *b, bool async) {
   if (int rc = check_batch(e, b, false)) return rc;
   if (b->n == 0) return SA_OK;
   if (int rc = set_dev(e)) return rc;
-  if (int rc = join_checked(e)) return rc;
+  // No join: ingest_launch orders each launch itself (slab-set and record-set
+  // events), so a binned record set still pending from an earlier call --
+  // host or device ingest -- pairs with this call's first launch instead of
+  // being aggregated alone.  A pending aggregate that failed earlier is
+  // reported here as at every read.
+  if (e->sticky_rc) return e->sticky_rc;
   if (!e->ev_async) SA_HIP(e, hipEventCreateWithFlags(&e->ev_async, hipEventDisableTiming));
   constexpr uint64_t kChunk = sa::kHostChunkSpans;
   constexpr size_t kSlotBytes = kChunk * 44 + 256;
@@ -1059,6 +1097,7 @@ int sa_join(sa_engine *e, void *stream) {
   if (int rc = set_dev(e)) return rc;
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
   if (int rc = bt_aggregate_pending(e)) return rc;
+  if (e->sticky_rc) return e->sticky_rc;
   for (uint32_t i = 0; i < e->nsets; ++i)
     if (e->set_stream[i] && e->set_stream[i] != s) SA_HIP(e, hipStreamWaitEvent(s, e->ev_set[i], 0));
   for (int k = 0; k < sa_engine::kBtSets; ++k)

@@ -330,6 +330,8 @@ struct sa_group {
   // (when the caller alternates streams), never the one of the same set
   std::vector<Buf> pcnt;
   unsigned long long *hcnt = nullptr;    // pinned host copy of the counts
+  // page-locked blocks the flush results' columns are copied into (sa_results.h)
+  std::shared_ptr<PinPool> pins = std::make_shared<PinPool>();
   // sa_group_ingest: per-member packed host shards, reused across calls
   std::vector<std::vector<uint64_t>> hcol;
   std::vector<std::vector<uint32_t>> hmeta;
@@ -855,12 +857,22 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
   const uint64_t len = nu * stride;
   // 3. dense rows per member (and its counters reset), 4. their sum, 5. the
   //    result's columns on member 0's device
+  // The result's columns go to one page-locked block (keys, counts, calls,
+  // ns sums, sums): DMA'd straight from the device, no zero fill, no staging.
   std::unique_ptr<red_holder> h(new red_holder());
-  h->keys.resize(nu);
-  h->counts.resize(nu * g->nbk);
-  h->calls.resize(nu);
-  h->sum_ns.resize(nu);
-  h->sum.resize(nu);
+  uint64_t *hk = nullptr, *hc = nullptr, *hcl = nullptr, *hns = nullptr;
+  double *hs = nullptr;
+  if (nu) {
+    const size_t need = (size_t)nu * (g->nbk + 4) * 8;
+    h->pool = g->pins;
+    h->pin = g->pins->take(need, &h->pin_bytes);
+    if (!h->pin) return gfail(g, SA_ENOMEM, "group flush: page-locked result block");
+    hk = static_cast<uint64_t *>(h->pin);
+    hc = hk + nu;
+    hcl = hc + nu * g->nbk;
+    hns = hcl + nu;
+    hs = reinterpret_cast<double *>(hns + nu);
+  }
   auto drop = [](int rc) { return rc; };
   if (nu) {
     for (uint32_t i = 0; i < n; ++i) {
@@ -902,30 +914,35 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
                        static_cast<const unsigned long long *>(g->rows[0].p), nu, g->nbk, d_counts, d_calls,
                        d_sum_ns, d_sum, div);
     SG_HIP(g, hipGetLastError());
-    SG_HIP(g, hipMemcpyAsync(h->keys.data(), union_of(0), nu * 8, hipMemcpyDeviceToHost, g->st[0]));
-    SG_HIP(g, hipMemcpyAsync(h->counts.data(), d_counts, nu * g->nbk * 8, hipMemcpyDeviceToHost, g->st[0]));
-    SG_HIP(g, hipMemcpyAsync(h->calls.data(), d_calls, nu * 8, hipMemcpyDeviceToHost, g->st[0]));
-    SG_HIP(g, hipMemcpyAsync(h->sum_ns.data(), d_sum_ns, nu * 8, hipMemcpyDeviceToHost, g->st[0]));
-    SG_HIP(g, hipMemcpyAsync(h->sum.data(), d_sum, nu * 8, hipMemcpyDeviceToHost, g->st[0]));
-    SG_HIP(g, hipStreamSynchronize(g->st[0]));
-  }
-  for (uint32_t i = 0; i < n; ++i) {
-    SG_HIP(g, hipSetDevice(g->dev[i]));
-    SG_HIP(g, hipStreamSynchronize(g->st[i]));
-    // the members' key tables: the flush-time reclamation sa_flush does
-    // (SA_ESTATE: nothing was gathered, the member's counters were never set)
-    if (nu) {
+    // (counts, calls, ns sums and sums are contiguous in fin: one copy)
+    SG_HIP(g, hipMemcpyAsync(hk, union_of(0), nu * 8, hipMemcpyDeviceToHost, g->st[0]));
+    SG_HIP(g, hipMemcpyAsync(hc, d_counts, fin_bytes, hipMemcpyDeviceToHost, g->st[0]));
+    (void)d_sum;
+    // every member's counters are reset (gather_dense), so its key table can
+    // be reclaimed now, while the result's copy is in flight (member 0, whose
+    // merge stream carries the copy, last)
+    for (uint32_t j = 0; j < n; ++j) {
+      const uint32_t i = (j + 1) % n;
+      SG_HIP(g, hipSetDevice(g->dev[i]));
+      SG_HIP(g, hipStreamSynchronize(g->st[i]));
       if (int rc = sa_reclaim_keys(g->eng[i], 0); rc != SA_OK && rc != SA_ESTATE)
         return drop(member_error(g, i, rc, "sa_reclaim_keys"));
     }
   }
+  // (the members' key-table reclamation above is the flush-time policy
+  // sa_flush applies; SA_ESTATE: nothing was gathered, the counters were
+  // never set)
+  for (uint32_t i = 0; i < n; ++i) {
+    SG_HIP(g, hipSetDevice(g->dev[i]));
+    SG_HIP(g, hipStreamSynchronize(g->st[i]));
+  }
   h->r.n_series = nu;
   h->r.n_buckets = g->nbk;
-  h->r.key_hash = h->keys.data();
-  h->r.bucket_counts = h->counts.data();
-  h->r.calls = h->calls.data();
-  h->r.sum_ns = h->sum_ns.data();
-  h->r.sum = h->sum.data();
+  h->r.key_hash = hk;
+  h->r.bucket_counts = hc;
+  h->r.calls = hcl;
+  h->r.sum_ns = hns;
+  h->r.sum = hs;
   *out = &h.release()->r;
   bool full = false;
   for (uint32_t i = 0; i < n; ++i) {

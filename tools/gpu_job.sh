@@ -138,6 +138,19 @@ for step in "$@"; do
        run "labtrace_${wl}_${knob//=/}" 300 rocprofv3 --kernel-trace --stats --output-format csv \
          -d "$OUT/labtrace_${wl}_${knob//=/}" -o run \
          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 100 --streams 1 --soak-s 0 --no-filter-off $BQ) || exit $? ;;
+    setev_*) wl=${step#setev_}  # slab-set event per launch on / off (laboratory build, one stream), rounds interleaved
+      for r in 1 2; do for ne in 0 1; do
+        if [ "$ne" = 1 ]; then export SPANAGG_NO_SETEV=1; else unset SPANAGG_NO_SETEV; fi
+        SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so \
+          run "setev_${wl}_ne${ne}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 50 --streams 1 --soak-s 0 --no-filter-off $BQ
+      done; done; unset SPANAGG_NO_SETEV ;;
+    trace2_*) wl=${step#trace2_}  # kernel trace of launches alternating over two streams (overlap or not)
+      (cd /tmp && run "trace2_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace2_$wl" -o run \
+         -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 100 --streams 2 --soak-s 0 --no-filter-off $BQ) || exit $? ;;
+    probe_*) p=${step#probe_}; run "probe_$p" 200 "$ROOTDIR/build/${p}_probe" ;;
+    groupbench_*) wl=${step#groupbench_}  # an 8-member group on this device, no profiler (flush_ms as a caller sees it)
+      run "groupbench_$wl" 300 python bench.py --workload "$wl" --sub "" --group 8 --steps 10 --warmup 2 --soak-s 0 \
+         --no-filter-off $BQ ;;
     trace_*) wl=${step#trace_}
       (cd /tmp && run "trace_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$wl" -o run \
          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 10 --warmup 2 --streams 1 --soak-s 0 --no-filter-off $BQ) || exit $? ;;
