@@ -63,7 +63,11 @@ typedef enum {
 
 typedef enum { SA_UNIT_MS = 0, SA_UNIT_S = 1 } sa_unit;
 
-/* Diagnostic ablations (sa_config.flags), used only to attribute kernel time.
+/* Test and profiling entry points (probes of single kernel stages, per-
+ * workgroup timestamps) are not connector operations: they are declared in
+ * spanagg_diag.h, which this header does not include.
+ *
+ * Diagnostic ablations (sa_config.flags), used only to attribute kernel time.
  * Only the laboratory build of the library accepts them (`make -C
  * opentelemetry-demo_amd ab` -> libspanagg_ab.so, used by tools/); the
  * product library returns SA_EINVAL for any flags != 0. */
@@ -249,25 +253,6 @@ int sa_reclaim_keys(sa_engine *e, int force);
  * SA_ESTATE there, and sa_flush_exp does on an explicit-bucket engine). */
 int sa_flush_exp(sa_engine *e, sa_exp_result **out);
 void sa_exp_result_free(sa_exp_result *r);
-/* Diagnostic: out[i] = the exponential bucket index of v[i] at scale[i] and
- * logs[i] = Go's math.Log(v[i]), both computed on the engine's GPU
- * (host arrays; n <= 2^20). */
-int sa_expo_probe(sa_engine *e, const double *v, const int32_t *scale, uint64_t n, int32_t *out, double *logs);
-/* Diagnostic: the bucket-index fast path the counting kernel uses.  For each
- * duration d_ns[i] > 0 at scale[i]: exact[i] = the Go-exact index of
- * d_ns / (1e6 or 1e9 by the engine's unit), fast[i] = the fast path's index
- * or INT32_MIN when it defers to the exact path (host arrays; n <= 2^20).
- * *log2_err (may be null) = max |v_log_f32(m) - log2(m)| over every float m
- * in [1, 2), the bound the fast path's margins assume. */
-int sa_expo_fast_probe(sa_engine *e, const uint64_t *d_ns, const int32_t *scale, uint64_t n, int32_t *fast,
-                       int32_t *exact, double *log2_err);
-
-/* Diagnostic: the device key union the group flush builds (sa::key_union:
- * bucket sort by the top bits, bitonic per bucket, repeats and 0 dropped) on
- * the engine's GPU.  out[0 .. *n_out) = the distinct non-zero ids of
- * in[0 .. n) ascending (host arrays; out holds n; n <= 2^28). */
-int sa_key_union_probe(sa_engine *e, const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *n_out);
-
 /* Sketches of one resident window (not cleared). */
 int sa_window_read(sa_engine *e, uint64_t window_id, sa_sketch_result **out);
 /* Retire every window < new_base (clears their ring slots); spans whose window
@@ -349,13 +334,6 @@ int sa_group_window_advance(sa_group *g, uint64_t new_base);
 /* Counters summed over members (n_keys and table_capacity too; window_base and
  * small_table from member 0). */
 int sa_group_get_stats(sa_group *g, sa_stats *out);
-
-/* Diagnostic only: per-workgroup s_memrealtime stamps (100 MHz) of the last
- * small-table ingest launch, [G][136] = {start, after LDS setup, after the span
- * loop, after the slab flush, 0 x 4, then per wave 8 segment cycle sums};
- * filled only when the engine was created with SA_OPT_STAMPS (*n_out = 0
- * otherwise). */
-int sa_debug_stamps(sa_engine *e, uint64_t *out, uint64_t cap, uint64_t *n_out);
 
 /* ---- pure host helpers (no device needed) ---- */
 /* Integer bucket thresholds: bucket(d_ns) = n_neg + #{i : d_ns > thr[i]} equals

@@ -108,7 +108,23 @@ struct IngestParams {
   // header slabs [G][cap] (XHdr) the rescale pass reduces
   uint32_t *slot_of;  // EXPO mode: [n] key slot of each span (kNotFound without one)
   XHdr *xslab;
+  // Small-table kernels with the tail pool (POOL): every workgroup owns the
+  // static range [b * wg_chunk, (b + 1) * wg_chunk); spans [pool_base, n)
+  // form pool_n blocks of kPoolSpans that workgroups take from *pool_ctr
+  // (x 64: one wave's claim) once their own range is claimed, so fast
+  // workgroups (and XCDs) finish the slow ones' share of the launch.
+  // pool_next: the counter of the launch nsets ahead (same slab set, so it
+  // starts after this one ends), zeroed here.
+  uint64_t pool_base;
+  uint32_t pool_n;
+  uint32_t *pool_ctr, *pool_next;
 };
+// the tail pool (IngestParams::pool_*): blocks of 8 claim chunks (2 x 128
+// spans each), at most kPoolMaxSteal of them per workgroup (its u16 LDS
+// counters bound the spans of one launch)
+constexpr uint32_t kPoolSpans = 2048;
+constexpr uint32_t kPoolMaxSteal = 8;
+constexpr uint32_t kPoolRing = 8;  // per-launch pool counters per engine
 // One workgroup's exponential-histogram header partial for one key slot
 // (EXPO kernel -> expo_reduce_rescale_kernel): counts, exact ns sum, the
 // largest ~d over positive durations (so the minimum starts from a zeroed
@@ -153,7 +169,15 @@ struct ExpoParams {
   uint32_t *slot_of_entry;  // [xc_ne] the entry's slot, ~0u: unused
   uint32_t *xcslab;         // [xG][xc_ne][(max_size + 1) / 2] per-workgroup u16 bucket-count pairs
   uint32_t xc_ne;           // LDS entries of the counting kernel (0: the cached-probe kernel)
+  // the counting kernel's tail (spans of series without an LDS entry): each
+  // workgroup's (slot << 12 | bucket) records, sorted by fold bin of
+  // kXtBinSlots slots, [xG][kXtCap], and the bins' offsets [xG][nbins + 1];
+  // expo_fold_tail_kernel sums them per bin (nullptr: HBM atomics)
+  uint32_t *xt_rec, *xt_off;  // (records past kXtCap take an HBM atomic)
 };
+constexpr uint32_t kXtCap = 4096;       // tail records per counting workgroup (16 KiB of LDS)
+constexpr uint32_t kXtBinSlots = 8;     // slots per tail fold bin
+__host__ __device__ inline uint32_t xt_bins(uint64_t cap) { return (uint32_t)((cap + kXtBinSlots - 1) / kXtBinSlots); }
 __host__ __device__ ExpoHdr expo_hdr_empty();
 constexpr uint32_t kExpoMaxSize = 4096;
 
@@ -337,18 +361,26 @@ constexpr uint32_t kHbmBlock = 256;
 // 12 / 13 = 8 / 11 specialised for cap 2048, 17 buckets, HLL p 14; 14 = 12 with
 // dynamic wave chunks; 15 = 14 generic; 16-18 = 14 with OPT 1 / 3 / 2; 19 = 16
 // with the batched end-of-launch write-back (v2_epilogue); 20 = 19 LEAN; 21 =
-// 20 with the TAG key lookup.
-constexpr int kNumLdsVariants = 22;
-constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
+// 20 with the TAG key lookup; 22 = 20 with the tail pool (POOL).
+constexpr int kNumLdsVariants = 23;
+constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
+constexpr int kLdsPoolVariant = 22;
 // v2 kernels keep u16 LDS counters for a whole launch: spans per workgroup per launch
 constexpr uint32_t kMaxWgSpans = 65532;
+// POOL launches: the static share per workgroup (whole 256-span chunks) leaves
+// room for kPoolMaxSteal stolen blocks under kMaxWgSpans; a launch averages at
+// most kPoolMaxWgSpans per workgroup, so the steal limits cover the pool
+constexpr uint32_t kPoolMaxStatic = (kMaxWgSpans - kPoolMaxSteal * kPoolSpans) / 256 * 256;
+constexpr uint32_t kPoolMaxWgSpans = kPoolMaxStatic + kPoolMaxSteal * kPoolSpans;
+constexpr uint32_t kPoolMinStatic = 32 * 256;  // two fixed chunks per wave before any claim
 constexpr uint32_t kDbgPerWg = 136;  // diagnostic stamps per workgroup: 8 + 16 waves x 8
 constexpr uint32_t kHllQueue = 2048;  // deferred HLL raises per workgroup (8 B each)
 constexpr uint32_t kErrTab = 1024;    // LDS (window, slot) -> ERROR count table per workgroup (4 B each)
 // ingest_lds_kernel LDS beyond the table: HLL queue + its count + bin table
 // (+ the ERROR table and HLL bounds of the v2 kernels; their TAG forms add
 // cap u32 key tags, see kLdsTagBytes)
-constexpr size_t kLdsExtraBytes = kHllQueue * 8 + 32 + kBins * sizeof(BinEntry) + kErrTab * 4 + kLbMaxSub;
+// (+ 64 B: the POOL kernels' map of stolen pool blocks)
+constexpr size_t kLdsExtraBytes = kHllQueue * 8 + 32 + kBins * sizeof(BinEntry) + kErrTab * 4 + kLbMaxSub + 64;
 constexpr size_t kLdsTagBytesPerSlot = 4;
 constexpr int kLdsTagVariant = 21;  // the only small-table variant with LDS key tags
 

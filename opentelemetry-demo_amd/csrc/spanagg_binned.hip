@@ -17,7 +17,8 @@
 //     are pre-aggregated in an LDS overflow table; past that, the direct path
 //     (key-table CAS + atomics into the spill array).
 //   bt_aggregate3_kernel (one 512-thread workgroup per bin; the laboratory
-//   build also keeps bt_aggregate2_kernel, the earlier form, SPANAGG_BT_AGG=2)
+//   build, lab/binned_lab.inc, also keeps bt_aggregate2_kernel, the earlier
+//   form, SPANAGG_BT_AGG=2)
 //     loads the bin's 2^log2sb key slots into LDS at the same positions,
 //     aggregates the bin's records there (u16 bucket-count pairs, u64 ns
 //     sums, an ERROR table keyed by (window slot, key slot)), then writes the
@@ -491,229 +492,6 @@ __host__ __device__ inline uint32_t bt_agg2_cnt_words(uint32_t sb) { return (sb 
 __host__ __device__ inline uint32_t bt_agg2_off_err(uint32_t sb) { return (sb * 16 + bt_agg2_cnt_words(sb) * 4 + 7) & ~7u; }
 __host__ __device__ inline uint32_t bt_agg2_off_reg(uint32_t sb) { return bt_agg2_off_err(sb) + kBtAgg2Err * 8; }
 
-#ifdef SPANAGG_AB
-// Aggregate, second form (laboratory build only).
-// MODE (ablation): 1 = no records aggregated, 2 = no key / row write-back,
-// 4 = records loaded only;
-// MAXPER = key slots per thread (sb <= MAXPER * BLOCK)
-template <int MODE = 0, int MAXPER = 2, int BLOCK = 512>
-__global__ __launch_bounds__(BLOCK) void bt_aggregate2_kernel(IngestParams P) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t log2sb = P.log2sb, sb = 1u << log2sb, smask = sb - 1;
-  const uint32_t G = P.bt_grid, bin = blockIdx.x, region = P.bt_region;
-  unsigned long long *lkeys = reinterpret_cast<unsigned long long *>(smem);
-  unsigned long long *lsum = lkeys + sb;
-  uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + sb);  // u16 [sb][17], packed
-  uint2 *etab = reinterpret_cast<uint2 *>(smem + bt_agg2_off_err(sb));
-  uint32_t *rcnt = reinterpret_cast<uint32_t *>(smem + bt_agg2_off_reg(sb));  // [G] region fills
-  uint32_t *misc = rcnt + G;  // [0] dropped
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  unsigned long long *gk = P.gkeys + ((uint64_t)bin << log2sb);
-  bt_stamp(P, (uint64_t)bin * 8, 0);
-
-  // 1. the bin's key slots (kept in registers to find the new ones later),
-  //    region fills, zeroed counters
-  constexpr int kMaxPer = MAXPER;
-  unsigned long long orig[kMaxPer];
-#pragma unroll
-  for (int u = 0; u < kMaxPer; ++u) {
-    const uint32_t s = tid + u * BLOCK;
-    orig[u] = s < sb ? gk[s] : 0ULL;
-  }
-  for (uint32_t g = tid; g < G; g += BLOCK) rcnt[g] = P.bt_cnt[(uint64_t)bin * G + g];
-#pragma unroll
-  for (int u = 0; u < kMaxPer; ++u) {
-    const uint32_t s = tid + u * BLOCK;
-    if (s < sb) {
-      lkeys[s] = orig[u];
-      lsum[s] = 0;
-    }
-  }
-  const uint32_t cw = bt_agg2_cnt_words(sb);
-  for (uint32_t i = tid; i < cw; i += BLOCK) lcnt[i] = 0;
-  for (uint32_t i = tid; i < kBtAgg2Err; i += BLOCK) etab[i] = make_uint2(0, 0);
-  if (tid == 0) misc[0] = 0;
-  __syncthreads();
-  bt_stamp(P, (uint64_t)bin * 8, 1);
-
-  // 2. the records (each carries its bucket: kRecDurBits)
-  const ulonglong2 *bin_rec = P.bt_rec + (uint64_t)bin * G * region;
-  const __amdgpu_buffer_rsrc_t rrec = rsrc(bin_rec, G * region * 16);
-  const uint32_t half = lane >> 5, r0 = lane & 31u;
-  uint32_t n_drop = 0;
-  auto agg = [&](const ulonglong2 &v) {
-    const uint64_t m = ((uint64_t)bin << kBinShift) | (v.x & kBinRest);
-    const uint64_t d = v.y & kRecDurMask;
-    const uint32_t bk = (uint32_t)(v.y >> kRecDurBits);  // bucketed by the scatter
-    // the key's two buckets (four independent 16-B reads), else the probe
-    // sequence (a new key, or one placed past its two buckets)
-    const BtSeq bq = bt_seq(m, log2sb);
-    const ulonglong2 *lk2 = reinterpret_cast<const ulonglong2 *>(lkeys);
-    const ulonglong2 a0 = lk2[bq.b1 * 2], a1 = lk2[bq.b1 * 2 + 1], c0 = lk2[bq.b2 * 2], c1 = lk2[bq.b2 * 2 + 1];
-    uint32_t s = a0.x == m ? bq.b1 * 4 : a0.y == m ? bq.b1 * 4 + 1 : a1.x == m ? bq.b1 * 4 + 2
-               : a1.y == m ? bq.b1 * 4 + 3 : c0.x == m ? bq.b2 * 4 : c0.y == m ? bq.b2 * 4 + 1
-               : c1.x == m ? bq.b2 * 4 + 2 : c1.y == m ? bq.b2 * 4 + 3 : kNotFound;
-    const uint32_t pmax = bt_probe_max(log2sb);
-    uint32_t i = 0;
-    if (s == kNotFound) {
-      for (; i < pmax; ++i) {
-        s = bt_pos(bq, i);
-        unsigned long long k = lkeys[s];
-        if (k == 0) k = atomicCAS(&lkeys[s], 0ULL, (unsigned long long)m);
-        if (k == 0 || k == m) break;
-      }
-    }
-    const bool err = (v.x >> 63) != 0;
-    const uint32_t ws = (uint32_t)(v.x >> kBinShift) & 1023u;
-    if (i == pmax) {  // the bin's sub-table is full: the span is dropped
-      ++n_drop;
-      if (err) bt_cms_add(kernel_params(), ws, m * P.kinv);
-      return;
-    }
-    const uint32_t h = s * kPartMaxBk + bk;
-    atomicAdd(&lcnt[h >> 1], 1u << ((h & 1u) * 16));
-    atomicAdd(&lsum[s], (unsigned long long)d);
-    if (err) {  // (window slot, key slot) -> count
-      const uint32_t ek = ((ws << log2sb) | s) + 1;
-      uint32_t e = (ek * 0x9E3779B1u) >> 25;  // kBtAgg2Err = 128
-      for (int pr = 0; pr < 8; ++pr, e = (e + 1) & (kBtAgg2Err - 1)) {
-        uint32_t kk = etab[e].x;
-        if (kk == 0) kk = atomicCAS(&etab[e].x, 0u, ek);
-        if (kk == 0 || kk == ek) {
-          atomicAdd(&etab[e].y, 1u);
-          return;
-        }
-      }
-      atomicAdd(P.errcnt + ((uint64_t)ws << P.log2cap) + ((uint64_t)bin << log2sb) + s, 1ULL);
-    }
-  };
-  // a batch: B region pairs of this wave, one record per lane, loaded with
-  // unconditional buffer loads (0 past a region's fill); the fills are read
-  // from LDS first, all of them before the loads
-  constexpr uint32_t kWaves = BLOCK / 64;
-  constexpr uint32_t B = 8;
-  const uint32_t pairs = (G + 1) / 2;
-  auto issue = [&](uint32_t p0, ulonglong2 (&v)[B], uint32_t (&cnt)[B]) {
-#pragma unroll
-    for (uint32_t b = 0; b < B; ++b) {
-      const uint32_t p = p0 + b * kWaves, g = 2 * p + half;
-      const bool ok = p < pairs && g < G;
-      cnt[b] = rcnt[ok ? g : 0u];
-      cnt[b] = ok ? cnt[b] : 0u;
-    }
-#pragma unroll
-    for (uint32_t b = 0; b < B; ++b) {
-      const uint32_t g = 2 * (p0 + b * kWaves) + half;
-      const uint32_t off = r0 < cnt[b] ? (g * region + r0) * 16 : 0xFFFFFFF0u;
-      const auto x = __builtin_amdgcn_raw_buffer_load_b128(rrec, (int)off, 0, 2);
-      v[b] = make_ulonglong2((uint64_t)x[0] | ((uint64_t)x[1] << 32), (uint64_t)x[2] | ((uint64_t)x[3] << 32));
-    }
-  };
-  auto process = [&](uint32_t p0, const ulonglong2 (&v)[B], const uint32_t (&cnt)[B]) {
-    if (MODE & 4) {  // ablation: records loaded, not aggregated
-#pragma unroll
-      for (uint32_t b = 0; b < B; ++b) n_drop += (r0 < cnt[b] && (v[b].x ^ v[b].y) == 0x12345ULL) ? 1u : 0u;
-      return;
-    }
-#pragma unroll
-    for (uint32_t b = 0; b < B; ++b)
-      if (r0 < cnt[b]) agg(v[b]);
-  };
-  // regions longer than 32 records: the rest, one record per lane, after the
-  // batches (loads inside the batch loop would make the compiler drain every
-  // outstanding load at its head)
-  auto tails = [&]() {
-#pragma unroll 1
-    for (uint32_t p = wave; p < pairs; p += kWaves) {
-      const uint32_t g = 2 * p + half;
-      const uint32_t c = g < G ? rcnt[g] : 0u;
-      for (uint32_t r = 32 + r0; r < c; r += 32) agg(bin_rec[(uint64_t)g * region + r]);
-    }
-  };
-  if (!(MODE & 1)) {
-    // one batch of 8 pairs at a time (two batches of 4 in flight, the next
-    // one's loads issued before this one is aggregated, measured 3 % slower:
-    // the conditional ERROR-path atomics make the compiler drain every load at
-    // the loop head, profiles/r2_analysis/c4_agg_pipeline.txt)
-    for (uint32_t p0 = wave; p0 < pairs; p0 += kWaves * B) {
-      ulonglong2 v[B];
-      uint32_t cnt[B];
-      issue(p0, v, cnt);
-      process(p0, v, cnt);
-    }
-    if (!(MODE & 4)) tails();
-  }
-  n_drop = wave_sum(n_drop);
-  if (lane == 0 && n_drop) atomicAdd(&misc[0], n_drop);
-  __syncthreads();
-  bt_stamp(P, (uint64_t)bin * 8, 2);
-
-  // 3. new keys and touched rows of the bin (one owner: plain stores; every
-  //    row read is issued before the first row is written)
-  if (MODE & 2) return;
-  const uint32_t nbk = P.nbk;
-  uint4 *rows = reinterpret_cast<uint4 *>(P.gcounts) + ((uint64_t)bin << log2sb) * (kRowBytes / 16);
-  uint4 rv[kMaxPer][2];
-  bool touched[kMaxPer];
-#pragma unroll
-  for (int u = 0; u < kMaxPer; ++u) {
-    const uint32_t s = tid + u * BLOCK;
-    touched[u] = s < sb && lsum[s] != 0;
-    if (s < sb && !touched[u]) {  // a zero ns sum: look at the counts
-      uint32_t any = 0;
-      for (uint32_t b = 0; b < nbk; ++b) {
-        const uint32_t h = s * kPartMaxBk + b;
-        any |= (lcnt[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu;
-      }
-      touched[u] = any != 0;
-    }
-#pragma unroll
-    for (uint32_t q = 0; q < 2; ++q) rv[u][q] = touched[u] ? rows[(uint64_t)s * 2 + q] : make_uint4(0, 0, 0, 0);
-  }
-#pragma unroll
-  for (int u = 0; u < kMaxPer; ++u) {
-    const uint32_t s = tid + u * BLOCK;
-    if (s >= sb) continue;
-    const unsigned long long k = lkeys[s];
-    if (k != orig[u]) gk[s] = k;
-    if (!touched[u]) continue;
-    // row: words 0-1 the ns sum, bytes 8 .. 8 + nbk the u8 counts
-    const uint32_t w[8] = {rv[u][0].x, rv[u][0].y, rv[u][0].z, rv[u][0].w,
-                           rv[u][1].x, rv[u][1].y, rv[u][1].z, rv[u][1].w};
-    const unsigned long long sum = ((unsigned long long)w[1] << 32 | w[0]) + lsum[s];
-    uint32_t c[kPartMaxBk];
-    bool spill = false;
-#pragma unroll
-    for (uint32_t b = 0; b < kPartMaxBk; ++b) {
-      const uint32_t h = s * kPartMaxBk + b;
-      c[b] = b < nbk ? ((w[2 + b / 4] >> ((b & 3u) * 8)) & 0xFFu) + ((lcnt[h >> 1] >> ((h & 1u) * 16)) & 0xFFFFu)
-                     : 0u;
-      spill |= c[b] > 0xFFu;
-    }
-    uint32_t o[6] = {0, 0, 0, 0, 0, 0};
-    if (spill) {  // the row's counts move to the spill array (atomics: the scatter adds there too)
-      unsigned long long *sp = P.base64 + ((uint64_t)bin << log2sb | s) * (nbk + 1);
-#pragma unroll
-      for (uint32_t b = 0; b < kPartMaxBk; ++b)
-        if (c[b]) atomicAdd(sp + b, (unsigned long long)c[b]);
-    } else {
-#pragma unroll
-      for (uint32_t b = 0; b < kPartMaxBk; ++b) o[b / 4] |= c[b] << ((b & 3u) * 8);
-    }
-    rows[(uint64_t)s * 2] = make_uint4((uint32_t)sum, (uint32_t)(sum >> 32), o[0], o[1]);
-    rows[(uint64_t)s * 2 + 1] = make_uint4(o[2], o[3], o[4], o[5]);
-  }
-  for (uint32_t i = tid; i < kBtAgg2Err; i += BLOCK) {
-    const uint2 e = etab[i];
-    if (e.x == 0) continue;
-    const uint32_t ek = e.x - 1, ws = ek >> log2sb, s = ek & smask;
-    unsigned long long *cell = P.errcnt + ((uint64_t)ws << P.log2cap) + ((uint64_t)bin << log2sb) + s;
-    *cell += e.y;
-  }
-  if (tid == 0 && misc[0]) atomicAdd(&P.stats[kStatDropped], (unsigned long long)misc[0]);
-  bt_stamp(P, (uint64_t)bin * 8, 3);
-}
-#endif  // SPANAGG_AB
 
 
 // Aggregate, third form (the default).  The layout, phases and row
@@ -1037,94 +815,12 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 1024 ? 8 : 6) void bt_aggregate3_ke
 }  // namespace
 
 #ifdef SPANAGG_AB
-// SA_DIAG bits of the ablation builds (profiling only)
-constexpr uint32_t kDiagBtAggNoRows = 1u << 21, kDiagBtNoAgg = 1u << 22, kDiagBtNoScatter = 1u << 23;
-constexpr uint32_t kDiagBtHotAcc = 1u << 25, kDiagBtHotErr = 1u << 26, kDiagBtSeqStore = 1u << 27,
-                   kDiagBtNoStore = 1u << 28;
-constexpr uint32_t kDiagBtFlush2 = 1u << 14;
-static const void *bt_scatter2_fn(uint32_t diag) {
-  if (diag & kDiagBtFlush2) return (const void *)&bt_scatter2_kernel<64>;
-  if (diag & kDiagBtSeqStore) return (const void *)&bt_scatter2_kernel<16>;
-  if (diag & kDiagBtNoStore) return (const void *)&bt_scatter2_kernel<32>;
-  if (diag & kDiagBtHotAcc) return (const void *)&bt_scatter2_kernel<4>;
-  if (diag & kDiagBtHotErr) return (const void *)&bt_scatter2_kernel<8>;
-  switch (diag & 3u) {
-    case 1: return (const void *)&bt_scatter2_kernel<1>;
-    case 2: return (const void *)&bt_scatter2_kernel<2>;
-    case 3: return (const void *)&bt_scatter2_kernel<3>;
-    default: return (const void *)&bt_scatter2_kernel<0>;
-  }
-}
-
-constexpr uint32_t kDiagBtAggWide = 1u << 30, kDiagBtAggLoadOnly = 1u << 31;
-constexpr uint32_t kDiagBtAggNoLookup = 1u << 17, kDiagBtAggNoAtomics = 1u << 18;
-static const void *bt_agg2_fn(uint32_t diag);
-static bool bt_agg_v2() {  // SPANAGG_BT_AGG=2: the second-form aggregate (A/B runs)
-  static const bool v2 = [] {
-    const char *v = std::getenv("SPANAGG_BT_AGG");
-    return v && std::atoi(v) == 2;
-  }();
-  return v2;
-}
-// SPANAGG_BT_AGG_BLOCK=1024: 1,024-thread aggregate workgroups, two per CU
-// (512 resident bins: the 2,048 bins in four full rounds instead of 2.67)
-static uint32_t bt_agg_block() {
-  static const uint32_t b = [] {
-    const char *v = std::getenv("SPANAGG_BT_AGG_BLOCK");
-    return v && std::atoi(v) == 1024 ? 1024u : kBtAgg2Block;
-  }();
-  return b;
-}
-static const void *bt_agg_fn(uint32_t diag) {
-  const int mode = ((diag & 1u) ? 1 : 0) | ((diag & kDiagBtAggNoRows) ? 2 : 0) |
-                   ((diag & kDiagBtAggNoLookup) ? 16 : 0) | ((diag & kDiagBtAggNoAtomics) ? 32 : 0);
-  if (bt_agg_block() == 1024 && mode == 0 && !(diag & kDiagBtAggLoadOnly) && !bt_agg_v2())
-    return (diag & kDiagBtAggWide) ? (const void *)&bt_aggregate3_kernel<0, 2, 1024>
-                                   : (const void *)&bt_aggregate3_kernel<0, 1, 1024>;
-  if (!bt_agg_v2() && !(diag & kDiagBtAggLoadOnly)) {
-    if (mode & 48) switch (mode) {  // ablations of the record loop
-        case 16: return (const void *)&bt_aggregate3_kernel<16, 2>;
-        case 32: return (const void *)&bt_aggregate3_kernel<32, 2>;
-        default: return (const void *)&bt_aggregate3_kernel<48, 2>;
-      }
-    if (diag & kDiagBtAggWide) switch (mode) {  // bins of 2,048 slots
-        case 1: return (const void *)&bt_aggregate3_kernel<1, 4>;
-        case 2: return (const void *)&bt_aggregate3_kernel<2, 4>;
-        case 3: return (const void *)&bt_aggregate3_kernel<3, 4>;
-        default: return (const void *)&bt_aggregate3_kernel<0, 4>;
-      }
-    switch (mode) {
-      case 1: return (const void *)&bt_aggregate3_kernel<1, 2>;
-      case 2: return (const void *)&bt_aggregate3_kernel<2, 2>;
-      case 3: return (const void *)&bt_aggregate3_kernel<3, 2>;
-      default: return (const void *)&bt_aggregate3_kernel<0, 2>;
-    }
-  }
-  return bt_agg2_fn(diag);
-}
-static const void *bt_agg2_fn(uint32_t diag) {
-  const int mode = ((diag & 1u) ? 1 : 0) | ((diag & kDiagBtAggNoRows) ? 2 : 0);
-  if (diag & kDiagBtAggLoadOnly) return (const void *)&bt_aggregate2_kernel<4, 2>;
-  if (diag & kDiagBtAggWide) switch (mode) {  // bins of 2,048 slots
-      case 1: return (const void *)&bt_aggregate2_kernel<1, 4>;
-      case 2: return (const void *)&bt_aggregate2_kernel<2, 4>;
-      case 3: return (const void *)&bt_aggregate2_kernel<3, 4>;
-      default: return (const void *)&bt_aggregate2_kernel<0, 4>;
-    }
-  switch (mode) {
-    case 1: return (const void *)&bt_aggregate2_kernel<1, 2>;
-    case 2: return (const void *)&bt_aggregate2_kernel<2, 2>;
-    case 3: return (const void *)&bt_aggregate2_kernel<3, 2>;
-    default: return (const void *)&bt_aggregate2_kernel<0, 2>;
-  }
-}
-
-#endif
-
-#ifndef SPANAGG_AB
+// the laboratory build's earlier aggregate form, ablation instances and
+// kernel selection (tools/ A/B runs; never in libspanagg.so)
+#include "lab/binned_lab.inc"
+#else
 // Product build: one scatter and one aggregate (bins of up to 1,024 slots, or
-// the wide form for 2,048); the ablation MODEs and the earlier aggregate form
-// live in the laboratory build.
+// the wide form for 2,048).
 static const void *bt_scatter2_fn(uint32_t) { return (const void *)&bt_scatter2_kernel<0>; }
 constexpr uint32_t kDiagBtAggWide = 1u << 30;
 static const void *bt_agg_fn(uint32_t diag) {
@@ -1141,27 +837,6 @@ hipError_t prepare_ingest_bt(size_t agg_lds) {
       return e;
   return hipSuccess;
 }
-#else
-hipError_t prepare_ingest_bt(size_t agg_lds) {
-  for (uint32_t d : {0u, 1u, 2u, 3u, kDiagBtHotAcc, kDiagBtHotErr, kDiagBtSeqStore, kDiagBtNoStore, kDiagBtFlush2})
-    if (hipError_t e = hipFuncSetAttribute(bt_scatter2_fn(d), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)kBt2ScatterLds);
-        e != hipSuccess)
-      return e;
-  for (uint32_t d : {0u, 1u, kDiagBtAggNoRows, 1u | kDiagBtAggNoRows, kDiagBtAggNoLookup, kDiagBtAggNoAtomics,
-                     kDiagBtAggNoLookup | kDiagBtAggNoAtomics})
-    for (uint32_t v : {0u, kDiagBtAggWide, kDiagBtAggLoadOnly})
-      for (const void *fn : {bt_agg_fn(d | v), bt_agg2_fn(d | v), (const void *)&bt_aggregate3_kernel<0, 1, 1024>,
-                             (const void *)&bt_aggregate3_kernel<0, 2, 1024>})
-        if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)agg_lds);
-            e != hipSuccess)
-          return e;
-  return hipSuccess;
-}
-
-#endif
-
-#ifndef SPANAGG_AB
 constexpr uint32_t kDiagBtNoScatter = 0, kDiagBtNoAgg = 0;
 static uint32_t bt_agg_block() { return kBtAgg2Block; }
 #endif

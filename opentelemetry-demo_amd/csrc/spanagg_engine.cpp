@@ -16,6 +16,7 @@
 #include "sa_internal.h"
 #include "sa_results.h"
 #include "spanagg.h"
+#include "spanagg_diag.h"
 
 using sa::IngestParams;
 
@@ -119,6 +120,7 @@ struct sa_engine {
   // slab bucket counting of small expo tables (spanagg_expo.hip expo_count_slab_kernel)
   uint32_t xc_ne = 0;
   uint32_t *xc_lcount = nullptr, *xc_slot_of_entry = nullptr, *xcslab = nullptr;
+  uint32_t *xt_rec = nullptr, *xt_off = nullptr;  // the counting kernel's tail records (ExpoParams::xt_*)
   sa::ExpoHdr *expo_hdr = nullptr;
   uint32_t *expo_buckets = nullptr, *expo_slot = nullptr;
   uint64_t expo_slot_cap = 0;
@@ -172,6 +174,11 @@ struct sa_engine {
   uint64_t win_base = 0, spans = 0, slab_load = 0, dropped_seen = 0;
   bool unflushed = false;   // spans ingested since the RED counters were last reset
   uint64_t reclaims = 0;    // key-table reclamations (sa_reclaim_keys)
+  // small-table kernel with the tail pool (sa::kLdsPoolVariant): per-launch
+  // pool counters [kPoolRing] (launch k zeroes launch k + nsets's)
+  bool pool = false;
+  uint32_t *pool_ring = nullptr;
+  uint32_t pool_seq = 0;
   std::string err;
 };
 
@@ -499,7 +506,9 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       if (e->xc_ne &&
           ((rc = alloc((void **)&e->xc_lcount, e->cap * 4)) ||
            (rc = alloc((void **)&e->xc_slot_of_entry, (size_t)e->xc_ne * 4)) ||
-           (rc = alloc((void **)&e->xcslab, (size_t)e->G * e->xc_ne * ((cfg->exp_max_size + 1) / 2) * 4))))
+           (rc = alloc((void **)&e->xcslab, (size_t)e->G * e->xc_ne * ((cfg->exp_max_size + 1) / 2) * 4)) ||
+           (rc = alloc((void **)&e->xt_rec, (size_t)e->G * sa::kXtCap * 4)) ||
+           (rc = alloc((void **)&e->xt_off, (size_t)e->G * (sa::xt_bins(e->cap) + 1) * 4))))
         return bail(rc);
       // (window, slot) keys of the LDS ERROR table are 16-bit
       if ((uint64_t)cfg->n_windows * e->cap < 65535 &&
@@ -561,6 +570,10 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
         (rc = alloc((void **)&e->errslab, gs * cfg->n_windows * e->cap * 4)))
       return bail(rc);
   }
+  // the tail pool: only the specialised default geometry has a POOL kernel
+  e->pool = e->small && e->variant == sa::kLdsPoolVariant && e->d_bins && e->log2cap == 11 &&
+            (e->nbk + 1) / 2 == 9 && cfg->hll_p == 14;
+  if (e->pool && (rc = alloc((void **)&e->pool_ring, sa::kPoolRing * 4))) return bail(rc);
   if (hipDeviceSynchronize() != hipSuccess) return bail(fail(e, SA_EDEVICE, "device sync failed"));
   *out = e;
   return SA_OK;
@@ -582,7 +595,8 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->part_fill, (void *)e->base64, (void *)e->hll_lb,
                   (void *)e->expo_hdr, (void *)e->expo_buckets, (void *)e->expo_slot, (void *)e->expo_out_keys,
                   (void *)e->expo_out_rows, (void *)e->expo_out_buckets, (void *)e->hll_filt, (void *)e->xslab,
-                  (void *)e->xc_lcount, (void *)e->xc_slot_of_entry, (void *)e->xcslab,
+                  (void *)e->xc_lcount, (void *)e->xc_slot_of_entry, (void *)e->xcslab, (void *)e->pool_ring,
+                  (void *)e->xt_rec, (void *)e->xt_off,
                   e->dstage[0], e->dstage[1]})
     if (p) (void)hipFree(p);
   for (int k = 0; k < sa_engine::kBtSets; ++k)
@@ -653,7 +667,8 @@ static int ingest_on(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   // 65532 spans per workgroup per launch (ingest_v2_kernel has no epoch flush)
   const uint64_t max_n = e->bt     ? (uint64_t)e->bt_grid * sa::kBtMaxWgSpans
                          : e->part ? sa::kPartMaxSpans
-                                   : (uint64_t)e->G * (((e->small && e->variant >= 8) || e->expo_small) ? sa::kMaxWgSpans
+                                   : e->pool ? (uint64_t)e->G * sa::kPoolMaxWgSpans
+                         : (uint64_t)e->G * (((e->small && e->variant >= 8) || e->expo_small) ? sa::kMaxWgSpans
                                                                                                        : (1u << 27));
   for (uint64_t off = 0; off < b->n; off += max_n) {
     const uint64_t m = std::min(max_n, b->n - off);
@@ -781,6 +796,16 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
   E.lcount = E.xc_ne ? e->xc_lcount : nullptr;
   E.slot_of_entry = e->xc_slot_of_entry;
   E.xcslab = e->xcslab;
+  {
+    // laboratory build: SPANAGG_XT=0 sends the counting kernel's tail to HBM
+    // atomics (the earlier form), for A/B runs
+    static const bool xt = [] {
+      const char *v = ab_env("SPANAGG_XT");
+      return !(v && std::atoi(v) == 0);
+    }();
+    E.xt_rec = xt && E.xc_ne ? e->xt_rec : nullptr;
+    E.xt_off = e->xt_off;
+  }
   return E;
 }
 
@@ -790,8 +815,24 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   const uint64_t tiles = (b->n + tile - 1) / tile;
   // each workgroup gets one contiguous range of >= one tile (kernel: wg_range)
   const uint32_t grid = (uint32_t)std::min<uint64_t>(tiles, e->G);
+  // tail pool (POOL kernel): each workgroup's static share is 7/8 of the
+  // average in whole 256-span chunks, the rest is the pool the workgroups
+  // that finish first take in blocks of kPoolSpans (a launch too small for two
+  // fixed chunks per wave has no pool)
+  uint64_t wg_chunk = ((b->n + grid - 1) / grid + 3) / 4 * 4, pool_base = 0;
+  uint32_t pool_n = 0;
+  if (e->pool) {
+    const uint64_t per = (b->n + grid - 1) / grid;
+    const uint64_t wc = std::min<uint64_t>(per * 7 / 8 / 256 * 256, sa::kPoolMaxStatic);
+    if (wc >= sa::kPoolMinStatic) {
+      wg_chunk = wc;
+      pool_base = grid * wc;
+      pool_n = (uint32_t)((b->n - pool_base + sa::kPoolSpans - 1) / sa::kPoolSpans);
+      if (pool_n > (uint64_t)grid * sa::kPoolMaxSteal) return fail(e, SA_EINVAL, "tail pool above the steal limits");
+    }
+  }
   if (e->small) {
-    const uint64_t per_wg = ((b->n + grid - 1) / grid + 3) / 4 * 4;
+    const uint64_t per_wg = pool_n ? wg_chunk + sa::kPoolMaxSteal * sa::kPoolSpans : wg_chunk;
     if (e->slab_load + per_wg > kSlabLimit) {  // fold every set into the counters first
       if (int rc = join_checked(e)) return rc;
       if (int rc = reduce_slabs(e, e->stream)) return rc;
@@ -816,7 +857,14 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.w1 = b->trace_w1;
   P.meta = b->meta;
   P.n = b->n;
-  P.wg_chunk = ((b->n + grid - 1) / grid + 3) / 4 * 4;
+  P.wg_chunk = wg_chunk;
+  P.pool_base = pool_base;
+  P.pool_n = pool_n;
+  if (e->pool) {
+    P.pool_ctr = e->pool_ring + e->pool_seq % sa::kPoolRing;
+    P.pool_next = e->pool_ring + (e->pool_seq + e->nsets) % sa::kPoolRing;
+    ++e->pool_seq;
+  }
   P.gkeys = e->gkeys;
   P.log2cap = e->log2cap;
   P.max_probe = sa::max_probe_of(e->log2cap);

@@ -392,6 +392,12 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
   int32_t *ent = reinterpret_cast<int32_t *>(meta + cap);         // [cap] entry or -1
   uint32_t *cnt = reinterpret_cast<uint32_t *>(ent + cap);        // [NE][wpe] u16 pairs
   uint32_t *scratch = cnt + NE * wpe;                             // [64] selection scratch
+  // the tail: records of the spans without an entry, their count, and the
+  // fold bins' histogram / cursors at the end
+  uint32_t *trec = scratch + 64;                                  // [kXtCap]
+  uint32_t *tmisc = trec + kXtCap;                                // [0] records, [1..] bin hist / cursors
+  const bool tail = E.xt_rec != nullptr;
+  if (threadIdx.x == 0) tmisc[0] = 0;
   uint32_t lc[2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) lc[k] = 2 * threadIdx.x + k < cap ? E.lcount[2 * threadIdx.x + k] : 0u;
@@ -414,12 +420,91 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
     if (!expo_index_fast(d, E.log2div, m.x, ix)) ix = expo_index(expo_value(d, E.div), m.x);
     const uint32_t at = expo_mod(ix, M);
     const int32_t en_ = ent[slot];
-    if (en_ >= 0) atomicAdd(&cnt[(uint32_t)en_ * wpe + (at >> 1)], 1u << ((at & 1u) * 16));
-    else if (!(E.diag & 1u)) atomicAdd(E.buckets + ((uint64_t)m.y * E.cap + slot) * M + at, 1u);
+    if (en_ >= 0) {
+      atomicAdd(&cnt[(uint32_t)en_ * wpe + (at >> 1)], 1u << ((at & 1u) * 16));
+    } else if (!(E.diag & 1u)) {
+      // a series without an entry: a record for the tail fold, not a
+      // scattered HBM atomic (past the record buffer: the atomic)
+      const uint32_t r = tail ? atomicAdd(&tmisc[0], 1u) : kXtCap;
+      if (r < kXtCap) trec[r] = slot << 12 | at;
+      else atomicAdd(E.buckets + ((uint64_t)m.y * E.cap + slot) * M + at, 1u);
+    }
   }
   __syncthreads();
   uint32_t *slab = E.xcslab + (uint64_t)blockIdx.x * NE * wpe;
   for (uint32_t i = threadIdx.x; i < NE * wpe; i += kXcBlock) slab[i] = cnt[i];
+  if (!tail) return;
+  // the tail records leave sorted by fold bin (slot / kXtBinSlots): a
+  // histogram, an exclusive scan, then each record at its bin's cursor
+  const uint32_t nt = min(tmisc[0], kXtCap), nb = xt_bins(cap);
+  uint32_t *hist = tmisc + 1;  // [nb]
+  for (uint32_t b = threadIdx.x; b < nb; b += kXcBlock) hist[b] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nt; i += kXcBlock) atomicAdd(&hist[(trec[i] >> 12) / kXtBinSlots], 1u);
+  __syncthreads();
+  // nb <= 256 bins (cap <= 2048): thread t < nb scans bin t
+  uint32_t total;
+  const uint32_t h = threadIdx.x < nb ? hist[threadIdx.x] : 0u;
+  const uint32_t ex = block_excl_scan(h, scratch + 48, total);
+  uint32_t *off = E.xt_off + (uint64_t)blockIdx.x * (nb + 1);
+  if (threadIdx.x < nb) {
+    off[threadIdx.x] = ex;
+    hist[threadIdx.x] = ex;  // the bin's cursor
+  }
+  if (threadIdx.x == 0) off[nb] = nt;
+  __syncthreads();
+  uint32_t *rec = E.xt_rec + (uint64_t)blockIdx.x * kXtCap;
+  for (uint32_t i = threadIdx.x; i < nt; i += kXcBlock) {
+    const uint32_t v = trec[i];
+    rec[atomicAdd(&hist[(v >> 12) / kXtBinSlots], 1u)] = v;
+  }
+}
+
+// The counting kernel's tail records, one workgroup per fold bin (kXtBinSlots
+// slots): every counting workgroup's run of the bin's records added in LDS
+// ([kXtBinSlots][M] u32), then each non-zero cell added to its bucket -- one
+// owner per slot (a slot is an entry in every workgroup or in none, so the
+// slab fold never touches these slots), no atomics on HBM.
+__global__ __launch_bounds__(1024) void expo_fold_tail_kernel(ExpoParams E, uint32_t grid) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t M = E.max_size, nb = xt_bins(E.cap), b = blockIdx.x;
+  uint32_t *acc = reinterpret_cast<uint32_t *>(smem);  // [kXtBinSlots][M]
+  __shared__ uint32_t cur[kXtBinSlots];
+  for (uint32_t i = threadIdx.x; i < kXtBinSlots * M; i += 1024) acc[i] = 0;
+  if (threadIdx.x < kXtBinSlots) {
+    const uint64_t sl = (uint64_t)b * kXtBinSlots + threadIdx.x;
+    cur[threadIdx.x] = sl < E.cap ? E.hdr[sl].cur : 0u;
+  }
+  __syncthreads();
+  // wave w takes the counting workgroups w, w + 16, ...: their runs' bounds
+  // for all of them first, then the records (64 lanes a run)
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  constexpr uint32_t kPer = 16;  // counting workgroups per wave and batch (grid <= 256 in one batch)
+  for (uint32_t g0 = wave; g0 < grid; g0 += 16 * kPer) {
+    uint32_t lo[kPer], n[kPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u) {
+      const uint32_t g = g0 + u * 16;
+      const uint32_t *off = E.xt_off + (uint64_t)g * (nb + 1) + b;
+      lo[u] = g < grid ? off[0] : 0u;
+      n[u] = g < grid ? off[1] - lo[u] : 0u;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u) {
+      const uint32_t *rec = E.xt_rec + (uint64_t)(g0 + u * 16) * kXtCap + lo[u];
+      for (uint32_t r = lane; r < n[u]; r += 64) {
+        const uint32_t v = rec[r];
+        atomicAdd(&acc[((v >> 12) % kXtBinSlots) * M + (v & 0xFFFu)], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < kXtBinSlots * M; i += 1024) {
+    const uint32_t c = acc[i];
+    if (!c) continue;
+    const uint32_t k = i / M, sl = b * kXtBinSlots + k;
+    E.buckets[((uint64_t)cur[k] * E.cap + sl) * M + i % M] += c;
+  }
 }
 
 // (entry, word) x 16 workgroup groups per block of 1024 threads
@@ -575,19 +660,27 @@ __host__ __device__ ExpoHdr expo_hdr_empty() {
   return h;
 }
 
+// the counting kernel's LDS: slot table, entries' counts, selection scratch,
+// the tail record buffer and its bin histogram
+static size_t xc_fixed_lds(uint64_t cap) { return (size_t)cap * 12 + 256 + (size_t)kXtCap * 4 + 4 + xt_bins(cap) * 4; }
+
 uint32_t expo_slab_entries(uint64_t cap, uint32_t max_size, size_t budget) {
-  const size_t fixed = (size_t)cap * 12 + 256, per = (size_t)((max_size + 1) / 2) * 4;
+  const size_t fixed = xc_fixed_lds(cap), per = (size_t)((max_size + 1) / 2) * 4;
   if (budget <= fixed + per) return 0;
   return (uint32_t)std::min<size_t>(cap, (budget - fixed) / per);
 }
 
 size_t expo_slab_lds_bytes(uint64_t cap, uint32_t max_size, uint32_t ne) {
-  return (size_t)cap * 12 + (size_t)ne * ((max_size + 1) / 2) * 4 + 256;
+  return xc_fixed_lds(cap) + (size_t)ne * ((max_size + 1) / 2) * 4;
 }
 
 hipError_t prepare_expo_slab(size_t lds_bytes) {
-  return hipFuncSetAttribute((const void *)&expo_count_slab_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)lds_bytes);
+  if (hipError_t e = hipFuncSetAttribute((const void *)&expo_count_slab_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+      e != hipSuccess)
+    return e;
+  return hipFuncSetAttribute((const void *)&expo_fold_tail_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)(kXtBinSlots * kExpoMaxSize * 4));
 }
 
 size_t expo_count_lds_bytes(uint64_t cap, uint32_t max_size) {
@@ -630,6 +723,9 @@ hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s) {
                        expo_slab_lds_bytes(E.cap, E.max_size, E.xc_ne), s, E, per_wg);
     const uint32_t words = E.xc_ne * ((E.max_size + 1) / 2);
     hipLaunchKernelGGL(expo_fold_slab_kernel, dim3((words + 63) / 64), dim3(1024), 0, s, E, grid);
+    if (E.xt_rec)
+      hipLaunchKernelGGL(expo_fold_tail_kernel, dim3(xt_bins(E.cap)), dim3(1024), kXtBinSlots * E.max_size * 4, s, E,
+                         grid);
     return hipGetLastError();
   }
   if (E.xslab) {  // small table: the ingest kernel left header partials and slots

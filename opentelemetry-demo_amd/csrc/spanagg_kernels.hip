@@ -547,8 +547,10 @@ __device__ __forceinline__ uint32_t wave_claim(uint32_t *ctr) {
 // or on an empty slot for a key whose tag is 0, fails the check and takes the
 // cold path, which probes full keys): 40 B of LDS per span instead of 64.
 template <int S, int NBUF, int AUX, bool DIAG, int LC = 0, int NWC = 0, int PC = 0, int HAUX = -1,
-          bool DYN = false, int OPT = 0, bool EPI = false, bool LEAN = false, bool EXPO = false, bool TAG = false>
+          bool DYN = false, int OPT = 0, bool EPI = false, bool LEAN = false, bool EXPO = false, bool TAG = false,
+          bool POOL = false>
 __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
+  static_assert(!POOL || (DYN && !(OPT & 2)), "the tail pool extends the chunk claims");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 0] = __builtin_amdgcn_s_memrealtime();
   const uint32_t log2cap = LC ? (uint32_t)LC : P.log2cap;
@@ -566,6 +568,10 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   uint32_t *etab = reinterpret_cast<uint32_t *>(lbins + kBins);  // [kErrTab]: (key+1) << 16 | count
   uint8_t *llb = reinterpret_cast<uint8_t *>(etab + kErrTab);       // [kLbMaxSub] HLL lower bounds
   uint32_t *ltag = reinterpret_cast<uint32_t *>(llb + kLbMaxSub);    // TAG: [cap] key_tag of each slot's key
+  // POOL: [kPoolMaxSteal] the pool block behind this workgroup's k-th stolen
+  // block (0 = not known yet, block + 1, or kPoolDone)
+  uint32_t *pmap = ltag + (TAG ? cap : 0u);
+  constexpr uint32_t kPoolDone = 0xFFFFFFFFu;
   const bool err_lds = P.errslab != nullptr;
   const bool lb_on = P.lb_n != 0 && !(diag & 2u);
   // EXPO header partials (zeroed with lsum / lcnt): lsum = ns sums
@@ -600,7 +606,13 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   auto tstart = [&](uint32_t unit, int b) -> uint32_t {  // step b's first span, relative to lo
     return kTileClaims ? unit * tile : DYN ? unit * chunk + (uint32_t)b * tile : unit + (uint32_t)b * tile;
   };
-  auto tremain = [&](uint32_t t) -> uint32_t { return len > t ? len - t : 0u; };
+  // spans readable from lo: the workgroup's range, or (POOL) the rest of the
+  // batch, which the workgroup's stolen pool blocks lie in (its own range is
+  // whole 256-span chunks then, so only a pool block at the batch end is short)
+  // (a launch too small for two fixed chunks per wave has no pool: pool_n 0)
+  const bool pool_on = POOL && cold_params().pool_n != 0;
+  const uint32_t lim = pool_on ? (uint32_t)(cold_params().n - lo) : len;
+  auto tremain = [&](uint32_t t) -> uint32_t { return lim > t ? lim - t : 0u; };
 
   // Prologue: key-table loads (16 B per lane, <= 4 per lane for cap <= 8192)
   // and the bin table first, then the first NBUF tiles; the LDS setup then
@@ -658,8 +670,9 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     hq_n[2] = 0;  // EPI: HLL updates the lower-bound filter skipped (summed over the waves)
   }
   if (threadIdx.x < 4) lstat[threadIdx.x] = 0;
-  {
-  }
+  if (POOL && threadIdx.x < kPoolMaxSteal) pmap[threadIdx.x] = 0;
+  // the pool counter of the launch nsets ahead (it starts after this one ends)
+  if (POOL && blockIdx.x == 0 && threadIdx.x == 0) *cold_params().pool_next = 0;
   etab[threadIdx.x] = 0;  // kErrTab == kLdsBlock
   // (filter off: the first bound word stays 0, and every span's sub-block
   // index is 0 or 1 below, so no rho can be at or below it)
@@ -720,7 +733,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     bool err[S];
 #pragma unroll
     for (int j = 0; j < S; ++j) {
-      const bool valid = lane_off + toff + (uint32_t)j < len;
+      const bool valid = lane_off + toff + (uint32_t)j < lim;
       // 0 past the range (buffer bounds check).  An explicit copy: the key is
       // used after the tile registers are re-filled, and sharing them would
       // make the allocator rotate the tile ring through copies that wait.
@@ -924,7 +937,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
             atomicMax(&xmax[f], d);
           }
         }
-        if (lane_off + toff + (uint32_t)j < len) P.slot_of[lo + toff + lane_off + j] = f;
+        if (lane_off + toff + (uint32_t)j < lim) P.slot_of[lo + toff + lane_off + j] = f;
       }
     } else if constexpr (LEAN) {
       const uint32_t lane = threadIdx.x & 63u;
@@ -996,12 +1009,59 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     // c0: this round's chunk (its tiles are in buf), c1: the next round's
     // (prefetched during this round), c2: claimed now for the round after.
     // The claim returns while the round runs; its result is read at the end.
-    while (c0 < n_chunks) {
-      const uint32_t c2 = wave_claim(&hq_n[1]);
+    // A chunk's first span relative to lo (t_of; lim: no work): the
+    // workgroup's own range, then (POOL) chunks of stolen pool blocks, 8 per
+    // block.  The wave whose claim is a block's first chunk takes the block
+    // from the pool counter during its round and publishes it in pmap at the
+    // round's end; the block's other chunks wait for that (claims are in
+    // order, so the earliest unpublished block's wave never waits itself).
+    // Every claim past a done block is done too.
+    auto t_of = [&](uint32_t c) -> uint32_t {
+      if (c < n_chunks) return c * chunk;
+      if constexpr (POOL) {
+        const uint32_t s = c - n_chunks, k = s >> 3, j = s & 7u;
+        if (!pool_on || k >= kPoolMaxSteal) return lim;
+        // (the host gives a pooled launch >= 32 own chunks per workgroup, so
+        // every block's first chunk is a claim whose wave publishes it; the
+        // bound only keeps a broken invariant from hanging the device)
+        uint32_t v, spin = 0;
+        while ((v = (uint32_t)__builtin_amdgcn_readfirstlane((int)__atomic_load_n(&pmap[k], __ATOMIC_RELAXED))) == 0 &&
+               ++spin < (1u << 22))
+          __builtin_amdgcn_s_sleep(2);
+        if (v == 0 || v == kPoolDone) return lim;
+        const uint64_t t = cold_params().pool_base - lo + (uint64_t)(v - 1) * kPoolSpans + j * chunk;
+        return t < lim ? (uint32_t)t : lim;
+      }
+      return lim;
+    };
+    if constexpr (!POOL) {
+      while (c0 < n_chunks) {
+        const uint32_t c2 = wave_claim(&hq_n[1]);
 #pragma unroll
-      for (int b = 0; b < NBUF; ++b) step(buf[b], tstart(c0, b), tstart(c1, b));
-      c0 = c1;
-      c1 = c2;
+        for (int b = 0; b < NBUF; ++b) step(buf[b], tstart(c0, b), tstart(c1, b));
+        c0 = c1;
+        c1 = c2;
+      }
+    }
+    if constexpr (POOL) {
+      // (state: this round's first span t0 and the next round's chunk c1, as
+      // c0 / c1 above; a block's wave takes it right at its claim, the
+      // block's other chunks resolve when they become c1)
+      uint32_t t0 = t_of(c0);
+      while (t0 < lim) {
+        const uint32_t c2 = wave_claim(&hq_n[1]);
+        if (pool_on && c2 >= n_chunks && ((c2 - n_chunks) & 7u) == 0 && ((c2 - n_chunks) >> 3) < kPoolMaxSteal) {
+          const uint32_t sid = (uint32_t)__builtin_amdgcn_readfirstlane((int)atomicAdd(cold_params().pool_ctr, 1u)) >> 6;
+          if ((threadIdx.x & 63u) == 0)
+            __atomic_store_n(&pmap[(c2 - n_chunks) >> 3], sid < cold_params().pool_n ? sid + 1 : kPoolDone,
+                             __ATOMIC_RELAXED);
+        }
+        const uint32_t t1 = t_of(c1);
+#pragma unroll
+        for (int b = 0; b < NBUF; ++b) step(buf[b], t0 + (uint32_t)b * tile, t1 + (uint32_t)b * tile);
+        t0 = t1;
+        c1 = c2;
+      }
     }
   } else {
     for (uint32_t t0 = 0; t0 < loop_len; t0 += NBUF * tile) {
@@ -1738,42 +1798,8 @@ static const void *small_fn(bool bt, int v, bool diag) {
 }
 constexpr int kSmallFnVariants[] = {15, 20};
 #else
-static const void *small_fn(bool bt, int v, bool diag) {
-  if (bt && v >= 8) {  // v2 kernels (bin-table bucketing only)
-    if (diag)
-      return (v >= 14) ? (const void *)&ingest_v2_kernel<2, 2, 2, true, 0, 0, 0, -1, true>
-                                  : (const void *)&ingest_v2_kernel<2, 2, 2, true>;
-    switch (v) {
-      case 9: return (const void *)&ingest_v2_kernel<2, 3, 0, false>;
-      case 10: return (const void *)&ingest_v2_kernel<4, 1, 0, false>;
-      case 11: return (const void *)&ingest_v2_kernel<2, 2, 0, false>;
-      case 12: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14>;
-      case 13: return (const void *)&ingest_v2_kernel<2, 2, 0, false, 11, 9, 14>;
-      case 14: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true>;
-      case 15: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true>;
-      case 16: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1>;
-      case 17: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 3>;
-      case 18: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 2>;
-      case 19: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1, true>;
-      case 20: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1, true, true>;
-      case 21: return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1, true, true, false, true>;
-      default: return (const void *)&ingest_v2_kernel<2, 2, 2, false>;
-    }
-  }
-  if (diag) return bt ? (const void *)&ingest_lds_kernel<1, 4, true, true>
-                      : (const void *)&ingest_lds_kernel<0, 4, true, true>;
-  if (!bt) return (const void *)&ingest_lds_kernel<0, 4, true, false>;
-  switch (v) {
-    case 1: return (const void *)&ingest_lds_kernel<1, 4, false, false>;
-    case 2: return (const void *)&ingest_lds_kernel<1, 2, true, false>;
-    case 3: return (const void *)&ingest_lds_kernel<1, 2, false, false>;
-    case 4: return (const void *)&ingest_lds_kernel<1, 4, true, false, 2>;
-    case 5: return (const void *)&ingest_lds_kernel<1, 4, false, false, 2>;
-    case 6: return (const void *)&ingest_lds_kernel<1, 2, true, false, 2>;
-    case 7: return (const void *)&ingest_lds_kernel<1, 2, false, false, 2>;
-    default: return (const void *)&ingest_lds_kernel<1, 4, true, false>;
-  }
-}
+// every variant and the diagnostic kernels (tools/ A/B runs)
+#include "lab/small_lab.inc"
 #endif
 
 template <int NB>

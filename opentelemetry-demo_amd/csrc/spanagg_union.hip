@@ -12,7 +12,8 @@
 //   3. union_scatter_kernel: each workgroup reserves one run per touched
 //      bucket with one global atomic, then places its ids in it (LDS cursors);
 //   4. union_sort_kernel: one workgroup per bucket sorts it in LDS (bitonic,
-//      padded with ~0 to a power of two), drops repeats and the padding id 0,
+//      padded with ~0 to a power of two), drops repeats (the padding id 0
+//      never reaches a bucket: steps 1 and 3 skip it),
 //      and writes the bucket's distinct ids at its offset (bucket counts);
 //   5. union_scan_kernel again over the distinct counts, then
 //      union_compact_kernel packs the buckets' runs into the output.
@@ -42,8 +43,12 @@ __global__ __launch_bounds__(kUnionBlock) void union_hist_kernel(const uint64_t 
   const uint32_t nb = 1u << bits;
   for (uint32_t b = threadIdx.x; b < nb; b += kUnionBlock) h[b] = 0;
   __syncthreads();
-  for (uint64_t i = blockIdx.x * (uint64_t)kUnionBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kUnionBlock)
-    atomicAdd(&h[ubucket(in[i], bits)], 1u);
+  // (the padding id 0 is neither counted nor placed: an RCCL group pads every
+  // member's list to the longest, and those zeros would all land in bucket 0)
+  for (uint64_t i = blockIdx.x * (uint64_t)kUnionBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kUnionBlock) {
+    const uint64_t k = in[i];
+    if (k != 0) atomicAdd(&h[ubucket(k, bits)], 1u);
+  }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nb; b += kUnionBlock)
     if (h[b]) atomicAdd(&hist[b], h[b]);
@@ -99,17 +104,15 @@ __global__ __launch_bounds__(kUnionBlock) void union_scatter_kernel(const uint64
     for (int u = 0; u < 8; ++u) {
       const uint64_t i = t0 + threadIdx.x + (uint64_t)u * kUnionBlock;
       k[u] = i < n ? in[i] : 0;
-      if (i < n) atomicAdd(&h[ubucket(k[u], bits)], 1u);
+      if (k[u] != 0) atomicAdd(&h[ubucket(k[u], bits)], 1u);
     }
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < nb; b += kUnionBlock)
       if (h[b]) h[b] = atomicAdd(&cur[b], h[b]);  // this tile's run of bucket b
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const uint64_t i = t0 + threadIdx.x + (uint64_t)u * kUnionBlock;
-      if (i < n) bucketed[atomicAdd(&h[ubucket(k[u], bits)], 1u)] = k[u];
-    }
+    for (int u = 0; u < 8; ++u)
+      if (k[u] != 0) bucketed[atomicAdd(&h[ubucket(k[u], bits)], 1u)] = k[u];  // (0 past n)
     __syncthreads();
   }
 }

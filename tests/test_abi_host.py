@@ -14,10 +14,20 @@ from spanagg.engine import Config, Engine
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_symbols():
-    text = open(os.path.join(ROOT, "include", "spanagg.h")).read()
+def declared_symbols(headers=("spanagg.h", "spanagg_diag.h")):
+    text = "".join(open(os.path.join(ROOT, "include", h)).read() for h in headers)
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(sa_[a-z_]+)\s*\(", text)))
+
+
+def test_diagnostic_entry_points_live_outside_the_product_header():
+    """Verdict r4: the probes and the stamp reader are declared in
+    spanagg_diag.h, which the drop-in header does not include."""
+    product, diag = declared_symbols(("spanagg.h",)), declared_symbols(("spanagg_diag.h",))
+    probes = {"sa_expo_probe", "sa_expo_fast_probe", "sa_key_union_probe", "sa_debug_stamps"}
+    assert probes <= set(diag)
+    assert not probes & set(product)
+    assert '#include "spanagg_diag.h"' not in open(os.path.join(ROOT, "include", "spanagg.h")).read()
 
 
 def test_library_exports_every_declared_symbol():
@@ -43,7 +53,8 @@ def test_product_library_has_no_laboratory():
     dyn = subprocess.run(["nm", "-D", "--undefined-only", so], capture_output=True, text=True, check=True).stdout
     assert "getenv" not in dyn
     strings = subprocess.run(["strings", so], capture_output=True, text=True, check=True).stdout
-    for lab in ("bt_aggregate2_kernel", "ingest_lds_kernelILi1E", "SPANAGG_VARIANT", "SPANAGG_BT_AGG"):
+    for lab in ("bt_aggregate2_kernel", "ingest_lds_kernelILi1E", "SPANAGG_VARIANT", "SPANAGG_BT_AGG",
+                "SPANAGG_XT", "SPANAGG_FAIL_AGG", "SPANAGG_NO_SETEV"):
         assert lab not in strings, lab
 
 

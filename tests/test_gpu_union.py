@@ -60,3 +60,17 @@ def test_union_oversized_bucket_takes_the_global_network(eng):
     ids = np.concatenate([skew, skew[:5000], rng.integers(1, 2**64 - 1, 100_000, dtype=np.uint64)])
     rng.shuffle(ids)
     assert np.array_equal(eng.key_union_probe(ids), _ref(ids))
+
+
+def test_union_of_ragged_members_mostly_padding(eng):
+    """Members whose key counts differ widely (one holds 1 M ids, seven hold
+    10 k): the all-gather's zero padding is ~7 M ids, 87 % of the input.  The
+    zeros are neither counted nor placed, so no bucket overflows into the
+    global-scratch network (advisor r4: they used to pile into bucket 0)."""
+    rng = np.random.Generator(np.random.PCG64(12))
+    big = rng.integers(1, 2**64 - 1, 1_000_000, dtype=np.uint64)
+    lists = [big] + [rng.choice(big, 10_000, replace=False) for _ in range(7)]
+    nmax = max(len(x) for x in lists)
+    gathered = np.concatenate([np.concatenate([x, np.zeros(nmax - len(x), np.uint64)]) for x in lists])
+    assert (gathered == 0).mean() > 0.8
+    assert np.array_equal(eng.key_union_probe(gathered), _ref(gathered))

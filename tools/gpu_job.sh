@@ -147,6 +147,11 @@ for step in "$@"; do
     trace2_*) wl=${step#trace2_}  # kernel trace of launches alternating over two streams (overlap or not)
       (cd /tmp && run "trace2_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace2_$wl" -o run \
          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 100 --streams 2 --soak-s 0 --no-filter-off $BQ) || exit $? ;;
+    xt_*) wl=${step#xt_}  # c2expo counting tail: LDS records + fold (1) / HBM atomics (0), laboratory build, rounds interleaved
+      for r in 1 2; do for xt in 1 0; do
+        SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_XT=$xt \
+          run "xt_${wl}_x${xt}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $BQ
+      done; done ;;
     probe_*) p=${step#probe_}; run "probe_$p" 200 "$ROOTDIR/build/${p}_probe" ;;
     groupbench_*) wl=${step#groupbench_}  # an 8-member group on this device, no profiler (flush_ms as a caller sees it)
       run "groupbench_$wl" 300 python bench.py --workload "$wl" --sub "" --group 8 --steps 10 --warmup 2 --soak-s 0 \
