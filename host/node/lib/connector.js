@@ -66,6 +66,11 @@ function parseDurationNs(s) {
 // reserved key strings (a real key never starts with U+0001 / U+0002)
 const OVERFLOW_KEY = '\u0001otel.metric.overflow';
 const EVENT_KEY_PREFIX = '\u0002events\u0000';
+// calls_dimensions / histogram.dimensions: the calls and the duration metric
+// keep separate series (upstream: separate sums and histograms maps), keyed
+// in their own namespaces
+const CALLS_KEY_PREFIX = '\u0003calls\u0000';
+const HIST_KEY_PREFIX = '\u0004hist\u0000';
 
 const NONE = [];
 const asBuffer = (b) => (Buffer.isBuffer(b) ? b : Buffer.from(b.buffer, b.byteOffset, b.byteLength));
@@ -103,12 +108,23 @@ function normalizeConfig(cfg = {}, addon) {
   }
   const temporality = cfg.aggregation_temporality || 'AGGREGATION_TEMPORALITY_CUMULATIVE';
   if (!(temporality in TEMPORALITY)) throw new Error(`unknown aggregation_temporality ${temporality}`);
-  const dims = (cfg.dimensions || []).map((x) => ({ name: x.name,
+  const dimList = (l) => (l || []).map((x) => ({ name: x.name,
     default: x.default === undefined || x.default === null ? undefined : String(x.default) }));
+  const dims = dimList(cfg.dimensions);
+  // [UPSTREAM] config.go (confidence M): calls_dimensions and histogram.dimensions
+  // add dimensions to one metric only, after `dimensions`
+  const callsDims = dims.concat(dimList(cfg.calls_dimensions));
+  const histDims = dims.concat(dimList(hist.dimensions));
   const sk = cfg.sketches || {};
   const windowNs = sk.window !== undefined ? BigInt(Math.round(parseDurationNs(sk.window))) : d.windowNs;
   return {
-    unit, bounds, dims, expMaxSize,
+    unit, bounds, dims, expMaxSize, callsDims, histDims,
+    splitKeys: callsDims.length !== dims.length || histDims.length !== dims.length,
+    // histogram.disable: no duration metric (the calls metric stays)
+    histogramDisable: !!hist.disable,
+    // metrics_expiration: cumulative resources not seen for this long are
+    // exported one last time and then dropped (0: never)
+    expirationNs: cfg.metrics_expiration !== undefined ? BigInt(Math.round(parseDurationNs(cfg.metrics_expiration))) : 0n,
     exclude: new Set(cfg.exclude_dimensions || []),
     temporality: TEMPORALITY[temporality],
     namespace: cfg.namespace === undefined ? 'traces.span.metrics' : cfg.namespace,
@@ -184,8 +200,10 @@ class SpanMetricsConnector {
     this.nativeBuffered = 0;
     this.nativeRequests = 0;
     this.jsRequests = 0;
+    // (calls_dimensions / histogram.dimensions key every span twice: the
+    // JavaScript columnizer does that)
     if (opts.native !== false && typeof this.addon.createColumnizer === 'function' &&
-        this.rules.every((r) => r.native)) {
+        this.rules.every((r) => r.native) && !c.splitKeys) {
       this.col = this.addon.createColumnizer(this.handle, { dims: c.dims,
         exclude: [...c.exclude], rules: this.rules.map((r) => r.native),
         keyAttributes: c.resourceKeyAttributes, threads: c.columnizerThreads,
@@ -256,7 +274,7 @@ class SpanMetricsConnector {
     const h = keys.resourceHash(hashAttrs);
     return this._touchResource(h) ||
       this._admitResource({ hash: h, attributes: resAttrs, startTs: this.clock(), byKey: new Map(),
-        sids: [], nSpanSeries: 0 });
+        sids: [], nSpanSeries: 0, nByKind: {} });
   }
 
   /** LRU hit (or revival from the evicted side map) by resource hash; undefined on a miss. */
@@ -265,6 +283,7 @@ class SpanMetricsConnector {
     if (r !== undefined) {
       this.resources.delete(h);  // refresh LRU position
       this.resources.set(h, r);
+      if (this.cfg.expirationNs) r.lastSeen = this.clock();
       return r;
     }
     r = this.evicted.get(h);
@@ -274,6 +293,7 @@ class SpanMetricsConnector {
   }
 
   _admitResource(r) {
+    if (this.cfg.expirationNs) r.lastSeen = this.clock();
     this.resources.set(r.hash, r);
     if (this.resources.size > this.cfg.resourceCacheSize) {
       const [oldest, rec] = this.resources.entries().next().value;
@@ -309,6 +329,7 @@ class SpanMetricsConnector {
         counts: null, sumNs: 0n, exemplars: [] });
       res.sids.push(sid);
       if (kind === 'span') res.nSpanSeries += 1;
+      res.nByKind[kind] = (res.nByKind[kind] || 0) + 1;
     }
     res.byKey.set(keyStr, sid);
     return sid;
@@ -319,6 +340,7 @@ class SpanMetricsConnector {
     const status = span.status ? span.status.code : 0;
     const keyStr = keys.buildKeyString(service, span.name, span.kind, status, c.dims, spanAttrs,
       resAttrs, c.exclude);
+    if (c.splitKeys) return this._splitId(res, service, span, resAttrs, spanAttrs, status, HIST_KEY_PREFIX);
     const known = res.byKey.get(keyStr);
     if (known !== undefined) return known;
     // aggregation_cardinality_limit: past `limit` series in a resource, new keys
@@ -329,6 +351,29 @@ class SpanMetricsConnector {
     }
     return this._intern(res, keyStr, 'span', status, () => keys.buildAttributes(service, span.name,
       span.kind, status, c.dims, spanAttrs, resAttrs, c.exclude));
+  }
+
+  /**
+   * calls_dimensions / histogram.dimensions: the span's duration-metric series
+   * (prefix HIST_KEY_PREFIX, dimensions + histogram.dimensions) or its
+   * calls-metric series (CALLS_KEY_PREFIX, dimensions + calls_dimensions); the
+   * cardinality limit applies to each metric's series on their own.
+   */
+  _splitId(res, service, span, resAttrs, spanAttrs, status, prefix) {
+    const c = this.cfg;
+    const calls = prefix === CALLS_KEY_PREFIX;
+    const d = calls ? c.callsDims : c.histDims;
+    const keyStr = prefix + keys.buildKeyString(service, span.name, span.kind, status, d, spanAttrs, resAttrs,
+      c.exclude);
+    const known = res.byKey.get(keyStr);
+    if (known !== undefined) return known;
+    const kind = calls ? 'calls' : 'hist';
+    if (c.cardinalityLimit > 0 && (res.nByKind[kind] || 0) >= c.cardinalityLimit) {
+      return this._intern(res, prefix + OVERFLOW_KEY, calls ? 'calls-overflow' : 'hist-overflow', 0,
+        () => [{ key: 'otel.metric.overflow', value: { type: 'bool', value: true } }]);
+    }
+    return this._intern(res, keyStr, kind, status, () => keys.buildAttributes(service, span.name,
+      span.kind, status, d, spanAttrs, resAttrs, c.exclude));
   }
 
   /** events.enabled: one record per span event, keyed by the span key + event dimensions. */
@@ -468,6 +513,10 @@ class SpanMetricsConnector {
           const spanAttrs = this.cfg.dims.length ? keys.attrMap(span.attributes) : undefined;
           const sid = this._seriesId(res, service, span, resAttrs, spanAttrs);
           if (this.cfg.exemplars) this._exemplar(sid, span);
+          if (this.cfg.splitKeys) {  // the calls series gets the span as a second record
+            const code = span.status ? span.status.code : 0;
+            this._pushSpan(this._splitId(res, service, span, resAttrs, spanAttrs, code, CALLS_KEY_PREFIX), span, svcId);
+          }
           const i = cols.n;
           cols.keyHash[i] = sid;
           cols.startNs[i] = BigInt.asUintN(64, BigInt(span.startTimeUnixNano || 0));
@@ -589,6 +638,29 @@ class SpanMetricsConnector {
       asDouble: Number(en > st ? en - st : 0n) / (this.cfg.unit === 's' ? 1e9 : 1e6) });
   }
 
+  /** One span record of series `sid` (the JavaScript columnizer's layout). */
+  _pushSpan(sid, span, svcId) {
+    const cols = this.cols;
+    const i = cols.n;
+    cols.keyHash[i] = sid;
+    cols.startNs[i] = BigInt.asUintN(64, BigInt(span.startTimeUnixNano || 0));
+    cols.endNs[i] = BigInt.asUintN(64, BigInt(span.endTimeUnixNano || 0));
+    const tid = span.traceId;
+    if (tid && tid.length === 16) {
+      cols.w0u8.set(tid.subarray(0, 8), 8 * i);
+      cols.w1u8.set(tid.subarray(8, 16), 8 * i);
+    } else {
+      cols.traceW0[i] = 0n;
+      cols.traceW1[i] = 0n;
+    }
+    const kind = span.kind >= 0 && span.kind <= 7 ? span.kind : 7;
+    const code = span.status ? span.status.code : 0;
+    const st = code >= 0 && code <= 3 ? code : 3;
+    cols.meta[i] = (svcId | (kind << 16) | (st << 19)) >>> 0;
+    cols.n = i + 1;
+    if (cols.n === cols.cap) this._drain();
+  }
+
   /** An event record: counted by the engine like a span of duration 0, with an
    * out-of-range service id so it touches no sketch. */
   _pushEvent(sid) {
@@ -689,7 +761,16 @@ class SpanMetricsConnector {
     };
     for (const res of this.resources.values()) emitResource(res);
     for (const res of this.evicted.values()) emitResource(res);
-    // resetState: delta purges; cumulative drops what the LRU evicted
+    // resetState: delta purges; cumulative drops what the LRU evicted and
+    // (metrics_expiration) the resources not seen within the expiration
+    if (!delta && this.cfg.expirationNs) {
+      for (const [h, res] of [...this.resources]) {
+        if (now - res.lastSeen >= this.cfg.expirationNs) {
+          this.resources.delete(h);
+          this.evicted.set(h, res);
+        }
+      }
+    }
     for (const res of this.evicted.values()) {
       for (const sid of res.sids) { this.series.delete(sid); this.lastDeltaTs.delete(sid); }
       if (this.col) this.addon.columnizerForget(this.col, res.hash);
@@ -753,7 +834,15 @@ class SpanMetricsConnector {
         events.push({ attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, asInt: count });
         continue;
       }
-      calls.push({ attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, asInt: count });
+      // (split keys: a 'calls' series feeds only the calls metric, a 'hist'
+      // series only the duration metric)
+      const isCalls = s.kind === 'calls' || s.kind === 'calls-overflow';
+      const isHist = s.kind === 'hist' || s.kind === 'hist-overflow';
+      if (!isHist) calls.push({ attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, asInt: count });
+      if (isCalls || c.histogramDisable) {
+        s.exemplars = [];
+        continue;
+      }
       const h = e
         ? { attributes: s.dpAttrs, startTimeUnixNano: start, timeUnixNano: now, count, sum: Number(e.sumNs) / div,
           scale: e.scale, zeroCount: e.zeroCount, positive: { offset: e.offset, bucketCounts: e.counts.slice() },
@@ -766,12 +855,13 @@ class SpanMetricsConnector {
     }
     if (this.col && c.exemplars && this.addon.columnizerResetExemplars) this.addon.columnizerResetExemplars(this.col);
     const out = [
-      { name: ns + 'calls', sum: { dataPoints: calls, aggregationTemporality: temporality, isMonotonic: true } },
-      c.expMaxSize
+      { name: ns + 'calls', sum: { dataPoints: calls, aggregationTemporality: temporality, isMonotonic: true } }];
+    if (!c.histogramDisable) {
+      out.push(c.expMaxSize
         ? { name: ns + 'duration', unit: c.unit,
           exponentialHistogram: { dataPoints: hists, aggregationTemporality: temporality } }
-        : { name: ns + 'duration', unit: c.unit, histogram: { dataPoints: hists, aggregationTemporality: temporality } },
-    ];
+        : { name: ns + 'duration', unit: c.unit, histogram: { dataPoints: hists, aggregationTemporality: temporality } });
+    }
     if (c.events) {
       out.push({ name: ns + 'events', sum: { dataPoints: events, aggregationTemporality: temporality,
         isMonotonic: true } });

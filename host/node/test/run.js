@@ -321,6 +321,52 @@ test('connector: dimensions, defaults, exclude_dimensions and first-seen attribu
   assert.strictEqual(attr(c[1], 'http.status_code'), undefined);
 });
 
+// connector options restated in tests/golden/gen_golden.py (connector_cases)
+const KAT = require(path.join(__dirname, '..', '..', '..', 'tests', 'golden', 'spanmetrics_kat.json'));
+const katCase = (name) => KAT.connector_cases.find((c) => c.name === name);
+const dpKey = (dp) => JSON.stringify(dp.attributes.map((a) => [a.key, a.value.value]));
+
+test('connector: metrics_expiration drops resources not seen within it, after one last export (KAT)', () => {
+  const c = katCase('metrics_expiration');
+  const t = { now: 0n };
+  const { conn } = mkConnector(c.config, t);
+  const got = [];
+  for (const op of c.ops) {
+    t.now = BigInt(op.t);
+    if (op.consume) {
+      conn.consumeTraces(request(op.consume.map(([svc, n]) => [{ 'service.name': svc },
+        Array.from({ length: n }, () => span('op'))])));
+    } else {
+      const e = {};
+      for (const dp of dpsOf(conn.exportMetrics(), 'traces.span.metrics.calls')) {
+        e[attr(dp, 'service.name').value] = [Number(dp.asInt), Number(dp.startTimeUnixNano)];
+      }
+      got.push(e);
+    }
+  }
+  assert.deepStrictEqual(got, c.expected);
+});
+
+for (const name of ['calls_and_histogram_dimensions', 'histogram_disable']) {
+  test(`connector: ${name.replace(/_/g, ' ')} (KAT)`, () => {
+    const c = katCase(name);
+    const { conn } = mkConnector(c.config);
+    for (const [svc, nm, kind, st, attrs] of c.spans) {
+      conn.consumeTraces(request([[{ 'service.name': svc }, [span(nm, { kind, status: { code: st, message: '' },
+        attributes: Object.entries(attrs).map(([key, v]) => ({ key, value: str(v) })) })]]]));
+    }
+    const out = conn.exportMetrics();
+    const calls = dpsOf(out, 'traces.span.metrics.calls').map((dp) => [dpKey(dp), Number(dp.asInt)]).sort();
+    const hist = dpsOf(out, 'traces.span.metrics.duration').map((dp) => [dpKey(dp), Number(dp.count)]).sort();
+    const want = (l) => l.map(([at, n]) => [JSON.stringify(at), n]).sort();
+    assert.deepStrictEqual(calls, want(c.expected.calls));
+    assert.deepStrictEqual(hist, want(c.expected.histogram));
+    if (name === 'histogram_disable') {
+      assert.ok(out.resourceMetrics.every((rm) => rm.scopeMetrics[0].metrics.every((m) => !m.histogram)));
+    }
+  });
+}
+
 test('connector: consumes OTLP bytes; columns carry trace ids and meta bits', () => {
   const { conn, addon } = mkConnector({ batch_size: 2 });
   const tid = Uint8Array.from({ length: 16 }, (_, i) => 0xA0 + i);

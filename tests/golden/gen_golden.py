@@ -204,6 +204,90 @@ def hash_vectors():
     return vec, sm
 
 
+# ---- connector-level options (host logic of the Node connector) -----------
+# Restated from [UPSTREAM] spanmetricsconnector config.go / connector.go
+# v0.125.0 (confidence M: the Go source is not in the container): resetState
+# drops, after an export, the cumulative resources whose lastSeen is at least
+# metrics_expiration old; calls_dimensions / histogram.dimensions add
+# dimensions to one metric's key only (separate sums / histograms maps).
+
+
+def restate_expiration(ops, exp_ns):
+    res, out = {}, []
+    for op in ops:
+        t = op["t"]
+        if "consume" in op:
+            for svc, n in op["consume"]:
+                r = res.setdefault(svc, dict(calls=0, start=t, last=t))
+                r["calls"] += n
+                r["last"] = t
+        else:  # an export (cumulative): every resource, then the expired ones go
+            out.append({svc: [r["calls"], r["start"]] for svc, r in sorted(res.items())})
+            for svc in [k for k, r in res.items() if t - r["last"] >= exp_ns]:
+                del res[svc]
+    return out
+
+
+def case_expiration():
+    s = 1_000_000_000
+    ops = [dict(t=0, consume=[["a", 1], ["b", 2]]), dict(t=1 * s, export=True),
+           dict(t=2 * s, consume=[["a", 1]]), dict(t=4 * s, export=True),
+           dict(t=6 * s, export=True),                      # b (last seen 0) expires after this one
+           dict(t=7 * s, consume=[["b", 5]]), dict(t=8 * s, export=True),   # b back, fresh start
+           dict(t=9 * s, export=True),                      # a (last seen 2 s) expires after this one
+           dict(t=10 * s, export=True)]
+    return dict(name="metrics_expiration", config={"metrics_expiration": "5s"}, ops=ops,
+                expected=restate_expiration(ops, 5 * s))
+
+
+KIND = ["SPAN_KIND_UNSPECIFIED", "SPAN_KIND_INTERNAL", "SPAN_KIND_SERVER", "SPAN_KIND_CLIENT",
+        "SPAN_KIND_PRODUCER", "SPAN_KIND_CONSUMER"]
+
+
+def restate_split(spans, dims, calls_dims, hist_dims):
+    """spans: (service, name, kind, status, {attr: str}); dims: [(name, default)].
+    Returns the calls and histogram data points as [[attrs...], count]."""
+    def point(svc, name, kind, st, attrs, ds):
+        key = [svc, name, KIND[kind], ["STATUS_CODE_UNSET", "STATUS_CODE_OK", "STATUS_CODE_ERROR"][st]]
+        at = [["service.name", svc], ["span.name", name], ["span.kind", KIND[kind]], ["status.code", key[3]]]
+        for dn, dd in ds:
+            v = attrs.get(dn, dd)
+            if v is None:
+                continue          # a missing dimension without a default adds nothing (A5)
+            key.append(v)
+            at.append([dn, v])
+        return "\0".join(key), at
+    calls, hist = {}, {}
+    for svc, name, kind, st, attrs in spans:
+        for table, ds in ((calls, dims + calls_dims), (hist, dims + hist_dims)):
+            k, at = point(svc, name, kind, st, attrs, ds)
+            e = table.setdefault(k, [at, 0])
+            e[1] += 1
+    return [v for _, v in sorted(calls.items())], [v for _, v in sorted(hist.items())]
+
+
+def case_split_dims():
+    spans = [("a", "GET /x", 2, 0, {"http.method": "GET", "http.route": "/x"}),
+             ("a", "GET /x", 2, 0, {"http.method": "GET", "http.route": "/y"}),
+             ("a", "GET /x", 2, 0, {"http.method": "POST"}),
+             ("a", "GET /x", 2, 2, {"http.route": "/x"}),
+             ("a", "op", 1, 0, {}),
+             ("b", "op", 3, 1, {"http.method": "GET", "region": "us"})]
+    dims, cd, hd = [["region", None]], [["http.method", None]], [["http.route", "none"]]
+    calls, hist = restate_split(spans, dims, cd, hd)
+    cfg = {"dimensions": [{"name": "region"}], "calls_dimensions": [{"name": "http.method"}],
+           "histogram": {"dimensions": [{"name": "http.route", "default": "none"}]}}
+    return dict(name="calls_and_histogram_dimensions", config=cfg,
+                spans=[[a, b, c, d, e] for a, b, c, d, e in spans], expected=dict(calls=calls, histogram=hist))
+
+
+def case_histogram_disable():
+    spans = [("a", "op", 2, 0, {}), ("a", "op", 2, 0, {}), ("b", "op", 2, 2, {})]
+    calls, _ = restate_split(spans, [], [], [])
+    return dict(name="histogram_disable", config={"histogram": {"disable": True}},
+                spans=[[a, b, c, d, e] for a, b, c, d, e in spans], expected=dict(calls=calls, histogram=[]))
+
+
 def main():
     cases = [
         build_case(case_kat_basic()),
@@ -214,7 +298,8 @@ def main():
     ]
     xv, sm = hash_vectors()
     out = dict(generator="tests/golden/gen_golden.py", xxhash_version=xxhash.VERSION, cases=cases,
-               xxh64_vectors=xv, splitmix64_vectors=sm)
+               xxh64_vectors=xv, splitmix64_vectors=sm,
+               connector_cases=[case_expiration(), case_split_dims(), case_histogram_disable()])
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "spanmetrics_kat.json")
     with open(path, "w") as f:
         json.dump(out, f, separators=(",", ":"))

@@ -188,8 +188,9 @@ def test_group_c4_8_members_device_flush():
     """Verdict r3: an 8-member group on device 0 at C4 cardinality (1 M series
     over 2,000 routes x 500 pods, 10 M spans per launch, two launches) through
     sa_group_ingest_device, flushed against the oracle.  Each member holds
-    ~0.75 M of the series, so the flush unions ~6 M ids on the device (rocPRIM
-    radix sort + unique), densifies 8 x 1 M rows, sums them on the device and
+    ~0.75 M of the series, so the flush unions ~6 M ids on the device (the
+    engine's own bucket sort + per-bucket bitonic sort and unique,
+    spanagg_union.hip), densifies 8 x 1 M rows, sums them on the device and
     builds the result's columns there (no host sort, no host row loop)."""
     import time
     import torch
