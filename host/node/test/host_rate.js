@@ -4,7 +4,8 @@
  * transform rules -> keying -> SoA columns -> addon.ingest.  SURVEY.md 8(d)
  * asks for the OTLP decode+aggregate rate from protobuf bytes.
  *
- *   node test/host_rate.js [spans] [--gpu] [--threads T] [--batch B] [--exemplars] [--events] [--dump FILE]
+ *   node test/host_rate.js [spans] [--gpu] [--threads T] [--batch B] [--exemplars] [--events] [--highcard]
+ *                          [--dump FILE]
  *
  * --threads T --batch B: requests go through consumeTracesBatch B at a time
  * (what the pipeline's queue does under load), decoded on T columnizer
@@ -13,7 +14,12 @@
  * --gpu the real addon ingests (host memory -> HBM -> kernel) and the result
  * is checked for span count.  --exemplars: exemplars.enabled (5 per data
  * point); --events: events.enabled on exception.type, with one span in 16
- * carrying an exception event.  Prints one JSON line.
+ * carrying an exception event.  --highcard: BASELINE config 4's vocabulary --
+ * 500 pods (resource attribute k8s.pod.name) x 2,000 routes (span attribute
+ * http.route, a configured dimension) = 1 M series over a binned engine
+ * table; the warm-up is a whole pass over the requests, so the timed pass
+ * sees every series known, as a long-running collector does.  Prints one
+ * JSON line.
  */
 const path = require('path');
 const lib = path.join(__dirname, '..', 'lib');
@@ -27,8 +33,9 @@ const jsOnly = process.argv.includes('--js');  // force the JavaScript columnize
 const argOf = (k, d) => { const i = process.argv.indexOf(k); return i > 0 ? parseInt(process.argv[i + 1], 10) : d; };
 const threads = argOf('--threads', 1), batch = argOf('--batch', 0);
 const exemplars = process.argv.includes('--exemplars'), events = process.argv.includes('--events');
+const highcard = process.argv.includes('--highcard');
 const PER_REQUEST = 512;  // an SDK batch span processor's default export batch
-const SERVICES = 20, NAMES = 25;
+const SERVICES = 20, NAMES = 25, PODS = 500, ROUTES = 2000;
 
 function makeRequests() {
   let seed = 42;
@@ -36,23 +43,28 @@ function makeRequests() {
   const reqs = [];
   const T0 = 1700000000000000000n;
   for (let done = 0; done < n; done += PER_REQUEST) {
-    const svc = Math.floor(rnd() * SERVICES);
+    const pod = highcard ? Math.floor(rnd() * PODS) : 0;
+    const svc = highcard ? pod % SERVICES : Math.floor(rnd() * SERVICES);
     const spans = [];
     for (let i = 0; i < Math.min(PER_REQUEST, n - done); i++) {
-      const name = Math.floor(rnd() * NAMES);
+      const route = highcard ? Math.floor(rnd() * ROUTES) : 0;
+      const name = highcard ? route % NAMES : Math.floor(rnd() * NAMES);
       const start = T0 + BigInt(Math.floor(rnd() * 6e10));
       const tid = new Uint8Array(16);
       for (let k = 0; k < 16; k++) tid[k] = Math.floor(rnd() * 256);
       spans.push({ traceId: tid, spanId: tid.subarray(0, 8), name: name % 5 === 0 ? `GET /api/products/${name}?x=1` : `op-${name}`,
         kind: 2, startTimeUnixNano: start, endTimeUnixNano: start + BigInt(Math.floor(rnd() * 2e7)),
-        attributes: [{ key: 'http.method', value: { type: 'string', value: 'GET' } }],
+        attributes: highcard ? [{ key: 'http.method', value: { type: 'string', value: 'GET' } },
+          { key: 'http.route', value: { type: 'string', value: `/api/r${route}` } }]
+          : [{ key: 'http.method', value: { type: 'string', value: 'GET' } }],
         status: { code: rnd() < 0.02 ? 2 : 0, message: '' },
         events: events && (i & 15) === 0 ? [{ timeUnixNano: start, name: 'exception',
           attributes: [{ key: 'exception.type', value: { type: 'string', value: `E${name % 3}` } }] }] : [] });
     }
-    reqs.push(otlp.encodeTraces({ resourceSpans: [{ resource: { attributes: [
-      { key: 'service.name', value: { type: 'string', value: `svc-${svc}` } },
-      { key: 'telemetry.sdk.language', value: { type: 'string', value: 'go' } }] },
+    const resAttrs = [{ key: 'service.name', value: { type: 'string', value: `svc-${svc}` } },
+      { key: 'telemetry.sdk.language', value: { type: 'string', value: 'go' } }];
+    if (highcard) resAttrs.push({ key: 'k8s.pod.name', value: { type: 'string', value: `pod-${pod}` } });
+    reqs.push(otlp.encodeTraces({ resourceSpans: [{ resource: { attributes: resAttrs },
       scopeSpans: [{ scope: { name: 'bench' }, spans }] }] }));
   }
   return reqs;
@@ -108,6 +120,7 @@ const phases = [0, 0, 0, 0, 0];
 }
 const p = new TracesToMetricsPipeline({ addon, receiver: false, exporter: false, memoryLimiter: false,
   native: !jsOnly, spanmetrics: Object.assign({ n_services: 64, columnizer_threads: threads },
+    highcard ? { dimensions: [{ name: 'http.route' }], key_capacity: 1200000 } : {},
     exemplars ? { exemplars: { enabled: true, max_per_data_point: 5 } } : {},
     events ? { events: { enabled: true, dimensions: [{ name: 'exception.type' }] } } : {}) });
 timed(p.connector, '_applyNative', 'apply');  // the host bookkeeping of the non-plain results
@@ -119,7 +132,8 @@ const consumeAll = (list) => {
   }
 };
 // warm-up on a tenth of the requests (JIT), then time the whole set
-const warm = reqs.slice(0, Math.max(1, Math.floor(reqs.length / 10)));
+// (--highcard: a whole pass, so every series is known when the timing starts)
+const warm = highcard ? reqs : reqs.slice(0, Math.max(1, Math.floor(reqs.length / 10)));
 consumeAll(warm);
 const warmSpans = BigInt(Math.min(n, warm.length * PER_REQUEST));
 p.connector.exportMetrics();
@@ -143,7 +157,8 @@ const st = p.connector.stats();
 const native = st.nativeRequests > 0 && st.jsRequests === 0;
 p.shutdown();
 console.log(JSON.stringify({ spans: n, requests: reqs.length, otlp_bytes: bytes, seconds: secs,
-  spans_per_s: n / secs, mb_per_s: bytes / secs / 1e6, cores: threads, batch, gpu,
+  spans_per_s: n / secs, mb_per_s: bytes / secs / 1e6, cores: threads, batch, gpu, highcard,
+  series: st.series,
   seconds_in: { columnize_batch: Number(spent.columnize) / 1e9, ingest: Number(spent.ingest) / 1e9,
     sync: Number(spent.sync) / 1e9, apply_native: Number(spent.apply) / 1e9,
     columnize_phases: { decode: phases[0] / 1e9, commit: phases[1] / 1e9, place: phases[2] / 1e9,
