@@ -13,6 +13,7 @@
 #include <string>
 #include <vector>
 
+#include "sa_group_hooks.h"
 #include "sa_internal.h"
 #include "sa_results.h"
 #include "spanagg.h"
@@ -1203,9 +1204,64 @@ static int reclaim_if_full(sa_engine *e) {
   uint64_t nk = 0;
   SA_HIP(e, hipMemcpyAsync(&nk, e->scratch, 8, hipMemcpyDeviceToHost, e->stream));
   SA_HIP(e, hipStreamSynchronize(e->stream));
-  const bool over = e->bt ? 20 * nk > 7 * (uint64_t)e->cap : 2 * nk > e->cap;
-  return over ? reclaim_now(e) : SA_OK;
+  return sa_grp::over_reclaim_threshold(e, nk) ? reclaim_now(e) : SA_OK;
 }
+
+}  // extern "C"
+
+namespace sa_grp {
+bool over_reclaim_threshold(const sa_engine *e, uint64_t nk) {
+  return e->bt ? 20 * nk > 7 * (uint64_t)e->cap : 2 * nk > e->cap;
+}
+
+int export_keys_async(sa_engine *e, uint64_t *d_keys, uint64_t cap, uint64_t *h_n, uint64_t *h_dropped,
+                      hipStream_t s) {
+  if (!e || !h_n || !h_dropped || (cap && !d_keys)) return SA_EINVAL;
+  if (e->expo) return fail(e, SA_ESTATE, "merge hooks cover explicit-bucket engines only");
+  if (int rc = set_dev(e)) return rc;
+  if (int rc = join_checked(e)) return rc;
+  SA_HIP(e, hipEventRecord(e->ev_a, e->stream));
+  SA_HIP(e, hipStreamWaitEvent(s, e->ev_a, 0));
+  if (int rc = reduce_slabs(e, s)) return rc;
+  SA_HIP(e, hipMemsetAsync(e->scratch, 0, 8, s));
+  SA_HIP(e, sa::launch_compact(e->gkeys, e->gcounts, e->cap, geom(e), reinterpret_cast<unsigned long long *>(d_keys),
+                               nullptr, e->scratch, cap, 0, s));
+  SA_HIP(e, hipMemcpyAsync(h_n, e->scratch, 8, hipMemcpyDeviceToHost, s));
+  SA_HIP(e, hipMemcpyAsync(h_dropped, e->stats + sa::kStatDropped, 8, hipMemcpyDeviceToHost, s));
+  // later engine work (the gather's counter reset) orders after these reads
+  SA_HIP(e, hipEventRecord(e->ev_b, s));
+  SA_HIP(e, hipStreamWaitEvent(e->stream, e->ev_b, 0));
+  return SA_OK;
+}
+
+int count_keys_async(sa_engine *e, uint64_t *h_n) {
+  if (!e || !h_n) return SA_EINVAL;
+  if (int rc = set_dev(e)) return rc;
+  if (int rc = join_checked(e)) return rc;
+  SA_HIP(e, hipMemsetAsync(e->scratch + 1, 0, 8, e->stream));
+  SA_HIP(e, sa::launch_count_keys(e->gkeys, e->cap, e->scratch + 1, e->stream));
+  SA_HIP(e, hipMemcpyAsync(h_n, e->scratch + 1, 8, hipMemcpyDeviceToHost, e->stream));
+  return SA_OK;
+}
+
+int reclaim_async(sa_engine *e) {
+  if (!e) return SA_EINVAL;
+  if (e->unflushed) return fail(e, SA_ESTATE, "reclaim: spans ingested since the last flush");
+  if (int rc = set_dev(e)) return rc;
+  return reclaim_now(e);
+}
+
+uint64_t table_capacity(const sa_engine *e) { return e ? e->cap : 0; }
+
+int sync_stream(sa_engine *e) {
+  if (!e) return SA_EINVAL;
+  if (int rc = set_dev(e)) return rc;
+  SA_HIP(e, hipStreamSynchronize(e->stream));
+  return SA_OK;
+}
+}  // namespace sa_grp
+
+extern "C" {
 
 int sa_reclaim_keys(sa_engine *e, int force) {
   if (!e) return SA_EINVAL;

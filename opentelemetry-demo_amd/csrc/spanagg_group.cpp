@@ -22,6 +22,7 @@
 #include <thread>
 #include <vector>
 
+#include "sa_group_hooks.h"
 #include "sa_internal.h"
 #include "sa_results.h"
 #include "spanagg.h"
@@ -330,6 +331,7 @@ struct sa_group {
   // (when the caller alternates streams), never the one of the same set
   std::vector<Buf> pcnt;
   unsigned long long *hcnt = nullptr;    // pinned host copy of the counts
+  uint64_t *hflush = nullptr;            // pinned [3][kMaxMembers]: flush key counts, drop counters, resident keys
   // page-locked blocks the flush results' columns are copied into (sa_results.h)
   std::shared_ptr<PinPool> pins = std::make_shared<PinPool>();
   // sa_group_ingest: per-member packed host shards, reused across calls
@@ -543,7 +545,8 @@ int sa_group_create(const sa_config *cfg, const int32_t *devices, uint32_t n, sa
         return SA_EDEVICE;
       }
   }
-  if (hipHostMalloc((void **)&g->hcnt, kMaxMembers * 8, hipHostMallocDefault) != hipSuccess) {
+  if (hipHostMalloc((void **)&g->hcnt, kMaxMembers * 8, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void **)&g->hflush, 3 * kMaxMembers * 8, hipHostMallocDefault) != hipSuccess) {
     sa_group_destroy(g);
     return SA_ENOMEM;
   }
@@ -594,6 +597,7 @@ void sa_group_destroy(sa_group *g) {
     sa_destroy(g->eng[i]);
   }
   if (g->hcnt) (void)hipHostFree(g->hcnt);
+  if (g->hflush) (void)hipHostFree(g->hflush);
   delete g;
 }
 
@@ -781,16 +785,21 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
   *out = nullptr;
   if (g->cfg.exp_max_size) return gfail(g, SA_ESTATE, "exponential-histogram group: use sa_group_flush_exp");
   const uint32_t n = (uint32_t)g->eng.size(), stride = g->nbk + 1;
-  // 1. each member's non-zero series ids (and its drop counter)
-  std::vector<uint64_t> cnt(n, 0), dropped(n, 0);
+  // 1. each member's non-zero series ids and its drop counter: every
+  //    member's export is enqueued first, then one wait per member stream
+  uint64_t *hn = g->hflush, *hdrop = g->hflush + kMaxMembers, *hkeys = g->hflush + 2 * kMaxMembers;
   for (uint32_t i = 0; i < n; ++i) {
-    sa_stats s;
-    if (int rc = sa_get_stats(g->eng[i], &s)) return member_error(g, i, rc, "sa_get_stats");
-    dropped[i] = s.dropped_table_full;
-    if (int rc = ensure(g, g->dev[i], g->keys[i], s.table_capacity * 8)) return rc;
-    if (int rc = sa_export_keys(g->eng[i], static_cast<uint64_t *>(g->keys[i].p), s.table_capacity, &cnt[i], g->st[i]))
+    const uint64_t tc = sa_grp::table_capacity(g->eng[i]);
+    if (int rc = ensure(g, g->dev[i], g->keys[i], tc * 8)) return rc;
+    if (int rc = sa_grp::export_keys_async(g->eng[i], static_cast<uint64_t *>(g->keys[i].p), tc, &hn[i], &hdrop[i],
+                                           g->st[i]))
       return member_error(g, i, rc, "sa_export_keys");
   }
+  for (uint32_t i = 0; i < n; ++i) {
+    SG_HIP(g, hipSetDevice(g->dev[i]));
+    SG_HIP(g, hipStreamSynchronize(g->st[i]));
+  }
+  std::vector<uint64_t> cnt(hn, hn + n), dropped(hdrop, hdrop + n);
   // 2. the sorted key union (the dense index every member densifies against),
   //    built on the devices: RCCL gathers every member's list onto every
   //    member, and each sorts / uniques its copy (identical bits everywhere,
@@ -919,19 +928,21 @@ int sa_group_flush(sa_group *g, sa_red_result **out) {
     SG_HIP(g, hipMemcpyAsync(hc, d_counts, fin_bytes, hipMemcpyDeviceToHost, g->st[0]));
     (void)d_sum;
     // every member's counters are reset (gather_dense), so its key table can
-    // be reclaimed now, while the result's copy is in flight (member 0, whose
-    // merge stream carries the copy, last)
-    for (uint32_t j = 0; j < n; ++j) {
-      const uint32_t i = (j + 1) % n;
-      SG_HIP(g, hipSetDevice(g->dev[i]));
-      SG_HIP(g, hipStreamSynchronize(g->st[i]));
-      if (int rc = sa_reclaim_keys(g->eng[i], 0); rc != SA_OK && rc != SA_ESTATE)
-        return drop(member_error(g, i, rc, "sa_reclaim_keys"));
-    }
+    // be reclaimed now, while the result's copy is in flight: the resident-key
+    // counts of all members first (one wait), then the reclamation of the
+    // tables over the threshold (sa_flush's policy), waited for at the end
+    for (uint32_t i = 0; i < n; ++i)
+      if (int rc = sa_grp::count_keys_async(g->eng[i], &hkeys[i])) return drop(member_error(g, i, rc, "count keys"));
+    for (uint32_t i = 0; i < n; ++i)
+      if (int rc = sa_grp::sync_stream(g->eng[i])) return drop(member_error(g, i, rc, "count keys"));
+    for (uint32_t i = 0; i < n; ++i)
+      if (sa_grp::over_reclaim_threshold(g->eng[i], hkeys[i]))
+        if (int rc = sa_grp::reclaim_async(g->eng[i])) return drop(member_error(g, i, rc, "sa_reclaim_keys"));
+    for (uint32_t i = 0; i < n; ++i)
+      if (int rc = sa_grp::sync_stream(g->eng[i])) return drop(member_error(g, i, rc, "sa_reclaim_keys"));
   }
   // (the members' key-table reclamation above is the flush-time policy
-  // sa_flush applies; SA_ESTATE: nothing was gathered, the counters were
-  // never set)
+  // sa_flush applies)
   for (uint32_t i = 0; i < n; ++i) {
     SG_HIP(g, hipSetDevice(g->dev[i]));
     SG_HIP(g, hipStreamSynchronize(g->st[i]));

@@ -245,6 +245,40 @@ __global__ __launch_bounds__(kBlock) void p_chunked(Args A) {
   if (acc == 0x1234567ULL) A.out[0] = acc;
 }
 
+// The same with 8-B records (C-byte chunks of C / 8 lanes): the store side of
+// a scatter whose records carry a resolved key slot instead of the key
+template <int C>
+__global__ __launch_bounds__(kBlock) void p_chunked8(Args A) {
+  constexpr unsigned L = C / 8;  // lanes per chunk
+  const u64 lo = min((u64)blockIdx.x * A.chunk, A.n), hi = min(lo + A.chunk, A.n);
+  const unsigned len = (unsigned)(hi - lo);
+  const unsigned wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const u64 nchunks = A.n * 8 / C * 4;  // 4x sparse target
+  u64 acc = 0, st = 0x9E3779B97F4A7C15ULL * (blockIdx.x * 64 + wave + 1);
+  u64 *rec = reinterpret_cast<u64 *>(A.rec);
+  Tile t[2];
+  unsigned off0 = wave * 128 + lane * 2;
+  load_tile(A, lo, len, off0, t[0]);
+  load_tile(A, lo, len, off0 + 2048, t[1]);
+  for (unsigned off = off0; off < len; off += 4096) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const unsigned o = off + h * 2048;
+      Tile c = t[h];
+      load_tile(A, lo, len, o + 4096, t[h]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const u64 d = c.e[j] > c.s[j] ? c.e[j] - c.s[j] : 0;
+        acc ^= c.a[j] ^ c.b[j] ^ c.m[j];
+        st = st * 6364136223846793005ULL + 1442695040888963407ULL;
+        const u64 ch = ((st >> 20) + (lane / L) * 0x9E3779B1ULL) % nchunks;
+        if (o + j < len) rec[ch * L + (lane % L)] = c.k[j] ^ d;
+      }
+    }
+  }
+  if (acc == 0x1234567ULL) A.out[0] = acc;
+}
+
 // Chunked read: 160 MB read as random C-byte chunks (lanes as above)
 template <int C>
 __global__ __launch_bounds__(512) void a_chunked(Args A) {
@@ -338,11 +372,15 @@ int main(int argc, char **argv) {
   CK(hipFuncSetAttribute((const void *)&p_tilesort<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ts4));
   if (argc > 2) {
     timeit("loads", L(p_direct<0>, 0), true);
+    timeit("chunk_32", L(p_chunked<32>, 0), true);
     timeit("chunk_64", L(p_chunked<64>, 0), true);
     timeit("chunk_128", L(p_chunked<128>, 0), true);
     timeit("chunk_256", L(p_chunked<256>, 0), true);
     timeit("chunk_512", L(p_chunked<512>, 0), true);
     timeit("chunk_1024", L(p_chunked<1024>, 0), true);
+    timeit("chunk8_32", L(p_chunked8<32>, 0), true);
+    timeit("chunk8_64", L(p_chunked8<64>, 0), true);
+    timeit("chunk8_128", L(p_chunked8<128>, 0), true);
     auto R = [&](auto kern) { return [=]() { hipLaunchKernelGGL(kern, dim3(2048), dim3(512), 0, 0, A); }; };
     timeit("read_chunk_16", R(a_chunked<16>), true);
     timeit("read_chunk_64", R(a_chunked<64>), true);

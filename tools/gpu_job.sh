@@ -152,6 +152,7 @@ for step in "$@"; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_XT=$xt \
           run "xt_${wl}_x${xt}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $BQ
       done; done ;;
+    c4chunks) run c4chunks 200 "$ROOTDIR/build/c4_probe" 10000000 chunks ;;
     probe_*) p=${step#probe_}; run "probe_$p" 200 "$ROOTDIR/build/${p}_probe" ;;
     groupbench_*) wl=${step#groupbench_}  # an 8-member group on this device, no profiler (flush_ms as a caller sees it)
       run "groupbench_$wl" 300 python bench.py --workload "$wl" --sub "" --group 8 --steps 10 --warmup 2 --soak-s 0 \
