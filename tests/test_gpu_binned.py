@@ -270,3 +270,54 @@ def test_binned_repeat_runs_identical():
             outs.append(e.flush())
     for f in ("key_hash", "bucket_counts", "sum_ns"):
         assert np.array_equal(getattr(outs[0], f), getattr(outs[1], f))
+
+
+_FAIL_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from spanagg import Config, Engine, _lib
+from spanagg.synth import generate_highcard
+batch, _, first = generate_highcard(200_000, seed=5)
+dev = torch.device("cuda", 0)
+cols = [torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(dev)
+        for c in batch.columns()]
+e = Engine(Config(n_services=1, n_windows=16, key_capacity=1_200_000))
+e.window_advance(first)
+e.ingest_device(*cols, n=len(batch))              # pending: aggregated with the next launch
+codes = []
+for call in (lambda: e.ingest_device(*cols, n=len(batch)),   # its paired aggregate fails (injected)
+             lambda: e.ingest(batch),                        # the host path reports it
+             lambda: e.flush(),                              # and every read
+             lambda: e.window_read(first)):
+    try:
+        call()
+        codes.append(0)
+    except _lib.SpanAggError as x:
+        codes.append(x.code)
+print("CODES", codes)
+"""
+
+
+def test_failed_pending_aggregate_is_reported_by_every_later_call():
+    """Advisor r4: a pending binned record set belongs to an ingest that
+    already returned SA_OK; when the aggregate that takes it fails to launch,
+    the failure sticks -- the ingest that launched it, later host ingests,
+    flushes and window reads all return SA_EDEVICE instead of results without
+    those records.  The launch failure is injected in the laboratory build
+    (SPANAGG_FAIL_AGG=1: the process's first aggregate launch fails), run in a
+    child process so the product library of this process stays untouched."""
+    import os
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "opentelemetry-demo_amd")
+    lab = os.path.join(pkg, "spanagg", "libspanagg_ab.so")
+    if not os.path.exists(lab):
+        pytest.skip("laboratory build (make -C opentelemetry-demo_amd ab) not present")
+    env = dict(os.environ, SPANAGG_LIB=lab, SPANAGG_FAIL_AGG="1")
+    p = subprocess.run([sys.executable, "-c", _FAIL_SCRIPT, pkg], env=env, capture_output=True, text=True,
+                       timeout=240)
+    line = [l for l in p.stdout.splitlines() if l.startswith("CODES")]
+    assert line, p.stdout + p.stderr
+    import ast
+    codes = ast.literal_eval(line[0][len("CODES "):])
+    assert codes == [-3, -3, -3, -3], codes
