@@ -409,12 +409,11 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
   expo_select_lds(E, ent, scratch, lc);
   __syncthreads();
   const uint64_t lo = blockIdx.x * per_wg, hi = lo + per_wg < E.n ? lo + per_wg : E.n;
-  for (uint64_t i = lo + threadIdx.x; i < hi; i += kXcBlock) {
-    const uint32_t slot = E.slot_of[i];
-    const uint64_t st = E.start[i], en = E.end[i];
-    if (slot == kNotFound) continue;
+  const uint32_t len = hi > lo ? (uint32_t)(hi - lo) : 0u;
+  auto count = [&](uint32_t slot, uint64_t st, uint64_t en) {
+    if (slot == kNotFound) return;
     const uint64_t d = en > st ? en - st : 0;
-    if (d == 0) continue;
+    if (d == 0) return;
     const int2 m = meta[slot];
     int32_t ix;
     if (!expo_index_fast(d, E.log2div, m.x, ix)) ix = expo_index(expo_value(d, E.div), m.x);
@@ -428,6 +427,48 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
       const uint32_t r = tail ? atomicAdd(&tmisc[0], 1u) : kXtCap;
       if (r < kXtCap) trec[r] = slot << 12 | at;
       else atomicAdd(E.buckets + ((uint64_t)m.y * E.cap + slot) * M + at, 1u);
+    }
+  };
+  if (!tail) {  // (the earlier form: one span per thread per round, A/B runs of SPANAGG_XT=0)
+    for (uint32_t i = threadIdx.x; i < len; i += kXcBlock) count(E.slot_of[lo + i], E.start[lo + i], E.end[lo + i]);
+  } else {
+    // four consecutive spans per thread through 16-B buffer loads (0 past the
+    // range), two rounds in flight: with the tail off HBM atomics the loop is
+    // bound by its loads, and one span per thread per round kept only ~20 KB
+    // per CU in flight
+    const __amdgpu_buffer_rsrc_t rsl = rsrc(E.slot_of + lo, len * 4), rst = rsrc(E.start + lo, len * 8),
+                                 ren = rsrc(E.end + lo, len * 8);
+    struct Quad {
+      uint32_t sl[4];
+      uint64_t s[4], e[4];
+    };
+    auto load = [&](uint32_t base, Quad &q) {
+      const int o = (int)(base + 4 * threadIdx.x);
+      const auto a = __builtin_amdgcn_raw_buffer_load_b128(rsl, o * 4, 0, 0);
+      q.sl[0] = a[0], q.sl[1] = a[1], q.sl[2] = a[2], q.sl[3] = a[3];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rst, o * 8 + 16 * h, 0, 0);
+        const auto y = __builtin_amdgcn_raw_buffer_load_b128(ren, o * 8 + 16 * h, 0, 0);
+        q.s[2 * h] = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+        q.s[2 * h + 1] = (uint64_t)x[2] | ((uint64_t)x[3] << 32);
+        q.e[2 * h] = (uint64_t)y[0] | ((uint64_t)y[1] << 32);
+        q.e[2 * h + 1] = (uint64_t)y[2] | ((uint64_t)y[3] << 32);
+      }
+    };
+    auto run = [&](uint32_t base, const Quad &q) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (base + 4 * threadIdx.x + j < len) count(q.sl[j], q.s[j], q.e[j]);
+    };
+    constexpr uint32_t kStep = 4 * kXcBlock;
+    Quad qa, qb;
+    load(0, qa);
+    for (uint32_t base = 0; base < len; base += 2 * kStep) {
+      load(base + kStep, qb);
+      run(base, qa);
+      load(base + 2 * kStep, qa);
+      run(base + kStep, qb);
     }
   }
   __syncthreads();
@@ -716,7 +757,8 @@ hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s) {
   if (E.xslab && E.xc_ne) {  // small table, slab counting (E.xG workgroups, <= kXcMaxSpans spans each)
     if (E.cap > 2048) return hipErrorInvalidValue;  // the selection's two slots per thread
     launch_reduce_rescale(E, s);
-    const uint64_t per_wg = (E.n + E.xG - 1) / E.xG;
+    // (a multiple of 4: the counting kernel's 16-B loads of four spans)
+    const uint64_t per_wg = ((E.n + E.xG - 1) / E.xG + 3) / 4 * 4;
     if (per_wg > kXcMaxSpans) return hipErrorInvalidValue;  // (the engine splits batches below this)
     const uint32_t grid = (uint32_t)((E.n + per_wg - 1) / per_wg);
     hipLaunchKernelGGL(expo_count_slab_kernel, dim3(grid), dim3(kXcBlock),
