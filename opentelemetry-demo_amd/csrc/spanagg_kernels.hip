@@ -1012,22 +1012,32 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     // A chunk's first span relative to lo (t_of; lim: no work): the
     // workgroup's own range, then (POOL) chunks of stolen pool blocks, 8 per
     // block.  The wave whose claim is a block's first chunk takes the block
-    // from the pool counter during its round and publishes it in pmap at the
-    // round's end; the block's other chunks wait for that (claims are in
-    // order, so the earliest unpublished block's wave never waits itself).
-    // Every claim past a done block is done too.
+    // from the pool counter right after its claim and publishes it in pmap;
+    // the block's other chunks wait for that.  A block is taken only after
+    // the workgroup's previous block is published (and not at all after a
+    // done one), so the blocks a workgroup takes increase with k: every claim
+    // past a done chunk is done too, which is what lets a wave leave the loop
+    // at its first done chunk with a claim in hand.  (Taken as soon as each
+    // claim returned, two waves' counter adds could complete out of order and
+    // a valid block could follow a done one: round-5 r5d lost 1,024 spans of
+    // a 40 M-span ingest that way.)  Claims are in order, so the earliest
+    // unpublished block's wave never waits on a later one.
+    auto published = [&](uint32_t k) -> uint32_t {
+      // (the host gives a pooled launch >= 32 own chunks per workgroup, so
+      // every block's first chunk is a claim whose wave publishes it; the
+      // bound only keeps a broken invariant from hanging the device)
+      uint32_t v, spin = 0;
+      while ((v = (uint32_t)__builtin_amdgcn_readfirstlane((int)__atomic_load_n(&pmap[k], __ATOMIC_RELAXED))) == 0 &&
+             ++spin < (1u << 22))
+        __builtin_amdgcn_s_sleep(2);
+      return v;
+    };
     auto t_of = [&](uint32_t c) -> uint32_t {
       if (c < n_chunks) return c * chunk;
       if constexpr (POOL) {
         const uint32_t s = c - n_chunks, k = s >> 3, j = s & 7u;
         if (!pool_on || k >= kPoolMaxSteal) return lim;
-        // (the host gives a pooled launch >= 32 own chunks per workgroup, so
-        // every block's first chunk is a claim whose wave publishes it; the
-        // bound only keeps a broken invariant from hanging the device)
-        uint32_t v, spin = 0;
-        while ((v = (uint32_t)__builtin_amdgcn_readfirstlane((int)__atomic_load_n(&pmap[k], __ATOMIC_RELAXED))) == 0 &&
-               ++spin < (1u << 22))
-          __builtin_amdgcn_s_sleep(2);
+        const uint32_t v = published(k);
         if (v == 0 || v == kPoolDone) return lim;
         const uint64_t t = cold_params().pool_base - lo + (uint64_t)(v - 1) * kPoolSpans + j * chunk;
         return t < lim ? (uint32_t)t : lim;
@@ -1051,10 +1061,15 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
       while (t0 < lim) {
         const uint32_t c2 = wave_claim(&hq_n[1]);
         if (pool_on && c2 >= n_chunks && ((c2 - n_chunks) & 7u) == 0 && ((c2 - n_chunks) >> 3) < kPoolMaxSteal) {
-          const uint32_t sid = (uint32_t)__builtin_amdgcn_readfirstlane((int)atomicAdd(cold_params().pool_ctr, 1u)) >> 6;
-          if ((threadIdx.x & 63u) == 0)
-            __atomic_store_n(&pmap[(c2 - n_chunks) >> 3], sid < cold_params().pool_n ? sid + 1 : kPoolDone,
-                             __ATOMIC_RELAXED);
+          const uint32_t k = (c2 - n_chunks) >> 3;
+          const uint32_t prev = k ? published(k - 1) : 1u;
+          uint32_t v = kPoolDone;
+          if (prev != 0 && prev != kPoolDone) {
+            const uint32_t sid =
+                (uint32_t)__builtin_amdgcn_readfirstlane((int)atomicAdd(cold_params().pool_ctr, 1u)) >> 6;
+            if (sid < cold_params().pool_n) v = sid + 1;
+          }
+          if ((threadIdx.x & 63u) == 0) __atomic_store_n(&pmap[k], v, __ATOMIC_RELAXED);
         }
         const uint32_t t1 = t_of(c1);
 #pragma unroll
