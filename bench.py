@@ -531,7 +531,7 @@ def roofline(name, n, r, traffic_path=None):
     piped = BYTES_PER_SPAN * n / (r["device_ms"] * 1e-3) / 1e9
     kern = {"c2": "ingest_v2_kernel (spanagg_kernels.hip)",
             "c2expo": "ingest_v2_kernel EXPO mode + expo_reduce_rescale_kernel + expo_count_slab_kernel + "
-                      "expo_fold_slab_kernel (spanagg_kernels.hip, spanagg_expo.hip)",
+                      "expo_fold_kernel (spanagg_kernels.hip, spanagg_expo.hip)",
             "c4": "bt_scatter2_kernel + bt_aggregate3_kernel (spanagg_binned.hip)",
             "c4zipf": "bt_scatter2_kernel + bt_aggregate3_kernel (spanagg_binned.hip)"}[name]
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -107,6 +107,9 @@ struct IngestParams {
   // slot of every span (for the bucket-counting pass) and the per-workgroup
   // header slabs [G][cap] (XHdr) the rescale pass reduces
   uint32_t *slot_of;  // EXPO mode: [n] key slot of each span (kNotFound without one)
+  // EXPO mode with slab counting: [n] span records instead (span_rec_of), so
+  // the counting pass reads 8 B per span instead of the slot and both times
+  unsigned long long *span_rec;
   XHdr *xslab;
   // Small-table kernels with the tail pool (POOL): every workgroup owns the
   // static range [b * wg_chunk, (b + 1) * wg_chunk); spans [pool_base, n)
@@ -161,6 +164,7 @@ struct ExpoParams {
   uint32_t diag;      // ablation bits (SPANAGG_XC_DIAG, profiling only; results wrong when set):
                       // 1 no HBM bucket atomics, 2 no LDS cache, 4 exact index path only, 8 no index
   uint32_t *slot_of;  // [n] key slot of each span (pass 1 / the small-table ingest kernel -> counting)
+  const unsigned long long *span_rec;  // [n] span records (slab counting: the small-table kernel -> counting)
   unsigned long long *dropped;
   XHdr *xslab;        // small-table engines: [xG][cap] per-workgroup header partials (nullptr: pass 1 atomics)
   uint32_t xG;
@@ -172,9 +176,20 @@ struct ExpoParams {
   // the counting kernel's tail (spans of series without an LDS entry): each
   // workgroup's (slot << 12 | bucket) records, sorted by fold bin of
   // kXtBinSlots slots, [xG][kXtCap], and the bins' offsets [xG][nbins + 1];
-  // expo_fold_tail_kernel sums them per bin (nullptr: HBM atomics)
+  // expo_fold_kernel sums them per bin (nullptr: HBM atomics)
   uint32_t *xt_rec, *xt_off;  // (records past kXtCap take an HBM atomic)
 };
+// A span record of the exponential-histogram slab path: the key slot in the
+// top 12 bits (kSpanRecNoSlot: none; slab tables have <= 2,048 slots) and the
+// duration in ns below; a duration of 2^52 - 1 ns (52 days) or more is stored
+// as kSpanRecDurMask and the counting pass reads that span's times instead.
+constexpr uint32_t kSpanRecShift = 52;
+constexpr uint32_t kSpanRecNoSlot = 0xFFFu;
+constexpr unsigned long long kSpanRecDurMask = (1ull << kSpanRecShift) - 1;
+__host__ __device__ inline unsigned long long span_rec_of(uint32_t slot, unsigned long long d) {
+  return (unsigned long long)(slot < kSpanRecNoSlot ? slot : kSpanRecNoSlot) << kSpanRecShift |
+         (d < kSpanRecDurMask ? d : kSpanRecDurMask);
+}
 constexpr uint32_t kXtCap = 4096;       // tail records per counting workgroup (16 KiB of LDS)
 constexpr uint32_t kXtBinSlots = 8;     // slots per tail fold bin
 __host__ __device__ inline uint32_t xt_bins(uint64_t cap) { return (uint32_t)((cap + kXtBinSlots - 1) / kXtBinSlots); }

@@ -790,6 +790,7 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
     E.diag = diag;
   }
   E.slot_of = e->expo_slot;
+  E.span_rec = e->expo_small && e->xc_ne ? reinterpret_cast<const unsigned long long *>(e->expo_slot) : nullptr;
   E.dropped = e->stats + sa::kStatDropped;
   E.xslab = e->expo_small ? e->xslab : nullptr;
   E.xG = e->G;
@@ -959,12 +960,14 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
       if (e->expo_slot) (void)hipFree(e->expo_slot);
       e->expo_slot = nullptr;
       e->expo_slot_cap = 0;
-      if (hipMalloc((void **)&e->expo_slot, b->n * 4) != hipSuccess) return fail(e, SA_ENOMEM, "expo slot buffer");
+      // (8 B per span: span records on the slab-counting path, else u32 slots)
+      if (hipMalloc((void **)&e->expo_slot, b->n * 8) != hipSuccess) return fail(e, SA_ENOMEM, "expo slot buffer");
       e->expo_slot_cap = b->n;
     }
     if (e->expo_small) {
       // the small-table kernel in EXPO mode: sketches, key slots, header partials
-      P.slot_of = e->expo_slot;
+      if (e->xc_ne) P.span_rec = reinterpret_cast<unsigned long long *>(e->expo_slot);
+      else P.slot_of = e->expo_slot;
       P.xslab = e->xslab;
       st = sa::launch_ingest_expo_small(P, grid, e->lds_bytes, s);
     } else {

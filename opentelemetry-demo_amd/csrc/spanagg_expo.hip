@@ -294,10 +294,15 @@ constexpr uint64_t kXcMaxSpans = 65535;  // u16 LDS counts: spans per counting w
 //                          bucket index at the series' scale; an entry's spans
 //                          add to LDS u16 counts, which leave as plain
 //                          coalesced stores into the workgroup's slab; other
-//                          spans add to the HBM buckets with an atomic
-//   expo_fold_slab_kernel  per (entry, bucket pair): the sum over the
-//                          workgroups' slabs, added to the series' buckets
-//                          (one owner, no atomics)
+//                          spans leave as (slot, bucket) tail records sorted
+//                          by fold bin.  The spans come as the 8-B records
+//                          the ingest kernel wrote (slot | duration,
+//                          span_rec_of), not as slot + both times (20 B)
+//   expo_fold_kernel       per (entry, bucket pair): the sum over the
+//                          workgroups' slabs, added to the series' buckets;
+//                          and per tail bin: every workgroup's records of the
+//                          bin counted in LDS, then added to the buckets
+//                          (one owner each, no atomics; one launch)
 // A launch's C2 mix (10 M spans, ~1.4 k series, Zipf) put ~6 M atomics on
 // HBM with per-workgroup caches flushed by atomics: ~200 us of the ~310 us
 // the counting took.  The selection was a one-block kernel of its own, 6 us
@@ -410,9 +415,7 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
   __syncthreads();
   const uint64_t lo = blockIdx.x * per_wg, hi = lo + per_wg < E.n ? lo + per_wg : E.n;
   const uint32_t len = hi > lo ? (uint32_t)(hi - lo) : 0u;
-  auto count = [&](uint32_t slot, uint64_t st, uint64_t en) {
-    if (slot == kNotFound) return;
-    const uint64_t d = en > st ? en - st : 0;
+  auto count = [&](uint32_t slot, uint64_t d) {
     if (d == 0) return;
     const int2 m = meta[slot];
     int32_t ix;
@@ -429,47 +432,48 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
       else atomicAdd(E.buckets + ((uint64_t)m.y * E.cap + slot) * M + at, 1u);
     }
   };
-  if (!tail) {  // (the earlier form: one span per thread per round, A/B runs of SPANAGG_XT=0)
-    for (uint32_t i = threadIdx.x; i < len; i += kXcBlock) count(E.slot_of[lo + i], E.start[lo + i], E.end[lo + i]);
-  } else {
-    // four consecutive spans per thread through 16-B buffer loads (0 past the
-    // range), two rounds in flight: with the tail off HBM atomics the loop is
-    // bound by its loads, and one span per thread per round kept only ~20 KB
-    // per CU in flight
-    const __amdgpu_buffer_rsrc_t rsl = rsrc(E.slot_of + lo, len * 4), rst = rsrc(E.start + lo, len * 8),
-                                 ren = rsrc(E.end + lo, len * 8);
-    struct Quad {
-      uint32_t sl[4];
-      uint64_t s[4], e[4];
-    };
-    auto load = [&](uint32_t base, Quad &q) {
-      const int o = (int)(base + 4 * threadIdx.x);
-      const auto a = __builtin_amdgcn_raw_buffer_load_b128(rsl, o * 4, 0, 0);
-      q.sl[0] = a[0], q.sl[1] = a[1], q.sl[2] = a[2], q.sl[3] = a[3];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rst, o * 8 + 16 * h, 0, 0);
-        const auto y = __builtin_amdgcn_raw_buffer_load_b128(ren, o * 8 + 16 * h, 0, 0);
-        q.s[2 * h] = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
-        q.s[2 * h + 1] = (uint64_t)x[2] | ((uint64_t)x[3] << 32);
-        q.e[2 * h] = (uint64_t)y[0] | ((uint64_t)y[1] << 32);
-        q.e[2 * h + 1] = (uint64_t)y[2] | ((uint64_t)y[3] << 32);
-      }
-    };
-    auto run = [&](uint32_t base, const Quad &q) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (base + 4 * threadIdx.x + j < len) count(q.sl[j], q.s[j], q.e[j]);
-    };
-    constexpr uint32_t kStep = 4 * kXcBlock;
-    Quad qa, qb;
-    load(0, qa);
-    for (uint32_t base = 0; base < len; base += 2 * kStep) {
-      load(base + kStep, qb);
-      run(base, qa);
-      load(base + 2 * kStep, qa);
-      run(base + kStep, qb);
+  // one span record (span_rec_of; 0 past the range: no duration); a duration
+  // past the record's field is read from the span's times
+  auto count_rec = [&](unsigned long long r, uint64_t i) {
+    const uint32_t slot = (uint32_t)(r >> kSpanRecShift);
+    if (slot == kSpanRecNoSlot) return;
+    uint64_t d = r & kSpanRecDurMask;
+    if (d == kSpanRecDurMask) {
+      const uint64_t st = E.start[i], en = E.end[i];
+      d = en > st ? en - st : 0;
     }
+    count(slot, d);
+  };
+  // four consecutive records per thread through two 16-B buffer loads (0 past
+  // the range), two rounds in flight: with the tail off HBM atomics the loop
+  // is bound by its loads, and one span per thread per round kept only ~20 KB
+  // per CU in flight
+  const __amdgpu_buffer_rsrc_t rr = rsrc(E.span_rec + lo, len * 8);
+  struct Quad {
+    unsigned long long r[4];
+  };
+  auto load = [&](uint32_t base, Quad &q) {
+    const int o = (int)(base + 4 * threadIdx.x);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const auto x = __builtin_amdgcn_raw_buffer_load_b128(rr, o * 8 + 16 * h, 0, 0);
+      q.r[2 * h] = (unsigned long long)x[0] | ((unsigned long long)x[1] << 32);
+      q.r[2 * h + 1] = (unsigned long long)x[2] | ((unsigned long long)x[3] << 32);
+    }
+  };
+  auto run = [&](uint32_t base, const Quad &q) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (base + 4 * threadIdx.x + j < len) count_rec(q.r[j], lo + base + 4 * threadIdx.x + j);
+  };
+  constexpr uint32_t kStep = 4 * kXcBlock;
+  Quad qa, qb;
+  load(0, qa);
+  for (uint32_t base = 0; base < len; base += 2 * kStep) {
+    load(base + kStep, qb);
+    run(base, qa);
+    load(base + 2 * kStep, qa);
+    run(base + kStep, qb);
   }
   __syncthreads();
   uint32_t *slab = E.xcslab + (uint64_t)blockIdx.x * NE * wpe;
@@ -506,11 +510,9 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
 // ([kXtBinSlots][M] u32), then each non-zero cell added to its bucket -- one
 // owner per slot (a slot is an entry in every workgroup or in none, so the
 // slab fold never touches these slots), no atomics on HBM.
-__global__ __launch_bounds__(1024) void expo_fold_tail_kernel(ExpoParams E, uint32_t grid) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const uint32_t M = E.max_size, nb = xt_bins(E.cap), b = blockIdx.x;
-  uint32_t *acc = reinterpret_cast<uint32_t *>(smem);  // [kXtBinSlots][M]
-  __shared__ uint32_t cur[kXtBinSlots];
+__device__ __forceinline__ void expo_fold_tail(const ExpoParams &E, uint32_t grid, uint32_t b, uint32_t *acc,
+                                               uint32_t *cur) {
+  const uint32_t M = E.max_size, nb = xt_bins(E.cap);
   for (uint32_t i = threadIdx.x; i < kXtBinSlots * M; i += 1024) acc[i] = 0;
   if (threadIdx.x < kXtBinSlots) {
     const uint64_t sl = (uint64_t)b * kXtBinSlots + threadIdx.x;
@@ -549,11 +551,11 @@ __global__ __launch_bounds__(1024) void expo_fold_tail_kernel(ExpoParams E, uint
 }
 
 // (entry, word) x 16 workgroup groups per block of 1024 threads
-__global__ __launch_bounds__(1024) void expo_fold_slab_kernel(ExpoParams E, uint32_t grid) {
-  __shared__ uint32_t part[16][64][2];
+__device__ __forceinline__ void expo_fold_slab(const ExpoParams &E, uint32_t grid, uint32_t blk,
+                                               uint32_t (*part)[64][2]) {
   const uint32_t M = E.max_size, wpe = (M + 1) / 2, total = E.xc_ne * wpe;
   const uint32_t wl = threadIdx.x & 63u, gq = threadIdx.x >> 6;
-  const uint32_t w = blockIdx.x * 64u + wl;
+  const uint32_t w = blk * 64u + wl;
   uint32_t lo = 0, hi = 0;
   if (w < total) {
 #pragma unroll 8
@@ -576,6 +578,17 @@ __global__ __launch_bounds__(1024) void expo_fold_slab_kernel(ExpoParams E, uint
   uint32_t *b = E.buckets + ((uint64_t)E.hdr[slot].cur * E.cap + slot) * M;
   if (lo) b[2 * q] += lo;
   if (hi && 2 * q + 1 < M) b[2 * q + 1] += hi;
+}
+
+// One launch for both folds of a counting pass: blocks [0, slab_blocks) fold
+// the entries' slabs, the rest one tail bin each (the two touch disjoint
+// slots: a slot is an entry in every workgroup or in none)
+__global__ __launch_bounds__(1024) void expo_fold_kernel(ExpoParams E, uint32_t grid, uint32_t slab_blocks) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ uint32_t part[16][64][2];
+  __shared__ uint32_t cur[kXtBinSlots];
+  if (blockIdx.x < slab_blocks) expo_fold_slab(E, grid, blockIdx.x, part);
+  else expo_fold_tail(E, grid, blockIdx.x - slab_blocks, reinterpret_cast<uint32_t *>(smem), cur);
 }
 
 // Bucket counting with per-workgroup LDS privatisation: the slots' (scale,
@@ -720,7 +733,7 @@ hipError_t prepare_expo_slab(size_t lds_bytes) {
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
       e != hipSuccess)
     return e;
-  return hipFuncSetAttribute((const void *)&expo_fold_tail_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+  return hipFuncSetAttribute((const void *)&expo_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)(kXtBinSlots * kExpoMaxSize * 4));
 }
 
@@ -755,7 +768,8 @@ void launch_reduce_rescale(const ExpoParams &E, hipStream_t s) {
 hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s) {
   if (E.n == 0) return hipSuccess;
   if (E.xslab && E.xc_ne) {  // small table, slab counting (E.xG workgroups, <= kXcMaxSpans spans each)
-    if (E.cap > 2048) return hipErrorInvalidValue;  // the selection's two slots per thread
+    // (the selection's two slots per thread; the span records' 12-bit slots)
+    if (E.cap > 2048 || !E.span_rec) return hipErrorInvalidValue;
     launch_reduce_rescale(E, s);
     // (a multiple of 4: the counting kernel's 16-B loads of four spans)
     const uint64_t per_wg = ((E.n + E.xG - 1) / E.xG + 3) / 4 * 4;
@@ -763,11 +777,10 @@ hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s) {
     const uint32_t grid = (uint32_t)((E.n + per_wg - 1) / per_wg);
     hipLaunchKernelGGL(expo_count_slab_kernel, dim3(grid), dim3(kXcBlock),
                        expo_slab_lds_bytes(E.cap, E.max_size, E.xc_ne), s, E, per_wg);
-    const uint32_t words = E.xc_ne * ((E.max_size + 1) / 2);
-    hipLaunchKernelGGL(expo_fold_slab_kernel, dim3((words + 63) / 64), dim3(1024), 0, s, E, grid);
-    if (E.xt_rec)
-      hipLaunchKernelGGL(expo_fold_tail_kernel, dim3(xt_bins(E.cap)), dim3(1024), kXtBinSlots * E.max_size * 4, s, E,
-                         grid);
+    const uint32_t words = E.xc_ne * ((E.max_size + 1) / 2), slab_blocks = (words + 63) / 64;
+    const uint32_t tail_blocks = E.xt_rec ? xt_bins(E.cap) : 0u;
+    hipLaunchKernelGGL(expo_fold_kernel, dim3(slab_blocks + tail_blocks), dim3(1024),
+                       tail_blocks ? kXtBinSlots * E.max_size * 4 : 0, s, E, grid, slab_blocks);
     return hipGetLastError();
   }
   if (E.xslab) {  // small table: the ingest kernel left header partials and slots

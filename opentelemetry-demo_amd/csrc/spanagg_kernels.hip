@@ -937,7 +937,10 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
             atomicMax(&xmax[f], d);
           }
         }
-        if (lane_off + toff + (uint32_t)j < lim) P.slot_of[lo + toff + lane_off + j] = f;
+        if (lane_off + toff + (uint32_t)j < lim) {
+          if (P.span_rec) P.span_rec[lo + toff + lane_off + j] = span_rec_of(f, dur[j]);
+          else P.slot_of[lo + toff + lane_off + j] = f;
+        }
       }
     } else if constexpr (LEAN) {
       const uint32_t lane = threadIdx.x & 63u;

@@ -188,6 +188,26 @@ def test_expo_huge_durations(path):
             _check(e.flush_exp(), batch, max_size)
 
 
+@pytest.mark.parametrize("max_size", [160, 8])
+def test_expo_huge_durations_in_a_mix(max_size):
+    """The slab path's span records hold a duration below 2^52 - 1 ns and
+    send longer ones back to the span's times (span_rec_of, sa_internal.h):
+    every 97th span of a C2 mix (~1.4 k series, so both the LDS entries and
+    the tail records see them) gets a duration of 2^52 - 1 + k ns, k = 0 .. 4,
+    and a few get exactly 2^52 - 2."""
+    wl = generate_c2(200_003, seed=29)
+    b = wl.batch
+    start = b.start_ns.copy()
+    idx = np.arange(0, len(b), 97)
+    start[idx] = b.end_ns[idx] - (np.uint64(2**52 - 1) + (idx % 5).astype(np.uint64))
+    start[idx[::7] + 1] = b.end_ns[idx[::7] + 1] - np.uint64(2**52 - 2)
+    batch = SpanBatch(b.key_hash, start, b.end_ns, b.trace_w0, b.trace_w1, b.meta)
+    with _engine(wl, exp_max_size=max_size) as e:
+        assert e.stats()["small_table"] == 1
+        e.ingest(batch)
+        _check(e.flush_exp(), batch, max_size)
+
+
 def test_expo_sketches_unchanged():
     wl = generate_c2(150_000, seed=23)
     with _engine(wl, exp_max_size=160) as e:
