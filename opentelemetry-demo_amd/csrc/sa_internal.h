@@ -160,7 +160,7 @@ struct ExpoParams {
   uint32_t *buckets;  // [2][cap][max_size]
   uint32_t max_size;
   double div;         // 1e6 (ms) or 1e9 (s)
-  double log2div;     // log2(div), for the bucket index's fast path
+  long long log2div_fx;  // log2(div) * 2^32 rounded, for the bucket index's fast path
   uint32_t diag;      // ablation bits (SPANAGG_XC_DIAG, profiling only; results wrong when set):
                       // 1 no HBM bucket atomics, 2 no LDS cache, 4 exact index path only, 8 no index
   uint32_t *slot_of;  // [n] key slot of each span (pass 1 / the small-table ingest kernel -> counting)

@@ -37,6 +37,10 @@ constexpr uint64_t kSlabLimit = 1ULL << 31;  // per-workgroup spans between slab
 constexpr int kDefaultVariant = 20;
 constexpr uint32_t kMaxSlabSets = 4;      // per-workgroup slab sets (small path)
 constexpr uint32_t kDefaultSlabSets = 2;  // SPANAGG_SLAB_SETS overrides (laboratory build)
+// exponential slab path: 8-B span records for the counting pass (expo_span_recs;
+// off: the slot + both times were faster, the ingest kernel's wider stores
+// costing more than the counting pass saves -- DESIGN.md section 4)
+constexpr bool kExpoSpanRecs = false;
 
 // Laboratory knobs: the SPANAGG_AB build (`make ab` -> libspanagg_ab.so, used
 // by tools/ for A/B runs and ablations) reads them from the environment; the
@@ -765,6 +769,19 @@ static int bt_aggregate_pending(sa_engine *e) {
   return rc;
 }
 
+
+// The exponential slab path hands the counting pass 8-B span records (slot |
+// duration) instead of the slot alone (laboratory build: SPANAGG_XREC=0 / 1
+// picks, for A/B runs)
+static bool expo_span_recs(const sa_engine *e) {
+  static const int knob = [] {
+    const char *v = ab_env("SPANAGG_XREC");
+    return v ? std::atoi(v) : -1;
+  }();
+  const bool on = knob < 0 ? kExpoSpanRecs : knob != 0;
+  return on && e->expo_small && e->xc_ne;
+}
+
 static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
   sa::ExpoParams E{};
   if (b) {
@@ -781,7 +798,7 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
   E.buckets = e->expo_buckets;
   E.max_size = e->cfg.exp_max_size;
   E.div = e->cfg.unit == SA_UNIT_S ? 1e9 : 1e6;
-  E.log2div = std::log2(E.div);
+  E.log2div_fx = std::llround(std::log2(E.div) * 4294967296.0);
   {
     static const uint32_t diag = [] {
       const char *v = ab_env("SPANAGG_XC_DIAG");
@@ -790,7 +807,7 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
     E.diag = diag;
   }
   E.slot_of = e->expo_slot;
-  E.span_rec = e->expo_small && e->xc_ne ? reinterpret_cast<const unsigned long long *>(e->expo_slot) : nullptr;
+  E.span_rec = expo_span_recs(e) ? reinterpret_cast<const unsigned long long *>(e->expo_slot) : nullptr;
   E.dropped = e->stats + sa::kStatDropped;
   E.xslab = e->expo_small ? e->xslab : nullptr;
   E.xG = e->G;
@@ -966,7 +983,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
     }
     if (e->expo_small) {
       // the small-table kernel in EXPO mode: sketches, key slots, header partials
-      if (e->xc_ne) P.span_rec = reinterpret_cast<unsigned long long *>(e->expo_slot);
+      if (expo_span_recs(e)) P.span_rec = reinterpret_cast<unsigned long long *>(e->expo_slot);
       else P.slot_of = e->expo_slot;
       P.xslab = e->xslab;
       st = sa::launch_ingest_expo_small(P, grid, e->lds_bytes, s);

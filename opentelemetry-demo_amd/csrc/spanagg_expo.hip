@@ -87,24 +87,33 @@ __device__ __forceinline__ double expo_value(uint64_t d_ns, double div) {
 // exact value at any scale <= 20); otherwise -- including every power of two
 // and every value near a bucket boundary -- false, and the caller takes the
 // exact path.
+// Integer arithmetic: z = log2(d / div) in 32.32 fixed point (l2d_fx =
+// log2(div) * 2^32 rounded, the hardware log2 of the mantissa converted with
+// its 32 fraction bits), so the scaled value's integer part is z's bits above
+// 32 - scale and its distance to an integer is read from the bits below (no
+// f64 ops: the counting kernel issues ~half the VALU work of the f64 form).
+// kFastFxErr: kFastLog2Err in those units plus the two conversions' 2^-32.
 constexpr double kFastLog2Err = 1.0 / (1 << 20) + 1.0 / (1 << 22);
-__device__ __forceinline__ bool expo_index_fast(uint64_t d, double log2div, int32_t scale, int32_t &idx) {
+constexpr uint64_t kFastFxErr = (uint64_t)(kFastLog2Err * 4294967296.0) + 4;
+__device__ __forceinline__ bool expo_index_fast(uint64_t d, long long l2d_fx, int32_t scale, int32_t &idx) {
   const int32_t e = 63 - (int32_t)__clzll((long long)d);
   const uint32_t top = (uint32_t)((d << (63 - e)) >> 40);  // 24 bits, the leading one at bit 23
   const float m = (float)top * 0x1p-23f;                    // exact, in [1, 2)
-  const double z = (double)e - log2div + (double)__builtin_amdgcn_logf(m);  // ~ log2(d / div)
-  const double fz = floor(z);
-  if (z - fz <= kFastLog2Err || fz + 1.0 - z <= kFastLog2Err) return false;  // near a power of two
+  const uint32_t t = (uint32_t)(__builtin_amdgcn_logf(m) * 0x1p32f);  // log2(m) < 1, 32 fraction bits
+  const long long z = ((long long)e << 32) - l2d_fx + (long long)t;   // ~ log2(d / div) * 2^32
+  const int32_t sh = scale > 0 ? 32 - scale : 32;
+  const uint64_t one = 1ull << sh, f = (uint64_t)z & (one - 1);
+  if (f <= kFastFxErr || one - f <= kFastFxErr) return false;  // near a bucket boundary / power of two
+  const int32_t fl = (int32_t)(z >> sh);                        // floor of the scaled value
   if (scale <= 0) {
-    idx = (int32_t)fz >> (-scale);  // Go: exponent >> -scale (z is not an integer)
+    idx = fl >> (-scale);  // Go: exponent >> -scale (z is not an integer)
     return true;
   }
-  const double y = ldexp(z, scale), fy = floor(y), err = ldexp(kFastLog2Err, scale);
-  if (y - fy <= err || fy + 1.0 - y <= err) return false;
-  const double max_index = (double)((1024 << scale) - 1);
-  idx = fy >= max_index ? (int32_t)max_index : (int32_t)fy;
+  const int32_t max_index = (1024 << scale) - 1;
+  idx = fl >= max_index ? max_index : fl;
   return true;
 }
+__host__ inline long long expo_l2d_fx(double div) { return std::llround(std::log2(div) * 4294967296.0); }
 
 constexpr int32_t kExpoMaxScale = 20, kExpoMinScale = -10;
 constexpr int32_t kExpoEmpty = 0x7FFFFFFF;  // ExpoHdr.lo when no positive value is kept
@@ -390,6 +399,9 @@ __device__ __forceinline__ void expo_select_lds(const ExpoParams &E, int32_t *en
   }
 }
 
+// REC: the spans as the ingest kernel's 8-B records (E.span_rec); else as
+// the key slot (E.slot_of) and both times (20 B per span)
+template <bool REC>
 __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uint64_t per_wg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t M = E.max_size, NE = E.xc_ne, cap = (uint32_t)E.cap, wpe = (M + 1) / 2;
@@ -406,9 +418,13 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
   uint32_t lc[2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) lc[k] = 2 * threadIdx.x + k < cap ? E.lcount[2 * threadIdx.x + k] : 0u;
+  // meta: {scale (8 bits) | buffer << 8 | (lo mod M) << 9, lo}: this launch's
+  // positive values lie in the kept range [lo, lo + M), so a bucket position
+  // is lo's plus ix - lo, wrapped once
   for (uint32_t i = threadIdx.x; i < cap; i += kXcBlock) {
     const ExpoHdr &h = E.hdr[i];
-    meta[i] = make_int2(h.scale, (int)h.cur);
+    const int32_t lo = h.lo == kExpoEmpty ? 0 : h.lo;
+    meta[i] = make_int2((h.scale & 0xFF) | (int)(h.cur << 8) | (int)(expo_mod(lo, M) << 9), lo);
   }
   for (uint32_t i = threadIdx.x; i < NE * wpe; i += kXcBlock) cnt[i] = 0;
   expo_select_lds(E, ent, scratch, lc);
@@ -418,9 +434,11 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
   auto count = [&](uint32_t slot, uint64_t d) {
     if (d == 0) return;
     const int2 m = meta[slot];
+    const int32_t sc = (int32_t)(int8_t)(m.x & 0xFF);
     int32_t ix;
-    if (!expo_index_fast(d, E.log2div, m.x, ix)) ix = expo_index(expo_value(d, E.div), m.x);
-    const uint32_t at = expo_mod(ix, M);
+    if (!expo_index_fast(d, E.log2div_fx, sc, ix)) ix = expo_index(expo_value(d, E.div), sc);
+    const uint32_t rel = (uint32_t)(ix - m.y), a0 = ((uint32_t)m.x >> 9) + rel;
+    const uint32_t at = rel < M ? (a0 >= M ? a0 - M : a0) : expo_mod(ix, M);
     const int32_t en_ = ent[slot];
     if (en_ >= 0) {
       atomicAdd(&cnt[(uint32_t)en_ * wpe + (at >> 1)], 1u << ((at & 1u) * 16));
@@ -429,7 +447,7 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
       // scattered HBM atomic (past the record buffer: the atomic)
       const uint32_t r = tail ? atomicAdd(&tmisc[0], 1u) : kXtCap;
       if (r < kXtCap) trec[r] = slot << 12 | at;
-      else atomicAdd(E.buckets + ((uint64_t)m.y * E.cap + slot) * M + at, 1u);
+      else atomicAdd(E.buckets + ((uint64_t)(((uint32_t)m.x >> 8) & 1u) * E.cap + slot) * M + at, 1u);
     }
   };
   // one span record (span_rec_of; 0 past the range: no duration); a duration
@@ -444,27 +462,52 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
     }
     count(slot, d);
   };
-  // four consecutive records per thread through two 16-B buffer loads (0 past
-  // the range), two rounds in flight: with the tail off HBM atomics the loop
-  // is bound by its loads, and one span per thread per round kept only ~20 KB
+  // four consecutive spans per thread through 16-B buffer loads (0 past the
+  // range), two rounds in flight: with the tail off HBM atomics the loop is
+  // bound by its loads, and one span per thread per round kept only ~20 KB
   // per CU in flight
-  const __amdgpu_buffer_rsrc_t rr = rsrc(E.span_rec + lo, len * 8);
+  const __amdgpu_buffer_rsrc_t rr = rsrc(REC ? (const void *)(E.span_rec + lo) : (const void *)(E.slot_of + lo),
+                                         REC ? len * 8 : len * 4);
+  const __amdgpu_buffer_rsrc_t rst = rsrc(E.start + lo, REC ? 0u : len * 8), ren = rsrc(E.end + lo, REC ? 0u : len * 8);
   struct Quad {
-    unsigned long long r[4];
+    unsigned long long r[4];  // REC: the records; else the slots
+    uint64_t s[REC ? 1 : 4], e[REC ? 1 : 4];
   };
   auto load = [&](uint32_t base, Quad &q) {
     const int o = (int)(base + 4 * threadIdx.x);
+    if constexpr (REC) {
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const auto x = __builtin_amdgcn_raw_buffer_load_b128(rr, o * 8 + 16 * h, 0, 0);
-      q.r[2 * h] = (unsigned long long)x[0] | ((unsigned long long)x[1] << 32);
-      q.r[2 * h + 1] = (unsigned long long)x[2] | ((unsigned long long)x[3] << 32);
+      for (int h = 0; h < 2; ++h) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rr, o * 8 + 16 * h, 0, 0);
+        q.r[2 * h] = (unsigned long long)x[0] | ((unsigned long long)x[1] << 32);
+        q.r[2 * h + 1] = (unsigned long long)x[2] | ((unsigned long long)x[3] << 32);
+      }
+    } else {
+      const auto a = __builtin_amdgcn_raw_buffer_load_b128(rr, o * 4, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) q.r[j] = a[j];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rst, o * 8 + 16 * h, 0, 0);
+        const auto y = __builtin_amdgcn_raw_buffer_load_b128(ren, o * 8 + 16 * h, 0, 0);
+        q.s[2 * h] = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+        q.s[2 * h + 1] = (uint64_t)x[2] | ((uint64_t)x[3] << 32);
+        q.e[2 * h] = (uint64_t)y[0] | ((uint64_t)y[1] << 32);
+        q.e[2 * h + 1] = (uint64_t)y[2] | ((uint64_t)y[3] << 32);
+      }
     }
   };
   auto run = [&](uint32_t base, const Quad &q) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (base + 4 * threadIdx.x + j < len) count_rec(q.r[j], lo + base + 4 * threadIdx.x + j);
+    for (int j = 0; j < 4; ++j) {
+      if (base + 4 * threadIdx.x + j >= len) continue;
+      if constexpr (REC) {
+        count_rec(q.r[j], lo + base + 4 * threadIdx.x + j);
+      } else {
+        const uint32_t slot = (uint32_t)q.r[j];
+        if (slot != kNotFound) count(slot, q.e[j] > q.s[j] ? q.e[j] - q.s[j] : 0);
+      }
+    }
   };
   constexpr uint32_t kStep = 4 * kXcBlock;
   Quad qa, qb;
@@ -627,7 +670,7 @@ __global__ __launch_bounds__(kXcBlock) void expo_count_cached_kernel(ExpoParams 
     const int2 m = meta[slot];
     int32_t ix;
     if (E.diag & 8u) ix = (int32_t)(d & 127u);
-    else if ((E.diag & 4u) || !expo_index_fast(d, E.log2div, m.x, ix)) ix = expo_index(expo_value(d, E.div), m.x);
+    else if ((E.diag & 4u) || !expo_index_fast(d, E.log2div_fx, m.x, ix)) ix = expo_index(expo_value(d, E.div), m.x);
     const uint32_t at = expo_mod(ix, M);
     uint32_t e = (((slot * 0x9E3779B1u) >> 16) & (NE / 4 - 1)) * 4, hit = kNotFound;  // home group of 4
 #pragma unroll
@@ -729,7 +772,13 @@ size_t expo_slab_lds_bytes(uint64_t cap, uint32_t max_size, uint32_t ne) {
 }
 
 hipError_t prepare_expo_slab(size_t lds_bytes) {
-  if (hipError_t e = hipFuncSetAttribute((const void *)&expo_count_slab_kernel,
+#ifdef SPANAGG_AB
+  if (hipError_t e = hipFuncSetAttribute((const void *)&expo_count_slab_kernel<true>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+      e != hipSuccess)
+    return e;
+#endif
+  if (hipError_t e = hipFuncSetAttribute((const void *)&expo_count_slab_kernel<false>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
       e != hipSuccess)
     return e;
@@ -769,14 +818,20 @@ hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s) {
   if (E.n == 0) return hipSuccess;
   if (E.xslab && E.xc_ne) {  // small table, slab counting (E.xG workgroups, <= kXcMaxSpans spans each)
     // (the selection's two slots per thread; the span records' 12-bit slots)
-    if (E.cap > 2048 || !E.span_rec) return hipErrorInvalidValue;
+    if (E.cap > 2048) return hipErrorInvalidValue;
     launch_reduce_rescale(E, s);
     // (a multiple of 4: the counting kernel's 16-B loads of four spans)
     const uint64_t per_wg = ((E.n + E.xG - 1) / E.xG + 3) / 4 * 4;
     if (per_wg > kXcMaxSpans) return hipErrorInvalidValue;  // (the engine splits batches below this)
     const uint32_t grid = (uint32_t)((E.n + per_wg - 1) / per_wg);
-    hipLaunchKernelGGL(expo_count_slab_kernel, dim3(grid), dim3(kXcBlock),
-                       expo_slab_lds_bytes(E.cap, E.max_size, E.xc_ne), s, E, per_wg);
+#ifdef SPANAGG_AB  // (span records: laboratory build only, SPANAGG_XREC=1)
+    if (E.span_rec)
+      hipLaunchKernelGGL(expo_count_slab_kernel<true>, dim3(grid), dim3(kXcBlock),
+                         expo_slab_lds_bytes(E.cap, E.max_size, E.xc_ne), s, E, per_wg);
+    else
+#endif
+      hipLaunchKernelGGL(expo_count_slab_kernel<false>, dim3(grid), dim3(kXcBlock),
+                         expo_slab_lds_bytes(E.cap, E.max_size, E.xc_ne), s, E, per_wg);
     const uint32_t words = E.xc_ne * ((E.max_size + 1) / 2), slab_blocks = (words + 63) / 64;
     const uint32_t tail_blocks = E.xt_rec ? xt_bins(E.cap) : 0u;
     hipLaunchKernelGGL(expo_fold_kernel, dim3(slab_blocks + tail_blocks), dim3(1024),
@@ -841,18 +896,18 @@ __global__ __launch_bounds__(256) void log2_err_probe_kernel(uint32_t i0, uint32
 }
 
 __global__ __launch_bounds__(256) void expo_fast_probe_kernel(const uint64_t *d, const int32_t *scale, uint64_t n,
-                                                             double div, double log2div, int32_t *fast,
+                                                             double div, long long l2d_fx, int32_t *fast,
                                                              int32_t *exact) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
     int32_t ix;
-    fast[i] = expo_index_fast(d[i], log2div, scale[i], ix) ? ix : INT32_MIN;
+    fast[i] = expo_index_fast(d[i], l2d_fx, scale[i], ix) ? ix : INT32_MIN;
     exact[i] = expo_index(expo_value(d[i], div), scale[i]);
   }
 }
 
 hipError_t launch_expo_fast_probe(const uint64_t *d, const int32_t *scale, uint64_t n, double div, int32_t *fast,
                                   int32_t *exact, hipStream_t s) {
-  hipLaunchKernelGGL(expo_fast_probe_kernel, dim3(grid_of(n)), dim3(256), 0, s, d, scale, n, div, std::log2(div), fast,
+  hipLaunchKernelGGL(expo_fast_probe_kernel, dim3(grid_of(n)), dim3(256), 0, s, d, scale, n, div, expo_l2d_fx(div), fast,
                      exact);
   return hipGetLastError();
 }

@@ -937,9 +937,24 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
             atomicMax(&xmax[f], d);
           }
         }
-        if (lane_off + toff + (uint32_t)j < lim) {
-          if (P.span_rec) P.span_rec[lo + toff + lane_off + j] = span_rec_of(f, dur[j]);
-          else P.slot_of[lo + toff + lane_off + j] = f;
+        if (!P.span_rec && lane_off + toff + (uint32_t)j < lim) P.slot_of[lo + toff + lane_off + j] = f;
+      }
+      // the lane's span records: one 16-B store for its two spans (two 8-B
+      // stores per lane cost the kernel ~24 us per 10 M spans)
+      if (P.span_rec) {
+        const uint32_t i0 = toff + lane_off;
+        unsigned long long *rp = P.span_rec + lo + i0;
+        if constexpr (S == 2) {
+          if (i0 + 1 < lim) {
+            *reinterpret_cast<ulonglong2 *>(rp) =
+                make_ulonglong2(span_rec_of(found[0], dur[0]), span_rec_of(found[1], dur[1]));
+          } else if (i0 < lim) {
+            rp[0] = span_rec_of(found[0], dur[0]);
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < S; ++j)
+            if (i0 + (uint32_t)j < lim) rp[j] = span_rec_of(found[j], dur[j]);
         }
       }
     } else if constexpr (LEAN) {

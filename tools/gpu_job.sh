@@ -19,6 +19,8 @@
 #   hostprof_<t>     host_rate.js (GPU ingest, t threads) under node --cpu-prof
 #   colab            colbench against host/node/build/$COL_OTHER (3 rounds, 16 and 8 threads)
 #   colbench         the native columnizer alone (host/node/build/colbench) at 1-16 threads
+#   labexpo_<KNOB=v> the exponential-histogram suites on the laboratory build with KNOB=v
+#   xrec_<wl>        bench of <wl> with the expo slab path's span records on / off (3 rounds)
 #   evscope_<wl>     bench of <wl> with the engine's events at device / system scope (2 rounds)
 #   labtrace_<wl>_<VAR=v>  rocprofv3 trace of a 100-step bench of <wl> on the laboratory build with VAR=v
 #   btpipe_<wl>      bench of <wl> with the binned launch pipeline on and off (2 rounds)
@@ -110,6 +112,15 @@ for step in "$@"; do
       (export SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so; export "$knob"; \
        run "labbin_${knob//=/}" 600 python -u -m pytest tests/test_gpu_binned.py "tests/test_gpu_regime.py" -m gpu -x -v \
          --timeout 300 --timeout-method thread) || exit $? ;;
+    labexpo_*) knob=${step#labexpo_}  # the exponential-histogram suites on the laboratory build with one knob, e.g. labexpo_SPANAGG_XREC=0
+      (export SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so; export "$knob"; \
+       run "labexpo_${knob//=/}" 300 python -u -m pytest tests/test_gpu_expo.py tests/test_gpu_churn.py -m gpu -x -v \
+         --timeout 300 --timeout-method thread) || exit $? ;;
+    xrec_*) wl=${step#xrec_}  # exponential slab path: span records (1) / slots + times (0), laboratory build, rounds interleaved
+      for r in 1 2 3; do for x in 1 0; do
+        SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_XREC=$x \
+          run "xrec_${wl}_x${x}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $BQ
+      done; done ;;
     evscope_*) wl=${step#evscope_}  # engine events at device scope (default) / system scope (laboratory build)
       for r in 1 2; do for es in 0 1; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_EV_SYS=$es \
