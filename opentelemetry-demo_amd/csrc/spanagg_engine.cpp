@@ -128,7 +128,13 @@ struct sa_engine {
   uint32_t *xt_rec = nullptr, *xt_off = nullptr;  // the counting kernel's tail records (ExpoParams::xt_*)
   sa::ExpoHdr *expo_hdr = nullptr;
   uint32_t *expo_buckets = nullptr, *expo_slot = nullptr;
-  uint64_t expo_slot_cap = 0;
+  uint64_t expo_slot_cap = 0;  // spans per set of expo_slot ([nsets][cap], 8 B each)
+  // Small-table exponential engines run launch k + 1's ingest kernel beside
+  // launch k's reduce / count / fold (two slab sets of header partials and
+  // span slots); launch k + 1's reduce waits for ev_expo, launch k's fold
+  // (the headers and buckets have one owner at a time)
+  hipEvent_t ev_expo = nullptr;
+  hipStream_t expo_last = nullptr;
   unsigned long long *expo_out_keys = nullptr;
   sa::ExpoRow *expo_out_rows = nullptr;
   uint32_t *expo_out_buckets = nullptr;
@@ -507,7 +513,12 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     if (sa::launch_expo_init(e->expo_hdr, e->cap, nullptr) != hipSuccess)
       return bail(fail(e, SA_EDEVICE, "expo state init failed"));
     if (e->expo_small) {
-      if ((rc = alloc((void **)&e->xslab, (size_t)e->G * e->cap * sizeof(sa::XHdr)))) return bail(rc);
+      e->nsets = kDefaultSlabSets;
+      if (const char *v = ab_env("SPANAGG_SLAB_SETS"))
+        e->nsets = (uint32_t)std::max(1, std::min((int)kMaxSlabSets, std::atoi(v)));
+      if ((rc = alloc((void **)&e->xslab, (size_t)e->nsets * e->G * e->cap * sizeof(sa::XHdr)))) return bail(rc);
+      if (hipEventCreateWithFlags(&e->ev_expo, ev_flags()) != hipSuccess)
+        return bail(fail(e, SA_EDEVICE, "event creation failed"));
       if (e->xc_ne &&
           ((rc = alloc((void **)&e->xc_lcount, e->cap * 4)) ||
            (rc = alloc((void **)&e->xc_slot_of_entry, (size_t)e->xc_ne * 4)) ||
@@ -517,7 +528,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
         return bail(rc);
       // (window, slot) keys of the LDS ERROR table are 16-bit
       if ((uint64_t)cfg->n_windows * e->cap < 65535 &&
-          (rc = alloc((void **)&e->errslab, (size_t)e->G * cfg->n_windows * e->cap * 4)))
+          (rc = alloc((void **)&e->errslab, (size_t)e->nsets * e->G * cfg->n_windows * e->cap * 4)))
         return bail(rc);
     }
   }
@@ -617,6 +628,7 @@ void sa_destroy(sa_engine *e) {
   for (hipEvent_t ev : e->ev_set)
     if (ev) (void)hipEventDestroy(ev);
   if (e->ev_ctl) (void)hipEventDestroy(e->ev_ctl);
+  if (e->ev_expo) (void)hipEventDestroy(e->ev_expo);
   for (int k = 0; k < sa_engine::kBtSets; ++k) {
     if (e->ev_scat[k]) (void)hipEventDestroy(e->ev_scat[k]);
     if (e->ev_agg[k]) (void)hipEventDestroy(e->ev_agg[k]);
@@ -782,7 +794,7 @@ static bool expo_span_recs(const sa_engine *e) {
   return on && e->expo_small && e->xc_ne;
 }
 
-static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
+static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b, uint32_t set = 0) {
   sa::ExpoParams E{};
   if (b) {
     E.key = b->key_hash;
@@ -806,10 +818,11 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b) {
     }();
     E.diag = diag;
   }
-  E.slot_of = e->expo_slot;
-  E.span_rec = expo_span_recs(e) ? reinterpret_cast<const unsigned long long *>(e->expo_slot) : nullptr;
+  // (this launch's set of span slots / records and header partials)
+  E.slot_of = e->expo_slot ? e->expo_slot + 2 * (size_t)set * e->expo_slot_cap : nullptr;
+  E.span_rec = expo_span_recs(e) ? reinterpret_cast<const unsigned long long *>(E.slot_of) : nullptr;
   E.dropped = e->stats + sa::kStatDropped;
-  E.xslab = e->expo_small ? e->xslab : nullptr;
+  E.xslab = e->expo_small ? e->xslab + (size_t)set * e->G * e->cap : nullptr;
   E.xG = e->G;
   E.xc_ne = e->expo_small ? e->xc_ne : 0u;
   E.lcount = E.xc_ne ? e->xc_lcount : nullptr;
@@ -977,16 +990,21 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
       if (e->expo_slot) (void)hipFree(e->expo_slot);
       e->expo_slot = nullptr;
       e->expo_slot_cap = 0;
-      // (8 B per span: span records on the slab-counting path, else u32 slots)
-      if (hipMalloc((void **)&e->expo_slot, b->n * 8) != hipSuccess) return fail(e, SA_ENOMEM, "expo slot buffer");
+      // (8 B per span and set: span records on the slab-counting path, else u32 slots)
+      if (hipMalloc((void **)&e->expo_slot, (size_t)e->nsets * b->n * 8) != hipSuccess)
+        return fail(e, SA_ENOMEM, "expo slot buffer");
       e->expo_slot_cap = b->n;
     }
+    uint32_t *slots = e->expo_slot + 2 * (size_t)set * e->expo_slot_cap;
     if (e->expo_small) {
       // the small-table kernel in EXPO mode: sketches, key slots, header partials
-      if (expo_span_recs(e)) P.span_rec = reinterpret_cast<unsigned long long *>(e->expo_slot);
-      else P.slot_of = e->expo_slot;
-      P.xslab = e->xslab;
+      if (expo_span_recs(e)) P.span_rec = reinterpret_cast<unsigned long long *>(slots);
+      else P.slot_of = slots;
+      P.xslab = e->xslab + (size_t)set * e->G * e->cap;
       st = sa::launch_ingest_expo_small(P, grid, e->lds_bytes, s);
+      // the histogram kernels after the previous launch's (one owner of the
+      // headers and buckets at a time); this ingest kernel may run beside them
+      if (st == hipSuccess && e->expo_last && e->expo_last != s) st = hipStreamWaitEvent(s, e->ev_expo, 0);
     } else {
       // sketches (and the zero-key / service / window counters) through the
       // HBM-table kernel with its RED part off
@@ -994,7 +1012,11 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
       st = sa::launch_ingest_hbm(P, grid, s, e->variant);
     }
     // then the histogram kernels
-    if (st == hipSuccess) st = sa::launch_expo_ingest(expo_params(e, b), s);
+    if (st == hipSuccess) st = sa::launch_expo_ingest(expo_params(e, b, set), s);
+    if (st == hipSuccess && e->ev_expo) {
+      st = hipEventRecord(e->ev_expo, s);
+      e->expo_last = s;
+    }
   } else {
     st = sa::launch_ingest_hbm(P, grid, s, e->variant);
   }

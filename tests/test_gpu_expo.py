@@ -208,6 +208,43 @@ def test_expo_huge_durations_in_a_mix(max_size):
         _check(e.flush_exp(), batch, max_size)
 
 
+def test_expo_launches_over_two_streams_pipelined():
+    """Small-table exponential engines run launch k + 1's ingest kernel beside
+    launch k's reduce / count / fold (two sets of header partials and span
+    slots; launch k + 1's reduce waits for launch k's fold).  Six
+    device-resident launches alternate over two streams; launches 3 and 5
+    stretch their durations (x 40, x 0.02) so the scales move under the
+    pipeline; a delta flush after the fourth launch."""
+    import torch
+    dev = torch.device("cuda", 0)
+    wl = generate_c2(600_000, seed=37)
+    parts = []
+    for i in range(6):
+        b = wl.batch.slice(i * 100_000, (i + 1) * 100_000)
+        f = {2: 40.0, 4: 0.02}.get(i)
+        start = b.start_ns.copy()
+        if f is not None:  # (spans with end > start; the others keep their zero duration)
+            pos = b.end_ns > b.start_ns
+            d = ((b.end_ns[pos] - b.start_ns[pos]).astype(np.float64) * f).astype(np.uint64)
+            start[pos] = b.end_ns[pos] - d
+        parts.append(SpanBatch(b.key_hash, start, b.end_ns, b.trace_w0, b.trace_w1, b.meta))
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    for st in streams:
+        st.wait_stream(torch.cuda.current_stream(dev))
+    dcols = [[torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(dev)
+              for c in p.columns()] for p in parts]
+    torch.cuda.synchronize(dev)
+    with _engine(wl, exp_max_size=160) as e:
+        assert e.stats()["small_table"] == 1
+        for i, cols in enumerate(dcols):
+            e.ingest_device(*cols, stream=streams[i % 2].cuda_stream)
+            if i == 3:
+                first = SpanBatch(*[np.concatenate(c) for c in zip(*[q.columns() for q in parts[:4]])])
+                _check(e.flush_exp(), first, 160)
+        second = SpanBatch(*[np.concatenate(c) for c in zip(*[q.columns() for q in parts[4:]])])
+        _check(e.flush_exp(), second, 160)
+
+
 def test_expo_sketches_unchanged():
     wl = generate_c2(150_000, seed=23)
     with _engine(wl, exp_max_size=160) as e:

@@ -112,6 +112,11 @@ for step in "$@"; do
       (export SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so; export "$knob"; \
        run "labbin_${knob//=/}" 600 python -u -m pytest tests/test_gpu_binned.py "tests/test_gpu_regime.py" -m gpu -x -v \
          --timeout 300 --timeout-method thread) || exit $? ;;
+    expoab_*) wl=${step#expoab_}  # c2expo: span records x slab sets (laboratory build), rounds interleaved
+      for r in 1 2; do for x in 0 1; do for ns in 1 2; do
+        SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_XREC=$x SPANAGG_SLAB_SETS=$ns \
+          run "expoab_${wl}_x${x}_s${ns}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $BQ
+      done; done; done ;;
     labexpo_*) knob=${step#labexpo_}  # the exponential-histogram suites on the laboratory build with one knob, e.g. labexpo_SPANAGG_XREC=0
       (export SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so; export "$knob"; \
        run "labexpo_${knob//=/}" 300 python -u -m pytest tests/test_gpu_expo.py tests/test_gpu_churn.py -m gpu -x -v \
