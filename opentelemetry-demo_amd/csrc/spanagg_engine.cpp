@@ -38,9 +38,9 @@ constexpr int kDefaultVariant = 20;
 constexpr uint32_t kMaxSlabSets = 4;      // per-workgroup slab sets (small path)
 constexpr uint32_t kDefaultSlabSets = 2;  // SPANAGG_SLAB_SETS overrides (laboratory build)
 // exponential slab path: 8-B span records for the counting pass (expo_span_recs;
-// off: the slot + both times were faster, the ingest kernel's wider stores
-// costing more than the counting pass saves -- DESIGN.md section 4)
-constexpr bool kExpoSpanRecs = false;
+// with two slab sets the fastest of the four combinations by A/B -- DESIGN.md
+// section 4)
+constexpr bool kExpoSpanRecs = true;
 
 // Laboratory knobs: the SPANAGG_AB build (`make ab` -> libspanagg_ab.so, used
 // by tools/ for A/B runs and ablations) reads them from the environment; the
@@ -783,8 +783,8 @@ static int bt_aggregate_pending(sa_engine *e) {
 
 
 // The exponential slab path hands the counting pass 8-B span records (slot |
-// duration) instead of the slot alone (laboratory build: SPANAGG_XREC=0 / 1
-// picks, for A/B runs)
+// duration) instead of the slot alone, so the counting pass reads 8 B per span
+// instead of 20 (laboratory build: SPANAGG_XREC=0 / 1 picks, for A/B runs)
 static bool expo_span_recs(const sa_engine *e) {
   static const int knob = [] {
     const char *v = ab_env("SPANAGG_XREC");

@@ -773,12 +773,12 @@ size_t expo_slab_lds_bytes(uint64_t cap, uint32_t max_size, uint32_t ne) {
 
 hipError_t prepare_expo_slab(size_t lds_bytes) {
 #ifdef SPANAGG_AB
-  if (hipError_t e = hipFuncSetAttribute((const void *)&expo_count_slab_kernel<true>,
+  if (hipError_t e = hipFuncSetAttribute((const void *)&expo_count_slab_kernel<false>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
       e != hipSuccess)
     return e;
 #endif
-  if (hipError_t e = hipFuncSetAttribute((const void *)&expo_count_slab_kernel<false>,
+  if (hipError_t e = hipFuncSetAttribute((const void *)&expo_count_slab_kernel<true>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
       e != hipSuccess)
     return e;
@@ -824,13 +824,13 @@ hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s) {
     const uint64_t per_wg = ((E.n + E.xG - 1) / E.xG + 3) / 4 * 4;
     if (per_wg > kXcMaxSpans) return hipErrorInvalidValue;  // (the engine splits batches below this)
     const uint32_t grid = (uint32_t)((E.n + per_wg - 1) / per_wg);
-#ifdef SPANAGG_AB  // (span records: laboratory build only, SPANAGG_XREC=1)
-    if (E.span_rec)
-      hipLaunchKernelGGL(expo_count_slab_kernel<true>, dim3(grid), dim3(kXcBlock),
+#ifdef SPANAGG_AB  // (slots + times: laboratory build only, SPANAGG_XREC=0)
+    if (!E.span_rec)
+      hipLaunchKernelGGL(expo_count_slab_kernel<false>, dim3(grid), dim3(kXcBlock),
                          expo_slab_lds_bytes(E.cap, E.max_size, E.xc_ne), s, E, per_wg);
     else
 #endif
-      hipLaunchKernelGGL(expo_count_slab_kernel<false>, dim3(grid), dim3(kXcBlock),
+      hipLaunchKernelGGL(expo_count_slab_kernel<true>, dim3(grid), dim3(kXcBlock),
                          expo_slab_lds_bytes(E.cap, E.max_size, E.xc_ne), s, E, per_wg);
     const uint32_t words = E.xc_ne * ((E.max_size + 1) / 2), slab_blocks = (words + 63) / 64;
     const uint32_t tail_blocks = E.xt_rec ? xt_bins(E.cap) : 0u;
