@@ -110,6 +110,7 @@ struct IngestParams {
   // EXPO mode with slab counting: [n] span records instead (span_rec_of), so
   // the counting pass reads 8 B per span instead of the slot and both times
   unsigned long long *span_rec;
+  unsigned long long *span_long;  // [n]: the duration of each span whose record holds kSpanRecDurMask
   XHdr *xslab;
   // Small-table kernels with the tail pool (POOL): every workgroup owns the
   // static range [b * wg_chunk, (b + 1) * wg_chunk); spans [pool_base, n)
@@ -165,6 +166,7 @@ struct ExpoParams {
                       // 1 no HBM bucket atomics, 2 no LDS cache, 4 exact index path only, 8 no index
   uint32_t *slot_of;  // [n] key slot of each span (pass 1 / the small-table ingest kernel -> counting)
   const unsigned long long *span_rec;  // [n] span records (slab counting: the small-table kernel -> counting)
+  const unsigned long long *span_long;  // [n] durations of the records holding kSpanRecDurMask
   unsigned long long *dropped;
   XHdr *xslab;        // small-table engines: [xG][cap] per-workgroup header partials (nullptr: pass 1 atomics)
   uint32_t xG;
@@ -182,7 +184,8 @@ struct ExpoParams {
 // A span record of the exponential-histogram slab path: the key slot in the
 // top 12 bits (kSpanRecNoSlot: none; slab tables have <= 2,048 slots) and the
 // duration in ns below; a duration of 2^52 - 1 ns (52 days) or more is stored
-// as kSpanRecDurMask and the counting pass reads that span's times instead.
+// as kSpanRecDurMask and in full at the span's index of span_long (so the
+// counting pass reads no caller memory).
 constexpr uint32_t kSpanRecShift = 52;
 constexpr uint32_t kSpanRecNoSlot = 0xFFFu;
 constexpr unsigned long long kSpanRecDurMask = (1ull << kSpanRecShift) - 1;

@@ -135,6 +135,12 @@ struct sa_engine {
   // (the headers and buckets have one owner at a time)
   hipEvent_t ev_expo = nullptr;
   hipStream_t expo_last = nullptr;
+  // With span records the histogram kernels read no caller memory: they run on
+  // the engine's xstream after an event on the launch's ingest kernel
+  // (ev_ing[set]), so a caller's next launch -- on any stream -- waits only for
+  // its slab set's previous user, never behind the histogram kernels
+  hipStream_t xstream = nullptr;
+  hipEvent_t ev_ing[kMaxSlabSets] = {};
   unsigned long long *expo_out_keys = nullptr;
   sa::ExpoRow *expo_out_rows = nullptr;
   uint32_t *expo_out_buckets = nullptr;
@@ -519,6 +525,11 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       if ((rc = alloc((void **)&e->xslab, (size_t)e->nsets * e->G * e->cap * sizeof(sa::XHdr)))) return bail(rc);
       if (hipEventCreateWithFlags(&e->ev_expo, ev_flags()) != hipSuccess)
         return bail(fail(e, SA_EDEVICE, "event creation failed"));
+      if (hipStreamCreateWithFlags(&e->xstream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(e, SA_EDEVICE, "histogram stream creation failed"));
+      for (hipEvent_t &ev : e->ev_ing)
+        if (hipEventCreateWithFlags(&ev, ev_flags()) != hipSuccess)
+          return bail(fail(e, SA_EDEVICE, "event creation failed"));
       if (e->xc_ne &&
           ((rc = alloc((void **)&e->xc_lcount, e->cap * 4)) ||
            (rc = alloc((void **)&e->xc_slot_of_entry, (size_t)e->xc_ne * 4)) ||
@@ -629,6 +640,12 @@ void sa_destroy(sa_engine *e) {
     if (ev) (void)hipEventDestroy(ev);
   if (e->ev_ctl) (void)hipEventDestroy(e->ev_ctl);
   if (e->ev_expo) (void)hipEventDestroy(e->ev_expo);
+  for (hipEvent_t ev : e->ev_ing)
+    if (ev) (void)hipEventDestroy(ev);
+  if (e->xstream) {
+    (void)hipStreamSynchronize(e->xstream);
+    (void)hipStreamDestroy(e->xstream);
+  }
   for (int k = 0; k < sa_engine::kBtSets; ++k) {
     if (e->ev_scat[k]) (void)hipEventDestroy(e->ev_scat[k]);
     if (e->ev_agg[k]) (void)hipEventDestroy(e->ev_agg[k]);
@@ -819,8 +836,10 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b, uint32_t
     E.diag = diag;
   }
   // (this launch's set of span slots / records and header partials)
-  E.slot_of = e->expo_slot ? e->expo_slot + 2 * (size_t)set * e->expo_slot_cap : nullptr;
+  // (per set: n span records or u32 slots, then n long durations)
+  E.slot_of = e->expo_slot ? e->expo_slot + 4 * (size_t)set * e->expo_slot_cap : nullptr;
   E.span_rec = expo_span_recs(e) ? reinterpret_cast<const unsigned long long *>(E.slot_of) : nullptr;
+  E.span_long = E.span_rec ? E.span_rec + e->expo_slot_cap : nullptr;
   E.dropped = e->stats + sa::kStatDropped;
   E.xslab = e->expo_small ? e->xslab + (size_t)set * e->G * e->cap : nullptr;
   E.xG = e->G;
@@ -938,6 +957,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.lb_seq = e->lb_seq++;
   P.hll_filt = e->hll_filt;
   hipError_t st;
+  hipStream_t hs = s;  // the stream the launch's last kernel runs on (expo: the histogram kernels')
   if (e->small) {
     st = sa::launch_ingest_small(P, grid, e->lds_bytes, s, e->variant);
   } else if (e->bt) {
@@ -990,21 +1010,33 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
       if (e->expo_slot) (void)hipFree(e->expo_slot);
       e->expo_slot = nullptr;
       e->expo_slot_cap = 0;
-      // (8 B per span and set: span records on the slab-counting path, else u32 slots)
-      if (hipMalloc((void **)&e->expo_slot, (size_t)e->nsets * b->n * 8) != hipSuccess)
+      // (16 B per span and set: span records or u32 slots, then long durations)
+      if (hipMalloc((void **)&e->expo_slot, (size_t)e->nsets * b->n * 16) != hipSuccess)
         return fail(e, SA_ENOMEM, "expo slot buffer");
       e->expo_slot_cap = b->n;
     }
-    uint32_t *slots = e->expo_slot + 2 * (size_t)set * e->expo_slot_cap;
+    uint32_t *slots = e->expo_slot + 4 * (size_t)set * e->expo_slot_cap;
     if (e->expo_small) {
       // the small-table kernel in EXPO mode: sketches, key slots, header partials
-      if (expo_span_recs(e)) P.span_rec = reinterpret_cast<unsigned long long *>(slots);
-      else P.slot_of = slots;
+      const bool recs = expo_span_recs(e);
+      if (recs) {
+        P.span_rec = reinterpret_cast<unsigned long long *>(slots);
+        P.span_long = P.span_rec + e->expo_slot_cap;
+      } else {
+        P.slot_of = slots;
+      }
       P.xslab = e->xslab + (size_t)set * e->G * e->cap;
       st = sa::launch_ingest_expo_small(P, grid, e->lds_bytes, s);
-      // the histogram kernels after the previous launch's (one owner of the
-      // headers and buckets at a time); this ingest kernel may run beside them
-      if (st == hipSuccess && e->expo_last && e->expo_last != s) st = hipStreamWaitEvent(s, e->ev_expo, 0);
+      if (recs) {
+        // the histogram kernels on the engine's xstream, after this ingest kernel
+        hs = e->xstream;
+        if (st == hipSuccess) st = hipEventRecord(e->ev_ing[set], s);
+        if (st == hipSuccess) st = hipStreamWaitEvent(hs, e->ev_ing[set], 0);
+      } else if (st == hipSuccess && e->expo_last && e->expo_last != s) {
+        // (slots: the counting pass reads the caller's times, so it stays on the
+        // caller's stream, after the previous launch's histogram kernels)
+        st = hipStreamWaitEvent(s, e->ev_expo, 0);
+      }
     } else {
       // sketches (and the zero-key / service / window counters) through the
       // HBM-table kernel with its RED part off
@@ -1012,10 +1044,10 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
       st = sa::launch_ingest_hbm(P, grid, s, e->variant);
     }
     // then the histogram kernels
-    if (st == hipSuccess) st = sa::launch_expo_ingest(expo_params(e, b, set), s);
+    if (st == hipSuccess) st = sa::launch_expo_ingest(expo_params(e, b, set), hs);
     if (st == hipSuccess && e->ev_expo) {
-      st = hipEventRecord(e->ev_expo, s);
-      e->expo_last = s;
+      st = hipEventRecord(e->ev_expo, hs);
+      e->expo_last = hs;
     }
   } else {
     st = sa::launch_ingest_hbm(P, grid, s, e->variant);
@@ -1024,8 +1056,8 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   // (laboratory build: SPANAGG_NO_SETEV=1 skips the slab-set event -- only
   // valid when every launch uses one stream; it prices the event's cost)
   static const bool no_setev = ab_env("SPANAGG_NO_SETEV") != nullptr;
-  if (!no_setev) SA_HIP(e, hipEventRecord(e->ev_set[set], s));
-  e->set_stream[set] = s;
+  if (!no_setev) SA_HIP(e, hipEventRecord(e->ev_set[set], hs));
+  e->set_stream[set] = hs;
   e->set = (set + 1) % e->nsets;
   e->spans += b->n;
   e->unflushed = true;

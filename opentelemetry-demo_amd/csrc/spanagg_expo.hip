@@ -451,15 +451,12 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
     }
   };
   // one span record (span_rec_of; 0 past the range: no duration); a duration
-  // past the record's field is read from the span's times
+  // past the record's field is read from span_long
   auto count_rec = [&](unsigned long long r, uint64_t i) {
     const uint32_t slot = (uint32_t)(r >> kSpanRecShift);
     if (slot == kSpanRecNoSlot) return;
     uint64_t d = r & kSpanRecDurMask;
-    if (d == kSpanRecDurMask) {
-      const uint64_t st = E.start[i], en = E.end[i];
-      d = en > st ? en - st : 0;
-    }
+    if (d == kSpanRecDurMask) d = E.span_long[i];
     count(slot, d);
   };
   // four consecutive spans per thread through 16-B buffer loads (0 past the

@@ -956,6 +956,10 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
           for (int j = 0; j < S; ++j)
             if (i0 + (uint32_t)j < lim) rp[j] = span_rec_of(found[j], dur[j]);
         }
+        // (durations past the record's field, 52 days or more: in full beside it)
+#pragma unroll
+        for (int j = 0; j < S; ++j)
+          if (dur[j] >= kSpanRecDurMask && i0 + (uint32_t)j < lim) P.span_long[lo + i0 + j] = dur[j];
       }
     } else if constexpr (LEAN) {
       const uint32_t lane = threadIdx.x & 63u;

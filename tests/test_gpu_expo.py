@@ -212,7 +212,8 @@ def test_expo_launches_over_two_streams_pipelined():
     """Small-table exponential engines run launch k + 1's ingest kernel beside
     launch k's reduce / count / fold (two sets of header partials and span
     slots; launch k + 1's reduce waits for launch k's fold).  Six
-    device-resident launches alternate over two streams; launches 3 and 5
+    device-resident launches alternate over two streams, each batch's times
+    overwritten on its stream right after the call; launches 3 and 5
     stretch their durations (x 40, x 0.02) so the scales move under the
     pipeline; a delta flush after the fourth launch."""
     import torch
@@ -237,7 +238,14 @@ def test_expo_launches_over_two_streams_pipelined():
     with _engine(wl, exp_max_size=160) as e:
         assert e.stats()["small_table"] == 1
         for i, cols in enumerate(dcols):
-            e.ingest_device(*cols, stream=streams[i % 2].cuda_stream)
+            st = streams[i % 2]
+            e.ingest_device(*cols, stream=st.cuda_stream)
+            # the columns are the caller's again once its stream passes the
+            # call: overwritten there at once (the histogram kernels must
+            # read the engine's span records, not these)
+            with torch.cuda.stream(st):
+                cols[1].fill_(7)
+                cols[2].fill_(3)
             if i == 3:
                 first = SpanBatch(*[np.concatenate(c) for c in zip(*[q.columns() for q in parts[:4]])])
                 _check(e.flush_exp(), first, 160)
