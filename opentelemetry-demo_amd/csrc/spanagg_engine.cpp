@@ -135,10 +135,10 @@ struct sa_engine {
   // (the headers and buckets have one owner at a time)
   hipEvent_t ev_expo = nullptr;
   hipStream_t expo_last = nullptr;
-  // With span records the histogram kernels read no caller memory: they run on
-  // the engine's xstream after an event on the launch's ingest kernel
-  // (ev_ing[set]), so a caller's next launch -- on any stream -- waits only for
-  // its slab set's previous user, never behind the histogram kernels
+  // Laboratory build (SPANAGG_XSTREAM=1): with span records the histogram
+  // kernels read no caller memory, so they can run on an engine stream after
+  // an event on the launch's ingest kernel (ev_ing[set]); slower than the
+  // caller's stream by A/B (the ingest kernel starves them), so off
   hipStream_t xstream = nullptr;
   hipEvent_t ev_ing[kMaxSlabSets] = {};
   unsigned long long *expo_out_keys = nullptr;
@@ -525,11 +525,15 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       if ((rc = alloc((void **)&e->xslab, (size_t)e->nsets * e->G * e->cap * sizeof(sa::XHdr)))) return bail(rc);
       if (hipEventCreateWithFlags(&e->ev_expo, ev_flags()) != hipSuccess)
         return bail(fail(e, SA_EDEVICE, "event creation failed"));
-      if (hipStreamCreateWithFlags(&e->xstream, hipStreamNonBlocking) != hipSuccess)
-        return bail(fail(e, SA_EDEVICE, "histogram stream creation failed"));
-      for (hipEvent_t &ev : e->ev_ing)
-        if (hipEventCreateWithFlags(&ev, ev_flags()) != hipSuccess)
-          return bail(fail(e, SA_EDEVICE, "event creation failed"));
+      // (laboratory build, SPANAGG_XSTREAM=1: the histogram kernels on an
+      // engine stream -- slower by A/B)
+      if (const char *v = ab_env("SPANAGG_XSTREAM"); v && std::atoi(v) != 0) {
+        if (hipStreamCreateWithFlags(&e->xstream, hipStreamNonBlocking) != hipSuccess)
+          return bail(fail(e, SA_EDEVICE, "histogram stream creation failed"));
+        for (hipEvent_t &ev : e->ev_ing)
+          if (hipEventCreateWithFlags(&ev, ev_flags()) != hipSuccess)
+            return bail(fail(e, SA_EDEVICE, "event creation failed"));
+      }
       if (e->xc_ne &&
           ((rc = alloc((void **)&e->xc_lcount, e->cap * 4)) ||
            (rc = alloc((void **)&e->xc_slot_of_entry, (size_t)e->xc_ne * 4)) ||
@@ -1027,14 +1031,14 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
       }
       P.xslab = e->xslab + (size_t)set * e->G * e->cap;
       st = sa::launch_ingest_expo_small(P, grid, e->lds_bytes, s);
-      if (recs) {
+      if (recs && e->xstream) {
         // the histogram kernels on the engine's xstream, after this ingest kernel
         hs = e->xstream;
         if (st == hipSuccess) st = hipEventRecord(e->ev_ing[set], s);
         if (st == hipSuccess) st = hipStreamWaitEvent(hs, e->ev_ing[set], 0);
       } else if (st == hipSuccess && e->expo_last && e->expo_last != s) {
-        // (slots: the counting pass reads the caller's times, so it stays on the
-        // caller's stream, after the previous launch's histogram kernels)
+        // on the caller's stream, after the previous launch's histogram kernels
+        // (one owner of the headers and buckets at a time)
         st = hipStreamWaitEvent(s, e->ev_expo, 0);
       }
     } else {
