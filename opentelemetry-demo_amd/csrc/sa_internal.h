@@ -33,6 +33,7 @@ struct BinEntry {
 constexpr int kBins = 65;
 
 struct XHdr;
+struct ExpoHdr;
 // Everything the ingest kernels need, passed by value (kernel-argument segment,
 // read through the scalar cache).
 struct IngestParams {
@@ -111,6 +112,13 @@ struct IngestParams {
   // the counting pass reads 8 B per span instead of the slot and both times
   unsigned long long *span_rec;
   unsigned long long *span_long;  // [n]: the duration of each span whose record holds kSpanRecDurMask
+  // EXPO mode, index records (xidx != 0): slot_of holds ixrec words -- each
+  // span's bucket index at the scale its series had when the kernel started
+  // (xhdr[].scale, read in the prologue) -- and span_long the durations the
+  // fast index path declined
+  const ExpoHdr *xhdr;
+  long long l2d_fx;  // log2(div) * 2^32 rounded (expo_index_fast)
+  uint32_t xidx;
   XHdr *xslab;
   // Small-table kernels with the tail pool (POOL): every workgroup owns the
   // static range [b * wg_chunk, (b + 1) * wg_chunk); spans [pool_base, n)
@@ -167,6 +175,7 @@ struct ExpoParams {
   uint32_t *slot_of;  // [n] key slot of each span (pass 1 / the small-table ingest kernel -> counting)
   const unsigned long long *span_rec;  // [n] span records (slab counting: the small-table kernel -> counting)
   const unsigned long long *span_long;  // [n] durations of the records holding kSpanRecDurMask
+  uint32_t xidx;  // slot_of holds index records (ixrec), the counting pass shifts them to the new scale
   unsigned long long *dropped;
   XHdr *xslab;        // small-table engines: [xG][cap] per-workgroup header partials (nullptr: pass 1 atomics)
   uint32_t xG;
@@ -192,6 +201,21 @@ constexpr unsigned long long kSpanRecDurMask = (1ull << kSpanRecShift) - 1;
 __host__ __device__ inline unsigned long long span_rec_of(uint32_t slot, unsigned long long d) {
   return (unsigned long long)(slot < kSpanRecNoSlot ? slot : kSpanRecNoSlot) << kSpanRecShift |
          (d < kSpanRecDurMask ? d : kSpanRecDurMask);
+}
+// An index record (the exponential slab path's span word, u32): the key slot
+// in the top 12 bits (kSpanRecNoSlot: none), the scale the ingest kernel read
+// for the slot + 10 (5 bits), the bucket index at that scale (14 bits,
+// signed) and a flag bit.  Flag with index field 0: the duration is in
+// span_long (the fast path declined, or the index needs more bits); flag with
+// index field 1: zero duration.  A series' scale only falls within a flush
+// interval, so the counting pass gets the index at the scale the reduce pass
+// settled on by an arithmetic shift (go-expohisto: bucket i at scale s - 1
+// holds buckets 2i and 2i + 1 at scale s).
+constexpr uint32_t kIxSlotShift = 20, kIxScaleShift = 15, kIxScaleBias = 10;
+constexpr int32_t kIxMin = -(1 << 13), kIxMax = (1 << 13) - 1;
+constexpr uint32_t kIxLong = 1u, kIxZero = 3u;  // flag | index field 0 / 1
+__host__ __device__ inline uint32_t ixrec_of(uint32_t slot, int32_t scale, int32_t ix) {
+  return slot << kIxSlotShift | (uint32_t)(scale + (int32_t)kIxScaleBias) << kIxScaleShift | ((uint32_t)ix & 0x3FFFu) << 1;
 }
 constexpr uint32_t kXtCap = 4096;       // tail records per counting workgroup (16 KiB of LDS)
 constexpr uint32_t kXtBinSlots = 8;     // slots per tail fold bin

@@ -37,10 +37,11 @@ constexpr uint64_t kSlabLimit = 1ULL << 31;  // per-workgroup spans between slab
 constexpr int kDefaultVariant = 20;
 constexpr uint32_t kMaxSlabSets = 4;      // per-workgroup slab sets (small path)
 constexpr uint32_t kDefaultSlabSets = 2;  // SPANAGG_SLAB_SETS overrides (laboratory build)
-// exponential slab path: 8-B span records for the counting pass (expo_span_recs;
-// with two slab sets the fastest of the four combinations by A/B -- DESIGN.md
-// section 4)
-constexpr bool kExpoSpanRecs = true;
+// exponential slab path: what the ingest kernel hands the counting pass per
+// span (expo_rec_mode): 0 the key slot (the pass reads both times too), 1 an
+// 8-B span record (slot | duration), 2 an index record (slot | scale | bucket
+// index, ixrec_of) -- DESIGN.md section 4
+constexpr int kExpoRecMode = 2;
 
 // Laboratory knobs: the SPANAGG_AB build (`make ab` -> libspanagg_ab.so, used
 // by tools/ for A/B runs and ablations) reads them from the environment; the
@@ -423,7 +424,8 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   e->expo = cfg->exp_max_size != 0;
   e->small = e->lds_bytes <= kLdsBudget && !e->expo;
   if (e->expo) {  // key mirror + 32-B header partials per slot (nw = 6 counter words)
-    const size_t xl = (size_t)e->cap * 8 + (size_t)e->cap * 32 + sa::kLdsExtraBytes;
+    // (+ cap: the index records' per-slot scales)
+    const size_t xl = (size_t)e->cap * 8 + (size_t)e->cap * 32 + sa::kLdsExtraBytes + (size_t)e->cap;
     e->expo_small = xl <= kLdsBudget && !(cfg->options & SA_OPT_EXPO_HBM);
     if (e->expo_small) e->lds_bytes = xl;
   }
@@ -803,17 +805,17 @@ static int bt_aggregate_pending(sa_engine *e) {
 }
 
 
-// The exponential slab path hands the counting pass 8-B span records (slot |
-// duration) instead of the slot alone, so the counting pass reads 8 B per span
-// instead of 20 (laboratory build: SPANAGG_XREC=0 / 1 picks, for A/B runs)
-static bool expo_span_recs(const sa_engine *e) {
+// The exponential slab path's span words (kExpoRecMode; laboratory build:
+// SPANAGG_XREC=0 / 1 / 2 picks, for A/B runs); slab counting only
+static int expo_rec_mode(const sa_engine *e) {
   static const int knob = [] {
     const char *v = ab_env("SPANAGG_XREC");
     return v ? std::atoi(v) : -1;
   }();
-  const bool on = knob < 0 ? kExpoSpanRecs : knob != 0;
-  return on && e->expo_small && e->xc_ne;
+  if (!e->expo_small || !e->xc_ne) return 0;
+  return knob >= 0 && knob <= 2 ? knob : kExpoRecMode;
 }
+static bool expo_span_recs(const sa_engine *e) { return expo_rec_mode(e) == 1; }
 
 static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b, uint32_t set = 0) {
   sa::ExpoParams E{};
@@ -843,7 +845,10 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b, uint32_t
   // (per set: n span records or u32 slots, then n long durations)
   E.slot_of = e->expo_slot ? e->expo_slot + 4 * (size_t)set * e->expo_slot_cap : nullptr;
   E.span_rec = expo_span_recs(e) ? reinterpret_cast<const unsigned long long *>(E.slot_of) : nullptr;
-  E.span_long = E.span_rec ? E.span_rec + e->expo_slot_cap : nullptr;
+  E.xidx = expo_rec_mode(e) == 2 ? 1u : 0u;
+  E.span_long = (E.span_rec || E.xidx) && e->expo_slot
+                    ? reinterpret_cast<const unsigned long long *>(E.slot_of) + e->expo_slot_cap
+                    : nullptr;
   E.dropped = e->stats + sa::kStatDropped;
   E.xslab = e->expo_small ? e->xslab + (size_t)set * e->G * e->cap : nullptr;
   E.xG = e->G;
@@ -1022,12 +1027,19 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
     uint32_t *slots = e->expo_slot + 4 * (size_t)set * e->expo_slot_cap;
     if (e->expo_small) {
       // the small-table kernel in EXPO mode: sketches, key slots, header partials
-      const bool recs = expo_span_recs(e);
+      const int mode = expo_rec_mode(e);
+      const bool recs = mode == 1;
       if (recs) {
         P.span_rec = reinterpret_cast<unsigned long long *>(slots);
         P.span_long = P.span_rec + e->expo_slot_cap;
       } else {
         P.slot_of = slots;
+        if (mode == 2) {
+          P.xidx = 1;
+          P.xhdr = e->expo_hdr;
+          P.l2d_fx = std::llround(std::log2(e->cfg.unit == SA_UNIT_S ? 1e9 : 1e6) * 4294967296.0);
+          P.span_long = reinterpret_cast<unsigned long long *>(slots) + e->expo_slot_cap;
+        }
       }
       P.xslab = e->xslab + (size_t)set * e->G * e->cap;
       st = sa::launch_ingest_expo_small(P, grid, e->lds_bytes, s);

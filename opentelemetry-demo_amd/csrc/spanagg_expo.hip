@@ -77,42 +77,8 @@ __device__ __forceinline__ double expo_value(uint64_t d_ns, double div) {
   return (double)d_ns / div;
 }
 
-// Fast path of the bucket index of a duration d > 0 ns at `scale`: log2 of the
-// value from d's exponent, v_log_f32 of its top 24 bits and log2(div), all
-// exact or nearly so -- |error| <= kFastLog2Err (the hardware log2 over every
-// float in [1, 2), measured exhaustively by test_gpu_expo.py's
-// test_fast_log2_error_bound, plus the 24-bit truncation of d).  When the
-// scaled value is farther than its error bound from an integer, its floor is
-// the index Go's math.Log computation gives (that one is within ~1e-9 of the
-// exact value at any scale <= 20); otherwise -- including every power of two
-// and every value near a bucket boundary -- false, and the caller takes the
-// exact path.
-// Integer arithmetic: z = log2(d / div) in 32.32 fixed point (l2d_fx =
-// log2(div) * 2^32 rounded, the hardware log2 of the mantissa converted with
-// its 32 fraction bits), so the scaled value's integer part is z's bits above
-// 32 - scale and its distance to an integer is read from the bits below (no
-// f64 ops: the counting kernel issues ~half the VALU work of the f64 form).
-// kFastFxErr: kFastLog2Err in those units plus the two conversions' 2^-32.
-constexpr double kFastLog2Err = 1.0 / (1 << 20) + 1.0 / (1 << 22);
-constexpr uint64_t kFastFxErr = (uint64_t)(kFastLog2Err * 4294967296.0) + 4;
-__device__ __forceinline__ bool expo_index_fast(uint64_t d, long long l2d_fx, int32_t scale, int32_t &idx) {
-  const int32_t e = 63 - (int32_t)__clzll((long long)d);
-  const uint32_t top = (uint32_t)((d << (63 - e)) >> 40);  // 24 bits, the leading one at bit 23
-  const float m = (float)top * 0x1p-23f;                    // exact, in [1, 2)
-  const uint32_t t = (uint32_t)(__builtin_amdgcn_logf(m) * 0x1p32f);  // log2(m) < 1, 32 fraction bits
-  const long long z = ((long long)e << 32) - l2d_fx + (long long)t;   // ~ log2(d / div) * 2^32
-  const int32_t sh = scale > 0 ? 32 - scale : 32;
-  const uint64_t one = 1ull << sh, f = (uint64_t)z & (one - 1);
-  if (f <= kFastFxErr || one - f <= kFastFxErr) return false;  // near a bucket boundary / power of two
-  const int32_t fl = (int32_t)(z >> sh);                        // floor of the scaled value
-  if (scale <= 0) {
-    idx = fl >> (-scale);  // Go: exponent >> -scale (z is not an integer)
-    return true;
-  }
-  const int32_t max_index = (1024 << scale) - 1;
-  idx = fl >= max_index ? max_index : fl;
-  return true;
-}
+// (the fast bucket index, expo_index_fast, is in sa_device.h: the ingest
+// kernel computes it too)
 __host__ inline long long expo_l2d_fx(double div) { return std::llround(std::log2(div) * 4294967296.0); }
 
 constexpr int32_t kExpoMaxScale = 20, kExpoMinScale = -10;
@@ -399,10 +365,12 @@ __device__ __forceinline__ void expo_select_lds(const ExpoParams &E, int32_t *en
   }
 }
 
-// REC: the spans as the ingest kernel's 8-B records (E.span_rec); else as
-// the key slot (E.slot_of) and both times (20 B per span)
-template <bool REC>
+// IN: the spans as 0 = the key slot (E.slot_of) and both times (20 B per
+// span), 1 = the ingest kernel's 8-B span records (E.span_rec), 2 = its index
+// records (E.slot_of, ixrec: 4 B, the bucket index already computed)
+template <int IN>
 __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uint64_t per_wg) {
+  constexpr bool REC = IN == 1, IXR = IN == 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t M = E.max_size, NE = E.xc_ne, cap = (uint32_t)E.cap, wpe = (M + 1) / 2;
   int2 *meta = reinterpret_cast<int2 *>(smem);                   // [cap] {scale, cur}
@@ -431,12 +399,8 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
   __syncthreads();
   const uint64_t lo = blockIdx.x * per_wg, hi = lo + per_wg < E.n ? lo + per_wg : E.n;
   const uint32_t len = hi > lo ? (uint32_t)(hi - lo) : 0u;
-  auto count = [&](uint32_t slot, uint64_t d) {
-    if (d == 0) return;
-    const int2 m = meta[slot];
-    const int32_t sc = (int32_t)(int8_t)(m.x & 0xFF);
-    int32_t ix;
-    if (!expo_index_fast(d, E.log2div_fx, sc, ix)) ix = expo_index(expo_value(d, E.div), sc);
+  // the span's bucket index ix at its series' scale -> its LDS entry or a tail record
+  auto add = [&](uint32_t slot, int32_t ix, int2 m) {
     const uint32_t rel = (uint32_t)(ix - m.y), a0 = ((uint32_t)m.x >> 9) + rel;
     const uint32_t at = rel < M ? (a0 >= M ? a0 - M : a0) : expo_mod(ix, M);
     const int32_t en_ = ent[slot];
@@ -449,6 +413,30 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
       if (r < kXtCap) trec[r] = slot << 12 | at;
       else atomicAdd(E.buckets + ((uint64_t)(((uint32_t)m.x >> 8) & 1u) * E.cap + slot) * M + at, 1u);
     }
+  };
+  auto count = [&](uint32_t slot, uint64_t d) {
+    if (d == 0) return;
+    const int2 m = meta[slot];
+    const int32_t sc = (int32_t)(int8_t)(m.x & 0xFF);
+    int32_t ix;
+    if (!expo_index_fast(d, E.log2div_fx, sc, ix)) ix = expo_index(expo_value(d, E.div), sc);
+    add(slot, ix, m);
+  };
+  // one index record (ixrec_of): the index at the scale the ingest kernel
+  // read, shifted to the scale the reduce pass settled on (never higher: a
+  // series' scale only falls within a flush interval)
+  auto count_ix = [&](uint32_t w, uint64_t i) {
+    const uint32_t slot = w >> kIxSlotShift;
+    if (slot == kSpanRecNoSlot || w == (slot << kIxSlotShift | kIxZero)) return;
+    if (w & 1u) {
+      count(slot, E.span_long[i]);
+      return;
+    }
+    const int2 m = meta[slot];
+    const int32_t sn = (int32_t)(int8_t)(m.x & 0xFF);
+    const int32_t su = (int32_t)((w >> kIxScaleShift) & 31u) - (int32_t)kIxScaleBias;
+    const int32_t ix = ((int32_t)(w << 17) >> 18) >> (su - sn);  // the 14-bit field, sign-extended
+    add(slot, ix, m);
   };
   // one span record (span_rec_of; 0 past the range: no duration); a duration
   // past the record's field is read from span_long
@@ -465,10 +453,12 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
   // per CU in flight
   const __amdgpu_buffer_rsrc_t rr = rsrc(REC ? (const void *)(E.span_rec + lo) : (const void *)(E.slot_of + lo),
                                          REC ? len * 8 : len * 4);
-  const __amdgpu_buffer_rsrc_t rst = rsrc(E.start + lo, REC ? 0u : len * 8), ren = rsrc(E.end + lo, REC ? 0u : len * 8);
+  constexpr bool kTimes = IN == 0;
+  const __amdgpu_buffer_rsrc_t rst = rsrc(E.start + lo, kTimes ? len * 8 : 0u),
+                               ren = rsrc(E.end + lo, kTimes ? len * 8 : 0u);
   struct Quad {
     unsigned long long r[4];  // REC: the records; else the slots
-    uint64_t s[REC ? 1 : 4], e[REC ? 1 : 4];
+    uint64_t s[kTimes ? 4 : 1], e[kTimes ? 4 : 1];
   };
   auto load = [&](uint32_t base, Quad &q) {
     const int o = (int)(base + 4 * threadIdx.x);
@@ -483,14 +473,16 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
       const auto a = __builtin_amdgcn_raw_buffer_load_b128(rr, o * 4, 0, 0);
 #pragma unroll
       for (int j = 0; j < 4; ++j) q.r[j] = a[j];
+      if constexpr (kTimes) {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const auto x = __builtin_amdgcn_raw_buffer_load_b128(rst, o * 8 + 16 * h, 0, 0);
-        const auto y = __builtin_amdgcn_raw_buffer_load_b128(ren, o * 8 + 16 * h, 0, 0);
-        q.s[2 * h] = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
-        q.s[2 * h + 1] = (uint64_t)x[2] | ((uint64_t)x[3] << 32);
-        q.e[2 * h] = (uint64_t)y[0] | ((uint64_t)y[1] << 32);
-        q.e[2 * h + 1] = (uint64_t)y[2] | ((uint64_t)y[3] << 32);
+        for (int h = 0; h < 2; ++h) {
+          const auto x = __builtin_amdgcn_raw_buffer_load_b128(rst, o * 8 + 16 * h, 0, 0);
+          const auto y = __builtin_amdgcn_raw_buffer_load_b128(ren, o * 8 + 16 * h, 0, 0);
+          q.s[2 * h] = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+          q.s[2 * h + 1] = (uint64_t)x[2] | ((uint64_t)x[3] << 32);
+          q.e[2 * h] = (uint64_t)y[0] | ((uint64_t)y[1] << 32);
+          q.e[2 * h + 1] = (uint64_t)y[2] | ((uint64_t)y[3] << 32);
+        }
       }
     }
   };
@@ -500,6 +492,8 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
       if (base + 4 * threadIdx.x + j >= len) continue;
       if constexpr (REC) {
         count_rec(q.r[j], lo + base + 4 * threadIdx.x + j);
+      } else if constexpr (IXR) {
+        count_ix((uint32_t)q.r[j], lo + base + 4 * threadIdx.x + j);
       } else {
         const uint32_t slot = (uint32_t)q.r[j];
         if (slot != kNotFound) count(slot, q.e[j] > q.s[j] ? q.e[j] - q.s[j] : 0);
@@ -770,12 +764,12 @@ size_t expo_slab_lds_bytes(uint64_t cap, uint32_t max_size, uint32_t ne) {
 
 hipError_t prepare_expo_slab(size_t lds_bytes) {
 #ifdef SPANAGG_AB
-  if (hipError_t e = hipFuncSetAttribute((const void *)&expo_count_slab_kernel<false>,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-      e != hipSuccess)
-    return e;
+  for (const void *f : {(const void *)&expo_count_slab_kernel<0>, (const void *)&expo_count_slab_kernel<1>})
+    if (hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+        e != hipSuccess)
+      return e;
 #endif
-  if (hipError_t e = hipFuncSetAttribute((const void *)&expo_count_slab_kernel<true>,
+  if (hipError_t e = hipFuncSetAttribute((const void *)&expo_count_slab_kernel<2>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
       e != hipSuccess)
     return e;
@@ -821,13 +815,16 @@ hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s) {
     const uint64_t per_wg = ((E.n + E.xG - 1) / E.xG + 3) / 4 * 4;
     if (per_wg > kXcMaxSpans) return hipErrorInvalidValue;  // (the engine splits batches below this)
     const uint32_t grid = (uint32_t)((E.n + per_wg - 1) / per_wg);
-#ifdef SPANAGG_AB  // (slots + times: laboratory build only, SPANAGG_XREC=0)
-    if (!E.span_rec)
-      hipLaunchKernelGGL(expo_count_slab_kernel<false>, dim3(grid), dim3(kXcBlock),
+#ifdef SPANAGG_AB  // (slots + times, span records: laboratory build only, SPANAGG_XREC=0 / 1)
+    if (!E.xidx && !E.span_rec)
+      hipLaunchKernelGGL(expo_count_slab_kernel<0>, dim3(grid), dim3(kXcBlock),
+                         expo_slab_lds_bytes(E.cap, E.max_size, E.xc_ne), s, E, per_wg);
+    else if (!E.xidx)
+      hipLaunchKernelGGL(expo_count_slab_kernel<1>, dim3(grid), dim3(kXcBlock),
                          expo_slab_lds_bytes(E.cap, E.max_size, E.xc_ne), s, E, per_wg);
     else
 #endif
-      hipLaunchKernelGGL(expo_count_slab_kernel<true>, dim3(grid), dim3(kXcBlock),
+      hipLaunchKernelGGL(expo_count_slab_kernel<2>, dim3(grid), dim3(kXcBlock),
                          expo_slab_lds_bytes(E.cap, E.max_size, E.xc_ne), s, E, per_wg);
     const uint32_t words = E.xc_ne * ((E.max_size + 1) / 2), slab_blocks = (words + 63) / 64;
     const uint32_t tail_blocks = E.xt_rec ? xt_bins(E.cap) : 0u;

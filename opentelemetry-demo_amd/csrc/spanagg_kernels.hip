@@ -571,6 +571,8 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   // POOL: [kPoolMaxSteal] the pool block behind this workgroup's k-th stolen
   // block (0 = not known yet, block + 1, or kPoolDone)
   uint32_t *pmap = ltag + (TAG ? cap : 0u);
+  // EXPO with index records: [cap] each slot's scale when the kernel started
+  int8_t *lsc = reinterpret_cast<int8_t *>(pmap + (POOL ? kPoolMaxSteal : 0u));
   constexpr uint32_t kPoolDone = 0xFFFFFFFFu;
   const bool err_lds = P.errslab != nullptr;
   const bool lb_on = P.lb_n != 0 && !(diag & 2u);
@@ -671,6 +673,9 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   }
   if (threadIdx.x < 4) lstat[threadIdx.x] = 0;
   if (POOL && threadIdx.x < kPoolMaxSteal) pmap[threadIdx.x] = 0;
+  if constexpr (EXPO)
+    if (P.xidx)
+      for (uint32_t i = threadIdx.x; i < cap; i += kLdsBlock) lsc[i] = (int8_t)P.xhdr[i].scale;
   // the pool counter of the launch nsets ahead (it starts after this one ends)
   if (POOL && blockIdx.x == 0 && threadIdx.x == 0) *cold_params().pool_next = 0;
   etab[threadIdx.x] = 0;  // kErrTab == kLdsBlock
@@ -937,7 +942,27 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
             atomicMax(&xmax[f], d);
           }
         }
-        if (!P.span_rec && lane_off + toff + (uint32_t)j < lim) P.slot_of[lo + toff + lane_off + j] = f;
+        if (!P.span_rec && lane_off + toff + (uint32_t)j < lim) {
+          uint32_t w = f;
+          if (P.xidx) {  // the index record: the bucket index at the slot's starting scale
+            const unsigned long long d = dur[j];
+            if (f == kNotFound) {
+              w = kSpanRecNoSlot << kIxSlotShift;
+            } else if (d == 0) {
+              w = f << kIxSlotShift | kIxZero;
+            } else {
+              const int32_t sc = lsc[f];
+              int32_t ix;
+              if (expo_index_fast(d, P.l2d_fx, sc, ix) && ix >= kIxMin && ix <= kIxMax) {
+                w = ixrec_of(f, sc, ix);
+              } else {
+                w = f << kIxSlotShift | kIxLong;
+                P.span_long[lo + toff + lane_off + j] = d;
+              }
+            }
+          }
+          P.slot_of[lo + toff + lane_off + j] = w;
+        }
       }
       // the lane's span records: one 16-B store for its two spans (two 8-B
       // stores per lane cost the kernel ~24 us per 10 M spans)
