@@ -131,8 +131,8 @@ for step in "$@"; do
       (export SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so; export "$knob"; \
        run "labexpo_${knob//=/}" 300 python -u -m pytest tests/test_gpu_expo.py tests/test_gpu_churn.py -m gpu -x -v \
          --timeout 300 --timeout-method thread) || exit $? ;;
-    xrec_*) wl=${step#xrec_}  # exponential slab path: span records (1) / slots + times (0), laboratory build, rounds interleaved
-      for r in 1 2 3; do for x in 1 0; do
+    xrec_*) wl=${step#xrec_}  # exponential slab path: index records (2) / span records (1) / slots + times (0), laboratory build, rounds interleaved
+      for r in 1 2 3; do for x in 2 1 0; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_XREC=$x \
           run "xrec_${wl}_x${x}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $BQ
       done; done ;;
