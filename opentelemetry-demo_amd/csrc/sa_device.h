@@ -16,33 +16,37 @@ constexpr uint64_t XP5 = 0x27D4EB2F165667C5ULL;
 __device__ __forceinline__ uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
 
 // Fast path of the bucket index of a duration d > 0 ns at `scale`: log2 of the
-// value from d's exponent, v_log_f32 of its top 24 bits and log2(div), all
-// exact or nearly so -- |error| <= kFastLog2Err (the hardware log2 over every
-// float in [1, 2), measured exhaustively by test_gpu_expo.py's
-// test_fast_log2_error_bound, plus the 24-bit truncation of d).  When the
-// scaled value is farther than its error bound from an integer, its floor is
-// the index Go's math.Log computation gives (that one is within ~1e-9 of the
-// exact value at any scale <= 20); otherwise -- including every power of two
-// and every value near a bucket boundary -- false, and the caller takes the
-// exact path.
-// Integer arithmetic: z = log2(d / div) in 32.32 fixed point (l2d_fx =
-// log2(div) * 2^32 rounded, the hardware log2 of the mantissa converted with
-// its 32 fraction bits), so the scaled value's integer part is z's bits above
-// 32 - scale and its distance to an integer is read from the bits below (no
-// f64 ops: the counting kernel issues ~half the VALU work of the f64 form).
-// kFastFxErr: kFastLog2Err in those units plus the two conversions' 2^-32.
-constexpr double kFastLog2Err = 1.0 / (1 << 20) + 1.0 / (1 << 22);
-constexpr uint64_t kFastFxErr = (uint64_t)(kFastLog2Err * 4294967296.0) + 4;
-__device__ __forceinline__ bool expo_index_fast(uint64_t d, long long l2d_fx, int32_t scale, int32_t &idx) {
-  const int32_t e = 63 - (int32_t)__clzll((long long)d);
-  const uint32_t top = (uint32_t)((d << (63 - e)) >> 40);  // 24 bits, the leading one at bit 23
-  const float m = (float)top * 0x1p-23f;                    // exact, in [1, 2)
-  const uint32_t t = (uint32_t)(__builtin_amdgcn_logf(m) * 0x1p32f);  // log2(m) < 1, 32 fraction bits
-  const long long z = ((long long)e << 32) - l2d_fx + (long long)t;   // ~ log2(d / div) * 2^32
-  const int32_t sh = scale > 0 ? 32 - scale : 32;
-  const uint64_t one = 1ull << sh, f = (uint64_t)z & (one - 1);
-  if (f <= kFastFxErr || one - f <= kFastFxErr) return false;  // near a bucket boundary / power of two
-  const int32_t fl = (int32_t)(z >> sh);                        // floor of the scaled value
+// value from d's exponent, v_log_f32 of its leading 24 bits (as a mantissa in
+// [1, 2)) and log2(div), all exact or nearly so (the hardware log2 over every
+// float in [1, 2) is within 2^-20, measured exhaustively by test_gpu_expo.py's
+// test_fast_log2_error_bound; d's rounding to a float and the fixed-point
+// conversions add the rest of kFastFxErr).  When the scaled value is farther than its error bound from an
+// integer, its floor is the index Go's math.Log computation gives (that one is
+// within ~1e-9 of the exact value at any scale <= 20); otherwise -- including
+// every power of two and every value near a bucket boundary -- false, and the
+// caller takes the exact path.
+// 32-bit arithmetic only: z = log2(d / div) in 8.24 fixed point (l2d_q24 =
+// log2(div) * 2^24 rounded; d as a float, split by frexp; the mantissa's log2
+// converted with 24 fraction bits),
+// so the scaled value's integer part is z's bits above 24 - scale and its
+// distance to an integer is read from the bits below.  kFastFxErr, in units
+// of 2^-24: the hardware log2's 2^-20 (16), d as a float (|f / d - 1| <=
+// 2^-23: <= 2.9 in log2), the mantissa log's and log2(div)'s conversions
+// (< 1.5), rounded up with margin.
+constexpr int32_t kFastFxErr = 24;
+__device__ __forceinline__ bool expo_index_fast(uint64_t d, int32_t l2d_q24, int32_t scale, int32_t &idx) {
+  // d as a float: the high word exactly below 2^24 (else rounded), the low
+  // word rounded, one rounding of the sum -- |f / d - 1| <= 2^-23
+  const float f = __builtin_fmaf((float)(uint32_t)(d >> 32), 0x1p32f, (float)(uint32_t)d);
+  int32_t ef;
+  const float m = frexpf(f, &ef) * 2.0f;  // f = m * 2^(ef - 1), m in [1, 2)
+  const int32_t e = ef - 1;
+  const int32_t t = (int32_t)(__builtin_amdgcn_logf(m) * 0x1p24f);  // log2(m) < 1, 24 fraction bits
+  const int32_t z = (e << 24) - l2d_q24 + t;                         // ~ log2(d / div) * 2^24
+  const int32_t sh = scale > 0 ? 24 - scale : 24;
+  const int32_t one = 1 << sh, fr = z & (one - 1);
+  if (fr <= kFastFxErr || one - fr <= kFastFxErr) return false;  // near a bucket boundary / power of two
+  const int32_t fl = z >> sh;                                     // floor of the scaled value
   if (scale <= 0) {
     idx = fl >> (-scale);  // Go: exponent >> -scale (z is not an integer)
     return true;

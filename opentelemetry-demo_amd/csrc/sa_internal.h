@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdint>
 
 namespace sa {
@@ -117,7 +118,7 @@ struct IngestParams {
   // (xhdr[].scale, read in the prologue) -- and span_long the durations the
   // fast index path declined
   const ExpoHdr *xhdr;
-  long long l2d_fx;  // log2(div) * 2^32 rounded (expo_index_fast)
+  int32_t l2d_q24;  // log2(div) * 2^24 rounded (expo_index_fast)
   uint32_t xidx;
   XHdr *xslab;
   // Small-table kernels with the tail pool (POOL): every workgroup owns the
@@ -169,7 +170,7 @@ struct ExpoParams {
   uint32_t *buckets;  // [2][cap][max_size]
   uint32_t max_size;
   double div;         // 1e6 (ms) or 1e9 (s)
-  long long log2div_fx;  // log2(div) * 2^32 rounded, for the bucket index's fast path
+  int32_t log2div_q24;  // log2(div) * 2^24 rounded, for the bucket index's fast path
   uint32_t diag;      // ablation bits (SPANAGG_XC_DIAG, profiling only; results wrong when set):
                       // 1 no HBM bucket atomics, 2 no LDS cache, 4 exact index path only, 8 no index
   uint32_t *slot_of;  // [n] key slot of each span (pass 1 / the small-table ingest kernel -> counting)
@@ -217,6 +218,8 @@ constexpr uint32_t kIxLong = 1u, kIxZero = 3u;  // flag | index field 0 / 1
 __host__ __device__ inline uint32_t ixrec_of(uint32_t slot, int32_t scale, int32_t ix) {
   return slot << kIxSlotShift | (uint32_t)(scale + (int32_t)kIxScaleBias) << kIxScaleShift | ((uint32_t)ix & 0x3FFFu) << 1;
 }
+// log2(div) in the fast bucket index's 8.24 fixed point (expo_index_fast)
+__host__ inline int32_t expo_l2d_q24(double div) { return (int32_t)std::llround(std::log2(div) * 16777216.0); }
 constexpr uint32_t kXtCap = 4096;       // tail records per counting workgroup (16 KiB of LDS)
 constexpr uint32_t kXtBinSlots = 8;     // slots per tail fold bin
 __host__ __device__ inline uint32_t xt_bins(uint64_t cap) { return (uint32_t)((cap + kXtBinSlots - 1) / kXtBinSlots); }

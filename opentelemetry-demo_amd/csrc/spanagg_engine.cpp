@@ -833,7 +833,7 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b, uint32_t
   E.buckets = e->expo_buckets;
   E.max_size = e->cfg.exp_max_size;
   E.div = e->cfg.unit == SA_UNIT_S ? 1e9 : 1e6;
-  E.log2div_fx = std::llround(std::log2(E.div) * 4294967296.0);
+  E.log2div_q24 = sa::expo_l2d_q24(E.div);
   {
     static const uint32_t diag = [] {
       const char *v = ab_env("SPANAGG_XC_DIAG");
@@ -1037,7 +1037,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
         if (mode == 2) {
           P.xidx = 1;
           P.xhdr = e->expo_hdr;
-          P.l2d_fx = std::llround(std::log2(e->cfg.unit == SA_UNIT_S ? 1e9 : 1e6) * 4294967296.0);
+          P.l2d_q24 = sa::expo_l2d_q24(e->cfg.unit == SA_UNIT_S ? 1e9 : 1e6);
           P.span_long = reinterpret_cast<unsigned long long *>(slots) + e->expo_slot_cap;
         }
       }

@@ -79,7 +79,6 @@ __device__ __forceinline__ double expo_value(uint64_t d_ns, double div) {
 
 // (the fast bucket index, expo_index_fast, is in sa_device.h: the ingest
 // kernel computes it too)
-__host__ inline long long expo_l2d_fx(double div) { return std::llround(std::log2(div) * 4294967296.0); }
 
 constexpr int32_t kExpoMaxScale = 20, kExpoMinScale = -10;
 constexpr int32_t kExpoEmpty = 0x7FFFFFFF;  // ExpoHdr.lo when no positive value is kept
@@ -419,7 +418,7 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
     const int2 m = meta[slot];
     const int32_t sc = (int32_t)(int8_t)(m.x & 0xFF);
     int32_t ix;
-    if (!expo_index_fast(d, E.log2div_fx, sc, ix)) ix = expo_index(expo_value(d, E.div), sc);
+    if (!expo_index_fast(d, E.log2div_q24, sc, ix)) ix = expo_index(expo_value(d, E.div), sc);
     add(slot, ix, m);
   };
   // one index record (ixrec_of): the index at the scale the ingest kernel
@@ -661,7 +660,7 @@ __global__ __launch_bounds__(kXcBlock) void expo_count_cached_kernel(ExpoParams 
     const int2 m = meta[slot];
     int32_t ix;
     if (E.diag & 8u) ix = (int32_t)(d & 127u);
-    else if ((E.diag & 4u) || !expo_index_fast(d, E.log2div_fx, m.x, ix)) ix = expo_index(expo_value(d, E.div), m.x);
+    else if ((E.diag & 4u) || !expo_index_fast(d, E.log2div_q24, m.x, ix)) ix = expo_index(expo_value(d, E.div), m.x);
     const uint32_t at = expo_mod(ix, M);
     uint32_t e = (((slot * 0x9E3779B1u) >> 16) & (NE / 4 - 1)) * 4, hit = kNotFound;  // home group of 4
 #pragma unroll
@@ -890,18 +889,18 @@ __global__ __launch_bounds__(256) void log2_err_probe_kernel(uint32_t i0, uint32
 }
 
 __global__ __launch_bounds__(256) void expo_fast_probe_kernel(const uint64_t *d, const int32_t *scale, uint64_t n,
-                                                             double div, long long l2d_fx, int32_t *fast,
+                                                             double div, int32_t l2d_q24, int32_t *fast,
                                                              int32_t *exact) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
     int32_t ix;
-    fast[i] = expo_index_fast(d[i], l2d_fx, scale[i], ix) ? ix : INT32_MIN;
+    fast[i] = expo_index_fast(d[i], l2d_q24, scale[i], ix) ? ix : INT32_MIN;
     exact[i] = expo_index(expo_value(d[i], div), scale[i]);
   }
 }
 
 hipError_t launch_expo_fast_probe(const uint64_t *d, const int32_t *scale, uint64_t n, double div, int32_t *fast,
                                   int32_t *exact, hipStream_t s) {
-  hipLaunchKernelGGL(expo_fast_probe_kernel, dim3(grid_of(n)), dim3(256), 0, s, d, scale, n, div, expo_l2d_fx(div), fast,
+  hipLaunchKernelGGL(expo_fast_probe_kernel, dim3(grid_of(n)), dim3(256), 0, s, d, scale, n, div, expo_l2d_q24(div), fast,
                      exact);
   return hipGetLastError();
 }

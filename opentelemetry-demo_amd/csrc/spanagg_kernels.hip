@@ -629,6 +629,15 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   }
   uint4 bv = make_uint4(0, 0, 0, 0);
   if (!EXPO && threadIdx.x < kBins * 2) bv = reinterpret_cast<const uint4 *>(P.bintab)[threadIdx.x];  // (EXPO: no buckets)
+  // EXPO with index records: the slots' scales (cap <= 2,048: two per thread),
+  // issued with the key table so the LDS setup waits for them and not for the
+  // first tiles
+  int32_t xsc[2] = {0, 0};
+  if constexpr (EXPO)
+    if (P.xidx)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (threadIdx.x + u * kLdsBlock < cap) xsc[u] = P.xhdr[threadIdx.x + u * kLdsBlock].scale;
   uint32_t lbw = 0;
   if (lb_on && threadIdx.x * 4 < P.lb_n) lbw = *reinterpret_cast<const uint32_t *>(P.hll_lb + threadIdx.x * 4);
   if constexpr (DYN && (OPT & 1)) {
@@ -675,7 +684,9 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   if (POOL && threadIdx.x < kPoolMaxSteal) pmap[threadIdx.x] = 0;
   if constexpr (EXPO)
     if (P.xidx)
-      for (uint32_t i = threadIdx.x; i < cap; i += kLdsBlock) lsc[i] = (int8_t)P.xhdr[i].scale;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (threadIdx.x + u * kLdsBlock < cap) lsc[threadIdx.x + u * kLdsBlock] = (int8_t)xsc[u];
   // the pool counter of the launch nsets ahead (it starts after this one ends)
   if (POOL && blockIdx.x == 0 && threadIdx.x == 0) *cold_params().pool_next = 0;
   etab[threadIdx.x] = 0;  // kErrTab == kLdsBlock
@@ -953,7 +964,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
             } else {
               const int32_t sc = lsc[f];
               int32_t ix;
-              if (expo_index_fast(d, P.l2d_fx, sc, ix) && ix >= kIxMin && ix <= kIxMax) {
+              if (expo_index_fast(d, P.l2d_q24, sc, ix) && ix >= kIxMin && ix <= kIxMax) {
                 w = ixrec_of(f, sc, ix);
               } else {
                 w = f << kIxSlotShift | kIxLong;
@@ -1915,17 +1926,23 @@ hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_
   return hipLaunchKernel(fn, dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);
 }
 
-static const void *expo_small_fn() {
-  return (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true, 1, true, true, true>;
+// the EXPO kernel: specialised for the default small table (2,048 slots, HLL
+// p = 14: C2's geometry) like variant 20, generic otherwise
+static const void *expo_small_fn(bool spec) {
+  return spec ? (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 0, 14, -1, true, 1, true, true, true>
+              : (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true, 1, true, true, true>;
 }
 
 hipError_t prepare_ingest_expo_small(size_t lds_bytes) {
-  return hipFuncSetAttribute(expo_small_fn(), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+  for (bool spec : {false, true})
+    if (hipError_t e = hipFuncSetAttribute(expo_small_fn(spec), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+        e != hipSuccess)
+      return e;
+  return hipSuccess;
 }
-
 hipError_t launch_ingest_expo_small(const IngestParams &P, uint32_t grid, size_t lds_bytes, hipStream_t s) {
   void *args[] = {const_cast<IngestParams *>(&P)};
-  return hipLaunchKernel(expo_small_fn(), dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);
+  return hipLaunchKernel(expo_small_fn(P.log2cap == 11 && P.p == 14), dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);
 }
 
 hipError_t launch_ingest_part(const IngestParams &P, hipStream_t s) {

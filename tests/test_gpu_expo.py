@@ -58,11 +58,12 @@ def test_gpu_log_and_index_bit_exact():
 
 
 def test_fast_log2_error_bound():
-    """The counting kernel's fast path assumes |v_log_f32(m) - log2(m)| <=
-    2^-20 over every float m in [1, 2) (kFastLog2Err in spanagg_expo.hip adds
-    the 24-bit truncation of the duration): measured here exhaustively on the
-    device, so a part whose hardware log2 were less accurate fails this test
-    instead of mis-bucketing near bucket boundaries."""
+    """The fast bucket index (expo_index_fast, sa_device.h) assumes
+    |v_log_f32(m) - log2(m)| <= 2^-20 over every float m in [1, 2) (its
+    kFastFxErr adds the duration's rounding to a float and the fixed-point
+    conversions): measured here exhaustively on the device, so a part whose
+    hardware log2 were less accurate fails this test instead of mis-bucketing
+    near bucket boundaries."""
     with Engine(Config(exp_max_size=160)) as e:
         _, _, err = e.expo_fast_probe([], [])
     assert 0 < err <= 2.0 ** -20, err
