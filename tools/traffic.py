@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """profiles/traffic[_<wl>].json from the rocprofv3 FETCH_SIZE / WRITE_SIZE
 passes of tools/gpu_job.sh (pmc_<wl>_fetch, pmc_<wl>_write over
-tools/prof_driver.py): per ingest launch -- the mean over launches (first
-dropped) of each hot-path kernel, summed over the kernels of one launch (C2:
-ingest_v2_kernel; C4: bt_scatter2 + bt_aggregate3;
-c2expo: ingest_v2 + the expo_* kernels of a launch) -- FETCH_SIZE doubled per
+tools/prof_driver.py): per ingest launch -- every hot-path kernel's bytes
+from the first averaged launch on (the last PMC_LAST launches, else all but
+the first), divided by those launches (C2: ingest_v2_kernel; C4: bt_scatter2
++ bt_aggregate3, whose paired dispatches cover two launches; c2expo:
+ingest_v2 + the expo_* kernels) -- FETCH_SIZE doubled per
 MI355X_MICROARCH.md's gfx950 correction, KB = 1024 B.
 
   python tools/traffic.py <job dir> <workload> <round> <out.json>"""
@@ -25,17 +26,27 @@ def _pick(ids):
 HOT = ("ingest", "bt_scatter", "bt_aggregate", "expo_")
 
 
+PRIMARY = ("ingest", "bt_scatter")  # one dispatch per ingest launch
+
+
 def per_launch(path, counter):
+    """Bytes per ingest launch: every hot kernel's counter summed over the
+    dispatches from the first picked launch on, divided by the number of
+    picked launches (a binned aggregate that covers two launches' records --
+    the paired aggregates -- is counted once, not once per launch)."""
     d = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
         if r["Counter_Name"] == counter and any(h in name for h in HOT):
-            short = next(h for h in HOT if h in name) + name[name.index(next(h for h in HOT if h in name)):].split("(")[0][len(next(h for h in HOT if h in name)):]
+            h = next(h for h in HOT if h in name)
+            short = h + name[name.index(h):].split("(")[0][len(h):]
             d[short][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+    prim = sorted(i for name, per in d.items() if any(name.startswith(p) for p in PRIMARY) for i in per)
+    launches = _pick(prim)
+    first = launches[0]
     total, kernels = 0.0, {}
     for name, per in d.items():
-        ids = _pick(sorted(per))
-        kernels[name] = sum(per[i] for i in ids) / len(ids)
+        kernels[name] = sum(v for i, v in per.items() if i >= first) / len(launches)
         total += kernels[name]
     return total, kernels
 
