@@ -643,7 +643,7 @@ struct Columnizer::Worker {
   SigCache cache;
   std::vector<Attr> rattrs, sattrs, eattrs;
   std::vector<const Attr *> hv;
-  std::string tmp, keystr, sname, service, evkey;
+  std::string tmp, keystr, sname, service, evkey, sigbuf;
   std::vector<uint8_t> hbuf;
   std::vector<std::pair<const uint8_t *, const uint8_t *>> evs;  // the span's Event messages
   std::unordered_map<uint64_t, uint32_t> exl;                     // this request's exemplar candidates per series
@@ -794,8 +794,12 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
   std::string &tmp = w.tmp, &keystr = w.keystr, &sname = w.sname, &service = w.service;
   auto &hbuf = w.hbuf;
   // the signature cache skips building the key string (a span with events
-  // builds it anyway, for the event keys)
-  const bool use_cache = opt_.dims.empty();
+  // builds it anyway, for the event keys).  With dimensions the signature's
+  // name is the span name followed by each dimension's string value (span
+  // attribute, else resource attribute) or a marker for "absent": the key is
+  // a function of exactly these, the service and the resource identity (a
+  // non-string value takes the full path)
+  const bool dims = !opt_.dims.empty();
   w.exl.clear();
   PB req(buf, buf + len);
   uint32_t f;
@@ -877,6 +881,8 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
     }
     auto &keys = rit->second;
     res.resources.push_back(rhash);
+    const int64_t res_off = has_resource ? (int64_t)(resource.p - buf) : -1;
+    const uint32_t res_len = has_resource ? (uint32_t)(resource.end - resource.p) : 0u;
     // a new series id for `key` of this resource (exclusive calls only): seed
     // 0, 1, ... until the id is neither 0 (reserved) nor another series'
     auto intern = [&](const std::string &key) -> uint64_t {
@@ -984,9 +990,33 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
         uint64_t sid;
         uint64_t sig = 0;
         SigCache::Entry *hit = nullptr;
+        std::string_view signame = name;
+        bool use_cache = true;
+        if (dims) {
+          std::string &sb = w.sigbuf;
+          sb.assign(name);
+          for (const Dim &d : opt_.dims) {
+            const Any *v = find_attr(sattrs, d.name);
+            char tag = '\x02';
+            if (!v) v = find_attr(rattrs, d.name), tag = '\x04';
+            if (!v) {
+              sb += '\x03';
+              continue;
+            }
+            if (v->type != kStr) {
+              use_cache = false;
+              break;
+            }
+            const uint32_t n = (uint32_t)v->s.size();
+            sb += tag;
+            sb.append(reinterpret_cast<const char *>(&n), 4);
+            sb.append(v->s);
+          }
+          signame = sb;
+        }
         if (use_cache) {
-          sig = SigCache::hash(rhash, svc_id, name, kind, code);
-          hit = cache.find(sig, rhash, svc_id, name, kind, code);
+          sig = SigCache::hash(rhash, svc_id, signame, kind, code);
+          hit = cache.find(sig, rhash, svc_id, signame, kind, code);
         }
         // key = buildKey, into keystr (0 = built; else the failure to return)
         auto build_key = [&]() -> int {
@@ -1047,16 +1077,17 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
               } else {
                 sid = intern(kOverflowKey);
                 res.new_series.push_back(
-                    {sid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});
+                    {sid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin), res_off, res_len});
               }
             } else {
               sid = intern(keystr);
               res.new_series.push_back(
-                  {sid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin)});
+                  {sid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin), res_off, res_len});
             }
           }
           // (an overflowed key is decided again each time: the count it met may change)
-          if (use_cache && !overflow) cache.insert(sig, rhash, svc_id, name, kind, code, sid, opt_.events ? keystr : kNoKey);
+          if (use_cache && !overflow)
+            cache.insert(sig, rhash, svc_id, signame, kind, code, sid, opt_.events ? keystr : kNoKey);
         }
         // candidates; accept_exemplars keeps the interval's first ones.  A
         // series seen full this interval is marked in its signature-cache
@@ -1132,7 +1163,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
             if constexpr (kShared) return false;
             esid = intern(ek);
             res.new_event_series.push_back(
-                {esid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin), ei});
+                {esid, rhash, (uint32_t)(span_begin - buf), (uint32_t)(span_end - span_begin), ei, res_off, res_len});
           }
           out.push(esid, 0, 0, 0, 0, 0xFFFFu);
           ++res.event_records;

@@ -71,6 +71,8 @@ struct Options {
 struct NewSeries {
   uint64_t sid, res_hash;
   uint32_t span_off, span_len;  // the Span message inside the request bytes
+  int64_t res_off = -1;         // its Resource message (-1: absent); the host keys
+  uint32_t res_len = 0;         // dimensions with this resource's own attributes
 };
 
 // An exemplar candidate / a new event series: the span (offsets in the
@@ -87,6 +89,8 @@ struct SpanRef {
 struct NewEventSeries {
   uint64_t sid, res_hash;
   uint32_t span_off, span_len, event;
+  int64_t res_off = -1;  // as NewSeries
+  uint32_t res_len = 0;
 };
 
 struct NewResource {

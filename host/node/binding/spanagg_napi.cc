@@ -791,6 +791,8 @@ napi_value result_obj(napi_env env, const otlpcol::Result &r, bool lean) {
       set(env, e, "resHash", big(env, r.new_series[i].res_hash));
       set(env, e, "off", num(env, r.new_series[i].span_off));
       set(env, e, "len", num(env, r.new_series[i].span_len));
+      set(env, e, "resOff", num(env, (double)r.new_series[i].res_off));
+      set(env, e, "resLen", num(env, r.new_series[i].res_len));
       napi_set_element(env, arr, (uint32_t)i, e);
     }
     set(env, o, "newSeries", arr);
@@ -832,6 +834,8 @@ napi_value result_obj(napi_env env, const otlpcol::Result &r, bool lean) {
       set(env, e, "off", num(env, r.new_event_series[i].span_off));
       set(env, e, "len", num(env, r.new_event_series[i].span_len));
       set(env, e, "event", num(env, r.new_event_series[i].event));
+      set(env, e, "resOff", num(env, (double)r.new_event_series[i].res_off));
+      set(env, e, "resLen", num(env, r.new_event_series[i].res_len));
       napi_set_element(env, arr, (uint32_t)i, e);
     }
     set(env, o, "newEventSeries", arr);

@@ -277,6 +277,19 @@ class SpanMetricsConnector {
         sids: [], nSpanSeries: 0, nByKind: {} });
   }
 
+  /**
+   * The attributes of the resource a natively keyed span came from: its own
+   * Resource message when dimensions are configured (resources that share a
+   * resource hash -- resource_metrics_key_attributes -- can differ in the
+   * attributes a dimension reads, as the JavaScript path keys them), else the
+   * resource entry's.
+   */
+  _spanResourceAttrs(bytes, rec, res) {
+    if (!this.cfg.dims.length || rec.resOff === undefined) return res.attributes;
+    if (rec.resOff < 0) return new Map();
+    return keys.attrMap(otlp.decodeResource(new otlp.Reader(bytes, rec.resOff, rec.resOff + rec.resLen)).attributes);
+  }
+
   /** LRU hit (or revival from the evicted side map) by resource hash; undefined on a miss. */
   _touchResource(h) {
     let r = this.resources.get(h);
@@ -583,10 +596,11 @@ class SpanMetricsConnector {
       const svc = res.attributes.get(keys.SERVICE_NAME_KEY);
       const service = svc && svc.type === 'string' ? svc.value : '';
       const spanAttrs = this.cfg.dims.length ? keys.attrMap(span.attributes) : undefined;
+      const resAttrs = this._spanResourceAttrs(bytes, ns, res);
       this._verifyingNative = true;
       let sid;
       try {
-        sid = this._seriesId(res, service, span, res.attributes, spanAttrs);
+        sid = this._seriesId(res, service, span, resAttrs, spanAttrs);
       } finally {
         this._verifyingNative = false;
       }
@@ -606,10 +620,11 @@ class SpanMetricsConnector {
       const svc = res.attributes.get(keys.SERVICE_NAME_KEY);
       const service = svc && svc.type === 'string' ? svc.value : '';
       const spanAttrs = this.cfg.dims.length ? keys.attrMap(span.attributes) : undefined;
+      const resAttrs = this._spanResourceAttrs(bytes, ne, res);
       this._verifyingNative = true;
       let sid;
       try {
-        sid = this._eventId(res, service, span, res.attributes, spanAttrs, span.events[ne.event]);
+        sid = this._eventId(res, service, span, resAttrs, spanAttrs, span.events[ne.event]);
       } finally {
         this._verifyingNative = false;
       }

@@ -5,7 +5,7 @@
 // N-API or the engine).  Prints one JSON line with the rate and the time in
 // each columnize_batch phase.  A profiling tool, not part of the addon.
 //
-//   colbench FILE [--threads T] [--batch B] [--reps R] [--exemplars] [--events]
+//   colbench FILE [--threads T] [--batch B] [--reps R] [--exemplars] [--events] [--dim NAME]...
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -19,11 +19,12 @@
 
 int main(int argc, char **argv) {
   if (argc < 2) {
-    std::fprintf(stderr, "usage: colbench FILE [--threads T] [--batch B] [--reps R] [--exemplars] [--events]\n");
+    std::fprintf(stderr, "usage: colbench FILE [--threads T] [--batch B] [--reps R] [--exemplars] [--events] [--dim NAME]...\n");
     return 2;
   }
   unsigned threads = 1, batch = 128, reps = 5;
   bool exemplars = false, events = false;
+  std::vector<std::string> dims;
   for (int i = 2; i < argc; ++i) {
     const std::string a = argv[i];
     if (a == "--threads" && i + 1 < argc) threads = (unsigned)std::atoi(argv[++i]);
@@ -31,6 +32,7 @@ int main(int argc, char **argv) {
     else if (a == "--reps" && i + 1 < argc) reps = (unsigned)std::atoi(argv[++i]);
     else if (a == "--exemplars") exemplars = true;
     else if (a == "--events") events = true;
+    else if (a == "--dim" && i + 1 < argc) dims.push_back(argv[++i]);  // a dimension (no default)
   }
   std::ifstream f(argv[1], std::ios::binary);
   const std::vector<uint8_t> raw((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
@@ -52,6 +54,7 @@ int main(int argc, char **argv) {
   o.exemplars = exemplars;
   o.events = events;
   if (events) o.event_dims.push_back({"exception.type", false, ""});
+  for (const std::string &d : dims) o.dims.push_back({d, false, ""});
   otlpcol::Columnizer col(o);
   using clk = std::chrono::steady_clock;
   double best = 1e30, dec = 0, com = 0, pla = 0;

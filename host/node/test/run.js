@@ -598,6 +598,10 @@ test('native columnizer: cardinality limit, exemplars and events == the JavaScri
     [{ aggregation_cardinality_limit: 4, dimensions: [{ name: 'k8s.pod.name' }] }, DEMO_SPAN_NAME_RULES],
     [{ events: { enabled: true, dimensions: [{ name: 'exception.type' }] },
       aggregation_cardinality_limit: 4 }, DEMO_SPAN_NAME_RULES],
+    // a resource-level dimension with resource identity on service.name only:
+    // the signature cache must key on the pod, not on the resource hash
+    [{ dimensions: [{ name: 'k8s.pod.name' }, { name: 'http.status_code' }],
+      resource_metrics_key_attributes: ['service.name'] }, DEMO_SPAN_NAME_RULES],
     [{ events: { enabled: true, dimensions: [{ name: 'exception.type' }] }, exemplars: { enabled: true, max_per_data_point: 3 },
       aggregation_cardinality_limit: 4, dimensions: [{ name: 'k8s.pod.name' }] }, DEMO_SPAN_NAME_RULES],
   ]) {

@@ -75,6 +75,9 @@ for step in "$@"; do
         node test/host_rate.js 2000000 --events --dump /tmp/req_ev.bin > /dev/null) || exit 1
       for t in ${COL_THREADS:-1 4 8 16}; do run "colbench_t$t" 120 host/node/build/colbench /tmp/req_plain.bin --threads "$t"; done
       run colbench_ex_t16 120 host/node/build/colbench /tmp/req_ev.bin --threads 16 --exemplars --events ;;
+    colabhc) (cd host/node && node test/host_rate.js 2000000 --highcard --dump /tmp/req_hc.bin > /dev/null) || exit 1  # C4 vocabulary, http.route dimension
+      for r in 1 2 3; do for b in colbench ${COL_OTHER:-colbench_olddim}; do
+        run "colabhc_${b}_r$r" 120 host/node/build/$b /tmp/req_hc.bin --threads 16 --dim http.route; done; done ;;
     colab) (cd host/node && node test/host_rate.js 2000000 --dump /tmp/req_plain.bin > /dev/null) || exit 1  # colbench against build/colbench_<other>
       for r in 1 2 3; do for t in 16 8; do for b in colbench ${COL_OTHER:-colbench_condvar}; do
         run "colab_${b}_t${t}_r$r" 120 host/node/build/$b /tmp/req_plain.bin --threads "$t"; done; done; done ;;
