@@ -608,34 +608,44 @@ uint64_t SigCache::hash(uint64_t rhash, uint32_t svc, std::string_view name, int
 
 SigCache::Entry *SigCache::find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
                                 int32_t code) {
-  if (t_.empty()) return nullptr;
-  const size_t mask = t_.size() - 1;
+  if (slots_.empty()) return nullptr;
+  const size_t mask = slots_.size() - 1;
   for (size_t i = h & mask;; i = (i + 1) & mask) {
-    Entry &e = t_[i];
-    if (!e.used) return nullptr;
-    if (e.h == h && e.rhash == rhash && e.svc == svc && e.kind == kind && e.code == code && e.name == name)
+    const Slot &sl = slots_[i];
+    if (!sl.h) return nullptr;
+    if (sl.h != h) continue;
+    Entry &e = entries_[sl.idx];
+    if (e.rhash == rhash && e.svc == svc && e.kind == kind && e.code == code && e.name_len == name.size() &&
+        std::memcmp(names_.data() + e.name_off, name.data(), name.size()) == 0)
       return &e;
   }
 }
 
 void SigCache::insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
                       int32_t code, uint64_t sid, const std::string &key) {
-  if (2 * (n_ + 1) > t_.size()) {  // load <= 1/2
-    std::vector<Entry> old;
-    old.swap(t_);
-    t_.resize(old.empty() ? 256 : old.size() * 2);
-    n_ = 0;
-    for (Entry &e : old)
-      if (e.used) insert(e.h, e.rhash, e.svc, e.name, e.kind, e.code, e.sid, e.key);
+  if (2 * (entries_.size() + 1) > slots_.size()) {  // load <= 1/2: rebuild the slots from the entries
+    std::vector<Slot> old;
+    old.swap(slots_);
+    slots_.resize(old.empty() ? 256 : old.size() * 2);
+    const size_t mask = slots_.size() - 1;
+    for (const Slot &o : old) {
+      if (!o.h) continue;
+      size_t i = o.h & mask;
+      while (slots_[i].h) i = (i + 1) & mask;
+      slots_[i] = o;
+    }
   }
-  const size_t mask = t_.size() - 1;
+  const size_t mask = slots_.size() - 1;
   size_t i = h & mask;
-  while (t_[i].used) i = (i + 1) & mask;
-  Entry &e = t_[i];
-  e.h = h, e.rhash = rhash, e.sid = sid, e.svc = svc, e.kind = kind, e.code = code, e.used = true, e.ex_full = 0;
-  e.name.assign(name);
+  while (slots_[i].h) i = (i + 1) & mask;
+  slots_[i].h = h;  // (never 0: hash() sets bit 0)
+  slots_[i].idx = (uint32_t)entries_.size();
+  Entry e;
+  e.rhash = rhash, e.sid = sid, e.svc = svc, e.kind = kind, e.code = code;
+  e.name_off = (uint32_t)names_.size(), e.name_len = (uint32_t)name.size();
+  names_.append(name);
   e.key = key;
-  ++n_;
+  entries_.push_back(std::move(e));
 }
 
 struct Columnizer::Worker {

@@ -182,22 +182,29 @@ class SigCache {
   // keys extend it), empty otherwise
   void insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code,
               uint64_t sid, const std::string &key);
-  void clear() { t_.clear(), n_ = 0; }
+  void clear() { slots_.clear(), entries_.clear(), names_.clear(); }
   uint64_t gen = 0;  // the dictionary generation the entries belong to
 
   struct Entry {
-    uint64_t h = 0, rhash = 0, sid = 0;
+    uint64_t rhash = 0, sid = 0;
     uint64_t ex_full = 0;  // the exemplar interval (Columnizer::ex_gen_) in which the series was seen full
     uint32_t svc = 0;
     int32_t kind = 0, code = 0;
-    bool used = false;
-    std::string name;
-    std::string key;  // events.enabled: the span key string (see insert)
+    uint32_t name_off = 0, name_len = 0;  // the signature name in names_
+    std::string key;                      // events.enabled: the span key string (see insert)
   };
 
  private:
-  std::vector<Entry> t_;
-  size_t n_ = 0;
+  // open addressing over 16-B slots (the full hash and the entry), so a probe
+  // touches one line and only a hash match reads the entry and its name (a
+  // high-cardinality stream's table is larger than the caches)
+  struct Slot {
+    uint64_t h = 0;  // 0: free
+    uint32_t idx = 0, pad = 0;
+  };
+  std::vector<Slot> slots_;
+  std::vector<Entry> entries_;
+  std::string names_;
 };
 
 class Columnizer {
