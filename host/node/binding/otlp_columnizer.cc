@@ -607,17 +607,17 @@ uint64_t SigCache::hash(uint64_t rhash, uint32_t svc, std::string_view name, int
 }
 
 SigCache::Entry *SigCache::find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
-                                int32_t code) {
+                                int32_t code) const {
   if (slots_.empty()) return nullptr;
   const size_t mask = slots_.size() - 1;
   for (size_t i = h & mask;; i = (i + 1) & mask) {
     const Slot &sl = slots_[i];
     if (!sl.h) return nullptr;
     if (sl.h != h) continue;
-    Entry &e = entries_[sl.idx];
+    const Entry &e = entries_[sl.idx];
     if (e.rhash == rhash && e.svc == svc && e.kind == kind && e.code == code && e.name_len == name.size() &&
         std::memcmp(names_.data() + e.name_off, name.data(), name.size()) == 0)
-      return &e;
+      return const_cast<Entry *>(&e);
   }
 }
 
@@ -640,8 +640,9 @@ void SigCache::insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view
   while (slots_[i].h) i = (i + 1) & mask;
   slots_[i].h = h;  // (never 0: hash() sets bit 0)
   slots_[i].idx = (uint32_t)entries_.size();
+  fresh_.push_back((uint32_t)entries_.size());
   Entry e;
-  e.rhash = rhash, e.sid = sid, e.svc = svc, e.kind = kind, e.code = code;
+  e.h = h, e.rhash = rhash, e.sid = sid, e.svc = svc, e.kind = kind, e.code = code;
   e.name_off = (uint32_t)names_.size(), e.name_len = (uint32_t)name.size();
   names_.append(name);
   e.key = key;
@@ -794,7 +795,8 @@ void Columnizer::remap(uint64_t from, uint64_t to) {
 // redone exclusively).  Exclusive: new entries go into the dictionaries and
 // `undo`; false = res.status / res.error say why (the caller rolls back).
 template <bool kShared>
-bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCache &cache, Result &res,
+bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCache &cache, const SigCache *l2,
+                     Result &res,
                      Undo *undo) {
   auto fail = [&](Result::Status st, const char *why) {
     if constexpr (!kShared) res.status = st, res.error = why;
@@ -1024,9 +1026,11 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
           }
           signame = sb;
         }
+        bool l2_hit = false;  // (an entry of the shared cache is read only here)
         if (use_cache) {
           sig = SigCache::hash(rhash, svc_id, signame, kind, code);
           hit = cache.find(sig, rhash, svc_id, signame, kind, code);
+          if (!hit && l2 && (hit = l2->find(sig, rhash, svc_id, signame, kind, code))) l2_hit = true;
         }
         // key = buildKey, into keystr (0 = built; else the failure to return)
         auto build_key = [&]() -> int {
@@ -1119,7 +1123,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
               res.exemplars.push_back(x);
             }
           } else if (hit) {
-            hit->ex_full = ex_gen_;
+            if (!l2_hit) hit->ex_full = ex_gen_;
           }
         }
         if (en > out.max_end) out.max_end = en;
@@ -1189,6 +1193,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
 
 Result Columnizer::columnize(const uint8_t *buf, size_t len) {
   Result r = columnize_into(buf, len, buf_);
+  cache_.drop_fresh();  // (one thread: no shared cache to fill)
   accept_exemplars(r);
   return r;
 }
@@ -1199,7 +1204,7 @@ Result Columnizer::columnize_into(const uint8_t *buf, size_t len, Cols &out) {
   Undo undo;
   const size_t n0 = out.size();
   const uint64_t max0 = out.max_end;
-  if (run<false>(buf, len, *main_, out, cache_, res, &undo)) return res;
+  if (run<false>(buf, len, *main_, out, cache_, &shared_, res, &undo)) return res;
   // all or nothing: drop this call's columns and dictionary entries
   out.truncate(n0);
   out.max_end = max0;
@@ -1245,9 +1250,13 @@ BatchResult Columnizer::columnize_batch(const uint8_t *const *bufs, const size_t
   std::vector<Slot> slots(n);
   while (workers_.size() < opt_.threads) workers_.emplace_back(new Worker);
   if (!pool_) pool_.reset(new Pool(opt_.threads));
+  // the threads' own caches stay small (a high-cardinality stream would give
+  // every thread a copy of every series); the shared one holds them all
+  constexpr size_t kOwnCacheMax = 1u << 15;
+  if (shared_.gen != gen_) shared_.clear(), shared_.gen = gen_;
   for (auto &w : workers_) {
     w->cols.clear();
-    if (w->cache.gen != gen_) w->cache.clear(), w->cache.gen = gen_;
+    if (w->cache.gen != gen_ || w->cache.size() > kOwnCacheMax) w->cache.clear(), w->cache.gen = gen_;
   }
   using clk = std::chrono::steady_clock;
   const auto ns_since = [](clk::time_point t) {
@@ -1264,7 +1273,7 @@ BatchResult Columnizer::columnize_batch(const uint8_t *const *bufs, const size_t
       s.off = w.cols.size();
       w.cols.max_end = 0;
       try {
-        s.ok = run<true>(bufs[i], lens[i], w, w.cols, w.cache, s.r, nullptr);
+        s.ok = run<true>(bufs[i], lens[i], w, w.cols, w.cache, &shared_, s.r, nullptr);
       } catch (...) {  // e.g. bad_alloc: redone (and reported) on the caller's thread
         s.ok = false;
       }
@@ -1324,6 +1333,14 @@ BatchResult Columnizer::columnize_batch(const uint8_t *const *bufs, const size_t
   };
   pool_->run(T, place);
   br.ns_place = ns_since(t_ph);
+  // the signatures the threads resolved this batch -> the shared cache
+  const auto merge = [&](const SigCache::Entry &e, std::string_view name) {
+    if (!shared_.find(e.h, e.rhash, e.svc, name, e.kind, e.code))
+      shared_.insert(e.h, e.rhash, e.svc, name, e.kind, e.code, e.sid, e.key);
+  };
+  for (auto &w : workers_) w->cache.take_fresh(merge);
+  if (cache_.gen == gen_) cache_.take_fresh(merge);  // (the requests redone on this thread)
+  shared_.drop_fresh();
   br.results.reserve(taken);
   for (size_t i = 0; i < taken; ++i) br.results.push_back(std::move(slots[i].r));
   br.done = taken;

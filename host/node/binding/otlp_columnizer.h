@@ -177,16 +177,27 @@ class SigCache {
  public:
   static uint64_t hash(uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code);
   struct Entry;
-  Entry *find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code);
+  Entry *find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code) const;
   // key: the span's key string, kept for events.enabled (its spans' event
   // keys extend it), empty otherwise
   void insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code,
               uint64_t sid, const std::string &key);
-  void clear() { slots_.clear(), entries_.clear(), names_.clear(); }
+  void clear() { slots_.clear(), entries_.clear(), names_.clear(), fresh_.clear(); }
+  size_t size() const { return entries_.size(); }
   uint64_t gen = 0;  // the dictionary generation the entries belong to
+  // entries inserted since the last take_fresh (a worker's, merged into the
+  // shared cache after each batch)
+  template <typename F> void take_fresh(F &&f) {
+    for (uint32_t i : fresh_) {
+      const Entry &e = entries_[i];
+      f(e, std::string_view(names_.data() + e.name_off, e.name_len));
+    }
+    fresh_.clear();
+  }
+  void drop_fresh() { fresh_.clear(); }
 
   struct Entry {
-    uint64_t rhash = 0, sid = 0;
+    uint64_t h = 0, rhash = 0, sid = 0;
     uint64_t ex_full = 0;  // the exemplar interval (Columnizer::ex_gen_) in which the series was seen full
     uint32_t svc = 0;
     int32_t kind = 0, code = 0;
@@ -205,6 +216,7 @@ class SigCache {
   std::vector<Slot> slots_;
   std::vector<Entry> entries_;
   std::string names_;
+  std::vector<uint32_t> fresh_;
 };
 
 class Columnizer {
@@ -251,13 +263,17 @@ class Columnizer {
   struct Undo;    // dictionary entries made by one exclusive call
   struct Pool;
   Result columnize_into(const uint8_t *buf, size_t len, Cols &out);
+  // cache: the thread's own signature cache; l2: the shared one (read only
+  // while workers decode; filled from the workers' new entries between batches)
   template <bool kShared>
-  bool run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCache &cache, Result &res, Undo *undo);
+  bool run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCache &cache, const SigCache *l2, Result &res,
+           Undo *undo);
 
   Options opt_;
   Cols buf_{true}, excl_;  // buf_: page-locked when possible; excl_: a batch's exclusively redone requests
   Cols spare_{true};       // the other page-locked buffer (swap_buffers)
   SigCache cache_;
+  SigCache shared_;  // every thread's signatures, second level (see run)
   uint64_t gen_ = 0;  // bumped whenever an existing dictionary entry may change
   std::unique_ptr<Worker> main_;
   std::vector<std::unique_ptr<Worker>> workers_;

@@ -84,6 +84,7 @@ for step in "$@"; do
     hostprof_*) t=${step#hostprof_}; run "hostprof_t$t" 200 node --cpu-prof --cpu-prof-dir="$OUT/hostprof_t$t" \
         --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 ;;
     hostex_*) t=${step#hostex_}; run "hostex_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 --exemplars --events ;;
+    hostc4_*) t=${step#hostc4_}; run "hostc4_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 --highcard ;;
     host_*) t=${step#host_}; run "host_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 ;;
     bench_*) wl=${step#bench_}; run "bench_$wl" 300 python bench.py --workload "$wl" --sub "" --steps 20 $BQ ;;
     abvar_*) vs=${step#abvar_}  # A/B of small-table kernel variants (laboratory build), rounds interleaved
