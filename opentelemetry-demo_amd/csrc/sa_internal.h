@@ -115,9 +115,9 @@ struct IngestParams {
   unsigned long long *span_long;  // [n]: the duration of each span whose record holds kSpanRecDurMask
   // EXPO mode, index records (xidx != 0): slot_of holds ixrec words -- each
   // span's bucket index at the scale its series had when the kernel started
-  // (xhdr[].scale, read in the prologue) -- and span_long the durations the
+  // (xscale[], read in the prologue) -- and span_long the durations the
   // fast index path declined
-  const ExpoHdr *xhdr;
+  const int8_t *xscale;  // [cap] each slot's scale (expo_reduce_rescale_kernel keeps it)
   int32_t l2d_q24;  // log2(div) * 2^24 rounded (expo_index_fast)
   uint32_t xidx;
   XHdr *xslab;
@@ -177,6 +177,7 @@ struct ExpoParams {
   const unsigned long long *span_rec;  // [n] span records (slab counting: the small-table kernel -> counting)
   const unsigned long long *span_long;  // [n] durations of the records holding kSpanRecDurMask
   uint32_t xidx;  // slot_of holds index records (ixrec), the counting pass shifts them to the new scale
+  int8_t *xscale;  // [cap] each slot's scale as the reduce pass left it, for the ingest kernel (nullptr: none)
   unsigned long long *dropped;
   XHdr *xslab;        // small-table engines: [xG][cap] per-workgroup header partials (nullptr: pass 1 atomics)
   uint32_t xG;
@@ -477,7 +478,7 @@ hipError_t key_union(const uint64_t *in, uint64_t n, uint64_t *out, uint32_t *d_
 hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s);
 hipError_t launch_expo_compact(const ExpoParams &E, unsigned long long *out_keys, ExpoRow *out_rows,
                                uint32_t *out_buckets, unsigned long long *out_n, hipStream_t s);
-hipError_t launch_expo_init(ExpoHdr *hdr, uint64_t cap, hipStream_t s);
+hipError_t launch_expo_init(ExpoHdr *hdr, int8_t *xscale, uint64_t cap, hipStream_t s);
 size_t expo_count_lds_bytes(uint64_t cap, uint32_t max_size);
 // LDS entries of the slab counting kernel for one workgroup's LDS budget, and its LDS bytes
 uint32_t expo_slab_entries(uint64_t cap, uint32_t max_size, size_t budget);

@@ -128,6 +128,7 @@ struct sa_engine {
   uint32_t *xc_lcount = nullptr, *xc_slot_of_entry = nullptr, *xcslab = nullptr;
   uint32_t *xt_rec = nullptr, *xt_off = nullptr;  // the counting kernel's tail records (ExpoParams::xt_*)
   sa::ExpoHdr *expo_hdr = nullptr;
+  int8_t *expo_xscale = nullptr;  // [cap] the slots' scales for the ingest kernel (index records)
   uint32_t *expo_buckets = nullptr, *expo_slot = nullptr;
   uint64_t expo_slot_cap = 0;  // spans per set of expo_slot ([nsets][cap], 8 B each)
   // Small-table exponential engines run launch k + 1's ingest kernel beside
@@ -518,7 +519,8 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
     if ((rc = alloc((void **)&e->expo_hdr, (size_t)e->cap * sizeof(sa::ExpoHdr))) ||
         (rc = alloc((void **)&e->expo_buckets, (size_t)2 * e->cap * cfg->exp_max_size * 4)))
       return bail(rc);
-    if (sa::launch_expo_init(e->expo_hdr, e->cap, nullptr) != hipSuccess)
+    if (e->expo_small && (rc = alloc((void **)&e->expo_xscale, (size_t)e->cap))) return bail(rc);
+    if (sa::launch_expo_init(e->expo_hdr, e->expo_xscale, e->cap, nullptr) != hipSuccess)
       return bail(fail(e, SA_EDEVICE, "expo state init failed"));
     if (e->expo_small) {
       e->nsets = kDefaultSlabSets;
@@ -626,7 +628,8 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->slab_cnt, (void *)e->hll, (void *)e->errcnt, (void *)e->d_seeds,
                   (void *)e->dbg, (void *)e->d_bins, (void *)e->errslab, (void *)e->part_rec,
                   (void *)e->part_fill, (void *)e->base64, (void *)e->hll_lb,
-                  (void *)e->expo_hdr, (void *)e->expo_buckets, (void *)e->expo_slot, (void *)e->expo_out_keys,
+                  (void *)e->expo_hdr, (void *)e->expo_xscale, (void *)e->expo_buckets, (void *)e->expo_slot,
+                  (void *)e->expo_out_keys,
                   (void *)e->expo_out_rows, (void *)e->expo_out_buckets, (void *)e->hll_filt, (void *)e->xslab,
                   (void *)e->xc_lcount, (void *)e->xc_slot_of_entry, (void *)e->xcslab, (void *)e->pool_ring,
                   (void *)e->xt_rec, (void *)e->xt_off,
@@ -830,6 +833,7 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b, uint32_t
   E.max_probe = sa::max_probe_of(e->log2cap);
   E.cap = e->cap;
   E.hdr = e->expo_hdr;
+  E.xscale = e->expo_xscale;
   E.buckets = e->expo_buckets;
   E.max_size = e->cfg.exp_max_size;
   E.div = e->cfg.unit == SA_UNIT_S ? 1e9 : 1e6;
@@ -1036,7 +1040,8 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
         P.slot_of = slots;
         if (mode == 2) {
           P.xidx = 1;
-          P.xhdr = e->expo_hdr;
+          if (const char *v = ab_env("SPANAGG_XIDX_OFF")) P.xidx = std::atoi(v) == 2 ? 3 : 2;  // (ablation: results wrong)
+          P.xscale = e->expo_xscale;
           P.l2d_q24 = sa::expo_l2d_q24(e->cfg.unit == SA_UNIT_S ? 1e9 : 1e6);
           P.span_long = reinterpret_cast<unsigned long long *>(slots) + e->expo_slot_cap;
         }

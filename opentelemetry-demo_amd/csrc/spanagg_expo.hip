@@ -164,6 +164,7 @@ __device__ __forceinline__ void rescale_slot(const ExpoParams &E, uint64_t s) {
   if (h.maxpos_ns == 0) return;
   rescale_hdr(E, s, h);
   E.hdr[s] = h;
+  if (E.xscale) E.xscale[s] = (int8_t)h.scale;
 }
 
 // (one thread per slot)
@@ -241,7 +242,10 @@ __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E)
 #pragma unroll
   for (uint32_t k = 1; k < 16; ++k) xhdr_add(acc, part[k][sl]);
   if (E.lcount) E.lcount[s] = acc.cnt - acc.zero;  // this launch's positive durations (the entry selection)
-  if (!acc.cnt) return;  // no new values: the header (scale, range) stays as it is
+  if (!acc.cnt) {  // no new values: the header (scale, range) stays as it is
+    if (E.xscale) E.xscale[s] = (int8_t)h.scale;
+    return;
+  }
   const unsigned long long minpos = ~acc.minx;  // UINT64_MAX when no positive duration
   const unsigned long long mn = acc.zero ? 0ULL : minpos;
   h.count += acc.cnt;
@@ -253,6 +257,7 @@ __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E)
   h.maxpos_ns = acc.max > h.maxpos_ns ? acc.max : h.maxpos_ns;
   rescale_hdr(E, s, h);
   E.hdr[s] = h;
+  if (E.xscale) E.xscale[s] = (int8_t)h.scale;
 }
 
 constexpr uint32_t kXcBlock = 1024;
@@ -725,12 +730,15 @@ __global__ __launch_bounds__(256) void expo_compact_kernel(ExpoParams E, unsigne
       src[at] = 0;
     }
     h = expo_hdr_empty();
+    if (E.xscale) E.xscale[s] = (int8_t)kExpoMaxScale;
   }
 }
 
-__global__ void expo_init_kernel(ExpoHdr *hdr, uint64_t cap) {
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x)
+__global__ void expo_init_kernel(ExpoHdr *hdr, int8_t *xscale, uint64_t cap) {
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < cap; s += (uint64_t)gridDim.x * blockDim.x) {
     hdr[s] = expo_hdr_empty();
+    if (xscale) xscale[s] = (int8_t)kExpoMaxScale;
+  }
 }
 
 uint32_t grid_of(uint64_t n) { return (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192); }
@@ -853,8 +861,8 @@ hipError_t launch_expo_compact(const ExpoParams &E, unsigned long long *out_keys
   return hipGetLastError();
 }
 
-hipError_t launch_expo_init(ExpoHdr *hdr, uint64_t cap, hipStream_t s) {
-  hipLaunchKernelGGL(expo_init_kernel, dim3(grid_of(cap)), dim3(256), 0, s, hdr, cap);
+hipError_t launch_expo_init(ExpoHdr *hdr, int8_t *xscale, uint64_t cap, hipStream_t s) {
+  hipLaunchKernelGGL(expo_init_kernel, dim3(grid_of(cap)), dim3(256), 0, s, hdr, xscale, cap);
   return hipGetLastError();
 }
 

@@ -629,15 +629,12 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   }
   uint4 bv = make_uint4(0, 0, 0, 0);
   if (!EXPO && threadIdx.x < kBins * 2) bv = reinterpret_cast<const uint4 *>(P.bintab)[threadIdx.x];  // (EXPO: no buckets)
-  // EXPO with index records: the slots' scales (cap <= 2,048: two per thread),
-  // issued with the key table so the LDS setup waits for them and not for the
-  // first tiles
-  int32_t xsc[2] = {0, 0};
+  // EXPO with index records: the slots' scales (cap <= 2,048 bytes: a 16-bit
+  // pair per thread), issued with the key table so the LDS setup waits for
+  // them and not for the first tiles
+  uint32_t xsc = 0;
   if constexpr (EXPO)
-    if (P.xidx)
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-        if (threadIdx.x + u * kLdsBlock < cap) xsc[u] = P.xhdr[threadIdx.x + u * kLdsBlock].scale;
+    if (P.xidx && 2 * threadIdx.x < cap) xsc = *reinterpret_cast<const uint16_t *>(P.xscale + 2 * threadIdx.x);
   uint32_t lbw = 0;
   if (lb_on && threadIdx.x * 4 < P.lb_n) lbw = *reinterpret_cast<const uint32_t *>(P.hll_lb + threadIdx.x * 4);
   if constexpr (DYN && (OPT & 1)) {
@@ -683,10 +680,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   if (threadIdx.x < 4) lstat[threadIdx.x] = 0;
   if (POOL && threadIdx.x < kPoolMaxSteal) pmap[threadIdx.x] = 0;
   if constexpr (EXPO)
-    if (P.xidx)
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-        if (threadIdx.x + u * kLdsBlock < cap) lsc[threadIdx.x + u * kLdsBlock] = (int8_t)xsc[u];
+    if (P.xidx && 2 * threadIdx.x < cap) *reinterpret_cast<uint16_t *>(lsc + 2 * threadIdx.x) = (uint16_t)xsc;
   // the pool counter of the launch nsets ahead (it starts after this one ends)
   if (POOL && blockIdx.x == 0 && threadIdx.x == 0) *cold_params().pool_next = 0;
   etab[threadIdx.x] = 0;  // kErrTab == kLdsBlock
@@ -961,6 +955,10 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
               w = kSpanRecNoSlot << kIxSlotShift;
             } else if (d == 0) {
               w = f << kIxSlotShift | kIxZero;
+#ifdef SPANAGG_AB
+            } else if (P.xidx >= 2) {  // ablation (laboratory, SPANAGG_XIDX_OFF=1 / 2): no index work
+              w = ixrec_of(f, P.xidx == 2 ? lsc[f] : 0, (int32_t)(d & 7u));  // (2: and no scale read; wrong buckets)
+#endif
             } else {
               const int32_t sc = lsc[f];
               int32_t ix;

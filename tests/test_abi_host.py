@@ -54,7 +54,7 @@ def test_product_library_has_no_laboratory():
     assert "getenv" not in dyn
     strings = subprocess.run(["strings", so], capture_output=True, text=True, check=True).stdout
     for lab in ("bt_aggregate2_kernel", "ingest_lds_kernelILi1E", "SPANAGG_VARIANT", "SPANAGG_BT_AGG",
-                "SPANAGG_XT", "SPANAGG_FAIL_AGG", "SPANAGG_NO_SETEV", "SPANAGG_XREC", "SPANAGG_XSTREAM"):
+                "SPANAGG_XT", "SPANAGG_FAIL_AGG", "SPANAGG_NO_SETEV", "SPANAGG_XREC", "SPANAGG_XSTREAM", "SPANAGG_XIDX_OFF"):
         assert lab not in strings, lab
 
 

@@ -131,6 +131,19 @@ for step in "$@"; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_XSTREAM=$x \
           run "xstream_${wl}_x${x}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $BQ
       done; done ;;
+    xrectrace_*) wl=${step#xrectrace_}  # per-kernel trace of c2expo with span words 0 / 2 (laboratory build)
+      for r in 1 2; do for x in 0 2; do
+        (cd /tmp && SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_XREC=$x run "xrectrace_${wl}_x${x}_r$r" 200 \
+          rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/xrectrace_${wl}_x${x}_r$r" -o run \
+          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 100 --streams 1 --soak-s 0 --no-filter-off $BQ) || exit $?
+      done; done ;;
+    xidxoff_*) wl=${step#xidxoff_}  # c2expo: the ingest kernel's bucket index work on / off (ablation, laboratory build)
+      for r in 1 2; do for x in 0 1 2; do
+        if [ $x != 0 ]; then export SPANAGG_XIDX_OFF=$x; else unset SPANAGG_XIDX_OFF; fi
+        (cd /tmp && SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so run "xidxoff_${wl}_x${x}_r$r" 200 \
+          rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/xidxoff_${wl}_x${x}_r$r" -o run \
+          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 100 --streams 1 --soak-s 0 --no-filter-off $BQ) || exit $?
+      done; done; unset SPANAGG_XIDX_OFF ;;
     labexpo_*) knob=${step#labexpo_}  # the exponential-histogram suites on the laboratory build with one knob, e.g. labexpo_SPANAGG_XREC=0
       (export SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so; export "$knob"; \
        run "labexpo_${knob//=/}" 300 python -u -m pytest tests/test_gpu_expo.py tests/test_gpu_churn.py -m gpu -x -v \
