@@ -239,7 +239,8 @@ def n_variants(args, launches, device):
     want = launches if args.variants <= 0 else min(args.variants, launches)
     import torch
     free, _ = torch.cuda.mem_get_info(device)
-    fit = max(2, int(free // 2 // (16 * args.spans)))
+    per_span = 44 if getattr(args, "fresh_cols", False) else 16  # (--fresh-cols: every column per variant)
+    fit = max(2, int(free // 2 // (per_span * args.spans)))
     if want > fit:
         print(f"bench: {want} trace-id variants do not fit; using {fit} (variants repeat)", file=sys.stderr)
     return min(want, fit)
@@ -284,6 +285,12 @@ def run_workload(name, n, args, device, rank, world, barrier):
     n_iso = max(3, args.steps // 5)
     n_var = n_variants(args, 1 + args.settle + args.warmup + 2 * n_iso + args.steps, device)
     variants = trace_variants(cols[3], cols[4], n_var, seed=1000 + rank, rank=rank, world=world)
+    # every variant's own copy of the other columns too (--fresh-cols): no
+    # launch re-reads an address an earlier launch read, so no column can be
+    # served from the last-level cache across launches
+    full = [(cols[0].clone(), cols[1].clone(), cols[2].clone(), w0, w1, cols[5].clone())
+            if getattr(args, "fresh_cols", False) else (cols[0], cols[1], cols[2], w0, w1, cols[5])
+            for w0, w1 in variants]
     if world > 1:  # every span of every variant belongs to this rank's trace-id shard
         from spanagg.dist import shard_of
         for _, vw1 in variants[:2]:
@@ -298,9 +305,9 @@ def run_workload(name, n, args, device, rank, world, barrier):
 
     def step(i, s=None):
         s = s or streams[i % len(streams)]
-        v = variants[launches[0] % len(variants)]
+        v = full[launches[0] % len(full)]
         launches[0] += 1
-        eng.ingest_device(cols[0], cols[1], cols[2], v[0], v[1], cols[5], n=n, stream=s.cuda_stream)
+        eng.ingest_device(v[0], v[1], v[2], v[3], v[4], v[5], n=n, stream=s.cuda_stream)
 
     def ev():
         return torch.cuda.Event(enable_timing=True)
@@ -554,6 +561,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--fresh-cols", dest="fresh_cols", action="store_true",
+                    help="every launch reads its own copy of every column (not only of the trace ids)")
     ap.add_argument("--spans", type=int, default=10_000_000, help="spans per step per GPU")
     ap.add_argument("--workload", choices=list(WORKLOADS), default="c2")
     ap.add_argument("--streams", type=int, default=2,

@@ -144,6 +144,11 @@ for step in "$@"; do
           rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/xidxoff_${wl}_x${x}_r$r" -o run \
           -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 100 --streams 1 --soak-s 0 --no-filter-off $BQ) || exit $?
       done; done; unset SPANAGG_XIDX_OFF ;;
+    fresh_*) wl=${step#fresh_}  # every column fresh per launch (--fresh-cols) against trace ids only, rounds interleaved
+      for r in 1 2; do for f in 0 1; do
+        if [ $f = 1 ]; then fc=--fresh-cols; else fc=; fi
+        run "fresh_${wl}_f${f}_r$r" 300 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $fc $BQ
+      done; done ;;
     labexpo_*) knob=${step#labexpo_}  # the exponential-histogram suites on the laboratory build with one knob, e.g. labexpo_SPANAGG_XREC=0
       (export SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so; export "$knob"; \
        run "labexpo_${knob//=/}" 300 python -u -m pytest tests/test_gpu_expo.py tests/test_gpu_churn.py -m gpu -x -v \
