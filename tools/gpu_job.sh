@@ -135,7 +135,7 @@ for step in "$@"; do
       for r in 1 2; do for x in 0 2; do
         (cd /tmp && SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_XREC=$x run "xrectrace_${wl}_x${x}_r$r" 200 \
           rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/xrectrace_${wl}_x${x}_r$r" -o run \
-          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 100 --streams 1 --soak-s 0 --no-filter-off $BQ) || exit $?
+          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps 100 --streams 1 --soak-s 0 --no-filter-off ${XFC:-} $BQ) || exit $?
       done; done ;;
     xidxoff_*) wl=${step#xidxoff_}  # c2expo: the ingest kernel's bucket index work on / off (ablation, laboratory build)
       for r in 1 2; do for x in 0 1 2; do
