@@ -541,6 +541,14 @@ __device__ __forceinline__ uint32_t wave_claim(uint32_t *ctr) {
   return (uint32_t)__builtin_amdgcn_readfirstlane((int)atomicAdd(ctr, 1u)) >> 6;
 }
 
+// the scale read of the index records (the laboratory's SPANAGG_XIDX_OFF=3
+// ablation skips it; the product build always reads it)
+#ifdef SPANAGG_AB
+#define SA_XIDX_SCALE(P) ((P).xidx != 3)
+#else
+#define SA_XIDX_SCALE(P) true
+#endif
+
 // TAG: the key lookup reads 32-bit tags (key_tag) of the two candidate
 // buckets -- one ds_read_b128 per bucket instead of two -- and verifies the
 // matching slot's full key with one ds_read_b64 (a tag match on another key,
@@ -634,7 +642,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   // them and not for the first tiles
   uint32_t xsc = 0;
   if constexpr (EXPO)
-    if (P.xidx && 2 * threadIdx.x < cap) xsc = *reinterpret_cast<const uint16_t *>(P.xscale + 2 * threadIdx.x);
+    if (P.xidx && SA_XIDX_SCALE(P) && 2 * threadIdx.x < cap) xsc = *reinterpret_cast<const uint16_t *>(P.xscale + 2 * threadIdx.x);
   uint32_t lbw = 0;
   if (lb_on && threadIdx.x * 4 < P.lb_n) lbw = *reinterpret_cast<const uint32_t *>(P.hll_lb + threadIdx.x * 4);
   if constexpr (DYN && (OPT & 1)) {
@@ -680,7 +688,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   if (threadIdx.x < 4) lstat[threadIdx.x] = 0;
   if (POOL && threadIdx.x < kPoolMaxSteal) pmap[threadIdx.x] = 0;
   if constexpr (EXPO)
-    if (P.xidx && 2 * threadIdx.x < cap) *reinterpret_cast<uint16_t *>(lsc + 2 * threadIdx.x) = (uint16_t)xsc;
+    if (P.xidx && SA_XIDX_SCALE(P) && 2 * threadIdx.x < cap) *reinterpret_cast<uint16_t *>(lsc + 2 * threadIdx.x) = (uint16_t)xsc;
   // the pool counter of the launch nsets ahead (it starts after this one ends)
   if (POOL && blockIdx.x == 0 && threadIdx.x == 0) *cold_params().pool_next = 0;
   etab[threadIdx.x] = 0;  // kErrTab == kLdsBlock
@@ -950,25 +958,27 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
         if (!P.span_rec && lane_off + toff + (uint32_t)j < lim) {
           uint32_t w = f;
           if (P.xidx) {  // the index record: the bucket index at the slot's starting scale
+            // (branch-free but for the rare long-duration store: every lane
+            // computes the index, the record is picked by selects)
             const unsigned long long d = dur[j];
-            if (f == kNotFound) {
-              w = kSpanRecNoSlot << kIxSlotShift;
-            } else if (d == 0) {
-              w = f << kIxSlotShift | kIxZero;
+            const bool nf = f == kNotFound;
+            const uint32_t fs = nf ? 0u : f;
 #ifdef SPANAGG_AB
-            } else if (P.xidx >= 2) {  // ablation (laboratory, SPANAGG_XIDX_OFF=1 / 2): no index work
-              w = ixrec_of(f, P.xidx == 2 ? lsc[f] : 0, (int32_t)(d & 7u));  // (2: and no scale read; wrong buckets)
+            const int32_t sc = P.xidx == 3 ? 0 : lsc[fs];
+#else
+            const int32_t sc = lsc[fs];
 #endif
-            } else {
-              const int32_t sc = lsc[f];
-              int32_t ix;
-              if (expo_index_fast(d, P.l2d_q24, sc, ix) && ix >= kIxMin && ix <= kIxMax) {
-                w = ixrec_of(f, sc, ix);
-              } else {
-                w = f << kIxSlotShift | kIxLong;
-                P.span_long[lo + toff + lane_off + j] = d;
-              }
-            }
+            int32_t ix = 0;
+            bool ok;
+#ifdef SPANAGG_AB
+            if (P.xidx >= 2) ok = true, ix = (int32_t)(d & 7u);  // ablation (SPANAGG_XIDX_OFF): wrong buckets
+            else
+#endif
+            ok = expo_index_fast(d ? d : 1u, P.l2d_q24, sc, ix) && ix >= kIxMin && ix <= kIxMax;
+            w = nf ? kSpanRecNoSlot << kIxSlotShift
+                   : d == 0 ? (f << kIxSlotShift | kIxZero)
+                            : ok ? ixrec_of(f, sc, ix) : (f << kIxSlotShift | kIxLong);
+            if (!nf && d != 0 && !ok) P.span_long[lo + toff + lane_off + j] = d;
           }
           P.slot_of[lo + toff + lane_off + j] = w;
         }

@@ -78,6 +78,9 @@ for step in "$@"; do
     colabhc) (cd host/node && node test/host_rate.js 2000000 --highcard --dump /tmp/req_hc.bin > /dev/null) || exit 1  # C4 vocabulary, http.route dimension
       for r in 1 2 3; do for b in colbench ${COL_OTHER:-colbench_olddim}; do
         run "colabhc_${b}_r$r" 120 host/node/build/$b /tmp/req_hc.bin --threads 16 --dim http.route; done; done ;;
+    colabex) (cd host/node && node test/host_rate.js 2000000 --events --dump /tmp/req_ev.bin > /dev/null) || exit 1  # exemplars + events
+      for r in 1 2 3; do for b in colbench ${COL_OTHER:-colbench_olddim}; do
+        run "colabex_${b}_r$r" 120 host/node/build/$b /tmp/req_ev.bin --threads 16 --exemplars --events; done; done ;;
     colab) (cd host/node && node test/host_rate.js 2000000 --dump /tmp/req_plain.bin > /dev/null) || exit 1  # colbench against build/colbench_<other>
       for r in 1 2 3; do for t in 16 8; do for b in colbench ${COL_OTHER:-colbench_condvar}; do
         run "colab_${b}_t${t}_r$r" 120 host/node/build/$b /tmp/req_plain.bin --threads "$t"; done; done; done ;;
