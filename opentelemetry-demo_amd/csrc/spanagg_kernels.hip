@@ -940,6 +940,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     //    on the readlane'd key) make one LDS add of their count, from the
     //    first of them; the other lanes add their own span.
     if constexpr (EXPO) {
+      uint32_t xw[S] = {};
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         const uint32_t f = found[j];
@@ -955,7 +956,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
             atomicMax(&xmax[f], d);
           }
         }
-        if (!P.span_rec && lane_off + toff + (uint32_t)j < lim) {
+        if (!P.span_rec) {
           uint32_t w = f;
           if (P.xidx) {  // the index record: the bucket index at the slot's starting scale
             // (branch-free but for the rare long-duration store: every lane
@@ -978,9 +979,23 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
             w = nf ? kSpanRecNoSlot << kIxSlotShift
                    : d == 0 ? (f << kIxSlotShift | kIxZero)
                             : ok ? ixrec_of(f, sc, ix) : (f << kIxSlotShift | kIxLong);
-            if (!nf && d != 0 && !ok) P.span_long[lo + toff + lane_off + j] = d;
+            if (!nf && d != 0 && !ok && lane_off + toff + (uint32_t)j < lim) P.span_long[lo + toff + lane_off + j] = d;
           }
-          P.slot_of[lo + toff + lane_off + j] = w;
+          xw[j] = w;
+        }
+      }
+      // the lane's slots / index records: one 8-B store for its two spans
+      // (lo, toff and lane_off are even)
+      if (!P.span_rec) {
+        const uint32_t i0 = toff + lane_off;
+        uint32_t *wp = P.slot_of + lo + i0;
+        if constexpr (S == 2) {
+          if (i0 + 1 < lim) *reinterpret_cast<uint2 *>(wp) = make_uint2(xw[0], xw[1]);
+          else if (i0 < lim) wp[0] = xw[0];
+        } else {
+#pragma unroll
+          for (int j = 0; j < S; ++j)
+            if (i0 + (uint32_t)j < lim) wp[j] = xw[j];
         }
       }
       // the lane's span records: one 16-B store for its two spans (two 8-B
