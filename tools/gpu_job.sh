@@ -180,6 +180,10 @@ for step in "$@"; do
       (cd /tmp && run "ptrace_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ptrace_$wl" -o run \
          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --steps ${PSTEPS:-400} --streams 1 --soak-s 0 \
          --no-filter-off $BQ) || exit $? ;;
+    kab_*) rest=${step#kab_}; wl=${rest%%_*}; lib=${rest#*_}  # ptrace of <wl> on spanagg/lib<lib>.so (per-kernel times of a variant)
+      (cd /tmp && SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/lib$lib.so run "kab_${wl}_$lib" 300 rocprofv3 --kernel-trace --stats \
+         --output-format csv -d "$OUT/kab_${wl}_$lib" -o run -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" \
+         --steps ${PSTEPS:-200} --streams 1 --soak-s 0 --no-filter-off $BQ) || exit $? ;;
     group_*) wl=${step#group_}  # an 8-member group on this device: partition kernels + group flush
       (cd /tmp && run "group_$wl" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/group_$wl" -o run \
          -- python3 "$ROOTDIR/bench.py" --workload "$wl" --sub "" --group 8 --steps 20 --warmup 3 --soak-s 0 \
