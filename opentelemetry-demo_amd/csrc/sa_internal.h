@@ -407,9 +407,10 @@ constexpr uint32_t kHbmBlock = 256;
 // 12 / 13 = 8 / 11 specialised for cap 2048, 17 buckets, HLL p 14; 14 = 12 with
 // dynamic wave chunks; 15 = 14 generic; 16-18 = 14 with OPT 1 / 3 / 2; 19 = 16
 // with the batched end-of-launch write-back (v2_epilogue); 20 = 19 LEAN; 21 =
-// 20 with the TAG key lookup; 22 = 20 with the tail pool (POOL).
-constexpr int kNumLdsVariants = 23;
-constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
+// 20 with the TAG key lookup; 22 = 20 with the tail pool (POOL); 23 / 24 = 20
+// with tile claims (OPT 3 / 2: NBUF claims of one wave tile per round).
+constexpr int kNumLdsVariants = 25;
+constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
 constexpr int kLdsPoolVariant = 22;
 // v2 kernels keep u16 LDS counters for a whole launch: spans per workgroup per launch
 constexpr uint32_t kMaxWgSpans = 65532;
