@@ -274,8 +274,10 @@ def run_workload(name, n, args, device, rank, world, barrier):
 
     exp_max = 160 if name == "c2expo" else 0
     if name in ("c2", "c2expo"):
-        wl = generate_c2(n, seed=42 + rank)
-        batch, first_window, n_services, key_capacity = wl.batch, wl.first_window, wl.n_services, 1500
+        nps = getattr(args, "names_per_service", 25)
+        wl = generate_c2(n, seed=42 + rank, names_per_service=nps)
+        # (20 services x nps names x 3 status codes: 1,500 series at the default 25)
+        batch, first_window, n_services, key_capacity = wl.batch, wl.first_window, wl.n_services, 60 * nps
     else:
         batch, _, first_window = generate_highcard(n, seed=7 + rank, zipf_s=1.1 if name == "c4zipf" else 0.0)
         wl, n_services, key_capacity = None, 1, 1_200_000
@@ -565,6 +567,8 @@ def main():
                     help="every launch reads its own copy of every column (not only of the trace ids)")
     ap.add_argument("--spans", type=int, default=10_000_000, help="spans per step per GPU")
     ap.add_argument("--workload", choices=list(WORKLOADS), default="c2")
+    ap.add_argument("--names-per-service", dest="names_per_service", type=int, default=25,
+                    help="span names per service of the C2 vocabulary (probe runs only; the C2 config is 25)")
     ap.add_argument("--streams", type=int, default=2,
                     help="launch streams the steps alternate over (the engine's two slab sets "
                          "let consecutive launches overlap); 1 = strictly serial launches")

@@ -408,9 +408,12 @@ constexpr uint32_t kHbmBlock = 256;
 // dynamic wave chunks; 15 = 14 generic; 16-18 = 14 with OPT 1 / 3 / 2; 19 = 16
 // with the batched end-of-launch write-back (v2_epilogue); 20 = 19 LEAN; 21 =
 // 20 with the TAG key lookup; 22 = 20 with the tail pool (POOL); 23 / 24 = 20
-// with tile claims (OPT 3 / 2: NBUF claims of one wave tile per round).
-constexpr int kNumLdsVariants = 25;
-constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
+// with tile claims (OPT 3 / 2: NBUF claims of one wave tile per round); 25 =
+// 15 with 512-thread workgroups (kLdsHalfBlockVariant).
+constexpr int kNumLdsVariants = 26;
+constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
+constexpr int kLdsHalfBlockVariant = 25;
+constexpr uint32_t lds_variant_block(int v) { return v == kLdsHalfBlockVariant ? 512u : 1024u; }
 constexpr int kLdsPoolVariant = 22;
 // v2 kernels keep u16 LDS counters for a whole launch: spans per workgroup per launch
 constexpr uint32_t kMaxWgSpans = 65532;

@@ -444,7 +444,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   }
   if (e->small) {
     e->spl = (uint32_t)sa::kLdsSpl[e->variant];
-    e->block = 1024;
+    e->block = sa::lds_variant_block(e->variant);
     const uint32_t per_cu = std::max<uint32_t>(
         1, std::min<uint32_t>(2048 / e->block, (uint32_t)((160 * 1024) / e->lds_bytes)));
     e->G = e->cus * per_cu;

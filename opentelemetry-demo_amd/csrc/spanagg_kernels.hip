@@ -84,12 +84,11 @@ __device__ __forceinline__ void flush_lds(const IngestParams &P, uint32_t cap, u
 // sums, ERROR cells, HLL CAS, bound refresh: ~7 in a row).  A stale HLL word
 // only makes the CAS retry; a stale register read for the bound can only lower
 // it, which keeps it a lower bound.
-template <int UPT, int SPT, typename PT>
+template <int UPT, int SPT, uint32_t B, typename PT>
 __device__ __forceinline__ void v2_epilogue(const PT &P, uint32_t cap, uint32_t nw, uint32_t log2cap,
                                             const unsigned long long *lsum, const uint32_t *lcnt,
                                             const uint32_t *etab, bool err_lds, const uint2 *hq,
                                             uint32_t nq) {
-  constexpr uint32_t B = kLdsBlock;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const bool slabs = !(P.diag & 8u);
   // 1. reads
@@ -108,10 +107,16 @@ __device__ __forceinline__ void v2_epilogue(const PT &P, uint32_t cap, uint32_t 
   for (int u = 0; u < SPT; ++u) sv[u] = slabs ? ls[tid + u * B] : make_ulonglong2(0, 0);
 #pragma unroll
   for (int u = 0; u < SPT; ++u) sg[u] = (sv[u].x | sv[u].y) ? ss[tid + u * B] : make_ulonglong2(0, 0);
-  const uint32_t e = err_lds ? etab[tid] : 0u;
-  uint32_t *ecell =
-      e ? P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1) : nullptr;
-  const uint32_t ev = e ? *ecell : 0u;
+  constexpr uint32_t kE = kErrTab / B;  // ERROR table entries per thread
+  uint32_t e[kE], ev[kE];
+  uint32_t *ecell[kE];
+#pragma unroll
+  for (uint32_t i = 0; i < kE; ++i) {
+    e[i] = err_lds ? etab[tid + i * B] : 0u;
+    ecell[i] = e[i] ? P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e[i] >> 16) - 1)
+                    : nullptr;
+    ev[i] = e[i] ? *ecell[i] : 0u;
+  }
   constexpr uint32_t kQ = kHllQueue / B;
   uint2 q[kQ];
   uint32_t qv[kQ];
@@ -149,7 +154,9 @@ __device__ __forceinline__ void v2_epilogue(const PT &P, uint32_t cap, uint32_t 
       ss[tid + u * B] = sg[u];
     }
   }
-  if (e) *ecell = ev + (e & 0xFFFFu);
+#pragma unroll
+  for (uint32_t i = 0; i < kE; ++i)
+    if (e[i]) *ecell[i] = ev[i] + (e[i] & 0xFFFFu);
 #pragma unroll
   for (uint32_t i = 0; i < kQ; ++i) {
     if (!q[i].y) continue;
@@ -556,8 +563,9 @@ __device__ __forceinline__ uint32_t wave_claim(uint32_t *ctr) {
 // cold path, which probes full keys): 40 B of LDS per span instead of 64.
 template <int S, int NBUF, int AUX, bool DIAG, int LC = 0, int NWC = 0, int PC = 0, int HAUX = -1,
           bool DYN = false, int OPT = 0, bool EPI = false, bool LEAN = false, bool EXPO = false, bool TAG = false,
-          bool POOL = false>
-__global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
+          bool POOL = false, uint32_t BLK = kLdsBlock>
+__global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
+  static_assert(BLK % 64 == 0 && kErrTab % BLK == 0 && kHllQueue % BLK == 0 && BLK * 4 >= kLbMaxSub, "block size");
   static_assert(!POOL || (DYN && !(OPT & 2)), "the tail pool extends the chunk claims");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (P.dbg && threadIdx.x == 0) P.dbg[blockIdx.x * kDbgPerWg + 0] = __builtin_amdgcn_s_memrealtime();
@@ -591,14 +599,14 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   uint64_t lo, hi;
   wg_range_p(P, lo, hi);
   const uint32_t len = (uint32_t)(hi - lo);
-  // static: a step covers one workgroup tile (kLdsBlock * S spans, lane_off
+  // static: a step covers one workgroup tile (BLK * S spans, lane_off
   // by thread); DYN: one wave tile (64 * S spans, lane_off by lane) and a
   // claim is NBUF consecutive wave tiles
-  constexpr uint32_t tile = DYN ? 64 * S : kLdsBlock * S;
+  constexpr uint32_t tile = DYN ? 64 * S : BLK * S;
   constexpr bool kTileClaims = DYN && (OPT & 2);
   constexpr uint32_t chunk = kTileClaims ? tile : NBUF * tile;
   const uint32_t lane_off = (DYN ? (threadIdx.x & 63u) : threadIdx.x) * S;
-  constexpr uint32_t kWaves = kLdsBlock / 64;
+  constexpr uint32_t kWaves = BLK / 64;
   const uint32_t n_chunks = DYN ? (len + chunk - 1) / chunk : 0u;
   // wave-uniform by construction; readfirstlane keeps it (and every tile
   // base derived from it) in SGPRs for the buffer descriptors
@@ -628,10 +636,10 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   // and the bin table first, then the first NBUF tiles; the LDS setup then
   // waits only for the key-table loads (vmcnt counts in issue order).
   ulonglong2 kv[4];
-  const uint32_t per = (cap + 2 * kLdsBlock - 1) / (2 * kLdsBlock);
+  const uint32_t per = (cap + 2 * BLK - 1) / (2 * BLK);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    const uint32_t i = 2 * (threadIdx.x + u * kLdsBlock);
+    const uint32_t i = 2 * (threadIdx.x + u * BLK);
     kv[u] = (u < (int)per && i < cap) ? *reinterpret_cast<const ulonglong2 *>(P.gkeys + i)
                                       : make_ulonglong2(0, 0);
   }
@@ -669,7 +677,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
   }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    const uint32_t i = 2 * (threadIdx.x + u * kLdsBlock);
+    const uint32_t i = 2 * (threadIdx.x + u * BLK);
     if (u < (int)per && i < cap) {
       reinterpret_cast<ulonglong2 *>(lkeys)[i / 2] = kv[u];
       reinterpret_cast<ulonglong2 *>(lsum)[i / 2] = make_ulonglong2(0, 0);
@@ -677,7 +685,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     }
   }
   if (threadIdx.x < kBins * 2) reinterpret_cast<uint4 *>(lbins)[threadIdx.x] = bv;
-  for (uint32_t i = threadIdx.x * 4; i < cap * nw; i += kLdsBlock * 4)
+  for (uint32_t i = threadIdx.x * 4; i < cap * nw; i += BLK * 4)
     *reinterpret_cast<uint4 *>(lcnt + i) = make_uint4(0, 0, 0, 0);
   if (threadIdx.x == 0) {
     hq_n[0] = 0;
@@ -691,7 +699,7 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     if (P.xidx && SA_XIDX_SCALE(P) && 2 * threadIdx.x < cap) *reinterpret_cast<uint16_t *>(lsc + 2 * threadIdx.x) = (uint16_t)xsc;
   // the pool counter of the launch nsets ahead (it starts after this one ends)
   if (POOL && blockIdx.x == 0 && threadIdx.x == 0) *cold_params().pool_next = 0;
-  etab[threadIdx.x] = 0;  // kErrTab == kLdsBlock
+  for (uint32_t i = threadIdx.x; i < kErrTab; i += BLK) etab[i] = 0;
   // (filter off: the first bound word stays 0, and every span's sub-block
   // index is 0 or 1 below, so no rho can be at or below it)
   if (threadIdx.x * 4 < (lb_on ? P.lb_n : 4u)) reinterpret_cast<uint32_t *>(llb)[threadIdx.x] = lbw;
@@ -1188,33 +1196,37 @@ __global__ __launch_bounds__(kLdsBlock) void ingest_v2_kernel(IngestParams P) {
     // this workgroup's header partials -> its slab (touched slots only; the
     // reduce pass zeroes what it consumed)
     XHdr *xs = P.xslab + (uint64_t)blockIdx.x * cap;
-    for (uint32_t sl = threadIdx.x; sl < cap; sl += kLdsBlock)
+    for (uint32_t sl = threadIdx.x; sl < cap; sl += BLK)
       if (const uint32_t c = xcnt[sl]) xs[sl] = XHdr{c, xzero[sl], lsum[sl], xminx[sl], xmax[sl]};
     if (err_lds) {  // this workgroup's ERROR counts -> its private slab (plain RMW)
-      const uint32_t e = etab[threadIdx.x];
-      if (e) {
-        uint32_t *cell = P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1);
-        *cell += e & 0xFFFFu;
+      for (uint32_t t = threadIdx.x; t < kErrTab; t += BLK) {
+        const uint32_t e = etab[t];
+        if (e) {
+          uint32_t *cell = P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1);
+          *cell += e & 0xFFFFu;
+        }
       }
     }
-    for (uint32_t i = threadIdx.x; i < nq; i += kLdsBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
+    for (uint32_t i = threadIdx.x; i < nq; i += BLK) hll_raise(P.hll + hq[i].x, hq[i].y);
     hll_lb_refresh(P, threadIdx.x >> 6, kWaves);
   } else if constexpr (LC != 0 && NWC != 0 && EPI) {
     // compile-time geometry: the batched epilogue (one round trip)
     constexpr uint32_t kCap = 1u << LC;
-    static_assert((kCap * NWC / 2) % kLdsBlock == 0 && (kCap / 2) % kLdsBlock == 0, "epilogue geometry");
-    v2_epilogue<kCap * NWC / 2 / kLdsBlock, kCap / 2 / kLdsBlock>(cold_params(), cap, nw, log2cap, lsum, lcnt, etab,
+    static_assert((kCap * NWC / 2) % BLK == 0 && (kCap / 2) % BLK == 0, "epilogue geometry");
+    v2_epilogue<kCap * NWC / 2 / BLK, kCap / 2 / BLK, BLK>(cold_params(), cap, nw, log2cap, lsum, lcnt, etab,
                                                                     err_lds, hq, nq);
   } else {
     flush_lds(P, cap, nw, lsum, lcnt);
     if (err_lds) {  // this workgroup's ERROR counts -> its private slab (plain RMW)
-      const uint32_t e = etab[threadIdx.x];
-      if (e) {
-        uint32_t *cell = P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1);
-        *cell += e & 0xFFFFu;
+      for (uint32_t t = threadIdx.x; t < kErrTab; t += BLK) {
+        const uint32_t e = etab[t];
+        if (e) {
+          uint32_t *cell = P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1);
+          *cell += e & 0xFFFFu;
+        }
       }
     }
-    for (uint32_t i = threadIdx.x; i < nq; i += kLdsBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
+    for (uint32_t i = threadIdx.x; i < nq; i += BLK) hll_raise(P.hll + hq[i].x, hq[i].y);
     hll_lb_refresh(P, threadIdx.x >> 6, kWaves);
   }
   if (dbg && threadIdx.x == 0) dbg[blockIdx.x * kDbgPerWg + 3] = __builtin_amdgcn_s_memrealtime();
@@ -1938,7 +1950,7 @@ hipError_t prepare_ingest_small(size_t lds_bytes) {
 hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,
                                hipStream_t s, int variant) {
   // the specialised v2 build is only valid for its compile-time geometry
-  if ((variant == 12 || variant == 13 || variant >= 14) &&
+  if ((variant == 12 || variant == 13 || (variant >= 14 && variant != kLdsHalfBlockVariant)) &&
       !(P.log2cap == 11 && (P.nbk + 1) / 2 == 9 && P.p == 14))
     variant = variant == 12 ? 8 : variant == 13 ? 11 : 15;
   // (the lean window quotient of variant 20 needs window_ns < 2^56, which
@@ -1946,7 +1958,7 @@ hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_
   // their workgroup and wave-end stamps are written whenever P.dbg is set)
   const void *fn = small_fn(P.bintab != nullptr, variant, P.diag != 0 || (P.dbg != nullptr && variant < 8));
   void *args[] = {const_cast<IngestParams *>(&P)};
-  return hipLaunchKernel(fn, dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);
+  return hipLaunchKernel(fn, dim3(grid), dim3(lds_variant_block(variant)), args, lds_bytes, s);
 }
 
 // the EXPO kernel: specialised for the default small table (2,048 slots, HLL

@@ -95,6 +95,12 @@ for step in "$@"; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_VARIANT=$v \
           run "abvar_v${v}_r$r" 200 python bench.py --workload c2 --sub "" --steps 50 --soak-s 0 --no-filter-off $BQ
       done; done ;;
+    abhalf_*) nps=${step#abhalf_}  # variant 15 against 25 (512-thread workgroups) on a C2 vocabulary of 20 x nps names
+      for r in 1 2 3; do for v in 15 25; do
+        SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_VARIANT=$v \
+          run "abhalf${nps}_v${v}_r$r" 200 python bench.py --workload c2 --sub "" --steps 50 --soak-s 0 --no-filter-off \
+          --names-per-service "$nps" $BQ
+      done; done ;;
     btpipe_*) wl=${step#btpipe_}  # the binned launch pipeline on / off (laboratory build), rounds interleaved
       for r in 1 2; do for pp in 1 0; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_BT_PIPE=$pp \
