@@ -409,7 +409,8 @@ constexpr uint32_t kHbmBlock = 256;
 // with the batched end-of-launch write-back (v2_epilogue); 20 = 19 LEAN; 21 =
 // 20 with the TAG key lookup; 22 = 20 with the tail pool (POOL); 23 / 24 = 20
 // with tile claims (OPT 3 / 2: NBUF claims of one wave tile per round); 25 =
-// 15 with 512-thread workgroups (kLdsHalfBlockVariant).
+// 15 with 512-thread workgroups (kLdsHalfBlockVariant: the product's choice for
+// a table with a bin table whose LDS state fits a CU twice, two per CU).
 constexpr int kNumLdsVariants = 26;
 constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
 constexpr int kLdsHalfBlockVariant = 25;
@@ -441,6 +442,9 @@ hipError_t launch_ingest_hbm(const IngestParams &P, uint32_t grid, hipStream_t s
 hipError_t launch_ingest_part(const IngestParams &P, hipStream_t s);
 hipError_t prepare_ingest_part();
 hipError_t prepare_ingest_small(size_t lds_bytes);
+uint32_t ingest_small_block(bool bt, int variant, uint32_t log2cap, uint32_t nbk, uint32_t p);
+uint32_t ingest_small_blocks_per_cu(bool bt, int variant, uint32_t log2cap, uint32_t nbk, uint32_t p,
+                                    size_t lds_bytes);
 // exponential-histogram engines with an LDS-sized key table: the small-table
 // kernel in EXPO mode (header partials + per-span slots; spanagg_expo.hip
 // reduces and counts)

@@ -443,13 +443,25 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       e->variant = kDefaultVariant;
   }
   if (e->small) {
+    sa::BinEntry bins_probe[sa::kBins];
+    const bool bins_ok = build_bins(e, bins_probe);
+    // a table other than the specialised default geometry whose LDS state
+    // fits a CU twice: 512-thread workgroups, two per CU, so one workgroup's
+    // prologue and write-back overlap the other's loop
+    if (e->variant == kDefaultVariant && bins_ok && 2 * e->lds_bytes <= (size_t)160 * 1024 &&
+        !(e->log2cap == 11 && nw == 9 && cfg->hll_p == 14))
+      e->variant = sa::kLdsHalfBlockVariant;
     e->spl = (uint32_t)sa::kLdsSpl[e->variant];
-    e->block = sa::lds_variant_block(e->variant);
-    const uint32_t per_cu = std::max<uint32_t>(
-        1, std::min<uint32_t>(2048 / e->block, (uint32_t)((160 * 1024) / e->lds_bytes)));
-    e->G = e->cus * per_cu;
+    e->block = sa::ingest_small_block(bins_ok, e->variant, e->log2cap, e->nbk, cfg->hll_p);
     if (hipError_t st = sa::prepare_ingest_small(e->lds_bytes); st != hipSuccess)
       return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
+    // one resident round of workgroups (registers and LDS decide how many
+    // share a CU; a second round would repeat every workgroup's prologue)
+    uint32_t per_cu = sa::ingest_small_blocks_per_cu(bins_ok, e->variant, e->log2cap, e->nbk, cfg->hll_p,
+                                                     e->lds_bytes);
+    if (per_cu == 0)
+      per_cu = std::max<uint32_t>(1, std::min<uint32_t>(2048 / e->block, (uint32_t)((160 * 1024) / e->lds_bytes)));
+    e->G = e->cus * per_cu;
   } else if (e->expo_small) {
     e->block = 1024;
     e->spl = 2;

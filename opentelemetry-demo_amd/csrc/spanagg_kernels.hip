@@ -1902,9 +1902,11 @@ static const void *small_fn(bool bt, int v, bool diag) {
   (void)diag;
   if (!bt) return (const void *)&ingest_lds_kernel<0, 4, true, false>;
   if (v == 20) return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1, true, true>;
+  if (v == kLdsHalfBlockVariant)
+    return (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true, 0, false, false, false, false, false, 512>;
   return (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true>;
 }
-constexpr int kSmallFnVariants[] = {15, 20};
+constexpr int kSmallFnVariants[] = {15, 20, kLdsHalfBlockVariant};
 #else
 // every variant and the diagnostic kernels (tools/ A/B runs)
 #include "lab/small_lab.inc"
@@ -1947,18 +1949,43 @@ hipError_t prepare_ingest_small(size_t lds_bytes) {
   return hipSuccess;
 }
 
+// the variant that runs for a geometry: the specialised v2 builds are only
+// valid for their compile-time geometry (2,048 slots, 17 buckets, HLL p 14)
+static int small_variant(int variant, uint32_t log2cap, uint32_t nbk, uint32_t p) {
+  if ((variant == 12 || variant == 13 || (variant >= 14 && variant != kLdsHalfBlockVariant)) &&
+      !(log2cap == 11 && (nbk + 1) / 2 == 9 && p == 14))
+    variant = variant == 12 ? 8 : variant == 13 ? 11 : 15;
+  return variant;
+}
+// (the linear-threshold kernel, for bounds no bin table holds, is 1,024 threads)
+static uint32_t small_block(bool bt, int variant) { return bt ? lds_variant_block(variant) : kLdsBlock; }
+
 hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_bytes,
                                hipStream_t s, int variant) {
-  // the specialised v2 build is only valid for its compile-time geometry
-  if ((variant == 12 || variant == 13 || (variant >= 14 && variant != kLdsHalfBlockVariant)) &&
-      !(P.log2cap == 11 && (P.nbk + 1) / 2 == 9 && P.p == 14))
-    variant = variant == 12 ? 8 : variant == 13 ? 11 : 15;
+  variant = small_variant(variant, P.log2cap, P.nbk, P.p);
   // (the lean window quotient of variant 20 needs window_ns < 2^56, which
   // sa_create enforces; SA_OPT_STAMPS engines keep the production v2 kernels:
   // their workgroup and wave-end stamps are written whenever P.dbg is set)
-  const void *fn = small_fn(P.bintab != nullptr, variant, P.diag != 0 || (P.dbg != nullptr && variant < 8));
+  const bool bt = P.bintab != nullptr;
+  const void *fn = small_fn(bt, variant, P.diag != 0 || (P.dbg != nullptr && variant < 8));
   void *args[] = {const_cast<IngestParams *>(&P)};
-  return hipLaunchKernel(fn, dim3(grid), dim3(lds_variant_block(variant)), args, lds_bytes, s);
+  return hipLaunchKernel(fn, dim3(grid), dim3(small_block(bt, variant)), args, lds_bytes, s);
+}
+
+uint32_t ingest_small_block(bool bt, int variant, uint32_t log2cap, uint32_t nbk, uint32_t p) {
+  return small_block(bt, small_variant(variant, log2cap, nbk, p));
+}
+
+// workgroups of the small-table kernel resident per CU (registers and LDS);
+// 0 when the runtime cannot tell.  After prepare_ingest_small.
+uint32_t ingest_small_blocks_per_cu(bool bt, int variant, uint32_t log2cap, uint32_t nbk, uint32_t p,
+                                    size_t lds_bytes) {
+  variant = small_variant(variant, log2cap, nbk, p);
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, small_fn(bt, variant, false), (int)small_block(bt, variant),
+                                                   lds_bytes) != hipSuccess)
+    return 0;
+  return n > 0 ? (uint32_t)n : 0u;
 }
 
 // the EXPO kernel: specialised for the default small table (2,048 slots, HLL
