@@ -409,12 +409,13 @@ constexpr uint32_t kHbmBlock = 256;
 // with the batched end-of-launch write-back (v2_epilogue); 20 = 19 LEAN; 21 =
 // 20 with the TAG key lookup; 22 = 20 with the tail pool (POOL); 23 / 24 = 20
 // with tile claims (OPT 3 / 2: NBUF claims of one wave tile per round); 25 =
-// 15 with 512-thread workgroups (kLdsHalfBlockVariant: the product's choice for
-// a table with a bin table whose LDS state fits a CU twice, two per CU).
-constexpr int kNumLdsVariants = 26;
-constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
-constexpr int kLdsHalfBlockVariant = 25;
-constexpr uint32_t lds_variant_block(int v) { return v == kLdsHalfBlockVariant ? 512u : 1024u; }
+// 15 with 512-thread workgroups; 26 = 25 with variant 20's options (OPT 1,
+// EPI, LEAN): kLdsHalfBlockVariant, the product's choice for a table with a
+// bin table whose LDS state fits a CU twice (two workgroups per CU).
+constexpr int kNumLdsVariants = 27;
+constexpr int kLdsSpl[kNumLdsVariants] = {4, 4, 2, 2, 4, 4, 2, 2, 2, 2, 4, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2};
+constexpr int kLdsHalfBlockVariant = 26;
+constexpr uint32_t lds_variant_block(int v) { return v == 25 || v == 26 ? 512u : 1024u; }
 constexpr int kLdsPoolVariant = 22;
 // v2 kernels keep u16 LDS counters for a whole launch: spans per workgroup per launch
 constexpr uint32_t kMaxWgSpans = 65532;
@@ -450,6 +451,7 @@ uint32_t ingest_small_blocks_per_cu(bool bt, int variant, uint32_t log2cap, uint
 // reduces and counts)
 hipError_t prepare_ingest_expo_small(size_t lds_bytes);
 hipError_t launch_ingest_expo_small(const IngestParams &P, uint32_t grid, size_t lds_bytes, hipStream_t s);
+uint32_t ingest_expo_blocks_per_cu(uint32_t log2cap, uint32_t p, size_t lds_bytes);
 hipError_t launch_reduce_slabs(uint32_t *slab_cnt, unsigned long long *slab_sum,
                                unsigned long long *gcounts, uint32_t G, uint64_t cap,
                                uint32_t nbk, hipStream_t s);

@@ -465,9 +465,12 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
   } else if (e->expo_small) {
     e->block = 1024;
     e->spl = 2;
-    e->G = e->cus * std::max<uint32_t>(1, (uint32_t)((160 * 1024) / e->lds_bytes));
     if (hipError_t st = sa::prepare_ingest_expo_small(e->lds_bytes); st != hipSuccess)
       return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
+    // one resident round of workgroups (registers and LDS), as the small tables
+    uint32_t per_cu = sa::ingest_expo_blocks_per_cu(e->log2cap, cfg->hll_p, e->lds_bytes);
+    if (per_cu == 0) per_cu = std::max<uint32_t>(1, (uint32_t)((160 * 1024) / e->lds_bytes));
+    e->G = e->cus * per_cu;
     if (hipError_t st = sa::prepare_expo_count(sa::expo_count_lds_bytes(e->cap, cfg->exp_max_size)); st != hipSuccess)
       return bail(fail(e, SA_EDEVICE, std::string("LDS attribute: ") + hipGetErrorString(st)));
     // slab counting: its workgroups (one per ingest workgroup) share a CU as the

@@ -1893,8 +1893,10 @@ uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap_blocks) {
 
 // Small-table kernels.  Product build: the v2 kernel specialised for the
 // default geometry (variant 20: 2,048 slots, 17 buckets, HLL p 14, LEAN), the
-// generic v2 kernel (variant 15) for any other geometry with a bucket bin
-// table, and the linear-threshold kernel for bounds no bin table can hold.
+// generic v2 kernel with 512-thread workgroups (variant 26, two per CU) for
+// other geometries whose LDS state fits a CU twice and with 1,024 threads
+// (variant 15) for the rest with a bucket bin table, and the
+// linear-threshold kernel for bounds no bin table can hold.
 // The laboratory build (SPANAGG_AB) keeps every variant and the diagnostic
 // (ablation) kernels.
 #ifndef SPANAGG_AB
@@ -1903,7 +1905,7 @@ static const void *small_fn(bool bt, int v, bool diag) {
   if (!bt) return (const void *)&ingest_lds_kernel<0, 4, true, false>;
   if (v == 20) return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1, true, true>;
   if (v == kLdsHalfBlockVariant)
-    return (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true, 0, false, false, false, false, false, 512>;
+    return (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true, 1, true, true, false, false, false, 512>;
   return (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true>;
 }
 constexpr int kSmallFnVariants[] = {15, 20, kLdsHalfBlockVariant};
@@ -1952,7 +1954,7 @@ hipError_t prepare_ingest_small(size_t lds_bytes) {
 // the variant that runs for a geometry: the specialised v2 builds are only
 // valid for their compile-time geometry (2,048 slots, 17 buckets, HLL p 14)
 static int small_variant(int variant, uint32_t log2cap, uint32_t nbk, uint32_t p) {
-  if ((variant == 12 || variant == 13 || (variant >= 14 && variant != kLdsHalfBlockVariant)) &&
+  if ((variant == 12 || variant == 13 || (variant >= 14 && variant != 25 && variant != 26)) &&
       !(log2cap == 11 && (nbk + 1) / 2 == 9 && p == 14))
     variant = variant == 12 ? 8 : variant == 13 ? 11 : 15;
   return variant;
@@ -2002,6 +2004,16 @@ hipError_t prepare_ingest_expo_small(size_t lds_bytes) {
       return e;
   return hipSuccess;
 }
+// workgroups of the EXPO kernel resident per CU; 0 when the runtime cannot
+// tell.  After prepare_ingest_expo_small.
+uint32_t ingest_expo_blocks_per_cu(uint32_t log2cap, uint32_t p, size_t lds_bytes) {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, expo_small_fn(log2cap == 11 && p == 14), (int)kLdsBlock,
+                                                   lds_bytes) != hipSuccess)
+    return 0;
+  return n > 0 ? (uint32_t)n : 0u;
+}
+
 hipError_t launch_ingest_expo_small(const IngestParams &P, uint32_t grid, size_t lds_bytes, hipStream_t s) {
   void *args[] = {const_cast<IngestParams *>(&P)};
   return hipLaunchKernel(expo_small_fn(P.log2cap == 11 && P.p == 14), dim3(grid), dim3(kLdsBlock), args, lds_bytes, s);

@@ -95,8 +95,9 @@ for step in "$@"; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_VARIANT=$v \
           run "abvar_v${v}_r$r" 200 python bench.py --workload c2 --sub "" --steps 50 --soak-s 0 --no-filter-off $BQ
       done; done ;;
-    abhalf_*) nps=${step#abhalf_}  # variant 15 against 25 (512-thread workgroups) on a C2 vocabulary of 20 x nps names
-      for r in 1 2 3; do for v in 15 25; do
+    abhalf_*) rest=${step#abhalf_}; nps=${rest%%_*}; vs=${rest#*_}; [ "$vs" = "$rest" ] && vs=15_25
+      # small-table variants (default 15 against 25, 512-thread workgroups) on a C2 vocabulary of 20 x nps names
+      for r in 1 2 3; do for v in ${vs//_/ }; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_VARIANT=$v \
           run "abhalf${nps}_v${v}_r$r" 200 python bench.py --workload c2 --sub "" --steps 50 --soak-s 0 --no-filter-off \
           --names-per-service "$nps" $BQ
