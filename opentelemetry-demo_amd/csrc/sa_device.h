@@ -433,20 +433,31 @@ __device__ __forceinline__ uint32_t window_slot(const IngestParams &P, uint64_t 
 // v_mad_u64_u32 plus a 24-bit multiply-add for the high word (q < 2^24 inside
 // the ring, window_ns < 2^56 -- checked by the host), and the +-1 correction
 // from the remainder's sign and size.
+//
+// Most spans skip the correction: inside the ring the estimate t = delta / W
+// is below n_windows, and its three roundings (the two conversions folded by
+// the fma, the multiply, 1 / W itself) put it within ~5 * 2^-24 * t of the
+// true quotient.  So when t's fraction is more than n_windows * 2^-20 from
+// an integer (|fract(t) - 1/2| < P.win_ok), floor(t) is the exact quotient;
+// the other lanes (~2^-15 of the spans at 16 windows) take the correction.
+// Out-of-ring spans return 0xFFFFFFFF whichever path they take.
 __device__ __forceinline__ uint32_t window_slot_lean(const IngestParams &P, uint64_t end, uint32_t win_mask) {
   const uint64_t delta = end - P.base_ns;  // wraps (huge) for end < base
   float fh, fl;
   asm("v_cvt_f32_u32 %0, %1" : "=v"(fh) : "v"((uint32_t)(delta >> 32)));
   asm("v_cvt_f32_u32 %0, %1" : "=v"(fl) : "v"((uint32_t)delta));
-  const uint32_t q = (uint32_t)(__builtin_fmaf(fh, 4294967296.0f, fl) * P.inv_window);
-  const uint64_t lo = (uint64_t)q * (uint32_t)P.window_ns;  // v_mad_u64_u32
-  uint32_t qh;
-  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(qh) : "v"(q), "s"((uint32_t)(P.window_ns >> 32)), "v"((uint32_t)(lo >> 32)));
-  const uint64_t r = delta - (((uint64_t)qh << 32) | (uint32_t)lo);
-  const uint32_t neg = (uint32_t)((int32_t)(r >> 32) >> 31);  // r < 0: q one too high (then r >= W too)
-  const uint32_t big = r >= P.window_ns ? 1u : 0u;            // r >= W: q one too low
-  const uint32_t qq = q + big + (neg << 1);
-  return delta < P.ring_ns ? ((P.base_slot + qq) & win_mask) : 0xFFFFFFFFu;
+  const float t = __builtin_fmaf(fh, 4294967296.0f, fl) * P.inv_window;
+  uint32_t q = (uint32_t)t;
+  if (__builtin_expect(!(__builtin_fabsf(__builtin_amdgcn_fractf(t) - 0.5f) < P.win_ok), 0)) {
+    const uint64_t lo = (uint64_t)q * (uint32_t)P.window_ns;  // v_mad_u64_u32
+    uint32_t qh;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(qh) : "v"(q), "s"((uint32_t)(P.window_ns >> 32)), "v"((uint32_t)(lo >> 32)));
+    const uint64_t r = delta - (((uint64_t)qh << 32) | (uint32_t)lo);
+    const uint32_t neg = (uint32_t)((int32_t)(r >> 32) >> 31);  // r < 0: q one too high (then r >= W too)
+    const uint32_t big = r >= P.window_ns ? 1u : 0u;            // r >= W: q one too low
+    q = q + big + (neg << 1);
+  }
+  return delta < P.ring_ns ? ((P.base_slot + q) & win_mask) : 0xFFFFFFFFu;
 }
 __device__ __forceinline__ uint32_t window_slot_lean(const IngestParams &P, uint64_t end) {
   return window_slot_lean(P, end, P.win_mask);

@@ -68,6 +68,9 @@ struct IngestParams {
   uint64_t window_ns, win_magic, win_base;
   uint64_t base_ns, ring_ns;  // win_base * window_ns, n_windows * window_ns (< 2^63)
   float inv_window;           // 1 / window_ns
+  // 0.5 - n_windows * 2^-20: a quotient estimate inside the ring whose
+  // fraction lies within this of 1/2 has the exact floor (window_slot_lean)
+  float win_ok;
   uint32_t base_slot;         // win_base & win_mask
   const BinEntry *bintab;     // [kBins] or nullptr (linear thresholds)
   uint32_t win_mask, n_windows;

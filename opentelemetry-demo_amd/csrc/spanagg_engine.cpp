@@ -966,6 +966,7 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   P.base_ns = e->win_base * e->cfg.window_ns;  // < 2^64: checked in sa_window_advance
   P.ring_ns = (uint64_t)e->cfg.n_windows * e->cfg.window_ns;
   P.inv_window = (float)(1.0 / (double)e->cfg.window_ns);
+  P.win_ok = (float)(0.5 - (double)e->cfg.n_windows * 0x1p-20);  // n_windows <= 4096: >= 0.496
   P.base_slot = (uint32_t)(e->win_base & (e->cfg.n_windows - 1));
   P.bintab = e->d_bins;
   P.win_mask = e->cfg.n_windows - 1;

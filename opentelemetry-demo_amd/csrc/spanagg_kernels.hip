@@ -76,104 +76,108 @@ __device__ __forceinline__ void flush_lds(const IngestParams &P, uint32_t cap, u
 }
 
 // End-of-launch write-back of ingest_v2_kernel for a compile-time geometry
-// (UPT slab-count pairs and SPT slab-sum pairs per thread): every global read
-// of the epilogue -- touched slab-count pairs, touched slab sums, the ERROR
-// slab cell, the words of the queued HLL raises and the lower-bound
-// sub-block -- is issued before the first dependent store, so the tail of a
-// workgroup is one memory round trip instead of one per phase (count rounds,
-// sums, ERROR cells, HLL CAS, bound refresh: ~7 in a row).  A stale HLL word
-// only makes the CAS retry; a stale register read for the bound can only lower
-// it, which keeps it a lower bound.
+// (UPT slab-count pairs and SPT slab-sum pairs per thread), in two phases.
+//
+// v2_epi_pre runs in each wave right after its own loop, before the
+// workgroup barrier: it loads the thread's slab-count and slab-sum words (all
+// of them: which ones the launch touched is known only after the barrier) and
+// the lower-bound sub-block of its wave.  The slabs are this workgroup's own
+// (no other workgroup of the launch writes them; the previous launch of the
+// slab set has completed), and a stale register read for the bound can only
+// lower it, which keeps it a lower bound.  Waves end their loops up to ~10 us
+// apart, so these loads land while the last waves still work.
+//
+// v2_epilogue runs after the barrier: LDS counters plus the prefetched words
+// -> dependent stores of the touched words, the ERROR counts as no-return
+// atomics on the workgroup's private ERROR slab, and the queued HLL raises as
+// CAS from the register word each span saw in the loop (queued beside it), so
+// the only memory round trip left after the barrier is a raise's CAS (one
+// more when another workgroup changed the word since).  Before, the slab, ERROR
+// and HLL words were read after the barrier: two round trips.
+template <int UPT, int SPT>
+struct EpiPre {
+  uint4 g[UPT];
+  ulonglong2 sg[SPT];
+  uint4 lv[4];
+};
+
 template <int UPT, int SPT, uint32_t B, typename PT>
+__device__ __forceinline__ void v2_epi_pre(const PT &P, uint32_t cap, uint32_t nw, EpiPre<UPT, SPT> &x) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint4 *scnt = reinterpret_cast<const uint4 *>(P.slab_cnt + (uint64_t)blockIdx.x * cap * 2 * nw);
+#pragma unroll
+  for (int u = 0; u < UPT; ++u) x.g[u] = scnt[tid + u * B];
+  const ulonglong2 *ss = reinterpret_cast<const ulonglong2 *>(P.slab_sum + (uint64_t)blockIdx.x * cap);
+#pragma unroll
+  for (int u = 0; u < SPT; ++u) x.sg[u] = ss[tid + u * B];
+  const uint32_t lbt = P.lb_n ? min(P.lb_n, gridDim.x * (B / 64)) : 0u, gi = blockIdx.x * (B / 64) + wave;
+  const uint32_t sb = gi < lbt ? (uint32_t)(((uint64_t)P.lb_seq * lbt + gi) % P.lb_n) : 0u;
+  const uint32_t quads = gi < lbt ? (1u << P.lb_shift) / 16 : 0u;
+  const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i)
+    x.lv[i] = lane + i * 64 < quads ? src[lane + i * 64] : make_uint4(~0u, ~0u, ~0u, ~0u);
+}
+
+template <int UPT, int SPT, uint32_t B, uint32_t Q, typename PT>
 __device__ __forceinline__ void v2_epilogue(const PT &P, uint32_t cap, uint32_t nw, uint32_t log2cap,
                                             const unsigned long long *lsum, const uint32_t *lcnt,
                                             const uint32_t *etab, bool err_lds, const uint2 *hq,
-                                            uint32_t nq) {
+                                            const uint32_t *hqv, uint32_t nq, const EpiPre<UPT, SPT> &x) {
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const bool slabs = !(P.diag & 8u);
-  // 1. reads
   uint4 *scnt = reinterpret_cast<uint4 *>(P.slab_cnt + (uint64_t)blockIdx.x * cap * 2 * nw);
   const uint2 *lw = reinterpret_cast<const uint2 *>(lcnt);
-  uint2 w[UPT];
-  uint4 g[UPT];
-#pragma unroll
-  for (int u = 0; u < UPT; ++u) w[u] = slabs ? lw[tid + u * B] : make_uint2(0, 0);
-#pragma unroll
-  for (int u = 0; u < UPT; ++u) g[u] = (w[u].x | w[u].y) ? scnt[tid + u * B] : make_uint4(0, 0, 0, 0);
-  ulonglong2 *ss = reinterpret_cast<ulonglong2 *>(P.slab_sum + (uint64_t)blockIdx.x * cap);
-  const ulonglong2 *ls = reinterpret_cast<const ulonglong2 *>(lsum);
-  ulonglong2 sv[SPT], sg[SPT];
-#pragma unroll
-  for (int u = 0; u < SPT; ++u) sv[u] = slabs ? ls[tid + u * B] : make_ulonglong2(0, 0);
-#pragma unroll
-  for (int u = 0; u < SPT; ++u) sg[u] = (sv[u].x | sv[u].y) ? ss[tid + u * B] : make_ulonglong2(0, 0);
-  constexpr uint32_t kE = kErrTab / B;  // ERROR table entries per thread
-  uint32_t e[kE], ev[kE];
-  uint32_t *ecell[kE];
-#pragma unroll
-  for (uint32_t i = 0; i < kE; ++i) {
-    e[i] = err_lds ? etab[tid + i * B] : 0u;
-    ecell[i] = e[i] ? P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e[i] >> 16) - 1)
-                    : nullptr;
-    ev[i] = e[i] ? *ecell[i] : 0u;
-  }
-  constexpr uint32_t kQ = kHllQueue / B;
-  uint2 q[kQ];
-  uint32_t qv[kQ];
-#pragma unroll
-  for (uint32_t i = 0; i < kQ; ++i) {
-    q[i] = tid + i * B < nq ? hq[tid + i * B] : make_uint2(0, 0);
-    qv[i] = q[i].y ? *reinterpret_cast<const uint32_t *>(P.hll + (q[i].x & ~3u)) : 0xFFFFFFFFu;
-  }
-  // the bound sub-block of this wave (as hll_lb_refresh); up to 4 quads per lane
-  const uint32_t lbt = P.lb_n ? min(P.lb_n, gridDim.x * (B / 64)) : 0u, gi = blockIdx.x * (B / 64) + wave;
-  const bool lb = gi < lbt;
-  const uint32_t sb = lb ? (uint32_t)(((uint64_t)P.lb_seq * lbt + gi) % P.lb_n) : 0u;
-  const uint32_t quads = lb ? (1u << P.lb_shift) / 16 : 0u;
-  const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
-  uint4 lv[4];
-#pragma unroll
-  for (uint32_t i = 0; i < 4; ++i)
-    lv[i] = lane + i * 64 < quads ? src[lane + i * 64] : make_uint4(~0u, ~0u, ~0u, ~0u);
-  // 2. dependent stores
 #pragma unroll
   for (int u = 0; u < UPT; ++u) {
-    if (w[u].x | w[u].y) {
-      g[u].x += w[u].x & 0xFFFFu;
-      g[u].y += w[u].x >> 16;
-      g[u].z += w[u].y & 0xFFFFu;
-      g[u].w += w[u].y >> 16;
-      scnt[tid + u * B] = g[u];
+    const uint2 w = slabs ? lw[tid + u * B] : make_uint2(0, 0);
+    if (w.x | w.y) {
+      uint4 g = x.g[u];
+      g.x += w.x & 0xFFFFu;
+      g.y += w.x >> 16;
+      g.z += w.y & 0xFFFFu;
+      g.w += w.y >> 16;
+      scnt[tid + u * B] = g;
     }
   }
+  ulonglong2 *ss = reinterpret_cast<ulonglong2 *>(P.slab_sum + (uint64_t)blockIdx.x * cap);
+  const ulonglong2 *ls = reinterpret_cast<const ulonglong2 *>(lsum);
 #pragma unroll
   for (int u = 0; u < SPT; ++u) {
-    if (sv[u].x | sv[u].y) {
-      sg[u].x += sv[u].x;
-      sg[u].y += sv[u].y;
-      ss[tid + u * B] = sg[u];
-    }
+    const ulonglong2 sv = slabs ? ls[tid + u * B] : make_ulonglong2(0, 0);
+    if (sv.x | sv.y) ss[tid + u * B] = make_ulonglong2(x.sg[u].x + sv.x, x.sg[u].y + sv.y);
   }
+  constexpr uint32_t kE = kErrTab / B;  // ERROR table entries per thread
 #pragma unroll
-  for (uint32_t i = 0; i < kE; ++i)
-    if (e[i]) *ecell[i] = ev[i] + (e[i] & 0xFFFFu);
+  for (uint32_t i = 0; i < kE; ++i) {
+    const uint32_t e = err_lds ? etab[tid + i * B] : 0u;
+    if (e)
+      atomicAdd(P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1),
+                e & 0xFFFFu);
+  }
+  constexpr uint32_t kQ = Q / B;
 #pragma unroll
   for (uint32_t i = 0; i < kQ; ++i) {
-    if (!q[i].y) continue;
-    SA_GLOBAL uint32_t *word = gbl(reinterpret_cast<uint32_t *>(P.hll + (q[i].x & ~3u)));
-    const uint32_t sh = (q[i].x & 3u) * 8;
-    uint32_t old = qv[i];
-    while (((old >> sh) & 0xFFu) < q[i].y) {  // a failed CAS refreshes `old`
-      const uint32_t nw = (old & ~(0xFFu << sh)) | (q[i].y << sh);
+    if (tid + i * B >= nq) continue;
+    const uint2 q = hq[tid + i * B];
+    SA_GLOBAL uint32_t *word = gbl(reinterpret_cast<uint32_t *>(P.hll + (q.x & ~3u)));
+    const uint32_t sh = (q.x & 3u) * 8;
+    uint32_t old = hqv[tid + i * B];
+    while (((old >> sh) & 0xFFu) < q.y) {  // a failed CAS refreshes `old`
+      const uint32_t nw = (old & ~(0xFFu << sh)) | (q.y << sh);
       if (__hip_atomic_compare_exchange_strong(word, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT))
         break;
     }
   }
-  if (lb) {
+  const uint32_t lbt = P.lb_n ? min(P.lb_n, gridDim.x * (B / 64)) : 0u, gi = blockIdx.x * (B / 64) + wave;
+  if (gi < lbt) {
+    const uint32_t sb = (uint32_t)(((uint64_t)P.lb_seq * lbt + gi) % P.lb_n);
+    const uint32_t quads = (1u << P.lb_shift) / 16;
+    const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
     uint32_t mn = 0xFFu;
 #pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) mn = min(mn, min_bytes(lv[i]));
+    for (uint32_t i = 0; i < 4; ++i) mn = min(mn, min_bytes(x.lv[i]));
     for (uint32_t o = lane + 256; o < quads; o += 64) mn = min(mn, min_bytes(src[o]));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
@@ -579,6 +583,12 @@ __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
   uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + cap);
   uint2 *hq = reinterpret_cast<uint2 *>(lcnt + cap * nw);
   uint32_t *hq_n = reinterpret_cast<uint32_t *>(hq + kHllQueue);
+  // the compile-time-geometry epilogue (v2_epilogue) raises from the word each
+  // span saw: the queue region holds kQcap (hoff, rho) pairs, then their words
+  constexpr bool kObs = LC != 0 && NWC != 0 && EPI && !EXPO;
+  constexpr uint32_t kQcap = kObs ? kHllQueue / 2 : kHllQueue;
+  static_assert(!kObs || kQcap * 12 <= kHllQueue * 8, "queue region");
+  uint32_t *hqv = reinterpret_cast<uint32_t *>(hq + kQcap);
   uint32_t *lstat = hq_n + 4;  // EPI: [4] event counts (zero key, bad service, out of ring, dropped)
   BinEntry *lbins = reinterpret_cast<BinEntry *>(hq_n + 8);
   uint32_t *etab = reinterpret_cast<uint32_t *>(lbins + kBins);  // [kErrTab]: (key+1) << 16 | count
@@ -744,8 +754,12 @@ __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
       // zero-extended by a v_and at the loop-carried copy, which waits for it)
       if (((q.hv[j] >> ((q.hoff[j] & 3u) * 8)) & 0xFFu) < q.rho[j]) {
         const uint32_t slot = atomicAdd(hq_n, 1u);
-        if (slot < kHllQueue) hq[slot] = make_uint2(q.hoff[j], q.rho[j]);
-        else cold_hll_raise(q.hoff[j], q.rho[j]);
+        if (slot < kQcap) {
+          hq[slot] = make_uint2(q.hoff[j], q.rho[j]);
+          if constexpr (kObs) hqv[slot] = q.hv[j];
+        } else {
+          cold_hll_raise(q.hoff[j], q.rho[j]);
+        }
       }
     }
   };
@@ -1190,8 +1204,15 @@ __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
   unsigned long long *const dbg = cold_params().dbg;
   const uint64_t wave_loop_end = dbg ? __builtin_amdgcn_s_memrealtime() : 0;
   if (dbg && threadIdx.x == 0) dbg[blockIdx.x * kDbgPerWg + 2] = __builtin_amdgcn_s_memrealtime();
+  constexpr uint32_t kCapC = 1u << (LC ? LC : 1);
+  constexpr int kUpt = kObs ? (int)(kCapC * NWC / 2 / BLK) : 1, kSpt = kObs ? (int)(kCapC / 2 / BLK) : 1;
+  EpiPre<kUpt, kSpt> epre;
+  if constexpr (kObs) {
+    static_assert((kCapC * NWC / 2) % BLK == 0 && (kCapC / 2) % BLK == 0, "epilogue geometry");
+    v2_epi_pre<kUpt, kSpt, BLK>(cold_params(), cap, nw, epre);
+  }
   __syncthreads();
-  const uint32_t nq = *hq_n < kHllQueue ? *hq_n : kHllQueue;
+  const uint32_t nq = *hq_n < kQcap ? *hq_n : kQcap;
   if constexpr (EXPO) {
     // this workgroup's header partials -> its slab (touched slots only; the
     // reduce pass zeroes what it consumed)
@@ -1210,11 +1231,9 @@ __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
     for (uint32_t i = threadIdx.x; i < nq; i += BLK) hll_raise(P.hll + hq[i].x, hq[i].y);
     hll_lb_refresh(P, threadIdx.x >> 6, kWaves);
   } else if constexpr (LC != 0 && NWC != 0 && EPI) {
-    // compile-time geometry: the batched epilogue (one round trip)
-    constexpr uint32_t kCap = 1u << LC;
-    static_assert((kCap * NWC / 2) % BLK == 0 && (kCap / 2) % BLK == 0, "epilogue geometry");
-    v2_epilogue<kCap * NWC / 2 / BLK, kCap / 2 / BLK, BLK>(cold_params(), cap, nw, log2cap, lsum, lcnt, etab,
-                                                                    err_lds, hq, nq);
+    // compile-time geometry: the two-phase epilogue (words prefetched above)
+    v2_epilogue<kUpt, kSpt, BLK, kQcap>(cold_params(), cap, nw, log2cap, lsum, lcnt, etab, err_lds, hq, hqv, nq,
+                                        epre);
   } else {
     flush_lds(P, cap, nw, lsum, lcnt);
     if (err_lds) {  // this workgroup's ERROR counts -> its private slab (plain RMW)

@@ -334,6 +334,59 @@ def test_window_ring_out_of_range_and_advance():
         assert s5.hll.sum() == 0 and s5.cms.sum() == 0
 
 
+@pytest.mark.parametrize("window_ns,n_windows,kcap", [
+    (10_000_000_000, 16, 1000),        # C2 geometry, LDS-mirrored table
+    (10_000_000_000, 16, 1_200_000),   # binned table (C4's scatter)
+    (3, 1024, 1000),                   # odd 3-ns windows, the largest small-path ring
+])
+def test_window_boundaries_vs_oracle(window_ns, n_windows, kcap):
+    """Ends on and next to every window boundary of the ring (the first and
+    last nanosecond of each window, and the ring's own edges): the kernels'
+    window slot takes a float estimate whose floor is exact away from the
+    boundaries and an integer correction near them (sa_device.h,
+    window_slot_lean).  Half the spans are ERROR, so each window's count-min
+    cells and HLL registers pin the window every span went to."""
+    rng = np.random.default_rng(window_ns + n_windows)
+    w0 = 176_722_560 if window_ns > 1000 else 5_000_000_011
+    ks = np.arange(n_windows, dtype=np.uint64)
+    if n_windows > 64:
+        ks = np.unique(np.concatenate([ks[:8], ks[-8:], rng.choice(ks, 48, replace=False)]))
+    offs = np.array(sorted({0, 1, 2, window_ns // 2, window_ns - 2, window_ns - 1}), dtype=np.uint64)
+    offs = offs[offs < window_ns]
+    ends = ((w0 + ks[:, None]) * np.uint64(window_ns) + offs[None, :]).ravel()
+    ends = np.concatenate([ends, (w0 + rng.integers(0, n_windows, 4000, dtype=np.uint64)) * np.uint64(window_ns)
+                           + rng.integers(0, window_ns, 4000, dtype=np.uint64)])
+    ends = np.repeat(ends, 3)  # three spans per end time: distinct series and traces
+    n = len(ends)
+    dur = rng.integers(0, 50_000_000, n, dtype=np.uint64)
+    starts = np.where(ends > dur, ends - dur, 0).astype(np.uint64)
+    b = SpanBatch(rng.integers(1, 41, n, dtype=np.uint64), starts, ends,
+                  rng.integers(1, 2**63, n, dtype=np.uint64), rng.integers(1, 2**63, n, dtype=np.uint64),
+                  pack_meta(np.zeros(n), 2, np.where(rng.random(n) < 0.5, 2, 1)))
+    with Engine(Config(n_services=1, n_windows=n_windows, window_ns=window_ns, key_capacity=kcap)) as e:
+        if n_windows == 16:
+            assert e.stats()["small_table"] == (1 if kcap == 1000 else 0)
+        e.window_advance(w0)
+        e.ingest(b)
+        assert e.stats()["window_out_of_range"] == 0
+        res = e.flush()
+        o = _oracle_run(b, 1, window_ns=window_ns)
+        assert_red_equal(res, o.series())
+        _check_windows(e, o, w0, 1)
+        # the ring's edges: the nanosecond before its first window and its
+        # end are out of range (sketches skip them; RED counts every span),
+        # the first and last nanoseconds inside are not
+        first, last = e.window_read(w0).cms.sum(), e.window_read(w0 + n_windows - 1).cms.sum()
+        edge = np.array([w0 * window_ns - 1, w0 * window_ns, (w0 + n_windows) * window_ns - 1,
+                         (w0 + n_windows) * window_ns], dtype=np.uint64)
+        e.ingest(SpanBatch(np.full(4, 7, np.uint64), edge - 1, edge, np.arange(1, 5, dtype=np.uint64),
+                           np.ones(4, np.uint64), pack_meta(np.zeros(4), 2, 2)))
+        assert e.stats()["window_out_of_range"] == 2
+        assert int(e.flush().calls.sum()) == 4
+        assert e.window_read(w0).cms.sum() == first + 4  # one ERROR span x cms_d rows
+        assert e.window_read(w0 + n_windows - 1).cms.sum() == last + 4
+
+
 def test_high_cardinality_hbm_table_vs_oracle():
     """Config 4 shape at reduced size: HBM key-table path with many keys."""
     batch, khash, w0 = generate_highcard(1_000_000, routes=400, pods=250)

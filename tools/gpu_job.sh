@@ -110,7 +110,7 @@ for step in "$@"; do
     libab_*) rest=${step#libab_}; wl=${rest%%_*}; other=${rest#*_}  # product library against spanagg/lib<other>.so, e.g. libab_c2_spanagg_prediet
       for r in 1 2 3; do for lib in libspanagg "lib$other"; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/$lib.so \
-          run "libab_${wl}_${lib}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 50 --soak-s 0 --no-filter-off \
+          run "libab_${wl}_${lib}$([ "$lib" = libspanagg ] && echo "_vs_$other")_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 50 --soak-s 0 --no-filter-off \
           ${NPS:+--names-per-service $NPS} $BQ
       done; done ;;
     btpair_*) wl=${step#btpair_}  # binned launches aggregated in pairs / alone (laboratory build), rounds interleaved
