@@ -94,6 +94,56 @@ __device__ __forceinline__ void flush_lds(const IngestParams &P, uint32_t cap, u
 // the only memory round trip left after the barrier is a raise's CAS (one
 // more when another workgroup changed the word since).  Before, the slab, ERROR
 // and HLL words were read after the barrier: two round trips.
+// The lower-bound sub-block of this wave (as hll_lb_refresh), loaded before
+// the workgroup barrier: up to 4 quads per lane.
+template <uint32_t B, typename PT>
+__device__ __forceinline__ void epi_bound_pre(const PT &P, uint4 (&lv)[4]) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t lbt = P.lb_n ? min(P.lb_n, gridDim.x * (B / 64)) : 0u, gi = blockIdx.x * (B / 64) + wave;
+  const uint32_t sb = gi < lbt ? (uint32_t)(((uint64_t)P.lb_seq * lbt + gi) % P.lb_n) : 0u;
+  const uint32_t quads = gi < lbt ? (1u << P.lb_shift) / 16 : 0u;
+  const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i)
+    lv[i] = lane + i * 64 < quads ? src[lane + i * 64] : make_uint4(~0u, ~0u, ~0u, ~0u);
+}
+
+// After the barrier: the queued HLL raises, each a CAS from the register word
+// its span saw in the loop (hqv), and the bound from the prefetched quads.
+template <uint32_t B, uint32_t Q, typename PT>
+__device__ __forceinline__ void epi_raise_and_bound(const PT &P, const uint2 *hq, const uint32_t *hqv, uint32_t nq,
+                                                    const uint4 (&lv)[4]) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  constexpr uint32_t kQ = Q / B;
+#pragma unroll
+  for (uint32_t i = 0; i < kQ; ++i) {
+    if (tid + i * B >= nq) continue;
+    const uint2 q = hq[tid + i * B];
+    SA_GLOBAL uint32_t *word = gbl(reinterpret_cast<uint32_t *>(P.hll + (q.x & ~3u)));
+    const uint32_t sh = (q.x & 3u) * 8;
+    uint32_t old = hqv[tid + i * B];
+    while (((old >> sh) & 0xFFu) < q.y) {  // a failed CAS refreshes `old`
+      const uint32_t nw = (old & ~(0xFFu << sh)) | (q.y << sh);
+      if (__hip_atomic_compare_exchange_strong(word, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT))
+        break;
+    }
+  }
+  const uint32_t lbt = P.lb_n ? min(P.lb_n, gridDim.x * (B / 64)) : 0u, gi = blockIdx.x * (B / 64) + wave;
+  if (gi < lbt) {
+    const uint32_t sb = (uint32_t)(((uint64_t)P.lb_seq * lbt + gi) % P.lb_n);
+    const uint32_t quads = (1u << P.lb_shift) / 16;
+    const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
+    uint32_t mn = 0xFFu;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) mn = min(mn, min_bytes(lv[i]));
+    for (uint32_t o = lane + 256; o < quads; o += 64) mn = min(mn, min_bytes(src[o]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+    if (lane == 0) P.hll_lb[sb] = (uint8_t)mn;
+  }
+}
+
 template <int UPT, int SPT>
 struct EpiPre {
   uint4 g[UPT];
@@ -103,20 +153,14 @@ struct EpiPre {
 
 template <int UPT, int SPT, uint32_t B, typename PT>
 __device__ __forceinline__ void v2_epi_pre(const PT &P, uint32_t cap, uint32_t nw, EpiPre<UPT, SPT> &x) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x;
   const uint4 *scnt = reinterpret_cast<const uint4 *>(P.slab_cnt + (uint64_t)blockIdx.x * cap * 2 * nw);
 #pragma unroll
   for (int u = 0; u < UPT; ++u) x.g[u] = scnt[tid + u * B];
   const ulonglong2 *ss = reinterpret_cast<const ulonglong2 *>(P.slab_sum + (uint64_t)blockIdx.x * cap);
 #pragma unroll
   for (int u = 0; u < SPT; ++u) x.sg[u] = ss[tid + u * B];
-  const uint32_t lbt = P.lb_n ? min(P.lb_n, gridDim.x * (B / 64)) : 0u, gi = blockIdx.x * (B / 64) + wave;
-  const uint32_t sb = gi < lbt ? (uint32_t)(((uint64_t)P.lb_seq * lbt + gi) % P.lb_n) : 0u;
-  const uint32_t quads = gi < lbt ? (1u << P.lb_shift) / 16 : 0u;
-  const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
-#pragma unroll
-  for (uint32_t i = 0; i < 4; ++i)
-    x.lv[i] = lane + i * 64 < quads ? src[lane + i * 64] : make_uint4(~0u, ~0u, ~0u, ~0u);
+  epi_bound_pre<B>(P, x.lv);
 }
 
 template <int UPT, int SPT, uint32_t B, uint32_t Q, typename PT>
@@ -124,7 +168,7 @@ __device__ __forceinline__ void v2_epilogue(const PT &P, uint32_t cap, uint32_t 
                                             const unsigned long long *lsum, const uint32_t *lcnt,
                                             const uint32_t *etab, bool err_lds, const uint2 *hq,
                                             const uint32_t *hqv, uint32_t nq, const EpiPre<UPT, SPT> &x) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x;
   const bool slabs = !(P.diag & 8u);
   uint4 *scnt = reinterpret_cast<uint4 *>(P.slab_cnt + (uint64_t)blockIdx.x * cap * 2 * nw);
   const uint2 *lw = reinterpret_cast<const uint2 *>(lcnt);
@@ -155,34 +199,7 @@ __device__ __forceinline__ void v2_epilogue(const PT &P, uint32_t cap, uint32_t 
       atomicAdd(P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1),
                 e & 0xFFFFu);
   }
-  constexpr uint32_t kQ = Q / B;
-#pragma unroll
-  for (uint32_t i = 0; i < kQ; ++i) {
-    if (tid + i * B >= nq) continue;
-    const uint2 q = hq[tid + i * B];
-    SA_GLOBAL uint32_t *word = gbl(reinterpret_cast<uint32_t *>(P.hll + (q.x & ~3u)));
-    const uint32_t sh = (q.x & 3u) * 8;
-    uint32_t old = hqv[tid + i * B];
-    while (((old >> sh) & 0xFFu) < q.y) {  // a failed CAS refreshes `old`
-      const uint32_t nw = (old & ~(0xFFu << sh)) | (q.y << sh);
-      if (__hip_atomic_compare_exchange_strong(word, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT))
-        break;
-    }
-  }
-  const uint32_t lbt = P.lb_n ? min(P.lb_n, gridDim.x * (B / 64)) : 0u, gi = blockIdx.x * (B / 64) + wave;
-  if (gi < lbt) {
-    const uint32_t sb = (uint32_t)(((uint64_t)P.lb_seq * lbt + gi) % P.lb_n);
-    const uint32_t quads = (1u << P.lb_shift) / 16;
-    const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
-    uint32_t mn = 0xFFu;
-#pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) mn = min(mn, min_bytes(x.lv[i]));
-    for (uint32_t o = lane + 256; o < quads; o += 64) mn = min(mn, min_bytes(src[o]));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
-    if (lane == 0) P.hll_lb[sb] = (uint8_t)mn;
-  }
+  epi_raise_and_bound<B, Q>(P, hq, hqv, nq, x.lv);
 }
 
 // Probe the LDS key mirror along the key's sequence from position i0 (the
@@ -585,7 +602,7 @@ __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
   uint32_t *hq_n = reinterpret_cast<uint32_t *>(hq + kHllQueue);
   // the compile-time-geometry epilogue (v2_epilogue) raises from the word each
   // span saw: the queue region holds kQcap (hoff, rho) pairs, then their words
-  constexpr bool kObs = LC != 0 && NWC != 0 && EPI && !EXPO;
+  constexpr bool kObs = (LC != 0 && NWC != 0 && EPI) || EXPO;
   constexpr uint32_t kQcap = kObs ? kHllQueue / 2 : kHllQueue;
   static_assert(!kObs || kQcap * 12 <= kHllQueue * 8, "queue region");
   uint32_t *hqv = reinterpret_cast<uint32_t *>(hq + kQcap);
@@ -1204,12 +1221,16 @@ __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
   unsigned long long *const dbg = cold_params().dbg;
   const uint64_t wave_loop_end = dbg ? __builtin_amdgcn_s_memrealtime() : 0;
   if (dbg && threadIdx.x == 0) dbg[blockIdx.x * kDbgPerWg + 2] = __builtin_amdgcn_s_memrealtime();
+  // the two-phase epilogues' loads, before the barrier (v2_epi_pre)
+  constexpr bool kSlabPre = LC != 0 && NWC != 0 && EPI && !EXPO;
   constexpr uint32_t kCapC = 1u << (LC ? LC : 1);
-  constexpr int kUpt = kObs ? (int)(kCapC * NWC / 2 / BLK) : 1, kSpt = kObs ? (int)(kCapC / 2 / BLK) : 1;
+  constexpr int kUpt = kSlabPre ? (int)(kCapC * NWC / 2 / BLK) : 1, kSpt = kSlabPre ? (int)(kCapC / 2 / BLK) : 1;
   EpiPre<kUpt, kSpt> epre;
-  if constexpr (kObs) {
+  if constexpr (kSlabPre) {
     static_assert((kCapC * NWC / 2) % BLK == 0 && (kCapC / 2) % BLK == 0, "epilogue geometry");
     v2_epi_pre<kUpt, kSpt, BLK>(cold_params(), cap, nw, epre);
+  } else if constexpr (EXPO) {
+    epi_bound_pre<BLK>(cold_params(), epre.lv);
   }
   __syncthreads();
   const uint32_t nq = *hq_n < kQcap ? *hq_n : kQcap;
@@ -1219,17 +1240,14 @@ __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
     XHdr *xs = P.xslab + (uint64_t)blockIdx.x * cap;
     for (uint32_t sl = threadIdx.x; sl < cap; sl += BLK)
       if (const uint32_t c = xcnt[sl]) xs[sl] = XHdr{c, xzero[sl], lsum[sl], xminx[sl], xmax[sl]};
-    if (err_lds) {  // this workgroup's ERROR counts -> its private slab (plain RMW)
+    if (err_lds) {  // this workgroup's ERROR counts -> its private slab (no-return atomics)
       for (uint32_t t = threadIdx.x; t < kErrTab; t += BLK) {
         const uint32_t e = etab[t];
-        if (e) {
-          uint32_t *cell = P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1);
-          *cell += e & 0xFFFFu;
-        }
+        if (e) atomicAdd(P.errslab + (uint64_t)blockIdx.x * ((uint64_t)P.n_windows << log2cap) + ((e >> 16) - 1),
+                         e & 0xFFFFu);
       }
     }
-    for (uint32_t i = threadIdx.x; i < nq; i += BLK) hll_raise(P.hll + hq[i].x, hq[i].y);
-    hll_lb_refresh(P, threadIdx.x >> 6, kWaves);
+    epi_raise_and_bound<BLK, kQcap>(cold_params(), hq, hqv, nq, epre.lv);
   } else if constexpr (LC != 0 && NWC != 0 && EPI) {
     // compile-time geometry: the two-phase epilogue (words prefetched above)
     v2_epilogue<kUpt, kSpt, BLK, kQcap>(cold_params(), cap, nw, log2cap, lsum, lcnt, etab, err_lds, hq, hqv, nq,
