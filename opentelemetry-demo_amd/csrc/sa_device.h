@@ -554,5 +554,38 @@ __device__ __forceinline__ void hll_lb_refresh(const IngestParams &P, uint32_t w
   if (lane == 0) P.hll_lb[sb] = (uint8_t)mn;
 }
 
+// hll_lb_refresh in two phases, for epilogues that issue their loads early:
+// hll_lb_pre loads the wave's sub-block (up to 4 quads per lane; a stale
+// register read can only lower the bound, which keeps it a lower bound),
+// hll_lb_finish reduces it (reading any quads past the first 256) and stores
+// the bound.  B = the workgroup's threads.
+template <uint32_t B, typename PT>
+__device__ __forceinline__ void hll_lb_pre(const PT &P, uint4 (&lv)[4]) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t lbt = P.lb_n ? min(P.lb_n, gridDim.x * (B / 64)) : 0u, gi = blockIdx.x * (B / 64) + wave;
+  const uint32_t sb = gi < lbt ? (uint32_t)(((uint64_t)P.lb_seq * lbt + gi) % P.lb_n) : 0u;
+  const uint32_t quads = gi < lbt ? (1u << P.lb_shift) / 16 : 0u;
+  const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i)
+    lv[i] = lane + i * 64 < quads ? src[lane + i * 64] : make_uint4(~0u, ~0u, ~0u, ~0u);
+}
+template <uint32_t B, typename PT>
+__device__ __forceinline__ void hll_lb_finish(const PT &P, const uint4 (&lv)[4]) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t lbt = P.lb_n ? min(P.lb_n, gridDim.x * (B / 64)) : 0u, gi = blockIdx.x * (B / 64) + wave;
+  if (gi >= lbt) return;
+  const uint32_t sb = (uint32_t)(((uint64_t)P.lb_seq * lbt + gi) % P.lb_n);
+  const uint32_t quads = (1u << P.lb_shift) / 16;
+  const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
+  uint32_t mn = 0xFFu;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) mn = min(mn, min_bytes(lv[i]));
+  for (uint32_t o = lane + 256; o < quads; o += 64) mn = min(mn, min_bytes(src[o]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+  if (lane == 0) P.hll_lb[sb] = (uint8_t)mn;
+}
+
 }  // namespace
 }  // namespace sa

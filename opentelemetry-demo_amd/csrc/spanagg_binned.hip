@@ -404,6 +404,10 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
   }
   hll_settle(pend2);
   hll_settle(pend);
+  // the wave's bound sub-block, loaded now (hll_lb_pre): it lands during the
+  // stage flush and the overflow table's key lookups below
+  uint4 lbv[4];
+  hll_lb_pre<kBtBlock>(P, lbv);
   bt_stamp(P, sbase, 2);
   // partial stages, then this workgroup's region fills
   for (uint32_t b = threadIdx.x; b < kPartBins; b += kBtBlock) {
@@ -415,6 +419,19 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
     }
   }
   __syncthreads();
+  // the queued HLL raises' register words, read now (the queue is final after
+  // the barrier above) and CAS-raised at the end: the reads overlap the
+  // overflow table's lookups instead of adding a round trip
+  const uint32_t nq = min(hq_n[0], kBtHq);
+  constexpr uint32_t kQ = (kBtHq + kBtBlock - 1) / kBtBlock;
+  uint32_t qv[kQ];
+#pragma unroll
+  for (uint32_t i = 0; i < kQ; ++i) {
+    const uint32_t t = threadIdx.x + i * kBtBlock;
+    qv[i] = t < nq ? __hip_atomic_load(reinterpret_cast<const uint32_t *>(P.hll + (hq[t].x & ~3u)), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT)
+                   : 0u;
+  }
   for (uint32_t b = threadIdx.x; b < kPartBins; b += kBtBlock)
     P.bt_cnt[(uint64_t)b * P.bt_grid + blockIdx.x] = min((rcnw[b >> 1] >> ((b & 1u) * 16)) & 0xFFFFu, region);
   __syncthreads();
@@ -460,8 +477,21 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
         for (uint32_t i = 0; i < e.y; ++i) bt_cms_add(kp, ws, hkey[h] * P.kinv);
     }
   }
-  const uint32_t nq = min(hq_n[0], kBtHq);
-  for (uint32_t i = threadIdx.x; i < nq; i += kBtBlock) hll_raise(P.hll + hq[i].x, hq[i].y);
+#pragma unroll
+  for (uint32_t i = 0; i < kQ; ++i) {
+    const uint32_t t = threadIdx.x + i * kBtBlock;
+    if (t >= nq) continue;
+    const uint2 q = hq[t];
+    SA_GLOBAL uint32_t *word = gbl(reinterpret_cast<uint32_t *>(P.hll + (q.x & ~3u)));
+    const uint32_t sh = (q.x & 3u) * 8;
+    uint32_t old = qv[i];
+    while (((old >> sh) & 0xFFu) < q.y) {  // a failed CAS refreshes `old`
+      const uint32_t nw = (old & ~(0xFFu << sh)) | (q.y << sh);
+      if (__hip_atomic_compare_exchange_strong(word, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT))
+        break;
+    }
+  }
   n_drop = wave_sum(n_drop);
   n_filt = wave_sum(n_filt);
   if (lane == 0) {
@@ -473,7 +503,7 @@ __global__ __launch_bounds__(kBtBlock) void bt_scatter2_kernel(IngestParams P) {
     if (n_oor) atomicAdd(&P.stats[kStatWindowOOR], (unsigned long long)n_oor);
     if (n_drop) atomicAdd(&P.stats[kStatDropped], (unsigned long long)n_drop);
   }
-  hll_lb_refresh(P, wave, kWaves);
+  hll_lb_finish<kBtBlock>(P, lbv);
   bt_stamp(P, sbase, 3);
 }
 
@@ -707,6 +737,20 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 1024 ? 8 : 6) void bt_aggregate3_ke
       }
     }
   }
+  // the rows of the slots the bin held at setup, loaded by each wave right
+  // after its records, before the barrier: waves end their records at
+  // different times, so these loads land while the last ones work, and the
+  // write-back below reads HBM only for keys new to the bin (a slot that held
+  // a key keeps it; the rows are this aggregate's alone)
+  uint4 *rows = reinterpret_cast<uint4 *>(P.gcounts) + ((uint64_t)bin << log2sb) * (kRowBytes / 16);
+  uint4 rpre[kMaxPer][2];
+#pragma unroll
+  for (int u = 0; u < kMaxPer; ++u) {
+    const uint32_t s = tid + u * BLOCK;
+#pragma unroll
+    for (uint32_t q = 0; q < 2; ++q)
+      rpre[u][q] = s < sb && orig[u] != 0 && !(MODE & 2) ? rows[(uint64_t)s * 2 + q] : make_uint4(0, 0, 0, 0);
+  }
   n_drop = wave_sum(n_drop);
   if (lane == 0 && n_drop) atomicAdd(&misc[0], n_drop);
   __syncthreads();
@@ -726,7 +770,6 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 1024 ? 8 : 6) void bt_aggregate3_ke
   //    left alone; lsum[s] then carries the relocated slot for the ERROR list.
   if (MODE & 2) return;
   const uint32_t nbk = P.nbk;
-  uint4 *rows = reinterpret_cast<uint4 *>(P.gcounts) + ((uint64_t)bin << log2sb) * (kRowBytes / 16);
   constexpr unsigned long long kMoved = 1ULL << 63;  // lsum[s] after the write-back: kMoved | new slot (or kNotFound)
   uint4 rv[kMaxPer][2];
   bool touched[kMaxPer];
@@ -751,7 +794,9 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 1024 ? 8 : 6) void bt_aggregate3_ke
     const bool own = hs[u] == ((bin << log2sb) | s);
 #pragma unroll
     for (uint32_t q = 0; q < 2; ++q)
-      rv[u][q] = touched[u] && own ? rows[(uint64_t)s * 2 + q] : make_uint4(0, 0, 0, 0);
+      rv[u][q] = !(touched[u] && own) ? make_uint4(0, 0, 0, 0)
+                 : orig[u] != 0  ? rpre[u][q]
+                                 : rows[(uint64_t)s * 2 + q];
   }
   uint32_t n_lost = 0;
 #pragma unroll

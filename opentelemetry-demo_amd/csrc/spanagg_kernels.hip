@@ -94,26 +94,12 @@ __device__ __forceinline__ void flush_lds(const IngestParams &P, uint32_t cap, u
 // the only memory round trip left after the barrier is a raise's CAS (one
 // more when another workgroup changed the word since).  Before, the slab, ERROR
 // and HLL words were read after the barrier: two round trips.
-// The lower-bound sub-block of this wave (as hll_lb_refresh), loaded before
-// the workgroup barrier: up to 4 quads per lane.
-template <uint32_t B, typename PT>
-__device__ __forceinline__ void epi_bound_pre(const PT &P, uint4 (&lv)[4]) {
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  const uint32_t lbt = P.lb_n ? min(P.lb_n, gridDim.x * (B / 64)) : 0u, gi = blockIdx.x * (B / 64) + wave;
-  const uint32_t sb = gi < lbt ? (uint32_t)(((uint64_t)P.lb_seq * lbt + gi) % P.lb_n) : 0u;
-  const uint32_t quads = gi < lbt ? (1u << P.lb_shift) / 16 : 0u;
-  const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
-#pragma unroll
-  for (uint32_t i = 0; i < 4; ++i)
-    lv[i] = lane + i * 64 < quads ? src[lane + i * 64] : make_uint4(~0u, ~0u, ~0u, ~0u);
-}
-
 // After the barrier: the queued HLL raises, each a CAS from the register word
 // its span saw in the loop (hqv), and the bound from the prefetched quads.
 template <uint32_t B, uint32_t Q, typename PT>
 __device__ __forceinline__ void epi_raise_and_bound(const PT &P, const uint2 *hq, const uint32_t *hqv, uint32_t nq,
                                                     const uint4 (&lv)[4]) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x;
   constexpr uint32_t kQ = Q / B;
 #pragma unroll
   for (uint32_t i = 0; i < kQ; ++i) {
@@ -129,19 +115,7 @@ __device__ __forceinline__ void epi_raise_and_bound(const PT &P, const uint2 *hq
         break;
     }
   }
-  const uint32_t lbt = P.lb_n ? min(P.lb_n, gridDim.x * (B / 64)) : 0u, gi = blockIdx.x * (B / 64) + wave;
-  if (gi < lbt) {
-    const uint32_t sb = (uint32_t)(((uint64_t)P.lb_seq * lbt + gi) % P.lb_n);
-    const uint32_t quads = (1u << P.lb_shift) / 16;
-    const uint4 *src = reinterpret_cast<const uint4 *>(P.hll + ((uint64_t)sb << P.lb_shift));
-    uint32_t mn = 0xFFu;
-#pragma unroll
-    for (uint32_t i = 0; i < 4; ++i) mn = min(mn, min_bytes(lv[i]));
-    for (uint32_t o = lane + 256; o < quads; o += 64) mn = min(mn, min_bytes(src[o]));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
-    if (lane == 0) P.hll_lb[sb] = (uint8_t)mn;
-  }
+  hll_lb_finish<B>(P, lv);
 }
 
 template <int UPT, int SPT>
@@ -160,7 +134,7 @@ __device__ __forceinline__ void v2_epi_pre(const PT &P, uint32_t cap, uint32_t n
   const ulonglong2 *ss = reinterpret_cast<const ulonglong2 *>(P.slab_sum + (uint64_t)blockIdx.x * cap);
 #pragma unroll
   for (int u = 0; u < SPT; ++u) x.sg[u] = ss[tid + u * B];
-  epi_bound_pre<B>(P, x.lv);
+  hll_lb_pre<B>(P, x.lv);
 }
 
 template <int UPT, int SPT, uint32_t B, uint32_t Q, typename PT>
@@ -1230,7 +1204,7 @@ __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
     static_assert((kCapC * NWC / 2) % BLK == 0 && (kCapC / 2) % BLK == 0, "epilogue geometry");
     v2_epi_pre<kUpt, kSpt, BLK>(cold_params(), cap, nw, epre);
   } else if constexpr (EXPO) {
-    epi_bound_pre<BLK>(cold_params(), epre.lv);
+    hll_lb_pre<BLK>(cold_params(), epre.lv);
   }
   __syncthreads();
   const uint32_t nq = *hq_n < kQcap ? *hq_n : kQcap;
