@@ -93,7 +93,9 @@ __device__ __forceinline__ void flush_lds(const IngestParams &P, uint32_t cap, u
 // CAS from the register word each span saw in the loop (queued beside it), so
 // the only memory round trip left after the barrier is a raise's CAS (one
 // more when another workgroup changed the word since).  Before, the slab, ERROR
-// and HLL words were read after the barrier: two round trips.
+// and HLL words were read after the barrier: two round trips.  (The EXPO
+// kernel's epilogue shares the raise and bound halves.)
+
 // After the barrier: the queued HLL raises, each a CAS from the register word
 // its span saw in the loop (hqv), and the bound from the prefetched quads.
 template <uint32_t B, uint32_t Q, typename PT>
