@@ -7,7 +7,12 @@ config 2 shape: 10M spans, ~500 (service, span) pairs -> <=1,500 series,
 default buckets, per-service HLL p=14 + count-min 4x2048 over 10 s windows).
 With N ranks every rank aggregates its own trace-id shard (weak scaling; no
 collective on the data path); after the timed region the ranks merge their
-partials once over RCCL (reported as merge_ms, outside `value`).
+partials once over RCCL (reported as merge_ms, outside `value`).  Under
+torch.distributed.run (WORLD_SIZE set) each process is one rank; a bare
+`python3 bench.py --gpus N` starts the N rank processes itself (launch_ranks:
+child processes, before this one imports torch) and passes rank 0's line on.
+The line's `distributed` object records the backend, the process group's
+world size (checked equal to N) and every rank's own figures.
 
 Steps alternate over `--streams` (default 2) launch streams: the engine keeps
 two sets of per-workgroup slabs, so a launch waits only for the launch two
@@ -396,6 +401,8 @@ def run_workload(name, n, args, device, rank, world, barrier):
                 "note": f"trace-id variants repeat every {len(variants)} launches here, so the window's HLL "
                         "registers saturate and their raises idle: the rate of a saturated window, not a "
                         "figure of the kernel on fresh traces (value's timed steps are all fresh variants)"}
+    own = {"rank": rank, "device": str(device), "ms_per_step": elapsed * 1e3 / max(1, args.steps),
+           "kernel_ms": kernel_ms, "device_ms_per_step": device_ms}
     if world > 1:
         t = torch.tensor([elapsed, kernel_ms, kernel_ms_bracketed, device_ms, cold_ms], dtype=torch.float64,
                          device=device)
@@ -413,6 +420,11 @@ def run_workload(name, n, args, device, rank, world, barrier):
         red = eng.flush_exp() if exp_max else eng.flush()
     torch.cuda.synchronize(device)
     merge_ms = (time.perf_counter() - tm) * 1e3
+    own["merge_ms"] = merge_ms
+    per_rank = [own]
+    if world > 1:  # every rank's own figures (value uses the max over ranks)
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, own)
     st = eng.stats()
     calls = int(red.count.sum()) if exp_max else int(red.calls.sum())
     calls_ok = calls == launches[0] * n * world - st["zero_key"] * (1 if world == 1 else world)
@@ -424,7 +436,7 @@ def run_workload(name, n, args, device, rank, world, barrier):
            "wl": wl, "batch": batch, "eng": eng, "first_window": first_window, "elapsed": elapsed,
            "kernel_ms": kernel_ms, "kernel_ms_bracketed": kernel_ms_bracketed, "device_ms": device_ms,
            "cold_ms": cold_ms, "settle_ms": settle_ms, "sustained": soak,
-           "merge_ms": merge_ms,
+           "merge_ms": merge_ms, "per_rank": per_rank,
            "calls_ok": calls_ok, "enqueue_s": enqueue_s, "streams": len(streams), "variants": n_var,
            "launches": launches[0], "hll_p": 14,
            "hll_filtered_frac": st["hll_filtered"] / max(1, launches[0] * n)}
@@ -558,6 +570,65 @@ def roofline(name, n, r, traffic_path=None):
     return roof
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv, script=None, timeout=None, env=None) -> int:
+    """`bench.py --gpus N` without an outer launcher: start N rank processes of
+    `script` (default this file) with `argv`, one per GPU (RANK = LOCAL_RANK =
+    i, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free port), as
+    torch.distributed.run would.  This parent never imports torch or touches a
+    GPU (it only spawns and waits), so no process that initialised the GPU is
+    ever replaced.  Rank 0's stdout passes through to ours (its one JSON
+    line); the other ranks' stdout goes to our stderr.  Returns 0 when every
+    rank exits 0; otherwise the first failing rank's code (or 1), after
+    terminating the ranks still running, so a rank that dies while the others
+    wait in a collective cannot hang the job."""
+    script = script or os.path.abspath(__file__)
+    base = dict(os.environ if env is None else env)
+    base.update({"WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                 "MASTER_PORT": str(free_port()), "GROUP_RANK": "0", "NODE_RANK": "0"})
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    base["SPANAGG_BENCH_LAUNCHER"] = "bench.py (one child process per rank)"
+    procs = []
+    for i in range(n):
+        e = dict(base, RANK=str(i), LOCAL_RANK=str(i))
+        procs.append(subprocess.Popen([sys.executable, "-u", script, *argv], env=e,
+                                      stdout=None if i == 0 else sys.stderr, start_new_session=True))
+    def signal_live(sig):
+        for j in live:
+            try:
+                os.killpg(procs[j].pid, sig)
+            except ProcessLookupError:
+                pass
+
+    t0, rc, kill_at = time.monotonic(), 0, None
+    live = list(range(n))
+    while live:
+        for i in list(live):
+            code = procs[i].poll()
+            if code is None:
+                continue
+            live.remove(i)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench: rank {i} exited with {code}; stopping the other ranks", file=sys.stderr)
+                signal_live(15)
+                kill_at = time.monotonic() + 20  # SIGKILL what SIGTERM did not end
+        now = time.monotonic()
+        if timeout is not None and live and now - t0 > timeout and rc == 0:
+            print(f"bench: ranks {live} still running after {timeout} s; stopping them", file=sys.stderr)
+            rc, kill_at = 124, now
+        if kill_at is not None and live and now >= kill_at:
+            signal_live(9)
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -600,6 +671,10 @@ def main():
     if args.cpu_worker is not None:  # child of cpu_baseline_multicore (no GPU use)
         cpu_worker(args.cpu_worker, args.cpu_seconds)
         return 0
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no outer launcher: start the N rank processes ourselves (before any
+        # torch import or GPU call in this process) and pass rank 0's line on
+        return launch_ranks(args.gpus, sys.argv[1:])
 
     import torch
     import torch.distributed as dist
@@ -608,19 +683,23 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("run N>1 under torch.distributed.run (one process per GPU)", file=sys.stderr)
-            return 2
+        print(f"bench: WORLD_SIZE {world} but --gpus {args.gpus}", file=sys.stderr)
+        return 2
     # SPANAGG_BENCH_ONE_DEVICE=1 rehearses the N-rank path on a one-GPU box:
     # every rank on cuda:0, gloo collectives (never for a reported number)
     one_dev = os.environ.get("SPANAGG_BENCH_ONE_DEVICE") == "1"
     torch.cuda.set_device(0 if one_dev else local_rank)
     device = torch.device("cuda", 0 if one_dev else local_rank)
+    backend = None
     if world > 1:
         if one_dev:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=device)
+        backend = dist.get_backend()
+        if dist.get_world_size() != args.gpus:
+            print(f"bench: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}", file=sys.stderr)
+            return 2
 
     def barrier():
         if world > 1:
@@ -696,6 +775,9 @@ def main():
             "trace_variants": main_r["variants"],
             "hll_filtered_frac": main_r["hll_filtered_frac"],
             "merge_ms": main_r["merge_ms"], "calls_check": main_r["calls_ok"],
+            "distributed": {"world_size": world, "backend": backend,
+                            "launcher": os.environ.get("SPANAGG_BENCH_LAUNCHER", "external" if world > 1 else None),
+                            "per_rank": main_r["per_rank"]},
             "host_enqueue_us_per_step": main_r["enqueue_s"] * 1e6 / max(1, args.steps),
         }
         result.update(subs)

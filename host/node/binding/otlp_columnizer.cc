@@ -1200,6 +1200,9 @@ Result Columnizer::columnize(const uint8_t *buf, size_t len) {
 
 Result Columnizer::columnize_into(const uint8_t *buf, size_t len, Cols &out) {
   if (cache_.gen != gen_) cache_.clear(), cache_.gen = gen_;
+  // the second level too: a remap or forget since the last batch filled it
+  // (both bump gen_) may have changed the series an entry names
+  if (shared_.gen != gen_) shared_.clear(), shared_.gen = gen_;
   Result res;
   Undo undo;
   const size_t n0 = out.size();

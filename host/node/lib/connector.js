@@ -70,6 +70,8 @@ const EVENT_KEY_PREFIX = '\u0002events\u0000';
 // keep separate series (upstream: separate sums and histograms maps), keyed
 // in their own namespaces
 const CALLS_KEY_PREFIX = '\u0003calls\u0000';
+// series kinds whose records feed the sketches (see _pushCalls, _pushEvent)
+const SKETCH_KINDS = new Set(['span', 'overflow', 'hist', 'hist-overflow']);
 const HIST_KEY_PREFIX = '\u0004hist\u0000';
 
 const NONE = [];
@@ -225,6 +227,7 @@ class SpanMetricsConnector {
     this.collisions = 0;          // series ids re-salted after a 64-bit collision
     this._verifyingNative = false;
     this.eventRecords = 0;
+    this.callsRecords = 0;  // calls-series records of split keys (_pushCalls)
     this.nativeRemaps = 0;  // native series ids the host dictionary replaced (collisions)
     this.ticker = null;
   }
@@ -528,7 +531,7 @@ class SpanMetricsConnector {
           if (this.cfg.exemplars) this._exemplar(sid, span);
           if (this.cfg.splitKeys) {  // the calls series gets the span as a second record
             const code = span.status ? span.status.code : 0;
-            this._pushSpan(this._splitId(res, service, span, resAttrs, spanAttrs, code, CALLS_KEY_PREFIX), span, svcId);
+            this._pushCalls(this._splitId(res, service, span, resAttrs, spanAttrs, code, CALLS_KEY_PREFIX), span);
           }
           const i = cols.n;
           cols.keyHash[i] = sid;
@@ -673,6 +676,29 @@ class SpanMetricsConnector {
     const st = code >= 0 && code <= 3 ? code : 3;
     cols.meta[i] = (svcId | (kind << 16) | (st << 19)) >>> 0;
     cols.n = i + 1;
+    if (cols.n === cols.cap) this._drain();
+  }
+
+  /**
+   * calls_dimensions / histogram.dimensions: the calls series' record of a
+   * span.  It carries the span's duration (the engine counts it into the
+   * series' calls) but the out-of-range service id of the event records and no
+   * kind or status bits, so the sketches see each span once, through its
+   * histogram series' record: its HLL raise and, for an ERROR span, its
+   * count-min cells.  Counted in callsRecords (stats() takes these records
+   * out of the engine's span count).
+   */
+  _pushCalls(sid, span) {
+    const cols = this.cols;
+    const i = cols.n;
+    cols.keyHash[i] = sid;
+    cols.startNs[i] = BigInt.asUintN(64, BigInt(span.startTimeUnixNano || 0));
+    cols.endNs[i] = BigInt.asUintN(64, BigInt(span.endTimeUnixNano || 0));
+    cols.traceW0[i] = 0n;
+    cols.traceW1[i] = 0n;
+    cols.meta[i] = 0xFFFF;
+    cols.n = i + 1;
+    this.callsRecords += 1;
     if (cols.n === cols.cap) this._drain();
   }
 
@@ -915,7 +941,9 @@ class SpanMetricsConnector {
     const topErrors = (k = this.cfg.topK) => {
       const out = [];
       for (const s of this.series.values()) {
-        if (s.status !== 2) continue;
+        // the series whose records carry the span's status: never a calls-only
+        // or event series (their records touch no sketch)
+        if (s.status !== 2 || !SKETCH_KINDS.has(s.kind)) continue;
         const n = errorCount(s.sid);
         if (n > 0) out.push({ sid: s.sid, key: s.keyStr, attributes: s.dpAttrs, errors: n });
       }
@@ -947,7 +975,12 @@ class SpanMetricsConnector {
 
   stats() {
     const s = this.addon.stats(this.handle);
-    return Object.assign(s, { resources: this.resources.size, series: this.series.size,
+    // the engine counts records: a span's own, plus the auxiliary ones (event
+    // records, split keys' calls records), which carry service id 0xFFFF
+    const aux = BigInt(this.eventRecords + this.callsRecords);
+    if (typeof s.spans === 'bigint') s.records = s.spans, s.spans -= aux;
+    if (typeof s.invalidService === 'bigint') s.invalidService -= aux;
+    return Object.assign(s, { callsRecords: this.callsRecords, resources: this.resources.size, series: this.series.size,
       services: this.services.size, droppedFlushes: this.droppedFlushes, droppedSpans: this.droppedSpans,
       collisions: this.collisions,
       eventRecords: this.eventRecords, nativeRequests: this.nativeRequests, jsRequests: this.jsRequests,

@@ -65,8 +65,10 @@ class FakeAddon {
     this.batches.push(copy);
     const nb = this.cfg.bounds.length + 1;
     const p = this.cfg.hllP;
+    this.nRecords = (this.nRecords || 0n) + BigInt(b.keyHash.length);
     for (let i = 0; i < b.keyHash.length; i++) {
       const sid = b.keyHash[i];
+      if ((b.meta[i] & 0xFFFF) >= this.cfg.nServices) this.nInvalid = (this.nInvalid || 0n) + 1n;
       const d = b.endNs[i] > b.startNs[i] ? b.endNs[i] - b.startNs[i] : 0n;
       let r = this.red.get(sid);
       if (!r) {
@@ -153,7 +155,9 @@ class FakeAddon {
     for (const wid of [...this.windows.keys()]) if (wid < base) this.windows.delete(wid);
     this.base = base;
   }
-  stats() { return { spans: 0n, droppedTableFull: this.dropped || 0n }; }
+  stats() {
+    return { spans: this.nRecords || 0n, invalidService: this.nInvalid || 0n, droppedTableFull: this.dropped || 0n };
+  }
 }
 
 /**

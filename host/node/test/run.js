@@ -363,6 +363,22 @@ for (const name of ['calls_and_histogram_dimensions', 'histogram_disable']) {
     assert.deepStrictEqual(hist, want(c.expected.histogram));
     if (name === 'histogram_disable') {
       assert.ok(out.resourceMetrics.every((rm) => rm.scopeMetrics[0].metrics.every((m) => !m.histogram)));
+    } else {
+      // the sketches see each span once: every count-min row holds the
+      // window's ERROR spans once, and the heavy hitters are the histogram
+      // series (never the calls series too); the engine's span count is the
+      // spans', its second (calls) records taken out
+      const w = conn.windowSketch(Number(span('x').endTimeUnixNano / 10000000000n));
+      for (let j = 0; j < w.raw.cmsD; j++) {
+        const row = w.raw.cms.subarray(j * w.raw.cmsW, (j + 1) * w.raw.cmsW);
+        assert.strictEqual(row.reduce((a, x) => a + x, 0), c.expected.window_error_spans);
+      }
+      const top = w.topErrors().map((e) => [JSON.stringify(e.attributes.map((a) => [a.key, a.value.value])), e.errors]);
+      assert.deepStrictEqual(top.sort(), want(c.expected.top_errors));
+      const st = conn.stats();
+      assert.strictEqual(st.spans, BigInt(c.spans.length));
+      assert.strictEqual(st.callsRecords, c.spans.length);
+      assert.strictEqual(st.invalidService, 0n);
     }
   });
 }
@@ -703,6 +719,44 @@ test('native columnizer: consumeTracesBatch on worker threads == consumeTraces o
     assert.strictEqual(batch.stats.jsRequests, 1);  // the non-UTF-8 request
     assert.strictEqual(batch.stats.eventRecords, one.stats.eventRecords);
     assert.strictEqual(batch.stats.nativeRequests, one.stats.nativeRequests);
+  }
+});
+
+test('native columnizer: after a threaded batch, a forget or remap is seen by single-request calls', () => {
+  // the threaded batch fills the columnizer's shared signature cache; an LRU
+  // eviction (columnizerForget at export) or a collision remap then changes
+  // the series its entries name, and a later one-request call must not
+  // return the stale id (its spans would land on a series the host no
+  // longer tracks and vanish from the export)
+  const reqs = mixedRequests().concat(eventRequests()).map((r) => otlp.encodeTraces(r));
+  for (const [cfg, collide] of [[{ resource_metrics_cache_size: 1 }, false], [{ resource_metrics_cache_size: 2 }, true],
+    [{}, true], [{ resource_metrics_cache_size: 1, dimensions: [{ name: 'k8s.pod.name' }] }, true]]) {
+    const out = [];
+    for (const native of [true, false]) {
+      const addon = native ? new NativeColumnizerFakeAddon() : new FakeAddon();
+      addon.collide = collide;
+      const t = { now: 1000n };
+      const conn = new SpanMetricsConnector(Object.assign({ batch_size: 16, columnizer_threads: 4 }, cfg),
+        { addon, rules: DEMO_SPAN_NAME_RULES, native, clock: () => (t.now += 1n) });
+      const real = keys.seriesHashSeeded;
+      if (collide) keys.seriesHashSeeded = (rh, k, seed) => (seed === 0n ? 42n : real(rh, k, seed));
+      const exports = [];
+      try {
+        const errs = conn.consumeTracesBatch(reqs.slice(0, 8));
+        assert.ok(errs.every((e) => e === null));
+        exports.push(otlp.encodeMetrics(conn.exportMetrics()).toString('hex'));
+        for (const r of reqs) conn.consumeTraces(r);  // one request at a time (the T <= 1 path)
+        exports.push(otlp.encodeMetrics(conn.exportMetrics()).toString('hex'));
+        assert.ok(conn.consumeTracesBatch(reqs.slice(3, 12)).every((e) => e === null));
+        for (const r of reqs.slice(0, 5)) conn.consumeTraces(r);
+        exports.push(otlp.encodeMetrics(conn.exportMetrics()).toString('hex'));
+      } finally {
+        keys.seriesHashSeeded = real;
+      }
+      if (native) assert.ok(conn.stats().nativeRequests > 0 && conn.stats().jsRequests === 0);
+      out.push(exports);
+    }
+    assert.deepStrictEqual(out[0], out[1], JSON.stringify([cfg, collide]));
   }
 });
 

@@ -272,13 +272,22 @@ def case_split_dims():
              ("a", "GET /x", 2, 0, {"http.method": "POST"}),
              ("a", "GET /x", 2, 2, {"http.route": "/x"}),
              ("a", "op", 1, 0, {}),
-             ("b", "op", 3, 1, {"http.method": "GET", "region": "us"})]
+             ("b", "op", 3, 1, {"http.method": "GET", "region": "us"}),
+             ("b", "op", 3, 2, {"http.method": "GET", "region": "us"}),
+             ("b", "op", 3, 2, {"http.method": "PUT", "region": "us"})]
     dims, cd, hd = [["region", None]], [["http.method", None]], [["http.route", "none"]]
     calls, hist = restate_split(spans, dims, cd, hd)
     cfg = {"dimensions": [{"name": "region"}], "calls_dimensions": [{"name": "http.method"}],
            "histogram": {"dimensions": [{"name": "http.route", "default": "none"}]}}
+    # the window's sketches see every span once (connector.go keeps one
+    # sums and one histograms map, but the sketches are this engine's own:
+    # one ERROR count per ERROR span, under its histogram-series key): each
+    # count-min row holds the window's ERROR spans exactly once
+    errors = sum(1 for s in spans if s[3] == 2)
+    err_points = sorted([at, n] for at, n in hist if ["status.code", "STATUS_CODE_ERROR"] in at)
     return dict(name="calls_and_histogram_dimensions", config=cfg,
-                spans=[[a, b, c, d, e] for a, b, c, d, e in spans], expected=dict(calls=calls, histogram=hist))
+                spans=[[a, b, c, d, e] for a, b, c, d, e in spans],
+                expected=dict(calls=calls, histogram=hist, window_error_spans=errors, top_errors=err_points))
 
 
 def case_histogram_disable():
