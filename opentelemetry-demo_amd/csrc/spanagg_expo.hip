@@ -439,6 +439,14 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
     const int2 m = meta[slot];
     const int32_t sn = (int32_t)(int8_t)(m.x & 0xFF);
     const int32_t su = (int32_t)((w >> kIxScaleShift) & 31u) - (int32_t)kIxScaleBias;
+    // (su < sn would need a shift the other way: the series' scale rose since
+    // the ingest kernel read it, which no reset path may allow -- compact and
+    // init reset xscale with the header.  Should one ever break that, the
+    // span is reported as dropped, never counted in a wrong bucket.)
+    if (__builtin_expect(su < sn, 0)) {
+      atomicAdd(E.dropped, 1ULL);
+      return;
+    }
     const int32_t ix = ((int32_t)(w << 17) >> 18) >> (su - sn);  // the 14-bit field, sign-extended
     add(slot, ix, m);
   };

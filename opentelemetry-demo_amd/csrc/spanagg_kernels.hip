@@ -553,15 +553,29 @@ __device__ __forceinline__ uint32_t wave_claim(uint32_t *ctr) {
 #define SA_XIDX_SCALE(P) true
 #endif
 
-// TAG: the key lookup reads 32-bit tags (key_tag) of the two candidate
-// buckets -- one ds_read_b128 per bucket instead of two -- and verifies the
-// matching slot's full key with one ds_read_b64 (a tag match on another key,
-// or on an empty slot for a key whose tag is 0, fails the check and takes the
-// cold path, which probes full keys): 40 B of LDS per span instead of 64.
-template <int S, int NBUF, int AUX, bool DIAG, int LC = 0, int NWC = 0, int PC = 0, int HAUX = -1,
-          bool DYN = false, int OPT = 0, bool EPI = false, bool LEAN = false, bool EXPO = false, bool TAG = false,
-          bool POOL = false, uint32_t BLK = kLdsBlock>
+//
+// The kernel's template: its geometry (LC = log2 slots, NWC = counter words
+// per slot, PC = HLL precision; 0 = read from P), EXPO, the block size and an
+// option set O (S spans per lane per step, NBUF tiles in flight, AUX cache
+// policy, DYN / OPT / EPI / LEAN above).  The product's two option sets are
+// V2Lean (the default table and every EXPO engine) and V2Plain; the
+// laboratory's switches (DIAG ablations, TAG, POOL, the A/B sets) are defined
+// in lab/small_lab.inc, which only the laboratory build compiles.
+struct V2Plain {  // variant 15: chunk claims only
+  static constexpr int S = 2, NBUF = 2, AUX = 2, HAUX = -1, OPT = 0;
+  static constexpr bool DYN = true, EPI = false, LEAN = false, DIAG = false, TAG = false, POOL = false;
+};
+struct V2Lean : V2Plain {  // variant 20: + prologue barrier, LDS event counters, lean hash, two-phase epilogue
+  static constexpr int OPT = 1;
+  static constexpr bool EPI = true, LEAN = true;
+};
+template <int LC, int NWC, int PC, bool EXPO, uint32_t BLK, typename O>
 __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
+  constexpr int S = O::S, NBUF = O::NBUF, AUX = O::AUX, HAUX = O::HAUX, OPT = O::OPT;
+  constexpr bool DYN = O::DYN, EPI = O::EPI, LEAN = O::LEAN, DIAG = O::DIAG, TAG = O::TAG, POOL = O::POOL;
+#ifndef SPANAGG_AB
+  static_assert(!DIAG && !TAG && !POOL, "laboratory switches: libspanagg_ab.so only");
+#endif
   static_assert(BLK % 64 == 0 && kErrTab % BLK == 0 && kHllQueue % BLK == 0 && BLK * 4 >= kLbMaxSub, "block size");
   static_assert(!POOL || (DYN && !(OPT & 2)), "the tail pool extends the chunk claims");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -592,7 +606,6 @@ __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
   uint32_t *pmap = ltag + (TAG ? cap : 0u);
   // EXPO with index records: [cap] each slot's scale when the kernel started
   int8_t *lsc = reinterpret_cast<int8_t *>(pmap + (POOL ? kPoolMaxSteal : 0u));
-  constexpr uint32_t kPoolDone = 0xFFFFFFFFu;
   const bool err_lds = P.errslab != nullptr;
   const bool lb_on = P.lb_n != 0 && !(diag & 2u);
   // EXPO header partials (zeroed with lsum / lcnt): lsum = ns sums
@@ -850,33 +863,12 @@ __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
     uint32_t found[S];
     if (!(diag & 1u)) {
       bool need[S];
+#ifdef SPANAGG_AB
       if constexpr (TAG) {
-        uint32_t f[S];
-#pragma unroll
-        for (int j = 0; j < S; ++j) {  // both spans' tag reads first, then both verifies
-          const ProbeSeq pr = probe_seq(key[j], log2cap);
-          const uint4 t1 = *reinterpret_cast<const uint4 *>(ltag + pr.b1 * 4);
-          const uint4 t2 = *reinterpret_cast<const uint4 *>(ltag + pr.b2 * 4);
-          const uint32_t tg = key_tag(key[j]);
-          uint32_t g = kNotFound;
-          g = t2.w == tg ? pr.b2 * 4 + 3 : g;
-          g = t2.z == tg ? pr.b2 * 4 + 2 : g;
-          g = t2.y == tg ? pr.b2 * 4 + 1 : g;
-          g = t2.x == tg ? pr.b2 * 4 + 0 : g;
-          g = t1.w == tg ? pr.b1 * 4 + 3 : g;
-          g = t1.z == tg ? pr.b1 * 4 + 2 : g;
-          g = t1.y == tg ? pr.b1 * 4 + 1 : g;
-          g = t1.x == tg ? pr.b1 * 4 + 0 : g;
-          f[j] = g;
-        }
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-          const unsigned long long kk = lkeys[f[j] != kNotFound ? f[j] : 0u];
-          const bool hit = key[j] != 0 && f[j] != kNotFound && kk == key[j];
-          found[j] = hit ? f[j] : kNotFound;
-          need[j] = key[j] != 0 && !hit;
-        }
-      } else {
+#include "lab/v2_tag_lookup.inc"
+      } else
+#endif
+      {
 #pragma unroll
       for (int j = 0; j < S; ++j) {
         const ProbeSeq pr = probe_seq(key[j], log2cap);
@@ -1105,41 +1097,7 @@ __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
     // c0: this round's chunk (its tiles are in buf), c1: the next round's
     // (prefetched during this round), c2: claimed now for the round after.
     // The claim returns while the round runs; its result is read at the end.
-    // A chunk's first span relative to lo (t_of; lim: no work): the
-    // workgroup's own range, then (POOL) chunks of stolen pool blocks, 8 per
-    // block.  The wave whose claim is a block's first chunk takes the block
-    // from the pool counter right after its claim and publishes it in pmap;
-    // the block's other chunks wait for that.  A block is taken only after
-    // the workgroup's previous block is published (and not at all after a
-    // done one), so the blocks a workgroup takes increase with k: every claim
-    // past a done chunk is done too, which is what lets a wave leave the loop
-    // at its first done chunk with a claim in hand.  (Taken as soon as each
-    // claim returned, two waves' counter adds could complete out of order and
-    // a valid block could follow a done one: round-5 r5d lost 1,024 spans of
-    // a 40 M-span ingest that way.)  Claims are in order, so the earliest
-    // unpublished block's wave never waits on a later one.
-    auto published = [&](uint32_t k) -> uint32_t {
-      // (the host gives a pooled launch >= 32 own chunks per workgroup, so
-      // every block's first chunk is a claim whose wave publishes it; the
-      // bound only keeps a broken invariant from hanging the device)
-      uint32_t v, spin = 0;
-      while ((v = (uint32_t)__builtin_amdgcn_readfirstlane((int)__atomic_load_n(&pmap[k], __ATOMIC_RELAXED))) == 0 &&
-             ++spin < (1u << 22))
-        __builtin_amdgcn_s_sleep(2);
-      return v;
-    };
-    auto t_of = [&](uint32_t c) -> uint32_t {
-      if (c < n_chunks) return c * chunk;
-      if constexpr (POOL) {
-        const uint32_t s = c - n_chunks, k = s >> 3, j = s & 7u;
-        if (!pool_on || k >= kPoolMaxSteal) return lim;
-        const uint32_t v = published(k);
-        if (v == 0 || v == kPoolDone) return lim;
-        const uint64_t t = cold_params().pool_base - lo + (uint64_t)(v - 1) * kPoolSpans + j * chunk;
-        return t < lim ? (uint32_t)t : lim;
-      }
-      return lim;
-    };
+    // (POOL, the laboratory's tail pool, has its own loop: lab/v2_pool_loop.inc.)
     if constexpr (!POOL) {
       while (c0 < n_chunks) {
         const uint32_t c2 = wave_claim(&hq_n[1]);
@@ -1149,31 +1107,11 @@ __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
         c1 = c2;
       }
     }
+#ifdef SPANAGG_AB
     if constexpr (POOL) {
-      // (state: this round's first span t0 and the next round's chunk c1, as
-      // c0 / c1 above; a block's wave takes it right at its claim, the
-      // block's other chunks resolve when they become c1)
-      uint32_t t0 = t_of(c0);
-      while (t0 < lim) {
-        const uint32_t c2 = wave_claim(&hq_n[1]);
-        if (pool_on && c2 >= n_chunks && ((c2 - n_chunks) & 7u) == 0 && ((c2 - n_chunks) >> 3) < kPoolMaxSteal) {
-          const uint32_t k = (c2 - n_chunks) >> 3;
-          const uint32_t prev = k ? published(k - 1) : 1u;
-          uint32_t v = kPoolDone;
-          if (prev != 0 && prev != kPoolDone) {
-            const uint32_t sid =
-                (uint32_t)__builtin_amdgcn_readfirstlane((int)atomicAdd(cold_params().pool_ctr, 1u)) >> 6;
-            if (sid < cold_params().pool_n) v = sid + 1;
-          }
-          if ((threadIdx.x & 63u) == 0) __atomic_store_n(&pmap[k], v, __ATOMIC_RELAXED);
-        }
-        const uint32_t t1 = t_of(c1);
-#pragma unroll
-        for (int b = 0; b < NBUF; ++b) step(buf[b], t0 + (uint32_t)b * tile, t1 + (uint32_t)b * tile);
-        t0 = t1;
-        c1 = c2;
-      }
+#include "lab/v2_pool_loop.inc"
     }
+#endif
   } else {
     for (uint32_t t0 = 0; t0 < loop_len; t0 += NBUF * tile) {
 #pragma unroll
@@ -1916,10 +1854,9 @@ uint32_t grid_for(uint64_t work, uint32_t block, uint32_t cap_blocks) {
 static const void *small_fn(bool bt, int v, bool diag) {
   (void)diag;
   if (!bt) return (const void *)&ingest_lds_kernel<0, 4, true, false>;
-  if (v == 20) return (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 9, 14, -1, true, 1, true, true>;
-  if (v == kLdsHalfBlockVariant)
-    return (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true, 1, true, true, false, false, false, 512>;
-  return (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true>;
+  if (v == 20) return (const void *)&ingest_v2_kernel<11, 9, 14, false, 1024, V2Lean>;
+  if (v == kLdsHalfBlockVariant) return (const void *)&ingest_v2_kernel<0, 0, 0, false, 512, V2Lean>;
+  return (const void *)&ingest_v2_kernel<0, 0, 0, false, 1024, V2Plain>;
 }
 constexpr int kSmallFnVariants[] = {15, 20, kLdsHalfBlockVariant};
 #else
@@ -2006,8 +1943,8 @@ uint32_t ingest_small_blocks_per_cu(bool bt, int variant, uint32_t log2cap, uint
 // the EXPO kernel: specialised for the default small table (2,048 slots, HLL
 // p = 14: C2's geometry) like variant 20, generic otherwise
 static const void *expo_small_fn(bool spec) {
-  return spec ? (const void *)&ingest_v2_kernel<2, 2, 2, false, 11, 0, 14, -1, true, 1, true, true, true>
-              : (const void *)&ingest_v2_kernel<2, 2, 2, false, 0, 0, 0, -1, true, 1, true, true, true>;
+  return spec ? (const void *)&ingest_v2_kernel<11, 0, 14, true, 1024, V2Lean>
+              : (const void *)&ingest_v2_kernel<0, 0, 0, true, 1024, V2Lean>;
 }
 
 hipError_t prepare_ingest_expo_small(size_t lds_bytes) {

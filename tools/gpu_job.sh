@@ -6,6 +6,7 @@
 #   tests            every -m gpu test (pytest, per-test timeout)
 #   tests:<file>     one test file, e.g. tests:tests/test_gpu_binned.py
 #   bench            the default bench line (C2 + C4 sub-objects, CPU baselines)
+#   selflaunch_<n>   bare `bench.py --gpus n` (it spawns its n ranks), every rank on this GPU, gloo
 #   rehearse_<n>     bench.py's n-rank path (torch.distributed.run) with every
 #                    rank on this one GPU and gloo collectives (a rehearsal)
 #   bench_<wl>       a short bench of one workload (c2, c4, c4zipf), no baselines
@@ -71,6 +72,8 @@ for step in "$@"; do
     rehearse_*) n=${step#rehearse_}; SPANAGG_BENCH_ONE_DEVICE=1 run "rehearse_n$n" 400 python -m torch.distributed.run \
         --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus "$n" --steps 10 \
         --warmup 2 --settle 4 --soak-s 0 ;;
+    selflaunch_*) n=${step#selflaunch_}; SPANAGG_BENCH_ONE_DEVICE=1 run "selflaunch_n$n" 400 python bench.py --gpus "$n" \
+        --steps ${SL_STEPS:-20} --soak-s 0 ;;  # bench.py starts its own n ranks (no outer launcher), all on this GPU
     colbench) (cd host/node && node test/host_rate.js 2000000 --dump /tmp/req_plain.bin > /dev/null && \
         node test/host_rate.js 2000000 --events --dump /tmp/req_ev.bin > /dev/null) || exit 1
       for t in ${COL_THREADS:-1 4 8 16}; do run "colbench_t$t" 120 host/node/build/colbench /tmp/req_plain.bin --threads "$t"; done
