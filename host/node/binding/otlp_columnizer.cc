@@ -1,6 +1,8 @@
 // otlp_columnizer.cc -- see otlp_columnizer.h.
 #include "otlp_columnizer.h"
 
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <charconv>
 #include <cmath>
@@ -449,6 +451,8 @@ const Any *find_attr(const std::vector<Attr> &v, std::string_view k) {
   return nullptr;
 }
 
+
+
 }  // namespace
 
 uint64_t xxh64(const void *data, size_t len, uint64_t seed) {
@@ -606,40 +610,66 @@ uint64_t SigCache::hash(uint64_t rhash, uint32_t svc, std::string_view name, int
   return (h ^ (h >> 29)) | 1;  // 0 never names a used slot
 }
 
-SigCache::Entry *SigCache::find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
-                                int32_t code) const {
-  if (slots_.empty()) return nullptr;
-  const size_t mask = slots_.size() - 1;
+template <typename T>
+void BigArray<T>::assign_zero(size_t n) {
+  std::free(p_);
+  p_ = nullptr, n_ = 0;
+  if (!n) return;
+  constexpr size_t kHuge = (size_t)2 << 20;
+  size_t bytes = n * sizeof(T);
+  void *q;
+  if (bytes >= kHuge) {
+    bytes = (bytes + kHuge - 1) / kHuge * kHuge;
+    q = std::aligned_alloc(kHuge, bytes);
+    if (q) madvise(q, bytes, MADV_HUGEPAGE);  // (advice only: a refusal changes nothing)
+  } else {
+    bytes = (bytes + 63) / 64 * 64;
+    q = std::aligned_alloc(64, bytes);
+  }
+  if (!q) throw std::bad_alloc();
+  std::memset(q, 0, bytes);
+  p_ = static_cast<T *>(q), n_ = n;
+}
+
+const SigCache::Rec *SigCache::find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
+                                    int32_t code) const {
+  if (recs_.empty()) return nullptr;
+  const size_t mask = recs_.size() - 1;
+  const uint32_t n = (uint32_t)name.size(), ni = n < kInline ? n : kInline;
   for (size_t i = h & mask;; i = (i + 1) & mask) {
-    const Slot &sl = slots_[i];
-    if (!sl.h) return nullptr;
-    if (sl.h != h) continue;
-    const Entry &e = entries_[sl.idx];
-    if (e.rhash == rhash && e.svc == svc && e.kind == kind && e.code == code && e.name_len == name.size() &&
-        std::memcmp(names_.data() + e.name_off, name.data(), name.size()) == 0)
-      return const_cast<Entry *>(&e);
+    const Rec &r = recs_[i];
+    if (!r.h) return nullptr;
+    if (r.h != h) continue;
+    if (r.rhash == rhash && r.svc == svc && r.kind == kind && r.code == code && r.name_len == n &&
+        std::memcmp(r.name, name.data(), ni) == 0 &&
+        (n <= kInline || std::memcmp(names_.data() + r.name_off + kInline, name.data() + kInline, n - kInline) == 0))
+      return &r;
   }
 }
 
 void SigCache::insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind,
                       int32_t code, uint64_t sid, const std::string &key) {
-  if (2 * (entries_.size() + 1) > slots_.size()) {  // load <= 1/2: rebuild the slots from the entries
-    std::vector<Slot> old;
-    old.swap(slots_);
-    slots_.resize(old.empty() ? 256 : old.size() * 2);
-    const size_t mask = slots_.size() - 1;
-    for (const Slot &o : old) {
+  if (!cacheable(kind, code)) return;
+  if (2 * (entries_.size() + 1) > recs_.size()) {  // load <= 1/2: rebuild the records
+    BigArray<Rec> old;
+    old.swap(recs_);
+    recs_.assign_zero(old.empty() ? 256 : old.size() * 2);
+    const size_t mask = recs_.size() - 1;
+    for (const Rec &o : old) {
       if (!o.h) continue;
       size_t i = o.h & mask;
-      while (slots_[i].h) i = (i + 1) & mask;
-      slots_[i] = o;
+      while (recs_[i].h) i = (i + 1) & mask;
+      recs_[i] = o;
     }
   }
-  const size_t mask = slots_.size() - 1;
+  const size_t mask = recs_.size() - 1;
   size_t i = h & mask;
-  while (slots_[i].h) i = (i + 1) & mask;
-  slots_[i].h = h;  // (never 0: hash() sets bit 0)
-  slots_[i].idx = (uint32_t)entries_.size();
+  while (recs_[i].h) i = (i + 1) & mask;
+  Rec &r = recs_[i];
+  r.h = h;  // (never 0: hash() sets bit 0)
+  r.sid = sid, r.rhash = rhash, r.svc = svc, r.kind = (int16_t)kind, r.code = (int16_t)code;
+  r.name_len = (uint32_t)name.size(), r.name_off = (uint32_t)names_.size(), r.idx = (uint32_t)entries_.size();
+  std::memcpy(r.name, name.data(), name.size() < kInline ? name.size() : kInline);
   fresh_.push_back((uint32_t)entries_.size());
   Entry e;
   e.h = h, e.rhash = rhash, e.sid = sid, e.svc = svc, e.kind = kind, e.code = code;
@@ -652,6 +682,8 @@ void SigCache::insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view
 struct Columnizer::Worker {
   Cols cols;
   SigCache cache;
+  bool own_cache_on = true;  // probe `cache` before the shared one (see columnize_batch)
+  uint64_t own_lookups = 0, own_hits = 0, batches = 0;
   std::vector<Attr> rattrs, sattrs, eattrs;
   std::vector<const Attr *> hv;
   std::string tmp, keystr, sname, service, evkey, sigbuf;
@@ -1001,7 +1033,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
         if (!sp.ok) return fail(Result::kError, "malformed Span");
         uint64_t sid;
         uint64_t sig = 0;
-        SigCache::Entry *hit = nullptr;
+        const SigCache::Rec *hit = nullptr;
         std::string_view signame = name;
         bool use_cache = true;
         if (dims) {
@@ -1027,10 +1059,12 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
           signame = sb;
         }
         bool l2_hit = false;  // (an entry of the shared cache is read only here)
-        if (use_cache) {
+        if (use_cache && SigCache::cacheable(kind, code)) {
           sig = SigCache::hash(rhash, svc_id, signame, kind, code);
-          hit = cache.find(sig, rhash, svc_id, signame, kind, code);
+          if (w.own_cache_on) hit = cache.find(sig, rhash, svc_id, signame, kind, code);
           if (!hit && l2 && (hit = l2->find(sig, rhash, svc_id, signame, kind, code))) l2_hit = true;
+          w.own_lookups += 1;
+          w.own_hits += hit && !l2_hit ? 1u : 0u;
         }
         // key = buildKey, into keystr (0 = built; else the failure to return)
         auto build_key = [&]() -> int {
@@ -1070,7 +1104,8 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
         if (hit) {
           sid = hit->sid;
           if (opt_.events && !w.evs.empty()) {  // the event keys extend the span key: kept in the entry
-            if (!hit->key.empty()) keystr = hit->key;
+            const std::string &hk = (l2_hit ? l2 : &cache)->rec_entry(hit).key;
+            if (!hk.empty()) keystr = hk;
             else if (const int why = build_key()) return key_fail(why);
           }
         } else {
@@ -1106,7 +1141,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
         // candidates; accept_exemplars keeps the interval's first ones.  A
         // series seen full this interval is marked in its signature-cache
         // entry, so its later spans cost no lookup.
-        if (opt_.exemplars && !(hit && hit->ex_full == ex_gen_)) {
+        if (opt_.exemplars && !(hit && (l2_hit ? l2 : &cache)->rec_entry(hit).ex_full == ex_gen_)) {
           auto ex = ex_count_.find(sid);
           const uint32_t taken = ex == ex_count_.end() ? 0u : ex->second;
           if (taken < opt_.exemplars_max) {
@@ -1123,7 +1158,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
               res.exemplars.push_back(x);
             }
           } else if (hit) {
-            if (!l2_hit) hit->ex_full = ex_gen_;
+            if (!l2_hit) cache.rec_entry(hit).ex_full = ex_gen_;
           }
         }
         if (en > out.max_end) out.max_end = en;
@@ -1260,6 +1295,16 @@ BatchResult Columnizer::columnize_batch(const uint8_t *const *bufs, const size_t
   for (auto &w : workers_) {
     w->cols.clear();
     if (w->cache.gen != gen_ || w->cache.size() > kOwnCacheMax) w->cache.clear(), w->cache.gen = gen_;
+    // a thread's own cache pays only when its hot set fits it: past ~4 k
+    // lookups with fewer than 1 in 8 answered there (a high-cardinality
+    // stream), it is not probed (its inserts still feed the shared cache);
+    // every 32nd batch probes it again to re-sample
+    w->batches += 1;
+    if (w->own_lookups >= 4096) {
+      w->own_cache_on = 8 * w->own_hits >= w->own_lookups;
+      w->own_lookups = w->own_hits = 0;
+    }
+    if (!w->own_cache_on && (w->batches & 31u) == 0) w->own_cache_on = true, w->own_lookups = w->own_hits = 0;
   }
   using clk = std::chrono::steady_clock;
   const auto ns_since = [](clk::time_point t) {

@@ -170,6 +170,32 @@ struct Cols {
   void clear() { n = 0, max_end = 0; }
 };
 
+// A zeroed array of trivially copyable T; from 2 MiB up 2 MiB-aligned and
+// madvise(MADV_HUGEPAGE)d: a high-cardinality signature table is far larger
+// than the TLB's 4 KiB-page reach, and a page walk on every lookup cost more
+// than the lookup's one cache miss.
+template <typename T>
+class BigArray {
+ public:
+  BigArray() = default;
+  BigArray(const BigArray &) = delete;
+  BigArray &operator=(const BigArray &) = delete;
+  ~BigArray() { std::free(p_); }
+  void assign_zero(size_t n);  // n elements, all zero bytes (the old contents are dropped)
+  void swap(BigArray &o) { std::swap(p_, o.p_), std::swap(n_, o.n_); }
+  void clear() { std::free(p_), p_ = nullptr, n_ = 0; }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  T &operator[](size_t i) { return p_[i]; }
+  const T &operator[](size_t i) const { return p_[i]; }
+  const T *begin() const { return p_; }
+  const T *end() const { return p_ + n_; }
+
+ private:
+  T *p_ = nullptr;
+  size_t n_ = 0;
+};
+
 // (resource hash, service id, raw span name, kind, status code) -> series id,
 // for keys without dimensions: a span of a known series skips UTF-8
 // validation, the rename rules and building its key string
@@ -177,12 +203,21 @@ class SigCache {
  public:
   static uint64_t hash(uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code);
   struct Entry;
-  Entry *find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code) const;
+  struct Rec;
+  // the record of the signature, or null; rec_entry gives its Entry (the
+  // rarely read fields: exemplar mark, event key)
+  const Rec *find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code) const;
+  Entry &rec_entry(const Rec *r) { return entries_[r->idx]; }
+  const Entry &rec_entry(const Rec *r) const { return entries_[r->idx]; }
   // key: the span's key string, kept for events.enabled (its spans' event
-  // keys extend it), empty otherwise
+  // keys extend it), empty otherwise.  A kind or code outside int16 is never
+  // cached (find misses, the caller keys the span the long way).
   void insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code,
               uint64_t sid, const std::string &key);
-  void clear() { slots_.clear(), entries_.clear(), names_.clear(), fresh_.clear(); }
+  static bool cacheable(int32_t kind, int32_t code) {
+    return kind == (int16_t)kind && code == (int16_t)code;
+  }
+  void clear() { recs_.clear(), entries_.clear(), names_.clear(), fresh_.clear(); }
   size_t size() const { return entries_.size(); }
   uint64_t gen = 0;  // the dictionary generation the entries belong to
   // entries inserted since the last take_fresh (a worker's, merged into the
@@ -204,16 +239,25 @@ class SigCache {
     uint32_t name_off = 0, name_len = 0;  // the signature name in names_
     std::string key;                      // events.enabled: the span key string (see insert)
   };
+  // One cache line holds everything a lookup compares and its answer: the
+  // full hash, the series id, the signature's fields and the first kInline
+  // bytes of its name (the rest, if any, in names_).  A high-cardinality
+  // stream's table is far larger than the CPU caches, so a hit costs one
+  // memory access (two for a longer name) instead of the three of a slot
+  // array, an entry array and a name arena.
+  static constexpr uint32_t kInline = 20;
+  struct alignas(64) Rec {
+    uint64_t h;  // 0: free
+    uint64_t sid, rhash;
+    uint32_t svc;
+    int16_t kind, code;
+    uint32_t name_len, name_off, idx;  // the name in names_, the Entry
+    char name[kInline];
+  };
+  static_assert(sizeof(Rec) == 64, "one cache line");
 
  private:
-  // open addressing over 16-B slots (the full hash and the entry), so a probe
-  // touches one line and only a hash match reads the entry and its name (a
-  // high-cardinality stream's table is larger than the caches)
-  struct Slot {
-    uint64_t h = 0;  // 0: free
-    uint32_t idx = 0, pad = 0;
-  };
-  std::vector<Slot> slots_;
+  BigArray<Rec> recs_;  // open addressing, linear probing, load <= 1/2
   std::vector<Entry> entries_;
   std::string names_;
   std::vector<uint32_t> fresh_;

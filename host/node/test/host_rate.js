@@ -38,8 +38,16 @@ const PER_REQUEST = 512;  // an SDK batch span processor's default export batch
 const SERVICES = 20, NAMES = 25, PODS = 500, ROUTES = 2000;
 
 function makeRequests() {
+  // mulberry32: successive draws independent enough that --highcard's pod x
+  // route pairs really span the 1 M combinations (the LCG used before had
+  // correlated consecutive outputs: ~112 k distinct series)
   let seed = 42;
-  const rnd = () => { seed = (seed * 1103515245 + 12345) >>> 0; return seed / 4294967296; };
+  const rnd = () => {
+    seed = (seed + 0x6D2B79F5) | 0;
+    let t = Math.imul(seed ^ (seed >>> 15), 1 | seed);
+    t = (t + Math.imul(t ^ (t >>> 7), 61 | t)) ^ t;
+    return ((t ^ (t >>> 14)) >>> 0) / 4294967296;
+  };
   const reqs = [];
   const T0 = 1700000000000000000n;
   for (let done = 0; done < n; done += PER_REQUEST) {
