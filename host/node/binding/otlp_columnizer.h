@@ -208,6 +208,9 @@ class SigCache {
   // rarely read fields: exemplar mark, event key)
   const Rec *find(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view name, int32_t kind, int32_t code) const;
   Entry &rec_entry(const Rec *r) { return entries_[r->idx]; }
+  void prefetch(uint64_t h) const {
+    if (!recs_.empty()) __builtin_prefetch(&recs_[h & (recs_.size() - 1)]);
+  }
   const Entry &rec_entry(const Rec *r) const { return entries_[r->idx]; }
   // key: the span's key string, kept for events.enabled (its spans' event
   // keys extend it), empty otherwise.  A kind or code outside int16 is never
