@@ -689,6 +689,7 @@ struct FastSpan {
   bool slow = false;
 };
 constexpr size_t kBatch = 16;
+constexpr size_t kBatchAbove = 1u << 16;  // own-cache signatures past which run() batches
 
 struct Columnizer::Worker {
   Cols cols;
@@ -979,8 +980,11 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
       }
     }
 
-    // pass 2: scope_spans -> spans (batched: see the span loop)
-    const bool batched = !opt_.events && !opt_.exemplars;
+    // pass 2: scope_spans -> spans.  Batched (see the span loop) when the
+    // lookups will miss the CPU caches: this thread's own cache is not probed
+    // (a high-cardinality stream, see columnize_batch) or holds more
+    // signatures than a core's caches do
+    const bool batched = !opt_.events && !opt_.exemplars && (!w.own_cache_on || cache.size() > kBatchAbove || opt_.test_batched);
     PB scan = rs;
     uint32_t g;
     int wt2;

@@ -54,6 +54,7 @@ struct Options {
   std::vector<Rule> rules;
   std::vector<std::string> key_attributes;  // resource_metrics_key_attributes (empty = all)
   bool test_collide_seed0 = false;          // tests only: every seed-0 series id is 42
+  bool test_batched = false;                // tests only: the batched span path whenever it applies
   unsigned threads = 1;                     // columnize_batch worker threads (caller included)
   // aggregation_cardinality_limit: past this many span series in a resource,
   // new keys share the resource's overflow series (0 = unlimited)

@@ -702,6 +702,10 @@ napi_value CreateColumnizer(napi_env env, napi_callback_info info) {
     bool b = false;
     if (!is_undefined(env, tc)) napi_get_value_bool(env, tc, &b);
     o.test_collide_seed0 = b;
+    napi_value tb = prop(env, argv[1], "testBatched");
+    b = false;
+    if (!is_undefined(env, tb)) napi_get_value_bool(env, tb, &b);
+    o.test_batched = b;
   }
   {  // aggregation_cardinality_limit, exemplars, events (connector.js normalizeConfig)
     napi_value v = prop(env, argv[1], "cardinalityLimit");

@@ -171,7 +171,8 @@ class NativeColumnizerFakeAddon extends FakeAddon {
     this.real = require('../lib/addon').load();
   }
   createColumnizer(h, opts) {
-    return this.real.createColumnizer(null, Object.assign({}, opts, this.collide ? { testCollideSeed0: true } : {}));
+    return this.real.createColumnizer(null, Object.assign({}, opts, this.collide ? { testCollideSeed0: true } : {},
+      this.batched ? { testBatched: true } : {}));
   }
   columnize(c, bytes) { return this.real.columnize(c, bytes); }
   columnizeBatch(c, bufs) { return this.real.columnizeBatch(c, bufs); }

@@ -544,11 +544,12 @@ function mixedRequests() {
   return reqs;
 }
 
-function runBoth(cfg, rules, reqs, collide = false) {
+function runBoth(cfg, rules, reqs, collide = false, batched = false) {
   const out = [];
   for (const native of [true, false]) {
     const addon = native ? new NativeColumnizerFakeAddon() : new FakeAddon();
     addon.collide = collide;
+    addon.batched = batched;
     const t = { now: 1000n };
     const conn = new SpanMetricsConnector(Object.assign({ batch_size: 16 }, cfg),
       { addon, rules, native, clock: () => (t.now += 1n) });
@@ -576,13 +577,15 @@ test('native columnizer: same columns and same OTLP metrics as the JavaScript pa
     [{ exclude_dimensions: ['span.kind', 'status.code'], resource_metrics_key_attributes: ['service.name'] }, []],
     [{ resource_metrics_cache_size: 1, aggregation_temporality: 'AGGREGATION_TEMPORALITY_DELTA' }, DEMO_SPAN_NAME_RULES],
   ]) {
-    const [nat, js] = runBoth(cfg, rules, reqs);
-    assert.ok(nat.stats.nativeRequests > 0 && nat.stats.jsRequests === 0, JSON.stringify(cfg));
-    assert.strictEqual(js.stats.nativeRequests, 0);
-    assert.deepStrictEqual(nat.cols, js.cols, JSON.stringify(cfg));
-    assert.deepStrictEqual(nat.exports, js.exports, JSON.stringify(cfg));
-    assert.deepStrictEqual(nat.services, js.services);
-    assert.strictEqual(nat.stats.nativeRemaps, 0, JSON.stringify(cfg));
+    for (const batched of [false, true]) {  // the columnizer's batched span path (high cardinality) too
+      const [nat, js] = runBoth(cfg, rules, reqs, false, batched);
+      assert.ok(nat.stats.nativeRequests > 0 && nat.stats.jsRequests === 0, JSON.stringify(cfg));
+      assert.strictEqual(js.stats.nativeRequests, 0);
+      assert.deepStrictEqual(nat.cols, js.cols, JSON.stringify(cfg));
+      assert.deepStrictEqual(nat.exports, js.exports, JSON.stringify(cfg));
+      assert.deepStrictEqual(nat.services, js.services);
+      assert.strictEqual(nat.stats.nativeRemaps, 0, JSON.stringify(cfg));
+    }
   }
 });
 
@@ -621,13 +624,15 @@ test('native columnizer: cardinality limit, exemplars and events == the JavaScri
     [{ events: { enabled: true, dimensions: [{ name: 'exception.type' }] }, exemplars: { enabled: true, max_per_data_point: 3 },
       aggregation_cardinality_limit: 4, dimensions: [{ name: 'k8s.pod.name' }] }, DEMO_SPAN_NAME_RULES],
   ]) {
-    const [nat, js] = runBoth(cfg, rules, reqs);
+    for (const batched of [false, true]) {
+    const [nat, js] = runBoth(cfg, rules, reqs, false, batched);
     assert.ok(nat.stats.nativeRequests === reqs.length && nat.stats.jsRequests === 0, `${nat.stats.nativeRequests} ${nat.stats.jsRequests}`);
     assert.deepStrictEqual(nat.cols, js.cols, JSON.stringify(cfg));
     assert.deepStrictEqual(nat.exports, js.exports, JSON.stringify(cfg));
     assert.strictEqual(nat.stats.eventRecords, js.stats.eventRecords);
     assert.strictEqual(nat.stats.nativeRemaps, 0, JSON.stringify(cfg));  // the native side keyed every series as the host does
     if (cfg.events) assert.ok(js.stats.eventRecords > 40);
+    }
   }
   // a limited resource really overflows, and exemplars really appear, on the native path
   const [nat] = runBoth({ aggregation_cardinality_limit: 2, exemplars: { enabled: true } }, [], eventRequests());
@@ -645,7 +650,7 @@ test('series ids: a 64-bit collision is re-salted on both paths (never thrown), 
   keys.seriesHashSeeded = (rh, k, seed) => (seed === 0n ? 42n : real(rh, k, seed));
   let nat, js;
   try {
-    [nat, js] = runBoth({}, DEMO_SPAN_NAME_RULES, reqs, true);
+    [nat, js] = runBoth({}, DEMO_SPAN_NAME_RULES, reqs, true, true);
   } finally {
     keys.seriesHashSeeded = real;
   }
@@ -695,10 +700,11 @@ test('native columnizer: consumeTracesBatch on worker threads == consumeTraces o
     { aggregation_cardinality_limit: 3, exemplars: { enabled: true }, events: { enabled: true, dimensions: [{ name: 'exception.type' }] } },
     { events: { enabled: true, dimensions: [{ name: 'exception.type' }] } }]) {
     const out = [];
-    for (const threads of [1, 4]) {
+    for (const threads of [1, 4, -4]) {  // -4: four threads, the batched span path forced
       const addon = new NativeColumnizerFakeAddon();
+      addon.batched = threads < 0;
       const t = { now: 1000n };
-      const conn = new SpanMetricsConnector(Object.assign({ batch_size: 16, columnizer_threads: threads }, cfg),
+      const conn = new SpanMetricsConnector(Object.assign({ batch_size: 16, columnizer_threads: Math.abs(threads) }, cfg),
         { addon, rules: DEMO_SPAN_NAME_RULES, clock: () => (t.now += 1n) });
       let errs;
       if (threads === 1) {
@@ -710,7 +716,8 @@ test('native columnizer: consumeTracesBatch on worker threads == consumeTraces o
       out.push({ errs: errs.map((e) => (e ? 'error' : null)), rows: rowsOf(addon), exp, services: [...conn.services],
         stats: conn.stats() });
     }
-    const [one, batch] = out;
+    const [one, batch, batched] = out;
+    assert.deepStrictEqual(batched, batch, JSON.stringify(cfg));
     assert.strictEqual(one.errs.filter(Boolean).length, 1);
     assert.deepStrictEqual(batch.errs, one.errs, JSON.stringify(cfg));
     assert.deepStrictEqual(batch.rows, one.rows, JSON.stringify(cfg));
@@ -729,12 +736,14 @@ test('native columnizer: after a threaded batch, a forget or remap is seen by si
   // return the stale id (its spans would land on a series the host no
   // longer tracks and vanish from the export)
   const reqs = mixedRequests().concat(eventRequests()).map((r) => otlp.encodeTraces(r));
-  for (const [cfg, collide] of [[{ resource_metrics_cache_size: 1 }, false], [{ resource_metrics_cache_size: 2 }, true],
-    [{}, true], [{ resource_metrics_cache_size: 1, dimensions: [{ name: 'k8s.pod.name' }] }, true]]) {
+  for (const [cfg, collide, batched] of [[{ resource_metrics_cache_size: 1 }, false, false],
+    [{ resource_metrics_cache_size: 2 }, true, false], [{}, true, true], [{ resource_metrics_cache_size: 1 }, false, true],
+    [{ resource_metrics_cache_size: 1, dimensions: [{ name: 'k8s.pod.name' }] }, true, true]]) {
     const out = [];
     for (const native of [true, false]) {
       const addon = native ? new NativeColumnizerFakeAddon() : new FakeAddon();
       addon.collide = collide;
+      addon.batched = batched;
       const t = { now: 1000n };
       const conn = new SpanMetricsConnector(Object.assign({ batch_size: 16, columnizer_threads: 4 }, cfg),
         { addon, rules: DEMO_SPAN_NAME_RULES, native, clock: () => (t.now += 1n) });
