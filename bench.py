@@ -160,8 +160,9 @@ def host_otlp_rate(spans: int, threads: int = 8, batch: int = 128, extra=()):
     except Exception as e:  # reported, never fatal for the bench line
         return {"error": str(e)[:200]}
     hc = "--highcard" in extra
-    vocab = ("500 pods (k8s.pod.name) x 2,000 routes (http.route dimension) = 1 M series, binned engine "
-             "table, every series known (a whole warm-up pass first)" if hc else "20 services x 25 names")
+    vocab = ("500 pods (k8s.pod.name) x 2,000 routes (http.route dimension) = 1 M possible series, "
+             f"{r.get('series', 0):,} distinct in the sample, binned engine table, every series known (a whole "
+             "warm-up pass first)" if hc else "20 services x 25 names")
     return {"value": r["spans_per_s"], "unit": "spans/s", "cores": r["cores"], "mb_per_s": r["mb_per_s"],
             "calls_check": r["calls_check"], "columnizer": r["columnizer"],
             "seconds_in": r.get("seconds_in"), "options": list(extra),

@@ -679,9 +679,10 @@ void SigCache::insert(uint64_t h, uint64_t rhash, uint32_t svc, std::string_view
   entries_.push_back(std::move(e));
 }
 
+namespace {
 // a span of the batched path (run): what a signature-cache hit needs
 struct FastSpan {
-  const uint8_t *b, *e;  // the span's bytes (span_body re-reads them on a miss)
+  const uint8_t *at;     // the span's field in its ScopeSpans (the full path restarts there on a miss)
   const uint8_t *name;   // the raw span name (no dimensions) or -- with dimensions -- noff into the arena
   uint32_t nlen = 0, noff = 0;
   int32_t kind = 0, code = 0;
@@ -690,6 +691,173 @@ struct FastSpan {
 };
 constexpr size_t kBatch = 16;
 constexpr size_t kBatchAbove = 1u << 16;  // own-cache signatures past which run() batches
+
+// One ScopeSpans of run()'s batched path (neither exemplars nor events, and
+// lookups that miss the CPU caches): spans are parsed kBatch at a time, each
+// one's signature-cache records prefetched as soon as its hash is known, then
+// resolved in order, so a batch's memory accesses overlap instead of
+// following each other.  A span it cannot resolve (unknown signature, a
+// dimension value that is not a string, anything malformed) goes back to
+// run()'s full path, which keys it, reports it or fails as always.
+struct BatchScope {
+  std::vector<FastSpan> &pend;
+  std::string &arena;
+  std::vector<std::string_view> &dv;
+  std::vector<uint8_t> &dt;
+  bool own;  // probe the thread's own cache
+  const std::vector<Dim> &dims;
+  const std::vector<Attr> &rattrs;
+  uint64_t rhash;
+  uint32_t svc_id;
+  const SigCache &cache;
+  const SigCache *l2;
+  Cols &out;
+  uint64_t &spans, &own_lookups, &own_hits;
+};
+// Emits the hits up to the next span the full path must take (true, with ss
+// back at that span's field) or to the scope's end (false).  Out of line:
+// run()'s plain loop stays as compact as it was without this path.
+__attribute__((noinline)) bool batch_hits(BatchScope &b, PB &ss) {
+  auto &pend = b.pend;
+  std::string &arena = b.arena;
+  const size_t nd = b.dims.size();
+  for (;;) {
+    {  // parse the next batch
+      pend.clear();
+      arena.clear();
+      uint32_t h;
+      int wt3;
+      const uint8_t *at = ss.p;
+      while (pend.size() < kBatch && ss.next(h, wt3)) {
+        if (h != 2 || wt3 != 2) {
+          ss.skip(wt3);
+          at = ss.p;
+          continue;
+        }
+      PB sp = ss.sub();
+      pend.emplace_back();
+      FastSpan &p = pend.back();
+      p.at = at;
+      at = ss.p;
+      const uint8_t *tid = nullptr;
+      size_t tid_len = 0;
+      std::string_view name;
+      int32_t kind = 0, code = 0;
+      uint64_t st = 0, en = 0;
+      // (per dimension: its last string value among the span attributes;
+      // type 2 = a value of another type, which span_body keys)
+      auto &dv = b.dv;
+      auto &dt = b.dt;
+      dv.assign(nd, std::string_view());
+      dt.assign(nd, 0);
+      bool slow = false;
+      uint32_t k;
+      int wt4;
+      while (sp.next(k, wt4)) {
+        if (k == 1 && wt4 == 2) {
+          const std::string_view t = sp.str();
+          tid = reinterpret_cast<const uint8_t *>(t.data());
+          tid_len = t.size();
+        } else if (k == 5 && wt4 == 2) {
+          name = sp.str();
+        } else if (k == 6 && wt4 == 0) {
+          kind = (int32_t)(uint32_t)sp.varint();
+        } else if (k == 7 && wt4 == 1) {
+          st = sp.fixed64();
+        } else if (k == 8 && wt4 == 1) {
+          en = sp.fixed64();
+        } else if (k == 9 && wt4 == 2 && nd) {
+          std::string_view key;
+          Any v;
+          if (!parse_kv(sp.sub(), key, v)) {
+            slow = true;
+            continue;
+          }
+          for (size_t d = 0; d < nd; ++d)
+            if (b.dims[d].name == key) dt[d] = v.type == kStr ? 1 : 2, dv[d] = v.s;
+        } else if (k == 15 && wt4 == 2) {
+          PB stt = sp.sub();
+          uint32_t m;
+          int wt5;
+          code = 0;  // a later Status message replaces an earlier one
+          while (stt.next(m, wt5)) {
+            if (m == 3 && wt5 == 0) code = (int32_t)(uint32_t)stt.varint();
+            else stt.skip(wt5);
+          }
+          if (!stt.ok) slow = true;
+        } else {
+          sp.skip(wt4);
+        }
+      }
+      if (!sp.ok || !SigCache::cacheable(kind, code)) slow = true;
+      p.name = reinterpret_cast<const uint8_t *>(name.data());
+      p.nlen = (uint32_t)name.size();
+      if (nd && !slow) {  // the signature name as span_body builds it
+        p.noff = (uint32_t)arena.size();
+        arena.append(name);
+        for (size_t d = 0; d < nd && !slow; ++d) {
+          char tag = '\x02';
+          std::string_view val = dv[d];
+          if (dt[d] == 2) {
+            slow = true;
+            break;
+          }
+          if (!dt[d]) {
+            const Any *v = find_attr(b.rattrs, b.dims[d].name);
+            if (!v) {
+              arena += '\x03';
+              continue;
+            }
+            if (v->type != kStr) {
+              slow = true;
+              break;
+            }
+            tag = '\x04', val = v->s;
+          }
+          const uint32_t n = (uint32_t)val.size();
+          arena += tag;
+          arena.append(reinterpret_cast<const char *>(&n), 4);
+          arena.append(val);
+        }
+        p.nlen = (uint32_t)(arena.size() - p.noff);
+      }
+      p.slow = slow;
+      if (!slow) {
+        p.kind = kind, p.code = code, p.st = st, p.en = en;
+        const bool has_tid = tid && tid_len == 16;
+        p.w0 = has_tid ? rd64(tid) : 0, p.w1 = has_tid ? rd64(tid + 8) : 0;
+        const std::string_view sn = nd ? std::string_view(arena.data() + p.noff, p.nlen) : name;
+        p.sig = SigCache::hash(b.rhash, b.svc_id, sn, kind, code);
+        if (b.own) b.cache.prefetch(p.sig);
+        if (b.l2) b.l2->prefetch(p.sig);
+      }
+      }
+      if (pend.empty()) return false;
+    }
+    for (const FastSpan &p : pend) {
+      const SigCache::Rec *hit = nullptr;
+      if (!p.slow) {
+        const std::string_view sn = nd ? std::string_view(arena.data() + p.noff, p.nlen)
+                                       : std::string_view(reinterpret_cast<const char *>(p.name), p.nlen);
+        if (b.own) hit = b.cache.find(p.sig, b.rhash, b.svc_id, sn, p.kind, p.code);
+        const SigCache::Rec *h1 = hit;
+        if (!hit && b.l2) hit = b.l2->find(p.sig, b.rhash, b.svc_id, sn, p.kind, p.code);
+        b.own_lookups += 1;
+        b.own_hits += h1 ? 1u : 0u;
+      }
+      if (!hit) {
+        ss.p = p.at;  // (a span's field was read whole: ss was fine there)
+        return true;
+      }
+      if (p.en > b.out.max_end) b.out.max_end = p.en;
+      const uint32_t kk = p.kind >= 0 && p.kind <= 7 ? (uint32_t)p.kind : 7u;
+      const uint32_t cc = p.code >= 0 && p.code <= 3 ? (uint32_t)p.code : 3u;
+      b.out.push(hit->sid, p.st, p.en, p.w0, p.w1, b.svc_id | (kk << 16) | (cc << 19));
+      ++b.spans;
+    }
+  }
+}
+}  // namespace
 
 struct Columnizer::Worker {
   Cols cols;
@@ -996,166 +1164,26 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
       PB ss = scan.sub();
       uint32_t h;
       int wt3;
-      // The batched path (neither exemplars nor events, and lookups that miss
-      // the CPU caches): spans are parsed kBatch at a time, each one's
-      // signature-cache records prefetched as soon as its hash is known, then
-      // resolved in order, so a batch's memory accesses overlap instead of
-      // following each other.  A span it cannot resolve (unknown signature, a
-      // dimension value that is not a string, anything malformed) goes through
-      // the full path below, which keys it, reports it or fails as always.
-      auto &pend = w.pend;
-      std::string &arena = w.arena;
-      pend.clear();
-      arena.clear();
-      size_t cur = 0;  // the next pending span to resolve
-      const bool own = w.own_cache_on;
-      const size_t nd = opt_.dims.size();
+      // One loop: in batched mode batch_hits emits the spans whose signature
+      // the caches hold and stops at the first it cannot resolve, with the
+      // scope's parser back at that span; the full path below takes that one
+      // span, then the batched mode resumes.  (Only copies of the parser go
+      // to batch_hits, so the plain loop's state stays in registers.)
+      BatchScope bs{w.pend, w.arena, w.dim_val, w.dim_type, w.own_cache_on, opt_.dims, rattrs, rhash, svc_id,
+                    cache, l2, out, res.spans, w.own_lookups, w.own_hits};
       for (;;) {
-        PB sp(nullptr, nullptr);
-        if (!batched) {
-          if (!ss.next(h, wt3)) break;
-          if (h != 2 || wt3 != 2) {
-            ss.skip(wt3);
-            continue;
-          }
-          sp = ss.sub();
-        } else {
-          if (cur == pend.size()) {  // parse the next batch
-            pend.clear();
-            arena.clear();
-            cur = 0;
-            while (pend.size() < kBatch && ss.next(h, wt3)) {
-              if (h != 2 || wt3 != 2) {
-                ss.skip(wt3);
-                continue;
-              }
-              PB sp = ss.sub();
-              pend.emplace_back();
-              FastSpan &p = pend.back();
-              p.b = sp.p, p.e = sp.end;
-              const uint8_t *tid = nullptr;
-              size_t tid_len = 0;
-              std::string_view name;
-              int32_t kind = 0, code = 0;
-              uint64_t st = 0, en = 0;
-              // (per dimension: its last string value among the span attributes;
-              // type 2 = a value of another type, which span_body keys)
-              auto &dv = w.dim_val;
-              auto &dt = w.dim_type;
-              dv.assign(nd, std::string_view());
-              dt.assign(nd, 0);
-              bool slow = false;
-              uint32_t k;
-              int wt4;
-              while (sp.next(k, wt4)) {
-                if (k == 1 && wt4 == 2) {
-                  const std::string_view t = sp.str();
-                  tid = reinterpret_cast<const uint8_t *>(t.data());
-                  tid_len = t.size();
-                } else if (k == 5 && wt4 == 2) {
-                  name = sp.str();
-                } else if (k == 6 && wt4 == 0) {
-                  kind = (int32_t)(uint32_t)sp.varint();
-                } else if (k == 7 && wt4 == 1) {
-                  st = sp.fixed64();
-                } else if (k == 8 && wt4 == 1) {
-                  en = sp.fixed64();
-                } else if (k == 9 && wt4 == 2 && nd) {
-                  std::string_view key;
-                  Any v;
-                  if (!parse_kv(sp.sub(), key, v)) {
-                    slow = true;
-                    continue;
-                  }
-                  for (size_t d = 0; d < nd; ++d)
-                    if (opt_.dims[d].name == key) dt[d] = v.type == kStr ? 1 : 2, dv[d] = v.s;
-                } else if (k == 15 && wt4 == 2) {
-                  PB stt = sp.sub();
-                  uint32_t m;
-                  int wt5;
-                  code = 0;  // a later Status message replaces an earlier one
-                  while (stt.next(m, wt5)) {
-                    if (m == 3 && wt5 == 0) code = (int32_t)(uint32_t)stt.varint();
-                    else stt.skip(wt5);
-                  }
-                  if (!stt.ok) slow = true;
-                } else {
-                  sp.skip(wt4);
-                }
-              }
-              if (!sp.ok || !SigCache::cacheable(kind, code)) slow = true;
-              p.name = reinterpret_cast<const uint8_t *>(name.data());
-              p.nlen = (uint32_t)name.size();
-              if (dims && !slow) {  // the signature name as span_body builds it
-                p.noff = (uint32_t)arena.size();
-                arena.append(name);
-                for (size_t d = 0; d < nd && !slow; ++d) {
-                  char tag = '\x02';
-                  std::string_view val = dv[d];
-                  if (dt[d] == 2) {
-                    slow = true;
-                    break;
-                  }
-                  if (!dt[d]) {
-                    const Any *v = find_attr(rattrs, opt_.dims[d].name);
-                    if (!v) {
-                      arena += '\x03';
-                      continue;
-                    }
-                    if (v->type != kStr) {
-                      slow = true;
-                      break;
-                    }
-                    tag = '\x04', val = v->s;
-                  }
-                  const uint32_t n = (uint32_t)val.size();
-                  arena += tag;
-                  arena.append(reinterpret_cast<const char *>(&n), 4);
-                  arena.append(val);
-                }
-                p.nlen = (uint32_t)(arena.size() - p.noff);
-              }
-              p.slow = slow;
-              if (!slow) {
-                p.kind = kind, p.code = code, p.st = st, p.en = en;
-                const bool has_tid = tid && tid_len == 16;
-                p.w0 = has_tid ? rd64(tid) : 0, p.w1 = has_tid ? rd64(tid + 8) : 0;
-                const std::string_view sn = dims ? std::string_view(arena.data() + p.noff, p.nlen) : name;
-                p.sig = SigCache::hash(rhash, svc_id, sn, kind, code);
-                if (own) cache.prefetch(p.sig);
-                if (l2) l2->prefetch(p.sig);
-              }
-            }
-            if (pend.empty()) break;
-          }
-          // resolve in order: the hits are emitted here, the first miss goes
-          // through the full path (the rest of the batch waits for it)
-          bool full = false;
-          while (cur < pend.size() && !full) {
-            const FastSpan &p = pend[cur++];
-            const SigCache::Rec *hit = nullptr;
-            if (!p.slow) {
-              const std::string_view sn = dims ? std::string_view(arena.data() + p.noff, p.nlen)
-                                               : std::string_view(reinterpret_cast<const char *>(p.name), p.nlen);
-              if (own) hit = cache.find(p.sig, rhash, svc_id, sn, p.kind, p.code);
-              const SigCache::Rec *h1 = hit;
-              if (!hit && l2) hit = l2->find(p.sig, rhash, svc_id, sn, p.kind, p.code);
-              w.own_lookups += 1;
-              w.own_hits += h1 ? 1u : 0u;
-            }
-            if (!hit) {
-              sp = PB(p.b, p.e);
-              full = true;
-              break;
-            }
-            if (p.en > out.max_end) out.max_end = p.en;
-            const uint32_t kk = p.kind >= 0 && p.kind <= 7 ? (uint32_t)p.kind : 7u;
-            const uint32_t cc = p.code >= 0 && p.code <= 3 ? (uint32_t)p.code : 3u;
-            out.push(hit->sid, p.st, p.en, p.w0, p.w1, svc_id | (kk << 16) | (cc << 19));
-            ++res.spans;
-          }
-          if (!full) continue;
+        if (batched) {
+          PB bss = ss;
+          const bool more = batch_hits(bs, bss);
+          ss = bss;
+          if (!more) break;
         }
+        if (!ss.next(h, wt3)) break;
+        if (h != 2 || wt3 != 2) {
+          ss.skip(wt3);
+          continue;
+        }
+        PB sp = ss.sub();
         // the full path: one span, any configuration
         const uint8_t *span_begin = sp.p, *span_end = sp.end;
         const uint8_t *tid = nullptr, *spid = nullptr;
@@ -1392,7 +1420,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
           out.push(esid, 0, 0, 0, 0, 0xFFFFu);
           ++res.event_records;
         }
-      }
+            }
       if (!ss.ok) return fail(Result::kError, "malformed ScopeSpans");
     }
     if (!scan.ok) return fail(Result::kError, "malformed ResourceSpans");
