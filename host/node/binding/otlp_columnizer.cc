@@ -296,6 +296,29 @@ bool valid_any_body(PB pb, int depth) {
   return pb.ok;
 }
 
+// parse_any and valid_any_body(pb, 0) in one walk over the body: the value
+// (last field wins) and, in ok, whether the body is well formed (every array
+// or kvlist field in it checked, as valid_any_body does)
+Any parse_any_valid(PB pb, bool &ok) {
+  Any a;
+  ok = true;
+  uint32_t f;
+  int wt;
+  while (pb.next(f, wt)) {
+    if (f == 1 && wt == 2) a = Any{}, a.type = kStr, a.s = pb.str();
+    else if (f == 2 && wt == 0) a = Any{}, a.type = kBool, a.b = pb.varint() != 0;
+    else if (f == 3 && wt == 0) a = Any{}, a.type = kInt, a.i = (int64_t)pb.varint();
+    else if (f == 4 && wt == 1) a = Any{}, a.type = kDouble, a.d = pb.dbl();
+    else if ((f == 5 || f == 6) && wt == 2) {
+      a = Any{}, a.type = f == 5 ? kArray : kKvlist, a.body = pb.sub();
+      if (ok && !valid_nested(a.body, f == 6, 0)) ok = false;
+    } else if (f == 7 && wt == 2) a = Any{}, a.type = kBytes, a.s = pb.str();
+    else pb.skip(wt);
+  }
+  if (!pb.ok) a.type = kEmpty, a.body = PB(nullptr, nullptr), a.s = {}, a.i = 0, ok = false;
+  return a;
+}
+
 // KeyValue -> (key, value); false on malformed input, a malformed or too
 // deeply nested value included (the request is then rejected, as the Go
 // collector's unmarshal and otlp.js reject it)
@@ -309,9 +332,7 @@ bool parse_kv(PB pb, std::string_view &key, Any &val) {
     if (f == 1 && wt == 2) {
       key = pb.str();
     } else if (f == 2 && wt == 2) {
-      const PB body = pb.sub();
-      val = parse_any(body);
-      vok = valid_any_body(body, 0);
+      val = parse_any_valid(pb.sub(), vok);
     } else {
       pb.skip(wt);
     }
