@@ -18,6 +18,7 @@
 #   btagg_<wl>       bench of <wl> with 512- and 1,024-thread aggregate workgroups (2 rounds)
 #   labbin_<KNOB=v>  the binned parity suites on the laboratory build with KNOB=v
 #   hostprof_<t>     host_rate.js (GPU ingest, t threads) under node --cpu-prof
+#   hostprofc4_<t>   the same over the C4 vocabulary (--highcard)
 #   colab            colbench against host/node/build/$COL_OTHER (3 rounds, 16 and 8 threads)
 #   colbench         the native columnizer alone (host/node/build/colbench) at 1-16 threads
 #   labexpo_<KNOB=v> the exponential-histogram suites on the laboratory build with KNOB=v
@@ -89,6 +90,8 @@ for step in "$@"; do
         run "colab_${b}_t${t}_r$r" 120 host/node/build/$b /tmp/req_plain.bin --threads "$t"; done; done; done ;;
     hostprof_*) t=${step#hostprof_}; run "hostprof_t$t" 200 node --cpu-prof --cpu-prof-dir="$OUT/hostprof_t$t" \
         --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 ;;
+    hostprofc4_*) t=${step#hostprofc4_}; run "hostprofc4_t$t" 300 node --cpu-prof --cpu-prof-dir="$OUT/hostprofc4_t$t" \
+        --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 --highcard ;;
     hostex_*) t=${step#hostex_}; run "hostex_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 --exemplars --events ;;
     hostc4_*) t=${step#hostc4_}; run "hostc4_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 --highcard ;;
     host_*) t=${step#host_}; run "host_t$t" 200 node --max-old-space-size=16000 host/node/test/host_rate.js 2000000 --gpu --threads "$t" --batch 128 ;;
