@@ -755,103 +755,103 @@ __attribute__((noinline)) bool batch_hits(BatchScope &b, PB &ss) {
           at = ss.p;
           continue;
         }
-      PB sp = ss.sub();
-      pend.emplace_back();
-      FastSpan &p = pend.back();
-      p.at = at;
-      at = ss.p;
-      const uint8_t *tid = nullptr;
-      size_t tid_len = 0;
-      std::string_view name;
-      int32_t kind = 0, code = 0;
-      uint64_t st = 0, en = 0;
-      // (per dimension: its last string value among the span attributes;
-      // type 2 = a value of another type, which span_body keys)
-      auto &dv = b.dv;
-      auto &dt = b.dt;
-      dv.assign(nd, std::string_view());
-      dt.assign(nd, 0);
-      bool slow = false;
-      uint32_t k;
-      int wt4;
-      while (sp.next(k, wt4)) {
-        if (k == 1 && wt4 == 2) {
-          const std::string_view t = sp.str();
-          tid = reinterpret_cast<const uint8_t *>(t.data());
-          tid_len = t.size();
-        } else if (k == 5 && wt4 == 2) {
-          name = sp.str();
-        } else if (k == 6 && wt4 == 0) {
-          kind = (int32_t)(uint32_t)sp.varint();
-        } else if (k == 7 && wt4 == 1) {
-          st = sp.fixed64();
-        } else if (k == 8 && wt4 == 1) {
-          en = sp.fixed64();
-        } else if (k == 9 && wt4 == 2 && nd) {
-          std::string_view key;
-          Any v;
-          if (!parse_kv(sp.sub(), key, v)) {
-            slow = true;
-            continue;
-          }
-          for (size_t d = 0; d < nd; ++d)
-            if (b.dims[d].name == key) dt[d] = v.type == kStr ? 1 : 2, dv[d] = v.s;
-        } else if (k == 15 && wt4 == 2) {
-          PB stt = sp.sub();
-          uint32_t m;
-          int wt5;
-          code = 0;  // a later Status message replaces an earlier one
-          while (stt.next(m, wt5)) {
-            if (m == 3 && wt5 == 0) code = (int32_t)(uint32_t)stt.varint();
-            else stt.skip(wt5);
-          }
-          if (!stt.ok) slow = true;
-        } else {
-          sp.skip(wt4);
-        }
-      }
-      if (!sp.ok || !SigCache::cacheable(kind, code)) slow = true;
-      p.name = reinterpret_cast<const uint8_t *>(name.data());
-      p.nlen = (uint32_t)name.size();
-      if (nd && !slow) {  // the signature name as span_body builds it
-        p.noff = (uint32_t)arena.size();
-        arena.append(name);
-        for (size_t d = 0; d < nd && !slow; ++d) {
-          char tag = '\x02';
-          std::string_view val = dv[d];
-          if (dt[d] == 2) {
-            slow = true;
-            break;
-          }
-          if (!dt[d]) {
-            const Any *v = find_attr(b.rattrs, b.dims[d].name);
-            if (!v) {
-              arena += '\x03';
+        PB sp = ss.sub();
+        pend.emplace_back();
+        FastSpan &p = pend.back();
+        p.at = at;
+        at = ss.p;
+        const uint8_t *tid = nullptr;
+        size_t tid_len = 0;
+        std::string_view name;
+        int32_t kind = 0, code = 0;
+        uint64_t st = 0, en = 0;
+        // (per dimension: its last string value among the span attributes;
+        // type 2 = a value of another type, which the full path keys)
+        auto &dv = b.dv;
+        auto &dt = b.dt;
+        dv.assign(nd, std::string_view());
+        dt.assign(nd, 0);
+        bool slow = false;
+        uint32_t k;
+        int wt4;
+        while (sp.next(k, wt4)) {
+          if (k == 1 && wt4 == 2) {
+            const std::string_view t = sp.str();
+            tid = reinterpret_cast<const uint8_t *>(t.data());
+            tid_len = t.size();
+          } else if (k == 5 && wt4 == 2) {
+            name = sp.str();
+          } else if (k == 6 && wt4 == 0) {
+            kind = (int32_t)(uint32_t)sp.varint();
+          } else if (k == 7 && wt4 == 1) {
+            st = sp.fixed64();
+          } else if (k == 8 && wt4 == 1) {
+            en = sp.fixed64();
+          } else if (k == 9 && wt4 == 2 && nd) {
+            std::string_view key;
+            Any v;
+            if (!parse_kv(sp.sub(), key, v)) {
+              slow = true;
               continue;
             }
-            if (v->type != kStr) {
+            for (size_t d = 0; d < nd; ++d)
+              if (b.dims[d].name == key) dt[d] = v.type == kStr ? 1 : 2, dv[d] = v.s;
+          } else if (k == 15 && wt4 == 2) {
+            PB stt = sp.sub();
+            uint32_t m;
+            int wt5;
+            code = 0;  // a later Status message replaces an earlier one
+            while (stt.next(m, wt5)) {
+              if (m == 3 && wt5 == 0) code = (int32_t)(uint32_t)stt.varint();
+              else stt.skip(wt5);
+            }
+            if (!stt.ok) slow = true;
+          } else {
+            sp.skip(wt4);
+          }
+        }
+        if (!sp.ok || !SigCache::cacheable(kind, code)) slow = true;
+        p.name = reinterpret_cast<const uint8_t *>(name.data());
+        p.nlen = (uint32_t)name.size();
+        if (nd && !slow) {  // the signature name as span_body builds it
+          p.noff = (uint32_t)arena.size();
+          arena.append(name);
+          for (size_t d = 0; d < nd && !slow; ++d) {
+            char tag = '\x02';
+            std::string_view val = dv[d];
+            if (dt[d] == 2) {
               slow = true;
               break;
             }
-            tag = '\x04', val = v->s;
+            if (!dt[d]) {
+              const Any *v = find_attr(b.rattrs, b.dims[d].name);
+              if (!v) {
+                arena += '\x03';
+                continue;
+              }
+              if (v->type != kStr) {
+                slow = true;
+                break;
+              }
+              tag = '\x04', val = v->s;
+            }
+            const uint32_t n = (uint32_t)val.size();
+            arena += tag;
+            arena.append(reinterpret_cast<const char *>(&n), 4);
+            arena.append(val);
           }
-          const uint32_t n = (uint32_t)val.size();
-          arena += tag;
-          arena.append(reinterpret_cast<const char *>(&n), 4);
-          arena.append(val);
+          p.nlen = (uint32_t)(arena.size() - p.noff);
         }
-        p.nlen = (uint32_t)(arena.size() - p.noff);
-      }
-      p.slow = slow;
-      if (!slow) {
-        p.kind = kind, p.code = code, p.st = st, p.en = en;
-        const bool has_tid = tid && tid_len == 16;
-        p.w0 = has_tid ? rd64(tid) : 0, p.w1 = has_tid ? rd64(tid + 8) : 0;
-        const std::string_view sn = nd ? std::string_view(arena.data() + p.noff, p.nlen) : name;
-        p.sig = SigCache::hash(b.rhash, b.svc_id, sn, kind, code);
-        if (b.own) b.cache.prefetch(p.sig);
-        if (b.l2) b.l2->prefetch(p.sig);
-      }
+        p.slow = slow;
+        if (!slow) {
+          p.kind = kind, p.code = code, p.st = st, p.en = en;
+          const bool has_tid = tid && tid_len == 16;
+          p.w0 = has_tid ? rd64(tid) : 0, p.w1 = has_tid ? rd64(tid + 8) : 0;
+          const std::string_view sn = nd ? std::string_view(arena.data() + p.noff, p.nlen) : name;
+          p.sig = SigCache::hash(b.rhash, b.svc_id, sn, kind, code);
+          if (b.own) b.cache.prefetch(p.sig);
+          if (b.l2) b.l2->prefetch(p.sig);
+        }
       }
       if (pend.empty()) return false;
     }
