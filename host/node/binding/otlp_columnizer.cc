@@ -813,7 +813,7 @@ __attribute__((noinline)) bool batch_hits(BatchScope &b, PB &ss) {
         if (!sp.ok || !SigCache::cacheable(kind, code)) slow = true;
         p.name = reinterpret_cast<const uint8_t *>(name.data());
         p.nlen = (uint32_t)name.size();
-        if (nd && !slow) {  // the signature name as span_body builds it
+        if (nd && !slow) {  // the signature name as the full path builds it
           p.noff = (uint32_t)arena.size();
           arena.append(name);
           for (size_t d = 0; d < nd && !slow; ++d) {
