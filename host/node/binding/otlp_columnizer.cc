@@ -656,14 +656,15 @@ const SigCache::Rec *SigCache::find(uint64_t h, uint64_t rhash, uint32_t svc, st
                                     int32_t code) const {
   if (recs_.empty()) return nullptr;
   const size_t mask = recs_.size() - 1;
-  const uint32_t n = (uint32_t)name.size(), ni = n < kInline ? n : kInline;
+  const uint32_t n = (uint32_t)name.size();
   for (size_t i = h & mask;; i = (i + 1) & mask) {
     const Rec &r = recs_[i];
     if (!r.h) return nullptr;
     if (r.h != h) continue;
+    // a short name is compared in the record, a longer one in the arena
+    // (which holds every name whole: one compare either way)
     if (r.rhash == rhash && r.svc == svc && r.kind == kind && r.code == code && r.name_len == n &&
-        std::memcmp(r.name, name.data(), ni) == 0 &&
-        (n <= kInline || std::memcmp(names_.data() + r.name_off + kInline, name.data() + kInline, n - kInline) == 0))
+        std::memcmp(n <= kInline ? r.name : names_.data() + r.name_off, name.data(), n) == 0)
       return &r;
   }
 }
@@ -733,7 +734,7 @@ struct BatchScope {
   const SigCache &cache;
   const SigCache *l2;
   Cols &out;
-  uint64_t &spans, &own_lookups, &own_hits;
+  uint64_t &spans, &own_misses;
 };
 // Emits the hits up to the next span the full path must take (true, with ss
 // back at that span's field) or to the scope's end (false).  Out of line:
@@ -861,10 +862,10 @@ __attribute__((noinline)) bool batch_hits(BatchScope &b, PB &ss) {
         const std::string_view sn = nd ? std::string_view(arena.data() + p.noff, p.nlen)
                                        : std::string_view(reinterpret_cast<const char *>(p.name), p.nlen);
         if (b.own) hit = b.cache.find(p.sig, b.rhash, b.svc_id, sn, p.kind, p.code);
-        const SigCache::Rec *h1 = hit;
-        if (!hit && b.l2) hit = b.l2->find(p.sig, b.rhash, b.svc_id, sn, p.kind, p.code);
-        b.own_lookups += 1;
-        b.own_hits += h1 ? 1u : 0u;
+        if (!hit) {
+          b.own_misses += 1;
+          if (b.l2) hit = b.l2->find(p.sig, b.rhash, b.svc_id, sn, p.kind, p.code);
+        }
       }
       if (!hit) {
         ss.p = p.at;  // (a span's field was read whole: ss was fine there)
@@ -888,7 +889,9 @@ struct Columnizer::Worker {
   std::vector<std::string_view> dim_val;
   std::vector<uint8_t> dim_type;
   bool own_cache_on = true;  // probe `cache` before the shared one (see columnize_batch)
-  uint64_t own_lookups = 0, own_hits = 0, batches = 0;
+  // spans decoded and own-cache misses (skipped probes included) since the
+  // last decision; the hits are the difference (see columnize_batch)
+  uint64_t own_spans = 0, own_misses = 0, batches = 0;
   std::vector<Attr> rattrs, sattrs, eattrs;
   std::vector<const Attr *> hv;
   std::string tmp, keystr, sname, service, evkey, sigbuf;
@@ -1049,6 +1052,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
   // a function of exactly these, the service and the resource identity (a
   // non-string value takes the full path)
   const bool dims = !opt_.dims.empty();
+  const bool own_on = w.own_cache_on;  // (fixed for the call: a local, not a load per span)
   w.exl.clear();
   PB req(buf, buf + len);
   uint32_t f;
@@ -1173,7 +1177,7 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
     // lookups will miss the CPU caches: this thread's own cache is not probed
     // (a high-cardinality stream, see columnize_batch) or holds more
     // signatures than a core's caches do
-    const bool batched = !opt_.events && !opt_.exemplars && (!w.own_cache_on || cache.size() > kBatchAbove || opt_.test_batched);
+    const bool batched = !opt_.events && !opt_.exemplars && (!own_on || cache.size() > kBatchAbove || opt_.test_batched);
     PB scan = rs;
     uint32_t g;
     int wt2;
@@ -1190,8 +1194,8 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
       // scope's parser back at that span; the full path below takes that one
       // span, then the batched mode resumes.  (Only copies of the parser go
       // to batch_hits, so the plain loop's state stays in registers.)
-      BatchScope bs{w.pend, w.arena, w.dim_val, w.dim_type, w.own_cache_on, opt_.dims, rattrs, rhash, svc_id,
-                    cache, l2, out, res.spans, w.own_lookups, w.own_hits};
+      BatchScope bs{w.pend, w.arena, w.dim_val, w.dim_type, own_on, opt_.dims, rattrs, rhash, svc_id,
+                    cache, l2, out, res.spans, w.own_misses};
       for (;;) {
         if (batched) {
           PB bss = ss;
@@ -1285,10 +1289,11 @@ bool Columnizer::run(const uint8_t *buf, size_t len, Worker &w, Cols &out, SigCa
         bool l2_hit = false;  // (an entry of the shared cache is read only here)
         if (use_cache && SigCache::cacheable(kind, code)) {
           sig = SigCache::hash(rhash, svc_id, signame, kind, code);
-          if (w.own_cache_on) hit = cache.find(sig, rhash, svc_id, signame, kind, code);
-          if (!hit && l2 && (hit = l2->find(sig, rhash, svc_id, signame, kind, code))) l2_hit = true;
-          w.own_lookups += 1;
-          w.own_hits += hit && !l2_hit ? 1u : 0u;
+          if (own_on) hit = cache.find(sig, rhash, svc_id, signame, kind, code);
+          if (!hit) {
+            w.own_misses += 1;  // (rare where the own cache pays: one store per miss)
+            if (l2 && (hit = l2->find(sig, rhash, svc_id, signame, kind, code))) l2_hit = true;
+          }
         }
         // key = buildKey, into keystr (0 = built; else the failure to return)
         auto build_key = [&]() -> int {
@@ -1517,18 +1522,20 @@ BatchResult Columnizer::columnize_batch(const uint8_t *const *bufs, const size_t
   constexpr size_t kOwnCacheMax = 1u << 15;
   if (shared_.gen != gen_) shared_.clear(), shared_.gen = gen_;
   for (auto &w : workers_) {
+    // a thread's own cache pays only when its hot set fits it: past ~4 k
+    // spans with fewer than 1 in 8 answered there (a high-cardinality
+    // stream), it is not probed (its inserts still feed the shared cache);
+    // every 32nd batch probes it again to re-sample.  (The spans are counted
+    // from the thread's columns of the last batch, the misses in run.)
+    w->own_spans += w->cols.size();
     w->cols.clear();
     if (w->cache.gen != gen_ || w->cache.size() > kOwnCacheMax) w->cache.clear(), w->cache.gen = gen_;
-    // a thread's own cache pays only when its hot set fits it: past ~4 k
-    // lookups with fewer than 1 in 8 answered there (a high-cardinality
-    // stream), it is not probed (its inserts still feed the shared cache);
-    // every 32nd batch probes it again to re-sample
     w->batches += 1;
-    if (w->own_lookups >= 4096) {
-      w->own_cache_on = 8 * w->own_hits >= w->own_lookups;
-      w->own_lookups = w->own_hits = 0;
+    if (w->own_spans >= 4096) {
+      w->own_cache_on = 8 * (w->own_spans - std::min(w->own_misses, w->own_spans)) >= w->own_spans;
+      w->own_spans = w->own_misses = 0;
     }
-    if (!w->own_cache_on && (w->batches & 31u) == 0) w->own_cache_on = true, w->own_lookups = w->own_hits = 0;
+    if (!w->own_cache_on && (w->batches & 31u) == 0) w->own_cache_on = true, w->own_spans = w->own_misses = 0;
   }
   using clk = std::chrono::steady_clock;
   const auto ns_since = [](clk::time_point t) {

@@ -249,11 +249,12 @@ class SigCache {
     std::string key;                      // events.enabled: the span key string (see insert)
   };
   // One cache line holds everything a lookup compares and its answer: the
-  // full hash, the series id, the signature's fields and the first kInline
-  // bytes of its name (the rest, if any, in names_).  A high-cardinality
-  // stream's table is far larger than the CPU caches, so a hit costs one
-  // memory access (two for a longer name) instead of the three of a slot
-  // array, an entry array and a name arena.
+  // full hash, the series id, the signature's fields and, for a name of at
+  // most kInline bytes, the name itself (a longer one is compared in names_,
+  // which holds every name).  A high-cardinality stream's table is far larger
+  // than the CPU caches, so a hit costs one memory access (two for a longer
+  // name) instead of the three of a slot array, an entry array and a name
+  // arena.
   static constexpr uint32_t kInline = 20;
   struct alignas(64) Rec {
     uint64_t h;  // 0: free
