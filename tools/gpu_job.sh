@@ -119,11 +119,6 @@ for step in "$@"; do
           run "libab_${wl}_${lib}$([ "$lib" = libspanagg ] && echo "_vs_$other")_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 50 --soak-s 0 --no-filter-off \
           ${NPS:+--names-per-service $NPS} $BQ
       done; done ;;
-    btpipe2_*) wl=${step#btpipe2_}  # paired aggregates on the engine stream (1) / the caller's stream (2), 1 and 2 launch streams
-      for r in 1 2; do for ns in 1 2; do for pp in 1 2; do
-        SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_BT_PIPE=$pp \
-          run "btpipe2_${wl}_p${pp}_s${ns}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --streams $ns --soak-s 0 --no-filter-off $BQ
-      done; done; done ;;
     btpair_*) wl=${step#btpair_}  # binned launches aggregated in pairs / alone (laboratory build), rounds interleaved
       for r in 1 2 3; do for pp in 1 0; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_BT_PAIR=$pp \
