@@ -186,14 +186,19 @@ struct ExpoParams {
   uint32_t xG;
   // small-table bucket counting (expo_count_slab with its entry selection / expo_fold_slab):
   uint32_t *lcount;         // [cap] this launch's positive durations per slot (reduce -> selection)
+  int2 *xmeta;              // [cap] {scale | buffer << 8, lo - (lo mod max_size)} per slot (reduce -> counting)
   uint32_t *slot_of_entry;  // [xc_ne] the entry's slot, ~0u: unused
-  uint32_t *xcslab;         // [xG][xc_ne][(max_size + 1) / 2] per-workgroup u16 bucket-count pairs
+  uint32_t *xcslab;         // [xG][xc_slab_stride] per-workgroup u16 bucket-count pairs ([xc_ne][(max_size + 1) / 2])
   uint32_t xc_ne;           // LDS entries of the counting kernel (0: the cached-probe kernel)
   // the counting kernel's tail (spans of series without an LDS entry): each
   // workgroup's (slot << 12 | bucket) records, sorted by fold bin of
-  // kXtBinSlots slots, [xG][kXtCap], and the bins' offsets [xG][nbins + 1];
+  // xt_bin_slots slots, [xG][kXtCap], and the bins' offsets [xG][nbins + 1];
   // expo_fold_kernel sums them per bin (nullptr: HBM atomics)
   uint32_t *xt_rec, *xt_off;  // (records past kXtCap take an HBM atomic)
+  // SA_OPT_STAMPS: the counting kernel's per-workgroup s_memrealtime stamps,
+  // in the ingest kernel's stamp rows (kDbgPerWg per workgroup; slots
+  // kXcStamp.. are the counting kernel's); nullptr: none
+  unsigned long long *dbg;
 };
 // A span record of the exponential-histogram slab path: the key slot in the
 // top 12 bits (kSpanRecNoSlot: none; slab tables have <= 2,048 slots) and the
@@ -225,8 +230,18 @@ __host__ __device__ inline uint32_t ixrec_of(uint32_t slot, int32_t scale, int32
 // log2(div) in the fast bucket index's 8.24 fixed point (expo_index_fast)
 __host__ inline int32_t expo_l2d_q24(double div) { return (int32_t)std::llround(std::log2(div) * 16777216.0); }
 constexpr uint32_t kXtCap = 4096;       // tail records per counting workgroup (16 KiB of LDS)
-constexpr uint32_t kXtBinSlots = 8;     // slots per tail fold bin
-__host__ __device__ inline uint32_t xt_bins(uint64_t cap) { return (uint32_t)((cap + kXtBinSlots - 1) / kXtBinSlots); }
+// slots per tail fold bin: 16 (a fold workgroup counts [16][max_size] u32 in
+// LDS), 8 past max_size 2,048; one fold round at C2's 2,048 slots (128 bins)
+constexpr uint32_t kXtBinSlotsMax = 16;
+__host__ __device__ inline uint32_t xt_bin_slots(uint32_t max_size) { return max_size <= 2048 ? 16u : 8u; }
+__host__ __device__ inline uint32_t xt_bins(uint64_t cap, uint32_t max_size) {
+  return (uint32_t)((cap + xt_bin_slots(max_size) - 1) / xt_bin_slots(max_size));
+}
+// the counting slab's words per workgroup: xc_ne entries of (max_size + 1) / 2
+// u16 pairs, padded to 16 B (the fold reads four words a lane)
+__host__ __device__ inline uint32_t xc_slab_stride(uint32_t ne, uint32_t max_size) {
+  return (ne * ((max_size + 1) / 2) + 3u) & ~3u;
+}
 __host__ __device__ ExpoHdr expo_hdr_empty();
 constexpr uint32_t kExpoMaxSize = 4096;
 
@@ -429,6 +444,10 @@ constexpr uint32_t kPoolMaxStatic = (kMaxWgSpans - kPoolMaxSteal * kPoolSpans) /
 constexpr uint32_t kPoolMaxWgSpans = kPoolMaxStatic + kPoolMaxSteal * kPoolSpans;
 constexpr uint32_t kPoolMinStatic = 32 * 256;  // two fixed chunks per wave before any claim
 constexpr uint32_t kDbgPerWg = 136;  // diagnostic stamps per workgroup: 8 + 16 waves x 8
+// the exponential counting kernel's stamps in the same rows (slots the ingest
+// kernel leaves free): start, prologue done, loop done, end at 4..7, and its
+// slab stores issued in the last slot
+constexpr uint32_t kXcStamp = 4, kXcStampSlab = kDbgPerWg - 1;
 constexpr uint32_t kHllQueue = 2048;  // deferred HLL raises per workgroup (8 B each)
 constexpr uint32_t kErrTab = 1024;    // LDS (window, slot) -> ERROR count table per workgroup (4 B each)
 // ingest_lds_kernel LDS beyond the table: HLL queue + its count + bin table

@@ -554,11 +554,11 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
             return bail(fail(e, SA_EDEVICE, "event creation failed"));
       }
       if (e->xc_ne &&
-          ((rc = alloc((void **)&e->xc_lcount, e->cap * 4)) ||
+          ((rc = alloc((void **)&e->xc_lcount, e->cap * 12)) ||  // lcount [cap], then xmeta [cap]
            (rc = alloc((void **)&e->xc_slot_of_entry, (size_t)e->xc_ne * 4)) ||
-           (rc = alloc((void **)&e->xcslab, (size_t)e->G * e->xc_ne * ((cfg->exp_max_size + 1) / 2) * 4)) ||
+           (rc = alloc((void **)&e->xcslab, (size_t)e->G * sa::xc_slab_stride(e->xc_ne, cfg->exp_max_size) * 4)) ||
            (rc = alloc((void **)&e->xt_rec, (size_t)e->G * sa::kXtCap * 4)) ||
-           (rc = alloc((void **)&e->xt_off, (size_t)e->G * (sa::xt_bins(e->cap) + 1) * 4))))
+           (rc = alloc((void **)&e->xt_off, (size_t)e->G * (sa::xt_bins(e->cap, cfg->exp_max_size) + 1) * 4))))
         return bail(rc);
       // (window, slot) keys of the LDS ERROR table are 16-bit
       if ((uint64_t)cfg->n_windows * e->cap < 65535 &&
@@ -873,6 +873,7 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b, uint32_t
   E.xG = e->G;
   E.xc_ne = e->expo_small ? e->xc_ne : 0u;
   E.lcount = E.xc_ne ? e->xc_lcount : nullptr;
+  E.xmeta = E.xc_ne ? reinterpret_cast<int2 *>(e->xc_lcount + e->cap) : nullptr;
   E.slot_of_entry = e->xc_slot_of_entry;
   E.xcslab = e->xcslab;
   {
@@ -885,6 +886,7 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b, uint32_t
     E.xt_rec = xt && E.xc_ne ? e->xt_rec : nullptr;
     E.xt_off = e->xt_off;
   }
+  E.dbg = e->dbg;
   return E;
 }
 

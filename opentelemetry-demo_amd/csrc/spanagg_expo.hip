@@ -206,6 +206,14 @@ __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E)
   const bool owner = gg == 0 && s < E.cap;
   ExpoHdr h{};
   if (owner) h = E.hdr[s];
+  // the counting kernel's word of the slot (its scale, bucket buffer and the
+  // multiple of M below its kept range), so its 256 workgroups read 8 B a
+  // slot instead of the 72-B header
+  auto put_meta = [&](const ExpoHdr &x) {
+    if (!E.xmeta) return;
+    const int32_t l = x.lo == kExpoEmpty ? 0 : x.lo;
+    E.xmeta[s] = make_int2((x.scale & 0xFF) | (int)(x.cur << 8), l - (int32_t)expo_mod(l, E.max_size));
+  };
   XHdr acc{0, 0, 0, 0, 0};
   if (s < E.cap) {
     for (uint32_t g0 = gg; g0 < E.xG; g0 += kXrBatch * kXrGroups) {
@@ -239,11 +247,14 @@ __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E)
   __syncthreads();
   if (!owner) return;
   acc = part[0][sl];
-#pragma unroll
+  // (two at a time: the 15 partials loaded at once held 120 registers and
+  // pushed the rescale's into scratch)
+#pragma unroll 2
   for (uint32_t k = 1; k < 16; ++k) xhdr_add(acc, part[k][sl]);
   if (E.lcount) E.lcount[s] = acc.cnt - acc.zero;  // this launch's positive durations (the entry selection)
   if (!acc.cnt) {  // no new values: the header (scale, range) stays as it is
     if (E.xscale) E.xscale[s] = (int8_t)h.scale;
+    put_meta(h);
     return;
   }
   const unsigned long long minpos = ~acc.minx;  // UINT64_MAX when no positive duration
@@ -258,9 +269,24 @@ __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E)
   rescale_hdr(E, s, h);
   E.hdr[s] = h;
   if (E.xscale) E.xscale[s] = (int8_t)h.scale;
+  put_meta(h);
 }
 
 constexpr uint32_t kXcBlock = 1024;
+
+// SA_OPT_STAMPS: a counting workgroup's phase stamp (thread 0, s_memrealtime)
+__device__ __forceinline__ void xc_stamp(const ExpoParams &E, uint32_t slot) {
+  if (threadIdx.x == 0) E.dbg[blockIdx.x * kDbgPerWg + slot] = __builtin_amdgcn_s_memrealtime();
+}
+// laboratory ablations of the counting and fold kernels (SPANAGG_XC_DIAG
+// bits; counts wrong): 2 = the counting loop's loads only, 4 = no slab
+// stores, 8 / 16 = no slab / tail fold.  (Bit 1, the tail's records off, is
+// older and in both builds.)
+#ifdef SPANAGG_AB
+#define XC_ABL(bit) ((E.diag & (bit)) != 0u)
+#else
+#define XC_ABL(bit) false
+#endif
 constexpr uint64_t kXcMaxSpans = 65535;  // u16 LDS counts: spans per counting workgroup
 
 // Bucket counting of small tables, two kernels:
@@ -315,13 +341,13 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *wsum, 
 }
 
 // The entry selection (cap <= 2,048: slots 2t and 2t + 1 of thread t) into
-// ent[cap] (LDS; -1: no entry).  scratch: 64 LDS words.  Workgroup 0 also
-// writes slot_of_entry (~0u past the selected ones) for expo_fold_slab_kernel.
-// lc: lcount of slots 2t and 2t + 1 (0 past cap), loaded by the caller ahead
-// of its other prologue reads.
-__device__ __forceinline__ void expo_select_lds(const ExpoParams &E, int32_t *ent, uint32_t *scratch,
-                                                const uint32_t (&lc)[2]) {
-  const uint32_t t = threadIdx.x, cap = (uint32_t)E.cap, K = E.xc_ne, lane = t & 63u;
+// en[2], the entries of thread t's two slots (-1: none).  scratch: 64 LDS
+// words.  Workgroup 0 also writes slot_of_entry (~0u past the selected ones)
+// for expo_fold_slab_kernel.  lc: lcount of slots 2t and 2t + 1 (0 past cap),
+// loaded by the caller ahead of its other prologue reads.
+__device__ __forceinline__ void expo_select_lds(const ExpoParams &E, uint32_t *scratch, const uint32_t (&lc)[2],
+                                                int32_t (&en)[2]) {
+  const uint32_t t = threadIdx.x, K = E.xc_ne, lane = t & 63u;
   uint32_t *hist = scratch, *wsum = scratch + 48;  // hist[33], wsum[16]
   uint32_t bl[2];
 #pragma unroll
@@ -360,8 +386,8 @@ __device__ __forceinline__ void expo_select_lds(const ExpoParams &E, int32_t *en
   const uint32_t n0 = sel0 ? 1u : 0u, n1 = sel1 ? 1u : 0u;
   uint32_t nsel;
   const uint32_t ex = block_excl_scan(n0 + n1, wsum, nsel);
-  if (2 * t < cap) ent[2 * t] = sel0 ? (int32_t)ex : -1;
-  if (2 * t + 1 < cap) ent[2 * t + 1] = sel1 ? (int32_t)(ex + n0) : -1;
+  en[0] = sel0 ? (int32_t)ex : -1;
+  en[1] = sel1 ? (int32_t)(ex + n0) : -1;
   if (blockIdx.x == 0) {
     if (sel0) E.slot_of_entry[ex] = 2 * t;
     if (sel1) E.slot_of_entry[ex + n0] = 2 * t + 1;
@@ -377,37 +403,42 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
   constexpr bool REC = IN == 1, IXR = IN == 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const uint32_t M = E.max_size, NE = E.xc_ne, cap = (uint32_t)E.cap, wpe = (M + 1) / 2;
-  int2 *meta = reinterpret_cast<int2 *>(smem);                   // [cap] {scale, cur}
-  int32_t *ent = reinterpret_cast<int32_t *>(meta + cap);         // [cap] entry or -1
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(ent + cap);        // [NE][wpe] u16 pairs
+  int2 *meta = reinterpret_cast<int2 *>(smem);                   // [cap] (below)
+  uint32_t *cnt = reinterpret_cast<uint32_t *>(meta + cap);       // [NE][wpe] u16 pairs
   uint32_t *scratch = cnt + NE * wpe;                             // [64] selection scratch
   // the tail: records of the spans without an entry, their count, and the
   // fold bins' histogram / cursors at the end
   uint32_t *trec = scratch + 64;                                  // [kXtCap]
   uint32_t *tmisc = trec + kXtCap;                                // [0] records, [1..] bin hist / cursors
   const bool tail = E.xt_rec != nullptr;
+  if (E.dbg) xc_stamp(E, kXcStamp);
   if (threadIdx.x == 0) tmisc[0] = 0;
   uint32_t lc[2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) lc[k] = 2 * threadIdx.x + k < cap ? E.lcount[2 * threadIdx.x + k] : 0u;
-  // meta: {scale (8 bits) | buffer << 8 | (lo mod M) << 9, lo}: this launch's
-  // positive values lie in the kept range [lo, lo + M), so a bucket position
-  // is lo's plus ix - lo, wrapped once
-  for (uint32_t i = threadIdx.x; i < cap; i += kXcBlock) {
-    const ExpoHdr &h = E.hdr[i];
-    const int32_t lo = h.lo == kExpoEmpty ? 0 : h.lo;
-    meta[i] = make_int2((h.scale & 0xFF) | (int)(h.cur << 8) | (int)(expo_mod(lo, M) << 9), lo);
-  }
+  // meta of slot s: {scale (8 bits) | buffer << 8 | (entry + 1) << 9, base},
+  // base = lo - (lo mod M), the multiple of M at or below the kept range's
+  // first index lo: a bucket index ix with ix - base in [0, 2M) sits at
+  // position (ix - base) wrapped once (this launch's positive values lie in
+  // [lo, lo + M)).  The reduce pass left all but the entry (xmeta); slots 2t
+  // and 2t + 1 are thread t's, as in the selection.
+  int4 xm = make_int4(0, 0, 0, 0);
+  if (2 * threadIdx.x < cap) xm = *reinterpret_cast<const int4 *>(E.xmeta + 2 * threadIdx.x);  // (cap even)
   for (uint32_t i = threadIdx.x; i < NE * wpe; i += kXcBlock) cnt[i] = 0;
-  expo_select_lds(E, ent, scratch, lc);
+  int32_t en[2];
+  expo_select_lds(E, scratch, lc, en);
+  if (2 * threadIdx.x < cap)
+    *reinterpret_cast<int4 *>(meta + 2 * threadIdx.x) =
+        make_int4(xm.x | (en[0] + 1) << 9, xm.y, xm.z | (en[1] + 1) << 9, xm.w);
   __syncthreads();
+  if (E.dbg) xc_stamp(E, kXcStamp + 1);
   const uint64_t lo = blockIdx.x * per_wg, hi = lo + per_wg < E.n ? lo + per_wg : E.n;
   const uint32_t len = hi > lo ? (uint32_t)(hi - lo) : 0u;
   // the span's bucket index ix at its series' scale -> its LDS entry or a tail record
   auto add = [&](uint32_t slot, int32_t ix, int2 m) {
-    const uint32_t rel = (uint32_t)(ix - m.y), a0 = ((uint32_t)m.x >> 9) + rel;
-    const uint32_t at = rel < M ? (a0 >= M ? a0 - M : a0) : expo_mod(ix, M);
-    const int32_t en_ = ent[slot];
+    const uint32_t rel = (uint32_t)(ix - m.y);
+    const uint32_t at = rel < 2 * M ? (rel >= M ? rel - M : rel) : expo_mod(ix, M);
+    const int32_t en_ = (int32_t)((uint32_t)m.x >> 9) - 1;
     if (en_ >= 0) {
       atomicAdd(&cnt[(uint32_t)en_ * wpe + (at >> 1)], 1u << ((at & 1u) * 16));
     } else if (!(E.diag & 1u)) {
@@ -512,26 +543,117 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
       }
     }
   };
+  // IXR: a thread's four index records with one LDS read each and no branch
+  // on the common path (a per-record early exit, long-duration branch and
+  // tail claim kept ~100 instructions a record under exec-mask branching;
+  // the loop was issue-bound at ~4x its loads' time): an entry's record is
+  // one LDS add; the tail's records of the quad claim their buffer slots with
+  // one LDS add per wave; the rare cases -- a long duration, a scale that
+  // rose, a bucket outside the kept range -- go through count_ix after a
+  // wave-uniform test.
+  auto count_quad = [&](uint32_t base, const Quad &q) {
+    uint32_t w[4], slot[4], at[4], en1[4];
+    bool tl[4], rare[4], add[4];
+    int2 m[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      w[j] = (uint32_t)q.r[j];
+      slot[j] = w[j] >> kIxSlotShift;
+      m[j] = meta[slot[j] & (cap - 1u)];
+    }
+    // (bitwise, not short-circuit, conditions: no branches)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool pos = (base + 4 * threadIdx.x + (uint32_t)j < len) & (slot[j] != kSpanRecNoSlot) &
+                       (w[j] != (slot[j] << kIxSlotShift | kIxZero));
+      const int32_t sn = (int32_t)(int8_t)(m[j].x & 0xFF);
+      const int32_t su = (int32_t)((w[j] >> kIxScaleShift) & 31u) - (int32_t)kIxScaleBias;
+      const int32_t ix = ((int32_t)(w[j] << 17) >> 18) >> ((su - sn) & 31);  // the 14-bit field, sign-extended
+      const uint32_t rel = (uint32_t)(ix - m[j].y);
+      at[j] = rel >= M ? rel - M : rel;
+      en1[j] = (uint32_t)m[j].x >> 9;
+      const bool ok = pos & !(w[j] & 1u) & (su >= sn) & (rel < 2 * M);
+      rare[j] = pos & !ok;
+      tl[j] = ok & (en1[j] == 0);
+      add[j] = ok & (en1[j] != 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (add[j]) atomicAdd(&cnt[__umul24(en1[j] - 1u, wpe) + (at[j] >> 1)], 1u << ((at[j] & 1u) * 16));
+    if (!(E.diag & 1u)) {
+      uint64_t tb[4];
+      uint32_t pre[4], total = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        tb[j] = __ballot(tl[j]);
+        pre[j] = total;
+        total += (uint32_t)__popcll(tb[j]);
+      }
+      if (total) {  // wave-uniform; every lane is active here
+        uint32_t t0 = kXtCap;
+        if ((threadIdx.x & 63u) == 0 && tail) t0 = atomicAdd(&tmisc[0], total);
+        t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (!tl[j]) continue;
+          const uint32_t r = t0 + pre[j] +
+                             __builtin_amdgcn_mbcnt_hi((uint32_t)(tb[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tb[j], 0u));
+          if (r < kXtCap) {
+            trec[r] = slot[j] << 12 | at[j];
+          } else {  // past the record buffer: the bucket's HBM atomic
+            const uint32_t cur = ((uint32_t)meta[slot[j]].x >> 8) & 1u;
+            atomicAdd(E.buckets + ((uint64_t)cur * E.cap + slot[j]) * M + at[j], 1u);
+          }
+        }
+      }
+    }
+    if (__builtin_expect(__ballot(rare[0] || rare[1] || rare[2] || rare[3]) != 0, 0)) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (rare[j]) count_ix(w[j], lo + base + 4 * threadIdx.x + j);
+    }
+  };
   constexpr uint32_t kStep = 4 * kXcBlock;
+  // (an 8-round ring of loads in flight instead of two measured slower: 41.9
+  // against 38.2 us per 10 M spans -- the loop is not waiting on its loads)
   Quad qa, qb;
   load(0, qa);
-  for (uint32_t base = 0; base < len; base += 2 * kStep) {
-    load(base + kStep, qb);
-    run(base, qa);
-    load(base + 2 * kStep, qa);
-    run(base + kStep, qb);
+  if (XC_ABL(2u)) {  // laboratory ablation: the loads only (their words folded into one sink)
+    uint32_t sink = 0;
+    for (uint32_t base = 0; base < len; base += 2 * kStep) {
+      load(base + kStep, qb);
+      sink ^= (uint32_t)(qa.r[0] ^ qa.r[1] ^ qa.r[2] ^ qa.r[3]);
+      load(base + 2 * kStep, qa);
+      sink ^= (uint32_t)(qb.r[0] ^ qb.r[1] ^ qb.r[2] ^ qb.r[3]);
+    }
+    if (sink == 0x9E3779B9u) atomicAdd(E.dropped, 1ULL);
+  } else {
+    for (uint32_t base = 0; base < len; base += 2 * kStep) {
+      load(base + kStep, qb);
+      if constexpr (IXR) count_quad(base, qa);
+      else run(base, qa);
+      load(base + 2 * kStep, qa);
+      if constexpr (IXR) count_quad(base + kStep, qb);
+      else run(base + kStep, qb);
+    }
   }
   __syncthreads();
-  uint32_t *slab = E.xcslab + (uint64_t)blockIdx.x * NE * wpe;
-  for (uint32_t i = threadIdx.x; i < NE * wpe; i += kXcBlock) slab[i] = cnt[i];
-  if (!tail) return;
-  // the tail records leave sorted by fold bin (slot / kXtBinSlots): a
+  if (E.dbg) xc_stamp(E, kXcStamp + 2);
+  uint32_t *slab = E.xcslab + (uint64_t)blockIdx.x * xc_slab_stride(NE, M);
+  if (!XC_ABL(4u))
+    for (uint32_t i = threadIdx.x; i < NE * wpe; i += kXcBlock) slab[i] = cnt[i];
+  if (E.dbg) xc_stamp(E, kXcStampSlab);
+  if (!tail) {
+    if (E.dbg) xc_stamp(E, kXcStamp + 3);
+    return;
+  }
+  // the tail records leave sorted by fold bin (slot / xt_bin_slots): a
   // histogram, an exclusive scan, then each record at its bin's cursor
-  const uint32_t nt = min(tmisc[0], kXtCap), nb = xt_bins(cap);
+  const uint32_t nt = min(tmisc[0], kXtCap), nb = xt_bins(cap, M), bs = xt_bin_slots(M);
   uint32_t *hist = tmisc + 1;  // [nb]
   for (uint32_t b = threadIdx.x; b < nb; b += kXcBlock) hist[b] = 0;
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nt; i += kXcBlock) atomicAdd(&hist[(trec[i] >> 12) / kXtBinSlots], 1u);
+  for (uint32_t i = threadIdx.x; i < nt; i += kXcBlock) atomicAdd(&hist[(trec[i] >> 12) / bs], 1u);
   __syncthreads();
   // nb <= 256 bins (cap <= 2048): thread t < nb scans bin t
   uint32_t total;
@@ -547,28 +669,34 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
   uint32_t *rec = E.xt_rec + (uint64_t)blockIdx.x * kXtCap;
   for (uint32_t i = threadIdx.x; i < nt; i += kXcBlock) {
     const uint32_t v = trec[i];
-    rec[atomicAdd(&hist[(v >> 12) / kXtBinSlots], 1u)] = v;
+    rec[atomicAdd(&hist[(v >> 12) / bs], 1u)] = v;
   }
+  if (E.dbg) xc_stamp(E, kXcStamp + 3);
 }
 
-// The counting kernel's tail records, one workgroup per fold bin (kXtBinSlots
+// The counting kernel's tail records, one workgroup per fold bin (xt_bin_slots
 // slots): every counting workgroup's run of the bin's records added in LDS
-// ([kXtBinSlots][M] u32), then each non-zero cell added to its bucket -- one
+// ([bin slots][M] u32), then each non-zero cell added to its bucket -- one
 // owner per slot (a slot is an entry in every workgroup or in none, so the
 // slab fold never touches these slots), no atomics on HBM.
 __device__ __forceinline__ void expo_fold_tail(const ExpoParams &E, uint32_t grid, uint32_t b, uint32_t *acc,
                                                uint32_t *cur) {
-  const uint32_t M = E.max_size, nb = xt_bins(E.cap);
-  for (uint32_t i = threadIdx.x; i < kXtBinSlots * M; i += 1024) acc[i] = 0;
-  if (threadIdx.x < kXtBinSlots) {
-    const uint64_t sl = (uint64_t)b * kXtBinSlots + threadIdx.x;
+  const uint32_t M = E.max_size, nb = xt_bins(E.cap, M), bs = xt_bin_slots(M);
+  for (uint32_t i = threadIdx.x; i < bs * M; i += 1024) acc[i] = 0;
+  if (threadIdx.x < bs) {
+    const uint64_t sl = (uint64_t)b * bs + threadIdx.x;
     cur[threadIdx.x] = sl < E.cap ? E.hdr[sl].cur : 0u;
   }
   __syncthreads();
   // wave w takes the counting workgroups w, w + 16, ...: their runs' bounds
-  // for all of them first, then the records (64 lanes a run)
+  // for all of them first, then the first 64 records of every run at once
+  // (64 lanes a run; a run is ~10 records at C2's mix), then what is left of
+  // longer runs.  (One run at a time kept one record round trip per run in a
+  // row: 16 of them per wave.)
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   constexpr uint32_t kPer = 16;  // counting workgroups per wave and batch (grid <= 256 in one batch)
+  constexpr uint32_t kNoRec = 0xFFFFFFFFu;  // (a record's slot is < 2^11)
+  auto add_rec = [&](uint32_t v) { atomicAdd(&acc[((v >> 12) % bs) * M + (v & 0xFFFu)], 1u); };
   for (uint32_t g0 = wave; g0 < grid; g0 += 16 * kPer) {
     uint32_t lo[kPer], n[kPer];
 #pragma unroll
@@ -578,63 +706,127 @@ __device__ __forceinline__ void expo_fold_tail(const ExpoParams &E, uint32_t gri
       lo[u] = g < grid ? off[0] : 0u;
       n[u] = g < grid ? off[1] - lo[u] : 0u;
     }
+    uint32_t v[kPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u)
+      v[u] = lane < n[u] ? E.xt_rec[(uint64_t)(g0 + u * 16) * kXtCap + lo[u] + lane] : kNoRec;
+#pragma unroll
+    for (uint32_t u = 0; u < kPer; ++u)
+      if (v[u] != kNoRec) add_rec(v[u]);
 #pragma unroll
     for (uint32_t u = 0; u < kPer; ++u) {
       const uint32_t *rec = E.xt_rec + (uint64_t)(g0 + u * 16) * kXtCap + lo[u];
-      for (uint32_t r = lane; r < n[u]; r += 64) {
-        const uint32_t v = rec[r];
-        atomicAdd(&acc[((v >> 12) % kXtBinSlots) * M + (v & 0xFFFu)], 1u);
-      }
+      for (uint32_t r = lane + 64; r < n[u]; r += 64) add_rec(rec[r]);
     }
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < kXtBinSlots * M; i += 1024) {
+  for (uint32_t i = threadIdx.x; i < bs * M; i += 1024) {
     const uint32_t c = acc[i];
     if (!c) continue;
-    const uint32_t k = i / M, sl = b * kXtBinSlots + k;
+    const uint32_t k = i / M, sl = b * bs + k;
     E.buckets[((uint64_t)cur[k] * E.cap + sl) * M + i % M] += c;
   }
 }
 
-// (entry, word) x 16 workgroup groups per block of 1024 threads
-__device__ __forceinline__ void expo_fold_slab(const ExpoParams &E, uint32_t grid, uint32_t blk,
-                                               uint32_t (*part)[64][2]) {
-  const uint32_t M = E.max_size, wpe = (M + 1) / 2, total = E.xc_ne * wpe;
+// (entry words x 16 workgroup groups) per block of 1024 threads: four words
+// a lane, 256 a block, so the slab blocks and the tail bins fit one resident
+// round (C2: 126 + 128 blocks; one word a lane took ~3 rounds).  part: the
+// 16 groups' sums, [16][64][8] u32 (the dynamic LDS).
+constexpr size_t kXfPartBytes = 16 * 64 * 8 * 4;
+__device__ __forceinline__ void expo_fold_slab(const ExpoParams &E, uint32_t grid, uint32_t blk, uint32_t *part) {
+  const uint32_t M = E.max_size, wpe = (M + 1) / 2, total = E.xc_ne * wpe, stride = xc_slab_stride(E.xc_ne, M);
   const uint32_t wl = threadIdx.x & 63u, gq = threadIdx.x >> 6;
-  const uint32_t w = blk * 64u + wl;
-  uint32_t lo = 0, hi = 0;
-  if (w < total) {
-#pragma unroll 8
-    for (uint32_t g = gq; g < grid; g += 16) {
-      const uint32_t v = E.xcslab[(uint64_t)g * total + w];
-      lo += v & 0xFFFFu;
-      hi += v >> 16;
+  const uint32_t w4 = blk * 256u + 4u * wl;  // the lane's first word
+  const bool live = w4 < total;
+  // the owner's chains (entry -> slot -> buffer) are read while the slab
+  // words are in flight; the bucket words after the barrier (no other thread
+  // of the fold touches them: a slot is an entry everywhere or nowhere)
+  const bool own = gq == 0 && live;
+  uint32_t slot[4] = {~0u, ~0u, ~0u, ~0u}, cur[4] = {}, q[4] = {};
+  if (own) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (w4 + c < total) {
+        q[c] = (w4 + c) % wpe;
+        slot[c] = E.slot_of_entry[(w4 + c) / wpe];
+      }
+  }
+  // grid <= 256 counting workgroups: at most 16 slab rows per thread, all in flight
+  // (buffer loads: one lane offset, the row step in the scalar offset; rows
+  // past the grid and lanes past the words read 0 through the bounds check)
+  constexpr uint32_t kG = 16;
+  const uint32_t nrec = min(grid, 256u) * stride * 4u;
+  const __amdgpu_buffer_rsrc_t rs = rsrc(E.xcslab, nrec);
+  const int vo = live ? (int)((gq * stride + w4) * 4u) : (int)0x80000000u;
+  uint4 v[kG];
+#pragma unroll
+  for (uint32_t k = 0; k < kG; ++k) {
+    const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, (int)(k * 16u * stride * 4u), 0);
+    v[k] = make_uint4(x[0], x[1], x[2], x[3]);
+  }
+  if (own) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (slot[c] != ~0u) cur[c] = E.hdr[slot[c]].cur;
+  }
+  uint32_t lo[4] = {}, hi[4] = {};
+#pragma unroll
+  for (uint32_t k = 0; k < kG; ++k) {
+    const uint32_t x[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      lo[c] += x[c] & 0xFFFFu;
+      hi[c] += x[c] >> 16;
     }
   }
-  part[gq][wl][0] = lo;
-  part[gq][wl][1] = hi;
-  __syncthreads();
-  if (gq != 0 || w >= total) return;
-  for (uint32_t k = 1; k < 16; ++k) {
-    lo += part[k][wl][0];
-    hi += part[k][wl][1];
+  // (grid > 256: the rest; the engine's grids do not get here)
+  for (uint32_t g = gq + 16 * kG; g < grid && live; g += 16) {
+    const uint4 y = *reinterpret_cast<const uint4 *>(E.xcslab + (uint64_t)g * stride + w4);
+    const uint32_t x[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      lo[c] += x[c] & 0xFFFFu;
+      hi[c] += x[c] >> 16;
+    }
   }
-  const uint32_t e = w / wpe, q = w % wpe, slot = E.slot_of_entry[e];
-  if (slot == ~0u || (lo | hi) == 0) return;
-  uint32_t *b = E.buckets + ((uint64_t)E.hdr[slot].cur * E.cap + slot) * M;
-  if (lo) b[2 * q] += lo;
-  if (hi && 2 * q + 1 < M) b[2 * q + 1] += hi;
+  uint4 *pp = reinterpret_cast<uint4 *>(part) + (gq * 64u + wl) * 2u;
+  pp[0] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+  pp[1] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+  __syncthreads();
+  if (!own) return;
+#pragma unroll 3
+  for (uint32_t k = 1; k < 16; ++k) {
+    const uint4 *o = reinterpret_cast<const uint4 *>(part) + (k * 64u + wl) * 2u;
+    const uint4 l = o[0], h = o[1];
+    lo[0] += l.x, lo[1] += l.y, lo[2] += l.z, lo[3] += l.w;
+    hi[0] += h.x, hi[1] += h.y, hi[2] += h.z, hi[3] += h.w;
+  }
+  uint32_t *bp[4], b0[4] = {}, b1[4] = {};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    bp[c] = E.buckets + ((uint64_t)cur[c] * E.cap + (slot[c] == ~0u ? 0u : slot[c])) * M + 2 * q[c];
+    if (slot[c] != ~0u && lo[c]) b0[c] = bp[c][0];
+    if (slot[c] != ~0u && hi[c] && 2 * q[c] + 1 < M) b1[c] = bp[c][1];
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (slot[c] == ~0u) continue;
+    if (lo[c]) bp[c][0] = b0[c] + lo[c];
+    if (hi[c] && 2 * q[c] + 1 < M) bp[c][1] = b1[c] + hi[c];
+  }
 }
 
 // One launch for both folds of a counting pass: blocks [0, slab_blocks) fold
 // the entries' slabs, the rest one tail bin each (the two touch disjoint
 // slots: a slot is an entry in every workgroup or in none)
 __global__ __launch_bounds__(1024) void expo_fold_kernel(ExpoParams E, uint32_t grid, uint32_t slab_blocks) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ uint32_t part[16][64][2];
-  __shared__ uint32_t cur[kXtBinSlots];
-  if (blockIdx.x < slab_blocks) expo_fold_slab(E, grid, blockIdx.x, part);
-  else expo_fold_tail(E, grid, blockIdx.x - slab_blocks, reinterpret_cast<uint32_t *>(smem), cur);
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // slab blocks: part; tail blocks: acc
+  __shared__ uint32_t cur[kXtBinSlotsMax];
+  if (blockIdx.x < slab_blocks) {
+    if (!XC_ABL(8u)) expo_fold_slab(E, grid, blockIdx.x, reinterpret_cast<uint32_t *>(smem));  // (laboratory ablations: 8 / 16 skip a kind)
+  } else if (!XC_ABL(16u)) {
+    expo_fold_tail(E, grid, blockIdx.x - slab_blocks, reinterpret_cast<uint32_t *>(smem), cur);
+  }
 }
 
 // Bucket counting with per-workgroup LDS privatisation: the slots' (scale,
@@ -765,16 +957,18 @@ __host__ __device__ ExpoHdr expo_hdr_empty() {
 
 // the counting kernel's LDS: slot table, entries' counts, selection scratch,
 // the tail record buffer and its bin histogram
-static size_t xc_fixed_lds(uint64_t cap) { return (size_t)cap * 12 + 256 + (size_t)kXtCap * 4 + 4 + xt_bins(cap) * 4; }
+static size_t xc_fixed_lds(uint64_t cap, uint32_t max_size) {
+  return (size_t)cap * 8 + 256 + (size_t)kXtCap * 4 + 4 + xt_bins(cap, max_size) * 4;
+}
 
 uint32_t expo_slab_entries(uint64_t cap, uint32_t max_size, size_t budget) {
-  const size_t fixed = xc_fixed_lds(cap), per = (size_t)((max_size + 1) / 2) * 4;
+  const size_t fixed = xc_fixed_lds(cap, max_size), per = (size_t)((max_size + 1) / 2) * 4;
   if (budget <= fixed + per) return 0;
   return (uint32_t)std::min<size_t>(cap, (budget - fixed) / per);
 }
 
 size_t expo_slab_lds_bytes(uint64_t cap, uint32_t max_size, uint32_t ne) {
-  return xc_fixed_lds(cap) + (size_t)ne * ((max_size + 1) / 2) * 4;
+  return xc_fixed_lds(cap, max_size) + (size_t)ne * ((max_size + 1) / 2) * 4;
 }
 
 hipError_t prepare_expo_slab(size_t lds_bytes) {
@@ -789,7 +983,7 @@ hipError_t prepare_expo_slab(size_t lds_bytes) {
       e != hipSuccess)
     return e;
   return hipFuncSetAttribute((const void *)&expo_fold_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)(kXtBinSlots * kExpoMaxSize * 4));
+                             (int)std::max<size_t>(kXfPartBytes, 8 * kExpoMaxSize * 4));  // (the largest bin x max_size)
 }
 
 size_t expo_count_lds_bytes(uint64_t cap, uint32_t max_size) {
@@ -841,10 +1035,10 @@ hipError_t launch_expo_ingest(const ExpoParams &E, hipStream_t s) {
 #endif
       hipLaunchKernelGGL(expo_count_slab_kernel<2>, dim3(grid), dim3(kXcBlock),
                          expo_slab_lds_bytes(E.cap, E.max_size, E.xc_ne), s, E, per_wg);
-    const uint32_t words = E.xc_ne * ((E.max_size + 1) / 2), slab_blocks = (words + 63) / 64;
-    const uint32_t tail_blocks = E.xt_rec ? xt_bins(E.cap) : 0u;
-    hipLaunchKernelGGL(expo_fold_kernel, dim3(slab_blocks + tail_blocks), dim3(1024),
-                       tail_blocks ? kXtBinSlots * E.max_size * 4 : 0, s, E, grid, slab_blocks);
+    const uint32_t words = E.xc_ne * ((E.max_size + 1) / 2), slab_blocks = (words + 255) / 256;
+    const uint32_t tail_blocks = E.xt_rec ? xt_bins(E.cap, E.max_size) : 0u;
+    const size_t lds = std::max<size_t>(kXfPartBytes, tail_blocks ? (size_t)xt_bin_slots(E.max_size) * E.max_size * 4 : 0);
+    hipLaunchKernelGGL(expo_fold_kernel, dim3(slab_blocks + tail_blocks), dim3(1024), lds, s, E, grid, slab_blocks);
     return hipGetLastError();
   }
   if (E.xslab) {  // small table: the ingest kernel left header partials and slots

@@ -28,6 +28,7 @@
 #   btpipe_<wl>      bench of <wl> with the binned launch pipeline on and off (2 rounds)
 #   ablate_<wl>      tools/ablate.py over the ABL_FLAGS / ABL_ENVS variant set for <wl>
 #   c2stamps         tools/stamps.py: per-workgroup phases of the C2 kernel (STAMP_VARS variants)
+#   xcstamps[_<d>]   tools/xc_stamps.py: c2expo counting-kernel phases (_d: laboratory, SPANAGG_XC_DIAG=d)
 #   stamps_<wl>      tools/bt_stamps.py: per-workgroup phase timeline (c4, c4zipf)
 #   sweep            C2 kernel time vs batch size (SIZES="1000000 5000000 ...")
 #   group_<wl>       rocprofv3 --kernel-trace --stats of bench.py --group 8 (an
@@ -221,6 +222,10 @@ for step in "$@"; do
         SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_XT=$xt \
           run "xt_${wl}_x${xt}_r$r" 200 python bench.py --workload "$wl" --sub "" --steps 40 --soak-s 0 --no-filter-off $BQ
       done; done ;;
+    xcstamps) run xcstamps 200 python tools/xc_stamps.py ;;  # c2expo counting-kernel phases (product build)
+    xcstamps_*) d=${step#xcstamps_}  # the same on the laboratory build with SPANAGG_XC_DIAG=d (ablations)
+      SPANAGG_LIB=$ROOTDIR/opentelemetry-demo_amd/spanagg/libspanagg_ab.so SPANAGG_XC_DIAG=$d \
+        run "xcstamps_d$d" 200 python tools/xc_stamps.py ;;
     c4chunks) run c4chunks 200 "$ROOTDIR/build/c4_probe" 10000000 chunks ;;
     probe_*) p=${step#probe_}; run "probe_$p" 200 "$ROOTDIR/build/${p}_probe" ;;
     groupbench_*) wl=${step#groupbench_}  # an 8-member group on this device, no profiler (flush_ms as a caller sees it)
