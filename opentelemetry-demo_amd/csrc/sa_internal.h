@@ -445,9 +445,11 @@ constexpr uint32_t kPoolMaxWgSpans = kPoolMaxStatic + kPoolMaxSteal * kPoolSpans
 constexpr uint32_t kPoolMinStatic = 32 * 256;  // two fixed chunks per wave before any claim
 constexpr uint32_t kDbgPerWg = 136;  // diagnostic stamps per workgroup: 8 + 16 waves x 8
 // the exponential counting kernel's stamps in the same rows (slots the ingest
-// kernel leaves free): start, prologue done, loop done, end at 4..7, and its
-// slab stores issued in the last slot
-constexpr uint32_t kXcStamp = 4, kXcStampSlab = kDbgPerWg - 1;
+// kernel leaves free): start, prologue done, loop done, end at 4..7; its slab
+// stores issued, its LDS zeroed and its entry selection done (thread 0) in
+// the last slots of the wave rows
+constexpr uint32_t kXcStamp = 4, kXcStampSlab = kDbgPerWg - 1, kXcStampZeroed = kDbgPerWg - 9,
+                   kXcStampSelected = kDbgPerWg - 17;
 constexpr uint32_t kHllQueue = 2048;  // deferred HLL raises per workgroup (8 B each)
 constexpr uint32_t kErrTab = 1024;    // LDS (window, slot) -> ERROR count table per workgroup (4 B each)
 // ingest_lds_kernel LDS beyond the table: HLL queue + its count + bin table

@@ -870,7 +870,10 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b, uint32_t
                     : nullptr;
   E.dropped = e->stats + sa::kStatDropped;
   E.xslab = e->expo_small ? e->xslab + (size_t)set * e->G * e->cap : nullptr;
-  E.xG = e->G;
+  // the workgroups whose header partials this launch wrote (ingest_launch's
+  // grid: each writes every slot of its slab row; rows past it are stale)
+  E.xG = b ? (uint32_t)std::min<uint64_t>((b->n + (uint64_t)e->block * e->spl - 1) / ((uint64_t)e->block * e->spl), e->G)
+           : e->G;
   E.xc_ne = e->expo_small ? e->xc_ne : 0u;
   E.lcount = E.xc_ne ? e->xc_lcount : nullptr;
   E.xmeta = E.xc_ne ? reinterpret_cast<int2 *>(e->xc_lcount + e->cap) : nullptr;

@@ -174,10 +174,10 @@ __global__ __launch_bounds__(256) void expo_rescale_kernel(ExpoParams E) {
 }
 
 // Small-table engines: the ingest kernel (EXPO mode) leaves per-workgroup
-// header partials in slabs [xG][cap].  One block per kXrSlots slots (8 by
-// default, 256 blocks at C2's 2,048 slots): the block's 1,024 / kXrSlots
-// groups sum a strided share of the workgroups' partials (coalesced runs,
-// zeroing what they consumed), the lanes of a wave holding the same slot
+// header partials in slabs [xG][cap] (every slot, each launch).  One block
+// per kXrSlots slots (8 by default, 256 blocks at C2's 2,048 slots): the
+// block's 1,024 / kXrSlots groups sum a strided share of the workgroups'
+// partials (coalesced runs), the lanes of a wave holding the same slot
 // combine by shuffles and the 16 waves through LDS, then one thread per slot
 // folds the sum into the series header and rescales it.  A thread issues all
 // its partial reads (kXrBatch at a time) and the owner its header read before
@@ -224,12 +224,8 @@ __global__ __launch_bounds__(1024) void expo_reduce_rescale_kernel(ExpoParams E)
         x[u] = g < E.xG ? E.xslab[(uint64_t)g * E.cap + s] : XHdr{0, 0, 0, 0, 0};
       }
 #pragma unroll
-      for (uint32_t u = 0; u < kXrBatch; ++u) {
-        if (x[u].cnt) {
-          xhdr_add(acc, x[u]);
-          E.xslab[(uint64_t)(g0 + u * kXrGroups) * E.cap + s] = XHdr{0, 0, 0, 0, 0};
-        }
-      }
+      for (uint32_t u = 0; u < kXrBatch; ++u)
+        if (x[u].cnt) xhdr_add(acc, x[u]);
     }
   }
   // lanes l, l ^ kXrSlots, ... of a wave hold the same slot
@@ -425,8 +421,10 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
   int4 xm = make_int4(0, 0, 0, 0);
   if (2 * threadIdx.x < cap) xm = *reinterpret_cast<const int4 *>(E.xmeta + 2 * threadIdx.x);  // (cap even)
   for (uint32_t i = threadIdx.x; i < NE * wpe; i += kXcBlock) cnt[i] = 0;
+  if (E.dbg) xc_stamp(E, kXcStampZeroed);
   int32_t en[2];
   expo_select_lds(E, scratch, lc, en);
+  if (E.dbg) xc_stamp(E, kXcStampSelected);
   if (2 * threadIdx.x < cap)
     *reinterpret_cast<int4 *>(meta + 2 * threadIdx.x) =
         make_int4(xm.x | (en[0] + 1) << 9, xm.y, xm.z | (en[1] + 1) << 9, xm.w);

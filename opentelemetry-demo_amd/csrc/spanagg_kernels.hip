@@ -1149,11 +1149,11 @@ __global__ __launch_bounds__(BLK) void ingest_v2_kernel(IngestParams P) {
   __syncthreads();
   const uint32_t nq = *hq_n < kQcap ? *hq_n : kQcap;
   if constexpr (EXPO) {
-    // this workgroup's header partials -> its slab (touched slots only; the
-    // reduce pass zeroes what it consumed)
+    // this workgroup's header partials -> its slab, every slot (untouched ones
+    // as zeros: the reduce pass reads the slab and leaves it as it is, no
+    // zeroing stores behind its reads)
     XHdr *xs = P.xslab + (uint64_t)blockIdx.x * cap;
-    for (uint32_t sl = threadIdx.x; sl < cap; sl += BLK)
-      if (const uint32_t c = xcnt[sl]) xs[sl] = XHdr{c, xzero[sl], lsum[sl], xminx[sl], xmax[sl]};
+    for (uint32_t sl = threadIdx.x; sl < cap; sl += BLK) xs[sl] = XHdr{xcnt[sl], xzero[sl], lsum[sl], xminx[sl], xmax[sl]};
     if (err_lds) {  // this workgroup's ERROR counts -> its private slab (no-return atomics)
       for (uint32_t t = threadIdx.x; t < kErrTab; t += BLK) {
         const uint32_t e = etab[t];

@@ -39,13 +39,21 @@ def phases(e):
     ing = rows[rows[:, 0] > 0][:, :4]
     cnt = rows[rows[:, 4] > 0]
     c, slab = cnt[:, 4:8], cnt[:, ROW - 1]
+    zeroed, selected = cnt[:, ROW - 9], cnt[:, ROW - 17]
+    wg = np.nonzero(rows[:, 4] > 0)[0]
+    loop = c[:, 2] - c[:, 1]
     t0 = ing[:, 0].min()
     return {
         "ingest": {"wgs": int(len(ing)), "prologue": q(ing[:, 1] - ing[:, 0]), "loop": q(ing[:, 2] - ing[:, 1]),
                    "epilogue": q(ing[:, 3] - ing[:, 2]), "end": q(ing[:, 3] - t0)},
         "count": {"wgs": int(len(c)), "start_after_ingest_end": q(c[:, 0] - ing[:, 3].max()),
                   "start_skew": q(c[:, 0] - c[:, 0].min()),
-                  "prologue": q(c[:, 1] - c[:, 0]), "loop": q(c[:, 2] - c[:, 1]),
+                  "prologue": q(c[:, 1] - c[:, 0]), "pro_to_zeroed": q(zeroed - c[:, 0]),
+                  "pro_zeroed_to_selected": q(selected - zeroed), "pro_selected_to_sync": q(c[:, 1] - selected),
+                  "loop": q(loop),
+                  # workgroup i runs on XCD i % 8: is the loop's spread per XCD?
+                  "loop_by_xcd": [q(loop[wg % 8 == x]) for x in range(8)],
+                  "loop_slowest_wgs": [int(x) for x in wg[np.argsort(loop)[-8:]]],
                   "slab_issue": q(slab - c[:, 2]), "tail": q(c[:, 3] - slab),
                   "lifetime": q(c[:, 3] - c[:, 0]), "end": q(c[:, 3] - c[:, 0].min())},
     }
