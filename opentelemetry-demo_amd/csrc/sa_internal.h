@@ -187,7 +187,10 @@ struct ExpoParams {
   // small-table bucket counting (expo_count_slab with its entry selection / expo_fold_slab):
   uint32_t *lcount;         // [cap] this launch's positive durations per slot (reduce -> selection)
   int2 *xmeta;              // [cap] {scale | buffer << 8, lo - (lo mod max_size)} per slot (reduce -> counting)
-  uint32_t *slot_of_entry;  // [xc_ne] the entry's slot, ~0u: unused
+  uint32_t *slot_of_entry;  // [xc_ne] the entry's slot, ~0u: unused (this launch's selection)
+  int32_t *xent;            // [cap] each slot's entry, -1: none (this launch's selection)
+  int32_t *xent_next;       // [cap] and the next launch's, by the counting kernel's workgroup 0
+  uint32_t *soe_next;       // [xc_ne] the next launch's slot_of_entry
   uint32_t *xcslab;         // [xG][xc_slab_stride] per-workgroup u16 bucket-count pairs ([xc_ne][(max_size + 1) / 2])
   uint32_t xc_ne;           // LDS entries of the counting kernel (0: the cached-probe kernel)
   // the counting kernel's tail (spans of series without an LDS entry): each

@@ -126,6 +126,12 @@ struct sa_engine {
   // slab bucket counting of small expo tables (spanagg_expo.hip expo_count_slab_kernel)
   uint32_t xc_ne = 0;
   uint32_t *xc_lcount = nullptr, *xc_slot_of_entry = nullptr, *xcslab = nullptr;
+  // the counting kernel's entry selections, double-buffered by launch parity
+  // (xc_sel): each launch counts with the selection the previous one made
+  // from its counts -- slot_of_entry [2][xc_ne], entry of each slot [2][cap]
+  int32_t *xc_ent = nullptr;
+  uint32_t xc_sel = 0;
+  bool xc_sel_made = false;
   uint32_t *xt_rec = nullptr, *xt_off = nullptr;  // the counting kernel's tail records (ExpoParams::xt_*)
   sa::ExpoHdr *expo_hdr = nullptr;
   int8_t *expo_xscale = nullptr;  // [cap] the slots' scales for the ingest kernel (index records)
@@ -555,11 +561,16 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
       }
       if (e->xc_ne &&
           ((rc = alloc((void **)&e->xc_lcount, e->cap * 12)) ||  // lcount [cap], then xmeta [cap]
-           (rc = alloc((void **)&e->xc_slot_of_entry, (size_t)e->xc_ne * 4)) ||
+           (rc = alloc((void **)&e->xc_slot_of_entry, (size_t)e->xc_ne * 8)) ||
+           (rc = alloc((void **)&e->xc_ent, (size_t)e->cap * 8)) ||
            (rc = alloc((void **)&e->xcslab, (size_t)e->G * sa::xc_slab_stride(e->xc_ne, cfg->exp_max_size) * 4)) ||
            (rc = alloc((void **)&e->xt_rec, (size_t)e->G * sa::kXtCap * 4)) ||
            (rc = alloc((void **)&e->xt_off, (size_t)e->G * (sa::xt_bins(e->cap, cfg->exp_max_size) + 1) * 4))))
         return bail(rc);
+      // no selection yet: no entries (the first launch counts every span through the tail)
+      if (e->xc_ne && (hipMemset(e->xc_slot_of_entry, 0xFF, (size_t)e->xc_ne * 8) != hipSuccess ||
+                       hipMemset(e->xc_ent, 0xFF, (size_t)e->cap * 8) != hipSuccess))
+        return bail(fail(e, SA_EDEVICE, "hipMemset failed"));
       // (window, slot) keys of the LDS ERROR table are 16-bit
       if ((uint64_t)cfg->n_windows * e->cap < 65535 &&
           (rc = alloc((void **)&e->errslab, (size_t)e->nsets * e->G * cfg->n_windows * e->cap * 4)))
@@ -646,7 +657,7 @@ void sa_destroy(sa_engine *e) {
                   (void *)e->expo_hdr, (void *)e->expo_xscale, (void *)e->expo_buckets, (void *)e->expo_slot,
                   (void *)e->expo_out_keys,
                   (void *)e->expo_out_rows, (void *)e->expo_out_buckets, (void *)e->hll_filt, (void *)e->xslab,
-                  (void *)e->xc_lcount, (void *)e->xc_slot_of_entry, (void *)e->xcslab, (void *)e->pool_ring,
+                  (void *)e->xc_lcount, (void *)e->xc_slot_of_entry, (void *)e->xc_ent, (void *)e->xcslab, (void *)e->pool_ring,
                   (void *)e->xt_rec, (void *)e->xt_off,
                   e->dstage[0], e->dstage[1]})
     if (p) (void)hipFree(p);
@@ -877,7 +888,16 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b, uint32_t
   E.xc_ne = e->expo_small ? e->xc_ne : 0u;
   E.lcount = E.xc_ne ? e->xc_lcount : nullptr;
   E.xmeta = E.xc_ne ? reinterpret_cast<int2 *>(e->xc_lcount + e->cap) : nullptr;
-  E.slot_of_entry = e->xc_slot_of_entry;
+  // (compact passes no batch and reads none of these)
+  const uint32_t cur = e->xc_sel & 1u, nxt = cur ^ 1u;
+  E.slot_of_entry = e->xc_slot_of_entry ? e->xc_slot_of_entry + (size_t)cur * e->xc_ne : nullptr;
+  E.soe_next = e->xc_slot_of_entry ? e->xc_slot_of_entry + (size_t)nxt * e->xc_ne : nullptr;
+  E.xent = e->xc_ent ? e->xc_ent + (size_t)cur * e->cap : nullptr;
+  E.xent_next = e->xc_ent ? e->xc_ent + (size_t)nxt * e->cap : nullptr;
+  if (!e->xc_sel_made) {  // the first launch: its own selection, in every counting workgroup
+    E.xent = nullptr;
+    E.slot_of_entry = E.soe_next;
+  }
   E.xcslab = e->xcslab;
   {
     // laboratory build: SPANAGG_XT=0 sends the counting kernel's tail to HBM
@@ -1087,6 +1107,10 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
     }
     // then the histogram kernels
     if (st == hipSuccess) st = sa::launch_expo_ingest(expo_params(e, b, set), hs);
+    if (st == hipSuccess && e->expo_small && e->xc_ne) {  // (the next launch counts with this one's selection)
+      e->xc_sel ^= 1u;
+      e->xc_sel_made = true;
+    }
     if (st == hipSuccess && e->ev_expo) {
       st = hipEventRecord(e->ev_expo, hs);
       e->expo_last = hs;

@@ -337,12 +337,11 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *wsum, 
 }
 
 // The entry selection (cap <= 2,048: slots 2t and 2t + 1 of thread t) into
-// en[2], the entries of thread t's two slots (-1: none).  scratch: 64 LDS
-// words.  Workgroup 0 also writes slot_of_entry (~0u past the selected ones)
-// for expo_fold_slab_kernel.  lc: lcount of slots 2t and 2t + 1 (0 past cap),
-// loaded by the caller ahead of its other prologue reads.
+// en[2], the entries of thread t's two slots (-1: none), and soe_next, the
+// slot of each entry (~0u past the selected ones; write_soe).  scratch: 64 LDS words.
+// lc: lcount of slots 2t and 2t + 1 (0 past cap).
 __device__ __forceinline__ void expo_select_lds(const ExpoParams &E, uint32_t *scratch, const uint32_t (&lc)[2],
-                                                int32_t (&en)[2]) {
+                                                int32_t (&en)[2], bool write_soe) {
   const uint32_t t = threadIdx.x, K = E.xc_ne, lane = t & 63u;
   uint32_t *hist = scratch, *wsum = scratch + 48;  // hist[33], wsum[16]
   uint32_t bl[2];
@@ -384,11 +383,10 @@ __device__ __forceinline__ void expo_select_lds(const ExpoParams &E, uint32_t *s
   const uint32_t ex = block_excl_scan(n0 + n1, wsum, nsel);
   en[0] = sel0 ? (int32_t)ex : -1;
   en[1] = sel1 ? (int32_t)(ex + n0) : -1;
-  if (blockIdx.x == 0) {
-    if (sel0) E.slot_of_entry[ex] = 2 * t;
-    if (sel1) E.slot_of_entry[ex + n0] = 2 * t + 1;
-    for (uint32_t k = nsel + t; k < K; k += 1024) E.slot_of_entry[k] = ~0u;
-  }
+  if (!write_soe) return;
+  if (sel0) E.soe_next[ex] = 2 * t;
+  if (sel1) E.soe_next[ex + n0] = 2 * t + 1;
+  for (uint32_t k = nsel + t; k < K; k += 1024) E.soe_next[k] = ~0u;
 }
 
 // IN: the spans as 0 = the key slot (E.slot_of) and both times (20 B per
@@ -409,25 +407,39 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
   const bool tail = E.xt_rec != nullptr;
   if (E.dbg) xc_stamp(E, kXcStamp);
   if (threadIdx.x == 0) tmisc[0] = 0;
-  uint32_t lc[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) lc[k] = 2 * threadIdx.x + k < cap ? E.lcount[2 * threadIdx.x + k] : 0u;
   // meta of slot s: {scale (8 bits) | buffer << 8 | (entry + 1) << 9, base},
   // base = lo - (lo mod M), the multiple of M at or below the kept range's
   // first index lo: a bucket index ix with ix - base in [0, 2M) sits at
   // position (ix - base) wrapped once (this launch's positive values lie in
-  // [lo, lo + M)).  The reduce pass left all but the entry (xmeta); slots 2t
-  // and 2t + 1 are thread t's, as in the selection.
+  // [lo, lo + M)).  The reduce pass left all but the entry (xmeta); the
+  // entries are the selection the previous launch's workgroup 0 made (xent:
+  // which series hold entries changes where counts are added, never the
+  // counts, and a mix's frequent series change slowly); slots 2t and 2t + 1
+  // are thread t's, as in the selection.
+  // (an engine's first launch has no selection yet, E.xent null: every
+  // workgroup makes this launch's, the same one, as workgroup 0 does)
   int4 xm = make_int4(0, 0, 0, 0);
-  if (2 * threadIdx.x < cap) xm = *reinterpret_cast<const int4 *>(E.xmeta + 2 * threadIdx.x);  // (cap even)
+  int2 ec = make_int2(-1, -1);
+  if (2 * threadIdx.x < cap) {  // (cap even)
+    xm = *reinterpret_cast<const int4 *>(E.xmeta + 2 * threadIdx.x);
+    if (E.xent) ec = *reinterpret_cast<const int2 *>(E.xent + 2 * threadIdx.x);
+  }
   for (uint32_t i = threadIdx.x; i < NE * wpe; i += kXcBlock) cnt[i] = 0;
   if (E.dbg) xc_stamp(E, kXcStampZeroed);
-  int32_t en[2];
-  expo_select_lds(E, scratch, lc, en);
+  if (blockIdx.x == 0 || !E.xent) {  // (workgroup-uniform) the next launch's entries, from this launch's counts
+    uint32_t lc[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) lc[k] = 2 * threadIdx.x + k < cap ? E.lcount[2 * threadIdx.x + k] : 0u;
+    int32_t en[2];
+    expo_select_lds(E, scratch, lc, en, blockIdx.x == 0);
+    if (blockIdx.x == 0 && 2 * threadIdx.x < cap)
+      *reinterpret_cast<int2 *>(E.xent_next + 2 * threadIdx.x) = make_int2(en[0], en[1]);
+    if (!E.xent) ec = make_int2(en[0], en[1]);
+  }
   if (E.dbg) xc_stamp(E, kXcStampSelected);
   if (2 * threadIdx.x < cap)
     *reinterpret_cast<int4 *>(meta + 2 * threadIdx.x) =
-        make_int4(xm.x | (en[0] + 1) << 9, xm.y, xm.z | (en[1] + 1) << 9, xm.w);
+        make_int4(xm.x | (ec.x + 1) << 9, xm.y, xm.z | (ec.y + 1) << 9, xm.w);
   __syncthreads();
   if (E.dbg) xc_stamp(E, kXcStamp + 1);
   const uint64_t lo = blockIdx.x * per_wg, hi = lo + per_wg < E.n ? lo + per_wg : E.n;
