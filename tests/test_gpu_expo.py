@@ -139,6 +139,25 @@ def test_expo_small_table_full_size_device_launches():
         assert int(res.count.sum()) == 2 * len(wl.batch) - 2 * int((wl.batch.key_hash == 0).sum())
 
 
+def test_expo_entry_selection_from_a_different_mix():
+    """Each counting launch uses the LDS entries the previous launch selected
+    from its own counts (the first launch selects its own).  A launch whose
+    series are all new to that selection (keys disjoint from the previous
+    launch's) counts everything through the tail and its overflow; then the
+    first mix again.  Every bucket as the oracle's."""
+    a = generate_c2(300_000, seed=21, names_per_service=10).batch
+    cols = a.columns()
+    b = SpanBatch(*[c ^ np.uint64(0x5DEECE66D12345) if i == 0 else c for i, c in enumerate(cols)])
+    b.key_hash[a.key_hash == 0] = 0  # (keep the zero keys zero)
+    wl = generate_c2(10, seed=21, names_per_service=10)
+    with _engine(wl, exp_max_size=160, key_capacity=1300) as e:
+        assert e.stats()["small_table"] == 1
+        for x in (a, b, a):
+            e.ingest(x)
+        both = SpanBatch(*[np.concatenate([p, q, r]) for p, q, r in zip(a.columns(), b.columns(), a.columns())])
+        _check(e.flush_exp(), both, 160)
+
+
 def test_expo_state_across_launches_and_delta_flushes():
     """Several ingests before one flush (kept buckets merged down when a later
     batch widens the range), then a second interval from scratch."""
