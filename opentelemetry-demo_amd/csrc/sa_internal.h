@@ -452,7 +452,7 @@ constexpr uint32_t kDbgPerWg = 136;  // diagnostic stamps per workgroup: 8 + 16 
 // stores issued, its LDS zeroed and its entry selection done (thread 0) in
 // the last slots of the wave rows
 constexpr uint32_t kXcStamp = 4, kXcStampSlab = kDbgPerWg - 1, kXcStampZeroed = kDbgPerWg - 9,
-                   kXcStampSelected = kDbgPerWg - 17;
+                   kXcStampSelected = kDbgPerWg - 17, kXcStampTail = kDbgPerWg - 25;
 constexpr uint32_t kHllQueue = 2048;  // deferred HLL raises per workgroup (8 B each)
 constexpr uint32_t kErrTab = 1024;    // LDS (window, slot) -> ERROR count table per workgroup (4 B each)
 // ingest_lds_kernel LDS beyond the table: HLL queue + its count + bin table

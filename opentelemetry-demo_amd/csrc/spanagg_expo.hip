@@ -284,6 +284,7 @@ __device__ __forceinline__ void xc_stamp(const ExpoParams &E, uint32_t slot) {
 #define XC_ABL(bit) false
 #endif
 constexpr uint64_t kXcMaxSpans = 65535;  // u16 LDS counts: spans per counting workgroup
+constexpr uint32_t kXcDefer = 256;       // long-duration records a counting workgroup defers to after its loop
 
 // Bucket counting of small tables, two kernels:
 //   expo_count_slab_kernel every workgroup first selects the xc_ne series with
@@ -404,9 +405,11 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
   // fold bins' histogram / cursors at the end
   uint32_t *trec = scratch + 64;                                  // [kXtCap]
   uint32_t *tmisc = trec + kXtCap;                                // [0] records, [1..] bin hist / cursors
+  // (IXR) long-duration records deferred to after the loop: their spans, slots and count
+  uint32_t *dl_i = tmisc + 1 + xt_bins(cap, M), *dl_s = dl_i + kXcDefer, *dl_n = dl_s + kXcDefer;
   const bool tail = E.xt_rec != nullptr;
   if (E.dbg) xc_stamp(E, kXcStamp);
-  if (threadIdx.x == 0) tmisc[0] = 0;
+  if (threadIdx.x == 0) tmisc[0] = tmisc[1] = *dl_n = 0;
   // meta of slot s: {scale (8 bits) | buffer << 8 | (entry + 1) << 9, base},
   // base = lo - (lo mod M), the multiple of M at or below the kept range's
   // first index lo: a bucket index ix with ix - base in [0, 2M) sits at
@@ -618,9 +621,24 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
       }
     }
     if (__builtin_expect(__ballot(rare[0] || rare[1] || rare[2] || rare[3]) != 0, 0)) {
+      if (E.dbg && (threadIdx.x & 63u) == 0) atomicAdd(&tmisc[1], 1u);  // (SA_OPT_STAMPS: waves on the rare path)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (rare[j]) count_ix(w[j], lo + base + 4 * threadIdx.x + j);
+      for (int j = 0; j < 4; ++j) {
+        if (!rare[j]) continue;
+        const uint32_t i = (uint32_t)(lo + base + 4 * threadIdx.x + j);
+        // a long duration (the fast index declined it in the ingest kernel: at
+        // high scales ~1e-3 of spans, near a bucket boundary) waits for the
+        // end of the loop, where every deferred record's side-array read goes
+        // out at once -- here each one held its wave for a memory round trip
+        uint32_t k = kXcDefer;
+        if (w[j] & 1u) k = atomicAdd(dl_n, 1u);
+        if (k < kXcDefer) {
+          dl_i[k] = i;
+          dl_s[k] = slot[j];
+        } else {
+          count_ix(w[j], i);
+        }
+      }
     }
   };
   constexpr uint32_t kStep = 4 * kXcBlock;
@@ -648,7 +666,17 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
     }
   }
   __syncthreads();
+  if (IXR) {  // the deferred long durations
+    const uint32_t nd = min(*dl_n, kXcDefer);
+    for (uint32_t k = threadIdx.x; k < nd; k += kXcBlock) count(dl_s[k], E.span_long[dl_i[k]]);
+    __syncthreads();
+  }
   if (E.dbg) xc_stamp(E, kXcStamp + 2);
+  if (E.dbg && threadIdx.x == 0) {  // (counts: tail records claimed, rare-path wave steps)
+    E.dbg[blockIdx.x * kDbgPerWg + kXcStampTail] = tmisc[0];
+    E.dbg[blockIdx.x * kDbgPerWg + kXcStampTail - 8] = tmisc[1];
+    E.dbg[blockIdx.x * kDbgPerWg + kXcStampTail - 16] = *dl_n;
+  }
   uint32_t *slab = E.xcslab + (uint64_t)blockIdx.x * xc_slab_stride(NE, M);
   if (!XC_ABL(4u))
     for (uint32_t i = threadIdx.x; i < NE * wpe; i += kXcBlock) slab[i] = cnt[i];
@@ -968,7 +996,7 @@ __host__ __device__ ExpoHdr expo_hdr_empty() {
 // the counting kernel's LDS: slot table, entries' counts, selection scratch,
 // the tail record buffer and its bin histogram
 static size_t xc_fixed_lds(uint64_t cap, uint32_t max_size) {
-  return (size_t)cap * 8 + 256 + (size_t)kXtCap * 4 + 4 + xt_bins(cap, max_size) * 4;
+  return (size_t)cap * 8 + 256 + (size_t)kXtCap * 4 + 4 + xt_bins(cap, max_size) * 4 + (size_t)kXcDefer * 8 + 4;
 }
 
 uint32_t expo_slab_entries(uint64_t cap, uint32_t max_size, size_t budget) {

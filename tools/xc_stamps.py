@@ -54,6 +54,17 @@ def phases(e):
                   # workgroup i runs on XCD i % 8: is the loop's spread per XCD?
                   "loop_by_xcd": [q(loop[wg % 8 == x]) for x in range(8)],
                   "loop_slowest_wgs": [int(x) for x in wg[np.argsort(loop)[-8:]]],
+                  # the workgroups' tail records (spans of series without an LDS entry; past 4,096: HBM atomics)
+                  "tail_records": {"min": int(cnt[:, ROW - 25].min()), "med": float(np.median(cnt[:, ROW - 25])),
+                                   "max": int(cnt[:, ROW - 25].max()),
+                                   "corr_with_loop": float(np.corrcoef(cnt[:, ROW - 25], loop)[0, 1])},
+                  # wave steps that took the rare path (long durations, a risen scale, out of range;
+                  # the long ones are deferred to after the loop)
+                  "rare_steps": {"min": int(cnt[:, ROW - 33].min()), "med": float(np.median(cnt[:, ROW - 33])),
+                                 "max": int(cnt[:, ROW - 33].max()),
+                                 "corr_with_loop": float(np.corrcoef(cnt[:, ROW - 33], loop)[0, 1]) if cnt[:, ROW - 33].std() > 0 else 0.0,
+                                 "slowest_wgs": [int(x) for x in cnt[np.argsort(loop)[-8:], ROW - 33]],
+                                 "deferred_long_med": float(np.median(cnt[:, ROW - 41]))},
                   "slab_issue": q(slab - c[:, 2]), "tail": q(c[:, 3] - slab),
                   "lifetime": q(c[:, 3] - c[:, 0]), "end": q(c[:, 3] - c[:, 0].min())},
     }
