@@ -758,11 +758,24 @@ __device__ __forceinline__ void expo_fold_tail(const ExpoParams &E, uint32_t gri
     }
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < bs * M; i += 1024) {
-    const uint32_t c = acc[i];
-    if (!c) continue;
-    const uint32_t k = i / M, sl = b * bs + k;
-    E.buckets[((uint64_t)cur[k] * E.cap + sl) * M + i % M] += c;
+  // the non-zero cells: every bucket word read before the first is written
+  // (a cell per thread per round, up to four rounds at C2's 16 x 160 cells;
+  // one round trip instead of one per round -- each cell has one owner)
+  constexpr uint32_t kR = 4;
+  for (uint32_t i0 = 0; i0 < bs * M; i0 += kR * 1024) {
+    uint32_t c[kR], old[kR];
+    uint32_t *p[kR];
+#pragma unroll
+    for (uint32_t r = 0; r < kR; ++r) {
+      const uint32_t i = i0 + r * 1024 + threadIdx.x;
+      c[r] = i < bs * M ? acc[i] : 0u;
+      const uint32_t k = i / M, sl = b * bs + k;
+      p[r] = c[r] ? E.buckets + ((uint64_t)cur[k] * E.cap + sl) * M + i % M : nullptr;
+      old[r] = c[r] ? *p[r] : 0u;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kR; ++r)
+      if (c[r]) *p[r] = old[r] + c[r];
   }
 }
 
