@@ -195,9 +195,10 @@ struct ExpoParams {
   uint32_t xc_ne;           // LDS entries of the counting kernel (0: the cached-probe kernel)
   // the counting kernel's tail (spans of series without an LDS entry): each
   // workgroup's (slot << 12 | bucket) records, sorted by fold bin of
-  // xt_bin_slots slots, [xG][kXtCap], and the bins' offsets [xG][nbins + 1];
+  // xt_bin_slots slots, each bin's run at a fixed place [xG][nbins][kXtRun],
+  // and the runs' lengths [xG][nbins + 1];
   // expo_fold_kernel sums them per bin (nullptr: HBM atomics)
-  uint32_t *xt_rec, *xt_off;  // (records past kXtCap take an HBM atomic)
+  uint32_t *xt_rec, *xt_off;  // (records past kXtCap, or past a full run, take an HBM atomic)
   // SA_OPT_STAMPS: the counting kernel's per-workgroup s_memrealtime stamps,
   // in the ingest kernel's stamp rows (kDbgPerWg per workgroup; slots
   // kXcStamp.. are the counting kernel's); nullptr: none
@@ -233,6 +234,7 @@ __host__ __device__ inline uint32_t ixrec_of(uint32_t slot, int32_t scale, int32
 // log2(div) in the fast bucket index's 8.24 fixed point (expo_index_fast)
 __host__ inline int32_t expo_l2d_q24(double div) { return (int32_t)std::llround(std::log2(div) * 16777216.0); }
 constexpr uint32_t kXtCap = 4096;       // tail records per counting workgroup (16 KiB of LDS)
+constexpr uint32_t kXtRun = 64;         // a counting workgroup's records of one fold bin (C2: ~23 on average)
 // slots per tail fold bin: 16 (a fold workgroup counts [16][max_size] u32 in
 // LDS), 8 past max_size 2,048; one fold round at C2's 2,048 slots (128 bins)
 constexpr uint32_t kXtBinSlotsMax = 16;

@@ -564,7 +564,7 @@ int sa_create(const sa_config *cfg, sa_engine **out) {
            (rc = alloc((void **)&e->xc_slot_of_entry, (size_t)e->xc_ne * 8)) ||
            (rc = alloc((void **)&e->xc_ent, (size_t)e->cap * 8)) ||
            (rc = alloc((void **)&e->xcslab, (size_t)e->G * sa::xc_slab_stride(e->xc_ne, cfg->exp_max_size) * 4)) ||
-           (rc = alloc((void **)&e->xt_rec, (size_t)e->G * sa::kXtCap * 4)) ||
+           (rc = alloc((void **)&e->xt_rec, (size_t)e->G * sa::xt_bins(e->cap, cfg->exp_max_size) * sa::kXtRun * 4)) ||
            (rc = alloc((void **)&e->xt_off, (size_t)e->G * (sa::xt_bins(e->cap, cfg->exp_max_size) + 1) * 4))))
         return bail(rc);
       // no selection yet: no entries (the first launch counts every span through the tail)

@@ -685,30 +685,28 @@ __global__ __launch_bounds__(1024) void expo_count_slab_kernel(ExpoParams E, uin
     if (E.dbg) xc_stamp(E, kXcStamp + 3);
     return;
   }
-  // the tail records leave sorted by fold bin (slot / xt_bin_slots): a
-  // histogram, an exclusive scan, then each record at its bin's cursor
+  // the tail records leave by fold bin (slot / xt_bin_slots), each bin's run
+  // at a fixed place (kXtRun records; a record past a full run takes its
+  // bucket's HBM atomic), with the runs' lengths: the fold reads a run and
+  // its length in one round trip
   const uint32_t nt = min(tmisc[0], kXtCap), nb = xt_bins(cap, M), bs = xt_bin_slots(M);
-  uint32_t *hist = tmisc + 1;  // [nb]
+  uint32_t *hist = tmisc + 1;  // [nb] the runs' cursors
   for (uint32_t b = threadIdx.x; b < nb; b += kXcBlock) hist[b] = 0;
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nt; i += kXcBlock) atomicAdd(&hist[(trec[i] >> 12) / bs], 1u);
-  __syncthreads();
-  // nb <= 256 bins (cap <= 2048): thread t < nb scans bin t
-  uint32_t total;
-  const uint32_t h = threadIdx.x < nb ? hist[threadIdx.x] : 0u;
-  const uint32_t ex = block_excl_scan(h, scratch + 48, total);
-  uint32_t *off = E.xt_off + (uint64_t)blockIdx.x * (nb + 1);
-  if (threadIdx.x < nb) {
-    off[threadIdx.x] = ex;
-    hist[threadIdx.x] = ex;  // the bin's cursor
-  }
-  if (threadIdx.x == 0) off[nb] = nt;
-  __syncthreads();
-  uint32_t *rec = E.xt_rec + (uint64_t)blockIdx.x * kXtCap;
+  uint32_t *rec = E.xt_rec + (uint64_t)blockIdx.x * nb * kXtRun;
   for (uint32_t i = threadIdx.x; i < nt; i += kXcBlock) {
-    const uint32_t v = trec[i];
-    rec[atomicAdd(&hist[(v >> 12) / bs], 1u)] = v;
+    const uint32_t v = trec[i], sl = v >> 12, b = sl / bs;
+    const uint32_t r = atomicAdd(&hist[b], 1u);
+    if (r < kXtRun) {
+      rec[b * kXtRun + r] = v;
+    } else {
+      const uint32_t cur = ((uint32_t)meta[sl].x >> 8) & 1u;
+      atomicAdd(E.buckets + ((uint64_t)cur * E.cap + sl) * M + (v & 0xFFFu), 1u);
+    }
   }
+  __syncthreads();
+  uint32_t *off = E.xt_off + (uint64_t)blockIdx.x * (nb + 1);
+  for (uint32_t b = threadIdx.x; b < nb; b += kXcBlock) off[b] = min(hist[b], kXtRun);
   if (E.dbg) xc_stamp(E, kXcStamp + 3);
 }
 
@@ -726,36 +724,26 @@ __device__ __forceinline__ void expo_fold_tail(const ExpoParams &E, uint32_t gri
     cur[threadIdx.x] = sl < E.cap ? E.hdr[sl].cur : 0u;
   }
   __syncthreads();
-  // wave w takes the counting workgroups w, w + 16, ...: their runs' bounds
-  // for all of them first, then the first 64 records of every run at once
-  // (64 lanes a run; a run is ~10 records at C2's mix), then what is left of
-  // longer runs.  (One run at a time kept one record round trip per run in a
-  // row: 16 of them per wave.)
+  // wave w takes the counting workgroups w, w + 16, ...: every run's length
+  // and records (64 lanes a run, at most kXtRun records) in flight together,
+  // one round trip.  (Runs at offsets from a sorted list took two, and one
+  // run at a time one per run in a row.)
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   constexpr uint32_t kPer = 16;  // counting workgroups per wave and batch (grid <= 256 in one batch)
   constexpr uint32_t kNoRec = 0xFFFFFFFFu;  // (a record's slot is < 2^11)
+  static_assert(kXtRun == 64, "a run is one record per lane");
   auto add_rec = [&](uint32_t v) { atomicAdd(&acc[((v >> 12) % bs) * M + (v & 0xFFFu)], 1u); };
   for (uint32_t g0 = wave; g0 < grid; g0 += 16 * kPer) {
-    uint32_t lo[kPer], n[kPer];
+    uint32_t n[kPer], v[kPer];
 #pragma unroll
     for (uint32_t u = 0; u < kPer; ++u) {
       const uint32_t g = g0 + u * 16;
-      const uint32_t *off = E.xt_off + (uint64_t)g * (nb + 1) + b;
-      lo[u] = g < grid ? off[0] : 0u;
-      n[u] = g < grid ? off[1] - lo[u] : 0u;
+      n[u] = g < grid ? E.xt_off[(uint64_t)g * (nb + 1) + b] : 0u;
+      v[u] = g < grid ? E.xt_rec[((uint64_t)g * nb + b) * kXtRun + lane] : kNoRec;  // (past the run: stale, masked below)
     }
-    uint32_t v[kPer];
 #pragma unroll
     for (uint32_t u = 0; u < kPer; ++u)
-      v[u] = lane < n[u] ? E.xt_rec[(uint64_t)(g0 + u * 16) * kXtCap + lo[u] + lane] : kNoRec;
-#pragma unroll
-    for (uint32_t u = 0; u < kPer; ++u)
-      if (v[u] != kNoRec) add_rec(v[u]);
-#pragma unroll
-    for (uint32_t u = 0; u < kPer; ++u) {
-      const uint32_t *rec = E.xt_rec + (uint64_t)(g0 + u * 16) * kXtCap + lo[u];
-      for (uint32_t r = lane + 64; r < n[u]; r += 64) add_rec(rec[r]);
-    }
+      if (lane < n[u]) add_rec(v[u]);
   }
   __syncthreads();
   // the non-zero cells: every bucket word read before the first is written
