@@ -122,6 +122,9 @@ function normalizeConfig(cfg = {}, addon) {
   return {
     unit, bounds, dims, expMaxSize, callsDims, histDims,
     splitKeys: callsDims.length !== dims.length || histDims.length !== dims.length,
+    // include_instrumentation_scope: scope names whose spans are keyed with
+    // their scope's name and version ([UPSTREAM] config.go, confidence L)
+    scopes: new Set(cfg.include_instrumentation_scope || []),
     // histogram.disable: no duration metric (the calls metric stays)
     histogramDisable: !!hist.disable,
     // metrics_expiration: cumulative resources not seen for this long are
@@ -202,10 +205,11 @@ class SpanMetricsConnector {
     this.nativeBuffered = 0;
     this.nativeRequests = 0;
     this.jsRequests = 0;
-    // (calls_dimensions / histogram.dimensions key every span twice: the
-    // JavaScript columnizer does that)
+    // (calls_dimensions / histogram.dimensions key every span twice, and
+    // include_instrumentation_scope keys by the scope: the JavaScript
+    // columnizer does both)
     if (opts.native !== false && typeof this.addon.createColumnizer === 'function' &&
-        this.rules.every((r) => r.native) && !c.splitKeys) {
+        this.rules.every((r) => r.native) && !c.splitKeys && c.scopes.size === 0) {
       this.col = this.addon.createColumnizer(this.handle, { dims: c.dims,
         exclude: [...c.exclude], rules: this.rules.map((r) => r.native),
         keyAttributes: c.resourceKeyAttributes, threads: c.columnizerThreads,
@@ -351,12 +355,12 @@ class SpanMetricsConnector {
     return sid;
   }
 
-  _seriesId(res, service, span, resAttrs, spanAttrs) {
+  _seriesId(res, service, span, resAttrs, spanAttrs, scope = null) {
     const c = this.cfg;
     const status = span.status ? span.status.code : 0;
+    if (c.splitKeys) return this._splitId(res, service, span, resAttrs, spanAttrs, status, HIST_KEY_PREFIX, scope);
     const keyStr = keys.buildKeyString(service, span.name, span.kind, status, c.dims, spanAttrs,
-      resAttrs, c.exclude);
-    if (c.splitKeys) return this._splitId(res, service, span, resAttrs, spanAttrs, status, HIST_KEY_PREFIX);
+      resAttrs, c.exclude, scope);
     const known = res.byKey.get(keyStr);
     if (known !== undefined) return known;
     // aggregation_cardinality_limit: past `limit` series in a resource, new keys
@@ -366,7 +370,7 @@ class SpanMetricsConnector {
         () => [{ key: 'otel.metric.overflow', value: { type: 'bool', value: true } }]);
     }
     return this._intern(res, keyStr, 'span', status, () => keys.buildAttributes(service, span.name,
-      span.kind, status, c.dims, spanAttrs, resAttrs, c.exclude));
+      span.kind, status, c.dims, spanAttrs, resAttrs, c.exclude, scope));
   }
 
   /**
@@ -375,12 +379,12 @@ class SpanMetricsConnector {
    * calls-metric series (CALLS_KEY_PREFIX, dimensions + calls_dimensions); the
    * cardinality limit applies to each metric's series on their own.
    */
-  _splitId(res, service, span, resAttrs, spanAttrs, status, prefix) {
+  _splitId(res, service, span, resAttrs, spanAttrs, status, prefix, scope = null) {
     const c = this.cfg;
     const calls = prefix === CALLS_KEY_PREFIX;
     const d = calls ? c.callsDims : c.histDims;
     const keyStr = prefix + keys.buildKeyString(service, span.name, span.kind, status, d, spanAttrs, resAttrs,
-      c.exclude);
+      c.exclude, scope);
     const known = res.byKey.get(keyStr);
     if (known !== undefined) return known;
     const kind = calls ? 'calls' : 'hist';
@@ -389,20 +393,20 @@ class SpanMetricsConnector {
         () => [{ key: 'otel.metric.overflow', value: { type: 'bool', value: true } }]);
     }
     return this._intern(res, keyStr, kind, status, () => keys.buildAttributes(service, span.name,
-      span.kind, status, d, spanAttrs, resAttrs, c.exclude));
+      span.kind, status, d, spanAttrs, resAttrs, c.exclude, scope));
   }
 
   /** events.enabled: one record per span event, keyed by the span key + event dimensions. */
-  _eventId(res, service, span, resAttrs, spanAttrs, event) {
+  _eventId(res, service, span, resAttrs, spanAttrs, event, scope = null) {
     const c = this.cfg;
     const status = span.status ? span.status.code : 0;
     const evAttrs = keys.attrMap(event.attributes);
     const base = keys.buildKeyString(service, span.name, span.kind, status, c.dims, spanAttrs,
-      resAttrs, c.exclude);
+      resAttrs, c.exclude, scope);
     const evKey = keys.buildKeyString('', '', 0, 0, c.eventDims, evAttrs, new Map(),
       new Set([keys.SERVICE_NAME_KEY, 'span.name', 'span.kind', 'status.code']));
     return this._intern(res, EVENT_KEY_PREFIX + base + evKey, 'event', status, () =>
-      keys.buildAttributes(service, span.name, span.kind, status, c.dims, spanAttrs, resAttrs, c.exclude)
+      keys.buildAttributes(service, span.name, span.kind, status, c.dims, spanAttrs, resAttrs, c.exclude, scope)
         .concat(keys.buildAttributes('', '', 0, 0, c.eventDims, evAttrs, new Map(),
           new Set([keys.SERVICE_NAME_KEY, 'span.name', 'span.kind', 'status.code']))));
   }
@@ -525,13 +529,14 @@ class SpanMetricsConnector {
       const res = this._resource(resAttrs);
       const svcId = this._serviceId(service);
       for (const ss of rs.scopeSpans || []) {
+        const scope = keys.includedScope(ss.scope, this.cfg.scopes);
         for (const span of ss.spans || []) {
           const spanAttrs = this.cfg.dims.length ? keys.attrMap(span.attributes) : undefined;
-          const sid = this._seriesId(res, service, span, resAttrs, spanAttrs);
+          const sid = this._seriesId(res, service, span, resAttrs, spanAttrs, scope);
           if (this.cfg.exemplars) this._exemplar(sid, span);
           if (this.cfg.splitKeys) {  // the calls series gets the span as a second record
             const code = span.status ? span.status.code : 0;
-            this._pushCalls(this._splitId(res, service, span, resAttrs, spanAttrs, code, CALLS_KEY_PREFIX), span);
+            this._pushCalls(this._splitId(res, service, span, resAttrs, spanAttrs, code, CALLS_KEY_PREFIX, scope), span);
           }
           const i = cols.n;
           cols.keyHash[i] = sid;
@@ -553,7 +558,7 @@ class SpanMetricsConnector {
           if (cols.n === cols.cap) this._drain();
           // events.enabled: the span's event records follow it (the native order)
           if (this.cfg.events && span.events && span.events.length) {
-            for (const ev of span.events) this._pushEvent(this._eventId(res, service, span, resAttrs, spanAttrs, ev));
+            for (const ev of span.events) this._pushEvent(this._eventId(res, service, span, resAttrs, spanAttrs, ev, scope));
           }
         }
       }

@@ -383,6 +383,27 @@ for (const name of ['calls_and_histogram_dimensions', 'histogram_disable']) {
   });
 }
 
+test('connector: include_instrumentation_scope keys listed scopes by name and version (KAT)', () => {
+  const c = katCase('include_instrumentation_scope');
+  const want = c.expected.calls.map(([at, n]) => [JSON.stringify(at), n]).sort();
+  // decoded requests, and the same spans as OTLP bytes (the scope goes
+  // through the decoder; the option keeps the JavaScript columnizer)
+  for (const bytes of [false, true]) {
+    const { conn } = mkConnector(c.config);
+    for (const [svc, nm, kind, st, attrs, sn, sv] of c.spans) {
+      const req = { resourceSpans: [{ resource: { attributes: [{ key: 'service.name', value: str(svc) }] },
+        scopeSpans: [{ scope: { name: sn, version: sv }, spans: [span(nm, { kind, status: { code: st, message: '' },
+          attributes: Object.entries(attrs).map(([key, v]) => ({ key, value: str(v) })) })] }] }] };
+      conn.consumeTraces(bytes ? otlp.encodeTraces(req) : req);
+    }
+    const out = conn.exportMetrics();
+    const calls = dpsOf(out, 'traces.span.metrics.calls').map((dp) => [dpKey(dp), Number(dp.asInt)]).sort();
+    assert.deepStrictEqual(calls, want);
+    const hist = dpsOf(out, 'traces.span.metrics.duration').map((dp) => [dpKey(dp), Number(dp.count)]).sort();
+    assert.deepStrictEqual(hist, want);
+  }
+});
+
 test('connector: consumes OTLP bytes; columns carry trace ids and meta bits', () => {
   const { conn, addon } = mkConnector({ batch_size: 2 });
   const tid = Uint8Array.from({ length: 16 }, (_, i) => 0xA0 + i);

@@ -297,6 +297,48 @@ def case_histogram_disable():
                 spans=[[a, b, c, d, e] for a, b, c, d, e in spans], expected=dict(calls=calls, histogram=[]))
 
 
+def restate_scope(spans, dims, scopes):
+    """include_instrumentation_scope ([UPSTREAM] connector.go buildKey /
+    buildAttributes, confidence L): a span whose scope name is listed is keyed
+    with the scope's name and version after the dimensions, and its data point
+    carries span.instrumentation.scope.name / .version.  spans: (service, name,
+    kind, status, {attr: str}, scope name, scope version).  Returns the calls
+    data points as [[attrs...], count]."""
+    table = {}
+    for svc, name, kind, st, attrs, sn, sv in spans:
+        stc = ["STATUS_CODE_UNSET", "STATUS_CODE_OK", "STATUS_CODE_ERROR"][st]
+        key = [svc, name, KIND[kind], stc]
+        at = [["service.name", svc], ["span.name", name], ["span.kind", KIND[kind]], ["status.code", stc]]
+        for dn, dd in dims:
+            v = attrs.get(dn, dd)
+            if v is None:
+                continue
+            key.append(v)
+            at.append([dn, v])
+        if sn in scopes:
+            key += [sn, sv]
+            at += [["span.instrumentation.scope.name", sn], ["span.instrumentation.scope.version", sv]]
+        e = table.setdefault("\0".join(key), [at, 0])
+        e[1] += 1
+    return [v for _, v in sorted(table.items())]
+
+
+def case_scope():
+    spans = [("a", "GET", 2, 0, {"region": "eu"}, "io.opentelemetry.http", "1.2.0"),
+             ("a", "GET", 2, 0, {"region": "eu"}, "io.opentelemetry.http", "1.3.0"),
+             ("a", "GET", 2, 0, {"region": "eu"}, "io.opentelemetry.http", "1.3.0"),
+             ("a", "GET", 2, 0, {"region": "eu"}, "io.opentelemetry.grpc", "1.3.0"),   # not listed
+             ("a", "GET", 2, 0, {"region": "eu"}, "", ""),                             # no scope
+             ("a", "GET", 2, 0, {}, "io.opentelemetry.http", ""),                     # empty version
+             ("b", "op", 1, 2, {"region": "us"}, "manual", "0.1"),
+             ("b", "op", 1, 2, {"region": "us"}, "manual", "0.1")]
+    scopes = ["io.opentelemetry.http", "manual"]
+    return dict(name="include_instrumentation_scope",
+                config={"dimensions": [{"name": "region"}], "include_instrumentation_scope": scopes},
+                spans=[list(s[:5]) + [s[5], s[6]] for s in spans],
+                expected=dict(calls=restate_scope(spans, [["region", None]], set(scopes))))
+
+
 def main():
     cases = [
         build_case(case_kat_basic()),
@@ -308,7 +350,8 @@ def main():
     xv, sm = hash_vectors()
     out = dict(generator="tests/golden/gen_golden.py", xxhash_version=xxhash.VERSION, cases=cases,
                xxh64_vectors=xv, splitmix64_vectors=sm,
-               connector_cases=[case_expiration(), case_split_dims(), case_histogram_disable()])
+               connector_cases=[case_expiration(), case_split_dims(), case_histogram_disable(),
+                                case_scope()])
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "spanmetrics_kat.json")
     with open(path, "w") as f:
         json.dump(out, f, separators=(",", ":"))
