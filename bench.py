@@ -291,7 +291,9 @@ def run_workload(name, n, args, device, rank, world, barrier):
     for c in batch.columns():
         cols.append(torch.from_numpy(c.view(np.int64) if c.dtype == np.uint64 else c.view(np.int32)).to(device))
     n_iso = max(3, args.steps // 5)
-    n_var = n_variants(args, 1 + args.settle + args.warmup + 2 * n_iso + args.steps, device)
+    gk = getattr(args, "graph_k", 0) if (name == "c2" and world == 1) else 0
+    g_calls = max(1, args.steps // gk) if gk > 0 else 0
+    n_var = n_variants(args, 1 + args.settle + args.warmup + 2 * n_iso + args.steps + (2 + g_calls) * gk, device)
     variants = trace_variants(cols[3], cols[4], n_var, seed=1000 + rank, rank=rank, world=world)
     # every variant's own copy of the other columns too (--fresh-cols): no
     # launch re-reads an address an earlier launch read, so no column can be
@@ -383,6 +385,35 @@ def run_workload(name, n, args, device, rank, world, barrier):
     elapsed = time.perf_counter() - t0
     barrier()
     device_ms = max(start.elapsed_time(e_) for e_ in ends) / max(1, args.steps)
+    # 2b) the same launches as groups of K through sa_ingest_device_many (one
+    #     HIP graph per call on small-table engines, so no dispatch gap between
+    #     the K kernels); both of the engine's graphs are instantiated by two
+    #     untimed calls, the timed calls re-point them at fresh variants
+    graph = None
+    if gk > 0:
+        def many(s):
+            bs = []
+            for _ in range(gk):
+                v = full[launches[0] % len(full)]
+                launches[0] += 1
+                bs.append((v[0], v[1], v[2], v[3], v[4], v[5], n))
+            eng.ingest_device_many(bs, stream=s.cuda_stream)
+
+        for _ in range(2):
+            many(stream)
+        eng.join(stream.cuda_stream)
+        torch.cuda.synchronize(device)
+        g0, g1 = ev(), ev()
+        tg = time.perf_counter()
+        g0.record(stream)
+        for _ in range(g_calls):
+            many(stream)
+        eng.join(stream.cuda_stream)
+        g1.record(stream)
+        torch.cuda.synchronize(device)
+        g_el = time.perf_counter() - tg
+        graph = {"k": gk, "steps": g_calls * gk, "ms_per_step": g_el * 1e3 / (g_calls * gk),
+                 "device_ms_per_step": g0.elapsed_time(g1) / (g_calls * gk)}
     # 3) sustained: back-to-back launches over the streams for --soak-s seconds
     #    (after the timed steps, never part of value; trace-id variants repeat
     #    here, so later HLL reads raise little) -- the rate a collector holds
@@ -436,7 +467,7 @@ def run_workload(name, n, args, device, rank, world, barrier):
     out = {"value_incl_settle": world * n * (1 + args.settle + args.steps) / incl_s,
            "wl": wl, "batch": batch, "eng": eng, "first_window": first_window, "elapsed": elapsed,
            "kernel_ms": kernel_ms, "kernel_ms_bracketed": kernel_ms_bracketed, "device_ms": device_ms,
-           "cold_ms": cold_ms, "settle_ms": settle_ms, "sustained": soak,
+           "cold_ms": cold_ms, "settle_ms": settle_ms, "sustained": soak, "graph": graph,
            "merge_ms": merge_ms, "per_rank": per_rank,
            "calls_ok": calls_ok, "enqueue_s": enqueue_s, "streams": len(streams), "variants": n_var,
            "launches": launches[0], "hll_p": 14,
@@ -665,6 +696,9 @@ def main():
                     help="processes for the multi-core CPU baseline (default: every usable host core; 0 = skip)")
     ap.add_argument("--group", type=int, default=0,
                     help="also time an N-member engine group on this one device (sa_group_ingest_device)")
+    ap.add_argument("--graph-k", dest="graph_k", type=int, default=10,
+                    help="C2 at N=1: also time the steps as groups of K through sa_ingest_device_many "
+                         "(one HIP graph per call; reported as the c2_graph sub-object; 0 = skip)")
     ap.add_argument("--no-filter-off", action="store_true",
                     help="skip the C2 kernel time with the HLL lower-bound filter off")
     ap.add_argument("--cpu-worker", type=int, default=None, help=argparse.SUPPRESS)
@@ -746,6 +780,18 @@ def main():
             torch.cuda.empty_cache()
 
     extra = {}
+    g = main_r.get("graph")
+    if g is not None:
+        # K steps per sa_ingest_device_many call (one HIP graph of K launches),
+        # fresh trace-id variants, one stream; wall clock around the calls
+        ach = BYTES_PER_SPAN * n / (g["ms_per_step"] * 1e-3) / 1e9
+        extra["c2_graph"] = {
+            "workload": WORKLOADS["c2"] + f"; K = {g['k']} batches per sa_ingest_device_many call (one HIP graph)",
+            "value": n / (g["ms_per_step"] * 1e-3), "unit": "spans/s", "ms_per_step": g["ms_per_step"],
+            "device_ms_per_step": g["device_ms_per_step"], "steps": g["steps"], "k": g["k"],
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": ach / HBM_PEAK_GBS, "per": "wall-clock step (launch gaps included)"},
+            "calls_check": main_r["calls_ok"]}
     if world == 1 and args.workload == "c2" and not args.no_filter_off:
         extra["hll_filter_off"] = kernel_ms_filter_off(n, args, device)
         torch.cuda.empty_cache()

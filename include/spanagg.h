@@ -222,6 +222,15 @@ void sa_host_free(void *p);
  * may run concurrently on the device (the engine orders them only where they
  * share state), which is how consecutive batches overlap. */
 int sa_ingest_device(sa_engine *e, const sa_span_batch *batch, void *stream);
+/* k device batches in order on `stream`: the same result as k
+ * sa_ingest_device calls on it (same ordering rules, every batch valid until
+ * the stream reaches the end of the k).  Small-table engines launch the k
+ * ingests as one HIP graph, so consecutive launches carry no per-launch
+ * dispatch gap; other engines (binned, exponential, laboratory options) and
+ * batches that would need a split take the one-by-one path.  Replaces a loop
+ * of ConsumeTraces calls over the batches a receiver queued (the connector's
+ * aggregateMetrics per request, connector.go [UPSTREAM]). */
+int sa_ingest_device_many(sa_engine *e, const sa_span_batch *batches, uint32_t k, void *stream);
 /* Orders `stream` (NULL = the engine's stream) after every launch the engine
  * has enqueued so far, including work it runs on its own streams: the
  * high-cardinality (binned) path aggregates launch k on an engine stream

@@ -472,6 +472,8 @@ hipError_t launch_ingest_hbm(const IngestParams &P, uint32_t grid, hipStream_t s
 hipError_t launch_ingest_part(const IngestParams &P, hipStream_t s);
 hipError_t prepare_ingest_part();
 hipError_t prepare_ingest_small(size_t lds_bytes);
+void ingest_small_node(const IngestParams &P, uint32_t grid, size_t lds_bytes, int variant, void **args,
+                       hipKernelNodeParams *np);
 uint32_t ingest_small_block(bool bt, int variant, uint32_t log2cap, uint32_t nbk, uint32_t p);
 uint32_t ingest_small_blocks_per_cu(bool bt, int variant, uint32_t log2cap, uint32_t nbk, uint32_t p,
                                     size_t lds_bytes);

@@ -93,6 +93,21 @@ struct sa_engine {
   uint32_t nsets = 1, set = 0;
   hipEvent_t ev_set[kMaxSlabSets] = {}, ev_ctl = nullptr;
   hipStream_t set_stream[kMaxSlabSets] = {};
+  // sa_ingest_device_many: two instantiated graphs of K small-table launches,
+  // used in turn; a graph's kernel nodes are re-pointed at the next K batches
+  // (hipGraphExecKernelNodeSetParams) only after its previous launch finished
+  // (gx_done), so no launch in flight sees its arguments change
+  struct GraphIngest {
+    hipGraph_t g = nullptr;
+    hipGraphExec_t x = nullptr;
+    hipEvent_t done = nullptr;
+    bool launched = false;
+    std::vector<hipGraphNode_t> nodes;
+    const void *fn = nullptr;
+    dim3 block{};
+    size_t lds = 0;
+  } gi[2];
+  uint32_t gi_next = 0;
   bool ctl_dirty = true;
   uint32_t nbk = 0, npos = 0, nneg = 0;
   uint64_t thr[sa::kMaxBounds]{};
@@ -669,6 +684,11 @@ void sa_destroy(sa_engine *e) {
     if (e->pin_ev[k]) (void)hipEventDestroy(e->pin_ev[k]);
   }
   if (e->ev_async) (void)hipEventDestroy(e->ev_async);
+  for (auto &g : e->gi) {
+    if (g.x) (void)hipGraphExecDestroy(g.x);
+    if (g.g) (void)hipGraphDestroy(g.g);
+    if (g.done) (void)hipEventDestroy(g.done);
+  }
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
   if (e->ev_b) (void)hipEventDestroy(e->ev_b);
   for (hipEvent_t ev : e->ev_set)
@@ -913,6 +933,69 @@ static sa::ExpoParams expo_params(sa_engine *e, const sa_span_batch *b, uint32_t
   return E;
 }
 
+// The launch parameters of one ingest of batch b into slab set `set` (the
+// workgroup ranges, pool and tables; every path's kernels read from these).
+static void fill_params(sa_engine *e, const sa_span_batch *b, uint32_t set, uint64_t wg_chunk,
+                        uint64_t pool_base, uint32_t pool_n, IngestParams &P) {
+  const size_t srow = (e->nbk + 1) & ~1u;
+  P.key = b->key_hash;
+  P.start = b->start_ns;
+  P.end = b->end_ns;
+  P.w0 = b->trace_w0;
+  P.w1 = b->trace_w1;
+  P.meta = b->meta;
+  P.n = b->n;
+  P.wg_chunk = wg_chunk;
+  P.pool_base = pool_base;
+  P.pool_n = pool_n;
+  if (e->pool) {
+    P.pool_ctr = e->pool_ring + e->pool_seq % sa::kPoolRing;
+    P.pool_next = e->pool_ring + (e->pool_seq + e->nsets) % sa::kPoolRing;
+    ++e->pool_seq;
+  }
+  P.gkeys = e->gkeys;
+  P.log2cap = e->log2cap;
+  P.max_probe = sa::max_probe_of(e->log2cap);
+  P.slab_cnt = e->slab_cnt ? e->slab_cnt + (size_t)set * e->G * e->cap * srow : nullptr;
+  P.slab_sum = e->slab_sum ? e->slab_sum + (size_t)set * e->G * e->cap : nullptr;
+  P.gcounts = e->gcounts;
+  P.base64 = e->base64;
+  std::memcpy(P.thr, e->thr, sizeof e->thr);
+  P.npos = e->npos;
+  P.nneg = e->nneg;
+  P.nbk = e->nbk;
+  P.epoch_tiles = (uint32_t)(65535 / ((uint64_t)e->block * e->spl));  // (the launch's tile)
+  P.hll = e->hll;
+  P.cms = e->cms;
+  P.errcnt = e->errcnt;
+  P.errslab = e->errslab ? e->errslab + (size_t)set * e->G * e->cfg.n_windows * e->cap : nullptr;
+  P.window_ns = e->cfg.window_ns;
+  P.win_magic = UINT64_MAX / e->cfg.window_ns;
+  P.win_base = e->win_base;
+  P.base_ns = e->win_base * e->cfg.window_ns;  // < 2^64: checked in sa_window_advance
+  P.ring_ns = (uint64_t)e->cfg.n_windows * e->cfg.window_ns;
+  P.inv_window = (float)(1.0 / (double)e->cfg.window_ns);
+  P.win_ok = (float)(0.5 - (double)e->cfg.n_windows * 0x1p-20);  // n_windows <= 4096: >= 0.496
+  P.base_slot = (uint32_t)(e->win_base & (e->cfg.n_windows - 1));
+  P.bintab = e->d_bins;
+  P.win_mask = e->cfg.n_windows - 1;
+  P.n_windows = e->cfg.n_windows;
+  P.p = e->cfg.hll_p;
+  P.n_services = e->cfg.n_services;
+  P.cms_d = e->cfg.cms_d;
+  P.cms_w = e->cfg.cms_w;
+  P.cms_shift = 64 - log2u(e->cfg.cms_w);
+  P.seeds = e->d_seeds;
+  P.stats = e->stats;
+  P.diag = e->cfg.flags;
+  P.dbg = e->dbg;
+  P.hll_lb = e->hll_lb;
+  P.lb_shift = e->lb_shift;
+  P.lb_n = e->lb_n;  // read (and refreshed) by the v2 and binned kernels; the others ignore it
+  P.lb_seq = e->lb_seq++;
+  P.hll_filt = e->hll_filt;
+}
+
 static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   if (b->n == 0) return SA_OK;
   const uint64_t tile = (uint64_t)e->block * e->spl;
@@ -952,64 +1035,8 @@ static int ingest_launch(sa_engine *e, const sa_span_batch *b, hipStream_t s) {
   if (s != e->stream) SA_HIP(e, hipStreamWaitEvent(s, e->ev_ctl, 0));
   const uint32_t set = e->set;
   if (e->set_stream[set] && e->set_stream[set] != s) SA_HIP(e, hipStreamWaitEvent(s, e->ev_set[set], 0));
-  const size_t srow = (e->nbk + 1) & ~1u;
   IngestParams P{};
-  P.key = b->key_hash;
-  P.start = b->start_ns;
-  P.end = b->end_ns;
-  P.w0 = b->trace_w0;
-  P.w1 = b->trace_w1;
-  P.meta = b->meta;
-  P.n = b->n;
-  P.wg_chunk = wg_chunk;
-  P.pool_base = pool_base;
-  P.pool_n = pool_n;
-  if (e->pool) {
-    P.pool_ctr = e->pool_ring + e->pool_seq % sa::kPoolRing;
-    P.pool_next = e->pool_ring + (e->pool_seq + e->nsets) % sa::kPoolRing;
-    ++e->pool_seq;
-  }
-  P.gkeys = e->gkeys;
-  P.log2cap = e->log2cap;
-  P.max_probe = sa::max_probe_of(e->log2cap);
-  P.slab_cnt = e->slab_cnt ? e->slab_cnt + (size_t)set * e->G * e->cap * srow : nullptr;
-  P.slab_sum = e->slab_sum ? e->slab_sum + (size_t)set * e->G * e->cap : nullptr;
-  P.gcounts = e->gcounts;
-  P.base64 = e->base64;
-  std::memcpy(P.thr, e->thr, sizeof e->thr);
-  P.npos = e->npos;
-  P.nneg = e->nneg;
-  P.nbk = e->nbk;
-  P.epoch_tiles = (uint32_t)(65535 / tile);
-  P.hll = e->hll;
-  P.cms = e->cms;
-  P.errcnt = e->errcnt;
-  P.errslab = e->errslab ? e->errslab + (size_t)set * e->G * e->cfg.n_windows * e->cap : nullptr;
-  P.window_ns = e->cfg.window_ns;
-  P.win_magic = UINT64_MAX / e->cfg.window_ns;
-  P.win_base = e->win_base;
-  P.base_ns = e->win_base * e->cfg.window_ns;  // < 2^64: checked in sa_window_advance
-  P.ring_ns = (uint64_t)e->cfg.n_windows * e->cfg.window_ns;
-  P.inv_window = (float)(1.0 / (double)e->cfg.window_ns);
-  P.win_ok = (float)(0.5 - (double)e->cfg.n_windows * 0x1p-20);  // n_windows <= 4096: >= 0.496
-  P.base_slot = (uint32_t)(e->win_base & (e->cfg.n_windows - 1));
-  P.bintab = e->d_bins;
-  P.win_mask = e->cfg.n_windows - 1;
-  P.n_windows = e->cfg.n_windows;
-  P.p = e->cfg.hll_p;
-  P.n_services = e->cfg.n_services;
-  P.cms_d = e->cfg.cms_d;
-  P.cms_w = e->cfg.cms_w;
-  P.cms_shift = 64 - log2u(e->cfg.cms_w);
-  P.seeds = e->d_seeds;
-  P.stats = e->stats;
-  P.diag = e->cfg.flags;
-  P.dbg = e->dbg;
-  P.hll_lb = e->hll_lb;
-  P.lb_shift = e->lb_shift;
-  P.lb_n = e->lb_n;  // read (and refreshed) by the v2 and binned kernels; the others ignore it
-  P.lb_seq = e->lb_seq++;
-  P.hll_filt = e->hll_filt;
+  fill_params(e, b, set, wg_chunk, pool_base, pool_n, P);
   hipError_t st;
   hipStream_t hs = s;  // the stream the launch's last kernel runs on (expo: the histogram kernels')
   if (e->small) {
@@ -1154,6 +1181,100 @@ int sa_ingest_device(sa_engine *e, const sa_span_batch *b, void *stream) {
   // overlap it (see sa_engine::nsets)
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
   return ingest_on(e, b, s);
+}
+
+// k device batches in order on `stream`, as k sa_ingest_device calls would
+// ingest them.  Small-table engines (no tail pool, no diagnostics) launch the
+// k kernels as one HIP graph: no per-launch dispatch gap between them.  Any
+// other engine, a batch that would split, or a slab reduction due inside the
+// k launches takes the stream path, one launch after another.
+int sa_ingest_device_many(sa_engine *e, const sa_span_batch *bs, uint32_t k, void *stream) {
+  if (!e) return SA_EINVAL;
+  if (k && !bs) return fail(e, SA_EINVAL, "null batch array");
+  for (uint32_t i = 0; i < k; ++i)
+    if (int rc = check_batch(e, &bs[i], true)) return rc;
+  if (int rc = set_dev(e)) return rc;
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+  bool graph = k > 1 && e->small && !e->expo && !e->bt && !e->part && !e->pool && !e->dbg && e->cfg.flags == 0;
+  const uint64_t tile = (uint64_t)e->block * e->spl;
+  const uint64_t max_wg = e->variant >= 8 ? sa::kMaxWgSpans : (1u << 27);
+  std::vector<uint32_t> grid(k);
+  std::vector<uint64_t> chunk(k);
+  uint64_t load = 0;
+  for (uint32_t i = 0; graph && i < k; ++i) {
+    const uint64_t n = bs[i].n;
+    if (n == 0 || n > (uint64_t)e->G * max_wg) {
+      graph = false;
+      break;
+    }
+    grid[i] = (uint32_t)std::min<uint64_t>((n + tile - 1) / tile, e->G);
+    chunk[i] = ((n + grid[i] - 1) / grid[i] + 3) / 4 * 4;
+    load += chunk[i];
+  }
+  if (graph && e->slab_load + load > kSlabLimit) {  // fold every set into the counters first
+    if (int rc = join_checked(e)) return rc;
+    if (int rc = reduce_slabs(e, e->stream)) return rc;
+    graph = load <= kSlabLimit;
+  }
+  if (!graph) {
+    for (uint32_t i = 0; i < k; ++i)
+      if (int rc = ingest_on(e, &bs[i], s)) return rc;
+    return SA_OK;
+  }
+  // the ordering ingest_launch gives each launch, once for the k
+  if (e->ctl_dirty) {
+    SA_HIP(e, hipEventRecord(e->ev_ctl, e->stream));
+    e->ctl_dirty = false;
+  }
+  if (s != e->stream) SA_HIP(e, hipStreamWaitEvent(s, e->ev_ctl, 0));
+  for (uint32_t j = 0; j < e->nsets && j < k; ++j) {
+    const uint32_t set = (e->set + j) % e->nsets;
+    if (e->set_stream[set] && e->set_stream[set] != s) SA_HIP(e, hipStreamWaitEvent(s, e->ev_set[set], 0));
+  }
+  sa_engine::GraphIngest &g = e->gi[e->gi_next];
+  if (g.launched) SA_HIP(e, hipEventSynchronize(g.done));  // its previous launch is over
+  std::vector<IngestParams> P(k);
+  std::vector<void *> args(k);
+  std::vector<hipKernelNodeParams> np(k);
+  for (uint32_t i = 0; i < k; ++i) {
+    fill_params(e, &bs[i], (e->set + i) % e->nsets, chunk[i], 0, 0, P[i]);
+    args[i] = &P[i];
+    sa::ingest_small_node(P[i], grid[i], e->lds_bytes, e->variant, &args[i], &np[i]);
+  }
+  const bool reuse = g.x && g.nodes.size() == k && g.fn == np[0].func && g.lds == e->lds_bytes &&
+                     g.block.x == np[0].blockDim.x;
+  if (reuse) {
+    for (uint32_t i = 0; i < k; ++i) SA_HIP(e, hipGraphExecKernelNodeSetParams(g.x, g.nodes[i], &np[i]));
+  } else {
+    if (g.x) (void)hipGraphExecDestroy(g.x);
+    if (g.g) (void)hipGraphDestroy(g.g);
+    g.x = nullptr;
+    g.g = nullptr;
+    g.nodes.assign(k, nullptr);
+    SA_HIP(e, hipGraphCreate(&g.g, 0));
+    for (uint32_t i = 0; i < k; ++i)
+      SA_HIP(e, hipGraphAddKernelNode(&g.nodes[i], g.g, i ? &g.nodes[i - 1] : nullptr, i ? 1 : 0, &np[i]));
+    SA_HIP(e, hipGraphInstantiate(&g.x, g.g, nullptr, nullptr, 0));
+    if (!g.done) SA_HIP(e, hipEventCreateWithFlags(&g.done, hipEventDisableTiming));
+    g.fn = np[0].func;
+    g.lds = e->lds_bytes;
+    g.block = np[0].blockDim;
+  }
+  if (hipError_t st = hipGraphLaunch(g.x, s); st != hipSuccess)
+    return fail(e, SA_EDEVICE, std::string("ingest graph launch: ") + hipGetErrorString(st));
+  SA_HIP(e, hipEventRecord(g.done, s));
+  g.launched = true;
+  e->gi_next ^= 1u;
+  for (uint32_t j = 0; j < e->nsets && j < k; ++j) {
+    const uint32_t set = (e->set + j) % e->nsets;
+    SA_HIP(e, hipEventRecord(e->ev_set[set], s));
+    e->set_stream[set] = s;
+  }
+  e->set = (e->set + k) % e->nsets;
+  for (uint32_t i = 0; i < k; ++i) e->spans += bs[i].n;
+  e->slab_load += load;
+  e->unflushed = true;
+  return SA_OK;
 }
 
 int sa_host_alloc(size_t bytes, void **out) {

@@ -1924,6 +1924,22 @@ hipError_t launch_ingest_small(const IngestParams &P, uint32_t grid, size_t lds_
   return hipLaunchKernel(fn, dim3(grid), dim3(small_block(bt, variant)), args, lds_bytes, s);
 }
 
+// The same launch as a HIP graph kernel node (sa_ingest_device_many): the
+// kernel, its geometry and `args` (args[0] = &P, owned by the caller, read
+// when the node is added or its parameters set).
+void ingest_small_node(const IngestParams &P, uint32_t grid, size_t lds_bytes, int variant, void **args,
+                       hipKernelNodeParams *np) {
+  variant = small_variant(variant, P.log2cap, P.nbk, P.p);
+  const bool bt = P.bintab != nullptr;
+  *np = hipKernelNodeParams{};
+  np->func = const_cast<void *>(small_fn(bt, variant, P.diag != 0 || (P.dbg != nullptr && variant < 8)));
+  np->gridDim = dim3(grid);
+  np->blockDim = dim3(small_block(bt, variant));
+  np->sharedMemBytes = (unsigned int)lds_bytes;
+  np->kernelParams = args;
+  np->extra = nullptr;
+}
+
 uint32_t ingest_small_block(bool bt, int variant, uint32_t log2cap, uint32_t nbk, uint32_t p) {
   return small_block(bt, small_variant(variant, log2cap, nbk, p));
 }

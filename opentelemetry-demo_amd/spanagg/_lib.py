@@ -94,6 +94,7 @@ SIGNATURES = [
     ("sa_ingest", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch)]),
     ("sa_ingest_async", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch)]),
     ("sa_ingest_device", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch), C.c_void_p]),
+    ("sa_ingest_device_many", C.c_int, [C.c_void_p, C.POINTER(sa_span_batch), C.c_uint32, C.c_void_p]),
     ("sa_host_alloc", C.c_int, [C.c_size_t, C.POINTER(C.c_void_p)]),
     ("sa_host_free", None, [C.c_void_p]),
     ("sa_sync", C.c_int, [C.c_void_p]),

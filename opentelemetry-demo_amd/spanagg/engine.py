@@ -288,6 +288,18 @@ class Engine:
         self._check(self.lib.sa_ingest_device(self._h, C.byref(b), C.c_void_p(stream or 0)),
                     "sa_ingest_device")
 
+    def ingest_device_many(self, batches, stream: Optional[int] = None):
+        """sa_ingest_device_many: device-resident batches in order, each a
+        (key, start, end, w0, w1, meta[, n]) tuple of torch tensors or raw
+        device pointers; one HIP graph of launches on small-table engines."""
+        arr = (_lib.sa_span_batch * max(1, len(batches)))()
+        for i, bt in enumerate(batches):
+            cols = bt[:6]
+            n = int(bt[6]) if len(bt) > 6 else int(cols[0].numel())
+            arr[i] = _lib.sa_span_batch(*[_ptr(c) for c in cols], n)
+        self._check(self.lib.sa_ingest_device_many(self._h, arr, len(batches), C.c_void_p(stream or 0)),
+                    "sa_ingest_device_many")
+
     def join(self, stream: Optional[int] = None):
         """sa_join: order `stream` (a hipStream_t handle, None = the engine's)
         after every launch enqueued so far, the binned path's aggregates on
