@@ -829,6 +829,13 @@ def main():
         }
         result.update(subs)
         result.update(extra)
+        if "c2_graph" in extra:
+            # the same kernel launched K at a time from a HIP graph (no dispatch
+            # gap between launches): device time per launch, HIP events around
+            # the calls on their stream; `frac` above stays the serial launches'
+            gd = extra["c2_graph"]["device_ms_per_step"]
+            result["roofline"]["graph_ms_per_launch"] = gd
+            result["roofline"]["frac_graph_launches"] = BYTES_PER_SPAN * n / (gd * 1e-3) / 1e9 / HBM_PEAK_GBS
         if h2d is not None:
             result["host_buffer_ingest"] = h2d
         wl = main_r["wl"]
